@@ -1,0 +1,75 @@
+"""Synthetic inputs of the shape BASELINE.json's configs name.
+
+Base events ``E in {0,1}^{N_raw x m}`` i.i.d. Bernoulli(rho) from ``default_rng(seed)``;
+lags ``[-L, ..., L-1]`` expanded in the shift-major layout of
+``sglm_ez.timeshift_cols`` (backend/sglm_ez.py:102-123: shifts ``[0] + [-L..-1] + [1..L-1]``);
+the first ``L-1`` and last ``L`` rows of the expansion hold the NaN fill and are dropped, so
+``N_raw = N + 2L - 1`` leaves exactly ``N`` rows.  ``beta_true ~ N(0, 0.1^2)`` (rng 1);
+Poisson ``y ~ Poisson(exp(X beta + b))`` with ``b = -1`` (rng 2); Gaussian
+``y = X beta + 0.5 + N(0, 1)``.  Trial ids ``t // 100``.
+
+The linear predictor is computed by per-event convolution of E with the lag kernel, so the
+1M x 2000 design never has to exist on the host.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+
+@dataclass
+class Synthetic:
+    E: np.ndarray            # (N_raw, m) float32 0/1 events
+    L: int                   # lags -L..L-1
+    shifts: list             # shift-major shift list
+    N: int                   # rows after the NaN drop
+    beta: np.ndarray         # (p,) true coefficients, shift-major column order
+    intercept: float
+    y: np.ndarray            # (N,) response
+    trial: np.ndarray        # (N,) trial ids
+    family: str
+
+    @property
+    def p(self):
+        return len(self.shifts) * self.E.shape[1]
+
+    def dense_X(self, dtype=np.float64):
+        """Materialise X (N x p) on the host — small configs / tests only."""
+        Nr, m = self.E.shape
+        X = np.empty((self.N, self.p), dtype=dtype)
+        r0 = self.L - 1
+        for bi, s in enumerate(self.shifts):
+            X[:, bi * m:(bi + 1) * m] = self.E[r0 - s:r0 - s + self.N]
+        return X
+
+
+def shift_list(L):
+    return [0] + list(range(-L, 0)) + list(range(1, L))
+
+
+def make(N, m, L, family="poisson", rho=0.02, seed=0, beta_scale=0.1, intercept=None):
+    rng = np.random.default_rng(seed)
+    N_raw = N + 2 * L - 1
+    E = (rng.random((N_raw, m)) < rho).astype(np.float32)
+    shifts = shift_list(L)
+    p = len(shifts) * m
+    beta = np.random.default_rng(seed + 1).normal(0.0, beta_scale, size=p)
+    b = (-1.0 if family == "poisson" else 0.5) if intercept is None else intercept
+    # eta[t] = sum_{shift s, event a} E[t + r0 - s, a] * beta[s, a]  (r0 = L-1)
+    eta = np.full(N, b, dtype=np.float64)
+    r0 = L - 1
+    B = beta.reshape(len(shifts), m)
+    for bi, s in enumerate(shifts):
+        eta += E[r0 - s:r0 - s + N].astype(np.float64) @ B[bi]
+    rng2 = np.random.default_rng(seed + 2)
+    if family == "poisson":
+        y = rng2.poisson(np.exp(eta)).astype(np.float64)
+    elif family == "gamma":
+        mu = np.exp(eta)
+        y = rng2.gamma(2.0, mu / 2.0)
+    else:
+        y = eta + rng2.normal(0.0, 1.0, size=N)
+    trial = np.arange(N) // 100
+    return Synthetic(E=E, L=L, shifts=shifts, N=N, beta=beta, intercept=b, y=y,
+                     trial=trial, family=family)

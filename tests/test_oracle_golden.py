@@ -1,0 +1,158 @@
+"""Pin the CPU oracle against the committed golden fixtures (no GPU)."""
+import json
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from oracle import cv_ref, folds_ref, glm_ref, pp_ref
+
+from conftest import GOLDEN
+
+
+def rel(a, b):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    return np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30)
+
+
+# ------------------------------------------------------------------ timeshift known answers
+def test_timeshift_known_answers(golden):
+    g = golden("timeshift_known.npz")
+    X = g["ts_X"]
+    assert np.array_equal(pp_ref.timeshift(X, shift_amt=0), X)
+    assert np.array_equal(pp_ref.timeshift(X, [0, 3], 0), X[:, [0, 3]])
+    assert np.array_equal(pp_ref.timeshift(X, shift_amt=1, fill_value=0), g["ts_fwd"])
+    assert np.array_equal(pp_ref.timeshift(X, [0, 3], 1, fill_value=0), g["ts_fwd"][:, [0, 3]])
+    assert np.array_equal(pp_ref.timeshift(X, shift_amt=-1, fill_value=0), g["ts_bwd"])
+    assert np.array_equal(pp_ref.timeshift(X, [0, 1], 1, keep_non_inx=True, fill_value=0),
+                          g["ts_keep_fwd"])
+    assert np.array_equal(pp_ref.timeshift(X, [0, 1], -1, keep_non_inx=True, fill_value=0),
+                          g["ts_keep_bwd"])
+    assert np.array_equal(pp_ref.timeshift_multiple(X, shift_amt_list=[-1, 0, 1], fill_value=0),
+                          g["ts_multi_all"])
+    assert np.array_equal(pp_ref.timeshift_multiple(X, [0, 3], [-1, 0, 1], fill_value=0),
+                          g["ts_multi_03"])
+
+
+def test_timeshift_by_dict_matches_pandas_shift():
+    rng = np.random.default_rng(0)
+    X = (rng.random((50, 3)) < 0.3).astype(float)
+    df = pd.DataFrame(X, columns=list("abc"))
+    orders = {0: (-2, 3), 2: (-1, 1)}
+    out = pp_ref.timeshift_by_dict(X, orders)
+    cols = [df]
+    for c, (ng, ps) in orders.items():
+        name = df.columns[c]
+        for s in range(ng, ps + 1):
+            cols.append(df[[name]].shift(s).rename({name: f"{name}_{s}"}, axis=1))
+    ref = pd.concat(cols, axis=1)
+    # setup_model_fit.py:88-94 uses the last entry's (neg, pos) = (-1, 1) for every column
+    ref = ref.dropna(subset=["a_-1", "c_-1", "a_1", "c_1"])
+    assert np.array_equal(out, ref.values, equal_nan=True)
+
+
+# ------------------------------------------------------------------ fits
+def test_poisson_fits(golden):
+    g = golden("fits.npz")
+    meta = json.load(open(os.path.join(GOLDEN, "fits_meta.json")))
+    X, y = g["pois_X"], g["pois_y"]
+    for m in meta:
+        coef, b = glm_ref.fit_tweedie_newton(X, y, m["alpha"], 1.0,
+                                             fit_intercept=m["fit_intercept"])
+        assert rel(coef, g[m["key"] + "_coef"]) < 1e-9, m
+        assert abs(b - float(g[m["key"] + "_b"])) < 1e-9
+
+
+def test_poisson_zero_column(golden):
+    g = golden("fits.npz")
+    coef, b = glm_ref.fit_tweedie_newton(g["pois_zero_X"], g["pois_y"], 0.0, 1.0)
+    # sklearn's newton-cholesky leaves lbfgs-level error on this singular Hessian
+    assert rel(coef, g["pois_zero_coef"]) < 1e-6
+    assert coef[3] == 0.0
+
+
+def test_gamma_fit(golden):
+    g = golden("fits.npz")
+    coef, b = glm_ref.fit_tweedie_newton(g["gam_X"], g["gam_y"], 0.05, 2.0)
+    assert rel(coef, g["gam_coef"]) < 1e-9
+    assert abs(b - float(g["gam_b"])) < 1e-9
+
+
+def test_gaussian_fits(golden):
+    g = golden("fits.npz")
+    X, y = g["gau_X"], g["gau_y"]
+    c, b = glm_ref.fit_ols(X, y)
+    assert rel(c, g["ols_coef"]) < 1e-10
+    for i, a in enumerate([0.1, 10.0, 1000.0]):
+        c, b = glm_ref.fit_ridge(X, y, a)
+        assert rel(c, g[f"ridge_a{i}_coef"]) < 1e-10
+        assert abs(b - float(g[f"ridge_a{i}_b"])) < 1e-10
+    for i, a in enumerate([1e-3, 1e-2]):
+        c, b = glm_ref.fit_enet_cd(X, y, a, 1.0)
+        assert rel(c, g[f"lasso_a{i}_coef"]) < 1e-7
+        c, b = glm_ref.fit_enet_cd(X, y, a, 0.5)
+        assert rel(c, g[f"enet_a{i}_coef"]) < 1e-7
+    c, b = glm_ref.fit_ols(g["olsr_X"], y)
+    assert rel(c, g["olsr_coef"]) < 1e-8
+
+
+def test_tweedie_via_spec_matches_ridge_scaling(golden):
+    """Tweedie(power=0) objective uses mean + alpha/2 (not Ridge's sum + alpha)."""
+    g = golden("fits.npz")
+    X, y = g["gau_X"], g["gau_y"]
+    n = X.shape[0]
+    c1, b1 = glm_ref.fit_tweedie_newton(X, y, 0.01, 0.0)
+    c2, b2 = glm_ref.fit_ridge(X, y, 0.01 * n)
+    assert rel(c1, c2) < 1e-9
+
+
+# ------------------------------------------------------------------ folds
+def test_group_shuffle_split_bit_exact(golden):
+    g = golden("folds.npz")
+    trial = np.arange(5000) // 100
+    for seed in (0, 3, 17):
+        codes = folds_ref.trial_bucket_codes([trial])
+        assert np.array_equal(codes, g[f"f{seed}_codes"])
+        np.random.seed(seed)
+        splits = folds_ref.cv_idx_from_bucket_ids(codes, num_folds=5)
+        for k, (tr, te) in enumerate(splits):
+            assert np.array_equal(tr, g[f"f{seed}_k{k}_train"])
+            assert np.array_equal(te, g[f"f{seed}_k{k}_test"])
+    assert np.array_equal(folds_ref.trial_bucket_codes([trial, trial // 7]),
+                          g["codes_two_backend"])
+    assert np.array_equal(folds_ref.trial_bucket_codes([trial, trial // 7], package_style=True),
+                          g["codes_two_package"])
+    bid = folds_ref.bucket_ids_by_timeframe(437, 20)
+    np.random.seed(5)
+    splits = folds_ref.cv_idx_from_bucket_ids(bid)
+    assert len(splits) == int(g["tf_nsplits"])
+    for k, (tr, te) in enumerate(splits):
+        assert np.array_equal(tr, g[f"tf_k{k}_train"])
+        assert np.array_equal(te, g[f"tf_k{k}_test"])
+
+
+# ------------------------------------------------------------------ CV grid
+def test_cv_grid_aggregation(golden):
+    g = golden("cv_grid.npz")
+    X, y = g["cvg_X"], g["cvg_y"]
+    cv_idx = [(g[f"cvg_k{k}_train"], g[f"cvg_k{k}_test"]) for k in range(3)]
+    kws = cv_ref.generate_mult_params({"alpha": list(g["cvg_alphas"])},
+                                      {"model_name": "Poisson"})
+    res = cv_ref.cv_mult(X, y, cv_idx, kws)
+    for j, r in enumerate(res["full_cv_results"]):
+        assert rel(r["cv_coefs"], g[f"cvg_a{j}_cv_coefs"]) < 1e-8
+        assert rel(r["cv_scores_test"], g[f"cvg_a{j}_scores_test"]) < 1e-9
+        assert abs(r["cv_R2_score"] - float(g[f"cvg_a{j}_R2"])) < 1e-9
+        assert abs(r["cv_mse_score"] - float(g[f"cvg_a{j}_mse"])) < 1e-9
+        assert rel(r["coef"], g[f"cvg_a{j}_full_coef"]) < 1e-8
+    best = int(np.argmax([float(g[f"cvg_a{j}_scores_test"].mean()) for j in range(3)]))
+    assert res["best_index"] == best
+
+
+def test_generate_mult_params_order():
+    out = cv_ref.generate_mult_params({"alpha": [1, 2], "l1_ratio": [0, 1]}, {"max_iter": 5})
+    assert out == [{"max_iter": 5, "alpha": 1, "l1_ratio": 0},
+                   {"max_iter": 5, "alpha": 1, "l1_ratio": 1},
+                   {"max_iter": 5, "alpha": 2, "l1_ratio": 0},
+                   {"max_iter": 5, "alpha": 2, "l1_ratio": 1}]
