@@ -1,0 +1,188 @@
+"""Benchmark: IRLS iterations/s and CV-grid wall-clock on the BASELINE.json north-star config.
+
+Workload (configs[3], the config the metric is quoted on; it fits one MI355X): Poisson/log,
+1M rows x 2000 time-shifted predictors (50 Bernoulli(0.02) events x 40 lags, synthetic per
+SURVEY.md §8(d)), 5 GroupShuffleSplit splits x 20 lambdas + 20 full refits = 120 fits.
+One step = one full CV grid (all 120 fits solved to convergence + scored).  With N ranks
+the 120 fits are dealt round-robin (strong scaling: the grid is fixed); results are
+all-gathered over RCCL once per grid.
+
+value = fit-iterations (sum over fits of Newton/IRLS iterations, all ranks) / wall time.
+
+Usage: python bench.py [--gpus N --steps K --warmup W] ; N > 1 under torch.distributed.run.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "sabatinilab-glm_amd"))
+sys.path.insert(0, ROOT)
+
+PEAK_BF16_TFLOPS = 2500.0          # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+CONFIGS = {
+    # name: (N rows, events m, L -> lags -L..L-1, n_splits, lambdas)
+    "c4": (1_000_000, 50, 20, 5, 20),
+    "c3": (100_000, 25, 10, 5, 20),
+    "small": (50_000, 10, 5, 5, 4),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-rows", type=int, default=50_000)
+    return ap.parse_args()
+
+
+def cpu_baseline(s, n_rows_unit, rows):
+    """Oracle (float64 numpy/LAPACK damped Newton) on a bounded slice of the same design."""
+    from oracle import glm_ref
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:  # pragma: no cover
+        cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    rows = min(rows, s.N)
+    m = s.E.shape[1]
+    X = np.empty((rows, s.p), dtype=np.float64)
+    r0 = s.L - 1
+    for bi, sh in enumerate(s.shifts):
+        X[:, bi * m:(bi + 1) * m] = s.E[r0 - sh:r0 - sh + rows]
+    y = s.y[:rows]
+    t0 = time.perf_counter()
+    _, _, iters = glm_ref.fit_tweedie_newton(X, y, 1e-2, 1.0, tol=1e-8, max_iter=50,
+                                             return_iters=True)
+    dt = time.perf_counter() - t0
+    per_iter_unit = dt / max(iters, 1) * (n_rows_unit / rows)
+    return {"value": 1.0 / per_iter_unit, "unit": "IRLS fit-iterations/s (1M-row unit)",
+            "cores": int(cores), "kind": "port",
+            "sample": f"oracle fp64 damped Newton, Poisson alpha=1e-2, {rows}x{s.p} slice of the "
+                      f"C4 design, {iters} iterations in {dt:.2f} s, per-iteration time scaled "
+                      f"x{n_rows_unit / rows:.0f} to 1M rows",
+            "grid_wall_s_extrapolated": None}
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from sglm_hip import engine as E, folds, grid, synth
+    from sglm_hip.estimators import Objective
+
+    N, m, L, K, nlam = CONFIGS[a.config]
+    t_setup = time.perf_counter()
+    s = synth.make(N=N, m=m, L=L, family="poisson", rho=0.02, seed=0)
+    design = E.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
+    codes = folds.trial_keys_codes(__import__("pandas").DataFrame({"nTrial": s.trial}), ["nTrial"]).values
+    np.random.seed(3)
+    cv_idx = folds.cv_idx_from_bucket_ids(codes, num_folds=K)
+    lams = np.logspace(-4, 1, nlam)
+    objs = [Objective("irls", E.FAM_TWEEDIE_LOG, 1.0, float(al), "n", True, 100) for al in lams]
+    rolls = [0] * nlam
+    torch.cuda.synchronize()
+    setup_s = time.perf_counter() - t_setup
+
+    def step(stats=None):
+        return grid.run(design, s.y, cv_idx, objs, rolls, stats=stats)
+
+    for _ in range(a.warmup):
+        step()
+    stats = E.IrlsStats(record=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        res = step(stats)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    # roofline of the dominant kernel (Gram) from HIP events on the launch stream
+    ktime = sum(e0.elapsed_time(e1) for e0, e1, _, _ in stats.syrk_events) / 1e3
+    kflop = sum(nact_flop for _, _, _, nact_flop in stats.syrk_events)
+    nlaunch = len(stats.syrk_events)
+    t = torch.tensor([elapsed, float(stats.fit_iters), ktime, kflop, float(nlaunch)],
+                     dtype=torch.float64, device="cuda")
+    if world > 1:
+        mx = t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = t.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        elapsed, fit_iters = float(mx[0]), float(sm[1])
+        ktime, kflop, nlaunch = float(sm[2]), float(sm[3]), int(sm[4])
+    else:
+        fit_iters = float(stats.fit_iters)
+    if rank == 0:
+        pa = s.p + 1
+        achieved = kflop / ktime / 1e12 if ktime > 0 else 0.0
+        cpu = None
+        if not a.no_cpu and world == 1:
+            cpu = cpu_baseline(s, 1_000_000, a.cpu_rows)
+        out = {
+            "metric": "IRLS iters/sec on 1M×2000 design mat; CV-grid wall-clock (5-fold×20 λ)",
+            "value": fit_iters / elapsed,
+            "unit": "IRLS fit-iterations/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic",
+            "config": {
+                "workload": f"Poisson/log IRLS CV grid: {s.N} rows x {s.p} timeshifted predictors "
+                            f"({m} events x {len(s.shifts)} lags), {K} GroupShuffleSplit splits x "
+                            f"{nlam} lambdas + {nlam} refits = {nlam * (K + 1)} fits",
+                "config_name": a.config,
+                "n_rows": s.N, "p": s.p, "fits": nlam * (K + 1),
+                "grid_wall_s": elapsed / a.steps,
+                "fit_iters_per_grid": fit_iters / a.steps,
+                "setup_s": setup_s,
+                "parallelism": f"fits round-robin over {world} rank(s), RCCL all-gather of results",
+            },
+            "roofline": {
+                "bound": "mfma",
+                "kernel": "syrk_kernel (X^T diag(w) X, v_mfma_f32_32x32x16_bf16)",
+                "achieved": achieved,
+                "peak": PEAK_BF16_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": achieved / PEAK_BF16_TFLOPS,
+                "traffic": None,
+                "algorithmic_flop_per_fit_iter": f"n_train*p'*(p'+1), p'={pa}",
+                "launches": nlaunch,
+                "avg_launch_ms": ktime / max(nlaunch, 1) * 1e3,
+            },
+            "cpu_baseline": cpu,
+        }
+        conv = all(r["converged"] for r in res)
+        out["config"]["all_converged"] = bool(conv)
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,166 @@
+/*
+ * sglm_hip.h — C ABI of libsglm_hip.so, the MI355X (gfx950) engine behind the sglm hot path.
+ *
+ * The reference (kimerein/sabatinilab-glm) is pure Python: its "FFI" for this path is the
+ * scikit-learn estimator protocol that GLM.__init__ instantiates (backend/sglm.py:128-130)
+ * and calls (fit backend/sglm.py:241, predict :347, score :184), plus numpy for the
+ * timeshift (backend/sglm_pp.py:298-357) and the CV fold copies (backend/sglm_cv.py:106-110).
+ * Each entry point below names the reference interface whose arithmetic it replaces.
+ * The Python host layer (sabatinilab-glm_amd/sglm_hip/_lib.py) binds these with ctypes.
+ *
+ * Conventions
+ *  - Every pointer is a DEVICE pointer owned by the caller (PyTorch-ROCm tensors), except
+ *    where a parameter says "host".
+ *  - Every call is asynchronous on `stream` (a hipStream_t; 0 = legacy default stream) and
+ *    performs no allocation and no host synchronisation; scratch is the caller's `work`
+ *    buffer, sized by the matching *_work_bytes() query.
+ *  - Return value: SGLM_OK (0) or an error code; sglm_last_error() gives a thread-local
+ *    message.  Launch-time HIP errors are reported as SGLM_EHIP.
+ *
+ * Data layout in HBM
+ *  - Design X: FEATURE-MAJOR ("column-major") X[a * ld + i], a in [0, P), i in [0, ld):
+ *    one contiguous row stream per predictor, the ones column (intercept) at a = p, zero
+ *    columns up to P (multiple of 256), zero rows up to ld (multiple of 256).
+ *    Stored bf16 (exact for 0/1 event designs) and, when X is not bf16-exact, also f32.
+ *  - Per-fit vectors are fit-major: eta/W/R[k * ld + i]; coefficients beta[k * P + a].
+ *  - Responses Y[r * ld + i] (f32); row masks M[f * ld + i] (uint8 multiplicities).
+ */
+#ifndef SGLM_HIP_H
+#define SGLM_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* sglm_stream_t; /* hipStream_t */
+
+enum sglm_status { SGLM_OK = 0, SGLM_EINVAL = 1, SGLM_EHIP = 2, SGLM_ENOTPD = 3 };
+
+/* Loss family codes: half-Tweedie losses of sklearn/_loss/loss.py.
+ *  SGLM_FAM_SQUARED   : 0.5 (eta - y)^2, identity link (LinearRegression / Ridge /
+ *                       TweedieRegressor(power=0) objectives; backend/sglm.py:96-105,116).
+ *  SGLM_FAM_TWEEDIE_LOG: HalfTweedieLoss(power) with log link, power in [1, 2] covers
+ *                       Poisson (1) and Gamma (2) (backend/sglm.py:112-115). */
+enum sglm_family { SGLM_FAM_SQUARED = 0, SGLM_FAM_TWEEDIE_LOG = 1 };
+
+enum sglm_xtype { SGLM_X_BF16 = 0, SGLM_X_F32 = 1 };
+
+const char* sglm_last_error(void);
+int sglm_version(void);
+
+/* --- design-matrix construction --------------------------------------------------------
+ * Generic strided timeshift/gather: out(t, j) = src(t + row0 - shift[j], src_col[j]) when
+ * that source row lies in [0, n_src), else the bit pattern `fill_bits`.  Element (r, c) of
+ * src is at src + (r * rs_src + c * cs_src) * elem_size; likewise for out.  elem_size in
+ * {1, 2, 4, 8} (int8 .. float64; NaN fill = its bit pattern).  src_col/shift are device
+ * int32 arrays of length ncols_out.
+ * Replaces: sglm_pp.shift / timeshift / timeshift_multiple (backend/sglm_pp.py:23-103,
+ * 298-486), sglm_ez.timeshift_cols (backend/sglm_ez.py:102-123) and
+ * setup_model_fit.timeshift_vals_by_dict (sglm/sglm/features/setup_model_fit.py:43-96). */
+int sglm_timeshift_expand(const void* src, int64_t n_src, int64_t rs_src, int64_t cs_src,
+                          const int32_t* src_col, const int32_t* shift, int32_t ncols_out,
+                          void* out, int64_t n_out, int64_t rs_out, int64_t cs_out,
+                          int64_t row0, int32_t elem_size, uint64_t fill_bits,
+                          sglm_stream_t stream);
+
+/* Pack a row-major (n x p) f32/f64 design (strides in elements) into the feature-major
+ * layout: Xb (bf16, required), Xf (f32, optional/nullable), ones column at a = p when
+ * add_ones, zero padding to (P, ld).  *inexact (device int32, caller-zeroed) is set to 1
+ * if any value is not exactly representable in bf16.
+ * Replaces: the float64 validation copy sklearn makes inside every fit (glm.py:191-198,
+ * X[idx_train,:] copies at backend/sglm_cv.py:107-110). */
+int sglm_pack_design(const void* src, int32_t src_is_f64, int64_t n, int32_t p,
+                     int64_t rs, int64_t cs, int32_t add_ones, uint16_t* Xb, float* Xf,
+                     int64_t ld, int32_t P, int32_t* inexact, sglm_stream_t stream);
+
+/* --- IRLS inner step (one batched Newton iteration over B fits) -------------------------
+ * Replaces the per-fit solver iterations inside self.model.fit (backend/sglm.py:241):
+ * TweedieRegressor lbfgs/newton (sklearn glm.py:266-306), Ridge cholesky (_ridge.py:201),
+ * LinearRegression lstsq (_base.py:701). */
+
+/* eta[k][i] = sum_a X[a][i] * beta[k][a]  for k < B, i < n (f32; also used for d_eta). */
+int sglm_gemv_eta(const void* X, int32_t xtype, int64_t ld, int32_t P, int64_t n,
+                  const float* beta, int32_t B, float* eta, sglm_stream_t stream);
+
+/* Link/variance update.  For fit k with response r = fit_resp[k], mask m = fit_mask[k]:
+ *   W[k][i] = M[m][i] * d2loss/deta2,   R[k][i] = M[m][i] * dloss/deta,   rows i < n.
+ * Rows n <= i < ld are written as 0. */
+int sglm_link_update(int32_t family, float power, int64_t n, int64_t ld, int32_t B,
+                     const float* eta, const float* Y, const uint8_t* M,
+                     const int32_t* fit_resp, const int32_t* fit_mask, float* W, float* R,
+                     sglm_stream_t stream);
+
+/* G[k][a] = sum_i X[a][i] * R[k][i] (float64 out; f32 MFMA partial sums, fixed-order
+ * float64 reduction over row chunks).  `work`: sglm_xtr_work_bytes(P, B, n). */
+size_t sglm_xtr_work_bytes(int32_t P, int32_t B, int64_t n);
+int sglm_xtr(const void* X, int32_t xtype, int64_t ld, int32_t P, int64_t n,
+             const float* R, int32_t B, double* G, void* work, sglm_stream_t stream);
+
+/* Batched weighted Gram, the X^T W X contraction, bf16 MFMA (v_mfma_f32_32x32x16_bf16),
+ * f32 accumulate:  H[k][a][b] = sum_i X[a][i] W[k][i] X[b][i] for every fit k in
+ * fits[0..nact) and every (a, b) whose 256-tiles satisfy tile(a) <= tile(b) (upper
+ * triangle incl. diagonal tiles).  `splits` > 1 splits the rows over workgroups and
+ * reduces slabs in `work` (sglm_syrk_work_bytes) in fixed order. */
+size_t sglm_syrk_work_bytes(int32_t P, int32_t nact, int32_t splits);
+int sglm_syrk(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, const float* W,
+              const int32_t* fits, int32_t nact, int32_t splits, float* H, void* work,
+              sglm_stream_t stream);
+
+/* Same contraction from the f32 design (v_mfma_f32_32x32x2_f32, exact f32 products) for
+ * designs that are not bf16-exact, where the Gram itself must be accurate (coordinate
+ * descent, Gaussian closed forms).  128-tiles; work sized by sglm_syrk_work_bytes. */
+int sglm_syrk_f32(const float* Xf, int64_t ld, int32_t P, int64_t n, const float* W,
+                  const int32_t* fits, int32_t nact, int32_t splits, float* H, void* work,
+                  sglm_stream_t stream);
+
+/* Penalised Newton solve per fit k in fits[]:  (H_k + diag(dshift_k)) delta_k = -g_k.
+ * H_k upper triangle (as written by sglm_syrk) is overwritten by its Cholesky factor.
+ * dshift[k][a] >= 0 adds to the diagonal (ridge penalty; 0 for the intercept); a negative
+ * entry freezes coordinate a (delta = 0: padding, fit_intercept=False).  Coordinates with
+ * a zero diagonal or a pivot collapsing below 1e-6 of its diagonal are frozen too and
+ * counted in info[k]; frozen[k][a] records the frozen set.  refactor = 0 skips the
+ * factorisation and reuses the factor (and frozen set) a previous call left in H — the
+ * constant-Hessian (Gaussian) refinement path.  P must be a multiple of 64, <= 8192. */
+int sglm_chol_solve_ex(float* H, int32_t P, const int32_t* fits, int32_t nact,
+                       const double* g, const float* dshift, float* delta, int32_t* info,
+                       uint8_t* frozen, int32_t refactor, sglm_stream_t stream);
+
+/* Line search: out[k][j] = sum_i M[m][i] * loss(y_i, eta_i + t[j] * deta_i) (float64),
+ * for j < T, fits k < B.  `work`: sglm_rowsum_work_bytes(B, T, n). */
+size_t sglm_rowsum_work_bytes(int32_t B, int32_t T, int64_t n);
+int sglm_loss_trials(int32_t family, float power, int64_t n, int64_t ld, int32_t B,
+                     const float* eta, const float* deta, const float* Y, const uint8_t* M,
+                     const int32_t* fit_resp, const int32_t* fit_mask, const float* t,
+                     int32_t T, double* out, void* work, sglm_stream_t stream);
+
+/* eta[k][i] += step[k] * deta[k][i]  (host-chosen step per fit, device array). */
+int sglm_eta_axpy(int64_t n, int64_t ld, int32_t B, const float* step, const float* deta,
+                  float* eta, sglm_stream_t stream);
+
+/* Scores (GLM.score / get_residuals, backend/sglm.py:150-184, 314-331): for fit k and each
+ * set s in {0, 1} with mask sets[2k + s] (-1 = empty):
+ *   out[k][s][0] = sum_i M * (y_i - mu_i)^2,  out[k][s][1] = sum_i M * loss(y_i, eta_i),
+ * mu = inverse link(eta).  `work`: sglm_rowsum_work_bytes(B, 4, n). */
+int sglm_score_sums(int32_t family, float power, int64_t n, int64_t ld, int32_t B,
+                    const float* eta, const float* Y, const uint8_t* M,
+                    const int32_t* fit_resp, const int32_t* sets, double* out, void* work,
+                    sglm_stream_t stream);
+
+/* Lasso / ElasticNet by Gram-space cyclic coordinate descent (float64), one workgroup per
+ * fit in fits[].  H: the augmented Gram of sglm_syrk formed with W = mask (ones column at
+ * index p); c[k]: X^T (m y) (sglm_xtr of R = m y); l1[k] = alpha rho n_k,
+ * l2[k] = alpha (1 - rho) n_k.  Stops when max|dw| <= tol * max|w| over a sweep or after
+ * max_sweeps.  coef[k][0..p) = w, coef[k][p] = intercept.  p <= 4096.
+ * Replaces sklearn cd_fast.enet_coordinate_descent behind backend/sglm.py:106-110. */
+size_t sglm_enet_work_bytes(int32_t p, int32_t nact);
+int sglm_enet_cd(const float* H, int32_t P, int32_t p, const int32_t* fits, int32_t nact,
+                 const double* c, const double* l1, const double* l2,
+                 const int32_t* fit_intercept, int32_t max_sweeps, double tol, double* coef,
+                 int32_t* sweeps, void* work, sglm_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SGLM_HIP_H */

@@ -1,0 +1,495 @@
+// libsglm_hip: design construction, GEMV-class and elementwise kernels of the IRLS step.
+// (The bf16-MFMA Gram lives in syrk.hip, the batched Cholesky in chol.hip.)
+#include "common.h"
+
+#include <stdarg.h>
+#include <string.h>
+
+namespace sglm {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+int check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error("%s: %s", what, hipGetErrorString(e));
+        return SGLM_EHIP;
+    }
+    return SGLM_OK;
+}
+
+// ------------------------------------------------------------------------------ timeshift
+// One output column per blockIdx.y (grid-strided), rows grid-strided over x.  For the
+// feature-major engine layout (rs = 1) both the read of the source column segment and the
+// write of the output column are contiguous: the lag expansion is a shifted memcpy.
+template <typename T>
+__global__ void __launch_bounds__(256) timeshift_kernel(
+    const T* __restrict__ src, int64_t n_src, int64_t rs_src, int64_t cs_src,
+    const int32_t* __restrict__ src_col, const int32_t* __restrict__ shift, int32_t ncols,
+    T* __restrict__ out, int64_t n_out, int64_t rs_out, int64_t cs_out, int64_t row0, T fill) {
+    for (int j = blockIdx.y; j < ncols; j += gridDim.y) {
+        const int64_t c = src_col[j];
+        const int64_t s = shift[j];
+        for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n_out;
+             t += (int64_t)gridDim.x * blockDim.x) {
+            const int64_t r = t + row0 - s;
+            out[t * rs_out + j * cs_out] =
+                (r >= 0 && r < n_src) ? src[r * rs_src + c * cs_src] : fill;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------ pack
+// 64x64 LDS transpose: row-major f32/f64 source -> feature-major bf16 (+ f32).
+template <typename TS>
+__global__ void __launch_bounds__(256) pack_kernel(
+    const TS* __restrict__ src, int64_t n, int32_t p, int64_t rs, int64_t cs, int32_t add_ones,
+    uint16_t* __restrict__ Xb, float* __restrict__ Xf, int64_t ld, int32_t* inexact) {
+    __shared__ float tile[64][65];
+    const int64_t i0 = (int64_t)blockIdx.x * 64;
+    const int32_t a0 = blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;   // 64 x 4
+    int bad = 0;
+    for (int r = ty; r < 64; r += 4) {           // r: row i offset, tx: column a offset
+        const int64_t i = i0 + r;
+        const int32_t a = a0 + tx;
+        float v = 0.0f;
+        if (i < n) {
+            if (a < p) {
+                const TS sv = src[i * rs + (int64_t)a * cs];
+                v = (float)sv;
+            } else if (a == p && add_ones) {
+                v = 1.0f;
+            }
+        }
+        tile[r][tx] = v;
+    }
+    __syncthreads();
+    for (int c = ty; c < 64; c += 4) {           // c: column a offset, tx: row i offset
+        const float v = tile[tx][c];
+        const __bf16 hb = (__bf16)v;
+        bad |= ((float)hb != v);
+        const int64_t off = (int64_t)(a0 + c) * ld + i0 + tx;
+        Xb[off] = __builtin_bit_cast(uint16_t, hb);
+        if (Xf) Xf[off] = v;
+    }
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(inexact, 1);
+}
+
+// ------------------------------------------------------------------------------ eta
+// eta[k][i] = sum_a X[a][i] beta[k][a] — VALU, 256 rows x 32 fits per block, the beta tile
+// staged transposed in LDS and read as wave-uniform broadcasts.  (f32 VALU FMA and f32
+// MFMA have the same peak on gfx950; this op is ~1 % of an IRLS step.)
+constexpr int kEtaFits = 32;
+constexpr int kEtaChunk = 128;
+template <typename TX>
+__global__ void __launch_bounds__(256) eta_kernel(const TX* __restrict__ X, int64_t ld, int32_t P,
+                                                  const float* __restrict__ beta, int32_t B,
+                                                  float* __restrict__ eta) {
+    __shared__ float bt[kEtaChunk][kEtaFits];
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int k0 = blockIdx.y * kEtaFits;
+    float acc[kEtaFits];
+#pragma unroll
+    for (int k = 0; k < kEtaFits; ++k) acc[k] = 0.0f;
+    for (int a0 = 0; a0 < P; a0 += kEtaChunk) {
+        __syncthreads();
+        for (int e = threadIdx.x; e < kEtaChunk * kEtaFits; e += 256) {
+            const int kk = e / kEtaChunk, aa = e % kEtaChunk;
+            const int k = k0 + kk, a = a0 + aa;
+            bt[aa][kk] = (k < B && a < P) ? beta[(int64_t)k * P + a] : 0.0f;
+        }
+        __syncthreads();
+        const int na = min(kEtaChunk, P - a0);
+        for (int aa = 0; aa < na; ++aa) {
+            const float x = (float)X[(int64_t)(a0 + aa) * ld + i];
+            const f32x4* bv = reinterpret_cast<const f32x4*>(&bt[aa][0]);
+#pragma unroll
+            for (int q = 0; q < kEtaFits / 4; ++q) {
+                const f32x4 b4 = bv[q];
+                acc[4 * q + 0] += x * b4[0];
+                acc[4 * q + 1] += x * b4[1];
+                acc[4 * q + 2] += x * b4[2];
+                acc[4 * q + 3] += x * b4[3];
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < kEtaFits; ++k)
+        if (k0 + k < B) eta[(int64_t)(k0 + k) * ld + i] = acc[k];
+}
+
+// ------------------------------------------------------------------------------ link
+__global__ void __launch_bounds__(256) link_kernel(int32_t family, float power, int64_t n,
+                                                   int64_t ld, const float* __restrict__ eta,
+                                                   const float* __restrict__ Y,
+                                                   const uint8_t* __restrict__ M,
+                                                   const int32_t* __restrict__ fit_resp,
+                                                   const int32_t* __restrict__ fit_mask,
+                                                   float* __restrict__ W, float* __restrict__ R) {
+    const int k = blockIdx.y;
+    const float* e = eta + (int64_t)k * ld;
+    const float* y = Y + (int64_t)fit_resp[k] * ld;
+    const uint8_t* m = M + (int64_t)fit_mask[k] * ld;
+    float* w = W + (int64_t)k * ld;
+    float* r = R + (int64_t)k * ld;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < ld;
+         i += (int64_t)gridDim.x * 256) {
+        float wi = 0.0f, ri = 0.0f;
+        if (i < n) {
+            const float mi = (float)m[i];
+            if (mi != 0.0f) {
+                const LossOut o = half_loss(family, power, y[i], e[i]);
+                wi = mi * o.h;
+                ri = mi * o.g;
+            }
+        }
+        w[i] = wi;
+        r[i] = ri;
+    }
+}
+
+// ------------------------------------------------------------------------------ X^T R
+// G[k][a] = sum_i X[a][i] R[k][i] with v_mfma_f32_32x32x2_f32 (exact f32 products).
+// Block: 4 waves, 128 predictors x 32 fits, one row chunk.  Lane (r, h) streams 8
+// consecutive rows of predictor a0+r and of fit k0+r; MFMA step j consumes row 8h+j of the
+// 16-row group on both operands, so A and B agree on the K index by construction.
+struct XtrPlan { int32_t nz; int64_t ch; };
+static XtrPlan xtr_plan(int32_t P, int32_t B, int64_t n) {
+    const int64_t tiles = (int64_t)((P + 127) / 128) * ((B + 31) / 32);
+    int64_t nz = (2048 + tiles - 1) / tiles;
+    const int64_t maxz = (n + 1023) / 1024;
+    if (nz > maxz) nz = maxz;
+    if (nz < 1) nz = 1;
+    int64_t ch = (n + nz - 1) / nz;
+    ch = (ch + 15) / 16 * 16;
+    nz = (n + ch - 1) / ch;
+    if (nz < 1) nz = 1;
+    return {(int32_t)nz, ch};
+}
+
+template <typename TX>
+__device__ __forceinline__ void load8(const TX* p, float (&v)[8]);
+template <>
+__device__ __forceinline__ void load8<__bf16>(const __bf16* p, float (&v)[8]) {
+    const bf16x8 x = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (float)x[j];
+}
+template <>
+__device__ __forceinline__ void load8<float>(const float* p, float (&v)[8]) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(p);
+    const f32x4 b = *reinterpret_cast<const f32x4*>(p + 4);
+    v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+    v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+}
+
+template <typename TX>
+__global__ void __launch_bounds__(256) xtr_kernel(const TX* __restrict__ X, int64_t ld, int32_t P,
+                                                  int64_t n, int64_t ch,
+                                                  const float* __restrict__ R, int32_t B,
+                                                  float* __restrict__ part) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int a = blockIdx.x * 128 + wave * 32 + r;        // P is a multiple of 256
+    const int k0 = blockIdx.y * 32;
+    const int k = k0 + r;
+    const bool kval = k < B;
+    const int64_t ib = (int64_t)blockIdx.z * ch;
+    const int64_t ie = min(ib + ch, ((n + 15) / 16) * 16);   // X/R rows padded with zeros
+    const TX* xp = X + (int64_t)a * ld;
+    const float* rp = R + (int64_t)(kval ? k : 0) * ld;
+    f32x16 acc = {};
+    for (int64_t i = ib + 8 * h; i < ie; i += 16) {
+        float xv[8], rv[8];
+        load8<TX>(xp + i, xv);
+        load8<float>(rp + i, rv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float rr = kval ? rv[j] : 0.0f;
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xv[j], rr, acc, 0, 0, 0);
+        }
+    }
+    // D[row = a][col = k]: reg j -> row (j&3) + 8(j>>2) + 4h, col r
+    if (kval) {
+        float* out = part + ((int64_t)blockIdx.z * B + k) * P + blockIdx.x * 128 + wave * 32;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) out[(j & 3) + 8 * (j >> 2) + 4 * h] = acc[j];
+    }
+}
+
+__global__ void __launch_bounds__(256) reduce_f32_to_f64(const float* __restrict__ part,
+                                                         int64_t len, int32_t nz,
+                                                         double* __restrict__ out) {
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < len;
+         e += (int64_t)gridDim.x * 256) {
+        double s = 0.0;
+        for (int z = 0; z < nz; ++z) s += (double)part[(int64_t)z * len + e];
+        out[e] = s;
+    }
+}
+
+// ------------------------------------------------------------------------------ row sums
+// Deterministic two-level float64 reductions over rows: block partials, then a fixed-order
+// sum over chunks.
+constexpr int64_t kRowChunk = 8192;
+static int32_t row_chunks(int64_t n) { return (int32_t)((n + kRowChunk - 1) / kRowChunk); }
+
+__device__ __forceinline__ double block_sum_d(double v, double* sh) {
+    v = wave_sum_d(v);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) sh[wave] = v;
+    __syncthreads();
+    double s = 0.0;
+    if (threadIdx.x == 0)
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += sh[w];
+    return s;
+}
+
+constexpr int kMaxTrials = 8;
+__global__ void __launch_bounds__(256) loss_trials_kernel(
+    int32_t family, float power, int64_t n, int64_t ld, const float* __restrict__ eta,
+    const float* __restrict__ deta, const float* __restrict__ Y, const uint8_t* __restrict__ M,
+    const int32_t* __restrict__ fit_resp, const int32_t* __restrict__ fit_mask,
+    const float* __restrict__ tv, int32_t T, double* __restrict__ part) {
+    __shared__ double sh[4];
+    const int k = blockIdx.y;
+    const int32_t nchunks = gridDim.x;
+    const float* e = eta + (int64_t)k * ld;
+    const float* d = deta + (int64_t)k * ld;
+    const float* y = Y + (int64_t)fit_resp[k] * ld;
+    const uint8_t* m = M + (int64_t)fit_mask[k] * ld;
+    double acc[kMaxTrials];
+    for (int j = 0; j < kMaxTrials; ++j) acc[j] = 0.0;
+    const int64_t i0 = (int64_t)blockIdx.x * kRowChunk;
+    const int64_t i1 = min(i0 + kRowChunk, n);
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += 256) {
+        const double mi = (double)m[i];
+        if (mi == 0.0) continue;
+        const double yi = y[i], ei = e[i], di = d[i];
+        for (int j = 0; j < T; ++j)
+            acc[j] += mi * half_loss_d(family, (double)power, yi, ei + (double)tv[j] * di);
+    }
+    for (int j = 0; j < T; ++j) {
+        const double s = block_sum_d(acc[j], sh);
+        if (threadIdx.x == 0) part[((int64_t)k * T + j) * nchunks + blockIdx.x] = s;
+    }
+}
+
+__global__ void __launch_bounds__(256) score_kernel(
+    int32_t family, float power, int64_t n, int64_t ld, const float* __restrict__ eta,
+    const float* __restrict__ Y, const uint8_t* __restrict__ M,
+    const int32_t* __restrict__ fit_resp, const int32_t* __restrict__ sets,
+    double* __restrict__ part) {
+    __shared__ double sh[4];
+    const int k = blockIdx.y;
+    const int32_t nchunks = gridDim.x;
+    const float* e = eta + (int64_t)k * ld;
+    const float* y = Y + (int64_t)fit_resp[k] * ld;
+    const int s0 = sets[2 * k], s1 = sets[2 * k + 1];
+    const uint8_t* m0 = s0 >= 0 ? M + (int64_t)s0 * ld : nullptr;
+    const uint8_t* m1 = s1 >= 0 ? M + (int64_t)s1 * ld : nullptr;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    const int64_t i0 = (int64_t)blockIdx.x * kRowChunk;
+    const int64_t i1 = min(i0 + kRowChunk, n);
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += 256) {
+        const double w0 = m0 ? (double)m0[i] : 0.0;
+        const double w1 = m1 ? (double)m1[i] : 0.0;
+        if (w0 == 0.0 && w1 == 0.0) continue;
+        const double yi = y[i], ei = e[i];
+        const double mu = inv_link_d(family, ei);
+        const double r2 = (yi - mu) * (yi - mu);
+        const double l = half_loss_d(family, (double)power, yi, ei);
+        acc[0] += w0 * r2; acc[1] += w0 * l;
+        acc[2] += w1 * r2; acc[3] += w1 * l;
+    }
+    for (int q = 0; q < 4; ++q) {
+        const double s = block_sum_d(acc[q], sh);
+        if (threadIdx.x == 0) part[((int64_t)k * 4 + q) * nchunks + blockIdx.x] = s;
+    }
+}
+
+__global__ void __launch_bounds__(256) reduce_chunks_d(const double* __restrict__ part,
+                                                       int64_t rows, int32_t nchunks,
+                                                       double* __restrict__ out) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= rows) return;
+    double s = 0.0;
+    for (int c = 0; c < nchunks; ++c) s += part[e * nchunks + c];
+    out[e] = s;
+}
+
+__global__ void __launch_bounds__(256) eta_axpy_kernel(int64_t n, int64_t ld,
+                                                       const float* __restrict__ step,
+                                                       const float* __restrict__ deta,
+                                                       float* __restrict__ eta) {
+    const int k = blockIdx.y;
+    const float t = step[k];
+    if (t == 0.0f) return;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * 256)
+        eta[(int64_t)k * ld + i] += t * deta[(int64_t)k * ld + i];
+}
+
+static unsigned grid1(int64_t work, int64_t per_block, unsigned cap = 8192) {
+    int64_t g = (work + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (unsigned)g;
+}
+
+}  // namespace sglm
+
+using namespace sglm;
+
+extern "C" {
+
+const char* sglm_last_error(void) { return g_err; }
+int sglm_version(void) { return 1; }
+
+int sglm_timeshift_expand(const void* src, int64_t n_src, int64_t rs_src, int64_t cs_src,
+                          const int32_t* src_col, const int32_t* shift, int32_t ncols_out,
+                          void* out, int64_t n_out, int64_t rs_out, int64_t cs_out,
+                          int64_t row0, int32_t elem_size, uint64_t fill_bits,
+                          sglm_stream_t stream) {
+    if (ncols_out <= 0 || n_out <= 0) return SGLM_OK;
+    if (!src || !out || !src_col || !shift || n_src < 0) {
+        set_error("sglm_timeshift_expand: null pointer or negative size");
+        return SGLM_EINVAL;
+    }
+    dim3 grid(grid1(n_out, 256, 1024), (unsigned)(ncols_out < 32768 ? ncols_out : 32768));
+    hipStream_t s = as_stream(stream);
+    switch (elem_size) {
+        case 1: timeshift_kernel<uint8_t><<<grid, 256, 0, s>>>((const uint8_t*)src, n_src, rs_src, cs_src, src_col, shift, ncols_out, (uint8_t*)out, n_out, rs_out, cs_out, row0, (uint8_t)fill_bits); break;
+        case 2: timeshift_kernel<uint16_t><<<grid, 256, 0, s>>>((const uint16_t*)src, n_src, rs_src, cs_src, src_col, shift, ncols_out, (uint16_t*)out, n_out, rs_out, cs_out, row0, (uint16_t)fill_bits); break;
+        case 4: timeshift_kernel<uint32_t><<<grid, 256, 0, s>>>((const uint32_t*)src, n_src, rs_src, cs_src, src_col, shift, ncols_out, (uint32_t*)out, n_out, rs_out, cs_out, row0, (uint32_t)fill_bits); break;
+        case 8: timeshift_kernel<uint64_t><<<grid, 256, 0, s>>>((const uint64_t*)src, n_src, rs_src, cs_src, src_col, shift, ncols_out, (uint64_t*)out, n_out, rs_out, cs_out, row0, (uint64_t)fill_bits); break;
+        default: set_error("sglm_timeshift_expand: elem_size %d not in {1,2,4,8}", elem_size); return SGLM_EINVAL;
+    }
+    return check_launch("timeshift_kernel");
+}
+
+int sglm_pack_design(const void* src, int32_t src_is_f64, int64_t n, int32_t p, int64_t rs,
+                     int64_t cs, int32_t add_ones, uint16_t* Xb, float* Xf, int64_t ld,
+                     int32_t P, int32_t* inexact, sglm_stream_t stream) {
+    if (!Xb || !inexact || (n > 0 && p > 0 && !src)) { set_error("sglm_pack_design: null pointer"); return SGLM_EINVAL; }
+    if (ld % 64 || P % 64 || ld < n || P < p + (add_ones ? 1 : 0)) {
+        set_error("sglm_pack_design: bad padding ld=%lld P=%d n=%lld p=%d", (long long)ld, P, (long long)n, p);
+        return SGLM_EINVAL;
+    }
+    dim3 grid((unsigned)(ld / 64), (unsigned)(P / 64));
+    hipStream_t s = as_stream(stream);
+    if (src_is_f64)
+        pack_kernel<double><<<grid, 256, 0, s>>>((const double*)src, n, p, rs, cs, add_ones, Xb, Xf, ld, inexact);
+    else
+        pack_kernel<float><<<grid, 256, 0, s>>>((const float*)src, n, p, rs, cs, add_ones, Xb, Xf, ld, inexact);
+    return check_launch("pack_kernel");
+}
+
+int sglm_gemv_eta(const void* X, int32_t xtype, int64_t ld, int32_t P, int64_t n,
+                  const float* beta, int32_t B, float* eta, sglm_stream_t stream) {
+    if (B <= 0) return SGLM_OK;
+    if (!X || !beta || !eta || ld % 256 || P % 256) { set_error("sglm_gemv_eta: bad args"); return SGLM_EINVAL; }
+    (void)n;
+    dim3 grid((unsigned)(ld / 256), (unsigned)((B + kEtaFits - 1) / kEtaFits));
+    hipStream_t s = as_stream(stream);
+    if (xtype == SGLM_X_BF16)
+        eta_kernel<__bf16><<<grid, 256, 0, s>>>((const __bf16*)X, ld, P, beta, B, eta);
+    else
+        eta_kernel<float><<<grid, 256, 0, s>>>((const float*)X, ld, P, beta, B, eta);
+    return check_launch("eta_kernel");
+}
+
+int sglm_link_update(int32_t family, float power, int64_t n, int64_t ld, int32_t B,
+                     const float* eta, const float* Y, const uint8_t* M,
+                     const int32_t* fit_resp, const int32_t* fit_mask, float* W, float* R,
+                     sglm_stream_t stream) {
+    if (B <= 0) return SGLM_OK;
+    if (!eta || !Y || !M || !fit_resp || !fit_mask || !W || !R) { set_error("sglm_link_update: null pointer"); return SGLM_EINVAL; }
+    dim3 grid(grid1(ld, 256, 1024), (unsigned)B);
+    link_kernel<<<grid, 256, 0, as_stream(stream)>>>(family, power, n, ld, eta, Y, M, fit_resp, fit_mask, W, R);
+    return check_launch("link_kernel");
+}
+
+size_t sglm_xtr_work_bytes(int32_t P, int32_t B, int64_t n) {
+    const XtrPlan pl = xtr_plan(P, B, n);
+    return (size_t)pl.nz * (size_t)B * (size_t)P * sizeof(float);
+}
+
+int sglm_xtr(const void* X, int32_t xtype, int64_t ld, int32_t P, int64_t n, const float* R,
+             int32_t B, double* G, void* work, sglm_stream_t stream) {
+    if (B <= 0) return SGLM_OK;
+    if (!X || !R || !G || !work || P % 256 || ld % 256 || n > ld) { set_error("sglm_xtr: bad args"); return SGLM_EINVAL; }
+    const XtrPlan pl = xtr_plan(P, B, n);
+    dim3 grid((unsigned)(P / 128), (unsigned)((B + 31) / 32), (unsigned)pl.nz);
+    hipStream_t s = as_stream(stream);
+    float* part = (float*)work;
+    if (xtype == SGLM_X_BF16)
+        xtr_kernel<__bf16><<<grid, 256, 0, s>>>((const __bf16*)X, ld, P, n, pl.ch, R, B, part);
+    else
+        xtr_kernel<float><<<grid, 256, 0, s>>>((const float*)X, ld, P, n, pl.ch, R, B, part);
+    int st = check_launch("xtr_kernel");
+    if (st) return st;
+    const int64_t len = (int64_t)B * P;
+    reduce_f32_to_f64<<<grid1(len, 256, 4096), 256, 0, s>>>(part, len, pl.nz, G);
+    return check_launch("reduce_f32_to_f64");
+}
+
+size_t sglm_rowsum_work_bytes(int32_t B, int32_t T, int64_t n) {
+    return (size_t)B * (size_t)T * (size_t)row_chunks(n) * sizeof(double);
+}
+
+int sglm_loss_trials(int32_t family, float power, int64_t n, int64_t ld, int32_t B,
+                     const float* eta, const float* deta, const float* Y, const uint8_t* M,
+                     const int32_t* fit_resp, const int32_t* fit_mask, const float* t,
+                     int32_t T, double* out, void* work, sglm_stream_t stream) {
+    if (B <= 0) return SGLM_OK;
+    if (T < 1 || T > kMaxTrials || !eta || !deta || !Y || !M || !t || !out || !work) {
+        set_error("sglm_loss_trials: bad args (T=%d)", T);
+        return SGLM_EINVAL;
+    }
+    (void)ld;
+    const int32_t nc = row_chunks(n);
+    hipStream_t s = as_stream(stream);
+    loss_trials_kernel<<<dim3((unsigned)nc, (unsigned)B), 256, 0, s>>>(family, power, n, ld, eta, deta, Y, M, fit_resp, fit_mask, t, T, (double*)work);
+    int st = check_launch("loss_trials_kernel");
+    if (st) return st;
+    const int64_t rows = (int64_t)B * T;
+    reduce_chunks_d<<<grid1(rows, 256), 256, 0, s>>>((const double*)work, rows, nc, out);
+    return check_launch("reduce_chunks_d");
+}
+
+int sglm_eta_axpy(int64_t n, int64_t ld, int32_t B, const float* step, const float* deta,
+                  float* eta, sglm_stream_t stream) {
+    if (B <= 0) return SGLM_OK;
+    if (!step || !deta || !eta) { set_error("sglm_eta_axpy: null pointer"); return SGLM_EINVAL; }
+    dim3 grid(grid1(n, 256, 1024), (unsigned)B);
+    eta_axpy_kernel<<<grid, 256, 0, as_stream(stream)>>>(n, ld, step, deta, eta);
+    return check_launch("eta_axpy_kernel");
+}
+
+int sglm_score_sums(int32_t family, float power, int64_t n, int64_t ld, int32_t B,
+                    const float* eta, const float* Y, const uint8_t* M,
+                    const int32_t* fit_resp, const int32_t* sets, double* out, void* work,
+                    sglm_stream_t stream) {
+    if (B <= 0) return SGLM_OK;
+    if (!eta || !Y || !M || !fit_resp || !sets || !out || !work) { set_error("sglm_score_sums: null pointer"); return SGLM_EINVAL; }
+    const int32_t nc = row_chunks(n);
+    hipStream_t s = as_stream(stream);
+    score_kernel<<<dim3((unsigned)nc, (unsigned)B), 256, 0, s>>>(family, power, n, ld, eta, Y, M, fit_resp, sets, (double*)work);
+    int st = check_launch("score_kernel");
+    if (st) return st;
+    const int64_t rows = (int64_t)B * 4;
+    reduce_chunks_d<<<grid1(rows, 256), 256, 0, s>>>((const double*)work, rows, nc, out);
+    return check_launch("reduce_chunks_d");
+}
+
+}  // extern "C"

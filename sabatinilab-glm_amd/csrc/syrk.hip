@@ -1,0 +1,338 @@
+// Batched weighted Gram  H_k = X^T diag(w_k) X  — the dominant IRLS kernel.
+//
+// Replaces the Hessian work of every solver iteration inside self.model.fit
+// (backend/sglm.py:241): sklearn's X^T diag(h) X for newton-cholesky / the X^T X of Ridge's
+// cholesky (_ridge.py:201-213) and, for lbfgs, the 2 GEMVs per evaluation it stands in for.
+//
+// Geometry (gfx950):
+//   * one workgroup = one 256x256 output tile (ti <= tj, upper triangle) of one fit,
+//     512 threads = 8 waves in a 2 (rows) x 4 (cols) grid, each wave 128 x 64 =
+//     4 x 2 tiles of v_mfma_f32_32x32x16_bf16 (128 f32 accumulators per lane);
+//   * K loop over rows of X in steps of BK = 32 (two 16-deep MFMA sub-steps);
+//   * X is feature-major, so a tile's K-slice of predictor a is 64 contiguous bytes:
+//     A panel = X[a0..a0+255][i..i+31] (unscaled), B panel = w_i * X[b0..b0+255][i..i+31]
+//     (scaled once while staging, in registers, then rounded to bf16);
+//   * LDS: 2 stages x 2 panels x 256 predictors x 80-byte rows (64 B + 16 B pad);
+//     the 20-dword row stride makes the 16-lane ds_read_b128 groups conflict-free
+//     (5r mod 16 is a bijection);
+//   * register-staged double buffering: tile t+1's global loads are issued before the
+//     MFMAs of tile t and written to the other LDS stage after them; one barrier per step.
+//   * optional split-K over rows (blockIdx.y) into fixed-order f32 slabs.
+#include "common.h"
+
+namespace sglm {
+
+constexpr int kBM = 256;       // output tile edge
+constexpr int kBK = 32;        // rows of X per K-step
+constexpr int kThreads = 512;
+constexpr int kRow = 40;       // bf16 elements per LDS predictor row (32 + 8 pad) = 80 B
+constexpr int kPanel = kBM * kRow;          // elements per panel
+constexpr int kStage = 2 * kPanel;          // A + B
+
+__device__ __forceinline__ void tile_coords(int t, int nt, int& ti, int& tj) {
+    // enumerate upper-triangular tiles row by row: (0,0),(0,1)..(0,nt-1),(1,1)...
+    ti = 0;
+    int rowlen = nt;
+    while (t >= rowlen) { t -= rowlen; ++ti; --rowlen; }
+    tj = ti + t;
+}
+
+__global__ void __launch_bounds__(kThreads) syrk_kernel(
+    const uint16_t* __restrict__ Xb, int64_t ld, int32_t P, int64_t nsteps_total,
+    int64_t steps_per_split, const float* __restrict__ W, const int32_t* __restrict__ fits,
+    int32_t ntiles, float* __restrict__ H, float* __restrict__ slab, int32_t nact) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+
+    const int nt = P / kBM;
+    const int tile = blockIdx.x % ntiles;
+    const int slot = blockIdx.x / ntiles;
+    const int split = blockIdx.y;
+    int ti, tj;
+    tile_coords(tile, nt, ti, tj);
+    const int fit = fits[slot];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 2, wc = wave & 3;   // 2 x 4 waves
+    const int r = lane & 31, h = lane >> 5;
+
+    const int64_t step0 = (int64_t)split * steps_per_split;
+    int64_t step1 = step0 + steps_per_split;
+    if (step1 > nsteps_total) step1 = nsteps_total;
+    const int64_t nsteps = step1 - step0;
+
+    const uint16_t* XA = Xb + (int64_t)(ti * kBM) * ld;
+    const uint16_t* XB = Xb + (int64_t)(tj * kBM) * ld;
+    const float* w = W + (int64_t)fit * ld;
+
+    // staging assignment: chunk q = tid + 512u (u = 0, 1): predictor col = q >> 2, part = q & 3
+    const int c0 = tid >> 2, part = tid & 3;
+    const int c1 = c0 + 128;
+
+    uint4 ra0, ra1, rb0, rb1;
+    f32x4 w0, w1;
+
+    auto gload = [&](int64_t step) {
+        const int64_t i = step * kBK + part * 8;
+        ra0 = *reinterpret_cast<const uint4*>(XA + (int64_t)c0 * ld + i);
+        ra1 = *reinterpret_cast<const uint4*>(XA + (int64_t)c1 * ld + i);
+        rb0 = *reinterpret_cast<const uint4*>(XB + (int64_t)c0 * ld + i);
+        rb1 = *reinterpret_cast<const uint4*>(XB + (int64_t)c1 * ld + i);
+        w0 = *reinterpret_cast<const f32x4*>(w + i);
+        w1 = *reinterpret_cast<const f32x4*>(w + i + 4);
+    };
+    auto scale = [&](uint4 v) -> uint4 {
+        const uint32_t in[4] = {v.x, v.y, v.z, v.w};
+        uint32_t o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float lo = __uint_as_float(in[q] << 16) * (q < 2 ? w0[2 * q] : w1[2 * q - 4]);
+            const float hi = __uint_as_float(in[q] & 0xffff0000u) * (q < 2 ? w0[2 * q + 1] : w1[2 * q - 3]);
+            const __bf16 blo = (__bf16)lo, bhi = (__bf16)hi;
+            o[q] = (uint32_t)__builtin_bit_cast(uint16_t, blo) |
+                   ((uint32_t)__builtin_bit_cast(uint16_t, bhi) << 16);
+        }
+        return make_uint4(o[0], o[1], o[2], o[3]);
+    };
+    auto swrite = [&](int stage) {
+        uint16_t* A = smem + stage * kStage;
+        uint16_t* Bp = A + kPanel;
+        *reinterpret_cast<uint4*>(A + c0 * kRow + part * 8) = ra0;
+        *reinterpret_cast<uint4*>(A + c1 * kRow + part * 8) = ra1;
+        *reinterpret_cast<uint4*>(Bp + c0 * kRow + part * 8) = scale(rb0);
+        *reinterpret_cast<uint4*>(Bp + c1 * kRow + part * 8) = scale(rb1);
+    };
+
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) acc[m][n] = (f32x16){};
+
+    if (nsteps > 0) {
+        gload(step0);
+        swrite(0);
+        __syncthreads();
+        for (int64_t s = 0; s < nsteps; ++s) {
+            const int stage = (int)(s & 1);
+            if (s + 1 < nsteps) gload(step0 + s + 1);
+            const uint16_t* A = smem + stage * kStage;
+            const uint16_t* Bp = A + kPanel;
+#pragma unroll
+            for (int ks = 0; ks < kBK / 16; ++ks) {
+                bf16x8 af[4], bfr[2];
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+                    af[m] = *reinterpret_cast<const bf16x8*>(
+                        A + (wr * 128 + m * 32 + r) * kRow + ks * 16 + h * 8);
+#pragma unroll
+                for (int n = 0; n < 2; ++n)
+                    bfr[n] = *reinterpret_cast<const bf16x8*>(
+                        Bp + (wc * 64 + n * 32 + r) * kRow + ks * 16 + h * 8);
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+#pragma unroll
+                    for (int n = 0; n < 2; ++n)
+                        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[m], bfr[n],
+                                                                            acc[m][n], 0, 0, 0);
+            }
+            if (s + 1 < nsteps) swrite(stage ^ 1);
+            __syncthreads();
+        }
+    }
+
+    // epilogue: D[row][col], reg j -> row (j&3) + 8(j>>2) + 4h, col r
+    float* out;
+    int64_t ldo = P;
+    if (slab) out = slab + ((int64_t)split * nact + slot) * (int64_t)P * P;
+    else out = H + (int64_t)fit * P * P;
+    const int64_t rbase = (int64_t)ti * kBM + wr * 128;
+    const int64_t cbase = (int64_t)tj * kBM + wc * 64;
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int64_t row = rbase + m * 32 + (j & 3) + 8 * (j >> 2) + 4 * h;
+                const int64_t col = cbase + n * 32 + r;
+                out[row * ldo + col] = acc[m][n][j];
+            }
+}
+
+// Sum the split slabs (fixed order) into H for the upper-triangular tiles only.
+__global__ void __launch_bounds__(256) syrk_reduce(const float* __restrict__ slab, int32_t P,
+                                                   int32_t nact, int32_t splits,
+                                                   const int32_t* __restrict__ fits,
+                                                   float* __restrict__ H) {
+    const int slot = blockIdx.y;
+    const int64_t PP = (int64_t)P * P;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < PP;
+         e += (int64_t)gridDim.x * 256) {
+        const int64_t a = e / P, b = e % P;
+        if (a / kBM > b / kBM) continue;
+        float s = 0.0f;
+        for (int z = 0; z < splits; ++z) s += slab[((int64_t)z * nact + slot) * PP + e];
+        H[(int64_t)fits[slot] * PP + e] = s;
+    }
+}
+
+}  // namespace sglm
+
+using namespace sglm;
+
+extern "C" {
+
+size_t sglm_syrk_work_bytes(int32_t P, int32_t nact, int32_t splits) {
+    if (splits <= 1) return 0;
+    return (size_t)splits * (size_t)nact * (size_t)P * (size_t)P * sizeof(float);
+}
+
+int sglm_syrk(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, const float* W,
+              const int32_t* fits, int32_t nact, int32_t splits, float* H, void* work,
+              sglm_stream_t stream) {
+    if (nact <= 0) return SGLM_OK;
+    if (!Xb || !W || !fits || !H || P % kBM || ld % kBK || n > ld || splits < 1 ||
+        (splits > 1 && !work)) {
+        set_error("sglm_syrk: bad args (P=%d ld=%lld n=%lld splits=%d)", P, (long long)ld,
+                  (long long)n, splits);
+        return SGLM_EINVAL;
+    }
+    const int nt = P / kBM;
+    const int ntiles = nt * (nt + 1) / 2;
+    const int64_t nsteps_total = (n + kBK - 1) / kBK;     // rows >= n carry w = 0
+    const int64_t sps = (nsteps_total + splits - 1) / splits;
+    const size_t lds = (size_t)2 * kStage * sizeof(uint16_t);
+    hipStream_t s = as_stream(stream);
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)syrk_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+        attr_set = true;
+    }
+    dim3 grid((unsigned)(ntiles * nact), (unsigned)splits);
+    float* slab = splits > 1 ? (float*)work : nullptr;
+    syrk_kernel<<<grid, kThreads, lds, s>>>(Xb, ld, P, nsteps_total, sps, W, fits, ntiles, H,
+                                            slab, nact);
+    int st = check_launch("syrk_kernel");
+    if (st || splits == 1) return st;
+    const int64_t PP = (int64_t)P * P;
+    unsigned gx = (unsigned)((PP + 255) / 256 < 4096 ? (PP + 255) / 256 : 4096);
+    syrk_reduce<<<dim3(gx, (unsigned)nact), 256, 0, s>>>(slab, P, nact, splits, fits, H);
+    return check_launch("syrk_reduce");
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------
+// Exact-f32 variant for designs that are not bf16-representable (real-valued predictors):
+// v_mfma_f32_32x32x2_f32 (exact f32 products, f32 accumulate).  Used where the Gram itself
+// must be accurate (coordinate descent, Gaussian closed forms); IRLS on such designs keeps
+// the bf16 Gram because the exact gradient corrects the Newton step.
+// 128x128 tile, 256 threads = 4 waves (2x2), each wave 64x64 = 2x2 tiles of 32x32;
+// K-step 16 rows; LDS panels [128 predictors][16 rows + 1 pad] f32.
+namespace sglm {
+constexpr int kFBM = 128, kFBK = 16, kFRow = kFBK + 1;
+
+__global__ void __launch_bounds__(256) syrk_f32_kernel(
+    const float* __restrict__ Xf, int64_t ld, int32_t P, int64_t nsteps_total,
+    int64_t steps_per_split, const float* __restrict__ W, const int32_t* __restrict__ fits,
+    int32_t ntiles, float* __restrict__ H, float* __restrict__ slab, int32_t nact) {
+    __shared__ float sA[kFBM][kFRow];
+    __shared__ float sB[kFBM][kFRow];
+    const int nt = P / kFBM;
+    const int tile = blockIdx.x % ntiles;
+    const int slot = blockIdx.x / ntiles;
+    const int split = blockIdx.y;
+    int ti, tj;
+    tile_coords(tile, nt, ti, tj);
+    const int fit = fits[slot];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t s0 = (int64_t)split * steps_per_split;
+    const int64_t s1 = min(s0 + steps_per_split, nsteps_total);
+    const float* XA = Xf + (int64_t)ti * kFBM * ld;
+    const float* XB = Xf + (int64_t)tj * kFBM * ld;
+    const float* w = W + (int64_t)fit * ld;
+    f32x16 acc[2][2];
+    for (int m = 0; m < 2; ++m)
+        for (int q = 0; q < 2; ++q) acc[m][q] = (f32x16){};
+    // staging: 128 predictors x 16 rows = 2048 floats per panel, 8 per thread (2 x f32x4)
+    const int col = tid >> 1, part = (tid & 1) * 8;
+    for (int64_t s = s0; s < s1; ++s) {
+        const int64_t i = s * kFBK + part;
+        const f32x4 a0 = *reinterpret_cast<const f32x4*>(XA + (int64_t)col * ld + i);
+        const f32x4 a1 = *reinterpret_cast<const f32x4*>(XA + (int64_t)col * ld + i + 4);
+        const f32x4 b0 = *reinterpret_cast<const f32x4*>(XB + (int64_t)col * ld + i);
+        const f32x4 b1 = *reinterpret_cast<const f32x4*>(XB + (int64_t)col * ld + i + 4);
+        const f32x4 w0 = *reinterpret_cast<const f32x4*>(w + i);
+        const f32x4 w1 = *reinterpret_cast<const f32x4*>(w + i + 4);
+        __syncthreads();
+        for (int e = 0; e < 4; ++e) {
+            sA[col][part + e] = a0[e];
+            sA[col][part + 4 + e] = a1[e];
+            sB[col][part + e] = b0[e] * w0[e];
+            sB[col][part + 4 + e] = b1[e] * w1[e];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kFBK; k += 2) {
+            float av[2], bv[2];
+            for (int m = 0; m < 2; ++m) av[m] = sA[wr * 64 + m * 32 + r][k + h];
+            for (int q = 0; q < 2; ++q) bv[q] = sB[wc * 64 + q * 32 + r][k + h];
+            for (int m = 0; m < 2; ++m)
+                for (int q = 0; q < 2; ++q)
+                    acc[m][q] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m], bv[q], acc[m][q], 0, 0, 0);
+        }
+    }
+    float* out = slab ? slab + ((int64_t)split * nact + slot) * (int64_t)P * P
+                      : H + (int64_t)fit * P * P;
+    const int64_t rb = (int64_t)ti * kFBM + wr * 64, cb = (int64_t)tj * kFBM + wc * 64;
+    for (int m = 0; m < 2; ++m)
+        for (int q = 0; q < 2; ++q)
+            for (int j = 0; j < 16; ++j)
+                out[(rb + m * 32 + (j & 3) + 8 * (j >> 2) + 4 * h) * P + cb + q * 32 + r] = acc[m][q][j];
+}
+
+__global__ void __launch_bounds__(256) syrk_reduce_t(const float* __restrict__ slab, int32_t P,
+                                                     int32_t nact, int32_t splits, int32_t tbm,
+                                                     const int32_t* __restrict__ fits,
+                                                     float* __restrict__ H) {
+    const int slot = blockIdx.y;
+    const int64_t PP = (int64_t)P * P;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < PP;
+         e += (int64_t)gridDim.x * 256) {
+        const int64_t a = e / P, b = e % P;
+        if (a / tbm > b / tbm) continue;
+        float s = 0.0f;
+        for (int z = 0; z < splits; ++z) s += slab[((int64_t)z * nact + slot) * PP + e];
+        H[(int64_t)fits[slot] * PP + e] = s;
+    }
+}
+}  // namespace sglm
+
+extern "C" int sglm_syrk_f32(const float* Xf, int64_t ld, int32_t P, int64_t n, const float* W,
+                             const int32_t* fits, int32_t nact, int32_t splits, float* H,
+                             void* work, sglm_stream_t stream) {
+    if (nact <= 0) return SGLM_OK;
+    if (!Xf || !W || !fits || !H || P % kFBM || ld % kFBK || n > ld || splits < 1 ||
+        (splits > 1 && !work)) {
+        set_error("sglm_syrk_f32: bad args");
+        return SGLM_EINVAL;
+    }
+    const int nt = P / kFBM;
+    const int ntiles = nt * (nt + 1) / 2;
+    const int64_t nst = (n + kFBK - 1) / kFBK;
+    const int64_t sps = (nst + splits - 1) / splits;
+    hipStream_t s = as_stream(stream);
+    float* slab = splits > 1 ? (float*)work : nullptr;
+    syrk_f32_kernel<<<dim3((unsigned)(ntiles * nact), (unsigned)splits), 256, 0, s>>>(
+        Xf, ld, P, nst, sps, W, fits, ntiles, H, slab, nact);
+    int st = check_launch("syrk_f32_kernel");
+    if (st || splits == 1) return st;
+    const int64_t PP = (int64_t)P * P;
+    unsigned gx = (unsigned)((PP + 255) / 256 < 4096 ? (PP + 255) / 256 : 4096);
+    syrk_reduce_t<<<dim3(gx, (unsigned)nact), 256, 0, s>>>(slab, P, nact, splits, kFBM, fits, H);
+    return check_launch("syrk_reduce_t");
+}

@@ -1,0 +1,87 @@
+"""ctypes binding of libsglm_hip.so (C ABI: include/sglm_hip.h).
+
+There is no fallback: if the shared library is missing or no ROCm GPU is visible, every
+entry point raises ``HipEngineUnavailable``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsglm_hip.so")
+
+_i32, _i64, _u64, _f32, _vp, _sz = C.c_int32, C.c_int64, C.c_uint64, C.c_float, C.c_void_p, C.c_size_t
+
+# name -> (restype, argtypes); kept in the order of include/sglm_hip.h
+SIGNATURES = {
+    "sglm_last_error": (C.c_char_p, []),
+    "sglm_version": (C.c_int, []),
+    "sglm_timeshift_expand": (C.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _i32, _vp, _i64, _i64,
+                                        _i64, _i64, _i32, _u64, _vp]),
+    "sglm_pack_design": (C.c_int, [_vp, _i32, _i64, _i32, _i64, _i64, _i32, _vp, _vp, _i64,
+                                   _i32, _vp, _vp]),
+    "sglm_gemv_eta": (C.c_int, [_vp, _i32, _i64, _i32, _i64, _vp, _i32, _vp, _vp]),
+    "sglm_link_update": (C.c_int, [_i32, _f32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
+                                   _vp, _vp]),
+    "sglm_xtr_work_bytes": (_sz, [_i32, _i32, _i64]),
+    "sglm_xtr": (C.c_int, [_vp, _i32, _i64, _i32, _i64, _vp, _i32, _vp, _vp, _vp]),
+    "sglm_syrk_work_bytes": (_sz, [_i32, _i32, _i32]),
+    "sglm_syrk": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
+    "sglm_syrk_f32": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
+    "sglm_chol_solve_ex": (C.c_int, [_vp, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp]),
+    "sglm_rowsum_work_bytes": (_sz, [_i32, _i32, _i64]),
+    "sglm_loss_trials": (C.c_int, [_i32, _f32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
+                                   _vp, _i32, _vp, _vp, _vp]),
+    "sglm_eta_axpy": (C.c_int, [_i64, _i64, _i32, _vp, _vp, _vp, _vp]),
+    "sglm_score_sums": (C.c_int, [_i32, _f32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
+                                  _vp, _vp]),
+    "sglm_enet_work_bytes": (_sz, [_i32, _i32]),
+    "sglm_enet_cd": (C.c_int, [_vp, _i32, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _i32, C.c_double,
+                               _vp, _vp, _vp, _vp]),
+}
+
+
+class HipEngineUnavailable(RuntimeError):
+    """The MI355X engine cannot run here (library not built, or no GPU)."""
+
+
+class HipEngineError(RuntimeError):
+    """A libsglm_hip call returned an error status."""
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load the shared library and attach signatures (no GPU needed)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(path):
+                raise HipEngineUnavailable(
+                    f"{path} not found: build it with `python -c 'import __graft_entry__ as g; "
+                    f"g.build()'` (hipcc --offload-arch=gfx950). There is no CPU fallback.")
+            lib = C.CDLL(path)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def call(name: str, *args):
+    """Invoke an int-returning entry point and raise on a non-zero status."""
+    lib = load()
+    st = getattr(lib, name)(*args)
+    if st != 0:
+        msg = lib.sglm_last_error().decode(errors="replace")
+        raise HipEngineError(f"{name} failed with status {st}: {msg}")
+    return st
+
+
+def query(name: str, *args) -> int:
+    return int(getattr(load(), name)(*args))

@@ -1,0 +1,503 @@
+"""Batched IRLS engine on MI355X (host driver of libsglm_hip).
+
+One call to :func:`irls` runs B independent fits — the (fold x lambda) cells of a CV grid,
+or a single ``GLM.fit`` — against ONE resident design matrix.  Each fit differs only in
+its row mask (train rows of its fold, as multiplicities), its response column (``roll``),
+its penalty and its family.  The reference runs these as separate sklearn fits on copies
+``X[idx_train, :]`` (backend/sglm_cv.py:106-131); here the copies never exist.
+
+Per batched Newton iteration (all device work on the current torch stream):
+
+  link_update   W = m * loss''(eta), R = m * loss'(eta)              (elementwise)
+  xtr           g = X^T R  (f32 MFMA, float64 reduction) + lam * beta  (gradient)
+  syrk          H = X^T diag(W) X  for the still-active fits          (bf16 MFMA)
+  chol_solve    delta = -(H + lam I')^-1 g                           (per-fit Cholesky)
+  gemv_eta      d_eta = X delta
+  loss_trials   Armijo line search on sum m*loss(eta + t d_eta) + lam/2 |w + t d|^2
+  eta_axpy      eta += t d_eta
+
+The Hessian is only an approximation (bf16 operands, f32 factor); the gradient and the
+objective are computed from exact X in f32/f64, so the fixed point is the exact minimiser
+(inexact Newton, SURVEY.md §7 "Hard parts").  Gaussian (squared-loss) fits have a
+Hessian that depends only on the mask: it is formed once per distinct mask and its factor
+is reused by the refinement iterations.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+
+try:
+    import torch
+except ImportError as e:  # pragma: no cover - torch is part of the image
+    raise _lib.HipEngineUnavailable("PyTorch-ROCm is required for device memory") from e
+
+FAM_SQUARED = 0
+FAM_TWEEDIE_LOG = 1
+X_BF16, X_F32 = 0, 1
+COL_PAD = 256
+ROW_PAD = 256
+ARMIJO_SIGMA = 2.0 ** -11      # sklearn _newton_solver.py:214
+
+
+def require_gpu():
+    """Raise unless the HIP engine can run (library present AND a ROCm device visible)."""
+    _lib.load()
+    if not torch.cuda.is_available():
+        raise _lib.HipEngineUnavailable(
+            "no ROCm GPU visible: the sglm HIP engine has no CPU fallback")
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def pad_to(x, m):
+    return (int(x) + m - 1) // m * m
+
+
+# ------------------------------------------------------------------------------ design
+class Design:
+    """Design matrix resident in HBM, feature-major, with the ones column at index p.
+
+    xb: bf16 [P, ld]  (Gram operand; exact for 0/1 event designs)
+    xf: f32  [P, ld]  or None (only when X is not bf16-exact; used for eta and X^T r)
+    """
+
+    def __init__(self, n: int, p: int, device="cuda", zero=True):
+        require_gpu()
+        self.n, self.p = int(n), int(p)
+        self.P = pad_to(self.p + 1, COL_PAD)
+        self.ld = pad_to(max(self.n, 1), ROW_PAD)
+        alloc = torch.zeros if zero else torch.empty
+        self.xb = alloc((self.P, self.ld), dtype=torch.bfloat16, device=device)
+        self.xf = None
+        self.device = device
+
+    @property
+    def xtype(self):
+        return X_F32 if self.xf is not None else X_BF16
+
+    @property
+    def xg(self):
+        """Operand for the exact GEMV-class kernels."""
+        return self.xf if self.xf is not None else self.xb
+
+    @classmethod
+    def from_host(cls, X, device="cuda"):
+        """Pack a host (n x p) array / DataFrame (row-major) into HBM."""
+        if hasattr(X, "values") and not isinstance(X, np.ndarray):
+            X = X.values
+        X = np.asarray(X)
+        if X.ndim == 1:
+            X = X.reshape(-1, 1)
+        if X.dtype not in (np.float32, np.float64):
+            X = X.astype(np.float64)
+        X = np.ascontiguousarray(X)
+        n, p = X.shape
+        d = cls(n, p, device, zero=False)
+        src = torch.from_numpy(X).to(device)
+        d._pack(src, is_f64=X.dtype == np.float64, rs=p, cs=1)
+        return d
+
+    @classmethod
+    def from_device(cls, Xt, device="cuda"):
+        """Pack a device torch tensor (n x p, f32/f64, any strides)."""
+        n, p = Xt.shape
+        if Xt.dtype not in (torch.float32, torch.float64):
+            Xt = Xt.to(torch.float64)
+        d = cls(n, p, device, zero=False)
+        d._pack(Xt, is_f64=Xt.dtype == torch.float64, rs=Xt.stride(0), cs=Xt.stride(1))
+        return d
+
+    def _pack(self, src, is_f64, rs, cs):
+        flag = torch.zeros(1, dtype=torch.int32, device=self.device)
+        _lib.call("sglm_pack_design", _p(src), int(is_f64), self.n, self.p, rs, cs, 1,
+                  _p(self.xb), None, self.ld, self.P, _p(flag), _stream())
+        if int(flag.item()):
+            self.xf = torch.empty((self.P, self.ld), dtype=torch.float32, device=self.device)
+            flag.zero_()
+            _lib.call("sglm_pack_design", _p(src), int(is_f64), self.n, self.p, rs, cs, 1,
+                      _p(self.xb), _p(self.xf), self.ld, self.P, _p(flag), _stream())
+
+    @classmethod
+    def from_events(cls, E, shifts: Sequence[int], row0: int, n: int, device="cuda",
+                    event_major=False):
+        """Expand base events E (N_raw x m) into lag columns directly on the device.
+
+        Output column (shift block b, event a) = E[t + row0 - shifts[b], a] for rows
+        t < n — the shift-major layout of sglm_ez.timeshift_cols (backend/sglm_ez.py:
+        102-123) after the NaN-row drop (row0 = max positive shift), or event-major when
+        ``event_major`` (setup_model_fit.timeshift_vals_by_dict, lag order as given).
+        Source rows outside E can only occur if row0/n exceed the valid window; they are
+        filled with 0.
+        """
+        require_gpu()
+        if isinstance(E, np.ndarray):
+            E = torch.from_numpy(np.ascontiguousarray(E, dtype=np.float32))
+        E = E.to(device=device, dtype=torch.float32)
+        N_raw, m = E.shape
+        K = len(shifts)
+        p = K * m
+        d = cls(n, p, device, zero=True)
+        Eb = E.t().contiguous().to(torch.bfloat16)          # feature-major bf16 (m, N_raw)
+        exact = bool(torch.equal(Eb.float(), E.t()))
+        if event_major:
+            cols = np.repeat(np.arange(m), K)
+            sh = np.tile(np.asarray(shifts), m)
+        else:
+            cols = np.tile(np.arange(m), K)
+            sh = np.repeat(np.asarray(shifts), m)
+        cols_d = torch.tensor(cols, dtype=torch.int32, device=device)
+        sh_d = torch.tensor(sh, dtype=torch.int32, device=device)
+        _lib.call("sglm_timeshift_expand", _p(Eb), N_raw, 1, N_raw, _p(cols_d), _p(sh_d), p,
+                  _p(d.xb), n, 1, d.ld, row0, 2, 0, _stream())
+        d.xb[p, :n] = 1.0
+        if not exact:
+            Ef = E.t().contiguous()
+            d.xf = torch.zeros((d.P, d.ld), dtype=torch.float32, device=device)
+            _lib.call("sglm_timeshift_expand", _p(Ef), N_raw, 1, N_raw, _p(cols_d), _p(sh_d),
+                      p, _p(d.xf), n, 1, d.ld, row0, 4, 0, _stream())
+            d.xf[p, :n] = 1.0
+        return d
+
+    def eta(self, beta_dev, out=None):
+        """eta[k] = X beta[k] for a (B, P) f32 device tensor."""
+        B = beta_dev.shape[0]
+        if out is None:
+            out = torch.empty((B, self.ld), dtype=torch.float32, device=self.device)
+        _lib.call("sglm_gemv_eta", _p(self.xg), self.xtype, self.ld, self.P, self.n,
+                  _p(beta_dev), B, _p(out), _stream())
+        return out
+
+
+# ------------------------------------------------------------------------------ problem
+class Problem:
+    """A design plus the response columns and row masks that a batch of fits refers to."""
+
+    def __init__(self, design: Design, ys: Sequence[np.ndarray], masks: Sequence[np.ndarray]):
+        self.design = design
+        n, ld, dev = design.n, design.ld, design.device
+        self.ys = [np.asarray(y, dtype=np.float64).reshape(-1) for y in ys]
+        self.masks = [np.asarray(m, dtype=np.uint8).reshape(-1) for m in masks]
+        for y in self.ys:
+            if y.shape[0] != n:
+                raise ValueError(f"response length {y.shape[0]} != n_samples {n}")
+        for m in self.masks:
+            if m.shape[0] != n:
+                raise ValueError(f"mask length {m.shape[0]} != n_samples {n}")
+        Y = np.zeros((len(self.ys), ld), dtype=np.float32)
+        for r, y in enumerate(self.ys):
+            Y[r, :n] = y
+        M = np.zeros((len(self.masks), ld), dtype=np.uint8)
+        for f, m in enumerate(self.masks):
+            M[f, :n] = m
+        self.Y = torch.from_numpy(Y).to(dev)
+        self.M = torch.from_numpy(M).to(dev)
+        self._stats = {}
+
+    def mask_stats(self, resp: int, mask: int):
+        """float64 (count, sum y, mean y) over a mask — host side, cached."""
+        key = (resp, mask)
+        if key not in self._stats:
+            m = self.masks[mask].astype(np.float64)
+            y = self.ys[resp]
+            cnt = m.sum()
+            s = float(m @ y)
+            self._stats[key] = (cnt, s, s / cnt if cnt else 0.0)
+        return self._stats[key]
+
+
+@dataclass
+class FitReq:
+    family: int
+    power: float
+    lam: float                      # penalty in units of the SUM objective (lam/2 |w|^2)
+    mask: int
+    resp: int
+    fit_intercept: bool = True
+    max_iter: int = 100
+    coef0: Optional[np.ndarray] = None
+    intercept0: Optional[float] = None
+
+
+@dataclass
+class FitResult:
+    coef: np.ndarray
+    intercept: float
+    n_iter: int
+    converged: bool
+    dropped: int = 0
+
+
+@dataclass
+class IrlsStats:
+    """Optional instrumentation: per-launch events of the Gram kernel (bench.py)."""
+    record: bool = False
+    syrk_events: list = field(default_factory=list)    # (start, end, algorithmic flop)
+    fit_iters: int = 0
+    newton_iters: int = 0
+
+
+class _Buffers:
+    """Re-usable device buffers keyed by (B, P, ld)."""
+
+    def __init__(self):
+        self.key = None
+
+    def get(self, B, P, ld, dev):
+        key = (B, P, ld)
+        if key != self.key:
+            f32 = torch.float32
+            self.beta = torch.zeros((B, P), dtype=f32, device=dev)
+            self.delta = torch.zeros((B, P), dtype=f32, device=dev)
+            self.eta = torch.zeros((B, ld), dtype=f32, device=dev)
+            self.deta = torch.zeros((B, ld), dtype=f32, device=dev)
+            self.W = torch.zeros((B, ld), dtype=f32, device=dev)
+            self.R = torch.zeros((B, ld), dtype=f32, device=dev)
+            self.H = torch.empty((B, P, P), dtype=f32, device=dev)
+            self.g = torch.zeros((B, P), dtype=torch.float64, device=dev)
+            self.gtot = torch.zeros((B, P), dtype=torch.float64, device=dev)
+            self.dshift = torch.zeros((B, P), dtype=f32, device=dev)
+            self.frozen = torch.zeros((B, P), dtype=torch.uint8, device=dev)
+            self.info = torch.zeros((B,), dtype=torch.int32, device=dev)
+            self.key = key
+        return self
+
+
+_BUF = _Buffers()
+_WORK = {}
+
+
+def _work(nbytes, dev):
+    nbytes = max(int(nbytes), 16)
+    t = _WORK.get(dev)
+    if t is None or t.numel() < nbytes:
+        t = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        _WORK[dev] = t
+    return t
+
+
+def syrk_splits(n_tiles_total: int, nsteps: int, cus: int = 256) -> int:
+    """Split the rows over workgroups when the tile count alone cannot fill the chip."""
+    best, best_eff = 1, 0.0
+    for s in (1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64):
+        if s > max(1, nsteps // 16):
+            break
+        wgs = n_tiles_total * s
+        rounds = math.ceil(wgs / cus)
+        eff = wgs / (rounds * cus)
+        if eff > best_eff + 0.02:
+            best, best_eff = s, eff
+    return best
+
+
+def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[IrlsStats] = None):
+    """Run the batched damped-Newton (IRLS) solve; returns (results, final eta tensor)."""
+    require_gpu()
+    if not reqs:
+        return [], None
+    d = prob.design
+    fam, power = reqs[0].family, float(reqs[0].power)
+    if any(r.family != fam or float(r.power) != power for r in reqs):
+        raise ValueError("irls(): one loss family per batch")
+    B, P, ld, n, p = len(reqs), d.P, d.ld, d.n, d.p
+    dev = d.device
+    bf = _BUF.get(B, P, ld, dev)
+    st = _stream()
+    log_link = fam == FAM_TWEEDIE_LOG
+
+    fit_resp = torch.tensor([r.resp for r in reqs], dtype=torch.int32, device=dev)
+    fit_mask = torch.tensor([r.mask for r in reqs], dtype=torch.int32, device=dev)
+    lam = np.array([float(r.lam) for r in reqs])
+    penal = np.zeros((B, P), dtype=np.float64)
+    penal[:, :p] = 1.0
+    dsh = np.full((B, P), -1.0, dtype=np.float32)
+    dsh[:, :p] = lam[:, None]
+    beta = np.zeros((B, P), dtype=np.float64)
+    for k, r in enumerate(reqs):
+        if r.fit_intercept:
+            dsh[k, p] = 0.0
+        if r.coef0 is not None:
+            beta[k, :p] = r.coef0
+            beta[k, p] = (r.intercept0 or 0.0) if r.fit_intercept else 0.0
+        elif r.fit_intercept:
+            cnt, s, ym = prob.mask_stats(r.resp, r.mask)
+            if log_link:
+                if ym <= 0:
+                    raise ValueError("Some value(s) of y are out of the valid range of the loss")
+                beta[k, p] = math.log(ym)
+            else:
+                beta[k, p] = ym
+    bf.dshift.copy_(torch.from_numpy(dsh))
+    bf.beta.copy_(torch.from_numpy(beta.astype(np.float32)))
+    d.eta(bf.beta, bf.eta)
+
+    const_hess = fam == FAM_SQUARED
+    active = np.ones(B, dtype=bool)
+    n_iter = np.zeros(B, dtype=np.int64)
+    converged = np.zeros(B, dtype=bool)
+    prev_rel = np.full(B, np.inf)
+    max_iter = np.array([max(1, int(r.max_iter)) for r in reqs])
+    factored = False
+    xtr_work = _work(max(_lib.query("sglm_xtr_work_bytes", P, B, n),
+                         _lib.query("sglm_rowsum_work_bytes", B, 8, n)), dev)
+    tv1 = torch.tensor([0.0, 1.0, 0.5, 0.25, 0.125], dtype=torch.float32, device=dev)
+    tv2 = torch.tensor([0.0625, 0.03125, 0.015625, 0.0078125, 2.0 ** -10, 2.0 ** -14, 2.0 ** -20],
+                       dtype=torch.float32, device=dev)
+    Ltr = torch.zeros(B * 8, dtype=torch.float64, device=dev)     # dense [B][T] per call
+    nsteps = (n + 31) // 32
+    ntile1 = (P // 256) * (P // 256 + 1) // 2
+    rows = np.array([prob.mask_stats(r.resp, r.mask)[0] for r in reqs], dtype=np.float64)
+
+    for it in range(int(max_iter.max()) + 1):
+        act = np.flatnonzero(active)
+        if act.size == 0:
+            break
+        _lib.call("sglm_link_update", fam, power, n, ld, B, _p(bf.eta), _p(prob.Y), _p(prob.M),
+                  _p(fit_resp), _p(fit_mask), _p(bf.W), _p(bf.R), st)
+        _lib.call("sglm_xtr", _p(d.xg), d.xtype, ld, P, n, _p(bf.R), B, _p(bf.g),
+                  _p(xtr_work), st)
+        g = bf.g.cpu().numpy() + lam[:, None] * penal * beta
+        # ---- Hessian
+        if const_hess:
+            if not factored:
+                reps = {}
+                for k in act:
+                    reps.setdefault(reqs[k].mask, k)
+                rep_idx = np.array(sorted(reps.values()), dtype=np.int32)
+                _syrk(d, bf, rep_idx, nsteps, ntile1, stats, st, exact=True, rows=rows)
+                for k in act:
+                    rk = reps[reqs[k].mask]
+                    if rk != k:
+                        bf.H[k].copy_(bf.H[rk])
+        else:
+            _syrk(d, bf, act.astype(np.int32), nsteps, ntile1, stats, st, rows=rows)
+        refactor = 0 if (const_hess and factored) else 1
+        bf.gtot.copy_(torch.from_numpy(g))
+        act_d = torch.tensor(act, dtype=torch.int32, device=dev)
+        bf.delta.zero_()
+        _lib.call("sglm_chol_solve_ex", _p(bf.H), P, _p(act_d), int(act.size), _p(bf.gtot),
+                  _p(bf.dshift), _p(bf.delta), _p(bf.info), _p(bf.frozen), refactor, st)
+        factored = True
+        d.eta(bf.delta, bf.deta)
+        delta = bf.delta.cpu().numpy().astype(np.float64)
+        # ---- line search
+        _lib.call("sglm_loss_trials", fam, power, n, ld, B, _p(bf.eta), _p(bf.deta), _p(prob.Y),
+                  _p(prob.M), _p(fit_resp), _p(fit_mask), _p(tv1), 5, _p(Ltr), _p(xtr_work), st)
+        L = Ltr[: B * 5].view(B, 5).cpu().numpy().copy()
+        ts = [0.0, 1.0, 0.5, 0.25, 0.125]
+        gdir = np.sum(g * delta, axis=1)
+        step = np.zeros(B)
+        need_more = []
+        for k in act:
+            obj = [L[k, j] + 0.5 * lam[k] * np.sum(penal[k] * (beta[k] + ts[j] * delta[k]) ** 2)
+                   for j in range(5)]
+            chosen = None
+            for j in range(1, 5):
+                if obj[j] - obj[0] <= ARMIJO_SIGMA * ts[j] * gdir[k] or \
+                        abs(obj[j] - obj[0]) <= 1e-13 * abs(obj[0]):
+                    chosen = ts[j]
+                    break
+            if chosen is None:
+                need_more.append(k)
+            else:
+                step[k] = chosen
+        if need_more:
+            _lib.call("sglm_loss_trials", fam, power, n, ld, B, _p(bf.eta), _p(bf.deta),
+                      _p(prob.Y), _p(prob.M), _p(fit_resp), _p(fit_mask), _p(tv2), 7, _p(Ltr),
+                      _p(xtr_work), st)
+            L2 = Ltr[: B * 7].view(B, 7).cpu().numpy()
+            ts2 = tv2.cpu().numpy().astype(np.float64)
+            for k in need_more:
+                obj0 = L[k, 0] + 0.5 * lam[k] * np.sum(penal[k] * beta[k] ** 2)
+                for j in range(7):
+                    o = L2[k, j] + 0.5 * lam[k] * np.sum(penal[k] * (beta[k] + ts2[j] * delta[k]) ** 2)
+                    if o - obj0 <= ARMIJO_SIGMA * ts2[j] * gdir[k]:
+                        step[k] = ts2[j]
+                        break
+        # ---- update
+        beta += step[:, None] * delta
+        bf.beta.copy_(torch.from_numpy(beta.astype(np.float32)))
+        step_d = torch.from_numpy(step.astype(np.float32)).to(dev)
+        _lib.call("sglm_eta_axpy", n, ld, B, _p(step_d), _p(bf.deta), _p(bf.eta), st)
+        n_iter[act] += 1
+        if stats is not None:
+            stats.newton_iters += 1
+            stats.fit_iters += int(act.size)
+        for k in act:
+            rel = np.max(np.abs(step[k] * delta[k])) / (1.0 + np.max(np.abs(beta[k])))
+            if step[k] == 0.0 or rel <= tol or (rel < 1e-4 and rel >= 0.5 * prev_rel[k]):
+                active[k] = False
+                converged[k] = step[k] != 0.0 or rel <= tol or np.max(np.abs(delta[k])) < 1e-5
+            elif n_iter[k] >= max_iter[k]:
+                active[k] = False
+            prev_rel[k] = rel
+
+    # final linear predictor from the final coefficients (no accumulated drift)
+    d.eta(bf.beta, bf.eta)
+    info = bf.info.cpu().numpy()
+    res = []
+    for k, r in enumerate(reqs):
+        res.append(FitResult(coef=beta[k, :p].copy(),
+                             intercept=float(beta[k, p]) if r.fit_intercept else 0.0,
+                             n_iter=int(n_iter[k]), converged=bool(converged[k]),
+                             dropped=int(info[k])))
+    return res, bf.eta
+
+
+def _syrk(d: Design, bf, fits: np.ndarray, nsteps: int, ntile1: int, stats, st, exact=False,
+          rows=None):
+    """H[k] = X^T diag(W[k]) X for k in fits.  bf16 MFMA, or the exact-f32 MFMA variant when
+    the design is not bf16-exact and the caller needs an accurate Gram (CD, Gaussian)."""
+    nact = int(fits.size)
+    if nact == 0:
+        return
+    use_f32 = exact and d.xf is not None
+    if use_f32:
+        nt = d.P // 128
+        ntile1 = nt * (nt + 1) // 2
+        nsteps = (d.n + 15) // 16
+    splits = syrk_splits(ntile1 * nact, nsteps)
+    wb = _lib.query("sglm_syrk_work_bytes", d.P, nact, splits)
+    work = _work(wb, d.device) if wb else None
+    fits_d = torch.tensor(fits, dtype=torch.int32, device=d.device)
+    if stats is not None and stats.record:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+    if use_f32:
+        _lib.call("sglm_syrk_f32", _p(d.xf), d.ld, d.P, d.n, _p(bf.W), _p(fits_d), nact, splits,
+                  _p(bf.H), _p(work), st)
+    else:
+        _lib.call("sglm_syrk", _p(d.xb), d.ld, d.P, d.n, _p(bf.W), _p(fits_d), nact, splits,
+                  _p(bf.H), _p(work), st)
+    if stats is not None and stats.record:
+        e1.record()
+        pa = d.p + 1
+        nrows = float(np.sum(rows[fits])) if rows is not None else float(d.n) * nact
+        stats.syrk_events.append((e0, e1, nact, nrows * pa * (pa + 1)))   # algorithmic flop
+
+
+def score_sums(prob: Problem, family: int, power: float, eta, fit_resp: Sequence[int],
+               sets: np.ndarray) -> np.ndarray:
+    """[B, 2, 2] float64: per fit and set (train, test): sum m (y - mu)^2, sum m loss."""
+    d = prob.design
+    B = len(fit_resp)
+    dev = d.device
+    fr = torch.tensor(list(fit_resp), dtype=torch.int32, device=dev)
+    sd = torch.tensor(np.asarray(sets, dtype=np.int32).reshape(-1), dtype=torch.int32, device=dev)
+    out = torch.zeros((B, 4), dtype=torch.float64, device=dev)
+    work = _work(_lib.query("sglm_rowsum_work_bytes", B, 4, d.n), dev)
+    _lib.call("sglm_score_sums", family, float(power), d.n, d.ld, B, _p(eta), _p(prob.Y),
+              _p(prob.M), _p(fr), _p(sd), _p(out), _p(work), _stream())
+    return out.cpu().numpy().reshape(B, 2, 2)

@@ -1,0 +1,313 @@
+"""sklearn-protocol estimators backed by the MI355X engine.
+
+``GLM.__init__`` (backend/sglm.py:95-130) picks an estimator class from the family and the
+kwargs and calls ``Base(*args, **kwargs)``; it then uses ``.fit(X, y)``, ``.predict(X)``,
+``.score(X, y)``, ``.coef_``, ``.intercept_`` (backend/sglm.py:184, 241, 347).  These
+classes keep the constructor signatures and defaults of the scikit-learn estimators the
+reference selects, so keyword errors surface the same way (``TypeError`` on unknown
+kwargs), and replace their numerics with the batched IRLS engine:
+
+  LinearRegression  min ||y - Xw - b||^2                      -> squared loss, lam = 0
+  Ridge(alpha)      ||y - Xw - b||^2 + alpha ||w||^2          -> squared loss, lam = alpha
+  TweedieRegressor  mean loss + alpha/2 ||w||^2                -> lam = alpha * n_train
+                    (power 0 identity -> squared loss; power >= 1 log link -> Tweedie-log)
+  Lasso/ElasticNet  1/(2n)||.||^2 + a rho |w|_1 + a(1-rho)/2 ||w||^2 -> Gram-space CD
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import engine as E
+
+
+class NotYetImplementedError(NotImplementedError):
+    """Defined here (the reference raises this name without defining it, sglm.py:126)."""
+
+
+@dataclass
+class Objective:
+    kind: str          # 'irls' | 'cd'
+    family: int
+    power: float
+    alpha: float
+    lam_scale: str     # 'abs' -> lam = alpha ; 'n' -> lam = alpha * n_train
+    fit_intercept: bool
+    max_iter: int
+    l1_ratio: float = 0.0
+    tol: float = 1e-4
+
+    def lam(self, n_train: float) -> float:
+        return self.alpha * n_train if self.lam_scale == "n" else self.alpha
+
+
+def _check_y_range(power: float, y: np.ndarray):
+    """``in_y_true_range`` of the half-Tweedie losses (sklearn glm.py:231-235)."""
+    if power == 0:
+        return
+    bad = np.any(y < 0) if 0 < power < 2 else np.any(y <= 0)
+    if power < 0:
+        bad = False
+    if bad:
+        name = {1: "HalfPoissonLoss", 2: "HalfGammaLoss"}.get(power, "HalfTweedieLoss")
+        raise ValueError(f"Some value(s) of y are out of the valid range of the loss {name!r}.")
+
+
+def _as2d(X):
+    if hasattr(X, "values") and not isinstance(X, np.ndarray):
+        X = X.values
+    X = np.asarray(X)
+    if X.ndim == 1:
+        raise ValueError("Expected 2D array, got 1D array instead")
+    return X
+
+
+class _EngineRegressor:
+    _params: tuple = ()
+
+    def __init__(self, **kw):
+        for k, v in kw.items():
+            setattr(self, k, v)
+
+    # ---- sklearn-ish plumbing
+    def get_params(self, deep=True):
+        return {k: getattr(self, k) for k in self._params}
+
+    def set_params(self, **kw):
+        for k, v in kw.items():
+            if k not in self._params:
+                raise ValueError(f"Invalid parameter {k!r} for estimator {type(self).__name__}")
+            setattr(self, k, v)
+        return self
+
+    def __repr__(self):
+        return f"{type(self).__name__}(" + ", ".join(f"{k}={getattr(self, k)!r}" for k in self._params) + ") [sglm_hip]"
+
+    # ---- objective
+    def objective(self) -> Objective:  # pragma: no cover - abstract
+        raise NotImplementedError
+
+    def _warm(self):
+        if getattr(self, "warm_start", False) and hasattr(self, "coef_"):
+            c = np.asarray(self.coef_, dtype=np.float64).reshape(-1)
+            b = float(np.asarray(getattr(self, "intercept_", 0.0)).reshape(-1)[0]) if \
+                np.ndim(getattr(self, "intercept_", 0.0)) else float(getattr(self, "intercept_", 0.0))
+            return c, b
+        return None, None
+
+    def fit(self, X, y, sample_weight=None):
+        if sample_weight is not None:
+            raise NotYetImplementedError("sample_weight is not used by the reference path")
+        X = _as2d(X)
+        y = np.asarray(y, dtype=np.float64).reshape(-1)
+        if X.shape[0] != y.shape[0]:
+            raise ValueError(f"Found input variables with inconsistent numbers of samples: "
+                             f"[{X.shape[0]}, {y.shape[0]}]")
+        obj = self.objective()
+        _check_y_range(obj.power if obj.family == E.FAM_TWEEDIE_LOG else 0, y)
+        d = E.Design.from_host(X)
+        prob = E.Problem(d, [y], [np.ones(X.shape[0], np.uint8)])
+        c0, b0 = self._warm()
+        if c0 is not None and c0.shape[0] != X.shape[1]:
+            c0, b0 = None, None
+        if obj.kind == "cd":
+            from . import cd
+            res = cd.enet_fit(prob, [obj], [0], [0], coef0=[c0])[0]
+        else:
+            req = E.FitReq(obj.family, obj.power, obj.lam(X.shape[0]), 0, 0, obj.fit_intercept,
+                           obj.max_iter, c0, b0)
+            (res,), _ = E.irls(prob, [req])
+        self._set_fitted(res.coef, res.intercept, res.n_iter)
+        return self
+
+    def _set_fitted(self, coef, intercept, n_iter):
+        self.coef_ = np.asarray(coef, dtype=np.float64)
+        self.intercept_ = float(intercept)
+        self.n_iter_ = int(n_iter)
+        self.n_features_in_ = self.coef_.shape[0]
+
+    def _linear_predictor(self, X):
+        import torch
+        X = _as2d(X)
+        if X.shape[1] != self.coef_.shape[0]:
+            raise ValueError(f"X has {X.shape[1]} features, but {type(self).__name__} is expecting "
+                             f"{self.coef_.shape[0]} features as input.")
+        d = E.Design.from_host(X)
+        beta = np.zeros((1, d.P), dtype=np.float32)
+        beta[0, : d.p] = self.coef_
+        beta[0, d.p] = self.intercept_
+        eta = d.eta(torch.from_numpy(beta).to(d.device))
+        return eta[0, : d.n].double().cpu().numpy()
+
+    def predict(self, X):
+        eta = self._linear_predictor(X)
+        obj = self.objective()
+        return np.exp(eta) if obj.family == E.FAM_TWEEDIE_LOG else eta
+
+    def score(self, X, y, sample_weight=None):
+        """R^2 (Gaussian estimators, sklearn RegressorMixin.score)."""
+        y = np.asarray(y, dtype=np.float64).reshape(-1)
+        pred = self.predict(X)
+        ssr = float(np.sum((y - pred) ** 2))
+        sst = float(np.sum((y - y.mean()) ** 2))
+        if sst == 0.0:
+            return 1.0 if ssr == 0.0 else 0.0
+        return 1.0 - ssr / sst
+
+
+class LinearRegression(_EngineRegressor):
+    _params = ("fit_intercept", "copy_X", "tol", "n_jobs", "positive")
+
+    def __init__(self, *, fit_intercept=True, copy_X=True, tol=1e-6, n_jobs=None, positive=False):
+        if positive:
+            raise NotYetImplementedError("positive=True is not supported by the engine")
+        super().__init__(fit_intercept=fit_intercept, copy_X=copy_X, tol=tol, n_jobs=n_jobs,
+                         positive=positive)
+
+    def objective(self):
+        return Objective("irls", E.FAM_SQUARED, 0.0, 0.0, "abs", self.fit_intercept, 100)
+
+
+class Ridge(_EngineRegressor):
+    _params = ("alpha", "fit_intercept", "copy_X", "max_iter", "tol", "solver", "positive",
+               "random_state")
+
+    def __init__(self, alpha=1.0, *, fit_intercept=True, copy_X=True, max_iter=None, tol=1e-4,
+                 solver="auto", positive=False, random_state=None):
+        if positive:
+            raise NotYetImplementedError("positive=True is not supported by the engine")
+        super().__init__(alpha=alpha, fit_intercept=fit_intercept, copy_X=copy_X,
+                         max_iter=max_iter, tol=tol, solver=solver, positive=positive,
+                         random_state=random_state)
+
+    def objective(self):
+        if np.ndim(self.alpha) or self.alpha < 0:
+            raise ValueError(f"The 'alpha' parameter of Ridge must be a float in the range [0.0, inf). Got {self.alpha!r} instead.")
+        return Objective("irls", E.FAM_SQUARED, 0.0, float(self.alpha), "abs", self.fit_intercept, 100)
+
+
+class ElasticNet(_EngineRegressor):
+    _params = ("alpha", "l1_ratio", "fit_intercept", "precompute", "max_iter", "copy_X", "tol",
+               "warm_start", "positive", "random_state", "selection")
+
+    def __init__(self, alpha=1.0, *, l1_ratio=0.5, fit_intercept=True, precompute=False,
+                 max_iter=1000, copy_X=True, tol=1e-4, warm_start=False, positive=False,
+                 random_state=None, selection="cyclic"):
+        if positive:
+            raise NotYetImplementedError("positive=True is not supported by the engine")
+        super().__init__(alpha=alpha, l1_ratio=l1_ratio, fit_intercept=fit_intercept,
+                         precompute=precompute, max_iter=max_iter, copy_X=copy_X, tol=tol,
+                         warm_start=warm_start, positive=positive, random_state=random_state,
+                         selection=selection)
+
+    def objective(self):
+        return Objective("cd", E.FAM_SQUARED, 0.0, float(self.alpha), "abs", self.fit_intercept,
+                         int(self.max_iter), float(self.l1_ratio), float(self.tol))
+
+
+class Lasso(ElasticNet):
+    _params = ("alpha", "fit_intercept", "precompute", "copy_X", "max_iter", "tol", "warm_start",
+               "positive", "random_state", "selection")
+
+    def __init__(self, alpha=1.0, *, fit_intercept=True, precompute=False, copy_X=True,
+                 max_iter=1000, tol=1e-4, warm_start=False, positive=False, random_state=None,
+                 selection="cyclic"):
+        super().__init__(alpha=alpha, l1_ratio=1.0, fit_intercept=fit_intercept,
+                         precompute=precompute, max_iter=max_iter, copy_X=copy_X, tol=tol,
+                         warm_start=warm_start, positive=positive, random_state=random_state,
+                         selection=selection)
+
+
+class TweedieRegressor(_EngineRegressor):
+    _params = ("power", "alpha", "fit_intercept", "link", "solver", "max_iter", "tol",
+               "warm_start", "verbose")
+
+    def __init__(self, *, power=0.0, alpha=1.0, fit_intercept=True, link="auto", solver="lbfgs",
+                 max_iter=100, tol=1e-4, warm_start=False, verbose=0):
+        super().__init__(power=power, alpha=alpha, fit_intercept=fit_intercept, link=link,
+                         solver=solver, max_iter=max_iter, tol=tol, warm_start=warm_start,
+                         verbose=verbose)
+
+    def _log_link(self):
+        if self.link == "auto":
+            return self.power > 0
+        if self.link not in ("log", "identity"):
+            raise ValueError(f"The 'link' parameter of TweedieRegressor must be a str among "
+                             f"{{'auto', 'identity', 'log'}}. Got {self.link!r} instead.")
+        return self.link == "log"
+
+    def objective(self):
+        p = float(self.power)
+        if 0 < p < 1:
+            raise ValueError("Tweedie power between 0 and 1 is not a valid distribution")
+        log = self._log_link()
+        if log and p >= 1:
+            fam = E.FAM_TWEEDIE_LOG
+        elif not log and p == 0:
+            fam = E.FAM_SQUARED
+        else:
+            raise NotYetImplementedError(f"TweedieRegressor(power={p}, link={self.link!r}) "
+                                         "is outside the engine's families")
+        if self.alpha < 0:
+            raise ValueError("alpha must be >= 0")
+        return Objective("irls", fam, p if fam == E.FAM_TWEEDIE_LOG else 0.0, float(self.alpha),
+                         "n", self.fit_intercept, int(self.max_iter))
+
+    def score(self, X, y, sample_weight=None):
+        """D^2, fraction of deviance explained (sklearn glm.py:371-444)."""
+        y = np.asarray(y, dtype=np.float64).reshape(-1)
+        obj = self.objective()
+        eta = self._linear_predictor(X)
+        if obj.family == E.FAM_SQUARED:            # D^2 of the squared loss == R^2
+            ssr = float(np.sum((y - eta) ** 2))
+            sst = float(np.sum((y - y.mean()) ** 2))
+            return (1.0 if ssr == 0 else 0.0) if sst == 0 else 1.0 - ssr / sst
+        _check_y_range(obj.power, y)
+        dev = np.mean(half_loss_np(obj.power, y, eta))
+        ym = y.mean()
+        dev0 = np.mean(half_loss_np(obj.power, y, np.full_like(y, math.log(ym))))
+        const = np.mean(loss_constant_np(obj.power, y))
+        return 1.0 - (dev + const) / (dev0 + const)
+
+
+class PoissonRegressor(TweedieRegressor):
+    _params = ("alpha", "fit_intercept", "solver", "max_iter", "tol", "warm_start", "verbose")
+
+    def __init__(self, *, alpha=1.0, fit_intercept=True, solver="lbfgs", max_iter=100, tol=1e-4,
+                 warm_start=False, verbose=0):
+        super().__init__(power=1.0, alpha=alpha, fit_intercept=fit_intercept, link="log",
+                         solver=solver, max_iter=max_iter, tol=tol, warm_start=warm_start,
+                         verbose=verbose)
+
+
+class LogisticRegression:
+    """Out of scope: the reference's Logistic/Multinomial path."""
+
+    def __init__(self, *a, **k):
+        raise NotYetImplementedError("Logistic/Multinomial GLMs are outside the MI355X engine's "
+                                     "scope (SURVEY.md §8(a) A2)")
+
+
+def half_loss_np(power, y, eta):
+    """Host float64 half-Tweedie loss (log link) for scores only."""
+    if power == 1:
+        return np.exp(eta) - y * eta
+    if power == 2:
+        return eta + y * np.exp(-eta)
+    return np.exp((2 - power) * eta) / (2 - power) - y * np.exp((1 - power) * eta) / (1 - power)
+
+
+def loss_constant_np(power, y):
+    if power == 1:
+        with np.errstate(divide="ignore", invalid="ignore"):
+            return np.where(y > 0, y * np.log(np.where(y > 0, y, 1.0)), 0.0) - y
+    if power == 2:
+        return -np.log(y) - 1
+    return np.power(np.maximum(y, 0), 2 - power) / (1 - power) / (2 - power)
+
+
+def objective_for(Base, kwargs) -> Objective:
+    """Construct the estimator (validating kwargs exactly as GLM would) and return its objective."""
+    return Base(**kwargs).objective()

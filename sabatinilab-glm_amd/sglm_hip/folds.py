@@ -1,0 +1,105 @@
+"""CV fold generation (host numpy; integer work, bit-exact with the reference).
+
+The reference draws its folds with sklearn ``GroupShuffleSplit`` on the GLOBAL numpy RNG
+(backend/sglm_pp.py:236-264; sklearn/model_selection/_split.py:1925-1945, 2181-2187,
+2433-2505).  This module restates that algorithm without sklearn so fold indices stay
+bit-exact while the rest of the grid runs on the GPU:
+
+    classes, gidx = unique(groups, return_inverse)
+    n_test = ceil(test_size * G)  (float test_size) | int(test_size);  n_train = G - n_test
+    per split: perm = rng.permutation(G); test = perm[:n_test]; train = perm[n_test:]
+    rows = flatnonzero(isin(gidx, train/test))   (ascending)
+
+Fold masks for the engine are multiplicity vectors (uint8), so user-supplied index lists
+with repeats keep the weight that ``X[idx]`` copies would give them.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+
+def bucket_ids_by_timeframe(total_timesteps, timesteps_per_bucket=20):
+    """backend/sglm_pp.py:218-234 (kept verbatim in behaviour, incl. the N//tpb divisor)."""
+    num_buckets = total_timesteps // timesteps_per_bucket
+    return np.arange(total_timesteps) // num_buckets
+
+
+def _validate(n_samples, test_size):
+    kind = np.asarray(test_size).dtype.kind
+    if (kind == "i" and (test_size >= n_samples or test_size <= 0)) or \
+            (kind == "f" and (test_size <= 0 or test_size >= 1)):
+        raise ValueError(f"test_size={test_size} should be either positive and smaller than the "
+                         f"number of samples {n_samples} or a float in the (0, 1) range")
+    n_test = math.ceil(test_size * n_samples) if kind == "f" else int(test_size)
+    n_train = n_samples - n_test
+    if n_train <= 0:
+        raise ValueError(f"With n_samples={n_samples}, test_size={test_size} and train_size=None, "
+                         "the resulting train set will be empty. Adjust any of the "
+                         "aforementioned parameters.")
+    return n_train, n_test
+
+
+def group_shuffle_split(groups, n_splits, test_size, random_state=None):
+    if random_state is None:
+        rng = np.random.mtrand._rand
+    elif isinstance(random_state, np.random.RandomState):
+        rng = random_state
+    else:
+        rng = np.random.RandomState(random_state)
+    groups = np.asarray(groups)
+    classes, gidx = np.unique(groups, return_inverse=True)
+    n_train, n_test = _validate(len(classes), test_size)
+    out = []
+    for _ in range(int(n_splits)):
+        perm = rng.permutation(len(classes))
+        tr_g = perm[n_test:n_test + n_train]
+        te_g = perm[:n_test]
+        is_tr = np.zeros(len(classes), bool)
+        is_tr[tr_g] = True
+        is_te = np.zeros(len(classes), bool)
+        is_te[te_g] = True
+        out.append((np.flatnonzero(is_tr[gidx]), np.flatnonzero(is_te[gidx])))
+    return out
+
+
+def cv_idx_from_bucket_ids(bucket_ids, X=None, y=None, num_folds=None, test_size=None):
+    """backend/sglm_pp.py:236-264 (X, y only validated for length by sklearn; unused)."""
+    bucket_ids = np.asarray(bucket_ids)
+    if num_folds is None:
+        num_folds = bucket_ids.max() + 1
+    if test_size is None:
+        test_size = 1 / num_folds
+    if X is not None and len(X) != len(bucket_ids):
+        raise ValueError(f"Found input variables with inconsistent numbers of samples: "
+                         f"[{len(X)}, {len(bucket_ids)}]")
+    return group_shuffle_split(bucket_ids, num_folds, test_size)
+
+
+def trial_keys_codes(df, id_cols, package_style=False):
+    """Categorical codes of the trial keys (backend/sglm_ez.py:334-340; package
+    sglm/sglm/models/split_data.py:146-152 when ``package_style``)."""
+    import pandas as pd
+    bucket = None
+    for i, idc in enumerate(id_cols):
+        s = df[idc].astype(str) if not package_style else df[idc].apply(str)
+        if i == 0:
+            bucket = s.str.len().astype(str) + ":" + s
+        elif package_style:
+            bucket = bucket + "__" + s.str.len().apply(str) + ":" + s
+        else:
+            bucket = bucket + "_" + s
+    return bucket.astype("category").cat.codes
+
+
+def masks_from_cv_idx(cv_idx, n):
+    """Per split: (train multiplicity mask, test multiplicity mask) as uint8 arrays."""
+    out = []
+    for tr, te in cv_idx:
+        mtr = np.bincount(np.asarray(tr, dtype=np.int64), minlength=n)[:n]
+        mte = np.bincount(np.asarray(te, dtype=np.int64), minlength=n)[:n]
+        if mtr.max(initial=0) > 255 or mte.max(initial=0) > 255:
+            raise ValueError("an index repeats more than 255 times in one split")
+        out.append((mtr.astype(np.uint8), mte.astype(np.uint8)))
+    return out

@@ -1,0 +1,169 @@
+"""Drop-in API (sglm / sglm_cv / sglm_ez / sglm_pp) on the MI355X vs golden fixtures & oracle.
+
+Tolerances (BASELINE.json north star): coefficients within 1e-4 relative (Poisson / Gamma)
+and 1e-5 relative (Gaussian) of the tight-tolerance sklearn minimiser; fold indices and
+timeshift outputs bit-exact.  Relative error = max|a - b| / max|b| over the vector.
+"""
+import json
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from conftest import GOLDEN
+from oracle import cv_ref, folds_ref, glm_ref, pp_ref
+
+pytestmark = pytest.mark.gpu
+TOL_POIS, TOL_GAUSS = 1e-4, 1e-5
+
+
+def rel(a, b):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    return np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30)
+
+
+def test_glm_all_families_vs_golden(engine, golden):
+    import sglm
+    g = golden("fits.npz")
+    meta = json.load(open(os.path.join(GOLDEN, "fits_meta.json")))
+    for m in meta:
+        glm = sglm.GLM("Poisson", alpha=m["alpha"], fit_intercept=m["fit_intercept"])
+        glm.fit(g["pois_X"], g["pois_y"])
+        assert rel(glm.coef_, g[m["key"] + "_coef"]) < TOL_POIS, m
+        assert glm.beta_ is glm.coef_ and glm.beta0_ == glm.intercept_
+    glm = sglm.GLM("Gamma", alpha=0.05)
+    glm.fit(g["gam_X"], g["gam_y"])
+    assert rel(glm.coef_, g["gam_coef"]) < TOL_POIS
+    X, y = g["gau_X"], g["gau_y"]
+    glm = sglm.GLM("Normal", alpha=0, l1_ratio=0, max_iter=1000)
+    glm.fit(X, y)
+    assert rel(glm.coef_, g["ols_coef"]) < TOL_GAUSS
+    for i, a in enumerate([0.1, 10.0, 1000.0]):
+        glm = sglm.GLM("Gaussian", alpha=a, l1_ratio=0)
+        glm.fit(X, y)
+        assert rel(glm.coef_, g[f"ridge_a{i}_coef"]) < TOL_GAUSS
+    for i, a in enumerate([1e-3, 1e-2]):
+        glm = sglm.GLM("Gaussian", alpha=a, l1_ratio=1)
+        glm.fit(X, y)
+        assert rel(glm.coef_, g[f"lasso_a{i}_coef"]) < TOL_GAUSS, a
+        glm = sglm.GLM("Gaussian", alpha=a, l1_ratio=0.5)
+        glm.fit(X, y)
+        assert rel(glm.coef_, g[f"enet_a{i}_coef"]) < TOL_GAUSS, a
+        assert abs(glm.intercept_ - float(g[f"enet_a{i}_b"])) < 1e-5 * max(1, abs(float(g[f"enet_a{i}_b"])))
+
+
+def test_glm_rank_deficient_ols(engine, golden):
+    """Duplicate + all-zero column, alpha = 0: the engine freezes the zero column and the
+    dropped duplicate pivot; predictions match the min-norm lstsq fit (coefficients of the
+    duplicated pair are not unique — parity is on the fitted values)."""
+    import sglm
+    g = golden("fits.npz")
+    X, y = g["olsr_X"], g["gau_y"]
+    glm = sglm.GLM("Normal", alpha=0)
+    glm.fit(X, y)
+    assert glm.coef_[7] == 0.0
+    pred_ref = X @ g["olsr_coef"] + float(g["olsr_b"])
+    assert rel(glm.predict(X), pred_ref) < 1e-5
+
+
+def test_glm_scores_and_residuals(engine, golden):
+    import sglm
+    g = golden("fits.npz")
+    X, y = g["pois_X"], g["pois_y"]
+    glm = sglm.GLM("Poisson", alpha=0.1, score_method="r2")
+    glm.fit(X, y)
+    spec = glm_ref.FitSpec("tweedie", alpha=0.1, power=1.0)
+    c, b = glm_ref.fit_tweedie_newton(X, y, 0.1, 1.0)
+    assert abs(glm.score(X, y) - glm_ref.r2_score(spec, c, b, X, y)) < 1e-6
+    assert abs(glm.neg_mse_score(X, y) - glm_ref.neg_mse_score(spec, c, b, X, y)) < 1e-6 * max(1, abs(glm_ref.neg_mse_score(spec, c, b, X, y)))
+    r, mr = glm.get_residuals(X, y)
+    assert rel(r, y - glm_ref.predict(spec, c, b, X)) < 1e-5
+    assert rel(mr, y - y.mean()) == 0
+
+
+def test_poisson_y_range_error(engine):
+    import sglm
+    X = np.random.default_rng(0).random((50, 3))
+    with pytest.raises(ValueError, match="out of the valid range"):
+        sglm.GLM("Poisson").fit(X, -np.ones(50))
+
+
+def test_cv_grid_vs_golden(engine, golden):
+    import sglm_cv
+    g = golden("cv_grid.npz")
+    X, y = g["cvg_X"], g["cvg_y"]
+    cv_idx = [(g[f"cvg_k{k}_train"], g[f"cvg_k{k}_test"]) for k in range(3)]
+    kws = sglm_cv.generate_mult_params({"alpha": list(g["cvg_alphas"])}, {"model_name": "Poisson"})
+    out = sglm_cv.cv_glm_mult_params(X, y, cv_idx, "Normal", kws)
+    assert all("model_name" not in k for k in kws)          # popped from the caller's dicts
+    for j, r in enumerate(out["full_cv_results"]):
+        assert rel(r["cv_coefs"], g[f"cvg_a{j}_cv_coefs"]) < TOL_POIS
+        assert rel(r["cv_intercepts"], g[f"cvg_a{j}_cv_intercepts"]) < TOL_POIS
+        assert rel(r["cv_scores_test"], g[f"cvg_a{j}_scores_test"]) < 1e-6
+        assert rel(r["cv_scores_train"], g[f"cvg_a{j}_scores_train"]) < 1e-6
+        assert abs(r["cv_R2_score"] - float(g[f"cvg_a{j}_R2"])) < 1e-6
+        assert abs(r["cv_mse_score"] - float(g[f"cvg_a{j}_mse"])) < 1e-6 * float(g[f"cvg_a{j}_mse"])
+        assert rel(r["model"].coef_, g[f"cvg_a{j}_full_coef"]) < TOL_POIS
+        assert set(r) == {"cv_coefs", "cv_intercepts", "cv_scores_train", "cv_scores_test",
+                          "cv_mean_score_train", "cv_mean_score", "cv_std_score", "cv_R2_score",
+                          "cv_mse_score", "glm_kwargs", "model"}
+    best = int(np.argmax([float(g[f"cvg_a{j}_scores_test"].mean()) for j in range(3)]))
+    assert out["best_params"] == out["full_cv_results"][best]["glm_kwargs"]
+
+
+def test_simple_cv_fit_gaussian_grid_vs_oracle(engine):
+    """Ridge/Lasso/OLS grid with rolls, r2 scoring, trial-id folds — against the oracle."""
+    import sglm_ez
+    import sglm_cv
+    from sglm_hip import synth
+    s = synth.make(N=6000, m=4, L=3, family="gaussian", rho=0.1, seed=21, beta_scale=0.5)
+    X = pd.DataFrame(s.dense_X(), columns=[f"c{i}" for i in range(s.p)])
+    X["nTrial"] = s.trial
+    y = pd.Series(s.y)
+    np.random.seed(3)
+    cv_idx = sglm_ez.cv_idx_by_trial_id(X, trial_id_columns=["nTrial"], num_folds=4)
+    np.random.seed(3)
+    ref_idx = folds_ref.cv_idx_from_bucket_ids(folds_ref.trial_bucket_codes([s.trial]), num_folds=4)
+    for (a, b), (c, d) in zip(cv_idx, ref_idx):
+        assert np.array_equal(a, c) and np.array_equal(b, d)
+    Xf = X.drop(columns="nTrial")
+    kws = sglm_cv.generate_mult_params({"alpha": [0, 0.5, 50.0], "l1_ratio": [0, 1]},
+                                       {"max_iter": 1000})
+    kws[1]["roll"] = 3
+    ref_kws = [dict(k) for k in kws]
+    out = sglm_ez.simple_cv_fit(Xf, y, cv_idx, kws, model_type="Normal", score_method="r2")
+    ref = cv_ref.cv_mult(Xf.values, y.values, cv_idx, ref_kws, score_method="r2")
+    for r, q in zip(out[4]["full_cv_results"], ref["full_cv_results"]):
+        assert rel(r["cv_coefs"], q["cv_coefs"]) < TOL_GAUSS, r["glm_kwargs"]
+        # R^2 is dimensionless and near 0 here: absolute tolerance
+        assert np.max(np.abs(r["cv_scores_test"] - q["cv_scores_test"])) < 1e-6
+        assert abs(r["cv_R2_score"] - q["cv_R2_score"]) < 1e-6
+        assert rel(r["model"].coef_, q["coef"]) < TOL_GAUSS
+    assert out[2] == ref["best_params"]
+
+
+def test_timeshift_cols_dataframe(engine):
+    import sglm_ez
+    X = pd.DataFrame(np.arange(200).reshape((100, 2)), columns=["A", "B"])
+    X["B"] = (X["B"] - 1) * 2 + 1
+    out = sglm_ez.timeshift_cols(X, ["A"], neg_order=-2, pos_order=2)
+    assert list(out.columns) == ["A", "B", "A_-2", "A_-1", "A_1", "A_2"]
+    ref = pp_ref.timeshift_multiple(X.values, [0], [0, -2, -1, 1, 2])
+    assert np.array_equal(out.values.astype(float), ref.astype(float), equal_nan=True)
+
+
+def test_c2_scale_poisson_parity(engine):
+    """C2 shape (Poisson 100k x 500, alpha = 1.0) against the float64 oracle."""
+    from sglm_hip import synth
+    import sglm
+    s = synth.make(N=100_000, m=25, L=10, family="poisson", rho=0.02, seed=0)
+    X = s.dense_X()
+    glm = sglm.GLM("Poisson", alpha=1.0)
+    glm.fit(X, s.y)
+    c, b = glm_ref.fit_tweedie_newton(X, s.y, 1.0, 1.0)
+    assert rel(glm.coef_, c) < TOL_POIS
+    glm = sglm.GLM("Poisson", alpha=1e-4)
+    glm.fit(X, s.y)
+    c, b = glm_ref.fit_tweedie_newton(X, s.y, 1e-4, 1.0)
+    assert rel(glm.coef_, c) < TOL_POIS

@@ -1,0 +1,247 @@
+"""HIP kernels vs the float64 oracle / numpy on the same seeded inputs (MI355X only)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle import glm_ref, pp_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    return np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30)
+
+
+@pytest.fixture(scope="module")
+def torch_mod(engine):
+    import torch
+    return torch
+
+
+def test_timeshift_bit_exact_all_widths(engine, torch_mod):
+    torch = torch_mod
+    from sglm_hip import _lib
+    rng = np.random.default_rng(1)
+    for dt in (np.float64, np.float32, np.int64, np.int32, np.int16, np.uint8):
+        X = (rng.random((37, 5)) * 100).astype(dt)
+        shifts = [0, -3, -1, 1, 2, 5]
+        fill = np.array(np.nan if np.issubdtype(dt, np.floating) else 0, dtype=dt)
+        src = torch.from_numpy(X).cuda()
+        cols, sh = np.tile(np.arange(5), len(shifts)), np.repeat(shifts, 5)
+        out = torch.empty((37, cols.size), dtype=src.dtype, device="cuda")
+        cols_d = torch.tensor(cols, dtype=torch.int32).cuda()    # keep alive across the launch
+        sh_d = torch.tensor(sh, dtype=torch.int32).cuda()
+        _lib.call("sglm_timeshift_expand", src.data_ptr(), 37, 5, 1,
+                  cols_d.data_ptr(), sh_d.data_ptr(), cols.size,
+                  out.data_ptr(), 37, cols.size, 1, 0, X.itemsize,
+                  int(fill.view(np.uint64 if X.itemsize == 8 else
+                                {4: np.uint32, 2: np.uint16, 1: np.uint8}[X.itemsize])), 0)
+        ref = pp_ref.timeshift_multiple(X, [], shifts, fill_value=fill)
+        got = out.cpu().numpy()
+        assert got.dtype == X.dtype
+        assert np.array_equal(got, ref.astype(X.dtype), equal_nan=True), dt
+
+
+def test_known_answers_through_kernel(engine, torch_mod, golden):
+    """backend/test/test_sglm_pp.py known answers, computed by the HIP kernel."""
+    import sglm_pp
+    g = golden("timeshift_known.npz")
+    X = g["ts_X"]
+    assert np.array_equal(sglm_pp.timeshift(X, shift_amt=1, fill_value=0), g["ts_fwd"])
+    assert np.array_equal(sglm_pp.timeshift(X, shift_amt=-1, fill_value=0), g["ts_bwd"])
+    assert np.array_equal(sglm_pp.timeshift(X, [0, 1], 1, keep_non_inx=True, fill_value=0),
+                          g["ts_keep_fwd"])
+    assert np.array_equal(sglm_pp.timeshift_multiple(X, shift_amt_list=[-1, 0, 1], fill_value=0),
+                          g["ts_multi_all"])
+    assert np.array_equal(sglm_pp.timeshift_multiple(X, [0, 3], [-1, 0, 1], fill_value=0),
+                          g["ts_multi_03"])
+
+
+def test_design_from_events_matches_dense(engine, torch_mod):
+    from sglm_hip import synth
+    s = synth.make(N=5000, m=7, L=6, rho=0.1, seed=3)
+    d = engine.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
+    X = d.xb[: s.p, : s.N].float().cpu().numpy().T
+    assert np.array_equal(X, s.dense_X(np.float32))
+    assert d.xf is None
+    assert np.all(d.xb[s.p, : s.N].float().cpu().numpy() == 1.0)
+    assert np.all(d.xb[:, s.N:].float().cpu().numpy() == 0.0)
+
+
+def test_pack_and_gemv(engine, torch_mod):
+    torch = torch_mod
+    rng = np.random.default_rng(2)
+    X = rng.normal(size=(3000, 77))
+    d = engine.Design.from_host(X)
+    assert d.xf is not None          # real-valued: not bf16-exact
+    beta = rng.normal(size=(5, d.P)).astype(np.float32)
+    beta[:, 78:] = 0
+    eta = d.eta(torch.from_numpy(beta).cuda()).cpu().numpy()[:, :3000]
+    ref = (np.hstack([X, np.ones((3000, 1))]) @ beta[:, :78].T.astype(np.float64)).T
+    assert rel(eta, ref) < 1e-5
+
+
+def test_xtr_and_syrk_match_numpy(engine, torch_mod):
+    torch = torch_mod
+    from sglm_hip import _lib, synth
+    s = synth.make(N=6000, m=9, L=5, rho=0.2, seed=4)
+    d = engine.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
+    Xa = np.hstack([s.dense_X(), np.ones((s.N, 1))])
+    rng = np.random.default_rng(5)
+    B = 3
+    W = np.zeros((B, d.ld), np.float32)
+    R = np.zeros((B, d.ld), np.float32)
+    W[:, : s.N] = rng.random((B, s.N))
+    R[:, : s.N] = rng.normal(size=(B, s.N))
+    Wd, Rd = torch.from_numpy(W).cuda(), torch.from_numpy(R).cuda()
+    G = torch.zeros((B, d.P), dtype=torch.float64, device="cuda")
+    work = torch.empty(_lib.query("sglm_xtr_work_bytes", d.P, B, d.n), dtype=torch.uint8, device="cuda")
+    _lib.call("sglm_xtr", d.xg.data_ptr(), d.xtype, d.ld, d.P, d.n, Rd.data_ptr(), B,
+              G.data_ptr(), work.data_ptr(), 0)
+    Gref = (Xa.T @ R[:, : s.N].T.astype(np.float64)).T
+    assert rel(G.cpu().numpy()[:, : Xa.shape[1]], Gref) < 1e-6
+    for splits in (1, 3):
+        H = torch.zeros((B, d.P, d.P), dtype=torch.float32, device="cuda")
+        fits = torch.tensor([2, 0], dtype=torch.int32, device="cuda")
+        wb = _lib.query("sglm_syrk_work_bytes", d.P, 2, splits)
+        wk = torch.empty(max(wb, 16), dtype=torch.uint8, device="cuda")
+        _lib.call("sglm_syrk", d.xb.data_ptr(), d.ld, d.P, d.n, Wd.data_ptr(), fits.data_ptr(), 2,
+                  splits, H.data_ptr(), wk.data_ptr(), 0)
+        Hc = H.cpu().numpy()
+        pa = Xa.shape[1]
+        for k in (2, 0):
+            wb16 = torch.from_numpy(W[k, : s.N]).to(torch.bfloat16).float().numpy().astype(np.float64)
+            Href = (Xa * wb16[:, None]).T @ Xa
+            up = np.triu(np.ones((pa, pa), bool))
+            assert rel(Hc[k][:pa, :pa][up], Href[up]) < 2e-6, (splits, k)
+        assert np.all(Hc[1] == 0)       # fit 1 not requested
+
+
+def test_chol_solve_matches_numpy(engine, torch_mod):
+    torch = torch_mod
+    from sglm_hip import _lib
+    rng = np.random.default_rng(6)
+    P, B, p = 512, 2, 300
+    A = rng.normal(size=(B, 2000, p + 1))
+    H = np.zeros((B, P, P), np.float32)
+    g = np.zeros((B, P))
+    for k in range(B):
+        H[k, : p + 1, : p + 1] = A[k].T @ A[k]
+        g[k, : p + 1] = rng.normal(size=p + 1)
+    dsh = np.full((B, P), -1.0, np.float32)
+    dsh[:, :p] = 3.0
+    dsh[:, p] = 0.0
+    Hd = torch.from_numpy(H).cuda()
+    gd = torch.from_numpy(g).cuda()
+    out = torch.zeros((B, P), dtype=torch.float32, device="cuda")
+    info = torch.zeros(B, dtype=torch.int32, device="cuda")
+    frozen = torch.zeros((B, P), dtype=torch.uint8, device="cuda")
+    fits = torch.tensor([0, 1], dtype=torch.int32, device="cuda")
+    dshd = torch.from_numpy(dsh).cuda()
+    _lib.call("sglm_chol_solve_ex", Hd.data_ptr(), P, fits.data_ptr(), 2, gd.data_ptr(),
+              dshd.data_ptr(), out.data_ptr(), info.data_ptr(), frozen.data_ptr(), 1, 0)
+    x = out.cpu().numpy()
+    for k in range(B):
+        M = H[k, : p + 1, : p + 1].astype(np.float64) + np.diag(np.r_[np.full(p, 3.0), 0.0])
+        ref = -np.linalg.solve(M, g[k, : p + 1])
+        assert rel(x[k, : p + 1], ref) < 1e-3
+        assert np.all(x[k, p + 1:] == 0)
+    # re-use the factor (refactor = 0) with a new right-hand side
+    g2 = rng.normal(size=(B, P))
+    g2[:, p + 1:] = 0
+    g2d = torch.from_numpy(g2).cuda()
+    _lib.call("sglm_chol_solve_ex", Hd.data_ptr(), P, fits.data_ptr(), 2, g2d.data_ptr(),
+              dshd.data_ptr(), out.data_ptr(), info.data_ptr(), frozen.data_ptr(), 0, 0)
+    x2 = out.cpu().numpy()
+    for k in range(B):
+        M = H[k, : p + 1, : p + 1].astype(np.float64) + np.diag(np.r_[np.full(p, 3.0), 0.0])
+        assert rel(x2[k, : p + 1], -np.linalg.solve(M, g2[k, : p + 1])) < 1e-3
+
+
+def _fit_one(engine, X, y, family, power, lam, fit_intercept=True):
+    d = engine.Design.from_host(X)
+    prob = engine.Problem(d, [y], [np.ones(len(y), np.uint8)])
+    req = engine.FitReq(family=family, power=power, lam=lam, mask=0, resp=0,
+                        fit_intercept=fit_intercept)
+    (res,), _ = engine.irls(prob, [req])
+    return res
+
+
+def test_engine_poisson_vs_golden(engine, golden):
+    g = golden("fits.npz")
+    meta = json.load(open(os.path.join(GOLDEN, "fits_meta.json")))
+    X, y = g["pois_X"], g["pois_y"]
+    n = X.shape[0]
+    for m in meta:
+        r = _fit_one(engine, X, y, engine.FAM_TWEEDIE_LOG, 1.0, m["alpha"] * n, m["fit_intercept"])
+        assert r.converged, m
+        assert rel(r.coef, g[m["key"] + "_coef"]) < 1e-4, m           # north-star tolerance
+        assert abs(r.intercept - float(g[m["key"] + "_b"])) < 1e-4 * max(1, abs(float(g[m["key"] + "_b"])))
+
+
+def test_engine_gaussian_vs_golden(engine, golden):
+    g = golden("fits.npz")
+    X, y = g["gau_X"], g["gau_y"]
+    r = _fit_one(engine, X, y, engine.FAM_SQUARED, 0.0, 0.0)
+    assert rel(r.coef, g["ols_coef"]) < 1e-5
+    for i, a in enumerate([0.1, 10.0, 1000.0]):
+        r = _fit_one(engine, X, y, engine.FAM_SQUARED, 0.0, a)
+        assert rel(r.coef, g[f"ridge_a{i}_coef"]) < 1e-5, a
+        assert abs(r.intercept - float(g[f"ridge_a{i}_b"])) < 1e-5 * max(1, abs(float(g[f"ridge_a{i}_b"])))
+
+
+def test_engine_gamma_vs_golden(engine, golden):
+    g = golden("fits.npz")
+    X, y = g["gam_X"], g["gam_y"]
+    r = _fit_one(engine, X, y, engine.FAM_TWEEDIE_LOG, 2.0, 0.05 * X.shape[0])
+    assert rel(r.coef, g["gam_coef"]) < 1e-4
+
+
+def test_engine_batched_masks_match_oracle(engine):
+    """Several (mask, lambda) fits in one batch == separate float64 fits on the row subsets."""
+    from sglm_hip import synth
+    s = synth.make(N=8000, m=5, L=4, rho=0.08, seed=9, beta_scale=0.3)
+    X = s.dense_X()
+    rng = np.random.default_rng(0)
+    masks = [(rng.random(s.N) < 0.8).astype(np.uint8) for _ in range(3)]
+    d = engine.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
+    prob = engine.Problem(d, [s.y], masks)
+    reqs, refs = [], []
+    for mi, m in enumerate(masks):
+        for a in (1e-3, 1e-1):
+            n_tr = int(m.sum())
+            reqs.append(engine.FitReq(engine.FAM_TWEEDIE_LOG, 1.0, a * n_tr, mi, 0))
+            refs.append(glm_ref.fit_tweedie_newton(X[m == 1], s.y[m == 1], a, 1.0))
+    res, _ = engine.irls(prob, reqs)
+    for r, (c, b) in zip(res, refs):
+        assert r.converged
+        assert rel(r.coef, c) < 1e-4
+
+
+def test_syrk_f32_exact_gram(engine, torch_mod):
+    """Real-valued (not bf16-exact) design: the f32-MFMA Gram matches float64 to ~1e-6."""
+    torch = torch_mod
+    from sglm_hip import _lib
+    rng = np.random.default_rng(8)
+    X = rng.normal(size=(5000, 140))
+    d = engine.Design.from_host(X)
+    assert d.xf is not None
+    W = np.zeros((2, d.ld), np.float32)
+    W[:, :5000] = rng.random((2, 5000))
+    Wd = torch.from_numpy(W).cuda()
+    Xa = np.hstack([X.astype(np.float32).astype(np.float64), np.ones((5000, 1))])
+    for splits in (1, 4):
+        H = torch.zeros((2, d.P, d.P), dtype=torch.float32, device="cuda")
+        fits = torch.tensor([1], dtype=torch.int32, device="cuda")
+        wk = torch.empty(max(_lib.query("sglm_syrk_work_bytes", d.P, 1, splits), 16),
+                         dtype=torch.uint8, device="cuda")
+        _lib.call("sglm_syrk_f32", d.xf.data_ptr(), d.ld, d.P, d.n, Wd.data_ptr(),
+                  fits.data_ptr(), 1, splits, H.data_ptr(), wk.data_ptr(), 0)
+        pa = Xa.shape[1]
+        Href = (Xa * W[1, :5000, None].astype(np.float64)).T @ Xa
+        up = np.triu(np.ones((pa, pa), bool))
+        assert rel(H[1].cpu().numpy()[:pa, :pa][up], Href[up]) < 1e-5, splits   # f32 accumulation
