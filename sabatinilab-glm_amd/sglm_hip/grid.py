@@ -65,6 +65,23 @@ def _dist():
     return None
 
 
+def shard_indices(total: int, rank: int, world: int):
+    """Round-robin deal of the fit table over ranks (fit i -> rank i mod world)."""
+    return [i for i in range(total) if i % world == rank]
+
+
+def merge_results(local: dict, dist=None) -> dict:
+    """All-gather every rank's {fit index: result} and merge (one collective per grid)."""
+    if dist is None:
+        return local
+    gathered = [None] * dist.get_world_size()
+    dist.all_gather_object(gathered, local)
+    out = {}
+    for g in gathered:
+        out.update(g)
+    return out
+
+
 def run(X, y, cv_idx, objectives: Sequence[Objective], rolls: Sequence[int],
         score_method: str = "mse", coef0=None, intercept0=None, stats=None, shard=True):
     """Return one result dict per objective (reference key set minus glm_kwargs/model)."""
@@ -100,7 +117,7 @@ def run(X, y, cv_idx, objectives: Sequence[Objective], rolls: Sequence[int],
         table.append((j, -1, FULL, 0, -1))
     dist = _dist() if shard else None
     rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (0, 1)
-    mine = [i for i in range(len(table)) if i % world == rank]
+    mine = shard_indices(len(table), rank, world)
 
     results = {}
     groups = {}
@@ -130,12 +147,7 @@ def run(X, y, cv_idx, objectives: Sequence[Objective], rolls: Sequence[int],
         for q, i in enumerate(idxs):
             rr = res[q]
             results[i] = (rr.coef, rr.intercept, rr.n_iter, rr.converged, sums[q])
-    if dist is not None:
-        gathered = [None] * world
-        dist.all_gather_object(gathered, results)
-        results = {}
-        for g in gathered:
-            results.update(g)
+    results = merge_results(results, dist)
 
     # ---- assemble per-param dicts (reference key order, backend/sglm_cv.py:188-200)
     out = []
