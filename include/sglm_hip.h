@@ -108,6 +108,15 @@ int sglm_syrk(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, const float*
               const int32_t* fits, int32_t nact, int32_t splits, float* H, void* work,
               sglm_stream_t stream);
 
+/* Development entries: a specific bf16 Gram variant (1 = register-staged, 2 = LDS-DMA
+ * staged; sglm_syrk uses the default), same arguments as sglm_syrk. */
+int sglm_syrk_v1(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, const float* W,
+                 const int32_t* fits, int32_t nact, int32_t splits, float* H, void* work,
+                 sglm_stream_t stream);
+int sglm_syrk_variant(int32_t variant, const uint16_t* Xb, int64_t ld, int32_t P, int64_t n,
+                      const float* W, const int32_t* fits, int32_t nact, int32_t splits,
+                      float* H, void* work, sglm_stream_t stream);
+
 /* Same contraction from the f32 design (v_mfma_f32_32x32x2_f32, exact f32 products) for
  * designs that are not bf16-exact, where the Gram itself must be accurate (coordinate
  * descent, Gaussian closed forms).  128-tiles; work sized by sglm_syrk_work_bytes. */
@@ -122,10 +131,14 @@ int sglm_syrk_f32(const float* Xf, int64_t ld, int32_t P, int64_t n, const float
  * a zero diagonal or a pivot collapsing below 1e-6 of its diagonal are frozen too and
  * counted in info[k]; frozen[k][a] records the frozen set.  refactor = 0 skips the
  * factorisation and reuses the factor (and frozen set) a previous call left in H — the
- * constant-Hessian (Gaussian) refinement path.  P must be a multiple of 64, <= 8192. */
+ * constant-Hessian (Gaussian) refinement path.  P must be a multiple of 64, <= 8192.
+ * B = rows of g/dshift/delta/frozen; `work`: sglm_chol_work_bytes(P, B).  Multi-workgroup
+ * blocked factorisation (diag / panel / trailing-update launches per 64-column block). */
+size_t sglm_chol_work_bytes(int32_t P, int32_t B);
 int sglm_chol_solve_ex(float* H, int32_t P, const int32_t* fits, int32_t nact,
                        const double* g, const float* dshift, float* delta, int32_t* info,
-                       uint8_t* frozen, int32_t refactor, sglm_stream_t stream);
+                       uint8_t* frozen, int32_t refactor, int32_t B, void* work,
+                       sglm_stream_t stream);
 
 /* Line search: out[k][j] = sum_i M[m][i] * loss(y_i, eta_i + t[j] * deta_i) (float64),
  * for j < T, fits k < B.  `work`: sglm_rowsum_work_bytes(B, T, n). */

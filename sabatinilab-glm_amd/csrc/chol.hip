@@ -4,17 +4,19 @@
 // (_newton_solver.py NewtonCholeskySolver.inner_solve -> scipy cho_solve; Ridge
 // _solve_cholesky -> linalg.solve(assume_a='pos'), _ridge.py:201-213).
 //
-// One 256-thread workgroup per fit.  H_k is row-major P x P; only a <= b is read (the
-// upper triangle that sglm_syrk writes).  Right-looking blocked Cholesky H = U^T U with
-// NB = 64:
-//   1. diagonal block factored in LDS by one wave (lane = column, no block barriers);
-//   2. row panel U_kj = U_kk^{-T} A_kj, one thread per column j (64-entry register vector);
-//      the forward substitution of the right-hand side is fused into this step;
-//   3. trailing update A_ij -= U_ki^T U_kj over 64x64 tiles, 4x4 register micro-tiles.
-// Then blocked back substitution.  Frozen coordinates (dshift < 0, zero diagonal, or a
-// pivot that collapses below 1e-6 of its original diagonal) get delta = 0.
-// `refactor` = 0 reuses the factor left in H by a previous call with the same fits
-// (constant-Hessian families: Gaussian refinement iterations).
+// H_k is row-major P x P; only a <= b is read (the upper triangle sglm_syrk writes).
+// Right-looking blocked Cholesky H = U^T U, NB = 64, spread over many workgroups so that a
+// handful of fits still fills the chip (8-GPU runs hold ~15 fits per rank):
+//   prep    (1 WG / fit)            penalty shift, frozen coordinates, rhs = g
+//   per block column kb:
+//     diag  (1 wave / fit)          U_kk in LDS (lane = column), forward solve z_k
+//     panel (fits x column chunks)  U_kj = U_kk^-T A_kj (thread = column), rhs_j -= U_kj.z_k
+//     update(fits x 64x64 tiles)    A_ij -= U_ki^T U_kj, 4x4 register micro-tiles
+//   back    (1 WG / fit)            blocked back substitution, delta = -x
+// Frozen coordinates (dshift < 0, zero diagonal, or a pivot collapsing below 1e-6 of its
+// original diagonal) get delta = 0.  refactor = 0 reuses the factor and frozen set left in
+// H by a previous call (constant-Hessian Gaussian refinement): only the two triangular
+// solves run.
 #include "common.h"
 
 namespace sglm {
@@ -23,173 +25,202 @@ constexpr int kNB = 64;
 constexpr int kCT = 256;
 constexpr int kMaxP = 8192;
 
-__global__ void __launch_bounds__(kCT) chol_solve_kernel(
+// rhs/z/x scratch per fit lives in `work` (float, [B][P]); the original diagonal in
+// `work + B*P` (float, [B][P]); the dropped-pivot counter is info[].
+
+__global__ void __launch_bounds__(kCT) chol_prep_kernel(
     float* __restrict__ Hall, int32_t P, const int32_t* __restrict__ fits,
     const double* __restrict__ gall, const float* __restrict__ dshift_all,
-    float* __restrict__ delta_all, int32_t* __restrict__ info, uint8_t* __restrict__ frozen_all,
-    int32_t refactor) {
-    __shared__ float sD[kNB][kNB + 1];
-    __shared__ __attribute__((aligned(16))) float sPi[kNB][kNB];
-    __shared__ __attribute__((aligned(16))) float sPj[kNB][kNB];
-    __shared__ float rhs[kMaxP];          // running right-hand side, then x
-    __shared__ uint8_t frz[kMaxP];
-    __shared__ int ndrop;
-
+    uint8_t* __restrict__ frozen_all, float* __restrict__ rhs_all, float* __restrict__ diag_all,
+    int32_t* __restrict__ info, int32_t refactor) {
     const int fit = fits[blockIdx.x];
     float* H = Hall + (int64_t)fit * P * P;
     const double* g = gall + (int64_t)fit * P;
     const float* dsh = dshift_all + (int64_t)fit * P;
-    float* delta = delta_all + (int64_t)fit * P;
-    uint8_t* frozen = frozen_all + (int64_t)fit * P;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int nb = P / kNB;
-
-    if (tid == 0) ndrop = 0;
+    uint8_t* frz = frozen_all + (int64_t)fit * P;
+    float* rhs = rhs_all + (int64_t)fit * P;
+    float* dg = diag_all + (int64_t)fit * P;
+    const int tid = threadIdx.x;
     if (refactor) {
-        // ---- pre-pass: penalty shift, frozen coordinates
+        if (tid == 0) info[fit] = 0;
         for (int j = tid; j < P; j += kCT) {
             const float d = H[(int64_t)j * P + j] + dsh[j];
             const bool f = dsh[j] < 0.0f || !(d > 0.0f);
             frz[j] = f;
+            dg[j] = f ? 1.0f : d;
             if (!f) H[(int64_t)j * P + j] = d;
         }
         __syncthreads();
         for (int j = 0; j < P; ++j) {
-            if (!frz[j]) continue;                       // uniform (LDS flag)
+            if (!frz[j]) continue;
             for (int e = tid; e < P; e += kCT) {
-                if (e > j) H[(int64_t)j * P + e] = 0.0f;     // row j, right of diagonal
-                if (e < j) H[(int64_t)e * P + j] = 0.0f;     // column j, above diagonal
+                if (e > j) H[(int64_t)j * P + e] = 0.0f;
+                if (e < j) H[(int64_t)e * P + j] = 0.0f;
             }
             if (tid == 0) H[(int64_t)j * P + j] = 1.0f;
         }
-    } else {
-        for (int j = tid; j < P; j += kCT) frz[j] = frozen[j];
     }
-    for (int j = tid; j < P; j += kCT) rhs[j] = frz[j] ? 0.0f : (float)g[j];
     __syncthreads();
+    for (int j = tid; j < P; j += kCT) rhs[j] = frz[j] ? 0.0f : (float)g[j];
+}
 
-    for (int kb = 0; kb < nb; ++kb) {
-        const int k0 = kb * kNB;
-        // ---- 1. diagonal block
-        for (int e = tid; e < kNB * kNB; e += kCT) {
-            const int r = e / kNB, c = e % kNB;
-            sD[r][c] = (r <= c) ? H[(int64_t)(k0 + r) * P + k0 + c] : 0.0f;
+// One wave per fit: factor the diagonal block (refactor) and forward-solve the rhs block.
+__global__ void __launch_bounds__(64) chol_diag_kernel(
+    float* __restrict__ Hall, int32_t P, int32_t k0, const int32_t* __restrict__ fits,
+    uint8_t* __restrict__ frozen_all, float* __restrict__ rhs_all,
+    const float* __restrict__ diag_all, int32_t* __restrict__ info, int32_t refactor) {
+    __shared__ float sD[kNB][kNB + 1];
+    const int fit = fits[blockIdx.x];
+    float* H = Hall + (int64_t)fit * P * P;
+    uint8_t* frz = frozen_all + (int64_t)fit * P + k0;
+    float* rhs = rhs_all + (int64_t)fit * P + k0;
+    const int c = threadIdx.x;
+    for (int r = 0; r < kNB; ++r) sD[r][c] = (r <= c) ? H[(int64_t)(k0 + r) * P + k0 + c] : 0.0f;
+    __syncthreads();
+    int myfrz = frz[c];
+    if (refactor) {
+        const float orig = diag_all[(int64_t)fit * P + k0 + c];
+        int dropped = 0;
+        for (int q = 0; q < kNB; ++q) {
+            const float piv = __shfl(sD[q][c], q, 64);
+            const float origq = __shfl(orig, q, 64);
+            const bool was = __shfl(myfrz, q, 64) != 0;
+            const bool drop = was || !(piv > 1e-6f * origq);
+            const float d = drop ? 1.0f : sqrtf(piv);
+            float u = sD[q][c];
+            if (c == q) u = d;
+            else if (c > q) u = drop ? 0.0f : u / d;
+            sD[q][c] = u;
+            if (c == q && drop && !was) { myfrz = 1; dropped = 1; }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            if (c > q)
+                for (int i = q + 1; i <= c; ++i) sD[i][c] -= sD[q][i] * u;
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         }
-        __syncthreads();
-        if (refactor && wave == 0) {
-            // lane = column c of the block; rows are walked sequentially
-            const int c = lane;
-            const float orig = sD[c][c];
-            for (int q = 0; q < kNB; ++q) {
-                float piv = __shfl(sD[q][c], q, 64);     // sD[q][q]
-                const float origq = __shfl(orig, q, 64);
-                bool drop = frz[k0 + q] || !(piv > 1e-6f * origq);
-                float d = drop ? 1.0f : sqrtf(piv);
-                // row q of U: U[q][c] = A[q][c] / d for c > q
-                float u = sD[q][c];
-                if (c == q) u = d;
-                else if (c > q) u = drop ? 0.0f : u / d;
-                sD[q][c] = u;
-                if (drop && c == q && !frz[k0 + q]) { frz[k0 + q] = 1; atomicAdd(&ndrop, 1); }
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                // trailing: for rows i in (q, c]: A[i][c] -= U[q][i] U[q][c]
-                if (c > q) {
-                    for (int i = q + 1; i <= c; ++i) sD[i][c] -= sD[q][i] * u;
-                }
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            }
-        }
-        __syncthreads();
-        if (refactor) {
-            for (int e = tid; e < kNB * kNB; e += kCT) {
-                const int r = e / kNB, c = e % kNB;
-                if (r <= c) H[(int64_t)(k0 + r) * P + k0 + c] = sD[r][c];
-            }
-        }
-        // forward substitution of the rhs block: U_kk^T z = rhs_k (one wave, lane = row)
-        if (wave == 0) {
-            float zc = rhs[k0 + lane];
-            for (int q = 0; q < kNB; ++q) {
-                const float zq = __shfl(zc, q, 64) / sD[q][q];
-                const float zz = frz[k0 + q] ? 0.0f : zq;
-                if (lane == q) zc = zz;
-                else if (lane > q) zc -= sD[q][lane] * zz;
-            }
-            rhs[k0 + lane] = zc;
-        }
-        __syncthreads();
-        // ---- 2. row panel + rhs update
-        for (int j = k0 + kNB + tid; j < P; j += kCT) {
-            float x[kNB];
-#pragma unroll
-            for (int r = 0; r < kNB; ++r) x[r] = H[(int64_t)(k0 + r) * P + j];
-            if (refactor) {
-#pragma unroll
-                for (int c = 0; c < kNB; ++c) {
-                    float v = x[c];
-#pragma unroll
-                    for (int r = 0; r < c; ++r) v -= sD[r][c] * x[r];
-                    x[c] = frz[k0 + c] ? 0.0f : v / sD[c][c];
-                }
-#pragma unroll
-                for (int r = 0; r < kNB; ++r) H[(int64_t)(k0 + r) * P + j] = x[r];
-            }
-            float s = 0.0f;
-#pragma unroll
-            for (int r = 0; r < kNB; ++r) s += x[r] * rhs[k0 + r];
-            rhs[j] -= s;
-        }
-        __syncthreads();
-        if (!refactor) continue;
-        // ---- 3. trailing update of the remaining upper triangle
-        const int ty = tid >> 4, tx = tid & 15;
-        for (int bi = kb + 1; bi < nb; ++bi) {
-            for (int e = tid; e < kNB * kNB; e += kCT) {
-                const int r = e / kNB, c = e % kNB;
-                sPi[r][c] = H[(int64_t)(k0 + r) * P + bi * kNB + c];
-            }
-            for (int bj = bi; bj < nb; ++bj) {
-                for (int e = tid; e < kNB * kNB / 4; e += kCT) {
-                    const int r = e / (kNB / 4), c4 = e % (kNB / 4);
-                    *reinterpret_cast<f32x4*>(&sPj[r][c4 * 4]) =
-                        *reinterpret_cast<const f32x4*>(&H[(int64_t)(k0 + r) * P + bj * kNB + c4 * 4]);
-                }
-                __syncthreads();
-                float acc[4][4] = {};
-#pragma unroll 8
-                for (int r = 0; r < kNB; ++r) {
-                    const f32x4 a = *reinterpret_cast<const f32x4*>(&sPi[r][ty * 4]);
-                    const f32x4 b = *reinterpret_cast<const f32x4*>(&sPj[r][tx * 4]);
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-#pragma unroll
-                        for (int v = 0; v < 4; ++v) acc[u][v] += a[u] * b[v];
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    float* row = &H[(int64_t)(bi * kNB + ty * 4 + u) * P + bj * kNB + tx * 4];
-                    f32x4 cur = *reinterpret_cast<f32x4*>(row);
-                    cur[0] -= acc[u][0]; cur[1] -= acc[u][1];
-                    cur[2] -= acc[u][2]; cur[3] -= acc[u][3];
-                    *reinterpret_cast<f32x4*>(row) = cur;
-                }
-                __syncthreads();
-            }
-        }
+        if (dropped) atomicAdd(&info[fit], 1);
+        frz[c] = (uint8_t)myfrz;
+        for (int r = 0; r <= c; ++r) H[(int64_t)(k0 + r) * P + k0 + c] = sD[r][c];
         __syncthreads();
     }
+    // forward solve U_kk^T z = rhs_k, lane = row
+    float zc = rhs[c];
+    for (int q = 0; q < kNB; ++q) {
+        const float zq = __shfl(zc, q, 64) / sD[q][q];
+        const float zz = __shfl(myfrz, q, 64) ? 0.0f : zq;
+        if (c == q) zc = zz;
+        else if (c > q) zc -= sD[q][c] * zz;
+    }
+    rhs[c] = zc;
+}
 
-    // ---- back substitution U x = z (rhs holds z), blocks from the bottom
+// Panel: columns j >= k0+NB in chunks of 256 per workgroup.
+__global__ void __launch_bounds__(kCT) chol_panel_kernel(
+    float* __restrict__ Hall, int32_t P, int32_t k0, const int32_t* __restrict__ fits,
+    const uint8_t* __restrict__ frozen_all, float* __restrict__ rhs_all, int32_t refactor) {
+    __shared__ float sD[kNB][kNB + 1];
+    __shared__ float z[kNB];
+    __shared__ uint8_t fz[kNB];
+    const int fit = fits[blockIdx.x];
+    float* H = Hall + (int64_t)fit * P * P;
+    float* rhs = rhs_all + (int64_t)fit * P;
+    const int tid = threadIdx.x;
+    for (int e = tid; e < kNB * kNB; e += kCT) {
+        const int r = e / kNB, c = e % kNB;
+        sD[r][c] = (r <= c) ? H[(int64_t)(k0 + r) * P + k0 + c] : 0.0f;
+    }
+    if (tid < kNB) {
+        z[tid] = rhs[k0 + tid];
+        fz[tid] = frozen_all[(int64_t)fit * P + k0 + tid];
+    }
+    __syncthreads();
+    const int j = k0 + kNB + blockIdx.y * kCT + tid;
+    if (j >= P) return;
+    float x[kNB];
+#pragma unroll
+    for (int r = 0; r < kNB; ++r) x[r] = H[(int64_t)(k0 + r) * P + j];
+    if (refactor) {
+#pragma unroll
+        for (int c = 0; c < kNB; ++c) {
+            float v = x[c];
+#pragma unroll
+            for (int r = 0; r < c; ++r) v -= sD[r][c] * x[r];
+            x[c] = fz[c] ? 0.0f : v / sD[c][c];
+        }
+#pragma unroll
+        for (int r = 0; r < kNB; ++r) H[(int64_t)(k0 + r) * P + j] = x[r];
+    }
+    float s = 0.0f;
+#pragma unroll
+    for (int r = 0; r < kNB; ++r) s += x[r] * z[r];
+    rhs[j] -= s;
+}
+
+// Trailing update of the upper triangle: one 64x64 tile (bi <= bj, both > kb) per WG.
+__global__ void __launch_bounds__(kCT) chol_update_kernel(float* __restrict__ Hall, int32_t P,
+                                                          int32_t kb,
+                                                          const int32_t* __restrict__ fits) {
+    __shared__ __attribute__((aligned(16))) float sPi[kNB][kNB];
+    __shared__ __attribute__((aligned(16))) float sPj[kNB][kNB];
+    const int fit = fits[blockIdx.x];
+    float* H = Hall + (int64_t)fit * P * P;
+    const int T = P / kNB - kb - 1;
+    int t = blockIdx.y, bi = 0, rowlen = T;
+    while (t >= rowlen) { t -= rowlen; ++bi; --rowlen; }
+    const int bj = bi + t;
+    const int k0 = kb * kNB;
+    const int c0i = (kb + 1 + bi) * kNB, c0j = (kb + 1 + bj) * kNB;
+    const int tid = threadIdx.x;
+    for (int e = tid; e < kNB * kNB / 4; e += kCT) {
+        const int r = e / (kNB / 4), c4 = e % (kNB / 4);
+        *reinterpret_cast<f32x4*>(&sPi[r][c4 * 4]) =
+            *reinterpret_cast<const f32x4*>(&H[(int64_t)(k0 + r) * P + c0i + c4 * 4]);
+        *reinterpret_cast<f32x4*>(&sPj[r][c4 * 4]) =
+            *reinterpret_cast<const f32x4*>(&H[(int64_t)(k0 + r) * P + c0j + c4 * 4]);
+    }
+    __syncthreads();
+    const int ty = tid >> 4, tx = tid & 15;
+    float acc[4][4] = {};
+#pragma unroll 8
+    for (int r = 0; r < kNB; ++r) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(&sPi[r][ty * 4]);
+        const f32x4 b = *reinterpret_cast<const f32x4*>(&sPj[r][tx * 4]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) acc[u][v] += a[u] * b[v];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        float* row = &H[(int64_t)(c0i + ty * 4 + u) * P + c0j + tx * 4];
+        f32x4 cur = *reinterpret_cast<f32x4*>(row);
+        cur[0] -= acc[u][0]; cur[1] -= acc[u][1]; cur[2] -= acc[u][2]; cur[3] -= acc[u][3];
+        *reinterpret_cast<f32x4*>(row) = cur;
+    }
+}
+
+// Blocked back substitution U x = z, then delta = -x.
+__global__ void __launch_bounds__(kCT) chol_back_kernel(
+    const float* __restrict__ Hall, int32_t P, const int32_t* __restrict__ fits,
+    const uint8_t* __restrict__ frozen_all, float* __restrict__ rhs_all,
+    float* __restrict__ delta_all) {
+    __shared__ float sD[kNB][kNB + 1];
     __shared__ float part[kNB];
+    __shared__ float x[kMaxP];
+    const int fit = fits[blockIdx.x];
+    const float* H = Hall + (int64_t)fit * P * P;
+    const uint8_t* frz = frozen_all + (int64_t)fit * P;
+    const float* z = rhs_all + (int64_t)fit * P;
+    float* delta = delta_all + (int64_t)fit * P;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nb = P / kNB;
     for (int kb = nb - 1; kb >= 0; --kb) {
         const int k0 = kb * kNB;
-        // s_r = z_r - sum_{j >= k0+NB} U[k0+r][j] x_j : each wave takes 16 rows
         for (int rr = 0; rr < kNB / 4; ++rr) {
             const int r = wave * (kNB / 4) + rr;
             float s = 0.0f;
-            for (int j = k0 + kNB + lane; j < P; j += 64) s += H[(int64_t)(k0 + r) * P + j] * rhs[j];
+            for (int j = k0 + kNB + lane; j < P; j += 64) s += H[(int64_t)(k0 + r) * P + j] * x[j];
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
             if (lane == 0) part[r] = s;
@@ -200,37 +231,59 @@ __global__ void __launch_bounds__(kCT) chol_solve_kernel(
         }
         __syncthreads();
         if (wave == 0) {
-            float v = rhs[k0 + lane] - part[lane];
+            float v = z[k0 + lane] - part[lane];
             for (int q = kNB - 1; q >= 0; --q) {
                 const float xq = frz[k0 + q] ? 0.0f : __shfl(v, q, 64) / sD[q][q];
                 if (lane == q) v = xq;
                 else if (lane < q) v -= sD[lane][q] * xq;
             }
-            rhs[k0 + lane] = v;
+            x[k0 + lane] = v;
         }
         __syncthreads();
     }
-    for (int j = tid; j < P; j += kCT) {
-        delta[j] = frz[j] ? 0.0f : -rhs[j];
-        if (refactor) frozen[j] = frz[j];
-    }
-    if (tid == 0 && refactor) info[fit] = ndrop;
+    for (int j = tid; j < P; j += kCT) delta[j] = frz[j] ? 0.0f : -x[j];
 }
 
 }  // namespace sglm
 
 using namespace sglm;
 
+extern "C" size_t sglm_chol_work_bytes(int32_t P, int32_t B) {
+    return (size_t)2 * (size_t)B * (size_t)P * sizeof(float);
+}
+
 extern "C" int sglm_chol_solve_ex(float* H, int32_t P, const int32_t* fits, int32_t nact,
                                   const double* g, const float* dshift, float* delta,
                                   int32_t* info, uint8_t* frozen, int32_t refactor,
-                                  sglm_stream_t stream) {
+                                  int32_t B, void* work, sglm_stream_t stream) {
     if (nact <= 0) return SGLM_OK;
-    if (!H || !fits || !g || !dshift || !delta || !info || !frozen || P % kNB || P > kMaxP) {
+    if (!H || !fits || !g || !dshift || !delta || !info || !frozen || !work || P % kNB ||
+        P > kMaxP || B < nact) {
         set_error("sglm_chol_solve: bad args (P=%d, max %d)", P, kMaxP);
         return SGLM_EINVAL;
     }
-    chol_solve_kernel<<<nact, kCT, 0, as_stream(stream)>>>(H, P, fits, g, dshift, delta, info,
-                                                           frozen, refactor);
-    return check_launch("chol_solve_kernel");
+    hipStream_t s = as_stream(stream);
+    float* rhs = (float*)work;
+    float* dg = rhs + (size_t)B * P;
+    chol_prep_kernel<<<nact, kCT, 0, s>>>(H, P, fits, g, dshift, frozen, rhs, dg, info, refactor);
+    int st = check_launch("chol_prep_kernel");
+    if (st) return st;
+    const int nb = P / kNB;
+    for (int kb = 0; kb < nb; ++kb) {
+        const int k0 = kb * kNB;
+        chol_diag_kernel<<<nact, 64, 0, s>>>(H, P, k0, fits, frozen, rhs, dg, info, refactor);
+        const int rem = P - k0 - kNB;
+        if (rem > 0) {
+            chol_panel_kernel<<<dim3(nact, (rem + kCT - 1) / kCT), kCT, 0, s>>>(H, P, k0, fits,
+                                                                               frozen, rhs, refactor);
+            if (refactor) {
+                const int T = nb - kb - 1;
+                chol_update_kernel<<<dim3(nact, T * (T + 1) / 2), kCT, 0, s>>>(H, P, kb, fits);
+            }
+        }
+    }
+    st = check_launch("chol block kernels");
+    if (st) return st;
+    chol_back_kernel<<<nact, kCT, 0, s>>>(H, P, fits, frozen, rhs, delta);
+    return check_launch("chol_back_kernel");
 }

@@ -20,6 +20,10 @@
 //   * optional split-K over rows (blockIdx.y) into fixed-order f32 slabs.
 #include "common.h"
 
+#ifndef SGLM_SYRK_DEFAULT
+#define SGLM_SYRK_DEFAULT 2
+#endif
+
 namespace sglm {
 
 constexpr int kBM = 256;       // output tile edge
@@ -188,9 +192,9 @@ size_t sglm_syrk_work_bytes(int32_t P, int32_t nact, int32_t splits) {
     return (size_t)splits * (size_t)nact * (size_t)P * (size_t)P * sizeof(float);
 }
 
-int sglm_syrk(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, const float* W,
-              const int32_t* fits, int32_t nact, int32_t splits, float* H, void* work,
-              sglm_stream_t stream) {
+int sglm_syrk_v1(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, const float* W,
+                 const int32_t* fits, int32_t nact, int32_t splits, float* H, void* work,
+                 sglm_stream_t stream) {
     if (nact <= 0) return SGLM_OK;
     if (!Xb || !W || !fits || !H || P % kBM || ld % kBK || n > ld || splits < 1 ||
         (splits > 1 && !work)) {
@@ -220,6 +224,17 @@ int sglm_syrk(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, const float*
     unsigned gx = (unsigned)((PP + 255) / 256 < 4096 ? (PP + 255) / 256 : 4096);
     syrk_reduce<<<dim3(gx, (unsigned)nact), 256, 0, s>>>(slab, P, nact, splits, fits, H);
     return check_launch("syrk_reduce");
+}
+
+int sglm_syrk_variant(int32_t variant, const uint16_t* Xb, int64_t ld, int32_t P, int64_t n,
+                      const float* W, const int32_t* fits, int32_t nact, int32_t splits,
+                      float* H, void* work, sglm_stream_t stream);
+
+int sglm_syrk(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, const float* W,
+              const int32_t* fits, int32_t nact, int32_t splits, float* H, void* work,
+              sglm_stream_t stream) {
+    return sglm_syrk_variant(SGLM_SYRK_DEFAULT, Xb, ld, P, n, W, fits, nact, splits, H, work,
+                             stream);
 }
 
 }  // extern "C"
@@ -335,4 +350,174 @@ extern "C" int sglm_syrk_f32(const float* Xf, int64_t ld, int32_t P, int64_t n, 
     unsigned gx = (unsigned)((PP + 255) / 256 < 4096 ? (PP + 255) / 256 : 4096);
     syrk_reduce_t<<<dim3(gx, (unsigned)nact), 256, 0, s>>>(slab, P, nact, splits, kFBM, fits, H);
     return check_launch("syrk_reduce_t");
+}
+
+// ---------------------------------------------------------------------------------------
+// v2: LDS-DMA staging.  Both X panels go global -> LDS with global_load_lds_dwordx4 (no
+// VGPR staging, no ds_write); the weights are applied in registers to the B fragments
+// after ds_read (8 v_mul + 4 v_cvt_pk per fragment, hidden between MFMAs).
+//   * BK = 64 rows per K-step; a predictor's K-slice is one 128-B LDS row; a panel is
+//     256 rows x 128 B = 32 KB = 32 wave-instructions of 1 KB (8 predictors each).
+//   * 16-B chunk q of predictor c is stored at position q ^ ((c >> 1) & 7): the 16-lane
+//     groups of ds_read_b128 (distinct r mod 16) then hit 16 distinct (bank-row half,
+//     chunk) pairs -> conflict-free.  The permutation is applied to the per-lane GLOBAL
+//     source address (the LDS destination of an LDS-DMA is lane-linear).
+//   * diagonal tiles (ti == tj) stage one panel and read both operands from it.
+//   * 2 stages x (A 32 KB + B 32 KB + w 256 B) = 128.5 KB LDS, one workgroup per CU.
+namespace sglm {
+typedef __attribute__((address_space(3))) void lds_void_t;
+constexpr int k2BK = 64;
+constexpr int k2Panel = 256 * 128;                 // bytes
+constexpr int k2Stage = 2 * k2Panel + 256;         // A, B, w[64]
+
+__device__ __forceinline__ void glds16(const void* g, char* l) {
+    __builtin_amdgcn_global_load_lds(g, (lds_void_t*)l, 16, 0, 0);
+}
+__device__ __forceinline__ void glds4(const void* g, char* l) {
+    __builtin_amdgcn_global_load_lds(g, (lds_void_t*)l, 4, 0, 0);
+}
+
+__global__ void __launch_bounds__(512) syrk2_kernel(
+    const uint16_t* __restrict__ Xb, int64_t ld, int32_t P, int64_t nsteps_total,
+    int64_t steps_per_split, const float* __restrict__ W, const int32_t* __restrict__ fits,
+    int32_t ntiles, float* __restrict__ H, float* __restrict__ slab, int32_t nact) {
+    extern __shared__ __attribute__((aligned(16))) char sm2[];
+    const int nt = P / 256;
+    const int tile = blockIdx.x % ntiles;
+    const int slot = blockIdx.x / ntiles;
+    const int split = blockIdx.y;
+    int ti, tj;
+    tile_coords(tile, nt, ti, tj);
+    const bool diag = ti == tj;
+    const int fit = fits[slot];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wave >> 2, wc = wave & 3;
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t step0 = (int64_t)split * steps_per_split;
+    const int64_t step1 = min(step0 + steps_per_split, nsteps_total);
+    const int64_t nsteps = step1 - step0;
+    const uint16_t* XA = Xb + (int64_t)(ti * 256) * ld;
+    const uint16_t* XB = Xb + (int64_t)(tj * 256) * ld;
+    const float* w = W + (int64_t)fit * ld;
+
+    // LDS-DMA lane mapping: wave handles column blocks cb = 4*wave + u (8 predictors each)
+    const int lc = lane >> 3, lpos = lane & 7;
+    int64_t goff[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int c = (4 * wave + u) * 8 + lc;
+        goff[u] = (int64_t)c * ld + 8 * (lpos ^ ((c >> 1) & 7));
+    }
+    auto stage = [&](int buf, int64_t step) {
+        char* base = sm2 + buf * k2Stage;
+        const int64_t i0 = step * k2BK;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            glds16(XA + goff[u] + i0, base + (4 * wave + u) * 1024);
+        if (!diag) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                glds16(XB + goff[u] + i0, base + k2Panel + (4 * wave + u) * 1024);
+        }
+        if (wave == 0) glds4(w + i0 + lane, base + 2 * k2Panel);
+    };
+
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) acc[m][n] = (f32x16){};
+
+    if (nsteps > 0) {
+        stage(0, step0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (int64_t s = 0; s < nsteps; ++s) {
+            const int cur = (int)(s & 1);
+            if (s + 1 < nsteps) stage(cur ^ 1, step0 + s + 1);
+            const char* A = sm2 + cur * k2Stage;
+            const char* Bp = diag ? A : A + k2Panel;
+            const float* wv = reinterpret_cast<const float*>(A + 2 * k2Panel);
+#pragma unroll
+            for (int ks = 0; ks < k2BK / 16; ++ks) {
+                const int q = 2 * ks + h;
+                bf16x8 af[4], bfr[2];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const int c = wr * 128 + m * 32 + r;
+                    af[m] = *reinterpret_cast<const bf16x8*>(A + c * 128 + 16 * (q ^ ((c >> 1) & 7)));
+                }
+                const f32x4 w0 = *reinterpret_cast<const f32x4*>(wv + 16 * ks + 8 * h);
+                const f32x4 w1 = *reinterpret_cast<const f32x4*>(wv + 16 * ks + 8 * h + 4);
+#pragma unroll
+                for (int n = 0; n < 2; ++n) {
+                    const int c = wc * 64 + n * 32 + r;
+                    const bf16x8 raw = *reinterpret_cast<const bf16x8*>(Bp + c * 128 + 16 * (q ^ ((c >> 1) & 7)));
+                    bf16x8 sc;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        sc[j] = (__bf16)((float)raw[j] * w0[j]);
+                        sc[4 + j] = (__bf16)((float)raw[4 + j] * w1[j]);
+                    }
+                    bfr[n] = sc;
+                }
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+#pragma unroll
+                    for (int n = 0; n < 2; ++n)
+                        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[m], bfr[n],
+                                                                            acc[m][n], 0, 0, 0);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+    }
+    float* out = slab ? slab + ((int64_t)split * nact + slot) * (int64_t)P * P
+                      : H + (int64_t)fit * P * P;
+    const int64_t rbase = (int64_t)ti * 256 + wr * 128;
+    const int64_t cbase = (int64_t)tj * 256 + wc * 64;
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                out[(rbase + m * 32 + (j & 3) + 8 * (j >> 2) + 4 * h) * P + cbase + n * 32 + r] =
+                    acc[m][n][j];
+}
+}  // namespace sglm
+
+// Development entry: run a specific Gram kernel variant (1 = register-staged, 2 = LDS-DMA).
+extern "C" int sglm_syrk_variant(int32_t variant, const uint16_t* Xb, int64_t ld, int32_t P,
+                                 int64_t n, const float* W, const int32_t* fits, int32_t nact,
+                                 int32_t splits, float* H, void* work, sglm_stream_t stream) {
+    if (variant == 1) return sglm_syrk_v1(Xb, ld, P, n, W, fits, nact, splits, H, work, stream);
+    if (nact <= 0) return SGLM_OK;
+    if (!Xb || !W || !fits || !H || P % 256 || ld % 256 || n > ld || splits < 1 ||
+        (splits > 1 && !work)) {
+        set_error("sglm_syrk_variant: bad args");
+        return SGLM_EINVAL;
+    }
+    const int nt = P / 256;
+    const int ntiles = nt * (nt + 1) / 2;
+    const int64_t nst = (n + k2BK - 1) / k2BK;
+    const int64_t sps = (nst + splits - 1) / splits;
+    const size_t lds = (size_t)2 * k2Stage;
+    hipStream_t s = as_stream(stream);
+    static bool attr2 = false;
+    if (!attr2) {
+        (void)hipFuncSetAttribute((const void*)syrk2_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr2 = true;
+    }
+    float* slab = splits > 1 ? (float*)work : nullptr;
+    syrk2_kernel<<<dim3((unsigned)(ntiles * nact), (unsigned)splits), 512, lds, s>>>(
+        Xb, ld, P, nst, sps, W, fits, ntiles, H, slab, nact);
+    int st = check_launch("syrk2_kernel");
+    if (st || splits == 1) return st;
+    const int64_t PP = (int64_t)P * P;
+    unsigned gx = (unsigned)((PP + 255) / 256 < 4096 ? (PP + 255) / 256 : 4096);
+    syrk_reduce<<<dim3(gx, (unsigned)nact), 256, 0, s>>>(slab, P, nact, splits, fits, H);
+    return check_launch("syrk_reduce");
 }

@@ -29,8 +29,13 @@ SIGNATURES = {
     "sglm_xtr": (C.c_int, [_vp, _i32, _i64, _i32, _i64, _vp, _i32, _vp, _vp, _vp]),
     "sglm_syrk_work_bytes": (_sz, [_i32, _i32, _i32]),
     "sglm_syrk": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
+    "sglm_syrk_v1": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
+    "sglm_syrk_variant": (C.c_int, [_i32, _vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _vp,
+                                    _vp]),
     "sglm_syrk_f32": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
-    "sglm_chol_solve_ex": (C.c_int, [_vp, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp]),
+    "sglm_chol_work_bytes": (_sz, [_i32, _i32]),
+    "sglm_chol_solve_ex": (C.c_int, [_vp, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _i32,
+                                     _vp, _vp]),
     "sglm_rowsum_work_bytes": (_sz, [_i32, _i32, _i64]),
     "sglm_loss_trials": (C.c_int, [_i32, _f32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
                                    _vp, _i32, _vp, _vp, _vp]),

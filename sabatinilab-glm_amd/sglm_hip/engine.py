@@ -270,6 +270,8 @@ class _Buffers:
             self.dshift = torch.zeros((B, P), dtype=f32, device=dev)
             self.frozen = torch.zeros((B, P), dtype=torch.uint8, device=dev)
             self.info = torch.zeros((B,), dtype=torch.int32, device=dev)
+            self.cwork = torch.empty(_lib.query("sglm_chol_work_bytes", P, B), dtype=torch.uint8,
+                                     device=dev)
             self.key = key
         return self
 
@@ -387,7 +389,8 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         act_d = torch.tensor(act, dtype=torch.int32, device=dev)
         bf.delta.zero_()
         _lib.call("sglm_chol_solve_ex", _p(bf.H), P, _p(act_d), int(act.size), _p(bf.gtot),
-                  _p(bf.dshift), _p(bf.delta), _p(bf.info), _p(bf.frozen), refactor, st)
+                  _p(bf.dshift), _p(bf.delta), _p(bf.info), _p(bf.frozen), refactor, B,
+                  _p(bf.cwork), st)
         factored = True
         d.eta(bf.delta, bf.deta)
         delta = bf.delta.cpu().numpy().astype(np.float64)

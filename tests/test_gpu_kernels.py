@@ -142,8 +142,10 @@ def test_chol_solve_matches_numpy(engine, torch_mod):
     frozen = torch.zeros((B, P), dtype=torch.uint8, device="cuda")
     fits = torch.tensor([0, 1], dtype=torch.int32, device="cuda")
     dshd = torch.from_numpy(dsh).cuda()
+    cw = torch.empty(_lib.query("sglm_chol_work_bytes", P, B), dtype=torch.uint8, device="cuda")
     _lib.call("sglm_chol_solve_ex", Hd.data_ptr(), P, fits.data_ptr(), 2, gd.data_ptr(),
-              dshd.data_ptr(), out.data_ptr(), info.data_ptr(), frozen.data_ptr(), 1, 0)
+              dshd.data_ptr(), out.data_ptr(), info.data_ptr(), frozen.data_ptr(), 1, B,
+              cw.data_ptr(), 0)
     x = out.cpu().numpy()
     for k in range(B):
         M = H[k, : p + 1, : p + 1].astype(np.float64) + np.diag(np.r_[np.full(p, 3.0), 0.0])
@@ -155,7 +157,8 @@ def test_chol_solve_matches_numpy(engine, torch_mod):
     g2[:, p + 1:] = 0
     g2d = torch.from_numpy(g2).cuda()
     _lib.call("sglm_chol_solve_ex", Hd.data_ptr(), P, fits.data_ptr(), 2, g2d.data_ptr(),
-              dshd.data_ptr(), out.data_ptr(), info.data_ptr(), frozen.data_ptr(), 0, 0)
+              dshd.data_ptr(), out.data_ptr(), info.data_ptr(), frozen.data_ptr(), 0, B,
+              cw.data_ptr(), 0)
     x2 = out.cpu().numpy()
     for k in range(B):
         M = H[k, : p + 1, : p + 1].astype(np.float64) + np.diag(np.r_[np.full(p, 3.0), 0.0])
