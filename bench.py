@@ -174,6 +174,8 @@ def main():
                 "algorithmic_flop_per_fit_iter": f"n_train*p'*(p'+1), p'={pa}",
                 "launches": nlaunch,
                 "avg_launch_ms": ktime / max(nlaunch, 1) * 1e3,
+                "per_launch": [[n_, round(e0.elapsed_time(e1), 2), round(f_ / e0.elapsed_time(e1) / 1e9, 1)]
+                               for e0, e1, n_, f_ in stats.syrk_events] if world == 1 else None,
             },
             "cpu_baseline": cpu,
         }

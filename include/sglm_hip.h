@@ -108,6 +108,15 @@ int sglm_syrk(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, const float*
               const int32_t* fits, int32_t nact, int32_t splits, float* H, void* work,
               sglm_stream_t stream);
 
+/* As sglm_syrk, but fit k only visits the 8-row groups row_groups[group_offset[k] ..
+ * + group_count[k]) (ascending group indices, group g = rows 8g..8g+7): groups holding no
+ * row of the fit's mask are skipped.  Indexed by fit id (like W).  Requires ld > n (a zero
+ * padding row).  This is the fold-copy-free replacement of X[idx_train, :]. */
+int sglm_syrk_masked(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, const float* W,
+                     const int32_t* fits, int32_t nact, int32_t splits, float* H, void* work,
+                     const int32_t* row_groups, const int64_t* group_offset,
+                     const int32_t* group_count, sglm_stream_t stream);
+
 /* Development entries: a specific bf16 Gram variant (1 = register-staged, 2 = LDS-DMA
  * staged; sglm_syrk uses the default), same arguments as sglm_syrk. */
 int sglm_syrk_v1(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, const float* W,

@@ -379,8 +379,10 @@ __device__ __forceinline__ void glds4(const void* g, char* l) {
 
 __global__ void __launch_bounds__(512) syrk2_kernel(
     const uint16_t* __restrict__ Xb, int64_t ld, int32_t P, int64_t nsteps_total,
-    int64_t steps_per_split, const float* __restrict__ W, const int32_t* __restrict__ fits,
-    int32_t ntiles, float* __restrict__ H, float* __restrict__ slab, int32_t nact) {
+    int32_t splits, const float* __restrict__ W, const int32_t* __restrict__ fits,
+    int32_t ntiles, float* __restrict__ H, float* __restrict__ slab, int32_t nact,
+    const int32_t* __restrict__ grp, const int64_t* __restrict__ grp_off,
+    const int32_t* __restrict__ grp_cnt) {
     extern __shared__ __attribute__((aligned(16))) char sm2[];
     const int nt = P / 256;
     const int tile = blockIdx.x % ntiles;
@@ -394,8 +396,14 @@ __global__ void __launch_bounds__(512) syrk2_kernel(
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = wave >> 2, wc = wave & 3;
     const int r = lane & 31, h = lane >> 5;
-    const int64_t step0 = (int64_t)split * steps_per_split;
-    const int64_t step1 = min(step0 + steps_per_split, nsteps_total);
+    // row-group gather: K-step s covers the 8-row groups grp[8s .. 8s+7] of this fit's list
+    // (groups holding no training row are skipped); identity when grp == nullptr.
+    const int32_t* gl = grp ? grp + grp_off[fit] : nullptr;
+    const int64_t ngrp = grp ? (int64_t)grp_cnt[fit] : nsteps_total * 8;
+    const int64_t nst_fit = (ngrp + 7) / 8;
+    const int64_t sps = (nst_fit + splits - 1) / splits;
+    const int64_t step0 = (int64_t)split * sps;
+    const int64_t step1 = min(step0 + sps, nst_fit);
     const int64_t nsteps = step1 - step0;
     const uint16_t* XA = Xb + (int64_t)(ti * 256) * ld;
     const uint16_t* XB = Xb + (int64_t)(tj * 256) * ld;
@@ -403,24 +411,47 @@ __global__ void __launch_bounds__(512) syrk2_kernel(
 
     // LDS-DMA lane mapping: wave handles column blocks cb = 4*wave + u (8 predictors each)
     const int lc = lane >> 3, lpos = lane & 7;
-    int64_t goff[4];
+    // column c = (4*wave + u)*8 + lc is the same lc for every u, so the swizzled chunk
+    // q(u) = lpos ^ ((c >> 1) & 7) only depends on u through (c >> 1) & 7 = (4u' + lc) >> 1 ...
+    int64_t coff[4];
+    int qsel[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int c = (4 * wave + u) * 8 + lc;
-        goff[u] = (int64_t)c * ld + 8 * (lpos ^ ((c >> 1) & 7));
+        coff[u] = (int64_t)c * ld;
+        qsel[u] = lpos ^ ((c >> 1) & 7);
     }
-    auto stage = [&](int buf, int64_t step) {
-        char* base = sm2 + buf * k2Stage;
-        const int64_t i0 = step * k2BK;
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            glds16(XA + goff[u] + i0, base + (4 * wave + u) * 1024);
-        if (!diag) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                glds16(XB + goff[u] + i0, base + k2Panel + (4 * wave + u) * 1024);
+    const int64_t glast = ngrp - 1;
+    // Group indices of K-step t (8 ints) ride the same LDS-DMA path as the data: wave 0
+    // loads those of step t+2 into ring slot (t+2) % 3 while step t+1's panels are issued,
+    // so no VGPR-destination global load ever sits in the loop (hipcc would drain the
+    // in-flight DMA at its first use).  Identity mapping when there is no list.
+    int32_t* iring = reinterpret_cast<int32_t*>(sm2 + 2 * k2Stage);   // 3 x 64 ints
+    auto idx_glds = [&](int t) {              // relative step t -> slot t % 3 (wave 0 only)
+        if (gl && wave == 0) {
+            const int64_t gi = (step0 + t) * 8 + (lane & 7);
+            glds4(gl + (gi < ngrp ? gi : glast), reinterpret_cast<char*>(iring + (t % 3) * 64));
         }
-        if (wave == 0) glds4(w + i0 + lane, base + 2 * k2Panel);
+    };
+    auto group_of = [&](int t, int k) -> int64_t {       // group index of chunk k of step t
+        if (!gl) return (step0 + t) * 8 + k;
+        return iring[(t % 3) * 64 + k];
+    };
+    auto stage = [&](int buf, int t) {
+        char* base = sm2 + buf * k2Stage;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t row = group_of(t, qsel[u]) * 8;
+            glds16(XA + coff[u] + row, base + (4 * wave + u) * 1024);
+            if (!diag) glds16(XB + coff[u] + row, base + k2Panel + (4 * wave + u) * 1024);
+        }
+        if (wave == 0) {
+            const int gsel = lane >> 3;
+            const int64_t wrow = ((step0 + t) * 8 + gsel < ngrp)
+                                     ? group_of(t, gsel) * 8 + (lane & 7)
+                                     : (int64_t)ld - 1;      // padding row: w == 0
+            glds4(w + wrow, base + 2 * k2Panel);
+        }
     };
 
     f32x16 acc[4][2];
@@ -430,12 +461,20 @@ __global__ void __launch_bounds__(512) syrk2_kernel(
         for (int n = 0; n < 2; ++n) acc[m][n] = (f32x16){};
 
     if (nsteps > 0) {
-        stage(0, step0);
+        idx_glds(0);
+        if (nsteps > 1) idx_glds(1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        for (int64_t s = 0; s < nsteps; ++s) {
-            const int cur = (int)(s & 1);
-            if (s + 1 < nsteps) stage(cur ^ 1, step0 + s + 1);
+        stage(0, 0);
+        if (nsteps > 2) idx_glds(2);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (int s = 0; s < (int)nsteps; ++s) {
+            const int cur = s & 1;
+            if (s + 1 < nsteps) {
+                stage(cur ^ 1, s + 1);
+                if (s + 3 < nsteps) idx_glds(s + 3);
+            }
             const char* A = sm2 + cur * k2Stage;
             const char* Bp = diag ? A : A + k2Panel;
             const float* wv = reinterpret_cast<const float*>(A + 2 * k2Panel);
@@ -489,10 +528,36 @@ __global__ void __launch_bounds__(512) syrk2_kernel(
 }  // namespace sglm
 
 // Development entry: run a specific Gram kernel variant (1 = register-staged, 2 = LDS-DMA).
+static int syrk2_launch(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, const float* W,
+                        const int32_t* fits, int32_t nact, int32_t splits, float* H, void* work,
+                        const int32_t* grp, const int64_t* grp_off, const int32_t* grp_cnt,
+                        sglm_stream_t stream);
+
+extern "C" int sglm_syrk_masked(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n,
+                                const float* W, const int32_t* fits, int32_t nact,
+                                int32_t splits, float* H, void* work, const int32_t* row_groups,
+                                const int64_t* group_offset, const int32_t* group_count,
+                                sglm_stream_t stream) {
+    if (!row_groups || !group_offset || !group_count) {
+        set_error("sglm_syrk_masked: null group list");
+        return SGLM_EINVAL;
+    }
+    return syrk2_launch(Xb, ld, P, n, W, fits, nact, splits, H, work, row_groups, group_offset,
+                        group_count, stream);
+}
+
 extern "C" int sglm_syrk_variant(int32_t variant, const uint16_t* Xb, int64_t ld, int32_t P,
                                  int64_t n, const float* W, const int32_t* fits, int32_t nact,
                                  int32_t splits, float* H, void* work, sglm_stream_t stream) {
     if (variant == 1) return sglm_syrk_v1(Xb, ld, P, n, W, fits, nact, splits, H, work, stream);
+    return syrk2_launch(Xb, ld, P, n, W, fits, nact, splits, H, work, nullptr, nullptr, nullptr,
+                        stream);
+}
+
+static int syrk2_launch(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, const float* W,
+                        const int32_t* fits, int32_t nact, int32_t splits, float* H, void* work,
+                        const int32_t* grp, const int64_t* grp_off, const int32_t* grp_cnt,
+                        sglm_stream_t stream) {
     if (nact <= 0) return SGLM_OK;
     if (!Xb || !W || !fits || !H || P % 256 || ld % 256 || n > ld || splits < 1 ||
         (splits > 1 && !work)) {
@@ -502,8 +567,7 @@ extern "C" int sglm_syrk_variant(int32_t variant, const uint16_t* Xb, int64_t ld
     const int nt = P / 256;
     const int ntiles = nt * (nt + 1) / 2;
     const int64_t nst = (n + k2BK - 1) / k2BK;
-    const int64_t sps = (nst + splits - 1) / splits;
-    const size_t lds = (size_t)2 * k2Stage;
+    const size_t lds = (size_t)2 * k2Stage + 3 * 64 * sizeof(int32_t);
     hipStream_t s = as_stream(stream);
     static bool attr2 = false;
     if (!attr2) {
@@ -513,7 +577,7 @@ extern "C" int sglm_syrk_variant(int32_t variant, const uint16_t* Xb, int64_t ld
     }
     float* slab = splits > 1 ? (float*)work : nullptr;
     syrk2_kernel<<<dim3((unsigned)(ntiles * nact), (unsigned)splits), 512, lds, s>>>(
-        Xb, ld, P, nst, sps, W, fits, ntiles, H, slab, nact);
+        Xb, ld, P, nst, splits, W, fits, ntiles, H, slab, nact, grp, grp_off, grp_cnt);
     int st = check_launch("syrk2_kernel");
     if (st || splits == 1) return st;
     const int64_t PP = (int64_t)P * P;

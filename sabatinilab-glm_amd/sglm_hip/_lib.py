@@ -29,6 +29,8 @@ SIGNATURES = {
     "sglm_xtr": (C.c_int, [_vp, _i32, _i64, _i32, _i64, _vp, _i32, _vp, _vp, _vp]),
     "sglm_syrk_work_bytes": (_sz, [_i32, _i32, _i32]),
     "sglm_syrk": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
+    "sglm_syrk_masked": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp,
+                                   _vp, _vp]),
     "sglm_syrk_v1": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
     "sglm_syrk_variant": (C.c_int, [_i32, _vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _vp,
                                     _vp]),

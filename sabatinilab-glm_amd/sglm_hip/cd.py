@@ -23,6 +23,7 @@ def enet_batch(prob: E.Problem, objectives, reqs):
     dev = d.device
     st = E._stream()
     bf = E._BUF.get(B, P, ld, dev)
+    bf.groups = None                     # exact (f32) Gram path below does not gather rows
     fit_resp = torch.tensor([r.resp for r in reqs], dtype=torch.int32, device=dev)
     fit_mask = torch.tensor([r.mask for r in reqs], dtype=torch.int32, device=dev)
     bf.eta.zero_()

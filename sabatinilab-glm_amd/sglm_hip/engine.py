@@ -77,7 +77,7 @@ class Design:
         require_gpu()
         self.n, self.p = int(n), int(p)
         self.P = pad_to(self.p + 1, COL_PAD)
-        self.ld = pad_to(max(self.n, 1), ROW_PAD)
+        self.ld = pad_to(self.n + 1, ROW_PAD)     # >= 1 zero padding row (w = 0 there)
         alloc = torch.zeros if zero else torch.empty
         self.xb = alloc((self.P, self.ld), dtype=torch.bfloat16, device=device)
         self.xf = None
@@ -204,6 +204,24 @@ class Problem:
         self.Y = torch.from_numpy(Y).to(dev)
         self.M = torch.from_numpy(M).to(dev)
         self._stats = {}
+        # Gram row gathering: the 8-row groups of every 64-row block (one K-step, one 128-B
+        # line per predictor) that holds at least one row of the mask.  Whole aligned blocks
+        # keep every LDS-DMA segment on a single cache line (group-level gathering was
+        # measured slower per step than it saved).
+        goff, gcnt, lists = [], [], []
+        off = 0
+        for m in self.masks:
+            mp = np.zeros(pad_to(n, 64), dtype=bool)
+            mp[:n] = m > 0
+            blk = np.flatnonzero(mp.reshape(-1, 64).any(axis=1))
+            g = (blk[:, None] * 8 + np.arange(8)[None, :]).reshape(-1).astype(np.int32)
+            lists.append(g)
+            goff.append(off)
+            gcnt.append(g.size)
+            off += g.size
+        self.group_offset = np.array(goff, dtype=np.int64)
+        self.group_count = np.array(gcnt, dtype=np.int32)
+        self.groups = torch.from_numpy(np.concatenate(lists) if off else np.zeros(1, np.int32)).to(dev)
 
     def mask_stats(self, resp: int, mask: int):
         """float64 (count, sum y, mean y) over a mask — host side, cached."""
@@ -360,6 +378,10 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
     nsteps = (n + 31) // 32
     ntile1 = (P // 256) * (P // 256 + 1) // 2
     rows = np.array([prob.mask_stats(r.resp, r.mask)[0] for r in reqs], dtype=np.float64)
+    mk = np.array([r.mask for r in reqs])
+    bf.goff = torch.from_numpy(prob.group_offset[mk]).to(dev)
+    bf.gcnt = torch.from_numpy(prob.group_count[mk]).to(dev)
+    bf.groups = prob.groups
 
     for it in range(int(max_iter.max()) + 1):
         act = np.flatnonzero(active)
@@ -481,6 +503,9 @@ def _syrk(d: Design, bf, fits: np.ndarray, nsteps: int, ntile1: int, stats, st, 
     if use_f32:
         _lib.call("sglm_syrk_f32", _p(d.xf), d.ld, d.P, d.n, _p(bf.W), _p(fits_d), nact, splits,
                   _p(bf.H), _p(work), st)
+    elif getattr(bf, "groups", None) is not None:
+        _lib.call("sglm_syrk_masked", _p(d.xb), d.ld, d.P, d.n, _p(bf.W), _p(fits_d), nact,
+                  splits, _p(bf.H), _p(work), _p(bf.groups), _p(bf.goff), _p(bf.gcnt), st)
     else:
         _lib.call("sglm_syrk", _p(d.xb), d.ld, d.P, d.n, _p(bf.W), _p(fits_d), nact, splits,
                   _p(bf.H), _p(work), st)

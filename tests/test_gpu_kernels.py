@@ -248,3 +248,38 @@ def test_syrk_f32_exact_gram(engine, torch_mod):
         Href = (Xa * W[1, :5000, None].astype(np.float64)).T @ Xa
         up = np.triu(np.ones((pa, pa), bool))
         assert rel(H[1].cpu().numpy()[:pa, :pa][up], Href[up]) < 1e-5, splits   # f32 accumulation
+
+
+def test_syrk_masked_row_groups(engine, torch_mod):
+    """Row-group gathering (skipped test-trial blocks) == the dense masked Gram, bitwise."""
+    torch = torch_mod
+    from sglm_hip import _lib, synth
+    s = synth.make(N=20000, m=9, L=5, rho=0.2, seed=12)
+    d = engine.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
+    rng = np.random.default_rng(13)
+    trial_test = rng.random(200) < 0.3                # 100-row trials held out
+    masks = [np.repeat(~trial_test, 100).astype(np.uint8), np.ones(s.N, np.uint8),
+             np.zeros(s.N, np.uint8)]
+    masks[2][:37] = 1                                  # a fit with a single partial group
+    prob = engine.Problem(d, [s.y], masks)
+    B = 3
+    W = torch.zeros((B, d.ld), dtype=torch.float32, device="cuda")
+    for k in range(B):
+        W[k, : s.N] = torch.from_numpy(masks[k].astype(np.float32) * rng.random(s.N).astype(np.float32))
+    fits = torch.tensor([0, 1, 2], dtype=torch.int32, device="cuda")
+    goff = torch.from_numpy(prob.group_offset).cuda()
+    gcnt = torch.from_numpy(prob.group_count).cuda()
+    for splits in (1, 2):
+        wk = torch.empty(max(_lib.query("sglm_syrk_work_bytes", d.P, B, splits), 16),
+                         dtype=torch.uint8, device="cuda")
+        H1 = torch.zeros((B, d.P, d.P), dtype=torch.float32, device="cuda")
+        H2 = torch.zeros_like(H1)
+        _lib.call("sglm_syrk", d.xb.data_ptr(), d.ld, d.P, d.n, W.data_ptr(), fits.data_ptr(), B,
+                  splits, H1.data_ptr(), wk.data_ptr(), 0)
+        _lib.call("sglm_syrk_masked", d.xb.data_ptr(), d.ld, d.P, d.n, W.data_ptr(),
+                  fits.data_ptr(), B, splits, H2.data_ptr(), wk.data_ptr(),
+                  prob.groups.data_ptr(), goff.data_ptr(), gcnt.data_ptr(), 0)
+        up = torch.triu(torch.ones((d.P, d.P), dtype=torch.bool, device="cuda"))
+        for k in range(B):
+            a, b = H1[k][up], H2[k][up]
+            assert torch.max(torch.abs(a - b)).item() <= 1e-6 * max(1.0, torch.max(torch.abs(a)).item()), (splits, k)

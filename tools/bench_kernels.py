@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--splits", type=int, default=1)
     ap.add_argument("--other", action="store_true", help="also time chol / eta / xtr")
+    ap.add_argument("--masked", action="store_true",
+                    help="also time sglm_syrk_masked with 20%% of 100-row trials held out")
     a = ap.parse_args()
     import torch
     from sglm_hip import _lib, engine as E, synth
@@ -61,6 +63,32 @@ def main():
         t = float(np.median(times[v]))
         res[f"syrk_v{v}"] = {"ms": t * 1e3, "exec_TFLOPs": exec_flop / t / 1e12,
                              "alg_TFLOPs": alg_flop / t / 1e12, "min_ms": min(times[v]) * 1e3}
+    if a.masked:
+        rng = np.random.default_rng(1)
+        ntr = (d.n + 99) // 100
+        m = np.repeat(rng.random(ntr) >= 0.2, 100)[: d.n].astype(np.uint8)
+        prob = E.Problem(d, [np.zeros(d.n)], [m])
+        Wm = W.clone()
+        Wm[:, : d.n] *= torch.from_numpy(m.astype(np.float32)).cuda()
+        goff = torch.zeros(B, dtype=torch.int64, device="cuda")
+        gcnt = torch.full((B,), int(prob.group_count[0]), dtype=torch.int32, device="cuda")
+        Hm = torch.zeros_like(H[list(H)[0]])
+        tm = []
+        for rep in range(a.reps + 1):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            _lib.call("sglm_syrk_masked", d.xb.data_ptr(), d.ld, d.P, d.n, Wm.data_ptr(),
+                      fits.data_ptr(), B, a.splits, Hm.data_ptr(), work.data_ptr(),
+                      prob.groups.data_ptr(), goff.data_ptr(), gcnt.data_ptr(), st)
+            e1.record()
+            torch.cuda.synchronize()
+            if rep:
+                tm.append(e0.elapsed_time(e1) / 1e3)
+        t = float(np.median(tm))
+        rows = float(m.sum())
+        res["syrk_masked"] = {"ms": t * 1e3, "train_rows": rows,
+                              "groups_frac": float(prob.group_count[0]) * 8 / d.n,
+                              "alg_TFLOPs": B * rows * pa * (pa + 1) / t / 1e12}
     vs = list(H)
     if len(vs) > 1:
         up = torch.triu(torch.ones((d.P, d.P), dtype=torch.bool, device="cuda"))
