@@ -117,6 +117,20 @@ int sglm_syrk_masked(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, const
                      const int32_t* row_groups, const int64_t* group_offset,
                      const int32_t* group_count, sglm_stream_t stream);
 
+/* Bit-plane form of a 0/1 design: bits[a * (ld/32) + q] bit b = (X[a][32q + b] != 0).
+ * *nonbinary (device int32, caller-zeroed) is set if any value is not exactly 0 or 1. */
+int sglm_pack_bits(const uint16_t* Xb, int64_t ld, int32_t P, uint32_t* bits,
+                   int32_t* nonbinary, sglm_stream_t stream);
+
+/* sglm_syrk(_masked) for a 0/1 design in bit-plane form (v3: 16x fewer bytes per K-step,
+ * the 1M x 2048 design is 256 MB and stays in the Infinity Cache).  Row lists, when given,
+ * must consist of whole aligned 64-row blocks (8 consecutive groups 8b..8b+7).  Bitwise
+ * identical to sglm_syrk on the same design. */
+int sglm_syrk_bits(const uint32_t* Xbits, int64_t ld, int32_t P, int64_t n, const float* W,
+                   const int32_t* fits, int32_t nact, int32_t splits, float* H, void* work,
+                   const int32_t* row_groups, const int64_t* group_offset,
+                   const int32_t* group_count, sglm_stream_t stream);
+
 /* Development entries: a specific bf16 Gram variant (1 = register-staged, 2 = LDS-DMA
  * staged; sglm_syrk uses the default), same arguments as sglm_syrk. */
 int sglm_syrk_v1(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, const float* W,

@@ -585,3 +585,220 @@ static int syrk2_launch(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, co
     syrk_reduce<<<dim3(gx, (unsigned)nact), 256, 0, s>>>(slab, P, nact, splits, fits, H);
     return check_launch("syrk_reduce");
 }
+
+// ---------------------------------------------------------------------------------------
+// v3: bit-packed 0/1 designs.  Event designs (the reference's time-shifted indicators) are
+// stored as bit-planes Xbits[a][i/32] (1 bit per element: 256 MB at 1M x 2048, resident in
+// the Infinity Cache), which removes the fabric bandwidth bound of v2 (16x fewer bytes per
+// K-step).  Per K-step each thread loads one 32-bit word per panel (32 rows of one
+// predictor), expands it to 16-bit masks (0x0000 / 0xFFFF) in LDS; fragments become bf16
+// by one v_and per dword: A = mask & bf16(1.0), B = mask & bf16(w) pair.  The result is
+// bitwise identical to v2 (bf16(1 * w) == bf16(w)).
+// LDS rows: 64 rows x 2 B = 128 B + 16 B pad (36-dword stride: conflict-free ds_read_b128).
+namespace sglm {
+constexpr int k3Row = 144;                      // bytes per predictor row
+constexpr int k3Panel = 256 * k3Row;            // 36 KB
+constexpr int k3Stage = 2 * k3Panel + 256;      // A, B masks + w[64]
+
+__device__ __forceinline__ void expand_store(uint32_t word, char* dst) {
+    uint32_t o[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_sbfe((int)word, 2 * k, 1);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_sbfe((int)word, 2 * k + 1, 1);
+        o[k] = (lo & 0x0000FFFFu) | (hi & 0xFFFF0000u);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<uint4*>(dst + 16 * q) = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+}
+
+__global__ void __launch_bounds__(512) syrk3_kernel(
+    const uint32_t* __restrict__ Xbits, int64_t ld, int32_t P, int64_t nsteps_total,
+    int32_t splits, const float* __restrict__ W, const int32_t* __restrict__ fits,
+    int32_t ntiles, float* __restrict__ H, float* __restrict__ slab, int32_t nact,
+    const int32_t* __restrict__ grp, const int64_t* __restrict__ grp_off,
+    const int32_t* __restrict__ grp_cnt) {
+    extern __shared__ __attribute__((aligned(16))) char sm3[];
+    const int nt = P / 256;
+    const int tile = blockIdx.x % ntiles;
+    const int slot = blockIdx.x / ntiles;
+    const int split = blockIdx.y;
+    int ti, tj;
+    tile_coords(tile, nt, ti, tj);
+    const bool diag = ti == tj;
+    const int fit = fits[slot];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wave >> 2, wc = wave & 3;
+    const int r = lane & 31, h = lane >> 5;
+    // aligned 64-row blocks: step t of this fit covers block gl[8t] / 8 (identity if no list)
+    const int32_t* gl = grp ? grp + grp_off[fit] : nullptr;
+    const int64_t nblk = grp ? (int64_t)grp_cnt[fit] / 8 : nsteps_total;
+    const int64_t sps = (nblk + splits - 1) / splits;
+    const int64_t step0 = (int64_t)split * sps;
+    const int nsteps = (int)(min(step0 + sps, nblk) - step0 > 0 ? min(step0 + sps, nblk) - step0 : 0);
+    const int64_t wpc = ld / 32;                       // bit words per predictor
+    const int col = tid >> 1, half = tid & 1;          // staging: one word per panel
+    const uint32_t* BA = Xbits + (int64_t)(ti * 256 + col) * wpc + half;
+    const uint32_t* BB = Xbits + (int64_t)(tj * 256 + col) * wpc + half;
+    const float* w = W + (int64_t)fit * ld;
+    auto blk_of = [&](int t) -> int64_t {
+        return gl ? (int64_t)gl[(step0 + t) * 8] / 8 : step0 + t;
+    };
+
+    uint32_t ra = 0, rb = 0;
+    f32x4 rw = {};
+    auto gload = [&](int64_t blk) {
+        ra = BA[blk * 2];
+        if (!diag) rb = BB[blk * 2];
+        if (tid < 16) rw = *reinterpret_cast<const f32x4*>(w + blk * 64 + 4 * tid);
+    };
+    auto swrite = [&](int buf) {
+        char* base = sm3 + buf * k3Stage;
+        expand_store(ra, base + col * k3Row + half * 64);
+        if (!diag) expand_store(rb, base + k3Panel + col * k3Row + half * 64);
+        if (tid < 16) *reinterpret_cast<f32x4*>(base + 2 * k3Panel + 16 * tid) = rw;
+    };
+
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) acc[m][n] = (f32x16){};
+
+    if (nsteps > 0) {
+        int64_t bnext = blk_of(0);
+        gload(bnext);
+        swrite(0);
+        if (nsteps > 1) bnext = blk_of(1);
+        __syncthreads();
+        for (int s = 0; s < nsteps; ++s) {
+            const int cur = s & 1;
+            if (s + 1 < nsteps) {
+                gload(bnext);                              // in flight during the MFMAs
+                if (s + 2 < nsteps) bnext = blk_of(s + 2);
+            }
+            const char* A = sm3 + cur * k3Stage;
+            const char* Bp = diag ? A : A + k3Panel;
+            const float* wv = reinterpret_cast<const float*>(A + 2 * k3Panel);
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) {
+                const int boff = 32 * ks + 16 * h;         // byte offset of rows 16ks+8h..+7
+                const f32x4 w0 = *reinterpret_cast<const f32x4*>(wv + 16 * ks + 8 * h);
+                const f32x4 w1 = *reinterpret_cast<const f32x4*>(wv + 16 * ks + 8 * h + 4);
+                uint32_t wp[4];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    wp[j] = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)w0[2 * j]) |
+                            ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)w0[2 * j + 1]) << 16);
+                    wp[2 + j] = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)w1[2 * j]) |
+                                ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)w1[2 * j + 1]) << 16);
+                }
+                bf16x8 af[4], bfr[2];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    uint4 mk = *reinterpret_cast<const uint4*>(A + (wr * 128 + m * 32 + r) * k3Row + boff);
+                    mk.x &= 0x3F803F80u; mk.y &= 0x3F803F80u; mk.z &= 0x3F803F80u; mk.w &= 0x3F803F80u;
+                    af[m] = __builtin_bit_cast(bf16x8, mk);
+                }
+#pragma unroll
+                for (int n = 0; n < 2; ++n) {
+                    uint4 mk = *reinterpret_cast<const uint4*>(Bp + (wc * 64 + n * 32 + r) * k3Row + boff);
+                    mk.x &= wp[0]; mk.y &= wp[1]; mk.z &= wp[2]; mk.w &= wp[3];
+                    bfr[n] = __builtin_bit_cast(bf16x8, mk);
+                }
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+#pragma unroll
+                    for (int n = 0; n < 2; ++n)
+                        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[m], bfr[n],
+                                                                            acc[m][n], 0, 0, 0);
+            }
+            if (s + 1 < nsteps) swrite(cur ^ 1);
+            __syncthreads();
+        }
+    }
+    float* out = slab ? slab + ((int64_t)split * nact + slot) * (int64_t)P * P
+                      : H + (int64_t)fit * P * P;
+    const int64_t rbase = (int64_t)ti * 256 + wr * 128;
+    const int64_t cbase = (int64_t)tj * 256 + wc * 64;
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                out[(rbase + m * 32 + (j & 3) + 8 * (j >> 2) + 4 * h) * P + cbase + n * 32 + r] =
+                    acc[m][n][j];
+}
+
+// Bit-plane packing of a feature-major bf16 design: bit b of word q of predictor a is
+// (X[a][32q + b] != 0).  One wave per 64 rows: __ballot gives two words at once.  Sets
+// *nonbinary if any value is not exactly 0 or 1.
+__global__ void __launch_bounds__(256) pack_bits_kernel(const uint16_t* __restrict__ Xb,
+                                                        int64_t ld, int32_t P,
+                                                        uint32_t* __restrict__ bits,
+                                                        int32_t* nonbinary) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wid = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;   // global wave id
+    const int64_t per_col = ld / 64;
+    const int64_t total = per_col * P;
+    for (int64_t g = wid; g < total; g += ((int64_t)gridDim.x * 256) >> 6) {
+        const int64_t a = g / per_col, blk = g % per_col;
+        const uint16_t v = Xb[a * ld + blk * 64 + lane];
+        const bool one = v == 0x3F80u;
+        const bool bad = !(one || v == 0 || v == 0x8000u);
+        const unsigned long long m = __ballot(one);
+        if (__any(bad) && lane == 0) atomicOr(nonbinary, 1);
+        if (lane == 0) {
+            bits[a * (ld / 32) + blk * 2] = (uint32_t)m;
+            bits[a * (ld / 32) + blk * 2 + 1] = (uint32_t)(m >> 32);
+        }
+    }
+}
+}  // namespace sglm
+
+extern "C" int sglm_pack_bits(const uint16_t* Xb, int64_t ld, int32_t P, uint32_t* bits,
+                              int32_t* nonbinary, sglm_stream_t stream) {
+    if (!Xb || !bits || !nonbinary || ld % 64) {
+        set_error("sglm_pack_bits: bad args");
+        return SGLM_EINVAL;
+    }
+    pack_bits_kernel<<<2048, 256, 0, as_stream(stream)>>>(Xb, ld, P, bits, nonbinary);
+    return check_launch("pack_bits_kernel");
+}
+
+extern "C" int sglm_syrk_bits(const uint32_t* Xbits, int64_t ld, int32_t P, int64_t n,
+                              const float* W, const int32_t* fits, int32_t nact, int32_t splits,
+                              float* H, void* work, const int32_t* row_groups,
+                              const int64_t* group_offset, const int32_t* group_count,
+                              sglm_stream_t stream) {
+    if (nact <= 0) return SGLM_OK;
+    if (!Xbits || !W || !fits || !H || P % 256 || ld % 256 || n > ld || splits < 1 ||
+        (splits > 1 && !work)) {
+        set_error("sglm_syrk_bits: bad args");
+        return SGLM_EINVAL;
+    }
+    const int nt = P / 256;
+    const int ntiles = nt * (nt + 1) / 2;
+    const int64_t nst = (n + 63) / 64;
+    const size_t lds = (size_t)2 * k3Stage;
+    hipStream_t s = as_stream(stream);
+    static bool attr3 = false;
+    if (!attr3) {
+        (void)hipFuncSetAttribute((const void*)syrk3_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr3 = true;
+    }
+    float* slab = splits > 1 ? (float*)work : nullptr;
+    syrk3_kernel<<<dim3((unsigned)(ntiles * nact), (unsigned)splits), 512, lds, s>>>(
+        Xbits, ld, P, nst, splits, W, fits, ntiles, H, slab, nact, row_groups, group_offset,
+        group_count);
+    int st = check_launch("syrk3_kernel");
+    if (st || splits == 1) return st;
+    const int64_t PP = (int64_t)P * P;
+    unsigned gx = (unsigned)((PP + 255) / 256 < 4096 ? (PP + 255) / 256 : 4096);
+    syrk_reduce<<<dim3(gx, (unsigned)nact), 256, 0, s>>>(slab, P, nact, splits, fits, H);
+    return check_launch("syrk_reduce");
+}

@@ -31,6 +31,9 @@ SIGNATURES = {
     "sglm_syrk": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
     "sglm_syrk_masked": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp,
                                    _vp, _vp]),
+    "sglm_pack_bits": (C.c_int, [_vp, _i64, _i32, _vp, _vp, _vp]),
+    "sglm_syrk_bits": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp,
+                                 _vp, _vp]),
     "sglm_syrk_v1": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
     "sglm_syrk_variant": (C.c_int, [_i32, _vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _vp,
                                     _vp]),

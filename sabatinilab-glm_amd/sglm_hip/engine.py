@@ -43,6 +43,7 @@ X_BF16, X_F32 = 0, 1
 COL_PAD = 256
 ROW_PAD = 256
 ARMIJO_SIGMA = 2.0 ** -11      # sklearn _newton_solver.py:214
+SYRK_BITS = True               # use the bit-plane Gram (v3) for 0/1 designs
 
 
 def require_gpu():
@@ -81,6 +82,7 @@ class Design:
         alloc = torch.zeros if zero else torch.empty
         self.xb = alloc((self.P, self.ld), dtype=torch.bfloat16, device=device)
         self.xf = None
+        self.xbits = None      # uint32 bit-planes [P, ld/32] when the design is 0/1
         self.device = device
 
     @property
@@ -128,6 +130,15 @@ class Design:
             flag.zero_()
             _lib.call("sglm_pack_design", _p(src), int(is_f64), self.n, self.p, rs, cs, 1,
                       _p(self.xb), _p(self.xf), self.ld, self.P, _p(flag), _stream())
+        else:
+            self._pack_bits()
+
+    def _pack_bits(self):
+        """Bit-plane copy for 0/1 designs (Gram v3); dropped again if X is not binary."""
+        bits = torch.empty((self.P, self.ld // 32), dtype=torch.int32, device=self.device)
+        flag = torch.zeros(1, dtype=torch.int32, device=self.device)
+        _lib.call("sglm_pack_bits", _p(self.xb), self.ld, self.P, _p(bits), _p(flag), _stream())
+        self.xbits = None if int(flag.item()) else bits
 
     @classmethod
     def from_events(cls, E, shifts: Sequence[int], row0: int, n: int, device="cuda",
@@ -162,6 +173,8 @@ class Design:
         _lib.call("sglm_timeshift_expand", _p(Eb), N_raw, 1, N_raw, _p(cols_d), _p(sh_d), p,
                   _p(d.xb), n, 1, d.ld, row0, 2, 0, _stream())
         d.xb[p, :n] = 1.0
+        if exact:
+            d._pack_bits()
         if not exact:
             Ef = E.t().contiguous()
             d.xf = torch.zeros((d.P, d.ld), dtype=torch.float32, device=device)
@@ -503,6 +516,12 @@ def _syrk(d: Design, bf, fits: np.ndarray, nsteps: int, ntile1: int, stats, st, 
     if use_f32:
         _lib.call("sglm_syrk_f32", _p(d.xf), d.ld, d.P, d.n, _p(bf.W), _p(fits_d), nact, splits,
                   _p(bf.H), _p(work), st)
+    elif d.xbits is not None and SYRK_BITS:
+        groups = getattr(bf, "groups", None)
+        _lib.call("sglm_syrk_bits", _p(d.xbits), d.ld, d.P, d.n, _p(bf.W), _p(fits_d), nact,
+                  splits, _p(bf.H), _p(work), _p(groups),
+                  _p(bf.goff) if groups is not None else None,
+                  _p(bf.gcnt) if groups is not None else None, st)
     elif getattr(bf, "groups", None) is not None:
         _lib.call("sglm_syrk_masked", _p(d.xb), d.ld, d.P, d.n, _p(bf.W), _p(fits_d), nact,
                   splits, _p(bf.H), _p(work), _p(bf.groups), _p(bf.goff), _p(bf.gcnt), st)

@@ -53,12 +53,19 @@ def main():
         for v in H:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            _lib.call("sglm_syrk_variant", v, d.xb.data_ptr(), d.ld, d.P, d.n, W.data_ptr(),
-                      fits.data_ptr(), B, a.splits, H[v].data_ptr(), work.data_ptr(), st)
+            if v == 3:
+                _lib.call("sglm_syrk_bits", d.xbits.data_ptr(), d.ld, d.P, d.n, W.data_ptr(),
+                          fits.data_ptr(), B, a.splits, H[v].data_ptr(), work.data_ptr(),
+                          None, None, None, st)
+            else:
+                _lib.call("sglm_syrk_variant", v, d.xb.data_ptr(), d.ld, d.P, d.n, W.data_ptr(),
+                          fits.data_ptr(), B, a.splits, H[v].data_ptr(), work.data_ptr(), st)
             e1.record()
             torch.cuda.synchronize()
             if rep:
                 times[v].append(e0.elapsed_time(e1) / 1e3)
+    if d.xbits is not None and 3 in H:
+        pass
     for v in H:
         t = float(np.median(times[v]))
         res[f"syrk_v{v}"] = {"ms": t * 1e3, "exec_TFLOPs": exec_flop / t / 1e12,
@@ -73,13 +80,19 @@ def main():
         goff = torch.zeros(B, dtype=torch.int64, device="cuda")
         gcnt = torch.full((B,), int(prob.group_count[0]), dtype=torch.int32, device="cuda")
         Hm = torch.zeros_like(H[list(H)[0]])
+        use_bits = d.xbits is not None and 3 in H
         tm = []
         for rep in range(a.reps + 1):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            _lib.call("sglm_syrk_masked", d.xb.data_ptr(), d.ld, d.P, d.n, Wm.data_ptr(),
-                      fits.data_ptr(), B, a.splits, Hm.data_ptr(), work.data_ptr(),
-                      prob.groups.data_ptr(), goff.data_ptr(), gcnt.data_ptr(), st)
+            if use_bits:
+                _lib.call("sglm_syrk_bits", d.xbits.data_ptr(), d.ld, d.P, d.n, Wm.data_ptr(),
+                          fits.data_ptr(), B, a.splits, Hm.data_ptr(), work.data_ptr(),
+                          prob.groups.data_ptr(), goff.data_ptr(), gcnt.data_ptr(), st)
+            else:
+                _lib.call("sglm_syrk_masked", d.xb.data_ptr(), d.ld, d.P, d.n, Wm.data_ptr(),
+                          fits.data_ptr(), B, a.splits, Hm.data_ptr(), work.data_ptr(),
+                          prob.groups.data_ptr(), goff.data_ptr(), gcnt.data_ptr(), st)
             e1.record()
             torch.cuda.synchronize()
             if rep:
