@@ -165,7 +165,7 @@ def main():
             },
             "roofline": {
                 "bound": "mfma",
-                "kernel": "syrk_kernel (X^T diag(w) X, v_mfma_f32_32x32x16_bf16)",
+                "kernel": "syrk6_kernel (X^T diag(w) X over row-compacted bit-planes, v_mfma_f32_32x32x16_bf16)",
                 "achieved": achieved,
                 "peak": PEAK_BF16_TFLOPS,
                 "unit": "TFLOP/s",

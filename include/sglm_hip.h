@@ -131,6 +131,28 @@ int sglm_syrk_bits(const uint32_t* Xbits, int64_t ld, int32_t P, int64_t n, cons
                    const int32_t* row_groups, const int64_t* group_offset,
                    const int32_t* group_count, sglm_stream_t stream);
 
+/* Row-compacted bit-plane design (Gram v6).  Output row k is X[.][rows[k]] (rows == NULL:
+ * row k) for k < nrows, zero up to the next multiple of 64.  Layout K-step-major:
+ * out[(blk * P + a) * 2 + {0,1}] = the two 32-row words of 64-row block blk of predictor a;
+ * inside a word, row rho is bit 4*(rho/8) + (rho%8)/2 + 16*(rho%2) (MFMA fragment order).
+ * Size: ceil(nrows/64) * P * 8 bytes.  *nonbinary as for sglm_pack_bits.
+ * Replaces the X[idx_train, :] copies of backend/sglm_cv.py:107-110 for 0/1 designs. */
+int sglm_pack_bits_rows(const uint16_t* Xb, int64_t ld, int32_t P, const int32_t* rows,
+                        int64_t nrows, uint32_t* out, int32_t* nonbinary, sglm_stream_t stream);
+
+/* Per-slot descriptor for Gram v6, 4 x int64 per slot: [0] device address of the slot's
+ * compacted bit-plane design, [1] its row count, [2] device address of the slot's compact
+ * bf16 weights (>= ceil(rows/64)*64 entries), [3] device address of its int32 row list
+ * (0 = identity).  sglm_gather_w fills [2]: bf16(W[fits[s]][row(k)]), zero padded. */
+int sglm_gather_w(const float* W, int64_t ld, const int32_t* fits, int32_t nact,
+                  const int64_t* desc, int64_t max_rows, sglm_stream_t stream);
+
+/* Gram v6: H[fits[s]] = X_s^T diag(w_s) X_s over each slot's compacted rows, bf16 MFMA from
+ * bit-planes expanded in registers; writes the 128-blocks with block row <= block col.
+ * work: sglm_syrk_work_bytes(P, nact, splits) when splits > 1. */
+int sglm_syrk_cbits(const int64_t* desc, int32_t P, const int32_t* fits, int32_t nact,
+                    int32_t splits, float* H, void* work, sglm_stream_t stream);
+
 /* Development entries: a specific bf16 Gram variant (1 = register-staged, 2 = LDS-DMA
  * staged; sglm_syrk uses the default), same arguments as sglm_syrk. */
 int sglm_syrk_v1(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, const float* W,

@@ -802,3 +802,317 @@ extern "C" int sglm_syrk_bits(const uint32_t* Xbits, int64_t ld, int32_t P, int6
     syrk_reduce<<<dim3(gx, (unsigned)nact), 256, 0, s>>>(slab, P, nact, splits, fits, H);
     return check_launch("syrk_reduce");
 }
+
+// ---------------------------------------------------------------------------------------
+// v6: row-compacted bit-plane designs, register-only (no LDS, no barriers).
+//   * Every distinct row mask gets its own bit-plane copy holding only its rows
+//     (sglm_pack_bits_rows), so the K loop runs over exactly the fit's rows.  The weights are
+//     gathered to the same compact order and rounded to bf16 once (sglm_gather_w).
+//   * Layout K-step-major: bits[step][predictor] = uint2 (64 rows), so the 128 predictors of
+//     a 128-column block are 1 KB contiguous per K-step.  Inside a 32-row word, row rho sits
+//     at bit 4*(rho/8) + (rho%8)/2 + 16*(rho%2): the dword of MFMA fragment rows (2j, 2j+1)
+//     of 8-row chunk g has its two bits 16 apart at p = 4g + j and p + 16.
+//   * A operand (unscaled): rotr(word, p - 14) & 0x40004000 = two bf16 values 2.0 / 0
+//     (2 VALU per dword; the factor 2 is removed exactly when storing).  B operand (weighted):
+//     pk_ashr_i16(rotr(word, p - 15), 15) -> 16-bit masks, AND bf16 weight pair (3 VALU).
+//   * One wave per workgroup computes a 128 x 128 block (4 x 4 tiles of
+//     v_mfma_f32_32x32x16_bf16, 256 AGPRs) of the upper triangle (block row <= block col);
+//     each lane loads the 8-byte words of its columns straight into registers, two K-steps
+//     ahead.  ~80 VALU per 16 MFMA, nothing else in the loop.
+//   * per-slot descriptor (4 x int64): bit-plane base, rows, bf16 compact weights, row list
+//     (0 = identity; used by the weight gather only).
+namespace sglm {
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x2 g_uint2;
+typedef __attribute__((address_space(1))) const u32x4 g_uint4;
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t rotr32(uint32_t x, uint32_t s) {
+    return __builtin_amdgcn_alignbit(x, x, s);
+}
+
+struct Step6 {
+    u32x2 a[4], b[4];
+    u32x4 w[4];
+};
+
+// Loads are inline asm so LLVM cannot sink them to their use (it does for plain loads, which
+// removes the prefetch); wait6 is the matching s_waitcnt, with every loaded register tied so
+// no consumer can be scheduled above it.
+__device__ __forceinline__ u32x2 gld2(g_uint2* p) {
+    u32x2 v;
+    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ u32x4 gld4(g_uint4* p) {
+    u32x4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+
+__device__ __forceinline__ void load6(Step6& t, g_uint2* pa, g_uint2* pb, g_uint4* pw,
+                                      int64_t s, int32_t P) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) t.a[m] = gld2(pa + s * P + 32 * m);
+#pragma unroll
+    for (int n = 0; n < 4; ++n) t.b[n] = gld2(pb + s * P + 32 * n);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) t.w[ks] = gld4(pw + s * 8 + 2 * ks);
+}
+
+__device__ __forceinline__ void wait6(Step6& t) {
+    asm volatile("s_waitcnt vmcnt(0)"
+                 : "+v"(t.a[0]), "+v"(t.a[1]), "+v"(t.a[2]), "+v"(t.a[3]), "+v"(t.b[0]),
+                   "+v"(t.b[1]), "+v"(t.b[2]), "+v"(t.b[3]), "+v"(t.w[0]), "+v"(t.w[1]),
+                   "+v"(t.w[2]), "+v"(t.w[3])
+                 :
+                 : "memory");
+}
+
+struct Frag6 {
+    bf16x8 a[4], b[4];
+};
+
+// fragments of sub-step ks (16 rows) of a K-step: A = 2.0/0 values, B = bf16 weights/0
+__device__ __forceinline__ void frags6(const Step6& t, int ks, int h, Frag6& f) {
+    const uint32_t p0 = 8 * (ks & 1) + 4 * h;            // bit of row pair j = 0
+    const uint32_t wp[4] = {t.w[ks].x, t.w[ks].y, t.w[ks].z, t.w[ks].w};
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const uint32_t word = ks < 2 ? t.a[m].x : t.a[m].y;
+        uint32_t d[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[j] = rotr32(word, (p0 + j + 18) & 31) & 0x40004000u;
+        f.a[m] = __builtin_bit_cast(bf16x8, make_uint4(d[0], d[1], d[2], d[3]));
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+        const uint32_t word = ks < 2 ? t.b[n].x : t.b[n].y;
+        uint32_t d[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const s16x2 v = __builtin_bit_cast(s16x2, rotr32(word, (p0 + j + 17) & 31));
+            d[j] = __builtin_bit_cast(uint32_t, (s16x2)(v >> (s16x2){15, 15})) & wp[j];
+        }
+        f.b[n] = __builtin_bit_cast(bf16x8, make_uint4(d[0], d[1], d[2], d[3]));
+    }
+}
+
+__device__ __forceinline__ void mfma16(const Frag6& f, f32x16 (&acc)[4][4]) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[m], f.b[n], acc[m][n], 0, 0, 0);
+}
+
+// one scheduling region: 16 MFMAs of the current fragments, each followed by 5 of the 80
+// VALU that build the next sub-step's fragments
+__device__ __forceinline__ void interleave16() {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);     // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);     // VALU
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// K-step held in `cur` (its sub-step 0 fragments already in F); loads step `snext` into
+// `nxt` first and leaves F = sub-step 0 fragments of `nxt`.
+__device__ __forceinline__ void half6(const Step6& cur, Step6& nxt, Frag6& F, int h,
+                                      f32x16 (&acc)[4][4], g_uint2* pa, g_uint2* pb,
+                                      g_uint4* pw, int64_t snext, int32_t P) {
+    load6(nxt, pa, pb, pw, snext, P);
+    __builtin_amdgcn_sched_barrier(0);
+    Frag6 G;
+    frags6(cur, 1, h, G);
+    mfma16(F, acc);
+    interleave16();
+    frags6(cur, 2, h, F);
+    mfma16(G, acc);
+    interleave16();
+    frags6(cur, 3, h, G);
+    mfma16(F, acc);
+    interleave16();
+    wait6(nxt);
+    frags6(nxt, 0, h, F);
+    mfma16(G, acc);
+    interleave16();
+}
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) syrk6_kernel(const int64_t* __restrict__ desc, int32_t P,
+                                                   int32_t splits,
+                                                   const int32_t* __restrict__ fits,
+                                                   int32_t nunits, float* __restrict__ H,
+                                                   float* __restrict__ slab, int32_t nact) {
+    const int unit = blockIdx.x % nunits;
+    const int slot = blockIdx.x / nunits;
+    const int split = blockIdx.y;
+    int bi, bj;
+    tile_coords(unit, P / 128, bi, bj);
+    const int fit = fits[slot];
+    const int64_t* dsc = desc + 4 * slot;
+    g_uint2* bits = reinterpret_cast<g_uint2*>(dsc[0]);
+    const int64_t nrows = dsc[1];
+    const int64_t wbf = dsc[2];                                 // bf16 weights (address)
+    const int64_t nblk = (nrows + 63) / 64;
+    const int64_t sps = (nblk + splits - 1) / splits;
+    const int64_t blk0 = (int64_t)split * sps;
+    const int64_t blk1 = min(blk0 + sps, nblk);
+    const int nsteps = blk1 > blk0 ? (int)(blk1 - blk0) : 0;
+    const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
+    g_uint2* pa = bits + blk0 * P + bi * 128 + r;
+    g_uint2* pb = bits + blk0 * P + bj * 128 + r;
+    g_uint4* pw = reinterpret_cast<g_uint4*>(wbf + 2 * (blk0 * 64 + 8 * h));
+
+    f32x16 acc[4][4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = (f32x16){};
+
+    if (nsteps > 0) {
+        Step6 A, B;                                  // two register sets, one step in flight
+        Frag6 F;
+        load6(A, pa, pb, pw, 0, P);
+        wait6(A);
+        frags6(A, 0, h, F);
+        int s = 0;
+        for (; s + 1 < nsteps; s += 2) {
+            half6(A, B, F, h, acc, pa, pb, pw, s + 1, P);
+            half6(B, A, F, h, acc, pa, pb, pw, s + 2 < nsteps ? s + 2 : nsteps - 1, P);
+        }
+        if (s < nsteps) {                            // odd step count: last step from A
+            Frag6 G;
+            frags6(A, 1, h, G);
+            mfma16(F, acc);
+            frags6(A, 2, h, F);
+            mfma16(G, acc);
+            frags6(A, 3, h, G);
+            mfma16(F, acc);
+            mfma16(G, acc);
+        }
+    }
+    float* out = slab ? slab + ((int64_t)split * nact + slot) * (int64_t)P * P
+                      : H + (int64_t)fit * P * P;
+    const int64_t rbase = (int64_t)bi * 128;
+    const int64_t cbase = (int64_t)bj * 128;
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                out[(rbase + m * 32 + (j & 3) + 8 * (j >> 2) + 4 * h) * P + cbase + n * 32 + r] =
+                    0.5f * acc[m][n][j];
+}
+
+// split-K reduction over the 128-blocks v6 writes (block row <= block col)
+__global__ void __launch_bounds__(256) syrk6_reduce(const float* __restrict__ slab, int32_t P,
+                                                    int32_t nact, int32_t splits,
+                                                    const int32_t* __restrict__ fits,
+                                                    float* __restrict__ H) {
+    const int slot = blockIdx.y;
+    const int64_t PP = (int64_t)P * P;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < PP;
+         e += (int64_t)gridDim.x * 256) {
+        const int64_t a = e / P, b = e % P;
+        if (a / 128 > b / 128) continue;
+        float s = 0.0f;
+        for (int z = 0; z < splits; ++z) s += slab[((int64_t)z * nact + slot) * PP + e];
+        H[(int64_t)fits[slot] * PP + e] = s;
+    }
+}
+
+// Compact bit-plane packing (layout above): output row k = X[.][rows[k]] (rows == nullptr:
+// row k) for k < nrows, zero to the next multiple of 64.  One wave per (64-row block,
+// predictor), consecutive waves -> consecutive predictors (contiguous 8-B stores); each
+// lane's bit is shuffled to its target lane, then one __ballot gives both words.
+__global__ void __launch_bounds__(256) pack_bits_rows_kernel(
+    const uint16_t* __restrict__ Xb, int64_t ld, int32_t P, const int32_t* __restrict__ rows,
+    int64_t nrows, uint2* __restrict__ out, int32_t* nonbinary) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wid = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+    const int64_t nblk = (nrows + 63) / 64;
+    const int64_t total = nblk * P;
+    const int t = lane & 31, tt = t & 15;
+    const int src = (lane & 32) | (8 * (tt >> 2) + 2 * (tt & 3) + (t >> 4));
+    for (int64_t g = wid; g < total; g += ((int64_t)gridDim.x * 256) >> 6) {
+        const int64_t blk = g / P, a = g % P;
+        const int64_t k = blk * 64 + lane;
+        uint16_t v = 0;
+        if (k < nrows) v = Xb[a * ld + (rows ? (int64_t)rows[k] : k)];
+        const bool one = v == 0x3F80u;
+        const bool bad = !(one || v == 0 || v == 0x8000u);
+        const int mine = __shfl((int)one, src, 64);
+        const unsigned long long m = __ballot(mine);
+        if (__any(bad) && lane == 0) atomicOr(nonbinary, 1);
+        if (lane == 0) out[g] = make_uint2((uint32_t)m, (uint32_t)(m >> 32));
+    }
+}
+
+// compact bf16 weights: wbf(slot)[k] = bf16(W[fits[slot]][row(k)]) for k < rows, 0 to pad 64
+__global__ void __launch_bounds__(256) gather_w_kernel(const float* __restrict__ W, int64_t ld,
+                                                       const int32_t* __restrict__ fits,
+                                                       const int64_t* __restrict__ desc) {
+    const int slot = blockIdx.y;
+    const int64_t* dsc = desc + 4 * slot;
+    const int64_t nrows = dsc[1];
+    __bf16* wc = reinterpret_cast<__bf16*>(dsc[2]);
+    const int32_t* rows = reinterpret_cast<const int32_t*>(dsc[3]);
+    const float* w = W + (int64_t)fits[slot] * ld;
+    const int64_t npad = (nrows + 63) / 64 * 64;
+    for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < npad;
+         k += (int64_t)gridDim.x * 256)
+        wc[k] = (__bf16)(k < nrows ? w[rows ? (int64_t)rows[k] : k] : 0.0f);
+}
+}  // namespace sglm
+
+extern "C" int sglm_pack_bits_rows(const uint16_t* Xb, int64_t ld, int32_t P, const int32_t* rows,
+                                   int64_t nrows, uint32_t* out, int32_t* nonbinary,
+                                   sglm_stream_t stream) {
+    if (!Xb || !out || !nonbinary || nrows < 0 || (!rows && nrows > ld)) {
+        set_error("sglm_pack_bits_rows: bad args");
+        return SGLM_EINVAL;
+    }
+    if (nrows == 0) return SGLM_OK;
+    pack_bits_rows_kernel<<<4096, 256, 0, as_stream(stream)>>>(
+        Xb, ld, P, rows, nrows, reinterpret_cast<uint2*>(out), nonbinary);
+    return check_launch("pack_bits_rows_kernel");
+}
+
+extern "C" int sglm_gather_w(const float* W, int64_t ld, const int32_t* fits, int32_t nact,
+                             const int64_t* desc, int64_t max_rows, sglm_stream_t stream) {
+    if (nact <= 0) return SGLM_OK;
+    if (!W || !fits || !desc || max_rows < 0) {
+        set_error("sglm_gather_w: bad args");
+        return SGLM_EINVAL;
+    }
+    const int64_t npad = (max_rows + 63) / 64 * 64;
+    unsigned gx = (unsigned)((npad + 2047) / 2048);
+    if (gx < 1) gx = 1;
+    gather_w_kernel<<<dim3(gx, (unsigned)nact), 256, 0, as_stream(stream)>>>(W, ld, fits, desc);
+    return check_launch("gather_w_kernel");
+}
+
+extern "C" int sglm_syrk_cbits(const int64_t* desc, int32_t P, const int32_t* fits, int32_t nact,
+                               int32_t splits, float* H, void* work, sglm_stream_t stream) {
+    if (nact <= 0) return SGLM_OK;
+    if (!desc || !fits || !H || P % 256 || splits < 1 || (splits > 1 && !work)) {
+        set_error("sglm_syrk_cbits: bad args");
+        return SGLM_EINVAL;
+    }
+    const int nb = P / 128;
+    const int nunits = nb * (nb + 1) / 2;
+    hipStream_t s = as_stream(stream);
+    float* slab = splits > 1 ? (float*)work : nullptr;
+    syrk6_kernel<<<dim3((unsigned)(nunits * nact), (unsigned)splits), 64, 0, s>>>(
+        desc, P, splits, fits, nunits, H, slab, nact);
+    int st = check_launch("syrk6_kernel");
+    if (st || splits == 1) return st;
+    const int64_t PP = (int64_t)P * P;
+    unsigned gx = (unsigned)((PP + 255) / 256 < 4096 ? (PP + 255) / 256 : 4096);
+    syrk6_reduce<<<dim3(gx, (unsigned)nact), 256, 0, s>>>(slab, P, nact, splits, fits, H);
+    return check_launch("syrk6_reduce");
+}

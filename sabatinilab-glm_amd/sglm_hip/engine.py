@@ -44,6 +44,8 @@ COL_PAD = 256
 ROW_PAD = 256
 ARMIJO_SIGMA = 2.0 ** -11      # sklearn _newton_solver.py:214
 SYRK_BITS = True               # use the bit-plane Gram (v3) for 0/1 designs
+SYRK_CBITS = True              # ... and its row-compacted register-only form (v6) when fits
+                               # carry masks (the default path for event designs)
 
 
 def require_gpu():
@@ -235,6 +237,25 @@ class Problem:
         self.group_offset = np.array(goff, dtype=np.int64)
         self.group_count = np.array(gcnt, dtype=np.int32)
         self.groups = torch.from_numpy(np.concatenate(lists) if off else np.zeros(1, np.int32)).to(dev)
+        self._compact = {}
+
+    def compact(self, mask: int):
+        """Row-compacted bit-plane design of one mask (Gram v6), built once and cached:
+        (bits, rows in the mask, device row list or None when the mask is every row)."""
+        c = self._compact.get(mask)
+        if c is None:
+            d = self.design
+            rows = np.flatnonzero(self.masks[mask] > 0).astype(np.int32)
+            nr = int(rows.size)
+            rows_d = None if nr == d.n else torch.from_numpy(rows).to(d.device)
+            bits = torch.empty(max(1, (nr + 63) // 64) * d.P * 2, dtype=torch.int32,
+                               device=d.device)
+            flag = torch.zeros(1, dtype=torch.int32, device=d.device)
+            _lib.call("sglm_pack_bits_rows", _p(d.xb), d.ld, d.P, _p(rows_d), nr, _p(bits),
+                      _p(flag), _stream())
+            c = (bits, nr, rows_d)
+            self._compact[mask] = c
+        return c
 
     def mask_stats(self, resp: int, mask: int):
         """float64 (count, sum y, mean y) over a mask — host side, cached."""
@@ -395,6 +416,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
     bf.goff = torch.from_numpy(prob.group_offset[mk]).to(dev)
     bf.gcnt = torch.from_numpy(prob.group_count[mk]).to(dev)
     bf.groups = prob.groups
+    bf.prob, bf.fit_mask = prob, mk
 
     for it in range(int(max_iter.max()) + 1):
         act = np.flatnonzero(active)
@@ -481,6 +503,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                 active[k] = False
             prev_rel[k] = rel
 
+    bf.prob = bf.keep = None            # drop the compacted designs with the problem
     # final linear predictor from the final coefficients (no accumulated drift)
     d.eta(bf.beta, bf.eta)
     info = bf.info.cpu().numpy()
@@ -501,38 +524,79 @@ def _syrk(d: Design, bf, fits: np.ndarray, nsteps: int, ntile1: int, stats, st, 
     if nact == 0:
         return
     use_f32 = exact and d.xf is not None
-    if use_f32:
-        nt = d.P // 128
-        ntile1 = nt * (nt + 1) // 2
-        nsteps = (d.n + 15) // 16
-    splits = syrk_splits(ntile1 * nact, nsteps)
-    wb = _lib.query("sglm_syrk_work_bytes", d.P, nact, splits)
-    work = _work(wb, d.device) if wb else None
-    fits_d = torch.tensor(fits, dtype=torch.int32, device=d.device)
+    prob = getattr(bf, "prob", None)
+    use_cb = (not use_f32 and d.xbits is not None and SYRK_CBITS and prob is not None
+              and getattr(bf, "groups", None) is not None)
+    ev = None
     if stats is not None and stats.record:
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-    if use_f32:
-        _lib.call("sglm_syrk_f32", _p(d.xf), d.ld, d.P, d.n, _p(bf.W), _p(fits_d), nact, splits,
-                  _p(bf.H), _p(work), st)
-    elif d.xbits is not None and SYRK_BITS:
-        groups = getattr(bf, "groups", None)
-        _lib.call("sglm_syrk_bits", _p(d.xbits), d.ld, d.P, d.n, _p(bf.W), _p(fits_d), nact,
-                  splits, _p(bf.H), _p(work), _p(groups),
-                  _p(bf.goff) if groups is not None else None,
-                  _p(bf.gcnt) if groups is not None else None, st)
-    elif getattr(bf, "groups", None) is not None:
-        _lib.call("sglm_syrk_masked", _p(d.xb), d.ld, d.P, d.n, _p(bf.W), _p(fits_d), nact,
-                  splits, _p(bf.H), _p(work), _p(bf.groups), _p(bf.goff), _p(bf.gcnt), st)
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    if use_cb:
+        _syrk_cbits(d, bf, prob, fits, st, ev)
     else:
-        _lib.call("sglm_syrk", _p(d.xb), d.ld, d.P, d.n, _p(bf.W), _p(fits_d), nact, splits,
-                  _p(bf.H), _p(work), st)
-    if stats is not None and stats.record:
-        e1.record()
+        if ev is not None:
+            ev[0].record()
+        if use_f32:
+            nt = d.P // 128
+            ntile1 = nt * (nt + 1) // 2
+            nsteps = (d.n + 15) // 16
+        splits = syrk_splits(ntile1 * nact, nsteps)
+        wb = _lib.query("sglm_syrk_work_bytes", d.P, nact, splits)
+        work = _work(wb, d.device) if wb else None
+        fits_d = torch.tensor(fits, dtype=torch.int32, device=d.device)
+        if use_f32:
+            _lib.call("sglm_syrk_f32", _p(d.xf), d.ld, d.P, d.n, _p(bf.W), _p(fits_d), nact,
+                      splits, _p(bf.H), _p(work), st)
+        elif d.xbits is not None and SYRK_BITS:
+            groups = getattr(bf, "groups", None)
+            _lib.call("sglm_syrk_bits", _p(d.xbits), d.ld, d.P, d.n, _p(bf.W), _p(fits_d),
+                      nact, splits, _p(bf.H), _p(work), _p(groups),
+                      _p(bf.goff) if groups is not None else None,
+                      _p(bf.gcnt) if groups is not None else None, st)
+        elif getattr(bf, "groups", None) is not None:
+            _lib.call("sglm_syrk_masked", _p(d.xb), d.ld, d.P, d.n, _p(bf.W), _p(fits_d), nact,
+                      splits, _p(bf.H), _p(work), _p(bf.groups), _p(bf.goff), _p(bf.gcnt), st)
+        else:
+            _lib.call("sglm_syrk", _p(d.xb), d.ld, d.P, d.n, _p(bf.W), _p(fits_d), nact,
+                      splits, _p(bf.H), _p(work), st)
+        if ev is not None:
+            ev[1].record()
+    if ev is not None:
         pa = d.p + 1
         nrows = float(np.sum(rows[fits])) if rows is not None else float(d.n) * nact
-        stats.syrk_events.append((e0, e1, nact, nrows * pa * (pa + 1)))   # algorithmic flop
+        stats.syrk_events.append((ev[0], ev[1], nact, nrows * pa * (pa + 1)))  # algorithmic flop
+
+
+def _syrk_cbits(d: Design, bf, prob: Problem, fits: np.ndarray, st, ev=None):
+    """Gram v6 over per-mask compacted bit-planes.  Slots are ordered by mask so that the
+    workgroups resident at any time read the same compacted design (Infinity Cache)."""
+    masks = np.asarray(bf.fit_mask)[fits]
+    order = np.argsort(masks, kind="stable")
+    fits, masks = fits[order], masks[order]
+    nact = int(fits.size)
+    cbs = [prob.compact(int(m)) for m in masks]
+    maxrows = max(c[1] for c in cbs)
+    stride = max(64, pad_to(maxrows, 64))
+    need = nact * stride
+    wc = getattr(bf, "wc", None)
+    if wc is None or wc.numel() < need:
+        wc = bf.wc = torch.empty(need, dtype=torch.bfloat16, device=d.device)
+    desc = np.array([[c[0].data_ptr(), c[1], wc.data_ptr() + 2 * i * stride,
+                      0 if c[2] is None else c[2].data_ptr()] for i, c in enumerate(cbs)],
+                    dtype=np.int64)
+    desc_d = torch.from_numpy(desc).to(d.device)
+    fits_d = torch.from_numpy(fits.astype(np.int32)).to(d.device)
+    nb = d.P // 128
+    splits = syrk_splits(nb * (nb + 1) // 2 * nact, max(1, maxrows // 64), cus=1024)
+    wb = _lib.query("sglm_syrk_work_bytes", d.P, nact, splits)
+    work = _work(wb, d.device) if wb else None
+    _lib.call("sglm_gather_w", _p(bf.W), d.ld, _p(fits_d), nact, _p(desc_d), maxrows, st)
+    if ev is not None:                  # the roofline times the Gram kernel alone
+        ev[0].record()
+    _lib.call("sglm_syrk_cbits", _p(desc_d), d.P, _p(fits_d), nact, splits, _p(bf.H), _p(work),
+              st)
+    if ev is not None:
+        ev[1].record()
+    bf.keep = (desc_d, fits_d)          # alive until the next launch is enqueued
 
 
 def score_sums(prob: Problem, family: int, power: float, eta, fit_resp: Sequence[int],

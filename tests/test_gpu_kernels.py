@@ -321,3 +321,88 @@ def test_syrk_bits_bitwise_equal_to_bf16(engine, torch_mod):
                     assert err <= 1e-6 * torch.max(torch.abs(Href[k][up])).item(), (splits, k)
                 else:
                     assert torch.equal(Hb[k][up], Href[k][up]), (splits, k)
+
+
+def _unpack_cbits(bits, P, nrows):
+    """Host decode of the v6 compact layout -> (nrows, P) 0/1 matrix."""
+    nblk = max(1, (nrows + 63) // 64)
+    w = bits.reshape(nblk, P, 2).astype(np.uint32)
+    rho = np.arange(32)
+    pos = 4 * (rho // 8) + (rho % 8) // 2 + 16 * (rho % 2)
+    out = np.zeros((nblk, 64, P), np.uint8)
+    for half in range(2):
+        out[:, 32 * half + rho, :] = ((w[:, :, half][:, None, :] >> pos[None, :, None]) & 1)
+    return out.reshape(nblk * 64, P)[:nrows]
+
+
+def test_pack_bits_rows_layout(engine, torch_mod):
+    """Compacted bit-planes decode back to X[rows] (ragged row count, zero tail)."""
+    torch = torch_mod
+    from sglm_hip import _lib, synth
+    s = synth.make(N=5000, m=7, L=3, rho=0.2, seed=21)
+    d = engine.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
+    Xh = d.xb.float().cpu().numpy().T[: s.N]                 # (n, P)
+    rng = np.random.default_rng(22)
+    for rows in (np.sort(rng.choice(s.N, 1234, replace=False)).astype(np.int32), None):
+        nr = 1234 if rows is not None else s.N
+        rows_d = None if rows is None else torch.from_numpy(rows).cuda()
+        bits = torch.zeros(((nr + 63) // 64) * d.P * 2, dtype=torch.int32, device="cuda")
+        flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+        _lib.call("sglm_pack_bits_rows", d.xb.data_ptr(), d.ld, d.P,
+                  None if rows_d is None else rows_d.data_ptr(), nr, bits.data_ptr(),
+                  flag.data_ptr(), 0)
+        torch.cuda.synchronize()
+        assert int(flag.item()) == 0
+        got = _unpack_cbits(bits.cpu().numpy().view(np.uint32), d.P, nr)
+        ref = Xh if rows is None else Xh[rows]
+        assert np.array_equal(got, ref.astype(np.uint8))
+        tail = _unpack_cbits(bits.cpu().numpy().view(np.uint32), d.P, ((nr + 63) // 64) * 64)
+        assert not tail[nr:].any()
+
+
+def test_syrk_cbits_compacted_gram(engine, torch_mod):
+    """Gram v6 (row-compacted bit-planes, register MFMA): bitwise equal to v2 on the full
+    mask; within f32 summation-order noise of the float64 Gram on subsets (incl. empty)."""
+    torch = torch_mod
+    from sglm_hip import _lib, synth
+    s = synth.make(N=20000, m=13, L=6, rho=0.1, seed=31)
+    d = engine.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
+    rng = np.random.default_rng(32)
+    masks = [np.ones(s.N, np.uint8), np.repeat(rng.random(200) >= 0.3, 100).astype(np.uint8),
+             np.zeros(s.N, np.uint8), (rng.random(s.N) < 0.5).astype(np.uint8)]
+    prob = engine.Problem(d, [s.y], masks)
+    B = len(masks)
+    W = torch.zeros((B, d.ld), dtype=torch.float32, device="cuda")
+    for k in range(B):
+        W[k, : s.N] = torch.from_numpy(masks[k] * (0.1 + rng.random(s.N)).astype(np.float32))
+    fits = torch.arange(B, dtype=torch.int32, device="cuda")
+    cbs = [prob.compact(k) for k in range(B)]
+    nr_max = max(c[1] for c in cbs)
+    stride = max(64, (nr_max + 63) // 64 * 64)
+    wc = torch.zeros(B * stride, dtype=torch.bfloat16, device="cuda")
+    desc = torch.tensor([[c[0].data_ptr(), c[1], wc.data_ptr() + 2 * k * stride,
+                          0 if c[2] is None else c[2].data_ptr()] for k, c in enumerate(cbs)],
+                        dtype=torch.int64).cuda()
+    _lib.call("sglm_gather_w", W.data_ptr(), d.ld, fits.data_ptr(), B, desc.data_ptr(), nr_max, 0)
+    Xh = d.xb.double().cpu().numpy()[:, : s.N]
+    Wb = W.to(torch.bfloat16).double().cpu().numpy()[:, : s.N]
+    blk = (np.arange(d.P)[:, None] // 128) <= (np.arange(d.P)[None, :] // 128)
+    Href = torch.zeros((1, d.P, d.P), dtype=torch.float32, device="cuda")
+    wk1 = torch.empty(16, dtype=torch.uint8, device="cuda")
+    _lib.call("sglm_syrk_variant", 2, d.xb.data_ptr(), d.ld, d.P, d.n, W.data_ptr(),
+              fits.data_ptr(), 1, 1, Href.data_ptr(), wk1.data_ptr(), 0)
+    for splits in (1, 4):
+        wk = torch.empty(max(_lib.query("sglm_syrk_work_bytes", d.P, B, splits), 16),
+                         dtype=torch.uint8, device="cuda")
+        H = torch.full((B, d.P, d.P), float("nan"), dtype=torch.float32, device="cuda")
+        _lib.call("sglm_syrk_cbits", desc.data_ptr(), d.P, fits.data_ptr(), B, splits,
+                  H.data_ptr(), wk.data_ptr(), 0)
+        Hh = H.cpu().numpy()
+        if splits == 1:
+            assert np.array_equal(Hh[0][blk], Href[0].cpu().numpy()[blk])
+        for k in range(B):
+            ref = (Xh * Wb[k]) @ Xh.T
+            got = Hh[k][blk]
+            assert np.all(np.isfinite(got)), (splits, k)
+            scale = max(np.max(np.abs(ref)), 1.0)
+            assert np.max(np.abs(got - ref[blk])) <= 2e-6 * scale, (splits, k)

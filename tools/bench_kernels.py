@@ -49,11 +49,29 @@ def main():
     alg_flop = B * float(d.n) * pa * (pa + 1)
     res = {"shape": {"n": d.n, "p": d.p, "P": d.P, "fits": B, "splits": a.splits}}
     times = {v: [] for v in H}
+
+    def cbits_setup(mask, Wsrc):
+        prob = E.Problem(d, [np.zeros(d.n)], [mask])
+        cb = prob.compact(0)
+        stride = max(64, (cb[1] + 63) // 64 * 64)
+        wc = torch.zeros(B * stride, dtype=torch.bfloat16, device="cuda")
+        desc = torch.tensor([[cb[0].data_ptr(), cb[1], wc.data_ptr() + 2 * k * stride,
+                              0 if cb[2] is None else cb[2].data_ptr()] for k in range(B)],
+                            dtype=torch.int64).cuda()
+        _lib.call("sglm_gather_w", Wsrc.data_ptr(), d.ld, fits.data_ptr(), B, desc.data_ptr(),
+                  cb[1], st)
+        return prob, wc, desc
+
+    if 6 in H:
+        cb6 = cbits_setup(np.ones(d.n, np.uint8), W)
     for rep in range(a.reps + 1):
         for v in H:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            if v == 3:
+            if v == 6:
+                _lib.call("sglm_syrk_cbits", cb6[2].data_ptr(), d.P, fits.data_ptr(), B, a.splits,
+                          H[v].data_ptr(), work.data_ptr(), st)
+            elif v == 3:
                 _lib.call("sglm_syrk_bits", d.xbits.data_ptr(), d.ld, d.P, d.n, W.data_ptr(),
                           fits.data_ptr(), B, a.splits, H[v].data_ptr(), work.data_ptr(),
                           None, None, None, st)
@@ -102,6 +120,25 @@ def main():
         res["syrk_masked"] = {"ms": t * 1e3, "train_rows": rows,
                               "groups_frac": float(prob.group_count[0]) * 8 / d.n,
                               "alg_TFLOPs": B * rows * pa * (pa + 1) / t / 1e12}
+        if 6 in H:
+            cbm = cbits_setup(m, Wm)
+            H6 = torch.zeros_like(Hm)
+            tm = []
+            for rep in range(a.reps + 1):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                _lib.call("sglm_syrk_cbits", cbm[2].data_ptr(), d.P, fits.data_ptr(), B, a.splits,
+                          H6.data_ptr(), work.data_ptr(), st)
+                e1.record()
+                torch.cuda.synchronize()
+                if rep:
+                    tm.append(e0.elapsed_time(e1) / 1e3)
+            t = float(np.median(tm))
+            up = torch.triu(torch.ones((d.P, d.P), dtype=torch.bool, device="cuda"))
+            res["syrk_masked_v6"] = {"ms": t * 1e3,
+                                     "alg_TFLOPs": B * rows * pa * (pa + 1) / t / 1e12,
+                                     "maxrel_vs_masked": float(((H6[:, up] - Hm[:, up]).abs().max()
+                                                                / Hm[:, up].abs().max()).item())}
     vs = list(H)
     if len(vs) > 1:
         up = torch.triu(torch.ones((d.P, d.P), dtype=torch.bool, device="cuda"))
