@@ -23,7 +23,7 @@ def enet_batch(prob: E.Problem, objectives, reqs):
     dev = d.device
     st = E._stream()
     bf = E._BUF.get(B, P, ld, dev)
-    bf.groups = None                     # exact (f32) Gram path below does not gather rows
+    bf.prob, bf.fit_mask = prob, np.array([r.mask for r in reqs])
     fit_resp = torch.tensor([r.resp for r in reqs], dtype=torch.int32, device=dev)
     fit_mask = torch.tensor([r.mask for r in reqs], dtype=torch.int32, device=dev)
     bf.eta.zero_()
@@ -57,6 +57,7 @@ def enet_batch(prob: E.Problem, objectives, reqs):
     _lib.call("sglm_enet_cd", E._p(bf.H), P, p, E._p(fits), B, E._p(c), E._p(l1d), E._p(l2d),
               E._p(fi), max_sweeps, CD_TOL, E._p(coef), E._p(sweeps), E._p(cw), st)
     bf.beta.copy_(coef.to(torch.float32))
+    bf.prob = bf.keep = None
     d.eta(bf.beta, bf.eta)
     ch = coef.cpu().numpy()
     sw = sweeps.cpu().numpy()

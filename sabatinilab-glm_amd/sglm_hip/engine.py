@@ -219,25 +219,41 @@ class Problem:
         self.Y = torch.from_numpy(Y).to(dev)
         self.M = torch.from_numpy(M).to(dev)
         self._stats = {}
-        # Gram row gathering: the 8-row groups of every 64-row block (one K-step, one 128-B
-        # line per predictor) that holds at least one row of the mask.  Whole aligned blocks
-        # keep every LDS-DMA segment on a single cache line (group-level gathering was
-        # measured slower per step than it saved).
-        goff, gcnt, lists = [], [], []
-        off = 0
-        for m in self.masks:
-            mp = np.zeros(pad_to(n, 64), dtype=bool)
-            mp[:n] = m > 0
-            blk = np.flatnonzero(mp.reshape(-1, 64).any(axis=1))
-            g = (blk[:, None] * 8 + np.arange(8)[None, :]).reshape(-1).astype(np.int32)
-            lists.append(g)
-            goff.append(off)
-            gcnt.append(g.size)
-            off += g.size
-        self.group_offset = np.array(goff, dtype=np.int64)
-        self.group_count = np.array(gcnt, dtype=np.int32)
-        self.groups = torch.from_numpy(np.concatenate(lists) if off else np.zeros(1, np.int32)).to(dev)
+        self._groups = None
         self._compact = {}
+
+    def _group_lists(self):
+        """Row lists for the masked v2/v3 Gram (non-binary designs): the 8-row groups of every
+        aligned 64-row block that holds a row of the mask (built on first use)."""
+        if self._groups is None:
+            n = self.design.n
+            goff, gcnt, lists = [], [], []
+            off = 0
+            for m in self.masks:
+                mp = np.zeros(pad_to(n, 64), dtype=bool)
+                mp[:n] = m > 0
+                blk = np.flatnonzero(mp.reshape(-1, 64).any(axis=1))
+                g = (blk[:, None] * 8 + np.arange(8)[None, :]).reshape(-1).astype(np.int32)
+                lists.append(g)
+                goff.append(off)
+                gcnt.append(g.size)
+                off += g.size
+            self._groups = (torch.from_numpy(np.concatenate(lists) if off else
+                                             np.zeros(1, np.int32)).to(self.design.device),
+                            np.array(goff, dtype=np.int64), np.array(gcnt, dtype=np.int32))
+        return self._groups
+
+    @property
+    def groups(self):
+        return self._group_lists()[0]
+
+    @property
+    def group_offset(self):
+        return self._group_lists()[1]
+
+    @property
+    def group_count(self):
+        return self._group_lists()[2]
 
     def compact(self, mask: int):
         """Row-compacted bit-plane design of one mask (Gram v6), built once and cached:
@@ -298,6 +314,16 @@ class IrlsStats:
     syrk_events: list = field(default_factory=list)    # (start, end, algorithmic flop)
     fit_iters: int = 0
     newton_iters: int = 0
+    trace_phases: bool = False                          # sync + time grid phases (tools)
+    phases: dict = field(default_factory=dict)          # host wall seconds per phase
+
+    def mark(self, name, t0):
+        """Add the wall time since t0 (after a device sync) to phase `name`; returns now."""
+        import time
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        self.phases[name] = self.phases.get(name, 0.0) + (t - t0)
+        return t
 
 
 class _Buffers:
@@ -412,12 +438,11 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
     nsteps = (n + 31) // 32
     ntile1 = (P // 256) * (P // 256 + 1) // 2
     rows = np.array([prob.mask_stats(r.resp, r.mask)[0] for r in reqs], dtype=np.float64)
-    mk = np.array([r.mask for r in reqs])
-    bf.goff = torch.from_numpy(prob.group_offset[mk]).to(dev)
-    bf.gcnt = torch.from_numpy(prob.group_count[mk]).to(dev)
-    bf.groups = prob.groups
-    bf.prob, bf.fit_mask = prob, mk
+    bf.prob, bf.fit_mask = prob, np.array([r.mask for r in reqs])
 
+    import time
+    tick = stats.mark if (stats is not None and stats.trace_phases) else (lambda name, t: t)
+    t0 = tick("irls_setup", time.perf_counter())
     for it in range(int(max_iter.max()) + 1):
         act = np.flatnonzero(active)
         if act.size == 0:
@@ -427,6 +452,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         _lib.call("sglm_xtr", _p(d.xg), d.xtype, ld, P, n, _p(bf.R), B, _p(bf.g),
                   _p(xtr_work), st)
         g = bf.g.cpu().numpy() + lam[:, None] * penal * beta
+        t0 = tick("it_gradient", t0)
         # ---- Hessian
         if const_hess:
             if not factored:
@@ -441,6 +467,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                         bf.H[k].copy_(bf.H[rk])
         else:
             _syrk(d, bf, act.astype(np.int32), nsteps, ntile1, stats, st, rows=rows)
+        t0 = tick("it_gram", t0)
         refactor = 0 if (const_hess and factored) else 1
         bf.gtot.copy_(torch.from_numpy(g))
         act_d = torch.tensor(act, dtype=torch.int32, device=dev)
@@ -451,6 +478,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         factored = True
         d.eta(bf.delta, bf.deta)
         delta = bf.delta.cpu().numpy().astype(np.float64)
+        t0 = tick("it_solve_eta", t0)
         # ---- line search
         _lib.call("sglm_loss_trials", fam, power, n, ld, B, _p(bf.eta), _p(bf.deta), _p(prob.Y),
                   _p(prob.M), _p(fit_resp), _p(fit_mask), _p(tv1), 5, _p(Ltr), _p(xtr_work), st)
@@ -485,6 +513,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                     if o - obj0 <= ARMIJO_SIGMA * ts2[j] * gdir[k]:
                         step[k] = ts2[j]
                         break
+        t0 = tick("it_linesearch", t0)
         # ---- update
         beta += step[:, None] * delta
         bf.beta.copy_(torch.from_numpy(beta.astype(np.float32)))
@@ -502,6 +531,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
             elif n_iter[k] >= max_iter[k]:
                 active[k] = False
             prev_rel[k] = rel
+        t0 = tick("it_update", t0)
 
     bf.prob = bf.keep = None            # drop the compacted designs with the problem
     # final linear predictor from the final coefficients (no accumulated drift)
@@ -525,8 +555,7 @@ def _syrk(d: Design, bf, fits: np.ndarray, nsteps: int, ntile1: int, stats, st, 
         return
     use_f32 = exact and d.xf is not None
     prob = getattr(bf, "prob", None)
-    use_cb = (not use_f32 and d.xbits is not None and SYRK_CBITS and prob is not None
-              and getattr(bf, "groups", None) is not None)
+    use_cb = not use_f32 and d.xbits is not None and SYRK_CBITS and prob is not None
     ev = None
     if stats is not None and stats.record:
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -546,15 +575,14 @@ def _syrk(d: Design, bf, fits: np.ndarray, nsteps: int, ntile1: int, stats, st, 
         if use_f32:
             _lib.call("sglm_syrk_f32", _p(d.xf), d.ld, d.P, d.n, _p(bf.W), _p(fits_d), nact,
                       splits, _p(bf.H), _p(work), st)
-        elif d.xbits is not None and SYRK_BITS:
-            groups = getattr(bf, "groups", None)
-            _lib.call("sglm_syrk_bits", _p(d.xbits), d.ld, d.P, d.n, _p(bf.W), _p(fits_d),
-                      nact, splits, _p(bf.H), _p(work), _p(groups),
-                      _p(bf.goff) if groups is not None else None,
-                      _p(bf.gcnt) if groups is not None else None, st)
-        elif getattr(bf, "groups", None) is not None:
+        elif prob is not None and not use_f32:          # non-binary design, masked fits
+            goff = torch.from_numpy(prob.group_offset[bf.fit_mask]).to(d.device)
+            gcnt = torch.from_numpy(prob.group_count[bf.fit_mask]).to(d.device)
             _lib.call("sglm_syrk_masked", _p(d.xb), d.ld, d.P, d.n, _p(bf.W), _p(fits_d), nact,
-                      splits, _p(bf.H), _p(work), _p(bf.groups), _p(bf.goff), _p(bf.gcnt), st)
+                      splits, _p(bf.H), _p(work), _p(prob.groups), _p(goff), _p(gcnt), st)
+        elif d.xbits is not None and SYRK_BITS:
+            _lib.call("sglm_syrk_bits", _p(d.xbits), d.ld, d.P, d.n, _p(bf.W), _p(fits_d),
+                      nact, splits, _p(bf.H), _p(work), None, None, None, st)
         else:
             _lib.call("sglm_syrk", _p(d.xb), d.ld, d.P, d.n, _p(bf.W), _p(fits_d), nact,
                       splits, _p(bf.H), _p(work), st)

@@ -26,31 +26,73 @@ import numpy as np
 
 from . import engine as E
 from . import folds as F
-from .estimators import Objective, half_loss_np, loss_constant_np
+from .estimators import Objective
 
 
 class _MaskStats:
-    """float64 per-(response, mask) statistics the scores need (host, cached)."""
+    """float64 statistics of every (response, mask) pair that the scores and the y-range check
+    need: count, mean, sum of squares about the mean, min y; per Tweedie power the summed
+    loss constant and null deviance.  Computed in one batched float64 pass on the device
+    (the reference computes them per fold on host copies, backend/sglm.py:150-184, 388-408)."""
 
-    def __init__(self, ys, masks):
-        self.ys, self.masks, self.c = ys, masks, {}
+    def __init__(self, prob: E.Problem):
+        import torch
+        self.torch = torch
+        n, dev = prob.design.n, prob.design.device
+        self.Md = prob.M[:, :n].to(torch.float64)                      # F x n multiplicities
+        self.Yd = torch.from_numpy(np.stack(prob.ys)).to(dev)           # R x n float64
+        cnt = self.Md.sum(1)
+        sy = self.Md @ self.Yd.T                                        # F x R
+        mean = torch.where(cnt[:, None] > 0, sy / cnt.clamp_min(1)[:, None], 0.0)
+        R = self.Yd.shape[0]
+        sst = torch.empty_like(sy)
+        ymin = torch.empty_like(sy)
+        for r in range(R):
+            dev_r = self.Yd[r][None, :] - mean[:, r][:, None]
+            sst[:, r] = (self.Md * dev_r * dev_r).sum(1)
+            ymin[:, r] = torch.where(self.Md > 0, self.Yd[r][None, :], torch.inf).amin(1)
+        self.cnt, self.sy, self.mean = cnt.cpu().numpy(), sy.cpu().numpy(), mean.cpu().numpy()
+        self.sst, self.ymin = sst.cpu().numpy(), ymin.cpu().numpy()
+        self.c = {}
+        self._const = {}
+
+    def _consts(self, power):
+        """Summed per-row loss constant of each (mask, response) for one Tweedie power."""
+        if power not in self._const:
+            torch = self.torch
+            y = self.Yd
+            if power == 1:
+                c = torch.where(y > 0, torch.xlogy(y, y), 0.0) - y
+            elif power == 2:
+                c = -torch.log(y) - 1
+            else:
+                c = torch.pow(y.clamp_min(0), 2 - power) / (1 - power) / (2 - power)
+            out = np.empty((self.Md.shape[0], y.shape[0]))
+            for r in range(y.shape[0]):
+                out[:, r] = torch.where(self.Md > 0, self.Md * c[r][None, :], 0.0).sum(1).cpu().numpy()
+            self._const[power] = out
+        return self._const[power]
 
     def get(self, r, m, power=None):
         key = (r, m, power)
         if key in self.c:
             return self.c[key]
-        w = self.masks[m].astype(np.float64)
-        y = self.ys[r]
-        cnt = w.sum()
-        ym = float(w @ y / cnt) if cnt else 0.0
-        sst = float(w @ (y - ym) ** 2)
-        out = {"cnt": cnt, "mean": ym, "sst": sst}
+        cnt = float(self.cnt[m])
+        ym = float(self.mean[m, r])
+        out = {"cnt": cnt, "mean": ym, "sst": float(self.sst[m, r]), "ymin": float(self.ymin[m, r])}
         if power is not None and cnt:
-            sel = w > 0
-            yy, ww = y[sel], w[sel]
-            out["const"] = float(ww @ loss_constant_np(power, yy))
-            out["null"] = float(ww @ half_loss_np(power, yy, np.full_like(yy, math.log(ym)))) \
-                if ym > 0 else np.inf
+            out["const"] = float(self._consts(power)[m, r])
+            sy = float(self.sy[m, r])
+            if ym > 0:                   # sum of half_loss(y, log(mean)) in closed form
+                if power == 1:
+                    out["null"] = cnt * ym - math.log(ym) * sy
+                elif power == 2:
+                    out["null"] = cnt * math.log(ym) + sy / ym
+                else:
+                    out["null"] = (cnt * ym ** (2 - power) / (2 - power)
+                                   - sy * ym ** (1 - power) / (1 - power))
+            else:
+                out["null"] = np.inf
         self.c[key] = out
         return out
 
@@ -85,6 +127,9 @@ def merge_results(local: dict, dist=None) -> dict:
 def run(X, y, cv_idx, objectives: Sequence[Objective], rolls: Sequence[int],
         score_method: str = "mse", coef0=None, intercept0=None, stats=None, shard=True):
     """Return one result dict per objective (reference key set minus glm_kwargs/model)."""
+    import time
+    tick = stats.mark if (stats is not None and stats.trace_phases) else (lambda name, t: t)
+    t0 = tick("-", time.perf_counter())
     design = X if isinstance(X, E.Design) else E.Design.from_host(X)
     n, p = design.n, design.p
     y = np.asarray(y, dtype=np.float64).reshape(-1)
@@ -101,7 +146,7 @@ def run(X, y, cv_idx, objectives: Sequence[Objective], rolls: Sequence[int],
     ridx = {r: i for i, r in enumerate(roll_list)}
     ys = [np.roll(y, r) for r in roll_list]
     prob = E.Problem(design, ys, masks)
-    ms = _MaskStats(ys, masks)
+    ms = _MaskStats(prob)
 
     # ---- fit table: (param j, split k) then refit (j, -1)
     table = []
@@ -109,12 +154,13 @@ def run(X, y, cv_idx, objectives: Sequence[Objective], rolls: Sequence[int],
         if obj.family == E.FAM_TWEEDIE_LOG:
             for r_, m_ in [(ridx[int(roll)], 2 * k) for k in range(K)] + [(0, FULL)]:
                 st = ms.get(r_, m_)
-                if st["cnt"] and (np.any(ys[r_][masks[m_] > 0] < 0) or st["mean"] <= 0):
+                if st["cnt"] and (st["ymin"] < 0 or st["mean"] <= 0):
                     raise ValueError("Some value(s) of y are out of the valid range of the loss "
                                      "'HalfPoissonLoss'.")
         for k in range(K):
             table.append((j, k, 2 * k, ridx[int(roll)], 2 * k + 1))
         table.append((j, -1, FULL, 0, -1))
+    t0 = tick("grid_setup", t0)
     dist = _dist() if shard else None
     rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (0, 1)
     mine = shard_indices(len(table), rank, world)
@@ -135,6 +181,7 @@ def run(X, y, cv_idx, objectives: Sequence[Objective], rolls: Sequence[int],
                                  obj.max_iter,
                                  None if coef0 is None else np.asarray(coef0, float),
                                  None if intercept0 is None else float(intercept0)))
+        t0 = tick("fit_table", t0)
         if key[0] == "cd":
             from . import cd
             res, eta = cd.enet_batch(prob, [objectives[table[i][0]] for i in idxs], reqs)
@@ -142,11 +189,13 @@ def run(X, y, cv_idx, objectives: Sequence[Objective], rolls: Sequence[int],
         else:
             res, eta = E.irls(prob, reqs, stats=stats)
             fam, power = key
+        t0 = tick("solve", t0)
         sets = np.array([[table[i][2], table[i][4]] for i in idxs], dtype=np.int32)
         sums = E.score_sums(prob, fam, power, eta, [table[i][3] for i in idxs], sets)
         for q, i in enumerate(idxs):
             rr = res[q]
             results[i] = (rr.coef, rr.intercept, rr.n_iter, rr.converged, sums[q])
+    t0 = tick("score_sums", t0)
     results = merge_results(results, dist)
 
     # ---- assemble per-param dicts (reference key order, backend/sglm_cv.py:188-200)
@@ -193,6 +242,7 @@ def run(X, y, cv_idx, objectives: Sequence[Objective], rolls: Sequence[int],
             "n_iter": n_iter,
             "converged": conv,
         })
+    tick("assemble", t0)
     return out
 
 
