@@ -153,6 +153,20 @@ int sglm_gather_w(const float* W, int64_t ld, const int32_t* fits, int32_t nact,
 int sglm_syrk_cbits(const int64_t* desc, int32_t P, const int32_t* fits, int32_t nact,
                     int32_t splits, float* H, void* work, sglm_stream_t stream);
 
+/* Row-major bit-planes of a 0/1 design for the MFMA GEMVs: out[(t * ld + i) * 2 + {0,1}] =
+ * the bits of X[64t + alpha][i], alpha = 0..63, fragment order (see sglm_pack_bits_rows).
+ * Size (P/64) * ld * 8 bytes.  *nonbinary as for sglm_pack_bits. */
+int sglm_pack_bits_t(const uint16_t* Xb, int64_t ld, int32_t P, uint32_t* out,
+                     int32_t* nonbinary, sglm_stream_t stream);
+
+/* eta[k] = X beta[k] (as sglm_gemv_eta) for a 0/1 design given as sglm_pack_bits_t planes:
+ * beta split into three bf16 pieces (exact), bf16 MFMA with f32 accumulation.  Writes all
+ * ld rows of eta (padding rows: 0).  work: sglm_eta_bits_work_bytes(P, B) bytes.
+ * Replaces X @ coef (backend/sglm.py:347 -> sklearn glm.py:350). */
+size_t sglm_eta_bits_work_bytes(int32_t P, int32_t B);
+int sglm_gemv_eta_bits(const uint32_t* rbits, int64_t ld, int32_t P, const float* beta,
+                       int32_t B, float* eta, void* work, sglm_stream_t stream);
+
 /* Development entries: a specific bf16 Gram variant (1 = register-staged, 2 = LDS-DMA
  * staged; sglm_syrk uses the default), same arguments as sglm_syrk. */
 int sglm_syrk_v1(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, const float* W,

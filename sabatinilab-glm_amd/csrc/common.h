@@ -68,4 +68,63 @@ __device__ __forceinline__ double wave_sum_d(double v) {
     return v;
 }
 
+// ---- bit-plane designs (Gram v6, eta/xtr on MFMA) -----------------------------------
+// Inside a 32-bit word, element rho (row or predictor) sits at bit
+// 4*(rho/8) + (rho%8)/2 + 16*(rho%2): the dword of MFMA fragment elements (2j, 2j+1) of 8-element
+// chunk g has its two bits at p = 4g + j and p + 16, so
+//   rotr(word, p - 14) & 0x40004000  = two bf16 values 2.0 / 0.0   (2 VALU)
+//   pk_ashr_i16(rotr(word, p - 15), 15) = two 16-bit masks          (2 VALU)
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x2 g_uint2;
+typedef __attribute__((address_space(1))) const u32x4 g_uint4;
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+// generic -> global address-space pointer (lets the compiler emit global_load)
+template <typename G>
+__device__ __forceinline__ G* as_global(const void* p) {
+    return reinterpret_cast<G*>(reinterpret_cast<uintptr_t>(p));
+}
+
+__device__ __forceinline__ uint32_t rotr32(uint32_t x, uint32_t s) {
+    return __builtin_amdgcn_alignbit(x, x, s);
+}
+
+// source element of target bit t (0..31) of a fragment-ordered word
+__device__ __forceinline__ int frag_bit_source(int t) {
+    const int tt = t & 15;
+    return 8 * (tt >> 2) + 2 * (tt & 3) + (t >> 4);
+}
+
+// bf16 2.0/0 fragment (8 elements of chunk q = 2*ks + h) from a 64-element word pair
+__device__ __forceinline__ bf16x8 frag_two(u32x2 w, int ks, int h) {
+    const uint32_t word = ks < 2 ? w.x : w.y;
+    const uint32_t p0 = 8 * (ks & 1) + 4 * h;
+    uint32_t d[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) d[j] = rotr32(word, (p0 + j + 18) & 31) & 0x40004000u;
+    return __builtin_bit_cast(bf16x8, make_uint4(d[0], d[1], d[2], d[3]));
+}
+
+// Loads in inline asm so LLVM cannot sink a prefetch to its use (it does for plain loads);
+// the consumer must first run an asm "s_waitcnt vmcnt(0)" that ties the loaded registers.
+__device__ __forceinline__ u32x2 gld2(g_uint2* p) {
+    u32x2 v;
+    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ u32x4 gld4(g_uint4* p) {
+    u32x4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+
+// three bf16 pieces hi + mid + lo == x exactly (f32 has 24 significand bits)
+__device__ __forceinline__ void split3(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
+    hi = (__bf16)x;
+    const float r1 = x - (float)hi;
+    mid = (__bf16)r1;
+    lo = (__bf16)(r1 - (float)mid);
+}
+
 }  // namespace sglm

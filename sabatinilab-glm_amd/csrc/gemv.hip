@@ -1,0 +1,188 @@
+// eta = X beta on the MFMA path for 0/1 designs (gfx950).
+//
+// The reference evaluates X @ coef for every loss/gradient evaluation and predict
+// (backend/sglm.py:347 -> sklearn glm.py:350).  Here, for a 0/1 design:
+//   * X is held a second time as ROW-major bit-planes, K-step-major: rbits[t][i] = uint2 with
+//     the 64 bits of predictors 64t..64t+63 of row i, fragment order (common.h), 256 MB at
+//     1M x 2048 — built once per design (sglm_pack_bits_t);
+//   * beta (f32) is split into three bf16 pieces hi + mid + lo == beta exactly, so the MFMA
+//     products (2.0 or 0) x piece are exact and the f32 accumulation is the only rounding —
+//     the same accuracy class as an f32 FMA GEMV;
+//   * one wave computes 32 fits x 128 rows: A = the 3 x 32 piece rows (loaded directly),
+//     B = row bits expanded in registers (2 VALU per dword), acc[3][4] of
+//     v_mfma_f32_32x32x16_bf16; the three pieces of a fit land in the same lane, so the
+//     result is summed in registers and written coalesced (eta is [fit][row]).
+#include "common.h"
+
+namespace sglm {
+
+// rbits[t * ld + i]: bits of X[64t + alpha][i], alpha = 0..63, fragment order.  One thread
+// per (row, 64-predictor step); consecutive threads -> consecutive rows (coalesced).
+__global__ void __launch_bounds__(256) pack_bits_t_kernel(const uint16_t* __restrict__ Xb,
+                                                          int64_t ld, int32_t P,
+                                                          u32x2* __restrict__ out,
+                                                          int32_t* nonbinary) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int t = blockIdx.y;
+    if (i >= ld) return;
+    uint32_t w[2] = {0u, 0u};
+    bool bad = false;
+#pragma unroll 8
+    for (int al = 0; al < 64; ++al) {
+        const uint16_t v = Xb[(int64_t)(64 * t + al) * ld + i];
+        bad |= !(v == 0x3F80u || v == 0 || v == 0x8000u);
+        const int rho = al & 31;
+        const int pos = 4 * (rho >> 3) + ((rho & 7) >> 1) + 16 * (rho & 1);
+        w[al >> 5] |= (uint32_t)(v == 0x3F80u) << pos;
+    }
+    out[(int64_t)t * ld + i] = (u32x2){w[0], w[1]};
+    if (bad) atomicOr(nonbinary, 1);
+}
+
+// out[p][f][e] (p = 0,1,2: hi, mid, lo) for f < Bp, e < len; rows f >= B are zero
+__global__ void __launch_bounds__(256) split3_kernel(const float* __restrict__ src, int64_t len,
+                                                     int32_t B, int32_t Bp,
+                                                     __bf16* __restrict__ out) {
+    const int64_t total = (int64_t)Bp * len;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * 256) {
+        const float x = (e / len) < B ? src[e] : 0.0f;
+        __bf16 hi, mid, lo;
+        split3(x, hi, mid, lo);
+        out[e] = hi;
+        out[total + e] = mid;
+        out[2 * total + e] = lo;
+    }
+}
+
+struct StepE {
+    u32x2 b[4];          // row bits of the 4 row tiles
+    u32x4 a[3][4];       // piece x sub-step: 8 bf16 of this lane's fit
+};
+
+__device__ __forceinline__ void loadE(StepE& t, g_uint2* pb, g_uint4* pa, int64_t ld,
+                                      int64_t pstride, int s) {
+#pragma unroll
+    for (int n = 0; n < 4; ++n) t.b[n] = gld2(pb + (int64_t)s * ld + 32 * n);
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) t.a[pc][ks] = gld4(pa + pc * pstride + s * 8 + 2 * ks);
+}
+
+__device__ __forceinline__ void waitE(StepE& t) {
+    asm volatile("s_waitcnt vmcnt(0)"
+                 : "+v"(t.b[0]), "+v"(t.b[1]), "+v"(t.b[2]), "+v"(t.b[3]), "+v"(t.a[0][0]),
+                   "+v"(t.a[0][1]), "+v"(t.a[0][2]), "+v"(t.a[0][3]), "+v"(t.a[1][0]),
+                   "+v"(t.a[1][1]), "+v"(t.a[1][2]), "+v"(t.a[1][3]), "+v"(t.a[2][0]),
+                   "+v"(t.a[2][1]), "+v"(t.a[2][2]), "+v"(t.a[2][3])
+                 :
+                 : "memory");
+}
+
+__device__ __forceinline__ void mmaE(const StepE& t, int h, f32x16 (&acc)[3][4]) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+        bf16x8 bx[4];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) bx[n] = frag_two(t.b[n], ks, h);
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc) {
+            const bf16x8 a = __builtin_bit_cast(bf16x8, t.a[pc][ks]);
+#pragma unroll
+            for (int n = 0; n < 4; ++n)
+                acc[pc][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bx[n], acc[pc][n], 0, 0, 0);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
+eta_bits_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
+                const __bf16* __restrict__ Dp, int32_t Bp, int32_t B, float* __restrict__ eta) {
+    const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
+    const int64_t row0 = (int64_t)blockIdx.x * 128;
+    const int g = blockIdx.y;
+    g_uint2* pb = as_global<g_uint2>(rbits + row0 + r);
+    g_uint4* pa = as_global<g_uint4>(Dp + (int64_t)(g * 32 + r) * P + 8 * h);
+    const int64_t pstride = (int64_t)Bp * P / 8;           // one piece plane, in uint4
+    const int nsteps = P / 64;
+
+    f32x16 acc[3][4];
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[pc][n] = (f32x16){};
+
+    StepE A, Bs;
+    loadE(A, pb, pa, ld, pstride, 0);
+    waitE(A);
+    int s = 0;
+    for (; s + 1 < nsteps; s += 2) {
+        loadE(Bs, pb, pa, ld, pstride, s + 1);
+        __builtin_amdgcn_sched_barrier(0);          // keep the prefetch ahead of the MFMAs
+        mmaE(A, h, acc);
+        __builtin_amdgcn_sched_barrier(0);          // ... and the wait behind them
+        waitE(Bs);
+        loadE(A, pb, pa, ld, pstride, s + 2 < nsteps ? s + 2 : nsteps - 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mmaE(Bs, h, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        waitE(A);
+    }
+    if (s < nsteps) mmaE(A, h, acc);
+
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int f = g * 32 + (j & 3) + 8 * (j >> 2) + 4 * h;
+            if (f < B)
+                eta[(int64_t)f * ld + row0 + n * 32 + r] =
+                    0.5f * ((acc[0][n][j] + acc[1][n][j]) + acc[2][n][j]);
+        }
+}
+
+}  // namespace sglm
+
+using namespace sglm;
+
+extern "C" {
+
+int sglm_pack_bits_t(const uint16_t* Xb, int64_t ld, int32_t P, uint32_t* out,
+                     int32_t* nonbinary, sglm_stream_t stream) {
+    if (!Xb || !out || !nonbinary || ld % 256 || P % 64) {
+        set_error("sglm_pack_bits_t: bad args");
+        return SGLM_EINVAL;
+    }
+    pack_bits_t_kernel<<<dim3((unsigned)(ld / 256), (unsigned)(P / 64)), 256, 0,
+                         as_stream(stream)>>>(Xb, ld, P, reinterpret_cast<u32x2*>(out),
+                                              nonbinary);
+    return check_launch("pack_bits_t_kernel");
+}
+
+size_t sglm_eta_bits_work_bytes(int32_t P, int32_t B) {
+    const int64_t Bp = ((int64_t)B + 31) / 32 * 32;
+    return (size_t)3 * (size_t)Bp * (size_t)P * 2;
+}
+
+int sglm_gemv_eta_bits(const uint32_t* rbits, int64_t ld, int32_t P, const float* beta,
+                       int32_t B, float* eta, void* work, sglm_stream_t stream) {
+    if (B <= 0) return SGLM_OK;
+    if (!rbits || !beta || !eta || !work || ld % 256 || P % 256) {
+        set_error("sglm_gemv_eta_bits: bad args");
+        return SGLM_EINVAL;
+    }
+    const int32_t Bp = (B + 31) / 32 * 32;
+    hipStream_t s = as_stream(stream);
+    __bf16* Dp = reinterpret_cast<__bf16*>(work);
+    const int64_t total = (int64_t)Bp * P;
+    split3_kernel<<<(unsigned)((total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048), 256, 0,
+                    s>>>(beta, P, B, Bp, Dp);
+    int st = check_launch("split3_kernel");
+    if (st) return st;
+    eta_bits_kernel<<<dim3((unsigned)(ld / 128), (unsigned)(Bp / 32)), 64, 0, s>>>(
+        reinterpret_cast<const u32x2*>(rbits), ld, P, Dp, Bp, B, eta);
+    return check_launch("eta_bits_kernel");
+}
+
+}  // extern "C"

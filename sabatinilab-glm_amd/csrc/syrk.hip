@@ -822,34 +822,11 @@ extern "C" int sglm_syrk_bits(const uint32_t* Xbits, int64_t ld, int32_t P, int6
 //   * per-slot descriptor (4 x int64): bit-plane base, rows, bf16 compact weights, row list
 //     (0 = identity; used by the weight gather only).
 namespace sglm {
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(1))) const u32x2 g_uint2;
-typedef __attribute__((address_space(1))) const u32x4 g_uint4;
-typedef short s16x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ uint32_t rotr32(uint32_t x, uint32_t s) {
-    return __builtin_amdgcn_alignbit(x, x, s);
-}
 
 struct Step6 {
     u32x2 a[4], b[4];
     u32x4 w[4];
 };
-
-// Loads are inline asm so LLVM cannot sink them to their use (it does for plain loads, which
-// removes the prefetch); wait6 is the matching s_waitcnt, with every loaded register tied so
-// no consumer can be scheduled above it.
-__device__ __forceinline__ u32x2 gld2(g_uint2* p) {
-    u32x2 v;
-    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-    return v;
-}
-__device__ __forceinline__ u32x4 gld4(g_uint4* p) {
-    u32x4 v;
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-    return v;
-}
 
 __device__ __forceinline__ void load6(Step6& t, g_uint2* pa, g_uint2* pb, g_uint4* pw,
                                       int64_t s, int32_t P) {
@@ -879,13 +856,7 @@ __device__ __forceinline__ void frags6(const Step6& t, int ks, int h, Frag6& f) 
     const uint32_t p0 = 8 * (ks & 1) + 4 * h;            // bit of row pair j = 0
     const uint32_t wp[4] = {t.w[ks].x, t.w[ks].y, t.w[ks].z, t.w[ks].w};
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        const uint32_t word = ks < 2 ? t.a[m].x : t.a[m].y;
-        uint32_t d[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) d[j] = rotr32(word, (p0 + j + 18) & 31) & 0x40004000u;
-        f.a[m] = __builtin_bit_cast(bf16x8, make_uint4(d[0], d[1], d[2], d[3]));
-    }
+    for (int m = 0; m < 4; ++m) f.a[m] = frag_two(t.a[m], ks, h);
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
         const uint32_t word = ks < 2 ? t.b[n].x : t.b[n].y;
@@ -1036,8 +1007,7 @@ __global__ void __launch_bounds__(256) pack_bits_rows_kernel(
     const int64_t wid = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
     const int64_t nblk = (nrows + 63) / 64;
     const int64_t total = nblk * P;
-    const int t = lane & 31, tt = t & 15;
-    const int src = (lane & 32) | (8 * (tt >> 2) + 2 * (tt & 3) + (t >> 4));
+    const int src = (lane & 32) | frag_bit_source(lane & 31);
     for (int64_t g = wid; g < total; g += ((int64_t)gridDim.x * 256) >> 6) {
         const int64_t blk = g / P, a = g % P;
         const int64_t k = blk * 64 + lane;

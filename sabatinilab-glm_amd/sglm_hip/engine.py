@@ -44,6 +44,7 @@ COL_PAD = 256
 ROW_PAD = 256
 ARMIJO_SIGMA = 2.0 ** -11      # sklearn _newton_solver.py:214
 SYRK_BITS = True               # use the bit-plane Gram (v3) for 0/1 designs
+ETA_BITS = True                # eta on the MFMA from row-major bit-planes for 0/1 designs
 SYRK_CBITS = True              # ... and its row-compacted register-only form (v6) when fits
                                # carry masks (the default path for event designs)
 
@@ -85,6 +86,7 @@ class Design:
         self.xb = alloc((self.P, self.ld), dtype=torch.bfloat16, device=device)
         self.xf = None
         self.xbits = None      # uint32 bit-planes [P, ld/32] when the design is 0/1
+        self.rbits = None      # row-major bit-planes [P/64][ld] x uint2 (MFMA eta) when 0/1
         self.device = device
 
     @property
@@ -136,11 +138,19 @@ class Design:
             self._pack_bits()
 
     def _pack_bits(self):
-        """Bit-plane copy for 0/1 designs (Gram v3); dropped again if X is not binary."""
+        """Bit-plane copies for 0/1 designs (column-packed for the Gram, row-major for eta);
+        dropped again if X is not binary."""
         bits = torch.empty((self.P, self.ld // 32), dtype=torch.int32, device=self.device)
         flag = torch.zeros(1, dtype=torch.int32, device=self.device)
         _lib.call("sglm_pack_bits", _p(self.xb), self.ld, self.P, _p(bits), _p(flag), _stream())
-        self.xbits = None if int(flag.item()) else bits
+        if int(flag.item()):
+            self.xbits = self.rbits = None
+            return
+        self.xbits = bits
+        self.rbits = torch.empty((self.P // 64) * self.ld * 2, dtype=torch.int32,
+                                 device=self.device)
+        _lib.call("sglm_pack_bits_t", _p(self.xb), self.ld, self.P, _p(self.rbits), _p(flag),
+                  _stream())
 
     @classmethod
     def from_events(cls, E, shifts: Sequence[int], row0: int, n: int, device="cuda",
@@ -190,8 +200,13 @@ class Design:
         B = beta_dev.shape[0]
         if out is None:
             out = torch.empty((B, self.ld), dtype=torch.float32, device=self.device)
-        _lib.call("sglm_gemv_eta", _p(self.xg), self.xtype, self.ld, self.P, self.n,
-                  _p(beta_dev), B, _p(out), _stream())
+        if self.rbits is not None and ETA_BITS:
+            work = _work(_lib.query("sglm_eta_bits_work_bytes", self.P, B), self.device, "eta")
+            _lib.call("sglm_gemv_eta_bits", _p(self.rbits), self.ld, self.P, _p(beta_dev), B,
+                      _p(out), _p(work), _stream())
+        else:
+            _lib.call("sglm_gemv_eta", _p(self.xg), self.xtype, self.ld, self.P, self.n,
+                      _p(beta_dev), B, _p(out), _stream())
         return out
 
 
@@ -358,12 +373,13 @@ _BUF = _Buffers()
 _WORK = {}
 
 
-def _work(nbytes, dev):
+def _work(nbytes, dev, tag="main"):
+    """Grow-only scratch buffer per (device, tag); stream-ordered reuse only."""
     nbytes = max(int(nbytes), 16)
-    t = _WORK.get(dev)
+    t = _WORK.get((dev, tag))
     if t is None or t.numel() < nbytes:
         t = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        _WORK[dev] = t
+        _WORK[(dev, tag)] = t
     return t
 
 

@@ -406,3 +406,34 @@ def test_syrk_cbits_compacted_gram(engine, torch_mod):
             assert np.all(np.isfinite(got)), (splits, k)
             scale = max(np.max(np.abs(ref)), 1.0)
             assert np.max(np.abs(got - ref[blk])) <= 2e-6 * scale, (splits, k)
+
+
+def test_eta_bits_matches_float64(engine, torch_mod):
+    """MFMA eta over row-major bit-planes (beta split in 3 bf16 pieces) == X @ beta to f32
+    accuracy, for every row incl. padding (0), with a ragged fit count (B = 37)."""
+    torch = torch_mod
+    from sglm_hip import _lib, synth
+    s = synth.make(N=7000, m=11, L=4, rho=0.1, seed=41)
+    d = engine.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
+    assert d.rbits is not None
+    rng = np.random.default_rng(42)
+    B = 37
+    beta = (rng.standard_normal((B, d.P)) * np.exp(rng.uniform(-8, 3, (B, d.P)))).astype(np.float32)
+    beta[:, d.p + 1:] = 0.0
+    bd = torch.from_numpy(beta).cuda()
+    out = torch.full((B, d.ld), float("nan"), dtype=torch.float32, device="cuda")
+    work = torch.empty(_lib.query("sglm_eta_bits_work_bytes", d.P, B), dtype=torch.uint8,
+                       device="cuda")
+    _lib.call("sglm_gemv_eta_bits", d.rbits.data_ptr(), d.ld, d.P, bd.data_ptr(), B,
+              out.data_ptr(), work.data_ptr(), 0)
+    ref_valu = torch.empty_like(out)
+    _lib.call("sglm_gemv_eta", d.xb.data_ptr(), 0, d.ld, d.P, d.n, bd.data_ptr(), B,
+              ref_valu.data_ptr(), 0)
+    X = d.xb.double().cpu().numpy()                       # (P, ld)
+    ref = beta.astype(np.float64) @ X                     # (B, ld)
+    got = out.cpu().numpy()
+    assert np.all(np.isfinite(got))
+    scale = np.abs(beta.astype(np.float64)) @ np.abs(X)   # error bound scale per entry
+    assert np.max(np.abs(got - ref) / np.maximum(scale, 1e-30)) < 2e-6
+    assert not got[:, s.N + 1:].any()                     # padding rows are exactly 0
+    assert np.max(np.abs(got - ref_valu.cpu().numpy()) / np.maximum(scale, 1e-30)) < 2e-6
