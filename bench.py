@@ -122,7 +122,8 @@ def main():
     ktime = sum(e0.elapsed_time(e1) for e0, e1, _, _ in stats.syrk_events) / 1e3
     kflop = sum(nact_flop for _, _, _, nact_flop in stats.syrk_events)
     nlaunch = len(stats.syrk_events)
-    t = torch.tensor([elapsed, float(stats.fit_iters), ktime, kflop, float(nlaunch)],
+    t = torch.tensor([elapsed, float(stats.fit_iters), ktime, kflop, float(nlaunch),
+                      float(stats.gram_fits)],
                      dtype=torch.float64, device="cuda")
     if world > 1:
         mx = t.clone()
@@ -131,8 +132,10 @@ def main():
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         elapsed, fit_iters = float(mx[0]), float(sm[1])
         ktime, kflop, nlaunch = float(sm[2]), float(sm[3]), int(sm[4])
+        gram_fits = float(sm[5])
     else:
         fit_iters = float(stats.fit_iters)
+        gram_fits = float(stats.gram_fits)
     if rank == 0:
         pa = s.p + 1
         achieved = kflop / ktime / 1e12 if ktime > 0 else 0.0
@@ -160,6 +163,7 @@ def main():
                 "n_rows": s.N, "p": s.p, "fits": nlam * (K + 1),
                 "grid_wall_s": elapsed / a.steps,
                 "fit_iters_per_grid": fit_iters / a.steps,
+                "distinct_hessians_per_grid": gram_fits / a.steps,
                 "setup_s": setup_s,
                 "parallelism": f"fits round-robin over {world} rank(s), RCCL all-gather of results",
             },

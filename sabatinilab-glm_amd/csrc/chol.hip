@@ -64,53 +64,61 @@ __global__ void __launch_bounds__(kCT) chol_prep_kernel(
     for (int j = tid; j < P; j += kCT) rhs[j] = frz[j] ? 0.0f : (float)g[j];
 }
 
+__device__ __forceinline__ float lanef(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
 // One wave per fit: factor the diagonal block (refactor) and forward-solve the rhs block.
+// Lane c holds column c of the block in registers (a[r] = A[k0+r][k0+c]); step q reads the
+// pivot and row q of U with v_readlane (scalar broadcasts), so the whole 64-step
+// factorisation is register FMAs (entries below the diagonal are updated too and ignored).
 __global__ void __launch_bounds__(64) chol_diag_kernel(
     float* __restrict__ Hall, int32_t P, int32_t k0, const int32_t* __restrict__ fits,
     uint8_t* __restrict__ frozen_all, float* __restrict__ rhs_all,
     const float* __restrict__ diag_all, int32_t* __restrict__ info, int32_t refactor) {
-    __shared__ float sD[kNB][kNB + 1];
     const int fit = fits[blockIdx.x];
     float* H = Hall + (int64_t)fit * P * P;
     uint8_t* frz = frozen_all + (int64_t)fit * P + k0;
     float* rhs = rhs_all + (int64_t)fit * P + k0;
     const int c = threadIdx.x;
-    for (int r = 0; r < kNB; ++r) sD[r][c] = (r <= c) ? H[(int64_t)(k0 + r) * P + k0 + c] : 0.0f;
-    __syncthreads();
+    float a[kNB];
+#pragma unroll
+    for (int r = 0; r < kNB; ++r) a[r] = (r <= c) ? H[(int64_t)(k0 + r) * P + k0 + c] : 0.0f;
     int myfrz = frz[c];
     if (refactor) {
         const float orig = diag_all[(int64_t)fit * P + k0 + c];
         int dropped = 0;
+#pragma unroll
         for (int q = 0; q < kNB; ++q) {
-            const float piv = __shfl(sD[q][c], q, 64);
-            const float origq = __shfl(orig, q, 64);
-            const bool was = __shfl(myfrz, q, 64) != 0;
-            const bool drop = was || !(piv > 1e-6f * origq);
+            const float piv = lanef(a[q], q);
+            const bool was = __builtin_amdgcn_readlane(myfrz, q) != 0;
+            const bool drop = was || !(piv > 1e-6f * lanef(orig, q));
             const float d = drop ? 1.0f : sqrtf(piv);
-            float u = sD[q][c];
-            if (c == q) u = d;
-            else if (c > q) u = drop ? 0.0f : u / d;
-            sD[q][c] = u;
-            if (c == q && drop && !was) { myfrz = 1; dropped = 1; }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            if (c > q)
-                for (int i = q + 1; i <= c; ++i) sD[i][c] -= sD[q][i] * u;
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            float u = 0.0f;
+            if (c > q && !drop) u = a[q] / d;
+            if (c == q) {
+                a[q] = d;
+                if (drop && !was) { myfrz = 1; dropped = 1; }
+            } else if (c > q) {
+                a[q] = u;
+            }
+#pragma unroll
+            for (int i = q + 1; i < kNB; ++i) a[i] -= lanef(u, i) * u;
         }
         if (dropped) atomicAdd(&info[fit], 1);
         frz[c] = (uint8_t)myfrz;
-        for (int r = 0; r <= c; ++r) H[(int64_t)(k0 + r) * P + k0 + c] = sD[r][c];
-        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kNB; ++r)
+            if (r <= c) H[(int64_t)(k0 + r) * P + k0 + c] = a[r];
     }
-    // forward solve U_kk^T z = rhs_k, lane = row
+    // forward solve U_kk^T z = rhs_k, lane = row: step q needs U[q][q] (lane q) and
+    // U[q][c] (this lane's a[q])
     float zc = rhs[c];
+#pragma unroll
     for (int q = 0; q < kNB; ++q) {
-        const float zq = __shfl(zc, q, 64) / sD[q][q];
-        const float zz = __shfl(myfrz, q, 64) ? 0.0f : zq;
-        if (c == q) zc = zz;
-        else if (c > q) zc -= sD[q][c] * zz;
+        const float zq = __builtin_amdgcn_readlane(myfrz, q) ? 0.0f : lanef(zc, q) / lanef(a[q], q);
+        if (c == q) zc = zq;
+        else if (c > q) zc -= a[q] * zq;
     }
     rhs[c] = zc;
 }
@@ -200,7 +208,10 @@ __global__ void __launch_bounds__(kCT) chol_update_kernel(float* __restrict__ Ha
     }
 }
 
-// Blocked back substitution U x = z, then delta = -x.
+// Blocked back substitution U x = z, then delta = -x.  Per 64-block (last to first): the
+// four waves form the 64 row dot products with the solved tail (16 independent accumulators
+// per wave, all loads in flight together), then wave 0 solves the 64 x 64 triangle with
+// readlane broadcasts.
 __global__ void __launch_bounds__(kCT) chol_back_kernel(
     const float* __restrict__ Hall, int32_t P, const int32_t* __restrict__ fits,
     const uint8_t* __restrict__ frozen_all, float* __restrict__ rhs_all,
@@ -217,13 +228,21 @@ __global__ void __launch_bounds__(kCT) chol_back_kernel(
     const int nb = P / kNB;
     for (int kb = nb - 1; kb >= 0; --kb) {
         const int k0 = kb * kNB;
-        for (int rr = 0; rr < kNB / 4; ++rr) {
-            const int r = wave * (kNB / 4) + rr;
-            float s = 0.0f;
-            for (int j = k0 + kNB + lane; j < P; j += 64) s += H[(int64_t)(k0 + r) * P + j] * x[j];
+        const int r0 = k0 + wave * (kNB / 4);
+        float acc[kNB / 4];
 #pragma unroll
-            for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-            if (lane == 0) part[r] = s;
+        for (int rr = 0; rr < kNB / 4; ++rr) acc[rr] = 0.0f;
+        for (int j = k0 + kNB + lane; j < P; j += 64) {
+            const float xj = x[j];
+#pragma unroll
+            for (int rr = 0; rr < kNB / 4; ++rr) acc[rr] += H[(int64_t)(r0 + rr) * P + j] * xj;
+        }
+#pragma unroll
+        for (int rr = 0; rr < kNB / 4; ++rr) {
+            float v = acc[rr];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+            if (lane == 0) part[wave * (kNB / 4) + rr] = v;
         }
         for (int e = tid; e < kNB * kNB; e += kCT) {
             const int r = e / kNB, c = e % kNB;
@@ -232,8 +251,11 @@ __global__ void __launch_bounds__(kCT) chol_back_kernel(
         __syncthreads();
         if (wave == 0) {
             float v = z[k0 + lane] - part[lane];
+            const int fr = frz[k0 + lane];
+            const float dgl = sD[lane][lane];
+#pragma unroll
             for (int q = kNB - 1; q >= 0; --q) {
-                const float xq = frz[k0 + q] ? 0.0f : __shfl(v, q, 64) / sD[q][q];
+                const float xq = __builtin_amdgcn_readlane(fr, q) ? 0.0f : lanef(v, q) / lanef(dgl, q);
                 if (lane == q) v = xq;
                 else if (lane < q) v -= sD[lane][q] * xq;
             }

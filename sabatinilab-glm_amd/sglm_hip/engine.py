@@ -329,6 +329,7 @@ class IrlsStats:
     syrk_events: list = field(default_factory=list)    # (start, end, algorithmic flop)
     fit_iters: int = 0
     newton_iters: int = 0
+    gram_fits: int = 0                                  # distinct Hessians formed
     trace_phases: bool = False                          # sync + time grid phases (tools)
     phases: dict = field(default_factory=dict)          # host wall seconds per phase
 
@@ -482,7 +483,23 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                     if rk != k:
                         bf.H[k].copy_(bf.H[rk])
         else:
-            _syrk(d, bf, act.astype(np.int32), nsteps, ntile1, stats, st, rows=rows)
+            # Fits whose weights are bitwise identical have identical Hessians: same mask,
+            # response and coefficients (every fit of a mask/response pair in the first
+            # iteration, which starts from the intercept-only model).  Form each distinct
+            # Hessian once and copy it.
+            reps = {}
+            dup = []
+            for k in act:
+                key = (reqs[k].mask, reqs[k].resp, beta[k].tobytes())
+                rk = reps.setdefault(key, k)
+                if rk != k:
+                    dup.append((k, rk))
+            uniq = np.array(sorted(reps.values()), dtype=np.int32)
+            _syrk(d, bf, uniq, nsteps, ntile1, stats, st, rows=rows)
+            for k, rk in dup:
+                bf.H[k].copy_(bf.H[rk])
+            if stats is not None:
+                stats.gram_fits += int(uniq.size)
         t0 = tick("it_gram", t0)
         refactor = 0 if (const_hess and factored) else 1
         bf.gtot.copy_(torch.from_numpy(g))
