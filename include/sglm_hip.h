@@ -140,6 +140,11 @@ int sglm_syrk_bits(const uint32_t* Xbits, int64_t ld, int32_t P, int64_t n, cons
 int sglm_pack_bits_rows(const uint16_t* Xb, int64_t ld, int32_t P, const int32_t* rows,
                         int64_t nrows, uint32_t* out, int32_t* nonbinary, sglm_stream_t stream);
 
+/* sglm_pack_bits_rows from the column-packed planes of sglm_pack_bits (same output; reads
+ * 1 bit per element instead of the bf16 design). */
+int sglm_compact_bits(const uint32_t* xbits, int64_t ld, int32_t P, const int32_t* rows,
+                      int64_t nrows, uint32_t* out, sglm_stream_t stream);
+
 /* Per-slot descriptor for Gram v6, 4 x int64 per slot: [0] device address of the slot's
  * compacted bit-plane design, [1] its row count, [2] device address of the slot's compact
  * bf16 weights (>= ceil(rows/64)*64 entries), [3] device address of its int32 row list
@@ -166,6 +171,14 @@ int sglm_pack_bits_t(const uint16_t* Xb, int64_t ld, int32_t P, uint32_t* out,
 size_t sglm_eta_bits_work_bytes(int32_t P, int32_t B);
 int sglm_gemv_eta_bits(const uint32_t* rbits, int64_t ld, int32_t P, const float* beta,
                        int32_t B, float* eta, void* work, sglm_stream_t stream);
+
+/* g[k] = X^T R[k] (as sglm_xtr, float64 out) for a 0/1 design given as its identity-row
+ * compacted planes (sglm_compact_bits with rows = NULL, nrows = n): R split into three bf16
+ * pieces (exact products), bf16 MFMA, f32 slabs reduced in float64 in a fixed order.
+ * work: sglm_xtr_bits_work_bytes(P, B, ld). */
+size_t sglm_xtr_bits_work_bytes(int32_t P, int32_t B, int64_t ld);
+int sglm_xtr_bits(const uint32_t* cbits, int64_t ld, int32_t P, int64_t n, const float* R,
+                  int32_t B, double* G, void* work, sglm_stream_t stream);
 
 /* Development entries: a specific bf16 Gram variant (1 = register-staged, 2 = LDS-DMA
  * staged; sglm_syrk uses the default), same arguments as sglm_syrk. */

@@ -142,6 +142,124 @@ eta_bits_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
         }
 }
 
+// ---------------------------------------------------------------------------------------
+// g = X^T R (the gradient, sklearn _linear_loss.py:266-330) on the MFMA for 0/1 designs.
+// A = the design's compacted bit-planes with identity rows ([ld/64][P] uint2, the Gram v6
+// layout, K = rows), B = R split into three bf16 pieces; one wave computes 128 predictors x
+// 32 fits (x 3 pieces) over one split-K slab of rows; slabs are reduced in float64 in a
+// fixed order.
+struct StepX {
+    u32x2 a[4];          // predictor bits of the 4 tiles, one 64-row block
+    u32x4 b[3][4];       // piece x sub-step: 8 bf16 of this lane's fit
+};
+
+__device__ __forceinline__ void loadX(StepX& t, g_uint2* pa, g_uint4* pb, int32_t P,
+                                      int64_t pstride, int64_t s) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) t.a[m] = gld2(pa + s * P + 32 * m);
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) t.b[pc][ks] = gld4(pb + pc * pstride + s * 8 + 2 * ks);
+}
+
+__device__ __forceinline__ void waitX(StepX& t) {
+    asm volatile("s_waitcnt vmcnt(0)"
+                 : "+v"(t.a[0]), "+v"(t.a[1]), "+v"(t.a[2]), "+v"(t.a[3]), "+v"(t.b[0][0]),
+                   "+v"(t.b[0][1]), "+v"(t.b[0][2]), "+v"(t.b[0][3]), "+v"(t.b[1][0]),
+                   "+v"(t.b[1][1]), "+v"(t.b[1][2]), "+v"(t.b[1][3]), "+v"(t.b[2][0]),
+                   "+v"(t.b[2][1]), "+v"(t.b[2][2]), "+v"(t.b[2][3])
+                 :
+                 : "memory");
+}
+
+__device__ __forceinline__ void mmaX(const StepX& t, int h, f32x16 (&acc)[4][3]) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+        bf16x8 ax[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) ax[m] = frag_two(t.a[m], ks, h);
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc) {
+            const bf16x8 b = __builtin_bit_cast(bf16x8, t.b[pc][ks]);
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+                acc[m][pc] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ax[m], b, acc[m][pc], 0, 0, 0);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
+xtr_bits_kernel(const u32x2* __restrict__ cbits, int64_t ld, int32_t P, int64_t nblk,
+                const __bf16* __restrict__ Rp, int32_t Bp, int32_t B, int32_t splits,
+                float* __restrict__ part) {
+    const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
+    const int pb = blockIdx.x, g = blockIdx.y, z = blockIdx.z;
+    const int64_t sps = (nblk + splits - 1) / splits;
+    const int64_t blk0 = (int64_t)z * sps;
+    const int64_t blk1 = min(blk0 + sps, nblk);
+    const int nsteps = blk1 > blk0 ? (int)(blk1 - blk0) : 0;
+    g_uint2* pa = as_global<g_uint2>(cbits + blk0 * P + pb * 128 + r);
+    g_uint4* pbp = as_global<g_uint4>(Rp + (int64_t)(g * 32 + r) * ld + blk0 * 64 + 8 * h);
+    const int64_t pstride = (int64_t)Bp * ld / 8;
+
+    f32x16 acc[4][3];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc) acc[m][pc] = (f32x16){};
+
+    if (nsteps > 0) {
+        StepX A, Bs;
+        loadX(A, pa, pbp, P, pstride, 0);
+        waitX(A);
+        int s = 0;
+        for (; s + 1 < nsteps; s += 2) {
+            loadX(Bs, pa, pbp, P, pstride, s + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            mmaX(A, h, acc);
+            __builtin_amdgcn_sched_barrier(0);
+            waitX(Bs);
+            loadX(A, pa, pbp, P, pstride, s + 2 < nsteps ? s + 2 : nsteps - 1);
+            __builtin_amdgcn_sched_barrier(0);
+            mmaX(Bs, h, acc);
+            __builtin_amdgcn_sched_barrier(0);
+            waitX(A);
+        }
+        if (s < nsteps) mmaX(A, h, acc);
+    }
+    // D[row = predictor][col = fit piece]: lane r = fit, reg j -> predictor (j&3)+8(j>>2)+4h
+    const int f = g * 32 + r;
+    if (f < B) {
+        float* out = part + ((int64_t)z * B + f) * P + pb * 128;
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                out[m * 32 + (j & 3) + 8 * (j >> 2) + 4 * h] =
+                    0.5f * ((acc[m][0][j] + acc[m][1][j]) + acc[m][2][j]);
+    }
+}
+
+__global__ void __launch_bounds__(256) reduce_slabs_f64(const float* __restrict__ part,
+                                                        int64_t len, int32_t nz,
+                                                        double* __restrict__ out) {
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < len;
+         e += (int64_t)gridDim.x * 256) {
+        double s = 0.0;
+        for (int z = 0; z < nz; ++z) s += (double)part[(int64_t)z * len + e];
+        out[e] = s;
+    }
+}
+
+static int xtr_bits_splits(int32_t P, int32_t B, int64_t nblk) {
+    const int tiles = (P / 128) * ((B + 31) / 32);
+    int s = (2048 + tiles - 1) / tiles;
+    const int64_t cap = nblk / 32 > 1 ? nblk / 32 : 1;      // >= 32 K-steps per slab
+    if (s > cap) s = (int)cap;
+    return s < 1 ? 1 : s;
+}
+
 }  // namespace sglm
 
 using namespace sglm;
@@ -183,6 +301,42 @@ int sglm_gemv_eta_bits(const uint32_t* rbits, int64_t ld, int32_t P, const float
     eta_bits_kernel<<<dim3((unsigned)(ld / 128), (unsigned)(Bp / 32)), 64, 0, s>>>(
         reinterpret_cast<const u32x2*>(rbits), ld, P, Dp, Bp, B, eta);
     return check_launch("eta_bits_kernel");
+}
+
+size_t sglm_xtr_bits_work_bytes(int32_t P, int32_t B, int64_t ld) {
+    const int64_t Bp = ((int64_t)B + 31) / 32 * 32;
+    const int64_t nblk = ld / 64;
+    const int splits = xtr_bits_splits(P, B, nblk);
+    return (size_t)3 * Bp * ld * 2 + (size_t)splits * B * P * sizeof(float);
+}
+
+int sglm_xtr_bits(const uint32_t* cbits, int64_t ld, int32_t P, int64_t n, const float* R,
+                  int32_t B, double* G, void* work, sglm_stream_t stream) {
+    if (B <= 0) return SGLM_OK;
+    if (!cbits || !R || !G || !work || ld % 256 || P % 256 || n > ld) {
+        set_error("sglm_xtr_bits: bad args");
+        return SGLM_EINVAL;
+    }
+    const int32_t Bp = (B + 31) / 32 * 32;
+    const int64_t nblk = (n + 63) / 64;
+    const int splits = xtr_bits_splits(P, B, ld / 64);
+    hipStream_t s = as_stream(stream);
+    __bf16* Rp = reinterpret_cast<__bf16*>(work);
+    float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(work) + (size_t)3 * Bp * ld * 2);
+    const int64_t total = (int64_t)Bp * ld;
+    split3_kernel<<<(unsigned)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192), 256, 0,
+                    s>>>(R, ld, B, Bp, Rp);
+    int st = check_launch("split3_kernel");
+    if (st) return st;
+    xtr_bits_kernel<<<dim3((unsigned)(P / 128), (unsigned)(Bp / 32), (unsigned)splits), 64, 0,
+                      s>>>(reinterpret_cast<const u32x2*>(cbits), ld, P, nblk, Rp, Bp, B, splits,
+                           part);
+    st = check_launch("xtr_bits_kernel");
+    if (st) return st;
+    const int64_t len = (int64_t)B * P;
+    reduce_slabs_f64<<<(unsigned)((len + 255) / 256 < 4096 ? (len + 255) / 256 : 4096), 256, 0,
+                       s>>>(part, len, splits, G);
+    return check_launch("reduce_slabs_f64");
 }
 
 }  // extern "C"

@@ -870,27 +870,34 @@ __device__ __forceinline__ void frags6(const Step6& t, int ks, int h, Frag6& f) 
     }
 }
 
+// 16 MFMAs of one sub-step; a diagonal block (DIAG) skips its 6 strictly-lower 32 x 32
+// tiles (never read: consumers use block row <= block col, element row <= col)
+template <bool DIAG>
 __device__ __forceinline__ void mfma16(const Frag6& f, f32x16 (&acc)[4][4]) {
 #pragma unroll
     for (int m = 0; m < 4; ++m)
 #pragma unroll
         for (int n = 0; n < 4; ++n)
-            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[m], f.b[n], acc[m][n], 0, 0, 0);
+            if (!DIAG || m <= n)
+                acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[m], f.b[n], acc[m][n],
+                                                                    0, 0, 0);
 }
 
-// one scheduling region: 16 MFMAs of the current fragments, each followed by 5 of the 80
-// VALU that build the next sub-step's fragments
+// one scheduling region: the sub-step's MFMAs, each followed by its share of the 80 VALU
+// that build the next sub-step's fragments (16 x 5, or 10 x 8 for a diagonal block)
+template <bool DIAG>
 __device__ __forceinline__ void interleave16() {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
+    for (int i = 0; i < (DIAG ? 10 : 16); ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);     // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);     // VALU
+        __builtin_amdgcn_sched_group_barrier(0x002, DIAG ? 8 : 5, 0);     // VALU
     }
     __builtin_amdgcn_sched_barrier(0);
 }
 
 // K-step held in `cur` (its sub-step 0 fragments already in F); loads step `snext` into
 // `nxt` first and leaves F = sub-step 0 fragments of `nxt`.
+template <bool DIAG>
 __device__ __forceinline__ void half6(const Step6& cur, Step6& nxt, Frag6& F, int h,
                                       f32x16 (&acc)[4][4], g_uint2* pa, g_uint2* pb,
                                       g_uint4* pw, int64_t snext, int32_t P) {
@@ -898,25 +905,49 @@ __device__ __forceinline__ void half6(const Step6& cur, Step6& nxt, Frag6& F, in
     __builtin_amdgcn_sched_barrier(0);
     Frag6 G;
     frags6(cur, 1, h, G);
-    mfma16(F, acc);
-    interleave16();
+    mfma16<DIAG>(F, acc);
+    interleave16<DIAG>();
     frags6(cur, 2, h, F);
-    mfma16(G, acc);
-    interleave16();
+    mfma16<DIAG>(G, acc);
+    interleave16<DIAG>();
     frags6(cur, 3, h, G);
-    mfma16(F, acc);
-    interleave16();
+    mfma16<DIAG>(F, acc);
+    interleave16<DIAG>();
     wait6(nxt);
     frags6(nxt, 0, h, F);
-    mfma16(G, acc);
-    interleave16();
+    mfma16<DIAG>(G, acc);
+    interleave16<DIAG>();
 }
 
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) syrk6_kernel(const int64_t* __restrict__ desc, int32_t P,
-                                                   int32_t splits,
-                                                   const int32_t* __restrict__ fits,
-                                                   int32_t nunits, float* __restrict__ H,
-                                                   float* __restrict__ slab, int32_t nact) {
+template <bool DIAG>
+__device__ __forceinline__ void gram6_loop(f32x16 (&acc)[4][4], g_uint2* pa, g_uint2* pb,
+                                           g_uint4* pw, int nsteps, int h, int32_t P) {
+    Step6 A, B;                                      // two register sets, one step in flight
+    Frag6 F;
+    load6(A, pa, pb, pw, 0, P);
+    wait6(A);
+    frags6(A, 0, h, F);
+    int s = 0;
+    for (; s + 1 < nsteps; s += 2) {
+        half6<DIAG>(A, B, F, h, acc, pa, pb, pw, s + 1, P);
+        half6<DIAG>(B, A, F, h, acc, pa, pb, pw, s + 2 < nsteps ? s + 2 : nsteps - 1, P);
+    }
+    if (s < nsteps) {                                // odd step count: last step from A
+        Frag6 G;
+        frags6(A, 1, h, G);
+        mfma16<DIAG>(F, acc);
+        frags6(A, 2, h, F);
+        mfma16<DIAG>(G, acc);
+        frags6(A, 3, h, G);
+        mfma16<DIAG>(F, acc);
+        mfma16<DIAG>(G, acc);
+    }
+}
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
+syrk6_kernel(const int64_t* __restrict__ desc, int32_t P, int32_t splits,
+             const int32_t* __restrict__ fits, int32_t nunits, float* __restrict__ H,
+             float* __restrict__ slab, int32_t nact) {
     const int unit = blockIdx.x % nunits;
     const int slot = blockIdx.x / nunits;
     const int split = blockIdx.y;
@@ -944,26 +975,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
         for (int n = 0; n < 4; ++n) acc[m][n] = (f32x16){};
 
     if (nsteps > 0) {
-        Step6 A, B;                                  // two register sets, one step in flight
-        Frag6 F;
-        load6(A, pa, pb, pw, 0, P);
-        wait6(A);
-        frags6(A, 0, h, F);
-        int s = 0;
-        for (; s + 1 < nsteps; s += 2) {
-            half6(A, B, F, h, acc, pa, pb, pw, s + 1, P);
-            half6(B, A, F, h, acc, pa, pb, pw, s + 2 < nsteps ? s + 2 : nsteps - 1, P);
-        }
-        if (s < nsteps) {                            // odd step count: last step from A
-            Frag6 G;
-            frags6(A, 1, h, G);
-            mfma16(F, acc);
-            frags6(A, 2, h, F);
-            mfma16(G, acc);
-            frags6(A, 3, h, G);
-            mfma16(F, acc);
-            mfma16(G, acc);
-        }
+        if (bi == bj)
+            gram6_loop<true>(acc, pa, pb, pw, nsteps, h, P);
+        else
+            gram6_loop<false>(acc, pa, pb, pw, nsteps, h, P);
     }
     float* out = slab ? slab + ((int64_t)split * nact + slot) * (int64_t)P * P
                       : H + (int64_t)fit * P * P;
@@ -1022,6 +1037,32 @@ __global__ void __launch_bounds__(256) pack_bits_rows_kernel(
     }
 }
 
+// Same output as pack_bits_rows_kernel, gathered from the column-packed bit-planes of
+// sglm_pack_bits (bit b of word q of predictor a = row 32q + b): 256 MB of source instead of
+// the 4 GB bf16 design, so building a fold's compacted design is L2/Infinity-Cache bound.
+__global__ void __launch_bounds__(256) compact_bits_kernel(
+    const uint32_t* __restrict__ xbits, int64_t ld, int32_t P, const int32_t* __restrict__ rows,
+    int64_t nrows, uint2* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wid = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+    const int64_t nblk = (nrows + 63) / 64;
+    const int64_t total = nblk * P;
+    const int64_t wpc = ld / 32;
+    const int src = (lane & 32) | frag_bit_source(lane & 31);
+    for (int64_t g = wid; g < total; g += ((int64_t)gridDim.x * 256) >> 6) {
+        const int64_t blk = g / P, a = g % P;
+        const int64_t k = blk * 64 + lane;
+        int one = 0;
+        if (k < nrows) {
+            const int64_t row = rows ? (int64_t)rows[k] : k;
+            one = (xbits[a * wpc + (row >> 5)] >> (row & 31)) & 1;
+        }
+        const int mine = __shfl(one, src, 64);
+        const unsigned long long m = __ballot(mine);
+        if (lane == 0) out[g] = make_uint2((uint32_t)m, (uint32_t)(m >> 32));
+    }
+}
+
 // compact bf16 weights: wbf(slot)[k] = bf16(W[fits[slot]][row(k)]) for k < rows, 0 to pad 64
 __global__ void __launch_bounds__(256) gather_w_kernel(const float* __restrict__ W, int64_t ld,
                                                        const int32_t* __restrict__ fits,
@@ -1050,6 +1091,19 @@ extern "C" int sglm_pack_bits_rows(const uint16_t* Xb, int64_t ld, int32_t P, co
     pack_bits_rows_kernel<<<4096, 256, 0, as_stream(stream)>>>(
         Xb, ld, P, rows, nrows, reinterpret_cast<uint2*>(out), nonbinary);
     return check_launch("pack_bits_rows_kernel");
+}
+
+extern "C" int sglm_compact_bits(const uint32_t* xbits, int64_t ld, int32_t P,
+                                 const int32_t* rows, int64_t nrows, uint32_t* out,
+                                 sglm_stream_t stream) {
+    if (!xbits || !out || nrows < 0 || ld % 64 || (!rows && nrows > ld)) {
+        set_error("sglm_compact_bits: bad args");
+        return SGLM_EINVAL;
+    }
+    if (nrows == 0) return SGLM_OK;
+    compact_bits_kernel<<<8192, 256, 0, as_stream(stream)>>>(xbits, ld, P, rows, nrows,
+                                                              reinterpret_cast<uint2*>(out));
+    return check_launch("compact_bits_kernel");
 }
 
 extern "C" int sglm_gather_w(const float* W, int64_t ld, const int32_t* fits, int32_t nact,

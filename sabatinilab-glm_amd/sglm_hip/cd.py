@@ -29,8 +29,7 @@ def enet_batch(prob: E.Problem, objectives, reqs):
     bf.eta.zero_()
     _lib.call("sglm_link_update", E.FAM_SQUARED, 0.0, n, ld, B, E._p(bf.eta), E._p(prob.Y),
               E._p(prob.M), E._p(fit_resp), E._p(fit_mask), E._p(bf.W), E._p(bf.R), st)
-    work = E._work(_lib.query("sglm_xtr_work_bytes", P, B, n), dev)
-    _lib.call("sglm_xtr", E._p(d.xg), d.xtype, ld, P, n, E._p(bf.R), B, E._p(bf.g), E._p(work), st)
+    d.xtr(bf.R, B, bf.g)
     c = -bf.g                                            # X^T (m y)
     # one Gram per distinct mask (W = mask), copied to every fit that uses it
     reps = {}

@@ -44,6 +44,7 @@ COL_PAD = 256
 ROW_PAD = 256
 ARMIJO_SIGMA = 2.0 ** -11      # sklearn _newton_solver.py:214
 SYRK_BITS = True               # use the bit-plane Gram (v3) for 0/1 designs
+XTR_BITS = True                # X^T R on the MFMA from compacted bit-planes for 0/1 designs
 ETA_BITS = True                # eta on the MFMA from row-major bit-planes for 0/1 designs
 SYRK_CBITS = True              # ... and its row-compacted register-only form (v6) when fits
                                # carry masks (the default path for event designs)
@@ -87,6 +88,7 @@ class Design:
         self.xf = None
         self.xbits = None      # uint32 bit-planes [P, ld/32] when the design is 0/1
         self.rbits = None      # row-major bit-planes [P/64][ld] x uint2 (MFMA eta) when 0/1
+        self._cbits = None     # identity-row compacted planes [n/64][P] x uint2 (MFMA X^T R)
         self.device = device
 
     @property
@@ -195,6 +197,29 @@ class Design:
             d.xf[p, :n] = 1.0
         return d
 
+    def cbits_full(self):
+        """Compacted bit-planes of all n rows (Gram v6 layout, K = rows): the A operand of
+        the MFMA gradient and the Gram of full-data fits.  Built once per design."""
+        if self._cbits is None and self.xbits is not None:
+            self._cbits = torch.empty(max(1, (self.n + 63) // 64) * self.P * 2,
+                                      dtype=torch.int32, device=self.device)
+            _lib.call("sglm_compact_bits", _p(self.xbits), self.ld, self.P, None, self.n,
+                      _p(self._cbits), _stream())
+        return self._cbits
+
+    def xtr(self, R, B, g_out, work=None):
+        """g_out[k] (float64) = X^T R[k] for k < B (R: [B][ld] f32 device)."""
+        st = _stream()
+        if self.xbits is not None and XTR_BITS:
+            w = _work(_lib.query("sglm_xtr_bits_work_bytes", self.P, B, self.ld), self.device,
+                      "xtr")
+            _lib.call("sglm_xtr_bits", _p(self.cbits_full()), self.ld, self.P, self.n, _p(R), B,
+                      _p(g_out), _p(w), st)
+        else:
+            w = _work(_lib.query("sglm_xtr_work_bytes", self.P, B, self.n), self.device, "xtr")
+            _lib.call("sglm_xtr", _p(self.xg), self.xtype, self.ld, self.P, self.n, _p(R), B,
+                      _p(g_out), _p(w), st)
+
     def eta(self, beta_dev, out=None):
         """eta[k] = X beta[k] for a (B, P) f32 device tensor."""
         B = beta_dev.shape[0]
@@ -279,11 +304,18 @@ class Problem:
             rows = np.flatnonzero(self.masks[mask] > 0).astype(np.int32)
             nr = int(rows.size)
             rows_d = None if nr == d.n else torch.from_numpy(rows).to(d.device)
+            if rows_d is None and d.xbits is not None:
+                c = self._compact[mask] = (d.cbits_full(), nr, None)
+                return c
             bits = torch.empty(max(1, (nr + 63) // 64) * d.P * 2, dtype=torch.int32,
                                device=d.device)
-            flag = torch.zeros(1, dtype=torch.int32, device=d.device)
-            _lib.call("sglm_pack_bits_rows", _p(d.xb), d.ld, d.P, _p(rows_d), nr, _p(bits),
-                      _p(flag), _stream())
+            if d.xbits is not None:
+                _lib.call("sglm_compact_bits", _p(d.xbits), d.ld, d.P, _p(rows_d), nr,
+                          _p(bits), _stream())
+            else:
+                flag = torch.zeros(1, dtype=torch.int32, device=d.device)
+                _lib.call("sglm_pack_bits_rows", _p(d.xb), d.ld, d.P, _p(rows_d), nr, _p(bits),
+                          _p(flag), _stream())
             c = (bits, nr, rows_d)
             self._compact[mask] = c
         return c
@@ -398,6 +430,22 @@ def syrk_splits(n_tiles_total: int, nsteps: int, cus: int = 256) -> int:
     return best
 
 
+def syrk6_splits(wgs1: int, nsteps: int, nact: int, P: int, slots: int = 1024) -> int:
+    """Split-K factor for Gram v6: minimise (rounds of one-wave workgroups) x (workgroup
+    time) + the split-K slab traffic (write + reduce-read of splits x nact x P^2 floats)."""
+    t_step = 2048 / 2.4e9                     # 64 MFMA x 32 cycles per K-step
+    best, best_t = 1, None
+    for s in (1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64):
+        if s > max(1, nsteps // 8):
+            break
+        t = math.ceil(wgs1 * s / slots) * math.ceil(nsteps / s) * t_step
+        if s > 1:
+            t += s * nact * P * P * 8.0 / 4e12
+        if best_t is None or t < best_t:
+            best, best_t = s, t
+    return best
+
+
 def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[IrlsStats] = None):
     """Run the batched damped-Newton (IRLS) solve; returns (results, final eta tensor)."""
     require_gpu()
@@ -466,8 +514,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
             break
         _lib.call("sglm_link_update", fam, power, n, ld, B, _p(bf.eta), _p(prob.Y), _p(prob.M),
                   _p(fit_resp), _p(fit_mask), _p(bf.W), _p(bf.R), st)
-        _lib.call("sglm_xtr", _p(d.xg), d.xtype, ld, P, n, _p(bf.R), B, _p(bf.g),
-                  _p(xtr_work), st)
+        d.xtr(bf.R, B, bf.g)
         g = bf.g.cpu().numpy() + lam[:, None] * penal * beta
         t0 = tick("it_gradient", t0)
         # ---- Hessian
@@ -647,7 +694,7 @@ def _syrk_cbits(d: Design, bf, prob: Problem, fits: np.ndarray, st, ev=None):
     desc_d = torch.from_numpy(desc).to(d.device)
     fits_d = torch.from_numpy(fits.astype(np.int32)).to(d.device)
     nb = d.P // 128
-    splits = syrk_splits(nb * (nb + 1) // 2 * nact, max(1, maxrows // 64), cus=1024)
+    splits = syrk6_splits(nb * (nb + 1) // 2 * nact, max(1, (maxrows + 63) // 64), nact, d.P)
     wb = _lib.query("sglm_syrk_work_bytes", d.P, nact, splits)
     work = _work(wb, d.device) if wb else None
     _lib.call("sglm_gather_w", _p(bf.W), d.ld, _p(fits_d), nact, _p(desc_d), maxrows, st)

@@ -386,7 +386,7 @@ def test_syrk_cbits_compacted_gram(engine, torch_mod):
     _lib.call("sglm_gather_w", W.data_ptr(), d.ld, fits.data_ptr(), B, desc.data_ptr(), nr_max, 0)
     Xh = d.xb.double().cpu().numpy()[:, : s.N]
     Wb = W.to(torch.bfloat16).double().cpu().numpy()[:, : s.N]
-    blk = (np.arange(d.P)[:, None] // 128) <= (np.arange(d.P)[None, :] // 128)
+    blk = np.triu(np.ones((d.P, d.P), dtype=bool))         # what the consumers read
     Href = torch.zeros((1, d.P, d.P), dtype=torch.float32, device="cuda")
     wk1 = torch.empty(16, dtype=torch.uint8, device="cuda")
     _lib.call("sglm_syrk_variant", 2, d.xb.data_ptr(), d.ld, d.P, d.n, W.data_ptr(),
@@ -437,3 +437,55 @@ def test_eta_bits_matches_float64(engine, torch_mod):
     assert np.max(np.abs(got - ref) / np.maximum(scale, 1e-30)) < 2e-6
     assert not got[:, s.N + 1:].any()                     # padding rows are exactly 0
     assert np.max(np.abs(got - ref_valu.cpu().numpy()) / np.maximum(scale, 1e-30)) < 2e-6
+
+
+def test_compact_bits_equals_pack_bits_rows(engine, torch_mod):
+    """Compaction from the 1-bit planes == compaction from the bf16 design, bit for bit."""
+    torch = torch_mod
+    from sglm_hip import _lib, synth
+    s = synth.make(N=9000, m=9, L=3, rho=0.15, seed=51)
+    d = engine.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
+    rng = np.random.default_rng(52)
+    for rows in (np.sort(rng.choice(s.N, 4321, replace=False)).astype(np.int32), None):
+        nr = 4321 if rows is not None else s.N
+        rows_d = None if rows is None else torch.from_numpy(rows).cuda()
+        size = ((nr + 63) // 64) * d.P * 2
+        a = torch.zeros(size, dtype=torch.int32, device="cuda")
+        b = torch.ones(size, dtype=torch.int32, device="cuda")
+        flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+        rp = None if rows_d is None else rows_d.data_ptr()
+        _lib.call("sglm_pack_bits_rows", d.xb.data_ptr(), d.ld, d.P, rp, nr, a.data_ptr(),
+                  flag.data_ptr(), 0)
+        _lib.call("sglm_compact_bits", d.xbits.data_ptr(), d.ld, d.P, rp, nr, b.data_ptr(), 0)
+        torch.cuda.synchronize()
+        assert torch.equal(a, b)
+
+
+def test_xtr_bits_matches_float64(engine, torch_mod):
+    """MFMA gradient X^T R from compacted bit-planes (R split in 3 bf16 pieces) == float64
+    X^T R to f32 accuracy, ragged B; also matches the f32-MFMA sglm_xtr."""
+    torch = torch_mod
+    from sglm_hip import _lib, synth
+    s = synth.make(N=30000, m=11, L=4, rho=0.1, seed=61)
+    d = engine.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
+    rng = np.random.default_rng(62)
+    B = 45
+    R = np.zeros((B, d.ld), np.float32)
+    R[:, : s.N] = (rng.standard_normal((B, s.N)) * np.exp(rng.uniform(-6, 3, (B, 1)))).astype(np.float32)
+    Rd = torch.from_numpy(R).cuda()
+    G = torch.zeros((B, d.P), dtype=torch.float64, device="cuda")
+    w = torch.empty(_lib.query("sglm_xtr_bits_work_bytes", d.P, B, d.ld), dtype=torch.uint8,
+                    device="cuda")
+    _lib.call("sglm_xtr_bits", d.cbits_full().data_ptr(), d.ld, d.P, d.n, Rd.data_ptr(), B,
+              G.data_ptr(), w.data_ptr(), 0)
+    G2 = torch.zeros_like(G)
+    w2 = torch.empty(_lib.query("sglm_xtr_work_bytes", d.P, B, d.n), dtype=torch.uint8,
+                     device="cuda")
+    _lib.call("sglm_xtr", d.xb.data_ptr(), 0, d.ld, d.P, d.n, Rd.data_ptr(), B, G2.data_ptr(),
+              w2.data_ptr(), 0)
+    X = d.xb.double().cpu().numpy()
+    ref = R.astype(np.float64) @ X.T                      # (B, P)
+    scale = np.abs(R.astype(np.float64)) @ np.abs(X.T)
+    got = G.cpu().numpy()
+    assert np.max(np.abs(got - ref) / np.maximum(scale, 1e-30)) < 2e-6
+    assert np.max(np.abs(got - G2.cpu().numpy()) / np.maximum(scale, 1e-30)) < 4e-6
