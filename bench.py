@@ -44,11 +44,11 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--cpu-rows", type=int, default=50_000)
+    ap.add_argument("--cpu-rows", type=int, default=300_000)
     return ap.parse_args()
 
 
-def cpu_baseline(s, n_rows_unit, rows):
+def cpu_baseline(s, n_rows_unit, rows, fit_iters_per_grid):
     """Oracle (float64 numpy/LAPACK damped Newton) on a bounded slice of the same design."""
     from oracle import glm_ref
     try:
@@ -70,10 +70,10 @@ def cpu_baseline(s, n_rows_unit, rows):
     per_iter_unit = dt / max(iters, 1) * (n_rows_unit / rows)
     return {"value": 1.0 / per_iter_unit, "unit": "IRLS fit-iterations/s (1M-row unit)",
             "cores": int(cores), "kind": "port",
-            "sample": f"oracle fp64 damped Newton, Poisson alpha=1e-2, {rows}x{s.p} slice of the "
-                      f"C4 design, {iters} iterations in {dt:.2f} s, per-iteration time scaled "
-                      f"x{n_rows_unit / rows:.0f} to 1M rows",
-            "grid_wall_s_extrapolated": None}
+            "sample": f"oracle fp64 damped Newton (numpy/LAPACK), Poisson alpha=1e-2, {rows}x{s.p} "
+                      f"slice of the C4 design, {iters} iterations in {dt:.2f} s; per-iteration "
+                      f"time scaled x{n_rows_unit / rows:.2f} to 1M rows",
+            "grid_wall_s_extrapolated": fit_iters_per_grid * per_iter_unit}
 
 
 def main():
@@ -141,7 +141,7 @@ def main():
         achieved = kflop / ktime / 1e12 if ktime > 0 else 0.0
         cpu = None
         if not a.no_cpu and world == 1:
-            cpu = cpu_baseline(s, 1_000_000, a.cpu_rows)
+            cpu = cpu_baseline(s, s.N, a.cpu_rows, fit_iters / a.steps)
         out = {
             "metric": "IRLS iters/sec on 1M×2000 design mat; CV-grid wall-clock (5-fold×20 λ)",
             "value": fit_iters / elapsed,

@@ -1043,23 +1043,35 @@ __global__ void __launch_bounds__(256) pack_bits_rows_kernel(
 __global__ void __launch_bounds__(256) compact_bits_kernel(
     const uint32_t* __restrict__ xbits, int64_t ld, int32_t P, const int32_t* __restrict__ rows,
     int64_t nrows, uint2* __restrict__ out) {
+    // one wave per (64-row output block, 32 predictors): the row index is loaded once and the
+    // 32 predictor words are gathered with 8 loads in flight per lane
     const int lane = threadIdx.x & 63;
     const int64_t wid = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
     const int64_t nblk = (nrows + 63) / 64;
-    const int64_t total = nblk * P;
+    const int64_t pg = P / 32;
+    const int64_t total = nblk * pg;
     const int64_t wpc = ld / 32;
     const int src = (lane & 32) | frag_bit_source(lane & 31);
     for (int64_t g = wid; g < total; g += ((int64_t)gridDim.x * 256) >> 6) {
-        const int64_t blk = g / P, a = g % P;
+        const int64_t blk = g / pg, a0 = (g % pg) * 32;
         const int64_t k = blk * 64 + lane;
-        int one = 0;
-        if (k < nrows) {
-            const int64_t row = rows ? (int64_t)rows[k] : k;
-            one = (xbits[a * wpc + (row >> 5)] >> (row & 31)) & 1;
+        const bool valid = k < nrows;
+        const int64_t row = valid ? (rows ? (int64_t)rows[k] : k) : 0;
+        const uint32_t* base = xbits + a0 * wpc + (row >> 5);
+        const int sh = (int)(row & 31);
+        for (int a8 = 0; a8 < 32; a8 += 8) {
+            uint32_t w[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) w[u] = base[(int64_t)(a8 + u) * wpc];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int one = valid ? (int)((w[u] >> sh) & 1u) : 0;
+                const int mine = __shfl(one, src, 64);
+                const unsigned long long m = __ballot(mine);
+                if (lane == 0)
+                    out[blk * P + a0 + a8 + u] = make_uint2((uint32_t)m, (uint32_t)(m >> 32));
+            }
         }
-        const int mine = __shfl(one, src, 64);
-        const unsigned long long m = __ballot(mine);
-        if (lane == 0) out[g] = make_uint2((uint32_t)m, (uint32_t)(m >> 32));
     }
 }
 
@@ -1101,7 +1113,11 @@ extern "C" int sglm_compact_bits(const uint32_t* xbits, int64_t ld, int32_t P,
         return SGLM_EINVAL;
     }
     if (nrows == 0) return SGLM_OK;
-    compact_bits_kernel<<<8192, 256, 0, as_stream(stream)>>>(xbits, ld, P, rows, nrows,
+    if (P % 32) {
+        set_error("sglm_compact_bits: P must be a multiple of 32");
+        return SGLM_EINVAL;
+    }
+    compact_bits_kernel<<<4096, 256, 0, as_stream(stream)>>>(xbits, ld, P, rows, nrows,
                                                               reinterpret_cast<uint2*>(out));
     return check_launch("compact_bits_kernel");
 }

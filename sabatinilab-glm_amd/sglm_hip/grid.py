@@ -42,7 +42,10 @@ class _MaskStats:
         self.Md = prob.M[:, :n].to(torch.float64)                      # F x n multiplicities
         self.Yd = torch.from_numpy(np.stack(prob.ys)).to(dev)           # R x n float64
         cnt = self.Md.sum(1)
-        sy = self.Md @ self.Yd.T                                        # F x R
+        # elementwise row sums, not a matmul: an F x n x R float64 GEMM with R ~ 1 runs as a
+        # slow library DGEMM
+        sy = torch.stack([(self.Md * self.Yd[r][None, :]).sum(1)
+                          for r in range(self.Yd.shape[0])], dim=1)     # F x R
         mean = torch.where(cnt[:, None] > 0, sy / cnt.clamp_min(1)[:, None], 0.0)
         R = self.Yd.shape[0]
         sst = torch.empty_like(sy)
