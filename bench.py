@@ -76,6 +76,22 @@ def cpu_baseline(s, n_rows_unit, rows, fit_iters_per_grid):
             "grid_wall_s_extrapolated": fit_iters_per_grid * per_iter_unit}
 
 
+def pmc_traffic():
+    """HBM bytes per Gram launch from the newest committed PMC summary (profiles/*_pmc_traffic.json,
+    written by tools/pmc_traffic.py from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this
+    bench's grid; gfx950 corrections applied there).  PMC counters cannot be read in-process."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    dom = d.get("dominant") or {}
+    if "syrk6_kernel" not in dom.get("kernel", ""):
+        return None, None
+    return dom["traffic_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+
+
 def main():
     a = parse()
     import torch
@@ -139,6 +155,7 @@ def main():
     if rank == 0:
         pa = s.p + 1
         achieved = kflop / ktime / 1e12 if ktime > 0 else 0.0
+        traffic, traffic_src = pmc_traffic()
         cpu = None
         if not a.no_cpu and world == 1:
             cpu = cpu_baseline(s, s.N, a.cpu_rows, fit_iters / a.steps)
@@ -174,7 +191,9 @@ def main():
                 "peak": PEAK_BF16_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": achieved / PEAK_BF16_TFLOPS,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_unit": "bytes per launch (HBM/fabric, PMC)",
+                "traffic_source": traffic_src,
                 "algorithmic_flop_per_fit_iter": f"n_train*p'*(p'+1), p'={pa}",
                 "launches": nlaunch,
                 "avg_launch_ms": ktime / max(nlaunch, 1) * 1e3,
