@@ -44,12 +44,28 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--cpu-rows", type=int, default=300_000)
+    ap.add_argument("--cpu-rows", type=int, default=200_000)
+    ap.add_argument("--sklearn-rows", type=int, default=100_000)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL over xGMI) for real runs; gloo to rehearse several ranks "
+                         "on fewer GPUs")
     return ap.parse_args()
 
 
-def cpu_baseline(s, n_rows_unit, rows, fit_iters_per_grid):
-    """Oracle (float64 numpy/LAPACK damped Newton) on a bounded slice of the same design."""
+def dense_slice(s, rows):
+    m = s.E.shape[1]
+    X = np.empty((rows, s.p), dtype=np.float64)
+    r0 = s.L - 1
+    for bi, sh in enumerate(s.shifts):
+        X[:, bi * m:(bi + 1) * m] = s.E[r0 - sh:r0 - sh + rows]
+    return X
+
+
+def cpu_baseline(s, n_rows_unit, rows, fit_iters_per_grid, sk_rows):
+    """Oracle (float64 numpy/LAPACK damped Newton) on a bounded slice of the same design, plus
+    scikit-learn called directly with the estimator the reference selects
+    (TweedieRegressor(power=1), backend/sglm.py:112-115): newton-cholesky (IRLS-equivalent)
+    and the reference's default lbfgs."""
     from oracle import glm_ref
     try:
         from threadpoolctl import threadpool_info
@@ -57,23 +73,47 @@ def cpu_baseline(s, n_rows_unit, rows, fit_iters_per_grid):
     except Exception:  # pragma: no cover
         cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     rows = min(rows, s.N)
-    m = s.E.shape[1]
-    X = np.empty((rows, s.p), dtype=np.float64)
-    r0 = s.L - 1
-    for bi, sh in enumerate(s.shifts):
-        X[:, bi * m:(bi + 1) * m] = s.E[r0 - sh:r0 - sh + rows]
+    X = dense_slice(s, rows)
     y = s.y[:rows]
     t0 = time.perf_counter()
     _, _, iters = glm_ref.fit_tweedie_newton(X, y, 1e-2, 1.0, tol=1e-8, max_iter=50,
                                              return_iters=True)
     dt = time.perf_counter() - t0
     per_iter_unit = dt / max(iters, 1) * (n_rows_unit / rows)
-    return {"value": 1.0 / per_iter_unit, "unit": "IRLS fit-iterations/s (1M-row unit)",
-            "cores": int(cores), "kind": "port",
-            "sample": f"oracle fp64 damped Newton (numpy/LAPACK), Poisson alpha=1e-2, {rows}x{s.p} "
-                      f"slice of the C4 design, {iters} iterations in {dt:.2f} s; per-iteration "
-                      f"time scaled x{n_rows_unit / rows:.2f} to 1M rows",
-            "grid_wall_s_extrapolated": fit_iters_per_grid * per_iter_unit}
+    out = {"value": 1.0 / per_iter_unit, "unit": "IRLS fit-iterations/s (1M-row unit)",
+           "cores": int(cores), "kind": "port",
+           "sample": f"oracle fp64 damped Newton (numpy/LAPACK), Poisson alpha=1e-2, {rows}x{s.p} "
+                     f"slice of the C4 design, {iters} iterations in {dt:.2f} s; per-iteration "
+                     f"time scaled x{n_rows_unit / rows:.2f} to 1M rows",
+           "grid_wall_s_extrapolated": fit_iters_per_grid * per_iter_unit}
+    del X
+    try:
+        import platform
+        from sklearn.linear_model import TweedieRegressor
+        sk_rows = min(sk_rows, s.N)
+        X = dense_slice(s, sk_rows)
+        y = s.y[:sk_rows]
+        model = platform.machine()
+        try:
+            with open("/proc/cpuinfo") as f:
+                model = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
+        except Exception:  # pragma: no cover
+            pass
+        sk = {"rows": sk_rows, "cpu": model, "nproc": os.cpu_count()}
+        for solver in ("newton-cholesky", "lbfgs"):
+            m = TweedieRegressor(power=1.0, alpha=1e-2, link="log", solver=solver, tol=1e-4,
+                                 max_iter=100)
+            t0 = time.perf_counter()
+            m.fit(X, y)
+            dt = time.perf_counter() - t0
+            it = int(m.n_iter_)
+            sk[solver] = {"n_iter": it, "fit_s": dt,
+                          "fit_s_1M_rows": dt * n_rows_unit / sk_rows,
+                          "iters_per_s_1M_rows": it / dt * sk_rows / n_rows_unit}
+        out["sklearn_direct"] = sk
+    except Exception as e:  # pragma: no cover - sklearn is part of the image
+        out["sklearn_direct"] = {"error": repr(e)}
+    return out
 
 
 def pmc_traffic():
@@ -99,9 +139,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    dev = local % max(1, torch.cuda.device_count())   # one rank per GPU; wraps only in rehearsals
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group("gloo")
     from sglm_hip import engine as E, folds, grid, synth
     from sglm_hip.estimators import Objective
 
@@ -139,8 +183,8 @@ def main():
     kflop = sum(nact_flop for _, _, _, nact_flop in stats.syrk_events)
     nlaunch = len(stats.syrk_events)
     t = torch.tensor([elapsed, float(stats.fit_iters), ktime, kflop, float(nlaunch),
-                      float(stats.gram_fits)],
-                     dtype=torch.float64, device="cuda")
+                      float(stats.gram_fits), stats.alg_flop],
+                     dtype=torch.float64, device="cuda" if a.dist_backend == "nccl" else "cpu")
     if world > 1:
         mx = t.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
@@ -148,17 +192,17 @@ def main():
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         elapsed, fit_iters = float(mx[0]), float(sm[1])
         ktime, kflop, nlaunch = float(sm[2]), float(sm[3]), int(sm[4])
-        gram_fits = float(sm[5])
+        gram_fits, alg_flop = float(sm[5]), float(sm[6])
     else:
         fit_iters = float(stats.fit_iters)
-        gram_fits = float(stats.gram_fits)
+        gram_fits, alg_flop = float(stats.gram_fits), stats.alg_flop
     if rank == 0:
         pa = s.p + 1
         achieved = kflop / ktime / 1e12 if ktime > 0 else 0.0
         traffic, traffic_src = pmc_traffic()
         cpu = None
         if not a.no_cpu and world == 1:
-            cpu = cpu_baseline(s, s.N, a.cpu_rows, fit_iters / a.steps)
+            cpu = cpu_baseline(s, s.N, a.cpu_rows, fit_iters / a.steps, a.sklearn_rows)
         out = {
             "metric": "IRLS iters/sec on 1M×2000 design mat; CV-grid wall-clock (5-fold×20 λ)",
             "value": fit_iters / elapsed,
@@ -181,6 +225,10 @@ def main():
                 "grid_wall_s": elapsed / a.steps,
                 "fit_iters_per_grid": fit_iters / a.steps,
                 "distinct_hessians_per_grid": gram_fits / a.steps,
+                "grid_roofline_frac": alg_flop / elapsed / (world * PEAK_BF16_TFLOPS * 1e12),
+                "grid_roofline_note": "SURVEY.md 8(d): sum over fit-iterations of "
+                                      "n p'(p'+1) + 4 n p' + p'^3/3 + 2 p'^2, / wall / "
+                                      "(n_gpus x 2.5 PF)",
                 "setup_s": setup_s,
                 "parallelism": f"fits round-robin over {world} rank(s), RCCL all-gather of results",
             },

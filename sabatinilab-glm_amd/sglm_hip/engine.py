@@ -362,6 +362,7 @@ class IrlsStats:
     fit_iters: int = 0
     newton_iters: int = 0
     gram_fits: int = 0                                  # distinct Hessians formed
+    alg_flop: float = 0.0       # SURVEY.md §8(d) F summed over fit-iterations
     trace_phases: bool = False                          # sync + time grid phases (tools)
     phases: dict = field(default_factory=dict)          # host wall seconds per phase
 
@@ -603,6 +604,10 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         if stats is not None:
             stats.newton_iters += 1
             stats.fit_iters += int(act.size)
+            pa = float(p + 1)
+            nr = rows[act]
+            stats.alg_flop += float(np.sum(nr * pa * (pa + 1) + 4.0 * nr * pa)
+                                    + act.size * (pa ** 3 / 3 + 2 * pa * pa))
         for k in act:
             rel = np.max(np.abs(step[k] * delta[k])) / (1.0 + np.max(np.abs(beta[k])))
             if step[k] == 0.0 or rel <= tol or (rel < 1e-4 and rel >= 0.5 * prev_rel[k]):

@@ -128,8 +128,12 @@ def merge_results(local: dict, dist=None) -> dict:
 
 
 def run(X, y, cv_idx, objectives: Sequence[Objective], rolls: Sequence[int],
-        score_method: str = "mse", coef0=None, intercept0=None, stats=None, shard=True):
-    """Return one result dict per objective (reference key set minus glm_kwargs/model)."""
+        score_method: str = "mse", coef0=None, intercept0=None, stats=None, shard=True,
+        simulate=None):
+    """Return one result dict per objective (reference key set minus glm_kwargs/model).
+
+    ``simulate=(rank, world)`` (development only) solves just that rank's share without a
+    process group and returns the raw per-fit results instead of the assembled dicts."""
     import time
     tick = stats.mark if (stats is not None and stats.trace_phases) else (lambda name, t: t)
     t0 = tick("-", time.perf_counter())
@@ -164,8 +168,8 @@ def run(X, y, cv_idx, objectives: Sequence[Objective], rolls: Sequence[int],
             table.append((j, k, 2 * k, ridx[int(roll)], 2 * k + 1))
         table.append((j, -1, FULL, 0, -1))
     t0 = tick("grid_setup", t0)
-    dist = _dist() if shard else None
-    rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (0, 1)
+    dist = _dist() if shard and simulate is None else None
+    rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (simulate or (0, 1))
     mine = shard_indices(len(table), rank, world)
 
     results = {}
@@ -199,6 +203,8 @@ def run(X, y, cv_idx, objectives: Sequence[Objective], rolls: Sequence[int],
             rr = res[q]
             results[i] = (rr.coef, rr.intercept, rr.n_iter, rr.converged, sums[q])
     t0 = tick("score_sums", t0)
+    if simulate is not None:
+        return results
     results = merge_results(results, dist)
 
     # ---- assemble per-param dicts (reference key order, backend/sglm_cv.py:188-200)

@@ -167,3 +167,34 @@ def test_c2_scale_poisson_parity(engine):
     glm.fit(X, s.y)
     c, b = glm_ref.fit_tweedie_newton(X, s.y, 1e-4, 1.0)
     assert rel(glm.coef_, c) < TOL_POIS
+
+
+def test_c3_shape_poisson_grid_vs_oracle(engine):
+    """C3 shape: Poisson 100k x 500 timeshifted design, 5 GroupShuffleSplit splits on trial
+    ids (seed 3), 3 lambdas of the logspace(-4, 1, 20) grid, r2 (D^2) scoring — every fold
+    fit, refit, score and the pooled R^2 against the float64 oracle; folds bit-exact."""
+    import sglm_cv
+    import sglm_ez
+    from sglm_hip import synth
+    s = synth.make(N=100_000, m=25, L=10, family="poisson", rho=0.02, seed=0)
+    X = s.dense_X()
+    np.random.seed(3)
+    df = pd.DataFrame({"nTrial": s.trial})
+    cv_idx = sglm_ez.cv_idx_by_trial_id(df, trial_id_columns=["nTrial"], num_folds=5)
+    np.random.seed(3)
+    ref_idx = folds_ref.cv_idx_from_bucket_ids(folds_ref.trial_bucket_codes([s.trial]), num_folds=5)
+    for (a, b), (c, d) in zip(cv_idx, ref_idx):
+        assert np.array_equal(a, c) and np.array_equal(b, d)
+    alphas = [float(v) for v in np.logspace(-4, 1, 20)[[0, 10, 19]]]
+    kws = sglm_cv.generate_mult_params({"alpha": alphas}, {"model_name": "Poisson"})
+    ref_kws = [dict(k) for k in kws]
+    out = sglm_cv.cv_glm_mult_params(X, s.y, cv_idx, "Normal", kws, score_method="r2")
+    ref = cv_ref.cv_mult(X, s.y, cv_idx, ref_kws, score_method="r2")
+    for r, q in zip(out["full_cv_results"], ref["full_cv_results"]):
+        assert rel(r["cv_coefs"], q["cv_coefs"]) < TOL_POIS, r["glm_kwargs"]
+        assert rel(r["cv_intercepts"], q["cv_intercepts"]) < TOL_POIS
+        assert np.max(np.abs(r["cv_scores_test"] - q["cv_scores_test"])) < 1e-6
+        assert np.max(np.abs(r["cv_scores_train"] - q["cv_scores_train"])) < 1e-6
+        assert abs(r["cv_R2_score"] - q["cv_R2_score"]) < 1e-6
+        assert rel(r["model"].coef_, q["coef"]) < TOL_POIS
+    assert out["best_params"] == ref["best_params"]

@@ -1,0 +1,56 @@
+"""Per-rank cost of an N-GPU C4 grid, simulated on one GPU (development tool).
+
+python tools/rank_sim.py --world 8 : solves rank 0's share (fits i % 8 == 0) of the C4 grid
+after a warm-up, with device syncs at phase boundaries, and prints the phase breakdown.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "sabatinilab-glm_amd")]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c4")
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--rank", type=int, default=0)
+    a = ap.parse_args()
+    import bench
+    import pandas as pd
+    import torch
+    from sglm_hip import engine as E, folds, grid, synth
+    from sglm_hip.estimators import Objective
+    N, m, L, K, nlam = bench.CONFIGS[a.config]
+    s = synth.make(N=N, m=m, L=L, family="poisson", rho=0.02, seed=0)
+    d = E.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
+    codes = folds.trial_keys_codes(pd.DataFrame({"nTrial": s.trial}), ["nTrial"]).values
+    np.random.seed(3)
+    cv_idx = folds.cv_idx_from_bucket_ids(codes, num_folds=K)
+    objs = [Objective("irls", E.FAM_TWEEDIE_LOG, 1.0, float(al), "n", True, 100)
+            for al in np.logspace(-4, 1, nlam)]
+    sim = (a.rank, a.world)
+    grid.run(d, s.y, cv_idx, objs, [0] * nlam, simulate=sim)
+    out = {}
+    for phases in (False, True):
+        st = E.IrlsStats(record=True, trace_phases=phases)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        grid.run(d, s.y, cv_idx, objs, [0] * nlam, stats=st, simulate=sim)
+        torch.cuda.synchronize()
+        key = "traced" if phases else "plain"
+        out[key] = {"wall_ms": (time.perf_counter() - t0) * 1e3, "fit_iters": st.fit_iters,
+                    "gram_fits": st.gram_fits,
+                    "gram_ms": [round(e0.elapsed_time(e1), 2) for e0, e1, _, _ in st.syrk_events]}
+        if phases:
+            out[key]["phases_ms"] = {k: round(v * 1e3, 2) for k, v in st.phases.items()}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
