@@ -138,10 +138,13 @@ __global__ void __launch_bounds__(kCT) chol_panel_kernel(
         const int r = e / kNB, c = e % kNB;
         sD[r][c] = (r <= c) ? H[(int64_t)(k0 + r) * P + k0 + c] : 0.0f;
     }
+    __shared__ float rd[kNB];
     if (tid < kNB) {
         z[tid] = rhs[k0 + tid];
         fz[tid] = frozen_all[(int64_t)fit * P + k0 + tid];
     }
+    __syncthreads();
+    if (tid < kNB) rd[tid] = 1.0f / sD[tid][tid];
     __syncthreads();
     const int j = k0 + kNB + blockIdx.y * kCT + tid;
     if (j >= P) return;
@@ -151,10 +154,18 @@ __global__ void __launch_bounds__(kCT) chol_panel_kernel(
     if (refactor) {
 #pragma unroll
         for (int c = 0; c < kNB; ++c) {
-            float v = x[c];
+            // four partial sums shorten the dependent FMA chain of the triangular solve
+            float v0 = x[c], v1 = 0.0f, v2 = 0.0f, v3 = 0.0f;
 #pragma unroll
-            for (int r = 0; r < c; ++r) v -= sD[r][c] * x[r];
-            x[c] = fz[c] ? 0.0f : v / sD[c][c];
+            for (int r = 0; r + 3 < c; r += 4) {
+                v0 -= sD[r][c] * x[r];
+                v1 -= sD[r + 1][c] * x[r + 1];
+                v2 -= sD[r + 2][c] * x[r + 2];
+                v3 -= sD[r + 3][c] * x[r + 3];
+            }
+#pragma unroll
+            for (int r = c & ~3; r < c; ++r) v0 -= sD[r][c] * x[r];
+            x[c] = fz[c] ? 0.0f : ((v0 + v1) + (v2 + v3)) * rd[c];
         }
 #pragma unroll
         for (int r = 0; r < kNB; ++r) H[(int64_t)(k0 + r) * P + j] = x[r];
@@ -165,46 +176,50 @@ __global__ void __launch_bounds__(kCT) chol_panel_kernel(
     rhs[j] -= s;
 }
 
-// Trailing update of the upper triangle: one 64x64 tile (bi <= bj, both > kb) per WG.
+// Trailing update of the upper triangle with `kc` rows of U (64 or 128: two block steps
+// folded into one pass over the trailing matrix), blocks counted from s0; rowonly: just block
+// row s0 (the look-ahead row the next diagonal step needs).  One 64x64 tile per workgroup,
+// one 32x32 quadrant per wave on v_mfma_f32_32x32x2f32 (exact f32 products, f32 accumulate),
+// operands loaded straight from the panel rows (L2-resident: grid x = tile, so one fit's
+// tiles run together), no LDS.  D[i][j] = sum_r U[k0+r][i] U[k0+r][j]; H[i][j] -= D.
 __global__ void __launch_bounds__(kCT) chol_update_kernel(float* __restrict__ Hall, int32_t P,
-                                                          int32_t kb,
+                                                          int32_t k0, int32_t kc, int32_t s0,
+                                                          int32_t rowonly,
                                                           const int32_t* __restrict__ fits) {
-    __shared__ __attribute__((aligned(16))) float sPi[kNB][kNB];
-    __shared__ __attribute__((aligned(16))) float sPj[kNB][kNB];
-    const int fit = fits[blockIdx.x];
+    const int fit = fits[blockIdx.y];
     float* H = Hall + (int64_t)fit * P * P;
-    const int T = P / kNB - kb - 1;
-    int t = blockIdx.y, bi = 0, rowlen = T;
-    while (t >= rowlen) { t -= rowlen; ++bi; --rowlen; }
-    const int bj = bi + t;
-    const int k0 = kb * kNB;
-    const int c0i = (kb + 1 + bi) * kNB, c0j = (kb + 1 + bj) * kNB;
-    const int tid = threadIdx.x;
-    for (int e = tid; e < kNB * kNB / 4; e += kCT) {
-        const int r = e / (kNB / 4), c4 = e % (kNB / 4);
-        *reinterpret_cast<f32x4*>(&sPi[r][c4 * 4]) =
-            *reinterpret_cast<const f32x4*>(&H[(int64_t)(k0 + r) * P + c0i + c4 * 4]);
-        *reinterpret_cast<f32x4*>(&sPj[r][c4 * 4]) =
-            *reinterpret_cast<const f32x4*>(&H[(int64_t)(k0 + r) * P + c0j + c4 * 4]);
+    const int T = P / kNB - s0;
+    int t = blockIdx.x, bi = 0, bj;
+    if (rowonly) {
+        bj = t;
+    } else {
+        int rowlen = T;
+        while (t >= rowlen) { t -= rowlen; ++bi; --rowlen; }
+        bj = bi + t;
     }
-    __syncthreads();
-    const int ty = tid >> 4, tx = tid & 15;
-    float acc[4][4] = {};
-#pragma unroll 8
-    for (int r = 0; r < kNB; ++r) {
-        const f32x4 a = *reinterpret_cast<const f32x4*>(&sPi[r][ty * 4]);
-        const f32x4 b = *reinterpret_cast<const f32x4*>(&sPj[r][tx * 4]);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r32 = lane & 31, kh = lane >> 5;
+    const int ci = (s0 + bi) * kNB + (wave >> 1) * 32;
+    const int cj = (s0 + bj) * kNB + (wave & 1) * 32;
+    const float* pa = H + (int64_t)(k0 + kh) * P + ci + r32;
+    const float* pb = H + (int64_t)(k0 + kh) * P + cj + r32;
+    f32x16 acc = {};
+    for (int r = 0; r < kc; r += 16) {
+        float av[8], bv[8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < 8; ++u) {
+            av[u] = pa[(int64_t)(r + 2 * u) * P];
+            bv[u] = pb[(int64_t)(r + 2 * u) * P];
+        }
 #pragma unroll
-            for (int v = 0; v < 4; ++v) acc[u][v] += a[u] * b[v];
+        for (int u = 0; u < 8; ++u)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
     }
+    // D[row i][col j]: reg q -> i = (q&3) + 8(q>>2) + 4*kh, j = r32
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        float* row = &H[(int64_t)(c0i + ty * 4 + u) * P + c0j + tx * 4];
-        f32x4 cur = *reinterpret_cast<f32x4*>(row);
-        cur[0] -= acc[u][0]; cur[1] -= acc[u][1]; cur[2] -= acc[u][2]; cur[3] -= acc[u][3];
-        *reinterpret_cast<f32x4*>(row) = cur;
+    for (int q = 0; q < 16; ++q) {
+        float* h = &H[(int64_t)(ci + (q & 3) + 8 * (q >> 2) + 4 * kh) * P + cj + r32];
+        *h -= acc[q];
     }
 }
 
@@ -291,18 +306,27 @@ extern "C" int sglm_chol_solve_ex(float* H, int32_t P, const int32_t* fits, int3
     int st = check_launch("chol_prep_kernel");
     if (st) return st;
     const int nb = P / kNB;
-    for (int kb = 0; kb < nb; ++kb) {
+    // block steps in pairs: diag/panel kb, look-ahead update of block row kb+1 only,
+    // diag/panel kb+1, then ONE rank-128 update of the remaining trailing matrix
+    auto factor_step = [&](int kb) {
         const int k0 = kb * kNB;
         chol_diag_kernel<<<nact, 64, 0, s>>>(H, P, k0, fits, frozen, rhs, dg, info, refactor);
         const int rem = P - k0 - kNB;
-        if (rem > 0) {
+        if (rem > 0)
             chol_panel_kernel<<<dim3(nact, (rem + kCT - 1) / kCT), kCT, 0, s>>>(H, P, k0, fits,
                                                                                frozen, rhs, refactor);
-            if (refactor) {
-                const int T = nb - kb - 1;
-                chol_update_kernel<<<dim3(nact, T * (T + 1) / 2), kCT, 0, s>>>(H, P, kb, fits);
-            }
-        }
+    };
+    for (int kb = 0; kb < nb; kb += 2) {
+        factor_step(kb);
+        if (kb + 1 >= nb) break;
+        if (refactor)
+            chol_update_kernel<<<dim3(nb - kb - 1, nact), kCT, 0, s>>>(H, P, kb * kNB, kNB,
+                                                                      kb + 1, 1, fits);
+        factor_step(kb + 1);
+        const int T = nb - kb - 2;
+        if (refactor && T > 0)
+            chol_update_kernel<<<dim3(T * (T + 1) / 2, nact), kCT, 0, s>>>(H, P, kb * kNB,
+                                                                          2 * kNB, kb + 2, 0, fits);
     }
     st = check_launch("chol block kernels");
     if (st) return st;
