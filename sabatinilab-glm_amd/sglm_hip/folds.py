@@ -95,11 +95,15 @@ def trial_keys_codes(df, id_cols, package_style=False):
 
 def masks_from_cv_idx(cv_idx, n):
     """Per split: (train multiplicity mask, test multiplicity mask) as uint8 arrays."""
-    out = []
-    for tr, te in cv_idx:
-        mtr = np.bincount(np.asarray(tr, dtype=np.int64), minlength=n)[:n]
-        mte = np.bincount(np.asarray(te, dtype=np.int64), minlength=n)[:n]
-        if mtr.max(initial=0) > 255 or mte.max(initial=0) > 255:
-            raise ValueError("an index repeats more than 255 times in one split")
-        out.append((mtr.astype(np.uint8), mte.astype(np.uint8)))
-    return out
+    def one(idx):
+        idx = np.asarray(idx, dtype=np.int64).reshape(-1)
+        if idx.size and (idx[0] < 0 or idx[-1] >= n or not np.all(idx[1:] > idx[:-1])):
+            m = np.bincount(idx, minlength=n)[:n]          # repeats (holdout resampling)
+            if m.max(initial=0) > 255:
+                raise ValueError("an index repeats more than 255 times in one split")
+            return m.astype(np.uint8)
+        m = np.zeros(n, dtype=np.uint8)                     # strictly increasing: 0/1 mask
+        m[idx] = 1
+        return m
+
+    return [(one(tr), one(te)) for tr, te in cv_idx]

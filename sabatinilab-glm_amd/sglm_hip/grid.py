@@ -144,6 +144,7 @@ def run(X, y, cv_idx, objectives: Sequence[Objective], rolls: Sequence[int],
         raise ValueError(f"y has {y.shape[0]} rows, X has {n}")
     K = len(cv_idx)
     fm = F.masks_from_cv_idx(cv_idx, n)
+    t0 = tick("setup_masks", t0)
     masks = []
     for tr, te in fm:
         masks += [tr, te]
@@ -153,7 +154,9 @@ def run(X, y, cv_idx, objectives: Sequence[Objective], rolls: Sequence[int],
     ridx = {r: i for i, r in enumerate(roll_list)}
     ys = [np.roll(y, r) for r in roll_list]
     prob = E.Problem(design, ys, masks)
+    t0 = tick("setup_problem", t0)
     ms = _MaskStats(prob)
+    t0 = tick("setup_maskstats", t0)
 
     # ---- fit table: (param j, split k) then refit (j, -1)
     table = []
