@@ -163,3 +163,10 @@ def calc_R2(residuals: np.ndarray, mean_residuals: np.ndarray) -> float:
     if tss == 0:
         return 0
     return 1 - rss / tss
+
+
+def fit_GLM(X, y, model_name='Gaussian', *args, **kwargs):
+    """Fit a GLM (sglm/sglm/models/sglm.py:461-485; backend/sglm_ez.py:149-171)."""
+    glm = GLM(model_name, *args, **kwargs)
+    glm.fit(X, y)
+    return glm

@@ -198,3 +198,33 @@ def test_c3_shape_poisson_grid_vs_oracle(engine):
         assert abs(r["cv_R2_score"] - q["cv_R2_score"]) < 1e-6
         assert rel(r["model"].coef_, q["coef"]) < TOL_POIS
     assert out["best_params"] == ref["best_params"]
+
+
+def test_setup_model_fit_timeshift_vals_by_dict(engine):
+    """Package event-major expansion (setup_model_fit.timeshift_vals_by_dict): lag 0
+    duplicated, int columns promoted to float64, NaN drop on the LAST entry's extreme lags —
+    against the oracle restatement and plain pandas shift()."""
+    from sglm.features import setup_model_fit as smf
+    rng = np.random.default_rng(31)
+    n = 500
+    df = pd.DataFrame({"ev_a": (rng.random(n) < 0.1).astype(np.int64),
+                       "ev_b": (rng.random(n) < 0.2).astype(np.float32),
+                       "sig": rng.standard_normal(n),
+                       "nTrial": np.arange(n) // 50})
+    orders = {"ev_a": (-3, 2), "ev_b": (-1, 4), "sig": (-2, 2)}
+    for keep in (True, False):
+        out, names = smf.timeshift_vals_by_dict(df, orders, keep_nans=keep)
+        assert names == [f"{c}_{s}" for c, (lo, hi) in orders.items() for s in range(lo, hi + 1)]
+        assert list(out.columns) == list(df.columns) + names
+        for c, (lo, hi) in orders.items():
+            for s in range(lo, hi + 1):
+                exp = df[[c]].shift(s)[c]
+                if not keep:
+                    exp = exp.loc[out.index]
+                assert out[f"{c}_{s}"].dtype == exp.dtype, (c, s)
+                assert np.array_equal(out[f"{c}_{s}"].values, exp.values, equal_nan=True), (c, s)
+        idx = {c: i for i, c in enumerate(df.columns)}
+        ref = pp_ref.timeshift_by_dict(df.values.astype(np.float64),
+                                       {idx[c]: o for c, o in orders.items()}, keep_nans=keep)
+        assert ref.shape == out.shape
+        assert np.array_equal(out.values.astype(np.float64), ref, equal_nan=True)
