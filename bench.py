@@ -34,7 +34,10 @@ CONFIGS = {
     "c4": (1_000_000, 50, 20, 5, 20),
     "c3": (100_000, 25, 10, 5, 20),
     "small": (50_000, 10, 5, 5, 4),
+    # C5: 64 responses x C4 design, Gaussian elastic-net lambda path (l1_ratio 0.5, 20 alphas)
+    "c5": (1_000_000, 50, 20, 5, 20),
 }
+C5_RESPONSES = 64
 
 
 def parse():
@@ -132,8 +135,72 @@ def pmc_traffic():
     return dom["traffic_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
 
 
+def bench_c5(a):
+    """64 responses (independent y draws, same X as C4), elastic net
+    l1_ratio 0.5 over 20 alphas, 5 splits + refit per (response, alpha) = 7680 fits, scored
+    on the splits' test rows.  One rank (the path batches all responses on one GPU)."""
+    import pandas as pd
+    import torch
+    from sglm_hip import engine as E, enet, folds, synth
+    N, m, L, K, nlam = CONFIGS["c5"]
+    R = C5_RESPONSES
+    s = synth.make(N=N, m=m, L=L, family="gaussian", rho=0.02, seed=0)
+    design = E.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
+    rng = np.random.default_rng(5)
+    Y = np.stack([s.y + rng.normal(0, 1, s.N) for _ in range(R)], 1)
+    codes = folds.trial_keys_codes(pd.DataFrame({"nTrial": s.trial}), ["nTrial"]).values
+    np.random.seed(3)
+    cv_idx = folds.cv_idx_from_bucket_ids(codes, num_folds=K)
+    alphas = np.logspace(-4, 1, nlam)
+    for _ in range(a.warmup):
+        enet.cv_enet_path(design, Y, cv_idx, alphas, l1_ratio=0.5)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        st = {}
+        out = enet.cv_enet_path(design, Y, cv_idx, alphas, l1_ratio=0.5, stats=st)
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / a.steps
+    cpu = None
+    if not a.no_cpu:
+        from sklearn.linear_model import ElasticNet
+        rows = min(a.sklearn_rows, s.N)
+        X = dense_slice(s, rows)
+        t1 = time.perf_counter()
+        en = ElasticNet(alpha=float(alphas[nlam // 2]), l1_ratio=0.5, max_iter=1000).fit(X, Y[:rows, 0])
+        dt = time.perf_counter() - t1
+        per_fit_1m = dt * s.N / rows
+        try:
+            from threadpoolctl import threadpool_info
+            cores = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+        except Exception:  # pragma: no cover
+            cores = int(os.environ.get("OMP_NUM_THREADS", 1))
+        cpu = {"value": 1.0 / per_fit_1m, "unit": "elastic-net fits/s (1M-row unit)",
+               "cores": int(cores), "kind": "port",
+               "sample": f"scikit-learn ElasticNet(alpha={alphas[nlam // 2]:.3g}, l1_ratio=0.5) "
+                         f"on a {rows}x{s.p} slice, {en.n_iter_} CD epochs in {dt:.2f} s, "
+                         f"scaled x{s.N / rows:.0f} to 1M rows",
+               "grid_wall_s_extrapolated": per_fit_1m * st["fits"]}
+    print(json.dumps({
+        "metric": "elastic-net CV lambda-path fits/s (C5: 64 responses x 1M x 2000)",
+        "value": st["fits"] / el, "unit": "fits/s", "n_gpus": 1, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": el * 1e3, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64 (CD) / bf16-exact Gram",
+        "data": "synthetic",
+        "config": {"workload": f"Gaussian elastic net l1_ratio 0.5, {R} responses x {nlam} "
+                               f"alphas x ({K} splits + refit) = {st['fits']} fits on "
+                               f"{s.N} x {s.p} timeshifted 0/1 predictors",
+                   "config_name": "c5", **st,
+                   "refit_nonzeros_r0": [int(np.sum(np.abs(out[0][j]["refit_coef"]) > 0))
+                                         for j in range(nlam)]},
+        "roofline": None,
+        "cpu_baseline": cpu}))
+
+
 def main():
     a = parse()
+    if a.config == "c5":
+        return bench_c5(a)
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -180,6 +180,18 @@ size_t sglm_xtr_bits_work_bytes(int32_t P, int32_t B, int64_t ld);
 int sglm_xtr_bits(const uint32_t* cbits, int64_t ld, int32_t P, int64_t n, const float* R,
                   int32_t B, double* G, void* work, sglm_stream_t stream);
 
+/* Shared-Gram elastic net for many fits per mask (multi-response lambda paths):
+ * sglm_center_gram: Q[m] (float64 p x p) = G_xx - g g^T / n (center) or G_xx from the
+ *   augmented Gram H[gram_of[m]] (ones column at index p, as sglm_syrk forms it with W = mask);
+ * sglm_enet_cd_shared: per fit f, minimise 1/2 w^T Q w - q^T w + l1|w|_1 + l2/2|w|^2 with
+ *   Q = Q[qidx[f]], q = q[f] (float64, p), cyclic CD to max|dw| <= tol max|w| -> w[f].
+ * Replaces sklearn ElasticNet/Lasso (cd_fast) per response and lambda, backend/sglm.py:106-110. */
+int sglm_center_gram(const float* H, int32_t P, int32_t p, const int32_t* gram_of, int32_t nmask,
+                     int32_t center, double* Q, sglm_stream_t stream);
+int sglm_enet_cd_shared(const double* Q, int32_t p, const int32_t* qidx, int32_t nfit,
+                        const double* q, const double* l1, const double* l2, int32_t max_sweeps,
+                        double tol, double* w, int32_t* sweeps, sglm_stream_t stream);
+
 /* Development entries: a specific bf16 Gram variant (1 = register-staged, 2 = LDS-DMA
  * staged; sglm_syrk uses the default), same arguments as sglm_syrk. */
 int sglm_syrk_v1(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, const float* W,

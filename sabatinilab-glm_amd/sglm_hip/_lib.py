@@ -43,6 +43,9 @@ SIGNATURES = {
     "sglm_gemv_eta_bits": (C.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _vp, _vp]),
     "sglm_xtr_bits_work_bytes": (_sz, [_i32, _i32, _i64]),
     "sglm_xtr_bits": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _i32, _vp, _vp, _vp]),
+    "sglm_center_gram": (C.c_int, [_vp, _i32, _i32, _vp, _i32, _i32, _vp, _vp]),
+    "sglm_enet_cd_shared": (C.c_int, [_vp, _i32, _vp, _i32, _vp, _vp, _vp, _i32, C.c_double,
+                                      _vp, _vp, _vp]),
     "sglm_syrk_v1": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
     "sglm_syrk_variant": (C.c_int, [_i32, _vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _vp,
                                     _vp]),

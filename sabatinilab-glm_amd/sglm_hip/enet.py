@@ -1,0 +1,259 @@
+"""Elastic net / Lasso on shared per-mask Grams (MI355X).
+
+Replaces sklearn's cd_fast behind backend/sglm.py:106-110 (ElasticNet / Lasso):
+  objective  1/(2n)|y - Xw - b|^2 + alpha rho |w|_1 + alpha (1 - rho)/2 |w|^2
+  (sklearn/linear_model/_coordinate_descent.py:420-422), multiplied by n it is
+  1/2 w^T Q w - q^T w + l1|w|_1 + l2/2|w|^2 on centred data, l1 = alpha rho n,
+  l2 = alpha (1 - rho) n.
+
+Everything that does not depend on the response or the penalty is formed once per row mask:
+the exact Gram G_m = X^T diag(m) X (MFMA, W = mask: integer counts, exact for 0/1 designs)
+and its centred float64 form Q_m (sglm_center_gram).  Per (response, mask) only
+c = X^T (m * y) (MFMA gradient kernel); per fit only q = c_x - g c_p / n and the coordinate
+descent (sglm_enet_cd_shared, one workgroup per fit, Q_m shared by index).
+
+``cv_enet_path`` is the multi-response lambda path of SURVEY.md §8(d) C5: for every response
+and every alpha, the K split fits and the full refit, scored on the split's test rows from
+Gram algebra (|y - Xw - b|^2 over a mask = y'My - 2 beta'c_t + beta' G_t beta with the test
+mask's Gram and X^T(m y)), so no linear predictor over n rows is ever formed.  The reference
+runs one ``simple_cv_fit`` per response (er_refactored_from_scratch_cleanup.py:388), each
+re-fitting sklearn ElasticNet on X[idx] copies (backend/sglm_cv.py:106-131).
+"""
+from __future__ import annotations
+
+import math
+from types import SimpleNamespace
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from . import engine as E
+from . import folds as F
+
+CD_TOL = 1e-10
+
+
+class SharedGrams:
+    """Exact Grams (augmented: ones column at p) of a problem's masks, formed on demand."""
+
+    def __init__(self, prob: E.Problem):
+        self.prob = prob
+        self.d = prob.design
+        self.slot = {}                   # mask -> row of self.H
+        self.H = None
+        self.Q = {}                      # (mask, center) -> row of Qt
+        self.Qt = None
+
+    def ensure(self, masks: Sequence[int]):
+        need = [int(m) for m in dict.fromkeys(masks) if int(m) not in self.slot]
+        if not need:
+            return
+        d, prob = self.d, self.prob
+        old = self.H
+        base = 0 if old is None else old.shape[0]
+        H = torch.empty((base + len(need), d.P, d.P), dtype=torch.float32, device=d.device)
+        if old is not None:
+            H[:base].copy_(old)
+        W = prob.M[need].to(torch.float32)                   # W = mask multiplicities
+        ns = SimpleNamespace(W=W, H=H[base:], prob=prob, fit_mask=np.array(need), wc=None,
+                             keep=None)
+        E._syrk(d, ns, np.arange(len(need), dtype=np.int32), (d.n + 31) // 32,
+                (d.P // 256) * (d.P // 256 + 1) // 2, None, E._stream(), exact=True)
+        for i, m in enumerate(need):
+            self.slot[m] = base + i
+        self.H = H
+
+    def centred(self, masks: Sequence[int], center: bool):
+        """float64 Q (p x p) per (mask, center); returns the index of each requested mask."""
+        self.ensure(masks)
+        need = [m for m in dict.fromkeys(int(x) for x in masks) if (m, center) not in self.Q]
+        if need:
+            d = self.d
+            base = 0 if self.Qt is None else self.Qt.shape[0]
+            Qt = torch.empty((base + len(need), d.p, d.p), dtype=torch.float64, device=d.device)
+            if self.Qt is not None:
+                Qt[:base].copy_(self.Qt)
+            g = torch.tensor([self.slot[m] for m in need], dtype=torch.int32, device=d.device)
+            _lib.call("sglm_center_gram", E._p(self.H), d.P, d.p, E._p(g), len(need),
+                      int(center), E._p(Qt[base:]), E._stream())
+            for i, m in enumerate(need):
+                self.Q[(m, center)] = base + i
+            self.Qt = Qt
+        return [self.Q[(int(m), center)] for m in masks]
+
+    def sym(self, mask: int):
+        """Full symmetric float64 augmented Gram (P x P) of one mask."""
+        H = self.H[self.slot[int(mask)]].to(torch.float64)
+        up = torch.triu(H)
+        return up + torch.triu(H, 1).T
+
+
+def xty(prob: E.Problem, pairs: Sequence[tuple]) -> torch.Tensor:
+    """c[(r, m)] = X^T (m * y_r) (float64 [len(pairs)][P]; c[p] = sum m y)."""
+    d = prob.design
+    out = torch.empty((len(pairs), d.P), dtype=torch.float64, device=d.device)
+    chunk = 256
+    for s in range(0, len(pairs), chunk):
+        pr = pairs[s:s + chunk]
+        R = torch.stack([prob.M[m].to(torch.float32) * prob.Y[r] for r, m in pr])
+        d.xtr(R, len(pr), out[s:s + len(pr)])
+    return out
+
+
+def solve(prob: E.Problem, grams: SharedGrams, fits: Sequence[dict], c: torch.Tensor,
+          cidx: Sequence[int]):
+    """ElasticNet per fit dict {mask, alpha, l1_ratio, fit_intercept, max_iter} with
+    c[cidx[f]] = X^T(m y) of its (response, mask).  Returns (w [B][p] f64, b [B] f64,
+    sweeps [B] int, converged [B] bool) as host arrays."""
+    d = prob.design
+    p, dev = d.p, d.device
+    B = len(fits)
+    if B == 0:
+        return np.zeros((0, p)), np.zeros(0), np.zeros(0, int), np.zeros(0, bool)
+    masks = [int(f["mask"]) for f in fits]
+    grams.ensure(masks)
+    cnt = np.array([float(prob.mask_count(m)) for m in masks])
+    q = torch.empty((B, p), dtype=torch.float64, device=dev)
+    qidx = np.zeros(B, dtype=np.int32)
+    cpv = torch.empty(B, dtype=torch.float64, device=dev)
+    gv = torch.zeros((B, p), dtype=torch.float64, device=dev)
+    for center in (True, False):
+        sel = [i for i, f in enumerate(fits) if bool(f["fit_intercept"]) == center]
+        if not sel:
+            continue
+        qi = grams.centred([masks[i] for i in sel], center)
+        qidx[sel] = qi
+        sel_t = torch.tensor(sel, device=dev)
+        cc = c[torch.tensor([cidx[i] for i in sel], device=dev)]
+        cpv[sel_t] = cc[:, p]
+        if center:
+            gslot = torch.tensor([grams.slot[masks[i]] for i in sel], device=dev)
+            g = grams.H[gslot][:, :p, p].to(torch.float64)      # X^T m (upper: rows < p)
+            n = torch.from_numpy(cnt[sel]).to(dev)
+            gv[sel_t] = g
+            q[sel_t] = cc[:, :p] - g * (cc[:, p] / n.clamp_min(1))[:, None]
+        else:
+            q[sel_t] = cc[:, :p]
+    l1 = torch.from_numpy(np.array([f["alpha"] * f["l1_ratio"] for f in fits]) * cnt).to(dev)
+    l2 = torch.from_numpy(np.array([f["alpha"] * (1 - f["l1_ratio"]) for f in fits]) * cnt).to(dev)
+    w = torch.empty((B, p), dtype=torch.float64, device=dev)
+    sw = torch.empty(B, dtype=torch.int32, device=dev)
+    max_sweeps = int(max(max(int(f["max_iter"]) for f in fits), 10000))
+    qidx_d = torch.from_numpy(qidx).to(dev)
+    _lib.call("sglm_enet_cd_shared", E._p(grams.Qt), p, E._p(qidx_d), B, E._p(q), E._p(l1),
+              E._p(l2), max_sweeps, CD_TOL, E._p(w), E._p(sw), E._stream())
+    fi = torch.tensor([bool(f["fit_intercept"]) for f in fits], device=dev)
+    n = torch.from_numpy(cnt).to(dev)
+    b = torch.where(fi & (n > 0), (cpv - (gv * w).sum(1)) / n.clamp_min(1), 0.0)
+    swh = sw.cpu().numpy()
+    return w.cpu().numpy(), b.cpu().numpy(), swh, swh < max_sweeps
+
+
+def cv_enet_path(X, Y, cv_idx, alphas: Sequence[float], l1_ratio: float = 0.5,
+                 fit_intercept: bool = True, max_iter: int = 1000, score_method: str = "mse",
+                 stats: Optional[dict] = None):
+    """Multi-response elastic-net CV path.  Returns ``out[r][j]``: the result dict of
+    response r and alpha j with the keys of ``grid.run`` (cv_coefs p x K, cv_intercepts,
+    cv_scores_train/test, cv_mean_score_train, cv_mean_score, cv_std_score, cv_R2_score,
+    cv_mse_score, refit_coef, refit_intercept, n_iter, converged)."""
+    design = X if isinstance(X, E.Design) else E.Design.from_host(X)
+    n, p, dev = design.n, design.p, design.device
+    Y = np.asarray(Y, dtype=np.float64)
+    if Y.ndim == 1:
+        Y = Y[:, None]
+    if Y.shape[0] != n:
+        raise ValueError(f"Y has {Y.shape[0]} rows, X has {n}")
+    R, A, K = Y.shape[1], len(alphas), len(cv_idx)
+    masks = []
+    for tr, te in F.masks_from_cv_idx(cv_idx, n):
+        masks += [tr, te]
+    FULL = len(masks)
+    masks.append(np.ones(n, np.uint8))
+    prob = E.Problem(design, [Y[:, r] for r in range(R)], masks)
+    grams = SharedGrams(prob)
+    grams.ensure(range(len(masks)))
+    pairs = [(r, m) for r in range(R) for m in range(len(masks))]
+    c = xty(prob, pairs)
+    ci = {pm: i for i, pm in enumerate(pairs)}
+    fits, keys = [], []
+    for r in range(R):
+        for j, al in enumerate(alphas):
+            for k in list(range(K)) + [-1]:
+                m = FULL if k < 0 else 2 * k
+                fits.append({"mask": m, "alpha": float(al), "l1_ratio": float(l1_ratio),
+                             "fit_intercept": fit_intercept, "max_iter": max_iter})
+                keys.append((r, j, k))
+    w, b, sw, conv = solve(prob, grams, fits, c, [ci[(r, f["mask"])] for (r, _, _), f in zip(keys, fits)])
+    # ---- scores from Gram algebra: SS(mask) = y'My - 2 beta'c + beta' G beta (augmented)
+    Yd = torch.from_numpy(Y.T.copy()).to(dev)                    # R x n float64
+    Md = prob.M[:, :n].to(torch.float64)
+    yyh = (Md @ (Yd * Yd).T).cpu().numpy()                       # F x R: sum m y^2
+    del Md, Yd
+    cnt = np.array([float(prob.mask_count(m)) for m in range(len(masks))])
+    c_p = c[:, p].cpu().numpy()                                  # sum m y per (r, m) pair
+    beta = np.zeros((len(fits), design.P))
+    beta[:, :p] = w
+    beta[:, p] = b
+    betad = torch.from_numpy(beta).to(dev)
+    ss = np.zeros((len(fits), 2))                                # [train, test] per split fit
+    kk = np.array([k for (_, _, k) in keys])
+    rr = np.array([r for (r, _, _) in keys])
+    for k in range(K):
+        rows = np.flatnonzero(kk == k)
+        bt = betad[torch.from_numpy(rows).to(dev)]
+        for side, mt in ((0, 2 * k), (1, 2 * k + 1)):
+            quad = ((bt @ grams.sym(mt)) * bt).sum(1)
+            cidx_t = torch.from_numpy(np.array([ci[(r, mt)] for r in rr[rows]])).to(dev)
+            lin = (bt * c[cidx_t]).sum(1)
+            yv = torch.from_numpy(yyh[mt, rr[rows]]).to(dev)
+            ss[rows, side] = (yv - 2 * lin + quad).clamp_min(0).cpu().numpy()
+    kpos = {key: i for i, key in enumerate(keys)}
+    out = []
+    for r in range(R):
+        per = []
+        for j in range(A):
+            cv_coefs = np.zeros((p, K))
+            cv_b = np.zeros(K)
+            s_tr, s_te = np.zeros(K), np.zeros(K)
+            ss_res = ss_tot = n_te = 0.0
+            n_iter, conv_all, refit = [], True, None
+            for k in list(range(K)) + [-1]:
+                i = kpos[(r, j, k)]
+                n_iter.append(int(sw[i]))
+                conv_all &= bool(conv[i])
+                if k < 0:
+                    refit = (w[i].copy(), float(b[i]))
+                    continue
+                cv_coefs[:, k], cv_b[k] = w[i], b[i]
+                for side, mt, dst in ((0, 2 * k, s_tr), (1, 2 * k + 1, s_te)):
+                    sres = float(ss[i, side])
+                    nm = cnt[mt]
+                    ym = float(c_p[ci[(r, mt)]]) / nm if nm else 0.0
+                    sst = max(yyh[mt, r] - nm * ym * ym, 0.0)
+                    if nm == 0:
+                        dst[k] = np.nan
+                    elif score_method == "r2":
+                        dst[k] = (1.0 if sres == 0 else 0.0) if sst == 0 else 1.0 - sres / sst
+                    else:
+                        dst[k] = -sres / nm
+                    if mt == 2 * k + 1:
+                        ss_res += sres
+                        ss_tot += sst
+                        n_te += nm
+            per.append({
+                "cv_coefs": cv_coefs, "cv_intercepts": cv_b,
+                "cv_scores_train": s_tr, "cv_scores_test": s_te,
+                "cv_mean_score_train": np.mean(s_tr), "cv_mean_score": np.mean(s_te),
+                "cv_std_score": np.std(s_te),
+                "cv_R2_score": 0 if ss_tot == 0 else 1 - ss_res / ss_tot,
+                "cv_mse_score": ss_res / n_te if n_te else np.nan,
+                "refit_coef": refit[0], "refit_intercept": refit[1],
+                "n_iter": n_iter, "converged": conv_all,
+            })
+        out.append(per)
+    if stats is not None:
+        stats.update({"fits": len(fits), "grams": len(masks), "xty_columns": len(pairs),
+                      "cd_sweeps_total": int(np.sum(sw)), "cd_sweeps_max": int(np.max(sw))})
+    return out

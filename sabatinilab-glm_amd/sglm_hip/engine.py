@@ -320,6 +320,13 @@ class Problem:
             self._compact[mask] = c
         return c
 
+    def mask_count(self, mask: int) -> float:
+        """Sum of a mask's multiplicities (rows of the fit), cached."""
+        key = ("count", int(mask))
+        if key not in self._stats:
+            self._stats[key] = float(self.masks[int(mask)].sum(dtype=np.int64))
+        return self._stats[key]
+
     def mask_stats(self, resp: int, mask: int):
         """float64 (count, sum y, mean y) over a mask — host side, cached."""
         key = (resp, mask)

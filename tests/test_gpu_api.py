@@ -228,3 +228,37 @@ def test_setup_model_fit_timeshift_vals_by_dict(engine):
                                        {idx[c]: o for c, o in orders.items()}, keep_nans=keep)
         assert ref.shape == out.shape
         assert np.array_equal(out.values.astype(np.float64), ref, equal_nan=True)
+
+
+def test_multi_response_enet_path_vs_oracle(engine):
+    """C5 path (small): 3 responses x 3 alphas elastic net (l1_ratio 0.5), 3 trial-id splits +
+    refits in ONE call with shared per-mask Grams and Gram-algebra scores — against the oracle
+    run per response (what the reference's per-response loop computes)."""
+    from sglm_hip import enet, synth
+    s = synth.make(N=6000, m=5, L=3, family="gaussian", rho=0.15, seed=41, beta_scale=0.5)
+    X = s.dense_X()
+    rng = np.random.default_rng(42)
+    B = rng.normal(0, 0.5, (s.p, 3))
+    Y = X @ B + 0.3 + rng.normal(0, 1.0, (s.N, 3))
+    np.random.seed(3)
+    cv_idx = folds_ref.cv_idx_from_bucket_ids(folds_ref.trial_bucket_codes([s.trial]), num_folds=3)
+    alphas = [1e-3, 1e-2, 1e-1]
+    for method in ("r2", "mse"):
+        st = {}
+        out = enet.cv_enet_path(X, Y, cv_idx, alphas, l1_ratio=0.5, max_iter=1000,
+                                score_method=method, stats=st)
+        assert st["grams"] == 7 and st["fits"] == 3 * 3 * 4
+        for r in range(3):
+            kws = [{"alpha": a, "l1_ratio": 0.5, "max_iter": 1000} for a in alphas]
+            ref = cv_ref.cv_mult(X, Y[:, r], cv_idx, kws, score_method=method)
+            for j, q in enumerate(ref["full_cv_results"]):
+                g = out[r][j]
+                assert rel(g["cv_coefs"], q["cv_coefs"]) < TOL_GAUSS, (r, j)
+                assert rel(g["cv_intercepts"], q["cv_intercepts"]) < TOL_GAUSS
+                tol = 1e-6 if method == "r2" else 1e-6 * np.max(np.abs(q["cv_scores_test"]))
+                assert np.max(np.abs(g["cv_scores_test"] - q["cv_scores_test"])) < tol
+                assert np.max(np.abs(g["cv_scores_train"] - q["cv_scores_train"])) < tol
+                assert abs(g["cv_R2_score"] - q["cv_R2_score"]) < 1e-6
+                assert rel(g["refit_coef"], q["coef"]) < TOL_GAUSS
+                assert abs(g["refit_intercept"] - q["intercept"]) < 1e-5 * max(1, abs(q["intercept"]))
+                assert g["converged"]
