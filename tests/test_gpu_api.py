@@ -262,3 +262,22 @@ def test_multi_response_enet_path_vs_oracle(engine):
                 assert rel(g["refit_coef"], q["coef"]) < TOL_GAUSS
                 assert abs(g["refit_intercept"] - q["intercept"]) < 1e-5 * max(1, abs(q["intercept"]))
                 assert g["converged"]
+
+
+def test_c1_shape_ols_vs_oracle(engine):
+    """C1 shape (Gaussian OLS 10k x 100, one trial-id split): the drop-in GLM on the MI355X
+    against the oracle's lstsq (1e-5 relative) and its train/test scores."""
+    import sglm
+    from sglm_hip import synth
+    s = synth.make(N=10_000, m=10, L=5, family="gaussian", rho=0.05, seed=7)
+    X = s.dense_X()
+    np.random.seed(3)
+    tr, te = folds_ref.cv_idx_from_bucket_ids(folds_ref.trial_bucket_codes([s.trial]),
+                                              num_folds=1, test_size=0.2)[0]
+    glm = sglm.GLM("Normal", alpha=0)
+    glm.fit(X[tr], s.y[tr])
+    c, b = glm_ref.fit_ols(X[tr], s.y[tr])
+    assert rel(glm.coef_, c) < TOL_GAUSS
+    assert abs(glm.intercept_ - b) < TOL_GAUSS * max(1.0, abs(b))
+    pred = X[te] @ c + b
+    assert abs(glm.neg_mse_score(X[te], s.y[te]) + np.mean((s.y[te] - pred) ** 2)) < 1e-6

@@ -156,3 +156,22 @@ def test_generate_mult_params_order():
                    {"max_iter": 5, "alpha": 1, "l1_ratio": 1},
                    {"max_iter": 5, "alpha": 2, "l1_ratio": 0},
                    {"max_iter": 5, "alpha": 2, "l1_ratio": 1}]
+
+
+def test_c1_ols_oracle_vs_sklearn():
+    """C1 shape (Gaussian OLS, 10k x 100 timeshifted design, 1 split): the oracle's lstsq
+    restatement against scikit-learn LinearRegression called directly (plumbing only)."""
+    import sys
+    from sklearn.linear_model import LinearRegression
+    sys.path.insert(0, __import__("conftest").PKG)
+    from sglm_hip import synth
+    s = synth.make(N=10_000, m=10, L=5, family="gaussian", rho=0.05, seed=7)
+    X = s.dense_X()
+    np.random.seed(3)
+    cv = folds_ref.cv_idx_from_bucket_ids(folds_ref.trial_bucket_codes([s.trial]), num_folds=1,
+                                          test_size=0.2)
+    tr, te = cv[0]
+    c, b = glm_ref.fit_ols(X[tr], s.y[tr])
+    sk = LinearRegression().fit(X[tr], s.y[tr])
+    assert np.max(np.abs(c - sk.coef_)) <= 1e-9 * max(1.0, np.max(np.abs(sk.coef_)))
+    assert abs(b - sk.intercept_) <= 1e-9 * max(1.0, abs(sk.intercept_))
