@@ -153,16 +153,39 @@ def solve(prob: E.Problem, grams: SharedGrams, fits: Sequence[dict], c: torch.Te
 
 def cv_enet_path(X, Y, cv_idx, alphas: Sequence[float], l1_ratio: float = 0.5,
                  fit_intercept: bool = True, max_iter: int = 1000, score_method: str = "mse",
-                 stats: Optional[dict] = None):
+                 stats: Optional[dict] = None, shard: bool = True):
     """Multi-response elastic-net CV path.  Returns ``out[r][j]``: the result dict of
     response r and alpha j with the keys of ``grid.run`` (cv_coefs p x K, cv_intercepts,
     cv_scores_train/test, cv_mean_score_train, cv_mean_score, cv_std_score, cv_R2_score,
-    cv_mse_score, refit_coef, refit_intercept, n_iter, converged)."""
-    design = X if isinstance(X, E.Design) else E.Design.from_host(X)
-    n, p, dev = design.n, design.p, design.device
+    cv_mse_score, refit_coef, refit_intercept, n_iter, converged).
+
+    With torch.distributed initialised the responses are dealt round-robin over the ranks
+    (each rank forms the shared Grams of the masks itself) and the per-response results are
+    all-gathered once (no data-path collective)."""
     Y = np.asarray(Y, dtype=np.float64)
     if Y.ndim == 1:
         Y = Y[:, None]
+    from .grid import _dist
+    dist = _dist() if shard else None
+    if dist is not None:
+        rank, world = dist.get_rank(), dist.get_world_size()
+        mine = list(range(rank, Y.shape[1], world))
+        local = {}
+        if mine:
+            st = {} if stats is not None else None
+            res = cv_enet_path(X, Y[:, mine], cv_idx, alphas, l1_ratio, fit_intercept, max_iter,
+                               score_method, st, shard=False)
+            local = {r: v for r, v in zip(mine, res)}
+            if stats is not None:
+                stats.update(st)
+        gathered = [None] * world
+        dist.all_gather_object(gathered, local)
+        merged = {}
+        for g in gathered:
+            merged.update(g)
+        return [merged[r] for r in range(Y.shape[1])]
+    design = X if isinstance(X, E.Design) else E.Design.from_host(X)
+    n, p, dev = design.n, design.p, design.device
     if Y.shape[0] != n:
         raise ValueError(f"Y has {Y.shape[0]} rows, X has {n}")
     R, A, K = Y.shape[1], len(alphas), len(cv_idx)
