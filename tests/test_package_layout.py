@@ -83,3 +83,35 @@ def test_setup_model_fit_dict_helpers():
     w = smf.xy_pairs_to_widest_orders([{"X_cols": {"a": (-2, 3), "b": (-1, 1)}},
                                        {"X_cols": {"a": (-4, 1), "c": (0, 2)}}])
     assert w == {"a": (-4, 3), "b": (-1, 1), "c": (0, 2)}
+
+
+def test_glm_data_roundtrip_and_output_formats(tmp_path):
+    """sglm_save.GLM_data: a fitted GLM (coefficients set as after a fit) pickles with the
+    container and loads back; coef_/intercept_ in the reference's np.save formats."""
+    import pickle
+    import sglm
+    import sglm_save
+    glm = sglm.GLM("Normal", alpha=1.0, l1_ratio=0.0)
+    glm._set_fitted(np.arange(5, dtype=np.float64) / 7, 0.25, 3)
+    gd = sglm_save.GLM_data(str(tmp_path), "run.pkl")
+    gd.set_uid("u1")
+    gd.set_X_cols(["a", "b", "c", "d", "e"])
+    gd.set_gss_info(5, 0.2, 0.2)
+    gd.set_timeshifts(-20, 20)
+    gd.append_fit_results("y", {"alpha": 1.0}, glm_model=glm, scores={"tr_witi": 0.5})
+    gd.save()
+    back = sglm_save.GLM_data(str(tmp_path), "run.pkl")
+    back.load()
+    fr = back.data["fit_results"][0]
+    assert back.data["uid"] == "u1" and fr["scores"]["holdout_noiti"] is None
+    assert np.array_equal(fr["glm_model_gss"].coef_, glm.coef_)
+    assert fr["glm_model_gss"].intercept_ == 0.25
+    with open(tmp_path / "raw.pkl", "wb") as f:          # a bare dict file loads too
+        pickle.dump({"fit_results": []}, f)
+    raw = sglm_save.GLM_data(str(tmp_path), "raw.pkl")
+    raw.load()
+    assert raw.data == {"fit_results": []}
+    np.save(tmp_path / "coef.npy", glm.coef_)
+    np.save(tmp_path / "icpt.npy", glm.intercept_)
+    c, b = np.load(tmp_path / "coef.npy"), np.load(tmp_path / "icpt.npy")
+    assert c.dtype == np.float64 and c.shape == (5,) and b.shape == () and float(b) == 0.25
