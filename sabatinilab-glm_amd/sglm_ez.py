@@ -160,3 +160,77 @@ def training_fit_holdout_score(X_setup, y_setup, X_holdout, y_holdout, best_para
     holdout_score = glm.r2_score(X_holdout, y_holdout)
     holdout_neg_mse_score = glm.neg_mse_score(X_holdout, y_holdout)
     return glm, holdout_score, holdout_neg_mse_score
+
+
+def holdout_resplit_cv(X, y, id_df, glm_kwarg_lst, num_runs=3, id_cols=('nTrial',),
+                       perc_holdout=0.2, num_folds=5, test_size=None, score_method='mse',
+                       package_style=False):
+    """Repeated holdout resplits batched on the resident design.
+
+    The production notebooks loop ``for irun in range(num_runs)``: holdout split by trial id,
+    folds on the setup rows, ``simple_cv_fit`` over the parameter list, then
+    ``training_fit_holdout_score`` (02-create_features-p50-Lass-Rid-rerun-smpl.ipynb cell 12).
+    Here the splits are drawn in that loop's RNG order (holdout, then folds, per run) and ALL
+    runs' fold fits, setup refits and holdout scores are one batched MI355X solve.
+
+    ``id_df`` holds the id columns aligned with the rows of X; ``package_style`` selects the
+    package split functions (sglm.models.split_data: ``'__'`` keys, holdout without
+    replacement) instead of the backend ones.  ``model_name`` is popped once from the kwargs
+    and used for every run (a sequential loop over the same dicts would fall back to
+    'Gaussian' after the first run, sglm_cv.py:288).  Returns, per run, a dict with
+    ``holdout`` (bool array), ``cv_idx`` (setup-relative, as the loop sees them),
+    ``best_score``, ``best_score_std``, ``best_params``, ``best_model``, ``full_cv_results``
+    and the best refit's ``holdout_score`` (R^2 / D^2) and ``holdout_neg_mse_score``."""
+    from sglm_hip import grid as _grid
+    if package_style:
+        from sglm.models import split_data as _sd
+        hsplit, cvsplit = _sd.holdout_split_by_trial_id, _sd.cv_idx_by_trial_id
+    else:
+        hsplit, cvsplit = holdout_split_by_trial_id, cv_idx_by_trial_id
+    id_df = pd.DataFrame(id_df).reset_index(drop=True)
+    id_cols = list(id_cols)
+    runs = []
+    for _ in range(num_runs):
+        hold = np.asarray(hsplit(id_df, id_cols=id_cols, perc_holdout=perc_holdout))
+        setup = np.flatnonzero(~hold)
+        cv_idx = cvsplit(id_df.iloc[setup].reset_index(drop=True),
+                         trial_id_columns=id_cols, num_folds=num_folds, test_size=test_size)
+        runs.append((hold, setup, cv_idx))
+    params = []
+    for glm_kwargs in glm_kwarg_lst:
+        glm_kwargs = dict(glm_kwargs)
+        mn = glm_kwargs.pop('model_name', 'Gaussian')
+        roll = glm_kwargs.pop('roll', 0)
+        params.append((mn, glm_kwargs, roll))
+    objectives = [sglm_.GLM(mn, **kw).model.objective() for mn, kw, _ in params]
+    rolls = [r for _, _, r in params]
+    groups = [{"cv_idx": [(setup[tr], setup[te]) for tr, te in cv_idx],
+               "objectives": objectives, "rolls": rolls, "refit_rows": setup,
+               "holdout_rows": np.flatnonzero(hold)} for hold, setup, cv_idx in runs]
+    Xv = X.values if hasattr(X, "values") and not isinstance(X, np.ndarray) else X
+    yv = np.asarray(y.values if hasattr(y, "values") else y, dtype=np.float64).reshape(-1)
+    res = _grid.run_multi(Xv, yv, groups, score_method=score_method)
+    out = []
+    for (hold, setup, cv_idx), rg in zip(runs, res):
+        full = []
+        for (mn, kw, roll), r in zip(params, rg):
+            glm = sglm_.GLM(mn, **kw)
+            glm._set_fitted(r["refit_coef"], r["refit_intercept"], max(r["n_iter"]))
+            d = {k: r[k] for k in ("cv_coefs", "cv_intercepts", "cv_scores_train",
+                                   "cv_scores_test", "cv_mean_score_train", "cv_mean_score",
+                                   "cv_std_score", "cv_R2_score", "cv_mse_score")}
+            d.update(glm_kwargs=kw, model=glm, holdout_score=r["refit_holdout_r2"],
+                     holdout_neg_mse_score=r["refit_holdout_neg_mse"])
+            full.append(d)
+        key = 'cv_R2_score' if score_method == 'r2' else 'cv_mean_score'
+        best = None
+        for i, d in enumerate(full):                 # first strict max (sglm_cv.py:402-415)
+            if best is None or d[key] > full[best][key]:
+                best = i
+        b = full[best]
+        out.append({"holdout": hold, "cv_idx": cv_idx, "best_score": b[key],
+                    "best_score_std": b["cv_std_score"], "best_params": b["glm_kwargs"],
+                    "best_model": b["model"], "full_cv_results": full,
+                    "holdout_score": b["holdout_score"],
+                    "holdout_neg_mse_score": b["holdout_neg_mse_score"]})
+    return out

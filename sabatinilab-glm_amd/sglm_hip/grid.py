@@ -134,6 +134,19 @@ def run(X, y, cv_idx, objectives: Sequence[Objective], rolls: Sequence[int],
 
     ``simulate=(rank, world)`` (development only) solves just that rank's share without a
     process group and returns the raw per-fit results instead of the assembled dicts."""
+    out = run_multi(X, y, [{"cv_idx": cv_idx, "objectives": objectives, "rolls": rolls}],
+                    score_method, coef0, intercept0, stats, shard, simulate)
+    return out if simulate is not None else out[0]
+
+
+def run_multi(X, y, groups: Sequence[dict], score_method: str = "mse", coef0=None,
+              intercept0=None, stats=None, shard=True, simulate=None):
+    """Several CV grids over ONE resident design, solved as one batch (SURVEY.md §8(f) 2:
+    holdout resplits).  Each group: ``cv_idx`` (global row indices), ``objectives``,
+    ``rolls``, optional ``refit_rows`` (the refit's rows; default all) and ``holdout_rows``
+    (rows the refits are also scored on).  Returns one list of per-param dicts per group;
+    with ``holdout_rows`` every dict also carries ``refit_holdout_r2`` (R^2 / D^2) and
+    ``refit_holdout_neg_mse`` — what ``training_fit_holdout_score`` reports for that param."""
     import time
     tick = stats.mark if (stats is not None and stats.trace_phases) else (lambda name, t: t)
     t0 = tick("-", time.perf_counter())
@@ -142,15 +155,31 @@ def run(X, y, cv_idx, objectives: Sequence[Objective], rolls: Sequence[int],
     y = np.asarray(y, dtype=np.float64).reshape(-1)
     if y.shape[0] != n:
         raise ValueError(f"y has {y.shape[0]} rows, X has {n}")
-    K = len(cv_idx)
-    fm = F.masks_from_cv_idx(cv_idx, n)
+    masks, mkey = [], {}
+
+    def add_mask(m):
+        k = m.tobytes()
+        if k not in mkey:
+            mkey[k] = len(masks)
+            masks.append(m)
+        return mkey[k]
+
+    def rows_mask(rows):
+        if rows is None:
+            return np.ones(n, np.uint8)
+        m = np.zeros(n, np.uint8)
+        m[np.asarray(rows, dtype=np.int64)] = 1
+        return m
+
+    gm = []                                  # per group: ([(train, test)], refit, holdout)
+    for g in groups:
+        fm = F.masks_from_cv_idx(g["cv_idx"], n)
+        splits = [(add_mask(tr), add_mask(te)) for tr, te in fm]
+        refit = add_mask(rows_mask(g.get("refit_rows")))
+        hold = g.get("holdout_rows")
+        gm.append((splits, refit, -1 if hold is None else add_mask(rows_mask(hold))))
     t0 = tick("setup_masks", t0)
-    masks = []
-    for tr, te in fm:
-        masks += [tr, te]
-    FULL = len(masks)
-    masks.append(np.ones(n, np.uint8))
-    roll_list = sorted(set(int(r) for r in rolls) | {0})
+    roll_list = sorted(set(int(r) for g in groups for r in g["rolls"]) | {0})
     ridx = {r: i for i, r in enumerate(roll_list)}
     ys = [np.roll(y, r) for r in roll_list]
     prob = E.Problem(design, ys, masks)
@@ -158,34 +187,39 @@ def run(X, y, cv_idx, objectives: Sequence[Objective], rolls: Sequence[int],
     ms = _MaskStats(prob)
     t0 = tick("setup_maskstats", t0)
 
-    # ---- fit table: (param j, split k) then refit (j, -1)
-    table = []
-    for j, (obj, roll) in enumerate(zip(objectives, rolls)):
-        if obj.family == E.FAM_TWEEDIE_LOG:
-            for r_, m_ in [(ridx[int(roll)], 2 * k) for k in range(K)] + [(0, FULL)]:
-                st = ms.get(r_, m_)
-                if st["cnt"] and (st["ymin"] < 0 or st["mean"] <= 0):
-                    raise ValueError("Some value(s) of y are out of the valid range of the loss "
-                                     "'HalfPoissonLoss'.")
-        for k in range(K):
-            table.append((j, k, 2 * k, ridx[int(roll)], 2 * k + 1))
-        table.append((j, -1, FULL, 0, -1))
+    # ---- fit table: per group, (param j, split k) then refit (j, -1)
+    table = []                               # (group, j, k, fit mask, resp, second score mask)
+    for gi, g in enumerate(groups):
+        splits, refit, hold = gm[gi]
+        for j, (obj, roll) in enumerate(zip(g["objectives"], g["rolls"])):
+            if obj.family == E.FAM_TWEEDIE_LOG:
+                for r_, m_ in [(ridx[int(roll)], tr) for tr, _ in splits] + [(0, refit)]:
+                    st = ms.get(r_, m_)
+                    if st["cnt"] and (st["ymin"] < 0 or st["mean"] <= 0):
+                        raise ValueError("Some value(s) of y are out of the valid range of the "
+                                         "loss 'HalfPoissonLoss'.")
+            for k, (tr, te) in enumerate(splits):
+                table.append((gi, j, k, tr, ridx[int(roll)], te))
+            table.append((gi, j, -1, refit, 0, hold))
     t0 = tick("grid_setup", t0)
     dist = _dist() if shard and simulate is None else None
     rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (simulate or (0, 1))
     mine = shard_indices(len(table), rank, world)
 
+    def objective(i):
+        return groups[table[i][0]]["objectives"][table[i][1]]
+
     results = {}
-    groups = {}
+    solve_groups = {}
     for i in mine:
-        obj = objectives[table[i][0]]
+        obj = objective(i)
         key = ("cd", 0.0) if obj.kind == "cd" else (obj.family, float(obj.power))
-        groups.setdefault(key, []).append(i)
-    for key, idxs in groups.items():
+        solve_groups.setdefault(key, []).append(i)
+    for key, idxs in solve_groups.items():
         reqs = []
         for i in idxs:
-            j, k, m, r, _ = table[i]
-            obj = objectives[j]
+            _, _, _, m, r, _ = table[i]
+            obj = objective(i)
             cnt = ms.get(r, m)["cnt"]
             reqs.append(E.FitReq(obj.family, obj.power, obj.lam(cnt), m, r, obj.fit_intercept,
                                  obj.max_iter,
@@ -194,14 +228,14 @@ def run(X, y, cv_idx, objectives: Sequence[Objective], rolls: Sequence[int],
         t0 = tick("fit_table", t0)
         if key[0] == "cd":
             from . import cd
-            res, eta = cd.enet_batch(prob, [objectives[table[i][0]] for i in idxs], reqs)
+            res, eta = cd.enet_batch(prob, [objective(i) for i in idxs], reqs)
             fam, power = E.FAM_SQUARED, 0.0
         else:
             res, eta = E.irls(prob, reqs, stats=stats)
             fam, power = key
         t0 = tick("solve", t0)
-        sets = np.array([[table[i][2], table[i][4]] for i in idxs], dtype=np.int32)
-        sums = E.score_sums(prob, fam, power, eta, [table[i][3] for i in idxs], sets)
+        sets = np.array([[table[i][3], table[i][5]] for i in idxs], dtype=np.int32)
+        sums = E.score_sums(prob, fam, power, eta, [table[i][4] for i in idxs], sets)
         for q, i in enumerate(idxs):
             rr = res[q]
             results[i] = (rr.coef, rr.intercept, rr.n_iter, rr.converged, sums[q])
@@ -211,51 +245,63 @@ def run(X, y, cv_idx, objectives: Sequence[Objective], rolls: Sequence[int],
     results = merge_results(results, dist)
 
     # ---- assemble per-param dicts (reference key order, backend/sglm_cv.py:188-200)
-    out = []
-    for j, obj in enumerate(objectives):
-        power = obj.power if obj.family == E.FAM_TWEEDIE_LOG else None
-        cv_coefs = np.zeros((p, K))
-        cv_b = np.zeros(K)
-        s_tr = np.zeros(K)
-        s_te = np.zeros(K)
-        ss_res = ss_tot = n_te = 0.0
-        n_iter = []
-        conv = True
-        refit = None
-        for i, (jj, k, m, r, mt) in enumerate(table):
-            if jj != j:
-                continue
-            coef, b, it, cv_ok, sums = results[i]
-            n_iter.append(it)
-            conv &= cv_ok
-            if k < 0:
-                refit = (coef, b)
-                continue
-            cv_coefs[:, k] = coef
-            cv_b[k] = b
-            s_tr[k] = _score(score_method, obj, sums[0], ms.get(r, m, power))
-            s_te[k] = _score(score_method, obj, sums[1], ms.get(r, mt, power))
-            ss_res += sums[1][0]
-            st_te = ms.get(r, mt)
-            ss_tot += st_te["sst"]
-            n_te += st_te["cnt"]
-        out.append({
-            "cv_coefs": cv_coefs,
-            "cv_intercepts": cv_b,
-            "cv_scores_train": s_tr,
-            "cv_scores_test": s_te,
-            "cv_mean_score_train": np.mean(s_tr),
-            "cv_mean_score": np.mean(s_te),
-            "cv_std_score": np.std(s_te),
-            "cv_R2_score": 0 if ss_tot == 0 else 1 - ss_res / ss_tot,
-            "cv_mse_score": ss_res / n_te if n_te else np.nan,
-            "refit_coef": refit[0],
-            "refit_intercept": refit[1],
-            "n_iter": n_iter,
-            "converged": conv,
-        })
+    out_all = []
+    for gi, g in enumerate(groups):
+        K = len(gm[gi][0])
+        out = []
+        for j, obj in enumerate(g["objectives"]):
+            power = obj.power if obj.family == E.FAM_TWEEDIE_LOG else None
+            cv_coefs = np.zeros((p, K))
+            cv_b = np.zeros(K)
+            s_tr = np.zeros(K)
+            s_te = np.zeros(K)
+            ss_res = ss_tot = n_te = 0.0
+            n_iter = []
+            conv = True
+            refit = None
+            hold_scores = None
+            for i, (gg, jj, k, m, r, mt) in enumerate(table):
+                if gg != gi or jj != j:
+                    continue
+                coef, b, it, cv_ok, sums = results[i]
+                n_iter.append(it)
+                conv &= cv_ok
+                if k < 0:
+                    refit = (coef, b)
+                    if mt >= 0:
+                        sth = ms.get(r, mt, power)
+                        hold_scores = (_score("r2", obj, sums[1], sth),
+                                       _score("mse", obj, sums[1], sth))
+                    continue
+                cv_coefs[:, k] = coef
+                cv_b[k] = b
+                s_tr[k] = _score(score_method, obj, sums[0], ms.get(r, m, power))
+                s_te[k] = _score(score_method, obj, sums[1], ms.get(r, mt, power))
+                ss_res += sums[1][0]
+                st_te = ms.get(r, mt)
+                ss_tot += st_te["sst"]
+                n_te += st_te["cnt"]
+            d = {
+                "cv_coefs": cv_coefs,
+                "cv_intercepts": cv_b,
+                "cv_scores_train": s_tr,
+                "cv_scores_test": s_te,
+                "cv_mean_score_train": np.mean(s_tr),
+                "cv_mean_score": np.mean(s_te),
+                "cv_std_score": np.std(s_te),
+                "cv_R2_score": 0 if ss_tot == 0 else 1 - ss_res / ss_tot,
+                "cv_mse_score": ss_res / n_te if n_te else np.nan,
+                "refit_coef": refit[0],
+                "refit_intercept": refit[1],
+                "n_iter": n_iter,
+                "converged": conv,
+            }
+            if hold_scores is not None:
+                d["refit_holdout_r2"], d["refit_holdout_neg_mse"] = hold_scores
+            out.append(d)
+        out_all.append(out)
     tick("assemble", t0)
-    return out
+    return out_all
 
 
 def _score(method, obj: Objective, sums, st):

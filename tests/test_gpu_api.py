@@ -281,3 +281,43 @@ def test_c1_shape_ols_vs_oracle(engine):
     assert abs(glm.intercept_ - b) < TOL_GAUSS * max(1.0, abs(b))
     pred = X[te] @ c + b
     assert abs(glm.neg_mse_score(X[te], s.y[te]) + np.mean((s.y[te] - pred) ** 2)) < 1e-6
+
+
+def test_holdout_resplit_cv_vs_sequential_oracle(engine):
+    """3 holdout resplits x (4 folds x 3 ridge/lasso params + refits) as ONE batched solve,
+    against the sequential loop restated with the oracle on the same RNG stream: splits
+    bit-exact, fold coefficients / scores and the best refit's holdout scores to tolerance."""
+    import sglm_ez
+    from sglm_hip import synth
+    s = synth.make(N=8000, m=5, L=3, family="gaussian", rho=0.12, seed=61, beta_scale=0.5)
+    X = s.dense_X()
+    ids = pd.DataFrame({"nTrial": s.trial})
+    kws = [{"alpha": 0.5, "l1_ratio": 0}, {"alpha": 5.0, "l1_ratio": 0},
+           {"alpha": 0.01, "l1_ratio": 1, "max_iter": 1000}]
+    np.random.seed(9)
+    out = sglm_ez.holdout_resplit_cv(X, s.y, ids, kws, num_runs=3, id_cols=["nTrial"],
+                                     perc_holdout=0.25, num_folds=4, score_method="r2")
+    np.random.seed(9)
+    codes = folds_ref.trial_bucket_codes([s.trial])
+    G = int(codes.max() + 1)
+    for run in out:
+        test_ids = np.random.choice(G, size=int(G * 0.25))          # backend: with replacement
+        hold = np.isin(codes, test_ids)
+        assert np.array_equal(run["holdout"], hold)
+        setup = np.flatnonzero(~hold)
+        sc = folds_ref.trial_bucket_codes([s.trial[setup]])
+        ref_idx = folds_ref.cv_idx_from_bucket_ids(sc, num_folds=4)
+        for (a, b), (c, d) in zip(run["cv_idx"], ref_idx):
+            assert np.array_equal(a, c) and np.array_equal(b, d)
+        ref = cv_ref.cv_mult(X[setup], s.y[setup], ref_idx, [dict(k) for k in kws],
+                             score_method="r2")
+        for g, q in zip(run["full_cv_results"], ref["full_cv_results"]):
+            assert rel(g["cv_coefs"], q["cv_coefs"]) < TOL_GAUSS
+            assert np.max(np.abs(g["cv_scores_test"] - q["cv_scores_test"])) < 1e-6
+        assert run["best_params"] == ref["best_params"]
+        qb = ref["full_cv_results"][ref["best_index"]]
+        pred = X[hold] @ qb["coef"] + qb["intercept"]
+        yh = s.y[hold]
+        r2 = 1 - np.sum((yh - pred) ** 2) / np.sum((yh - yh.mean()) ** 2)
+        assert abs(run["holdout_score"] - r2) < 1e-6
+        assert abs(run["holdout_neg_mse_score"] + np.mean((yh - pred) ** 2)) < 1e-6 * max(1, np.mean(yh ** 2))
