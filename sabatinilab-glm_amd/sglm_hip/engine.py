@@ -571,36 +571,35 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         _lib.call("sglm_loss_trials", fam, power, n, ld, B, _p(bf.eta), _p(bf.deta), _p(prob.Y),
                   _p(prob.M), _p(fit_resp), _p(fit_mask), _p(tv1), 5, _p(Ltr), _p(xtr_work), st)
         L = Ltr[: B * 5].view(B, 5).cpu().numpy().copy()
-        ts = [0.0, 1.0, 0.5, 0.25, 0.125]
+        ts = np.array([0.0, 1.0, 0.5, 0.25, 0.125])
         gdir = np.sum(g * delta, axis=1)
+        # penalty lam/2 |w + t d|^2 = lam/2 (A + 2 t Bq + t^2 C), vectorised over fits x trials
+        pb, pd_ = penal * beta, penal * delta
+        A_, B_, C_ = np.sum(pb * beta, 1), np.sum(pb * delta, 1), np.sum(pd_ * delta, 1)
+
+        def objectives(Lm, tv):
+            return Lm + 0.5 * lam[:, None] * (A_[:, None] + 2 * tv[None, :] * B_[:, None]
+                                              + tv[None, :] ** 2 * C_[:, None])
         step = np.zeros(B)
-        need_more = []
-        for k in act:
-            obj = [L[k, j] + 0.5 * lam[k] * np.sum(penal[k] * (beta[k] + ts[j] * delta[k]) ** 2)
-                   for j in range(5)]
-            chosen = None
-            for j in range(1, 5):
-                if obj[j] - obj[0] <= ARMIJO_SIGMA * ts[j] * gdir[k] or \
-                        abs(obj[j] - obj[0]) <= 1e-13 * abs(obj[0]):
-                    chosen = ts[j]
-                    break
-            if chosen is None:
-                need_more.append(k)
-            else:
-                step[k] = chosen
-        if need_more:
+        obj = objectives(L, ts)[act]
+        ok = ((obj[:, 1:] - obj[:, :1] <= ARMIJO_SIGMA * ts[None, 1:] * gdir[act, None]) |
+              (np.abs(obj[:, 1:] - obj[:, :1]) <= 1e-13 * np.abs(obj[:, :1])))
+        first = np.argmax(ok, axis=1)
+        hit = ok[np.arange(act.size), first]
+        step[act[hit]] = ts[1:][first[hit]]
+        need_more = act[~hit]
+        if need_more.size:
             _lib.call("sglm_loss_trials", fam, power, n, ld, B, _p(bf.eta), _p(bf.deta),
                       _p(prob.Y), _p(prob.M), _p(fit_resp), _p(fit_mask), _p(tv2), 7, _p(Ltr),
                       _p(xtr_work), st)
             L2 = Ltr[: B * 7].view(B, 7).cpu().numpy()
             ts2 = tv2.cpu().numpy().astype(np.float64)
-            for k in need_more:
-                obj0 = L[k, 0] + 0.5 * lam[k] * np.sum(penal[k] * beta[k] ** 2)
-                for j in range(7):
-                    o = L2[k, j] + 0.5 * lam[k] * np.sum(penal[k] * (beta[k] + ts2[j] * delta[k]) ** 2)
-                    if o - obj0 <= ARMIJO_SIGMA * ts2[j] * gdir[k]:
-                        step[k] = ts2[j]
-                        break
+            obj0 = objectives(L[:, :1], np.zeros(1))[need_more]
+            o2 = objectives(L2, ts2)[need_more]
+            ok2 = o2 - obj0 <= ARMIJO_SIGMA * ts2[None, :] * gdir[need_more, None]
+            f2 = np.argmax(ok2, axis=1)
+            h2 = ok2[np.arange(need_more.size), f2]
+            step[need_more[h2]] = ts2[f2[h2]]
         t0 = tick("it_linesearch", t0)
         # ---- update
         beta += step[:, None] * delta
@@ -615,14 +614,17 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
             nr = rows[act]
             stats.alg_flop += float(np.sum(nr * pa * (pa + 1) + 4.0 * nr * pa)
                                     + act.size * (pa ** 3 / 3 + 2 * pa * pa))
-        for k in act:
-            rel = np.max(np.abs(step[k] * delta[k])) / (1.0 + np.max(np.abs(beta[k])))
-            if step[k] == 0.0 or rel <= tol or (rel < 1e-4 and rel >= 0.5 * prev_rel[k]):
-                active[k] = False
-                converged[k] = step[k] != 0.0 or rel <= tol or np.max(np.abs(delta[k])) < 1e-5
-            elif n_iter[k] >= max_iter[k]:
-                active[k] = False
-            prev_rel[k] = rel
+        relv = (np.max(np.abs(step[act, None] * delta[act]), axis=1)
+                / (1.0 + np.max(np.abs(beta[act]), axis=1)))
+        stepa = step[act]
+        stop = (stepa == 0.0) | (relv <= tol) | ((relv < 1e-4) & (relv >= 0.5 * prev_rel[act]))
+        conv_now = stop & ((stepa != 0.0) | (relv <= tol) |
+                           (np.max(np.abs(delta[act]), axis=1) < 1e-5))
+        active[act[stop]] = False
+        converged[act[stop]] = conv_now[stop]
+        out_of_iters = ~stop & (n_iter[act] >= max_iter[act])
+        active[act[out_of_iters]] = False
+        prev_rel[act] = relv
         t0 = tick("it_update", t0)
 
     bf.prob = bf.keep = None            # drop the compacted designs with the problem

@@ -156,8 +156,12 @@ def run_multi(X, y, groups: Sequence[dict], score_method: str = "mse", coef0=Non
     if y.shape[0] != n:
         raise ValueError(f"y has {y.shape[0]} rows, X has {n}")
     masks, mkey = [], {}
+    dedup = len(groups) > 1                  # one grid's masks are distinct by construction
 
     def add_mask(m):
+        if not dedup:
+            masks.append(m)
+            return len(masks) - 1
         k = m.tobytes()
         if k not in mkey:
             mkey[k] = len(masks)
