@@ -321,3 +321,31 @@ def test_holdout_resplit_cv_vs_sequential_oracle(engine):
         r2 = 1 - np.sum((yh - pred) ** 2) / np.sum((yh - yh.mean()) ** 2)
         assert abs(run["holdout_score"] - r2) < 1e-6
         assert abs(run["holdout_neg_mse_score"] + np.mean((yh - pred) ** 2)) < 1e-6 * max(1, np.mean(yh ** 2))
+
+
+@pytest.mark.parametrize("n,p", [(7, 1), (63, 3), (65, 255), (1000, 256), (1000, 257),
+                                 (3000, 40)])
+def test_odd_shapes_vs_oracle(engine, n, p):
+    """Padding boundaries (P = 256, 512), rows below one 64-row K-step, ragged n, with and
+    without intercept, binary and real-valued designs: Poisson and ridge vs the oracle."""
+    import sglm
+    rng = np.random.default_rng(n * 1000 + p)
+    for binary in (True, False):
+        X = (rng.random((n, p)) < 0.3).astype(np.float64) if binary else rng.normal(0, 1, (n, p))
+        w = rng.normal(0, 0.3 / np.sqrt(p), p)
+        y = rng.poisson(np.exp(X @ w + 0.2)).astype(np.float64)
+        if y.sum() == 0:
+            y[0] = 1.0
+        for fi in (True, False):
+            a = 1.0
+            glm = sglm.GLM("Poisson", alpha=a, fit_intercept=fi)
+            glm.fit(X, y)
+            c, b = glm_ref.fit_tweedie_newton(X, y, a, 1.0, fit_intercept=fi)
+            assert rel(glm.coef_, c) < TOL_POIS, (n, p, binary, fi)
+            assert abs(glm.intercept_ - b) < TOL_POIS * max(1.0, abs(b)), (n, p, binary, fi)
+            yg = X @ w + rng.normal(0, 1, n)
+            glm = sglm.GLM("Normal", alpha=2.0, l1_ratio=0, fit_intercept=fi)
+            glm.fit(X, yg)
+            c, b = glm_ref.fit_ridge(X, yg, 2.0, fit_intercept=fi)
+            assert rel(glm.coef_, c) < TOL_GAUSS, (n, p, binary, fi, "ridge")
+            assert abs(glm.intercept_ - b) < TOL_GAUSS * max(1.0, abs(b))
