@@ -113,6 +113,26 @@ __device__ __forceinline__ u32x2 gld2(g_uint2* p) {
     asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
     return v;
 }
+// wave-uniform 64-bit base in an SGPR pair + per-lane 32-bit byte offset + immediate: no VALU
+// address arithmetic (the per-step advance is scalar)
+template <int IMM>
+__device__ __forceinline__ u32x2 gld2s(uint64_t sbase, uint32_t voff) {
+    u32x2 v;
+    asm volatile("global_load_dwordx2 %0, %1, %2 offset:%3"
+                 : "=v"(v)
+                 : "v"(voff), "s"(sbase), "i"(IMM)
+                 : "memory");
+    return v;
+}
+template <int IMM>
+__device__ __forceinline__ u32x4 gld4s(uint64_t sbase, uint32_t voff) {
+    u32x4 v;
+    asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3"
+                 : "=v"(v)
+                 : "v"(voff), "s"(sbase), "i"(IMM)
+                 : "memory");
+    return v;
+}
 __device__ __forceinline__ u32x4 gld4(g_uint4* p) {
     u32x4 v;
     asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");

@@ -828,14 +828,29 @@ struct Step6 {
     u32x4 w[4];
 };
 
-__device__ __forceinline__ void load6(Step6& t, g_uint2* pa, g_uint2* pb, g_uint4* pw,
-                                      int64_t s, int32_t P) {
-#pragma unroll
-    for (int m = 0; m < 4; ++m) t.a[m] = gld2(pa + s * P + 32 * m);
-#pragma unroll
-    for (int n = 0; n < 4; ++n) t.b[n] = gld2(pb + s * P + 32 * n);
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) t.w[ks] = gld4(pw + s * 8 + 2 * ks);
+// operand addresses of one wave: scalar bases at K-step 0 and per-step strides (bytes) plus
+// the lane's byte offsets (column r of the A / B blocks; row group h of the weights)
+struct Addr6 {
+    uint64_t a, b, w, stride_ab;
+    uint32_t voff_ab, voff_w;
+};
+
+__device__ __forceinline__ void load6(Step6& t, const Addr6& ad, int64_t s) {
+    const uint64_t sa = ad.a + (uint64_t)s * ad.stride_ab;
+    const uint64_t sb = ad.b + (uint64_t)s * ad.stride_ab;
+    const uint64_t sw = ad.w + (uint64_t)s * 128;
+    t.a[0] = gld2s<0>(sa, ad.voff_ab);
+    t.a[1] = gld2s<256>(sa, ad.voff_ab);
+    t.a[2] = gld2s<512>(sa, ad.voff_ab);
+    t.a[3] = gld2s<768>(sa, ad.voff_ab);
+    t.b[0] = gld2s<0>(sb, ad.voff_ab);
+    t.b[1] = gld2s<256>(sb, ad.voff_ab);
+    t.b[2] = gld2s<512>(sb, ad.voff_ab);
+    t.b[3] = gld2s<768>(sb, ad.voff_ab);
+    t.w[0] = gld4s<0>(sw, ad.voff_w);
+    t.w[1] = gld4s<32>(sw, ad.voff_w);
+    t.w[2] = gld4s<64>(sw, ad.voff_w);
+    t.w[3] = gld4s<96>(sw, ad.voff_w);
 }
 
 __device__ __forceinline__ void wait6(Step6& t) {
@@ -899,9 +914,8 @@ __device__ __forceinline__ void interleave16() {
 // `nxt` first and leaves F = sub-step 0 fragments of `nxt`.
 template <bool DIAG>
 __device__ __forceinline__ void half6(const Step6& cur, Step6& nxt, Frag6& F, int h,
-                                      f32x16 (&acc)[4][4], g_uint2* pa, g_uint2* pb,
-                                      g_uint4* pw, int64_t snext, int32_t P) {
-    load6(nxt, pa, pb, pw, snext, P);
+                                      f32x16 (&acc)[4][4], const Addr6& ad, int64_t snext) {
+    load6(nxt, ad, snext);
     __builtin_amdgcn_sched_barrier(0);
     Frag6 G;
     frags6(cur, 1, h, G);
@@ -920,17 +934,17 @@ __device__ __forceinline__ void half6(const Step6& cur, Step6& nxt, Frag6& F, in
 }
 
 template <bool DIAG>
-__device__ __forceinline__ void gram6_loop(f32x16 (&acc)[4][4], g_uint2* pa, g_uint2* pb,
-                                           g_uint4* pw, int nsteps, int h, int32_t P) {
+__device__ __forceinline__ void gram6_loop(f32x16 (&acc)[4][4], const Addr6& ad, int nsteps,
+                                           int h) {
     Step6 A, B;                                      // two register sets, one step in flight
     Frag6 F;
-    load6(A, pa, pb, pw, 0, P);
+    load6(A, ad, 0);
     wait6(A);
     frags6(A, 0, h, F);
     int s = 0;
     for (; s + 1 < nsteps; s += 2) {
-        half6<DIAG>(A, B, F, h, acc, pa, pb, pw, s + 1, P);
-        half6<DIAG>(B, A, F, h, acc, pa, pb, pw, s + 2 < nsteps ? s + 2 : nsteps - 1, P);
+        half6<DIAG>(A, B, F, h, acc, ad, s + 1);
+        half6<DIAG>(B, A, F, h, acc, ad, s + 2 < nsteps ? s + 2 : nsteps - 1);
     }
     if (s < nsteps) {                                // odd step count: last step from A
         Frag6 G;
@@ -964,9 +978,13 @@ syrk6_kernel(const int64_t* __restrict__ desc, int32_t P, int32_t splits,
     const int64_t blk1 = min(blk0 + sps, nblk);
     const int nsteps = blk1 > blk0 ? (int)(blk1 - blk0) : 0;
     const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
-    g_uint2* pa = bits + blk0 * P + bi * 128 + r;
-    g_uint2* pb = bits + blk0 * P + bj * 128 + r;
-    g_uint4* pw = reinterpret_cast<g_uint4*>(wbf + 2 * (blk0 * 64 + 8 * h));
+    Addr6 ad;
+    ad.a = reinterpret_cast<uint64_t>(bits + blk0 * P + bi * 128);
+    ad.b = reinterpret_cast<uint64_t>(bits + blk0 * P + bj * 128);
+    ad.w = (uint64_t)(wbf + 2 * blk0 * 64);
+    ad.stride_ab = (uint64_t)P * 8;
+    ad.voff_ab = 8u * r;
+    ad.voff_w = 16u * h;
 
     f32x16 acc[4][4];
 #pragma unroll
@@ -976,9 +994,9 @@ syrk6_kernel(const int64_t* __restrict__ desc, int32_t P, int32_t splits,
 
     if (nsteps > 0) {
         if (bi == bj)
-            gram6_loop<true>(acc, pa, pb, pw, nsteps, h, P);
+            gram6_loop<true>(acc, ad, nsteps, h);
         else
-            gram6_loop<false>(acc, pa, pb, pw, nsteps, h, P);
+            gram6_loop<false>(acc, ad, nsteps, h);
     }
     float* out = slab ? slab + ((int64_t)split * nact + slot) * (int64_t)P * P
                       : H + (int64_t)fit * P * P;
