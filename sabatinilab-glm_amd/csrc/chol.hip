@@ -68,10 +68,57 @@ __device__ __forceinline__ float lanef(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
+// rank-1 update of this lane's column by row q of U: a[i] -= U[q][i] * u for i > q, where
+// U[q][i] = lane i's u.  Chunks of 8 readlane + FMA pairs behind scheduling fences, so that the
+// scalar broadcasts are consumed as they are produced instead of all being hoisted (SGPR
+// spills).
+template <int Q>
+__device__ __forceinline__ void diag_rank1(float (&a)[kNB], float u) {
+#pragma unroll
+    for (int i0 = Q + 1; i0 < kNB; i0 += 8) {
+        float sc[8];                                 // broadcasts first: the readlane ->
+#pragma unroll                                       // VALU hazard is covered by distance
+        for (int i = i0; i < i0 + 8 && i < kNB; ++i) sc[i - i0] = lanef(u, i);
+#pragma unroll
+        for (int i = i0; i < i0 + 8 && i < kNB; ++i) a[i] = fmaf(-sc[i - i0], u, a[i]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int Q>
+__device__ __forceinline__ void diag_steps(float (&a)[kNB], float& rinv, int c, float thr,
+                                           int& myfrz, int& dropped) {
+    if constexpr (Q < kNB) {
+        // the pivot test runs lane-locally (lane Q's a[Q] against its own threshold) and only
+        // its verdict is broadcast: a broadcast of the loop-invariant threshold would be
+        // hoisted for all 64 steps and spilled
+        const int verdict = (myfrz ? 2 : 0) | (a[Q] > thr ? 0 : 1);
+        const int vq = __builtin_amdgcn_readlane(verdict, Q);
+        const bool was = (vq & 2) != 0;
+        const bool drop = vq != 0;
+        // uniform pivot arithmetic: d = sqrt(piv) and its reciprocal from one v_rsq
+        const float piv = lanef(a[Q], Q);
+        const float r = drop ? 0.0f : __builtin_amdgcn_rsqf(piv);
+        const float d = drop ? 1.0f : piv * r;
+        const float u = c > Q ? a[Q] * r : 0.0f;     // row Q of U (0 for a dropped pivot)
+        a[Q] = c == Q ? d : (c > Q ? u : a[Q]);
+        rinv = c == Q ? r : rinv;                    // lane Q keeps 1 / U[Q][Q] (0 if dropped)
+        // row Q is final from here on: materialise it now, or its selects sink to the store
+        // at the end and keep every step's masks and pivots live (SGPR spills)
+        asm volatile("" : "+v"(a[Q]), "+v"(rinv));
+        const bool newly = drop && !was && c == Q;
+        myfrz = newly ? 1 : myfrz;
+        dropped = newly ? 1 : dropped;
+        diag_rank1<Q>(a, u);
+        diag_steps<Q + 1>(a, rinv, c, thr, myfrz, dropped);
+    }
+}
+
 // One wave per fit: factor the diagonal block (refactor) and forward-solve the rhs block.
 // Lane c holds column c of the block in registers (a[r] = A[k0+r][k0+c]); step q reads the
 // pivot and row q of U with v_readlane (scalar broadcasts), so the whole 64-step
-// factorisation is register FMAs (entries below the diagonal are updated too and ignored).
+// factorisation is register FMAs (entries below the diagonal are updated too and ignored),
+// branch-free: lane-dependent choices are selects, pivot decisions are wave-uniform.
 __global__ void __launch_bounds__(64) chol_diag_kernel(
     float* __restrict__ Hall, int32_t P, int32_t k0, const int32_t* __restrict__ fits,
     uint8_t* __restrict__ frozen_all, float* __restrict__ rhs_all,
@@ -82,43 +129,45 @@ __global__ void __launch_bounds__(64) chol_diag_kernel(
     float* rhs = rhs_all + (int64_t)fit * P + k0;
     const int c = threadIdx.x;
     float a[kNB];
+    {
+        int cl = c;                                  // opaque copies of the lane index keep the
+        asm volatile("" : "+v"(cl));                 // load / store masks out of the steps' CSE
 #pragma unroll
-    for (int r = 0; r < kNB; ++r) a[r] = (r <= c) ? H[(int64_t)(k0 + r) * P + k0 + c] : 0.0f;
-    int myfrz = frz[c];
-    if (refactor) {
-        const float orig = diag_all[(int64_t)fit * P + k0 + c];
-        int dropped = 0;
-#pragma unroll
-        for (int q = 0; q < kNB; ++q) {
-            const float piv = lanef(a[q], q);
-            const bool was = __builtin_amdgcn_readlane(myfrz, q) != 0;
-            const bool drop = was || !(piv > 1e-6f * lanef(orig, q));
-            const float d = drop ? 1.0f : sqrtf(piv);
-            float u = 0.0f;
-            if (c > q && !drop) u = a[q] / d;
-            if (c == q) {
-                a[q] = d;
-                if (drop && !was) { myfrz = 1; dropped = 1; }
-            } else if (c > q) {
-                a[q] = u;
-            }
-#pragma unroll
-            for (int i = q + 1; i < kNB; ++i) a[i] -= lanef(u, i) * u;
+        for (int r = 0; r < kNB; ++r) {              // whole block (no branches), lower -> 0
+            const float v = H[(int64_t)(k0 + r) * P + k0 + c];
+            a[r] = r <= cl ? v : 0.0f;
         }
+    }
+    int myfrz = frz[c];
+    // lane q: 1 / U[q][q] (0 for a frozen pivot) -- one VGPR, not 64 uniform SGPRs
+    float rinv = 0.0f;
+    if (refactor) {
+        const float thr = 1e-6f * diag_all[(int64_t)fit * P + k0 + c];
+        int dropped = 0;
+        diag_steps<0>(a, rinv, c, thr, myfrz, dropped);
         if (dropped) atomicAdd(&info[fit], 1);
         frz[c] = (uint8_t)myfrz;
+        // whole block: the strictly-lower part is never read (consumers use row <= column)
 #pragma unroll
-        for (int r = 0; r < kNB; ++r)
-            if (r <= c) H[(int64_t)(k0 + r) * P + k0 + c] = a[r];
+        for (int r = 0; r < kNB; ++r) H[(int64_t)(k0 + r) * P + k0 + c] = a[r];
+    } else {
+        float ucc = 1.0f;                            // U[c][c] (selects: no dynamic index)
+#pragma unroll
+        for (int r = 0; r < kNB; ++r) ucc = r == c ? a[r] : ucc;
+        rinv = myfrz ? 0.0f : 1.0f / ucc;
     }
-    // forward solve U_kk^T z = rhs_k, lane = row: step q needs U[q][q] (lane q) and
-    // U[q][c] (this lane's a[q])
+    // forward solve U_kk^T z = rhs_k, lane = row: step q needs 1/U[q][q] and U[q][c] (this
+    // lane's a[q]); z_q = 0 for a frozen coordinate (rinv 0)
     float zc = rhs[c];
+    int cf = c;
+    asm volatile("" : "+v"(cf));                     // opaque copy: the factorisation's lane
+                                                     // masks are not CSE'd into 64 live pairs
 #pragma unroll
     for (int q = 0; q < kNB; ++q) {
-        const float zq = __builtin_amdgcn_readlane(myfrz, q) ? 0.0f : lanef(zc, q) / lanef(a[q], q);
-        if (c == q) zc = zq;
-        else if (c > q) zc -= a[q] * zq;
+        const float zq = lanef(zc, q) * lanef(rinv, q);
+        const float m = cf > q ? a[q] : 0.0f;
+        zc = fmaf(-m, zq, zc);
+        zc = cf == q ? zq : zc;
     }
     rhs[c] = zc;
 }
@@ -224,9 +273,9 @@ __global__ void __launch_bounds__(kCT) chol_update_kernel(float* __restrict__ Ha
 }
 
 // Blocked back substitution U x = z, then delta = -x.  Per 64-block (last to first): the
-// four waves form the 64 row dot products with the solved tail (16 independent accumulators
-// per wave, all loads in flight together), then wave 0 solves the 64 x 64 triangle with
-// readlane broadcasts.
+// four waves form the 64 row dot products with the solved tail (16 rows per wave, four
+// 64-column chunks per pass: 64 loads in flight per lane), then wave 0 solves the 64 x 64
+// triangle with readlane broadcasts, branch-free.
 __global__ void __launch_bounds__(kCT) chol_back_kernel(
     const float* __restrict__ Hall, int32_t P, const int32_t* __restrict__ fits,
     const uint8_t* __restrict__ frozen_all, float* __restrict__ rhs_all,
@@ -247,10 +296,24 @@ __global__ void __launch_bounds__(kCT) chol_back_kernel(
         float acc[kNB / 4];
 #pragma unroll
         for (int rr = 0; rr < kNB / 4; ++rr) acc[rr] = 0.0f;
-        for (int j = k0 + kNB + lane; j < P; j += 64) {
+        int j = k0 + kNB + lane;
+        for (; j + 3 * 64 < P; j += 4 * 64) {
+            float h[4][kNB / 4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int rr = 0; rr < kNB / 4; ++rr) h[u][rr] = H[(int64_t)(r0 + rr) * P + j + 64 * u];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const float xj = x[j + 64 * u];
+#pragma unroll
+                for (int rr = 0; rr < kNB / 4; ++rr) acc[rr] = fmaf(h[u][rr], xj, acc[rr]);
+            }
+        }
+        for (; j < P; j += 64) {
             const float xj = x[j];
 #pragma unroll
-            for (int rr = 0; rr < kNB / 4; ++rr) acc[rr] += H[(int64_t)(r0 + rr) * P + j] * xj;
+            for (int rr = 0; rr < kNB / 4; ++rr) acc[rr] = fmaf(H[(int64_t)(r0 + rr) * P + j], xj, acc[rr]);
         }
 #pragma unroll
         for (int rr = 0; rr < kNB / 4; ++rr) {
@@ -266,13 +329,19 @@ __global__ void __launch_bounds__(kCT) chol_back_kernel(
         __syncthreads();
         if (wave == 0) {
             float v = z[k0 + lane] - part[lane];
-            const int fr = frz[k0 + lane];
-            const float dgl = sD[lane][lane];
+            const float rd = frz[k0 + lane] ? 0.0f : 1.0f / sD[lane][lane];
+            int l = lane;                            // opaque per block: the lane masks are
+            asm volatile("" : "+v"(l));              // not hoisted out of the kb loop (spills)
+            // this lane's row of U_kk, read once (sD is 0 below the diagonal, and lane q's
+            // own update at step q is overwritten by x_q, so no mask is needed)
+            float row[kNB];
+#pragma unroll
+            for (int q = 0; q < kNB; ++q) row[q] = sD[lane][q];
 #pragma unroll
             for (int q = kNB - 1; q >= 0; --q) {
-                const float xq = __builtin_amdgcn_readlane(fr, q) ? 0.0f : lanef(v, q) / lanef(dgl, q);
-                if (lane == q) v = xq;
-                else if (lane < q) v -= sD[lane][q] * xq;
+                const float xq = lanef(v * rd, q);   // lane-local product, one broadcast
+                v = fmaf(-row[q], xq, v);
+                v = l == q ? xq : v;
             }
             x[k0 + lane] = v;
         }

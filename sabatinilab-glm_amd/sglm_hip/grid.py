@@ -13,9 +13,10 @@ Restates the arithmetic of ``cv_glm_single_params`` / ``cv_glm_mult_params``
 * ``cv_R2_score`` pools the test residuals of all splits against per-split test means
   (calc_R2 over concatenations, :196), ``cv_mse_score`` = mean squared pooled residual.
 
-Fits are independent, so with ``torch.distributed`` initialised the fit list is dealt
-round-robin over ranks and the per-fit results are all-gathered (one RCCL collective over
-xGMI at the end).
+Fits are independent, so with ``torch.distributed`` initialised the fit list is cut into
+contiguous, row-cost-balanced chunks of a mask-major order (``shard_plan``: each rank holds
+few masks, so it compacts and first-iterates few of them) and the per-fit results are
+all-gathered (one RCCL collective over xGMI at the end).
 """
 from __future__ import annotations
 
@@ -110,9 +111,36 @@ def _dist():
     return None
 
 
+SHARD_PLAN = "mask_major"                    # or "round_robin" (comparison runs)
+
+
 def shard_indices(total: int, rank: int, world: int):
-    """Round-robin deal of the fit table over ranks (fit i -> rank i mod world)."""
+    """Round-robin deal of a list over ranks (item i -> rank i mod world)."""
     return [i for i in range(total) if i % world == rank]
+
+
+def snake(j: int, count: int) -> int:
+    """Position of parameter j in the order 0, count-1, 1, count-2, ...: neighbours in this
+    order pair a weakly and a strongly penalised fit, so contiguous chunks of it mix fits
+    that need many and few Newton iterations."""
+    return 2 * j if j < (count + 1) // 2 else 2 * (count - 1 - j) + 1
+
+
+def shard_plan(keys: Sequence[tuple], costs: Sequence[float], rank: int, world: int):
+    """Indices of the fits rank ``rank`` of ``world`` solves: the fits sorted by ``keys``
+    (mask-major), then cut into ``world`` contiguous chunks of near-equal summed cost (a fit
+    goes to the chunk holding the midpoint of its cost interval).  Every fit lands on exactly
+    one rank; a rank's fits share few row masks, so its first Newton iteration (all fits of
+    one mask start from the same coefficients) and its per-mask bit-plane compaction cover
+    few masks instead of all of them, as a round-robin deal would."""
+    order = sorted(range(len(keys)), key=lambda i: keys[i])
+    c = np.asarray([float(costs[i]) for i in order])
+    total = c.sum()
+    if world <= 1 or total <= 0:
+        return sorted(order) if world <= 1 else shard_indices(len(keys), rank, world)
+    mid = np.cumsum(c) - 0.5 * c
+    owner = np.minimum((mid * world / total).astype(np.int64), world - 1)
+    return sorted(order[q] for q in range(len(order)) if owner[q] == rank)
 
 
 def merge_results(local: dict, dist=None) -> dict:
@@ -208,7 +236,15 @@ def run_multi(X, y, groups: Sequence[dict], score_method: str = "mse", coef0=Non
     t0 = tick("grid_setup", t0)
     dist = _dist() if shard and simulate is None else None
     rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (simulate or (0, 1))
-    mine = shard_indices(len(table), rank, world)
+    if world > 1 and SHARD_PLAN == "round_robin":
+        mine = shard_indices(len(table), rank, world)
+    elif world > 1:
+        njs = [len(g["objectives"]) for g in groups]
+        keys = [(t[3], t[4], snake(t[1], njs[t[0]]), t[0], t[1]) for t in table]
+        costs = [ms.get(t[4], t[3])["cnt"] for t in table]
+        mine = shard_plan(keys, costs, rank, world)
+    else:
+        mine = list(range(len(table)))
 
     def objective(i):
         return groups[table[i][0]]["objectives"][table[i][1]]

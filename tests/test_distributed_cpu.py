@@ -55,3 +55,28 @@ def test_shard_indices_cover_exactly_once():
     for world in (1, 2, 3, 8):
         allidx = sorted(i for r in range(world) for i in grid.shard_indices(120, r, world))
         assert allidx == list(range(120))
+
+
+def test_shard_plan_mask_major_balanced():
+    """C4's table (20 lambdas x (5 folds + refit)) over 1..8 ranks: every fit on exactly one
+    rank, per-rank row cost balanced, each rank spanning at most one mask more than its share
+    needs (round-robin gives every rank all 6), and each rank mixes weakly and strongly penalised fits."""
+    from sglm_hip import grid
+    nlam, K = 20, 5
+    table = [(j, k) for j in range(nlam) for k in list(range(K)) + [K]]   # (lambda, mask)
+    rows = [800_000] * K + [1_000_000]
+    keys = [(k, 0, grid.snake(j, nlam), 0, j) for j, k in table]
+    costs = [rows[k] for _, k in table]
+    for world in (1, 2, 3, 4, 8):
+        plan = [grid.shard_plan(keys, costs, r, world) for r in range(world)]
+        assert sorted(i for p in plan for i in p) == list(range(len(table)))
+        load = [sum(costs[i] for i in p) for p in plan]
+        assert max(load) - min(load) <= 2 * max(rows)
+        per_rank = -(-len(table) // world)
+        assert max(len({table[i][1] for i in p}) for p in plan) <= -(-per_rank // nlam) + 1
+        for p in plan:
+            if len(p) >= 4:
+                lams = [table[i][0] for i in p]
+                assert min(lams) < nlam // 2 <= max(lams)
+    assert [grid.snake(j, 5) for j in range(5)] == [0, 2, 4, 3, 1]
+    assert sorted(grid.snake(j, 6) for j in range(6)) == list(range(6))

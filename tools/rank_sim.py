@@ -1,7 +1,9 @@
 """Per-rank cost of an N-GPU C4 grid, simulated on one GPU (development tool).
 
-python tools/rank_sim.py --world 8 : solves rank 0's share (fits i % 8 == 0) of the C4 grid
-after a warm-up, with device syncs at phase boundaries, and prints the phase breakdown.
+python tools/rank_sim.py --world 8 [--rank R | --all] [--plan mask_major|round_robin] :
+solves one rank's share of the C4 grid (grid.shard_plan) after a warm-up, with device syncs
+at phase boundaries, and prints the phase breakdown; --all times every rank and reports the
+max over ranks (what an N-GPU grid's wall-clock follows).
 """
 import argparse
 import json
@@ -20,6 +22,8 @@ def main():
     ap.add_argument("--config", default="c4")
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--rank", type=int, default=0)
+    ap.add_argument("--all", action="store_true")
+    ap.add_argument("--plan", default="mask_major")
     a = ap.parse_args()
     import bench
     import pandas as pd
@@ -34,6 +38,22 @@ def main():
     cv_idx = folds.cv_idx_from_bucket_ids(codes, num_folds=K)
     objs = [Objective("irls", E.FAM_TWEEDIE_LOG, 1.0, float(al), "n", True, 100)
             for al in np.logspace(-4, 1, nlam)]
+    grid.SHARD_PLAN = a.plan
+    if a.all:
+        per = []
+        for r in range(a.world):
+            sim = (r, a.world)
+            grid.run(d, s.y, cv_idx, objs, [0] * nlam, simulate=sim)
+            st = E.IrlsStats(record=True)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            res = grid.run(d, s.y, cv_idx, objs, [0] * nlam, stats=st, simulate=sim)
+            torch.cuda.synchronize()
+            per.append({"rank": r, "wall_ms": round((time.perf_counter() - t0) * 1e3, 2),
+                        "fits": len(res), "fit_iters": st.fit_iters, "gram_fits": st.gram_fits})
+        print(json.dumps({"plan": a.plan, "world": a.world, "per_rank": per,
+                          "max_ms": max(q["wall_ms"] for q in per)}))
+        return
     sim = (a.rank, a.world)
     grid.run(d, s.y, cv_idx, objs, [0] * nlam, simulate=sim)
     out = {}
