@@ -269,7 +269,7 @@ def main():
     kflop = sum(nact_flop for _, _, _, nact_flop in stats.syrk_events)
     nlaunch = len(stats.syrk_events)
     t = torch.tensor([elapsed, float(stats.fit_iters), ktime, kflop, float(nlaunch),
-                      float(stats.gram_fits), stats.alg_flop],
+                      float(stats.gram_fits), stats.alg_flop, float(stats.reused)],
                      dtype=torch.float64, device="cuda" if a.dist_backend == "nccl" else "cpu")
     if world > 1:
         mx = t.clone()
@@ -278,10 +278,11 @@ def main():
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         elapsed, fit_iters = float(mx[0]), float(sm[1])
         ktime, kflop, nlaunch = float(sm[2]), float(sm[3]), int(sm[4])
-        gram_fits, alg_flop = float(sm[5]), float(sm[6])
+        gram_fits, alg_flop, reused = float(sm[5]), float(sm[6]), float(sm[7])
     else:
         fit_iters = float(stats.fit_iters)
         gram_fits, alg_flop = float(stats.gram_fits), stats.alg_flop
+        reused = float(stats.reused)
     if rank == 0:
         pa = s.p + 1
         achieved = kflop / ktime / 1e12 if ktime > 0 else 0.0
@@ -311,6 +312,8 @@ def main():
                 "grid_wall_s": elapsed / a.steps,
                 "fit_iters_per_grid": fit_iters / a.steps,
                 "distinct_hessians_per_grid": gram_fits / a.steps,
+                "kept_factor_fit_iters_per_grid": reused / a.steps,
+                "hess_reuse_tol": E.HESS_REUSE_TOL,
                 "grid_roofline_frac": alg_flop / elapsed / (world * PEAK_BF16_TFLOPS * 1e12),
                 "grid_roofline_note": "SURVEY.md 8(d): sum over fit-iterations of "
                                       "n p'(p'+1) + 4 n p' + p'^3/3 + 2 p'^2, / wall / "

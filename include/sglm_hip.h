@@ -236,6 +236,21 @@ int sglm_loss_trials(int32_t family, float power, int64_t n, int64_t ld, int32_t
 int sglm_eta_axpy(int64_t n, int64_t ld, int32_t B, const float* step, const float* deta,
                   float* eta, sglm_stream_t stream);
 
+/* sglm_eta_axpy plus dmax[k] = max over the rows of mask fit_mask[k] of |step[k] d_eta[k][i]|
+ * (B floats, zeroed by the call): the per-step drift of the linear predictor that bounds the
+ * relative change of the IRLS weights since a fit's Hessian was formed (engine.irls reuses a
+ * factor while the accumulated drift stays below SGLM Hessian-reuse tolerance). */
+int sglm_eta_axpy_max(int64_t n, int64_t ld, int32_t B, const float* step, const float* deta,
+                      const uint8_t* M, const int32_t* fit_mask, float* eta, float* dmax,
+                      sglm_stream_t stream);
+
+/* out[q] = max over the rows of mask fit_mask[a] of |eta[a][i] - eta[b][i]| for the fit pairs
+ * (a, b) = (pairs[2q], pairs[2q+1]) of one mask (npairs floats, zeroed by the call).  engine.irls
+ * lets fit b take its Hessian from fit a's Gram when this distance is within tolerance. */
+int sglm_eta_pair_absmax(int64_t n, int64_t ld, int32_t npairs, const int32_t* pairs,
+                         const uint8_t* M, const int32_t* fit_mask, const float* eta,
+                         float* out, sglm_stream_t stream);
+
 /* Scores (GLM.score / get_residuals, backend/sglm.py:150-184, 314-331): for fit k and each
  * set s in {0, 1} with mask sets[2k + s] (-1 = empty):
  *   out[k][s][0] = sum_i M * (y_i - mu_i)^2,  out[k][s][1] = sum_i M * loss(y_i, eta_i),

@@ -339,6 +339,62 @@ __global__ void __launch_bounds__(256) eta_axpy_kernel(int64_t n, int64_t ld,
         eta[(int64_t)k * ld + i] += t * deta[(int64_t)k * ld + i];
 }
 
+// eta += t * deta, and dmax[k] = max_i |t * deta[k][i]| over the fit's mask rows (the
+// drift bound that decides whether fit k may keep its Hessian factor).  dmax must be zeroed;
+// non-negative floats order like their bit patterns, so an unsigned atomicMax reduces them.
+__global__ void __launch_bounds__(256) eta_axpy_max_kernel(int64_t n, int64_t ld,
+                                                           const float* __restrict__ step,
+                                                           const float* __restrict__ deta,
+                                                           const uint8_t* __restrict__ M,
+                                                           const int32_t* __restrict__ fit_mask,
+                                                           float* __restrict__ eta,
+                                                           float* __restrict__ dmax) {
+    const int k = blockIdx.y;
+    const float t = step[k];
+    if (t == 0.0f) return;
+    const uint8_t* m = M + (int64_t)fit_mask[k] * ld;
+    float mx = 0.0f;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * 256) {
+        const float dv = t * deta[(int64_t)k * ld + i];
+        eta[(int64_t)k * ld + i] += dv;
+        if (m[i]) mx = fmaxf(mx, fabsf(dv));
+    }
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    __shared__ float sh[4];
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        mx = fmaxf(fmaxf(sh[0], sh[1]), fmaxf(sh[2], sh[3]));
+        atomicMax(reinterpret_cast<unsigned int*>(dmax + k), __float_as_uint(mx));
+    }
+}
+
+// out[q] = max over the rows of mask fit_mask[a] of |eta[a][i] - eta[b][i]|, (a, b) =
+// pairs[2q], pairs[2q+1] (same mask): how far apart the IRLS weights of two fits are, which
+// decides whether b may be factored from a's Gram.  out must be zeroed.
+__global__ void __launch_bounds__(256) eta_pair_absmax_kernel(
+    int64_t n, int64_t ld, const int32_t* __restrict__ pairs, const uint8_t* __restrict__ M,
+    const int32_t* __restrict__ fit_mask, const float* __restrict__ eta, float* __restrict__ out) {
+    const int q = blockIdx.y;
+    const int a = pairs[2 * q], b = pairs[2 * q + 1];
+    const float* ea = eta + (int64_t)a * ld;
+    const float* eb = eta + (int64_t)b * ld;
+    const uint8_t* m = M + (int64_t)fit_mask[a] * ld;
+    float mx = 0.0f;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * 256)
+        if (m[i]) mx = fmaxf(mx, fabsf(ea[i] - eb[i]));
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    __shared__ float sh[4];
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        mx = fmaxf(fmaxf(sh[0], sh[1]), fmaxf(sh[2], sh[3]));
+        atomicMax(reinterpret_cast<unsigned int*>(out + q), __float_as_uint(mx));
+    }
+}
+
 static unsigned grid1(int64_t work, int64_t per_block, unsigned cap = 8192) {
     int64_t g = (work + per_block - 1) / per_block;
     if (g < 1) g = 1;
@@ -474,6 +530,42 @@ int sglm_eta_axpy(int64_t n, int64_t ld, int32_t B, const float* step, const flo
     dim3 grid(grid1(n, 256, 1024), (unsigned)B);
     eta_axpy_kernel<<<grid, 256, 0, as_stream(stream)>>>(n, ld, step, deta, eta);
     return check_launch("eta_axpy_kernel");
+}
+
+int sglm_eta_axpy_max(int64_t n, int64_t ld, int32_t B, const float* step, const float* deta,
+                      const uint8_t* M, const int32_t* fit_mask, float* eta, float* dmax,
+                      sglm_stream_t stream) {
+    if (B <= 0) return SGLM_OK;
+    if (!step || !deta || !M || !fit_mask || !eta || !dmax) {
+        set_error("sglm_eta_axpy_max: null pointer");
+        return SGLM_EINVAL;
+    }
+    hipStream_t s = as_stream(stream);
+    if (hipMemsetAsync(dmax, 0, sizeof(float) * (size_t)B, s) != hipSuccess) {
+        set_error("sglm_eta_axpy_max: hipMemsetAsync failed");
+        return SGLM_EHIP;
+    }
+    dim3 grid(grid1(n, 256, 1024), (unsigned)B);
+    eta_axpy_max_kernel<<<grid, 256, 0, s>>>(n, ld, step, deta, M, fit_mask, eta, dmax);
+    return check_launch("eta_axpy_max_kernel");
+}
+
+int sglm_eta_pair_absmax(int64_t n, int64_t ld, int32_t npairs, const int32_t* pairs,
+                         const uint8_t* M, const int32_t* fit_mask, const float* eta,
+                         float* out, sglm_stream_t stream) {
+    if (npairs <= 0) return SGLM_OK;
+    if (!pairs || !M || !fit_mask || !eta || !out) {
+        set_error("sglm_eta_pair_absmax: null pointer");
+        return SGLM_EINVAL;
+    }
+    hipStream_t s = as_stream(stream);
+    if (hipMemsetAsync(out, 0, sizeof(float) * (size_t)npairs, s) != hipSuccess) {
+        set_error("sglm_eta_pair_absmax: hipMemsetAsync failed");
+        return SGLM_EHIP;
+    }
+    dim3 grid(grid1(n, 256, 256), (unsigned)npairs);
+    eta_pair_absmax_kernel<<<grid, 256, 0, s>>>(n, ld, pairs, M, fit_mask, eta, out);
+    return check_launch("eta_pair_absmax_kernel");
 }
 
 int sglm_score_sums(int32_t family, float power, int64_t n, int64_t ld, int32_t B,

@@ -57,6 +57,8 @@ SIGNATURES = {
     "sglm_loss_trials": (C.c_int, [_i32, _f32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
                                    _vp, _i32, _vp, _vp, _vp]),
     "sglm_eta_axpy": (C.c_int, [_i64, _i64, _i32, _vp, _vp, _vp, _vp]),
+    "sglm_eta_axpy_max": (C.c_int, [_i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "sglm_eta_pair_absmax": (C.c_int, [_i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "sglm_score_sums": (C.c_int, [_i32, _f32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
                                   _vp, _vp]),
     "sglm_enet_work_bytes": (_sz, [_i32, _i32]),

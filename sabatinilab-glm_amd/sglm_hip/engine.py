@@ -48,6 +48,17 @@ XTR_BITS = True                # X^T R on the MFMA from compacted bit-planes for
 ETA_BITS = True                # eta on the MFMA from row-major bit-planes for 0/1 designs
 SYRK_CBITS = True              # ... and its row-compacted register-only form (v6) when fits
                                # carry masks (the default path for event designs)
+# Hessian reuse (log-link families): a fit keeps its last Hessian factor while the drift of
+# its linear predictor since that Hessian was formed, D = sum of max_i |t d_eta_i| over the
+# steps taken since, stays <= HESS_REUSE_TOL.  The IRLS weights then differ from the ones the
+# factor holds by a factor in [e^-cD, e^cD] (c = max(1, |2 - power|)), which bounds the
+# contraction of the inexact-Newton step by e^cD - 1; the fixed point (exact gradient) is
+# unchanged.  0 disables reuse.
+HESS_REUSE_TOL = float(__import__("os").environ.get("SGLM_HESS_REUSE_TOL", "0.0625"))
+# Hessian sharing: among fits of one (mask, response) that need a new Hessian, a fit whose
+# predictor is within HESS_SHARE_TOL (max over its mask rows) of another's is factored from
+# that fit's Gram, and starts its drift count at that distance (same bound as above).
+HESS_SHARE_TOL = float(__import__("os").environ.get("SGLM_HESS_SHARE_TOL", "0.0625"))
 
 
 def require_gpu():
@@ -369,6 +380,7 @@ class IrlsStats:
     fit_iters: int = 0
     newton_iters: int = 0
     gram_fits: int = 0                                  # distinct Hessians formed
+    reused: int = 0                                     # fit-iterations that kept a factor
     alg_flop: float = 0.0       # SURVEY.md §8(d) F summed over fit-iterations
     trace_phases: bool = False                          # sync + time grid phases (tools)
     phases: dict = field(default_factory=dict)          # host wall seconds per phase
@@ -496,6 +508,13 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
     d.eta(bf.beta, bf.eta)
 
     const_hess = fam == FAM_SQUARED
+    reuse_tol = 0.0 if const_hess else HESS_REUSE_TOL / max(1.0, abs(2.0 - power))
+    share_tol = 0.0 if const_hess else min(HESS_SHARE_TOL / max(1.0, abs(2.0 - power)),
+                                           reuse_tol)
+    drift = np.full(B, np.inf)          # predictor drift since each fit's Hessian was formed
+    dmax_d = torch.zeros(B, dtype=torch.float32, device=dev)
+    dmax_h = torch.zeros(B, dtype=torch.float32).pin_memory()
+    gram_now = np.zeros(B, dtype=bool)
     active = np.ones(B, dtype=bool)
     n_iter = np.zeros(B, dtype=np.int64)
     converged = np.zeros(B, dtype=bool)
@@ -524,9 +543,12 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                   _p(fit_resp), _p(fit_mask), _p(bf.W), _p(bf.R), st)
         d.xtr(bf.R, B, bf.g)
         g = bf.g.cpu().numpy() + lam[:, None] * penal * beta
+        if it > 0 and not const_hess:
+            drift += dmax_h.numpy().astype(np.float64)
         t0 = tick("it_gradient", t0)
         # ---- Hessian
         if const_hess:
+            gram_now[:] = not factored
             if not factored:
                 reps = {}
                 for k in act:
@@ -541,28 +563,46 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
             # Fits whose weights are bitwise identical have identical Hessians: same mask,
             # response and coefficients (every fit of a mask/response pair in the first
             # iteration, which starts from the intercept-only model).  Form each distinct
-            # Hessian once and copy it.
+            # Hessian once and copy it.  Fits whose predictor drifted less than reuse_tol
+            # since their last Hessian keep its factor (no Gram, no factorisation).
+            keep = act[drift[act] <= reuse_tol]
+            form = act[drift[act] > reuse_tol]
             reps = {}
             dup = []
-            for k in act:
+            for k in form:
                 key = (reqs[k].mask, reqs[k].resp, beta[k].tobytes())
                 rk = reps.setdefault(key, k)
                 if rk != k:
                     dup.append((k, rk))
             uniq = np.array(sorted(reps.values()), dtype=np.int32)
+            drift[form] = 0.0
+            if share_tol > 0.0 and uniq.size > 1:
+                uniq, shared = _share_grams(bf, prob, reqs, lam, uniq, share_tol, n, ld, st)
+                for k, rk, dist_k in shared:
+                    dup.append((k, rk))
+                    drift[k] = dist_k
             _syrk(d, bf, uniq, nsteps, ntile1, stats, st, rows=rows)
             for k, rk in dup:
                 bf.H[k].copy_(bf.H[rk])
+            gram_now[:] = False
+            gram_now[form] = True
             if stats is not None:
                 stats.gram_fits += int(uniq.size)
+                stats.reused += int(keep.size)
         t0 = tick("it_gram", t0)
-        refactor = 0 if (const_hess and factored) else 1
         bf.gtot.copy_(torch.from_numpy(g))
-        act_d = torch.tensor(act, dtype=torch.int32, device=dev)
         bf.delta.zero_()
-        _lib.call("sglm_chol_solve_ex", _p(bf.H), P, _p(act_d), int(act.size), _p(bf.gtot),
-                  _p(bf.dshift), _p(bf.delta), _p(bf.info), _p(bf.frozen), refactor, B,
-                  _p(bf.cwork), st)
+        if const_hess:
+            solves = [(act, 0 if factored else 1)]
+        else:
+            solves = [(form, 1), (keep, 0)]
+        for fits_s, refactor in solves:
+            if fits_s.size == 0:
+                continue
+            fits_d = torch.tensor(fits_s, dtype=torch.int32, device=dev)
+            _lib.call("sglm_chol_solve_ex", _p(bf.H), P, _p(fits_d), int(fits_s.size),
+                      _p(bf.gtot), _p(bf.dshift), _p(bf.delta), _p(bf.info), _p(bf.frozen),
+                      refactor, B, _p(bf.cwork), st)
         factored = True
         d.eta(bf.delta, bf.deta)
         delta = bf.delta.cpu().numpy().astype(np.float64)
@@ -605,15 +645,22 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         beta += step[:, None] * delta
         bf.beta.copy_(torch.from_numpy(beta.astype(np.float32)))
         step_d = torch.from_numpy(step.astype(np.float32)).to(dev)
-        _lib.call("sglm_eta_axpy", n, ld, B, _p(step_d), _p(bf.deta), _p(bf.eta), st)
+        _lib.call("sglm_eta_axpy_max", n, ld, B, _p(step_d), _p(bf.deta), _p(prob.M),
+                  _p(fit_mask), _p(bf.eta), _p(dmax_d), st)
+        if not const_hess:
+            # read back with the next iteration's gradient sync (no extra stall here)
+            dmax_h.copy_(dmax_d, non_blocking=True)
         n_iter[act] += 1
         if stats is not None:
             stats.newton_iters += 1
             stats.fit_iters += int(act.size)
+            # SURVEY.md §8(d) F per fit-iteration; the Gram and factorisation terms only for
+            # fit-iterations that took a new Hessian (a kept factor costs two triangular solves)
             pa = float(p + 1)
             nr = rows[act]
-            stats.alg_flop += float(np.sum(nr * pa * (pa + 1) + 4.0 * nr * pa)
-                                    + act.size * (pa ** 3 / 3 + 2 * pa * pa))
+            newh = gram_now[act]
+            stats.alg_flop += float(np.sum(np.where(newh, nr * pa * (pa + 1) + pa ** 3 / 3, 0.0)
+                                           + 4.0 * nr * pa + 2 * pa * pa))
         relv = (np.max(np.abs(step[act, None] * delta[act]), axis=1)
                 / (1.0 + np.max(np.abs(beta[act]), axis=1)))
         stepa = step[act]
@@ -638,6 +685,42 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                              n_iter=int(n_iter[k]), converged=bool(converged[k]),
                              dropped=int(info[k])))
     return res, bf.eta
+
+
+def _share_grams(bf, prob, reqs, lam, uniq, tol, n, ld, st):
+    """Approximate Hessian dedup.  Fits of one (mask, response) are ordered by penalty (the
+    lambda path: neighbours have the closest solutions); the max-row distances of consecutive
+    predictors are measured on the device, and a greedy chain lets each fit share the Gram of
+    the chain's representative while the summed distance (a bound on the true one, triangle
+    inequality) stays <= tol.  Returns (representatives, [(fit, rep, distance bound)])."""
+    groups = {}
+    for k in uniq:
+        groups.setdefault((reqs[k].mask, reqs[k].resp), []).append(int(k))
+    chains = [sorted(g, key=lambda k: lam[k]) for g in groups.values() if len(g) > 1]
+    if not chains:
+        return uniq, []
+    pairs = np.array([(c[i], c[i + 1]) for c in chains for i in range(len(c) - 1)],
+                     dtype=np.int32)
+    dev = bf.eta.device
+    pd_ = torch.from_numpy(pairs.reshape(-1)).to(dev)
+    fm = torch.from_numpy(np.asarray(bf.fit_mask, dtype=np.int32)).to(dev)
+    out = torch.empty(len(pairs), dtype=torch.float32, device=dev)
+    _lib.call("sglm_eta_pair_absmax", n, ld, len(pairs), _p(pd_), _p(prob.M), _p(fm),
+              _p(bf.eta), _p(out), st)
+    dist = out.cpu().numpy().astype(np.float64)
+    shared, drop, q = [], set(), 0
+    for c in chains:
+        rep, acc = c[0], 0.0
+        for i in range(1, len(c)):
+            acc += dist[q]
+            q += 1
+            if acc <= tol:
+                shared.append((c[i], rep, acc))
+                drop.add(c[i])
+            else:
+                rep, acc = c[i], 0.0
+    keep = np.array([k for k in uniq if int(k) not in drop], dtype=np.int32)
+    return keep, shared
 
 
 def _syrk(d: Design, bf, fits: np.ndarray, nsteps: int, ntile1: int, stats, st, exact=False,
