@@ -224,6 +224,14 @@ int sglm_chol_solve_ex(float* H, int32_t P, const int32_t* fits, int32_t nact,
                        uint8_t* frozen, int32_t refactor, int32_t B, void* work,
                        sglm_stream_t stream);
 
+/* sglm_chol_solve_ex over a mixed set: fits[0 .. nrefac) are factored, fits[nrefac .. nact)
+ * reuse the factor a previous call left in H (engine.irls: fits whose Hessian is kept), in one
+ * launch chain (trailing updates over the refactored fits only). */
+int sglm_chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t nact,
+                          int32_t nrefac, const double* g, const float* dshift, float* delta,
+                          int32_t* info, uint8_t* frozen, int32_t B, void* work,
+                          sglm_stream_t stream);
+
 /* Line search: out[k][j] = sum_i M[m][i] * loss(y_i, eta_i + t[j] * deta_i) (float64),
  * for j < T, fits k < B.  `work`: sglm_rowsum_work_bytes(B, T, n). */
 size_t sglm_rowsum_work_bytes(int32_t B, int32_t T, int64_t n);

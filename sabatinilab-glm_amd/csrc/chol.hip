@@ -32,8 +32,9 @@ __global__ void __launch_bounds__(kCT) chol_prep_kernel(
     float* __restrict__ Hall, int32_t P, const int32_t* __restrict__ fits,
     const double* __restrict__ gall, const float* __restrict__ dshift_all,
     uint8_t* __restrict__ frozen_all, float* __restrict__ rhs_all, float* __restrict__ diag_all,
-    int32_t* __restrict__ info, int32_t refactor) {
+    int32_t* __restrict__ info, int32_t nrefac) {
     const int fit = fits[blockIdx.x];
+    const bool refactor = (int)blockIdx.x < nrefac;
     float* H = Hall + (int64_t)fit * P * P;
     const double* g = gall + (int64_t)fit * P;
     const float* dsh = dshift_all + (int64_t)fit * P;
@@ -122,8 +123,9 @@ __device__ __forceinline__ void diag_steps(float (&a)[kNB], float& rinv, int c, 
 __global__ void __launch_bounds__(64) chol_diag_kernel(
     float* __restrict__ Hall, int32_t P, int32_t k0, const int32_t* __restrict__ fits,
     uint8_t* __restrict__ frozen_all, float* __restrict__ rhs_all,
-    const float* __restrict__ diag_all, int32_t* __restrict__ info, int32_t refactor) {
+    const float* __restrict__ diag_all, int32_t* __restrict__ info, int32_t nrefac) {
     const int fit = fits[blockIdx.x];
+    const bool refactor = (int)blockIdx.x < nrefac;
     float* H = Hall + (int64_t)fit * P * P;
     uint8_t* frz = frozen_all + (int64_t)fit * P + k0;
     float* rhs = rhs_all + (int64_t)fit * P + k0;
@@ -175,11 +177,12 @@ __global__ void __launch_bounds__(64) chol_diag_kernel(
 // Panel: columns j >= k0+NB in chunks of 256 per workgroup.
 __global__ void __launch_bounds__(kCT) chol_panel_kernel(
     float* __restrict__ Hall, int32_t P, int32_t k0, const int32_t* __restrict__ fits,
-    const uint8_t* __restrict__ frozen_all, float* __restrict__ rhs_all, int32_t refactor) {
+    const uint8_t* __restrict__ frozen_all, float* __restrict__ rhs_all, int32_t nrefac) {
     __shared__ float sD[kNB][kNB + 1];
     __shared__ float z[kNB];
     __shared__ uint8_t fz[kNB];
     const int fit = fits[blockIdx.x];
+    const bool refactor = (int)blockIdx.x < nrefac;
     float* H = Hall + (int64_t)fit * P * P;
     float* rhs = rhs_all + (int64_t)fit * P;
     const int tid = threadIdx.x;
@@ -358,20 +361,22 @@ extern "C" size_t sglm_chol_work_bytes(int32_t P, int32_t B) {
     return (size_t)2 * (size_t)B * (size_t)P * sizeof(float);
 }
 
-extern "C" int sglm_chol_solve_ex(float* H, int32_t P, const int32_t* fits, int32_t nact,
-                                  const double* g, const float* dshift, float* delta,
-                                  int32_t* info, uint8_t* frozen, int32_t refactor,
-                                  int32_t B, void* work, sglm_stream_t stream) {
+// fits[0 .. nrefac) are factored, fits[nrefac .. nact) reuse the factor and frozen set a
+// previous call left in H (engine.irls' kept Hessians): one launch chain for both, the
+// trailing updates over the refactored fits only.
+static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t nact,
+                            int32_t nrefac, const double* g, const float* dshift, float* delta,
+                            int32_t* info, uint8_t* frozen, int32_t B, void* work,
+                            hipStream_t s) {
     if (nact <= 0) return SGLM_OK;
     if (!H || !fits || !g || !dshift || !delta || !info || !frozen || !work || P % kNB ||
-        P > kMaxP || B < nact) {
+        P > kMaxP || B < nact || nrefac < 0 || nrefac > nact) {
         set_error("sglm_chol_solve: bad args (P=%d, max %d)", P, kMaxP);
         return SGLM_EINVAL;
     }
-    hipStream_t s = as_stream(stream);
     float* rhs = (float*)work;
     float* dg = rhs + (size_t)B * P;
-    chol_prep_kernel<<<nact, kCT, 0, s>>>(H, P, fits, g, dshift, frozen, rhs, dg, info, refactor);
+    chol_prep_kernel<<<nact, kCT, 0, s>>>(H, P, fits, g, dshift, frozen, rhs, dg, info, nrefac);
     int st = check_launch("chol_prep_kernel");
     if (st) return st;
     const int nb = P / kNB;
@@ -379,26 +384,42 @@ extern "C" int sglm_chol_solve_ex(float* H, int32_t P, const int32_t* fits, int3
     // diag/panel kb+1, then ONE rank-128 update of the remaining trailing matrix
     auto factor_step = [&](int kb) {
         const int k0 = kb * kNB;
-        chol_diag_kernel<<<nact, 64, 0, s>>>(H, P, k0, fits, frozen, rhs, dg, info, refactor);
+        chol_diag_kernel<<<nact, 64, 0, s>>>(H, P, k0, fits, frozen, rhs, dg, info, nrefac);
         const int rem = P - k0 - kNB;
         if (rem > 0)
             chol_panel_kernel<<<dim3(nact, (rem + kCT - 1) / kCT), kCT, 0, s>>>(H, P, k0, fits,
-                                                                               frozen, rhs, refactor);
+                                                                               frozen, rhs, nrefac);
     };
     for (int kb = 0; kb < nb; kb += 2) {
         factor_step(kb);
         if (kb + 1 >= nb) break;
-        if (refactor)
-            chol_update_kernel<<<dim3(nb - kb - 1, nact), kCT, 0, s>>>(H, P, kb * kNB, kNB,
-                                                                      kb + 1, 1, fits);
+        if (nrefac > 0)
+            chol_update_kernel<<<dim3(nb - kb - 1, nrefac), kCT, 0, s>>>(H, P, kb * kNB, kNB,
+                                                                        kb + 1, 1, fits);
         factor_step(kb + 1);
         const int T = nb - kb - 2;
-        if (refactor && T > 0)
-            chol_update_kernel<<<dim3(T * (T + 1) / 2, nact), kCT, 0, s>>>(H, P, kb * kNB,
-                                                                          2 * kNB, kb + 2, 0, fits);
+        if (nrefac > 0 && T > 0)
+            chol_update_kernel<<<dim3(T * (T + 1) / 2, nrefac), kCT, 0, s>>>(H, P, kb * kNB,
+                                                                            2 * kNB, kb + 2, 0, fits);
     }
     st = check_launch("chol block kernels");
     if (st) return st;
     chol_back_kernel<<<nact, kCT, 0, s>>>(H, P, fits, frozen, rhs, delta);
     return check_launch("chol_back_kernel");
+}
+
+extern "C" int sglm_chol_solve_ex(float* H, int32_t P, const int32_t* fits, int32_t nact,
+                                  const double* g, const float* dshift, float* delta,
+                                  int32_t* info, uint8_t* frozen, int32_t refactor,
+                                  int32_t B, void* work, sglm_stream_t stream) {
+    return chol_solve_mixed(H, P, fits, nact, refactor ? nact : 0, g, dshift, delta, info,
+                            frozen, B, work, as_stream(stream));
+}
+
+extern "C" int sglm_chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t nact,
+                                     int32_t nrefac, const double* g, const float* dshift,
+                                     float* delta, int32_t* info, uint8_t* frozen, int32_t B,
+                                     void* work, sglm_stream_t stream) {
+    return chol_solve_mixed(H, P, fits, nact, nrefac, g, dshift, delta, info, frozen, B, work,
+                            as_stream(stream));
 }

@@ -54,11 +54,11 @@ SYRK_CBITS = True              # ... and its row-compacted register-only form (v
 # factor holds by a factor in [e^-cD, e^cD] (c = max(1, |2 - power|)), which bounds the
 # contraction of the inexact-Newton step by e^cD - 1; the fixed point (exact gradient) is
 # unchanged.  0 disables reuse.
-HESS_REUSE_TOL = float(__import__("os").environ.get("SGLM_HESS_REUSE_TOL", "0.0625"))
+HESS_REUSE_TOL = float(__import__("os").environ.get("SGLM_HESS_REUSE_TOL", "0.25"))
 # Hessian sharing: among fits of one (mask, response) that need a new Hessian, a fit whose
 # predictor is within HESS_SHARE_TOL (max over its mask rows) of another's is factored from
 # that fit's Gram, and starts its drift count at that distance (same bound as above).
-HESS_SHARE_TOL = float(__import__("os").environ.get("SGLM_HESS_SHARE_TOL", "0.0625"))
+HESS_SHARE_TOL = float(__import__("os").environ.get("SGLM_HESS_SHARE_TOL", "0.25"))
 
 
 def require_gpu():
@@ -593,16 +593,13 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         bf.gtot.copy_(torch.from_numpy(g))
         bf.delta.zero_()
         if const_hess:
-            solves = [(act, 0 if factored else 1)]
+            order, nref = act, (0 if factored else act.size)
         else:
-            solves = [(form, 1), (keep, 0)]
-        for fits_s, refactor in solves:
-            if fits_s.size == 0:
-                continue
-            fits_d = torch.tensor(fits_s, dtype=torch.int32, device=dev)
-            _lib.call("sglm_chol_solve_ex", _p(bf.H), P, _p(fits_d), int(fits_s.size),
-                      _p(bf.gtot), _p(bf.dshift), _p(bf.delta), _p(bf.info), _p(bf.frozen),
-                      refactor, B, _p(bf.cwork), st)
+            order, nref = np.concatenate([form, keep]), form.size
+        fits_d = torch.from_numpy(order.astype(np.int32)).to(dev)
+        _lib.call("sglm_chol_solve_mixed", _p(bf.H), P, _p(fits_d), int(order.size), int(nref),
+                  _p(bf.gtot), _p(bf.dshift), _p(bf.delta), _p(bf.info), _p(bf.frozen), B,
+                  _p(bf.cwork), st)
         factored = True
         d.eta(bf.delta, bf.deta)
         delta = bf.delta.cpu().numpy().astype(np.float64)

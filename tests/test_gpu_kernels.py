@@ -163,6 +163,19 @@ def test_chol_solve_matches_numpy(engine, torch_mod):
     for k in range(B):
         M = H[k, : p + 1, : p + 1].astype(np.float64) + np.diag(np.r_[np.full(p, 3.0), 0.0])
         assert rel(x2[k, : p + 1], -np.linalg.solve(M, g2[k, : p + 1])) < 1e-3
+    # mixed chain: fit 1 gets a new matrix and is factored, fit 0 keeps its factor
+    A1 = rng.normal(size=(2000, p + 1))
+    H1 = np.zeros((P, P), np.float32)
+    H1[: p + 1, : p + 1] = A1.T @ A1
+    Hd[1].copy_(torch.from_numpy(H1))
+    order = torch.tensor([1, 0], dtype=torch.int32, device="cuda")
+    _lib.call("sglm_chol_solve_mixed", Hd.data_ptr(), P, order.data_ptr(), 2, 1, g2d.data_ptr(),
+              dshd.data_ptr(), out.data_ptr(), info.data_ptr(), frozen.data_ptr(), B,
+              cw.data_ptr(), 0)
+    x3 = out.cpu().numpy()
+    for k, Hk in ((0, H[0]), (1, H1)):
+        M = Hk[: p + 1, : p + 1].astype(np.float64) + np.diag(np.r_[np.full(p, 3.0), 0.0])
+        assert rel(x3[k, : p + 1], -np.linalg.solve(M, g2[k, : p + 1])) < 1e-3, k
 
 
 def _fit_one(engine, X, y, family, power, lam, fit_intercept=True):

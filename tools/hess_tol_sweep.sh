@@ -1,8 +1,8 @@
 # Sweep the Hessian reuse / sharing tolerances over the C4 bench (development tool).
 set -e
-O=gpurun_out/tol2; mkdir -p $O
+O=gpurun_out/tol3; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1
-for rs in "0.03125 0" "0.03125 0.0078125" "0.03125 0.015625" "0.03125 0.03125" "0.0625 0.03125" "0.0625 0.0625"; do
+for rs in "0.0625 0.0625" "0.125 0.0625" "0.125 0.125" "0.25 0.125" "0.25 0.25" "0.5 0.25"; do
   set -- $rs
   SGLM_HESS_REUSE_TOL=$1 SGLM_HESS_SHARE_TOL=$2 timeout -k 10 300 python bench.py --no-cpu --steps 2 --warmup 1 > $O/b_$1_$2.json 2> $O/b_$1_$2.err
 done
