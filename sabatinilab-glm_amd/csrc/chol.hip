@@ -275,6 +275,71 @@ __global__ void __launch_bounds__(kCT) chol_update_kernel(float* __restrict__ Ha
     }
 }
 
+// Blocked forward substitution U^T z = rhs with a stored factor (no fit refactored: the
+// kept-Hessian iterations), one workgroup per fit, in place on rhs.  Per 64-block kb: the
+// four waves form the column dot products sum_{r < k0} U[r][k0 + c] z[r] (lane = column c,
+// wave w takes rows r = w mod 4, four rows per pass: 64-column row segments, coalesced),
+// then wave 0 solves the 64 x 64 lower-triangular U_kk^T with readlane broadcasts.
+__global__ void __launch_bounds__(kCT) chol_fwd_kernel(
+    const float* __restrict__ Hall, int32_t P, const int32_t* __restrict__ fits,
+    const uint8_t* __restrict__ frozen_all, float* __restrict__ rhs_all) {
+    __shared__ float part[4][kNB];
+    __shared__ float z[kMaxP];
+    const int fit = fits[blockIdx.x];
+    const float* H = Hall + (int64_t)fit * P * P;
+    const uint8_t* frz = frozen_all + (int64_t)fit * P;
+    float* rhs = rhs_all + (int64_t)fit * P;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nb = P / kNB;
+    for (int kb = 0; kb < nb; ++kb) {
+        const int k0 = kb * kNB;
+        const float* col = H + k0 + lane;
+        float acc0 = 0.0f, acc1 = 0.0f, acc2 = 0.0f, acc3 = 0.0f;
+        int r = wave;
+        for (; r + 12 < k0; r += 16) {
+            const float h0 = col[(int64_t)r * P], h1 = col[(int64_t)(r + 4) * P];
+            const float h2 = col[(int64_t)(r + 8) * P], h3 = col[(int64_t)(r + 12) * P];
+            acc0 = fmaf(h0, z[r], acc0);
+            acc1 = fmaf(h1, z[r + 4], acc1);
+            acc2 = fmaf(h2, z[r + 8], acc2);
+            acc3 = fmaf(h3, z[r + 12], acc3);
+        }
+        for (; r < k0; r += 4) acc0 = fmaf(col[(int64_t)r * P], z[r], acc0);
+        part[wave][lane] = (acc0 + acc1) + (acc2 + acc3);
+        __syncthreads();
+        if (wave == 0) {
+            float v = rhs[k0 + lane] - ((part[0][lane] + part[1][lane]) +
+                                        (part[2][lane] + part[3][lane]));
+            // lane c holds column c of U_kk strictly above the diagonal: a[q] = U[k0 + q][k0 + c]
+            // for q < c, else 0 (masked once at load, so the solve steps carry no masks)
+            const float* blk = H + (int64_t)k0 * P + k0 + lane;
+            const float ucc = blk[(int64_t)lane * P];
+            float a[kNB];
+            int cl = lane;
+            asm volatile("" : "+v"(cl));
+#pragma unroll
+            for (int q = 0; q < kNB; ++q) {
+                const float hv = blk[(int64_t)q * P];
+                a[q] = q < cl ? hv : 0.0f;
+            }
+            const float rinv = frz[k0 + lane] ? 0.0f : 1.0f / ucc;
+            // step q: z_q = v_q / U[q][q] (lane-local product, one broadcast); lanes c > q
+            // subtract U[q][c] z_q (a[q] = 0 for c <= q); lane q then keeps z_q
+            int cf = lane;
+            asm volatile("" : "+v"(cf));
+#pragma unroll
+            for (int q = 0; q < kNB; ++q) {
+                const float zq = lanef(v * rinv, q);
+                v = fmaf(-a[q], zq, v);
+                v = cf == q ? zq : v;
+            }
+            z[k0 + lane] = v;
+            rhs[k0 + lane] = v;
+        }
+        __syncthreads();
+    }
+}
+
 // Blocked back substitution U x = z, then delta = -x.  Per 64-block (last to first): the
 // four waves form the 64 row dot products with the solved tail (16 rows per wave, four
 // 64-column chunks per pass: 64 loads in flight per lane), then wave 0 solves the 64 x 64
@@ -379,6 +444,13 @@ static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t na
     chol_prep_kernel<<<nact, kCT, 0, s>>>(H, P, fits, g, dshift, frozen, rhs, dg, info, nrefac);
     int st = check_launch("chol_prep_kernel");
     if (st) return st;
+    if (nrefac == 0) {                       // stored factors only: two triangular solves
+        chol_fwd_kernel<<<nact, kCT, 0, s>>>(H, P, fits, frozen, rhs);
+        st = check_launch("chol_fwd_kernel");
+        if (st) return st;
+        chol_back_kernel<<<nact, kCT, 0, s>>>(H, P, fits, frozen, rhs, delta);
+        return check_launch("chol_back_kernel");
+    }
     const int nb = P / kNB;
     // block steps in pairs: diag/panel kb, look-ahead update of block row kb+1 only,
     // diag/panel kb+1, then ONE rank-128 update of the remaining trailing matrix

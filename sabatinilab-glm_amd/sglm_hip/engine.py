@@ -59,6 +59,10 @@ HESS_REUSE_TOL = float(__import__("os").environ.get("SGLM_HESS_REUSE_TOL", "0.25
 # predictor is within HESS_SHARE_TOL (max over its mask rows) of another's is factored from
 # that fit's Gram, and starts its drift count at that distance (same bound as above).
 HESS_SHARE_TOL = float(__import__("os").environ.get("SGLM_HESS_SHARE_TOL", "0.25"))
+# Batch compaction: once at most COMPACT_FRAC of the batch is still iterating (and at least
+# COMPACT_MIN fits have stopped), the active fits are moved to the front slots.
+COMPACT_FRAC = float(__import__("os").environ.get("SGLM_COMPACT_FRAC", "0.75"))
+COMPACT_MIN = 4
 
 
 def require_gpu():
@@ -475,20 +479,19 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
     fam, power = reqs[0].family, float(reqs[0].power)
     if any(r.family != fam or float(r.power) != power for r in reqs):
         raise ValueError("irls(): one loss family per batch")
-    B, P, ld, n, p = len(reqs), d.P, d.ld, d.n, d.p
+    B0, P, ld, n, p = len(reqs), d.P, d.ld, d.n, d.p
     dev = d.device
-    bf = _BUF.get(B, P, ld, dev)
+    bf = _BUF.get(B0, P, ld, dev)
     st = _stream()
     log_link = fam == FAM_TWEEDIE_LOG
+    reqs0 = list(reqs)
 
-    fit_resp = torch.tensor([r.resp for r in reqs], dtype=torch.int32, device=dev)
-    fit_mask = torch.tensor([r.mask for r in reqs], dtype=torch.int32, device=dev)
     lam = np.array([float(r.lam) for r in reqs])
-    penal = np.zeros((B, P), dtype=np.float64)
+    penal = np.zeros((B0, P), dtype=np.float64)
     penal[:, :p] = 1.0
-    dsh = np.full((B, P), -1.0, dtype=np.float32)
+    dsh = np.full((B0, P), -1.0, dtype=np.float32)
     dsh[:, :p] = lam[:, None]
-    beta = np.zeros((B, P), dtype=np.float64)
+    beta = np.zeros((B0, P), dtype=np.float64)
     for k, r in enumerate(reqs):
         if r.fit_intercept:
             dsh[k, p] = 0.0
@@ -511,26 +514,52 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
     reuse_tol = 0.0 if const_hess else HESS_REUSE_TOL / max(1.0, abs(2.0 - power))
     share_tol = 0.0 if const_hess else min(HESS_SHARE_TOL / max(1.0, abs(2.0 - power)),
                                            reuse_tol)
-    drift = np.full(B, np.inf)          # predictor drift since each fit's Hessian was formed
-    dmax_d = torch.zeros(B, dtype=torch.float32, device=dev)
-    dmax_h = torch.zeros(B, dtype=torch.float32).pin_memory()
-    gram_now = np.zeros(B, dtype=bool)
-    active = np.ones(B, dtype=bool)
-    n_iter = np.zeros(B, dtype=np.int64)
-    converged = np.zeros(B, dtype=bool)
-    prev_rel = np.full(B, np.inf)
+    # Device state is held per SLOT; slot s holds fit fid[s].  When enough fits have stopped,
+    # the batch is compacted to the active ones (their predictor, factor, frozen set and
+    # penalty rows move to the front), so the per-fit kernels of later iterations (link,
+    # gradient, eta, line search) run over the active fits only.
+    B = B0
+    fid = np.arange(B0)
+    fresp_h = np.array([r.resp for r in reqs], dtype=np.int32)
+    fmask_h = np.array([r.mask for r in reqs], dtype=np.int32)
+    fit_resp = torch.from_numpy(fresp_h).to(dev)
+    fit_mask = torch.from_numpy(fmask_h).to(dev)
+    drift = np.full(B0, np.inf)         # predictor drift since each fit's Hessian was formed
+    dmax_d = torch.zeros(B0, dtype=torch.float32, device=dev)
+    dmax_h = torch.zeros(B0, dtype=torch.float32).pin_memory()
+    dmax_pending = False
+    gram_now = np.zeros(B0, dtype=bool)
+    active = np.ones(B0, dtype=bool)
+    n_iter = np.zeros(B0, dtype=np.int64)
+    converged = np.zeros(B0, dtype=bool)
+    prev_rel = np.full(B0, np.inf)
     max_iter = np.array([max(1, int(r.max_iter)) for r in reqs])
+    out_beta = np.zeros((B0, P), dtype=np.float64)
+    out_iter = np.zeros(B0, dtype=np.int64)
+    out_conv = np.zeros(B0, dtype=bool)
+    out_info = np.zeros(B0, dtype=np.int64)
     factored = False
-    xtr_work = _work(max(_lib.query("sglm_xtr_work_bytes", P, B, n),
-                         _lib.query("sglm_rowsum_work_bytes", B, 8, n)), dev)
+    xtr_work = _work(max(_lib.query("sglm_xtr_work_bytes", P, B0, n),
+                         _lib.query("sglm_rowsum_work_bytes", B0, 8, n)), dev)
     tv1 = torch.tensor([0.0, 1.0, 0.5, 0.25, 0.125], dtype=torch.float32, device=dev)
     tv2 = torch.tensor([0.0625, 0.03125, 0.015625, 0.0078125, 2.0 ** -10, 2.0 ** -14, 2.0 ** -20],
                        dtype=torch.float32, device=dev)
-    Ltr = torch.zeros(B * 8, dtype=torch.float64, device=dev)     # dense [B][T] per call
+    Ltr = torch.zeros(B0 * 8, dtype=torch.float64, device=dev)    # dense [B][T] per call
     nsteps = (n + 31) // 32
     ntile1 = (P // 256) * (P // 256 + 1) // 2
     rows = np.array([prob.mask_stats(r.resp, r.mask)[0] for r in reqs], dtype=np.float64)
-    bf.prob, bf.fit_mask = prob, np.array([r.mask for r in reqs])
+    bf.prob, bf.fit_mask = prob, fmask_h
+
+    def retire(slots):
+        """Record the results of the fits in `slots` (they leave the batch or it ends)."""
+        if slots.size == 0:
+            return
+        info_h = bf.info[:B].cpu().numpy()
+        f = fid[slots]
+        out_beta[f] = beta[slots]
+        out_iter[f] = n_iter[slots]
+        out_conv[f] = converged[slots]
+        out_info[f] = info_h[slots]
 
     import time
     tick = stats.mark if (stats is not None and stats.trace_phases) else (lambda name, t: t)
@@ -539,12 +568,35 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         act = np.flatnonzero(active)
         if act.size == 0:
             break
+        if act.size <= COMPACT_FRAC * B and B - act.size >= COMPACT_MIN:
+            if dmax_pending:            # last step's drift, still in the old slot order
+                torch.cuda.current_stream().synchronize()
+                drift += dmax_h.numpy()[:B].astype(np.float64)
+                dmax_pending = False
+            retire(np.flatnonzero(~active))
+            m = int(act.size)
+            idx = torch.from_numpy(act).to(dev)
+            for t in (bf.eta, bf.frozen, bf.info, bf.H):
+                t[:m] = t[idx]
+            (lam, penal, dsh, beta, drift, gram_now, active, n_iter, converged, prev_rel,
+             max_iter, rows, fid, fresp_h, fmask_h) = (
+                x[act] for x in (lam, penal, dsh, beta, drift, gram_now, active, n_iter,
+                                 converged, prev_rel, max_iter, rows, fid, fresp_h, fmask_h))
+            reqs = [reqs[s_] for s_ in act]
+            bf.dshift[:m].copy_(torch.from_numpy(dsh))
+            fit_resp = torch.from_numpy(fresp_h).to(dev)
+            fit_mask = torch.from_numpy(fmask_h).to(dev)
+            bf.fit_mask = fmask_h
+            B = m
+            act = np.arange(m)
+            t0 = tick("it_compact", t0)
         _lib.call("sglm_link_update", fam, power, n, ld, B, _p(bf.eta), _p(prob.Y), _p(prob.M),
                   _p(fit_resp), _p(fit_mask), _p(bf.W), _p(bf.R), st)
         d.xtr(bf.R, B, bf.g)
-        g = bf.g.cpu().numpy() + lam[:, None] * penal * beta
-        if it > 0 and not const_hess:
-            drift += dmax_h.numpy().astype(np.float64)
+        g = bf.g[:B].cpu().numpy() + lam[:, None] * penal * beta
+        if dmax_pending:
+            drift += dmax_h.numpy()[:B].astype(np.float64)
+            dmax_pending = False
         t0 = tick("it_gradient", t0)
         # ---- Hessian
         if const_hess:
@@ -590,8 +642,8 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                 stats.gram_fits += int(uniq.size)
                 stats.reused += int(keep.size)
         t0 = tick("it_gram", t0)
-        bf.gtot.copy_(torch.from_numpy(g))
-        bf.delta.zero_()
+        bf.gtot[:B].copy_(torch.from_numpy(g))
+        bf.delta[:B].zero_()
         if const_hess:
             order, nref = act, (0 if factored else act.size)
         else:
@@ -601,8 +653,8 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                   _p(bf.gtot), _p(bf.dshift), _p(bf.delta), _p(bf.info), _p(bf.frozen), B,
                   _p(bf.cwork), st)
         factored = True
-        d.eta(bf.delta, bf.deta)
-        delta = bf.delta.cpu().numpy().astype(np.float64)
+        d.eta(bf.delta[:B], bf.deta)
+        delta = bf.delta[:B].cpu().numpy().astype(np.float64)
         t0 = tick("it_solve_eta", t0)
         # ---- line search
         _lib.call("sglm_loss_trials", fam, power, n, ld, B, _p(bf.eta), _p(bf.deta), _p(prob.Y),
@@ -640,13 +692,14 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         t0 = tick("it_linesearch", t0)
         # ---- update
         beta += step[:, None] * delta
-        bf.beta.copy_(torch.from_numpy(beta.astype(np.float32)))
+        bf.beta[:B].copy_(torch.from_numpy(beta.astype(np.float32)))
         step_d = torch.from_numpy(step.astype(np.float32)).to(dev)
         _lib.call("sglm_eta_axpy_max", n, ld, B, _p(step_d), _p(bf.deta), _p(prob.M),
                   _p(fit_mask), _p(bf.eta), _p(dmax_d), st)
         if not const_hess:
             # read back with the next iteration's gradient sync (no extra stall here)
-            dmax_h.copy_(dmax_d, non_blocking=True)
+            dmax_h[:B].copy_(dmax_d[:B], non_blocking=True)
+            dmax_pending = True
         n_iter[act] += 1
         if stats is not None:
             stats.newton_iters += 1
@@ -671,16 +724,18 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         prev_rel[act] = relv
         t0 = tick("it_update", t0)
 
+    retire(np.arange(B))
     bf.prob = bf.keep = None            # drop the compacted designs with the problem
-    # final linear predictor from the final coefficients (no accumulated drift)
+    # final linear predictor from the final coefficients, in request order (no accumulated
+    # drift)
+    bf.beta.copy_(torch.from_numpy(out_beta.astype(np.float32)))
     d.eta(bf.beta, bf.eta)
-    info = bf.info.cpu().numpy()
     res = []
-    for k, r in enumerate(reqs):
-        res.append(FitResult(coef=beta[k, :p].copy(),
-                             intercept=float(beta[k, p]) if r.fit_intercept else 0.0,
-                             n_iter=int(n_iter[k]), converged=bool(converged[k]),
-                             dropped=int(info[k])))
+    for k, r in enumerate(reqs0):
+        res.append(FitResult(coef=out_beta[k, :p].copy(),
+                             intercept=float(out_beta[k, p]) if r.fit_intercept else 0.0,
+                             n_iter=int(out_iter[k]), converged=bool(out_conv[k]),
+                             dropped=int(out_info[k])))
     return res, bf.eta
 
 

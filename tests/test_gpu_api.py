@@ -353,9 +353,9 @@ def test_odd_shapes_vs_oracle(engine, n, p):
 
 def test_hessian_reuse_keeps_the_fixed_point(engine, monkeypatch):
     """Hessian reuse / sharing (engine.HESS_REUSE_TOL, HESS_SHARE_TOL) only changes the
-    inexact-Newton contraction, not the minimiser: a C3-shape 5-split x 20-lambda Poisson grid
-    with the default tolerances matches the same grid with a fresh Hessian every iteration
-    (1e-5 relative), converges everywhere, and actually kept factors; two lambdas are also
+    inexact-Newton contraction, not the minimiser, and batch compaction only the slot order: a
+    C3-shape 5-split x 20-lambda Poisson grid with the defaults matches the same grid with a
+    fresh Hessian every iteration and a fixed batch (1e-5 relative), converges everywhere, and actually kept factors; two lambdas are also
     held to the float64 oracle."""
     import pandas as pd
     from sglm_hip import engine as E, folds, grid, synth
@@ -372,6 +372,7 @@ def test_hessian_reuse_keeps_the_fixed_point(engine, monkeypatch):
     assert st.reused > 0 and st.gram_fits < st.fit_iters
     monkeypatch.setattr(E, "HESS_REUSE_TOL", 0.0)
     monkeypatch.setattr(E, "HESS_SHARE_TOL", 0.0)
+    monkeypatch.setattr(E, "COMPACT_FRAC", 0.0)        # and no batch compaction
     st0 = E.IrlsStats()
     exact = grid.run(d, s.y, cv_idx, objs, [0] * len(objs), stats=st0)
     assert st0.reused == 0
