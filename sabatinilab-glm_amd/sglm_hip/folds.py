@@ -93,17 +93,20 @@ def trial_keys_codes(df, id_cols, package_style=False):
     return bucket.astype("category").cat.codes
 
 
+def mask_from_idx(idx, n):
+    """Multiplicity mask (uint8, length n) of one index list: 0/1 for strictly increasing
+    indices, counts for repeats (holdout resampling)."""
+    idx = np.asarray(idx, dtype=np.int64).reshape(-1)
+    if idx.size and (idx[0] < 0 or idx[-1] >= n or not np.all(idx[1:] > idx[:-1])):
+        m = np.bincount(idx, minlength=n)[:n]              # repeats (holdout resampling)
+        if m.max(initial=0) > 255:
+            raise ValueError("an index repeats more than 255 times in one split")
+        return m.astype(np.uint8)
+    m = np.zeros(n, dtype=np.uint8)                         # strictly increasing: 0/1 mask
+    m[idx] = 1
+    return m
+
+
 def masks_from_cv_idx(cv_idx, n):
     """Per split: (train multiplicity mask, test multiplicity mask) as uint8 arrays."""
-    def one(idx):
-        idx = np.asarray(idx, dtype=np.int64).reshape(-1)
-        if idx.size and (idx[0] < 0 or idx[-1] >= n or not np.all(idx[1:] > idx[:-1])):
-            m = np.bincount(idx, minlength=n)[:n]          # repeats (holdout resampling)
-            if m.max(initial=0) > 255:
-                raise ValueError("an index repeats more than 255 times in one split")
-            return m.astype(np.uint8)
-        m = np.zeros(n, dtype=np.uint8)                     # strictly increasing: 0/1 mask
-        m[idx] = 1
-        return m
-
-    return [(one(tr), one(te)) for tr, te in cv_idx]
+    return [(mask_from_idx(tr, n), mask_from_idx(te, n)) for tr, te in cv_idx]

@@ -183,53 +183,38 @@ def run_multi(X, y, groups: Sequence[dict], score_method: str = "mse", coef0=Non
     y = np.asarray(y, dtype=np.float64).reshape(-1)
     if y.shape[0] != n:
         raise ValueError(f"y has {y.shape[0]} rows, X has {n}")
-    masks, mkey = [], {}
+    # ---- row masks: specs first (index lists), arrays only for the masks this rank uses
+    specs, mkey = [], {}
     dedup = len(groups) > 1                  # one grid's masks are distinct by construction
 
-    def add_mask(m):
-        if not dedup:
-            masks.append(m)
-            return len(masks) - 1
-        k = m.tobytes()
-        if k not in mkey:
-            mkey[k] = len(masks)
-            masks.append(m)
-        return mkey[k]
-
-    def rows_mask(rows):
-        if rows is None:
-            return np.ones(n, np.uint8)
-        m = np.zeros(n, np.uint8)
-        m[np.asarray(rows, dtype=np.int64)] = 1
-        return m
+    def add_spec(idx, multiplicity):
+        """idx: row indices (None = every row); multiplicity: repeats count (fold lists)."""
+        if dedup:                            # resplit grids share masks: dedup by content
+            a = _mask_array(idx, multiplicity, n)
+            k = a.tobytes()
+            if k not in mkey:
+                mkey[k] = len(specs)
+                specs.append((idx, multiplicity, a))
+            return mkey[k]
+        specs.append((idx, multiplicity, None))
+        return len(specs) - 1
 
     gm = []                                  # per group: ([(train, test)], refit, holdout)
     for g in groups:
-        fm = F.masks_from_cv_idx(g["cv_idx"], n)
-        splits = [(add_mask(tr), add_mask(te)) for tr, te in fm]
-        refit = add_mask(rows_mask(g.get("refit_rows")))
+        splits = [(add_spec(tr, True), add_spec(te, True)) for tr, te in g["cv_idx"]]
+        refit = add_spec(g.get("refit_rows"), False)
         hold = g.get("holdout_rows")
-        gm.append((splits, refit, -1 if hold is None else add_mask(rows_mask(hold))))
+        gm.append((splits, refit, -1 if hold is None else add_spec(hold, False)))
+    counts = [_mask_count(sp[0], sp[1], n) for sp in specs]
     t0 = tick("setup_masks", t0)
     roll_list = sorted(set(int(r) for g in groups for r in g["rolls"]) | {0})
     ridx = {r: i for i, r in enumerate(roll_list)}
-    ys = [np.roll(y, r) for r in roll_list]
-    prob = E.Problem(design, ys, masks)
-    t0 = tick("setup_problem", t0)
-    ms = _MaskStats(prob)
-    t0 = tick("setup_maskstats", t0)
 
     # ---- fit table: per group, (param j, split k) then refit (j, -1)
     table = []                               # (group, j, k, fit mask, resp, second score mask)
     for gi, g in enumerate(groups):
         splits, refit, hold = gm[gi]
         for j, (obj, roll) in enumerate(zip(g["objectives"], g["rolls"])):
-            if obj.family == E.FAM_TWEEDIE_LOG:
-                for r_, m_ in [(ridx[int(roll)], tr) for tr, _ in splits] + [(0, refit)]:
-                    st = ms.get(r_, m_)
-                    if st["cnt"] and (st["ymin"] < 0 or st["mean"] <= 0):
-                        raise ValueError("Some value(s) of y are out of the valid range of the "
-                                         "loss 'HalfPoissonLoss'.")
             for k, (tr, te) in enumerate(splits):
                 table.append((gi, j, k, tr, ridx[int(roll)], te))
             table.append((gi, j, -1, refit, 0, hold))
@@ -241,10 +226,39 @@ def run_multi(X, y, groups: Sequence[dict], score_method: str = "mse", coef0=Non
     elif world > 1:
         njs = [len(g["objectives"]) for g in groups]
         keys = [(t[3], t[4], snake(t[1], njs[t[0]]), t[0], t[1]) for t in table]
-        costs = [ms.get(t[4], t[3])["cnt"] for t in table]
+        costs = [counts[t[3]] for t in table]
         mine = shard_plan(keys, costs, rank, world)
     else:
         mine = list(range(len(table)))
+
+    # only the masks (and responses) of this rank's fits are built and uploaded
+    used = sorted({table[i][3] for i in mine} | {table[i][5] for i in mine if table[i][5] >= 0})
+    local = {mid: q for q, mid in enumerate(used)}
+    masks = [specs[mid][2] if specs[mid][2] is not None else
+             _mask_array(specs[mid][0], specs[mid][1], n) for mid in used]
+    ys = [np.roll(y, r) for r in roll_list]
+    prob = E.Problem(design, ys, masks)
+    t0 = tick("setup_problem", t0)
+    ms = _MaskStats(prob)
+    # sklearn's y-range check of the log-link fits (y >= 0 on the fit's rows, positive mean;
+    # glm.py:231-235), on this rank's fits from the device mask statistics; the verdict is
+    # shared (one int all-reduce) so that every rank raises together
+    bad = 0
+    for i in mine:
+        _, _, _, m, r, _ = table[i]
+        if groups[table[i][0]]["objectives"][table[i][1]].family == E.FAM_TWEEDIE_LOG:
+            st_ = ms.get(r, local[m])
+            bad |= int(bool(st_["cnt"]) and (st_["ymin"] < 0 or st_["mean"] <= 0))
+    if dist is not None:
+        import torch
+        flag = torch.tensor([bad], dtype=torch.int32,
+                            device="cuda" if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        bad = int(flag.item())
+    if bad:
+        raise ValueError("Some value(s) of y are out of the valid range of the loss "
+                         "'HalfPoissonLoss'.")
+    t0 = tick("setup_maskstats", t0)
 
     def objective(i):
         return groups[table[i][0]]["objectives"][table[i][1]]
@@ -260,9 +274,9 @@ def run_multi(X, y, groups: Sequence[dict], score_method: str = "mse", coef0=Non
         for i in idxs:
             _, _, _, m, r, _ = table[i]
             obj = objective(i)
-            cnt = ms.get(r, m)["cnt"]
-            reqs.append(E.FitReq(obj.family, obj.power, obj.lam(cnt), m, r, obj.fit_intercept,
-                                 obj.max_iter,
+            cnt = counts[m]
+            reqs.append(E.FitReq(obj.family, obj.power, obj.lam(cnt), local[m], r,
+                                 obj.fit_intercept, obj.max_iter,
                                  None if coef0 is None else np.asarray(coef0, float),
                                  None if intercept0 is None else float(intercept0)))
         t0 = tick("fit_table", t0)
@@ -274,11 +288,27 @@ def run_multi(X, y, groups: Sequence[dict], score_method: str = "mse", coef0=Non
             res, eta = E.irls(prob, reqs, stats=stats)
             fam, power = key
         t0 = tick("solve", t0)
-        sets = np.array([[table[i][3], table[i][5]] for i in idxs], dtype=np.int32)
+        sets = np.array([[local[table[i][3]], local.get(table[i][5], -1)] for i in idxs],
+                        dtype=np.int32)
         sums = E.score_sums(prob, fam, power, eta, [table[i][4] for i in idxs], sets)
         for q, i in enumerate(idxs):
             rr = res[q]
-            results[i] = (rr.coef, rr.intercept, rr.n_iter, rr.converged, sums[q])
+            _, _, k, m, r, mt = table[i]
+            obj = objective(i)
+            pw = obj.power if obj.family == E.FAM_TWEEDIE_LOG else None
+            sc = {}
+            if k < 0:
+                if mt >= 0:
+                    sth = ms.get(r, local[mt], pw)
+                    sc["hold"] = (_score("r2", obj, sums[q][1], sth),
+                                  _score("mse", obj, sums[q][1], sth))
+            else:
+                st_te = ms.get(r, local[mt], pw)
+                sc["train"] = _score(score_method, obj, sums[q][0], ms.get(r, local[m], pw))
+                sc["test"] = _score(score_method, obj, sums[q][1], st_te)
+                sc["ss_res"] = float(sums[q][1][0])
+                sc["sst"], sc["cnt_te"] = st_te["sst"], st_te["cnt"]
+            results[i] = (rr.coef, rr.intercept, rr.n_iter, rr.converged, sc)
     t0 = tick("score_sums", t0)
     if simulate is not None:
         return results
@@ -290,7 +320,6 @@ def run_multi(X, y, groups: Sequence[dict], score_method: str = "mse", coef0=Non
         K = len(gm[gi][0])
         out = []
         for j, obj in enumerate(g["objectives"]):
-            power = obj.power if obj.family == E.FAM_TWEEDIE_LOG else None
             cv_coefs = np.zeros((p, K))
             cv_b = np.zeros(K)
             s_tr = np.zeros(K)
@@ -303,24 +332,20 @@ def run_multi(X, y, groups: Sequence[dict], score_method: str = "mse", coef0=Non
             for i, (gg, jj, k, m, r, mt) in enumerate(table):
                 if gg != gi or jj != j:
                     continue
-                coef, b, it, cv_ok, sums = results[i]
+                coef, b, it, cv_ok, sc = results[i]
                 n_iter.append(it)
                 conv &= cv_ok
                 if k < 0:
                     refit = (coef, b)
-                    if mt >= 0:
-                        sth = ms.get(r, mt, power)
-                        hold_scores = (_score("r2", obj, sums[1], sth),
-                                       _score("mse", obj, sums[1], sth))
+                    hold_scores = sc.get("hold")
                     continue
                 cv_coefs[:, k] = coef
                 cv_b[k] = b
-                s_tr[k] = _score(score_method, obj, sums[0], ms.get(r, m, power))
-                s_te[k] = _score(score_method, obj, sums[1], ms.get(r, mt, power))
-                ss_res += sums[1][0]
-                st_te = ms.get(r, mt)
-                ss_tot += st_te["sst"]
-                n_te += st_te["cnt"]
+                s_tr[k] = sc["train"]
+                s_te[k] = sc["test"]
+                ss_res += sc["ss_res"]
+                ss_tot += sc["sst"]
+                n_te += sc["cnt_te"]
             d = {
                 "cv_coefs": cv_coefs,
                 "cv_intercepts": cv_b,
@@ -342,6 +367,26 @@ def run_multi(X, y, groups: Sequence[dict], score_method: str = "mse", coef0=Non
         out_all.append(out)
     tick("assemble", t0)
     return out_all
+
+
+def _mask_array(idx, multiplicity, n):
+    """uint8 mask of one spec: fold index lists count repeats (holdout resampling), row lists
+    (refit / holdout rows) mark rows; None = every row."""
+    if idx is None:
+        return np.ones(n, np.uint8)
+    if multiplicity:
+        return F.mask_from_idx(idx, n)
+    m = np.zeros(n, np.uint8)
+    m[np.asarray(idx, dtype=np.int64).reshape(-1)] = 1
+    return m
+
+
+def _mask_count(idx, multiplicity, n):
+    """Row count of a spec (sum of multiplicities) without building the mask."""
+    if idx is None:
+        return float(n)
+    idx = np.asarray(idx).reshape(-1)
+    return float(idx.size if multiplicity else np.unique(idx).size)
 
 
 def _score(method, obj: Objective, sums, st):

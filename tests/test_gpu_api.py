@@ -87,6 +87,15 @@ def test_poisson_y_range_error(engine):
     X = np.random.default_rng(0).random((50, 3))
     with pytest.raises(ValueError, match="out of the valid range"):
         sglm.GLM("Poisson").fit(X, -np.ones(50))
+    # through the CV grid: one negative response on a training row of some split
+    import sglm_cv
+    y = np.ones(50)
+    y[7] = -1.0
+    cv_idx = [(np.setdiff1d(np.arange(50), np.arange(k, 50, 5)), np.arange(k, 50, 5))
+              for k in range(5)]
+    kws = sglm_cv.generate_mult_params({"alpha": [1.0]}, {"model_name": "Poisson"})
+    with pytest.raises(ValueError, match="out of the valid range"):
+        sglm_cv.cv_glm_mult_params(X, y, cv_idx, "Normal", kws)
 
 
 def test_cv_grid_vs_golden(engine, golden):
