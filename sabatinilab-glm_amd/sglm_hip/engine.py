@@ -25,6 +25,7 @@ is reused by the refinement iterations.
 from __future__ import annotations
 
 import math
+import threading
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
@@ -428,15 +429,37 @@ class _Buffers:
 
 _BUF = _Buffers()
 _WORK = {}
+_TLS = threading.local()        # .ns: scratch namespace of an IRLS group thread (0 = main)
+_GROUP_BUF = {}                 # group -> _Buffers
+_GROUP_STREAM = {}              # (device, group) -> torch stream
+_GRAM_LOCK = threading.Lock()   # orders the Gram launches of concurrent IRLS groups ...
+_GRAM_DONE = {}                 # device -> event after the last Gram enqueued (any stream)
+
+
+def _gram_turn():
+    """Make the current stream's next Gram wait for every Gram already enqueued on the device
+    (by any IRLS group): Grams of concurrent groups run one after another at full rate while
+    the groups' latency-bound work overlaps them.  Call with _GRAM_LOCK held."""
+    ev = _GRAM_DONE.get(torch.cuda.current_device())
+    if ev is not None:
+        torch.cuda.current_stream().wait_event(ev)
+
+
+def _gram_done():
+    ev = torch.cuda.Event()
+    ev.record()
+    _GRAM_DONE[torch.cuda.current_device()] = ev
 
 
 def _work(nbytes, dev, tag="main"):
-    """Grow-only scratch buffer per (device, tag); stream-ordered reuse only."""
+    """Grow-only scratch buffer per (group namespace, device, tag); stream-ordered reuse only
+    (each IRLS group thread has its own namespace and stream)."""
     nbytes = max(int(nbytes), 16)
-    t = _WORK.get((dev, tag))
+    key = (getattr(_TLS, "ns", 0), dev, tag)
+    t = _WORK.get(key)
     if t is None or t.numel() < nbytes:
         t = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        _WORK[(dev, tag)] = t
+        _WORK[key] = t
     return t
 
 
@@ -470,7 +493,8 @@ def syrk6_splits(wgs1: int, nsteps: int, nact: int, P: int, slots: int = 1024) -
     return best
 
 
-def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[IrlsStats] = None):
+def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[IrlsStats] = None,
+         bufs: Optional[_Buffers] = None):
     """Run the batched damped-Newton (IRLS) solve; returns (results, final eta tensor)."""
     require_gpu()
     if not reqs:
@@ -481,7 +505,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         raise ValueError("irls(): one loss family per batch")
     B0, P, ld, n, p = len(reqs), d.P, d.ld, d.n, d.p
     dev = d.device
-    bf = _BUF.get(B0, P, ld, dev)
+    bf = (bufs or _BUF).get(B0, P, ld, dev)
     st = _stream()
     log_link = fam == FAM_TWEEDIE_LOG
     reqs0 = list(reqs)
@@ -739,6 +763,111 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
     return res, bf.eta
 
 
+IRLS_GROUPS = int(__import__("os").environ.get("SGLM_IRLS_GROUPS", "2"))
+IRLS_GROUP_MIN = 24             # fits per group below which the batch is not split
+
+
+def _partition(reqs: List[FitReq], ngroups: int) -> List[List[int]]:
+    """Fit indices per group: whole row masks go to the lighter group (fits of one mask share
+    their first Hessian and the lambda-path Hessian sharing); with fewer masks than groups the
+    largest mask's fits are dealt alternately in penalty order."""
+    by_mask = {}
+    for i, r in enumerate(reqs):
+        by_mask.setdefault(r.mask, []).append(i)
+    units = [sorted(v, key=lambda i: reqs[i].lam) for v in by_mask.values()]
+    while len(units) < ngroups:
+        units.sort(key=len)
+        big = units.pop()
+        if len(big) < 2:
+            units.append(big)
+            break
+        units += [big[0::2], big[1::2]]
+    cost = [0.0] * ngroups
+    out = [[] for _ in range(ngroups)]
+    for u in sorted(units, key=len, reverse=True):
+        g = int(np.argmin(cost))
+        out[g] += u
+        cost[g] += len(u)
+    return [sorted(o) for o in out if o]
+
+
+def irls_scored(prob: Problem, reqs: List[FitReq], sets: np.ndarray,
+                stats: Optional[IrlsStats] = None, ngroups: Optional[int] = None):
+    """IRLS + score sums for a batch, as ``ngroups`` independent fit groups, each driven by
+    its own host thread on its own HIP stream.  A group's latency-bound phases (the blocked
+    Cholesky chain, the host decisions between iterations) then run while another group's
+    Gram keeps the MFMA busy.  Returns (results, score sums [B, 2, 2]) in request order."""
+    require_gpu()
+    ng = IRLS_GROUPS if ngroups is None else int(ngroups)
+    fam, power = reqs[0].family, float(reqs[0].power)
+    fresp = [r.resp for r in reqs]
+    # groups pay off when each still fills the chip with Gram work (C4 on one GPU: 120 fits);
+    # a rank's share at 8 GPUs (~15 fits) runs as one group
+    parts = (_partition(reqs, ng) if ng > 1 and len(reqs) >= IRLS_GROUP_MIN * ng
+             else [list(range(len(reqs)))])
+    if len(parts) == 1:
+        res, eta = irls(prob, reqs, stats=stats)
+        return res, score_sums(prob, fam, power, eta, fresp, sets)
+    d = prob.design
+    # shared lazily-built state, built once here before the threads start
+    for r in reqs:
+        prob.mask_stats(r.resp, r.mask)
+    if d.xbits is not None and SYRK_CBITS:
+        for m in sorted({r.mask for r in reqs}):
+            prob.compact(m)
+    if d.xbits is not None and XTR_BITS:
+        d.cbits_full()
+    main = torch.cuda.current_stream()
+    out = [None] * len(parts)
+    errs = []
+
+    def run(g, idx):
+        try:
+            _TLS.ns = g + 1
+            key = (d.device, g)
+            if key not in _GROUP_STREAM:
+                _GROUP_STREAM[key] = torch.cuda.Stream(device=d.device)
+            s = _GROUP_STREAM[key]
+            s.wait_stream(main)
+            with torch.cuda.stream(s):
+                sg = None
+                if stats is not None:
+                    sg = IrlsStats(record=stats.record, trace_phases=stats.trace_phases)
+                res, eta = irls(prob, [reqs[i] for i in idx], stats=sg,
+                                bufs=_GROUP_BUF.setdefault(g, _Buffers()))
+                sums = score_sums(prob, fam, power, eta, [fresp[i] for i in idx], sets[idx])
+            s.synchronize()
+            out[g] = (res, sums, sg)
+        except BaseException as e:  # re-raised in the caller's thread
+            errs.append(e)
+
+    ths = [threading.Thread(target=run, args=(g, idx)) for g, idx in enumerate(parts)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    if errs:
+        raise errs[0]
+    res = [None] * len(reqs)
+    sums = np.zeros((len(reqs), 2, 2))
+    for (rg, sg_sums, sg), idx in zip(out, parts):
+        for q, i in enumerate(idx):
+            res[i] = rg[q]
+            sums[i] = sg_sums[q]
+        if stats is not None and sg is not None:
+            stats.syrk_events += sg.syrk_events
+            stats.fit_iters += sg.fit_iters
+            stats.newton_iters = max(stats.newton_iters, sg.newton_iters)
+            stats.gram_fits += sg.gram_fits
+            stats.reused += sg.reused
+            stats.alg_flop += sg.alg_flop
+            for k, v in sg.phases.items():
+                stats.phases[k] = stats.phases.get(k, 0.0) + v
+    for s_ in {(d.device, g) for g in range(len(parts))}:
+        main.wait_stream(_GROUP_STREAM[s_])
+    return res, sums
+
+
 def _share_grams(bf, prob, reqs, lam, uniq, tol, n, ld, st):
     """Approximate Hessian dedup.  Fits of one (mask, response) are ordered by penalty (the
     lambda path: neighbours have the closest solutions); the max-row distances of consecutive
@@ -847,12 +976,15 @@ def _syrk_cbits(d: Design, bf, prob: Problem, fits: np.ndarray, st, ev=None):
     wb = _lib.query("sglm_syrk_work_bytes", d.P, nact, splits)
     work = _work(wb, d.device) if wb else None
     _lib.call("sglm_gather_w", _p(bf.W), d.ld, _p(fits_d), nact, _p(desc_d), maxrows, st)
-    if ev is not None:                  # the roofline times the Gram kernel alone
-        ev[0].record()
-    _lib.call("sglm_syrk_cbits", _p(desc_d), d.P, _p(fits_d), nact, splits, _p(bf.H), _p(work),
-              st)
-    if ev is not None:
-        ev[1].record()
+    with _GRAM_LOCK:
+        _gram_turn()
+        if ev is not None:              # the roofline times the Gram kernel alone
+            ev[0].record()
+        _lib.call("sglm_syrk_cbits", _p(desc_d), d.P, _p(fits_d), nact, splits, _p(bf.H),
+                  _p(work), st)
+        if ev is not None:
+            ev[1].record()
+        _gram_done()
     bf.keep = (desc_d, fits_d)          # alive until the next launch is enqueued
 
 

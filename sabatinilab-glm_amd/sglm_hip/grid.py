@@ -280,17 +280,16 @@ def run_multi(X, y, groups: Sequence[dict], score_method: str = "mse", coef0=Non
                                  None if coef0 is None else np.asarray(coef0, float),
                                  None if intercept0 is None else float(intercept0)))
         t0 = tick("fit_table", t0)
+        sets = np.array([[local[table[i][3]], local.get(table[i][5], -1)] for i in idxs],
+                        dtype=np.int32)
         if key[0] == "cd":
             from . import cd
             res, eta = cd.enet_batch(prob, [objective(i) for i in idxs], reqs)
-            fam, power = E.FAM_SQUARED, 0.0
+            sums = E.score_sums(prob, E.FAM_SQUARED, 0.0, eta, [table[i][4] for i in idxs],
+                                sets)
         else:
-            res, eta = E.irls(prob, reqs, stats=stats)
-            fam, power = key
+            res, sums = E.irls_scored(prob, reqs, sets, stats=stats)
         t0 = tick("solve", t0)
-        sets = np.array([[local[table[i][3]], local.get(table[i][5], -1)] for i in idxs],
-                        dtype=np.int32)
-        sums = E.score_sums(prob, fam, power, eta, [table[i][4] for i in idxs], sets)
         for q, i in enumerate(idxs):
             rr = res[q]
             _, _, k, m, r, mt = table[i]

@@ -1,9 +1,9 @@
-# Parity tests + C4 bench + phase breakdown + 8-rank share simulation (development loop).
+# Parity tests + C4 bench (grouped and single-group IRLS) + 8-rank share simulation.
 set -e
 export TMPDIR=/tmp
 O=gpurun_out/chk; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1
 timeout -k 10 300 python bench.py --no-cpu --steps 3 --warmup 1 > $O/bench.json 2> $O/bench.err
-timeout -k 10 300 python tools/grid_phases.py > $O/phases.json 2> $O/phases.err
+SGLM_IRLS_GROUPS=1 timeout -k 10 300 python bench.py --no-cpu --steps 3 --warmup 1 > $O/bench_g1.json 2> $O/bench_g1.err
 timeout -k 10 300 python tools/rank_sim.py --world 8 --all > $O/all8.log 2>&1
-timeout -k 10 300 python tools/rank_sim.py --world 8 --rank 2 > $O/r2of8.log 2>&1
+SGLM_IRLS_GROUPS=1 timeout -k 10 300 python tools/rank_sim.py --world 8 --all > $O/all8_g1.log 2>&1
