@@ -12,11 +12,11 @@
 //     diag  (1 wave / fit)          U_kk in LDS (lane = column), forward solve z_k
 //     panel (fits x column chunks)  U_kj = U_kk^-T A_kj (thread = column), rhs_j -= U_kj.z_k
 //     update(fits x 64x64 tiles)    A_ij -= U_ki^T U_kj, 4x4 register micro-tiles
-//   back    (1 WG / fit)            blocked back substitution, delta = -x
+//   back    (1 WG of 1024 / fit)    right-looking blocked back substitution, delta = -x
 // Frozen coordinates (dshift < 0, zero diagonal, or a pivot collapsing below 1e-6 of its
 // original diagonal) get delta = 0.  refactor = 0 reuses the factor and frozen set left in
-// H by a previous call (constant-Hessian Gaussian refinement): only the two triangular
-// solves run.
+// H by a previous call (kept Hessians, constant-Hessian Gaussian refinement): only the two
+// triangular solves run (chol_fwd2 / chol_back2).
 #include "common.h"
 
 namespace sglm {
@@ -275,81 +275,109 @@ __global__ void __launch_bounds__(kCT) chol_update_kernel(float* __restrict__ Ha
     }
 }
 
-// Blocked forward substitution U^T z = rhs with a stored factor (no fit refactored: the
-// kept-Hessian iterations), one workgroup per fit, in place on rhs.  Per 64-block kb: the
-// four waves form the column dot products sum_{r < k0} U[r][k0 + c] z[r] (lane = column c,
-// wave w takes rows r = w mod 4, four rows per pass: 64-column row segments, coalesced),
-// then wave 0 solves the 64 x 64 lower-triangular U_kk^T with readlane broadcasts.
-__global__ void __launch_bounds__(kCT) chol_fwd_kernel(
+// Triangular solves on a stored factor, right-looking, one 1024-thread workgroup per fit: per
+// 64-block, wave 0 solves the 64 x 64 diagonal triangle (readlane broadcasts, branch-free),
+// then all 16 waves fold the solved block into the rest of the right-hand side, which stays in
+// LDS.  The factor is streamed once with many loads in flight: forward, each thread takes 4
+// consecutive columns of the block's 64-row panel (float4 per row, coalesced per row);
+// backward, 16 lanes share one row of the block's 64-column slab (float4 each, a 16-lane
+// shuffle reduction), 64 rows per pass.
+constexpr int kST = 1024;
+
+__device__ __forceinline__ void tri_lower_solve64(const float* __restrict__ H, int32_t P,
+                                                  int k0, const uint8_t* __restrict__ frz,
+                                                  float* z, int lane) {
+    // U_kk^T z_k = r_k (lane = column c of U_kk; a[q] = U[k0+q][k0+c] for q < c, else 0)
+    const float* blk = H + (int64_t)k0 * P + k0 + lane;
+    const float ucc = blk[(int64_t)lane * P];
+    float a[kNB];
+    int cl = lane;
+    asm volatile("" : "+v"(cl));
+#pragma unroll
+    for (int q = 0; q < kNB; ++q) {
+        const float hv = blk[(int64_t)q * P];
+        a[q] = q < cl ? hv : 0.0f;
+    }
+    const float rinv = frz[k0 + lane] ? 0.0f : 1.0f / ucc;
+    float v = z[k0 + lane];
+    int cf = lane;
+    asm volatile("" : "+v"(cf));
+#pragma unroll
+    for (int q = 0; q < kNB; ++q) {
+        const float zq = lanef(v * rinv, q);
+        v = fmaf(-a[q], zq, v);
+        v = cf == q ? zq : v;
+    }
+    z[k0 + lane] = v;
+}
+
+__device__ __forceinline__ void tri_upper_solve64(const float* __restrict__ H, int32_t P,
+                                                  int k0, const uint8_t* __restrict__ frz,
+                                                  float* x, int lane) {
+    // U_kk x_k = r_k (lane = row r of U_kk; row[q] = U[k0+r][k0+q] for q > r, else 0)
+    const float* blk = H + (int64_t)(k0 + lane) * P + k0;
+    const float urr = blk[lane];
+    float row[kNB];
+    int cl = lane;
+    asm volatile("" : "+v"(cl));
+#pragma unroll
+    for (int q = 0; q < kNB; ++q) {
+        const float hv = blk[q];
+        row[q] = q > cl ? hv : 0.0f;
+    }
+    const float rd = frz[k0 + lane] ? 0.0f : 1.0f / urr;
+    float v = x[k0 + lane];
+    int l = lane;
+    asm volatile("" : "+v"(l));
+#pragma unroll
+    for (int q = kNB - 1; q >= 0; --q) {
+        const float xq = lanef(v * rd, q);
+        v = fmaf(-row[q], xq, v);
+        v = l == q ? xq : v;
+    }
+    x[k0 + lane] = v;
+}
+
+__global__ void __launch_bounds__(kST) chol_fwd2_kernel(
     const float* __restrict__ Hall, int32_t P, const int32_t* __restrict__ fits,
     const uint8_t* __restrict__ frozen_all, float* __restrict__ rhs_all) {
-    __shared__ float part[4][kNB];
     __shared__ float z[kMaxP];
     const int fit = fits[blockIdx.x];
     const float* H = Hall + (int64_t)fit * P * P;
     const uint8_t* frz = frozen_all + (int64_t)fit * P;
     float* rhs = rhs_all + (int64_t)fit * P;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int j = tid; j < P; j += kST) z[j] = rhs[j];
     const int nb = P / kNB;
     for (int kb = 0; kb < nb; ++kb) {
         const int k0 = kb * kNB;
-        const float* col = H + k0 + lane;
-        float acc0 = 0.0f, acc1 = 0.0f, acc2 = 0.0f, acc3 = 0.0f;
-        int r = wave;
-        for (; r + 12 < k0; r += 16) {
-            const float h0 = col[(int64_t)r * P], h1 = col[(int64_t)(r + 4) * P];
-            const float h2 = col[(int64_t)(r + 8) * P], h3 = col[(int64_t)(r + 12) * P];
-            acc0 = fmaf(h0, z[r], acc0);
-            acc1 = fmaf(h1, z[r + 4], acc1);
-            acc2 = fmaf(h2, z[r + 8], acc2);
-            acc3 = fmaf(h3, z[r + 12], acc3);
-        }
-        for (; r < k0; r += 4) acc0 = fmaf(col[(int64_t)r * P], z[r], acc0);
-        part[wave][lane] = (acc0 + acc1) + (acc2 + acc3);
         __syncthreads();
-        if (wave == 0) {
-            float v = rhs[k0 + lane] - ((part[0][lane] + part[1][lane]) +
-                                        (part[2][lane] + part[3][lane]));
-            // lane c holds column c of U_kk strictly above the diagonal: a[q] = U[k0 + q][k0 + c]
-            // for q < c, else 0 (masked once at load, so the solve steps carry no masks)
-            const float* blk = H + (int64_t)k0 * P + k0 + lane;
-            const float ucc = blk[(int64_t)lane * P];
-            float a[kNB];
-            int cl = lane;
-            asm volatile("" : "+v"(cl));
-#pragma unroll
-            for (int q = 0; q < kNB; ++q) {
-                const float hv = blk[(int64_t)q * P];
-                a[q] = q < cl ? hv : 0.0f;
-            }
-            const float rinv = frz[k0 + lane] ? 0.0f : 1.0f / ucc;
-            // step q: z_q = v_q / U[q][q] (lane-local product, one broadcast); lanes c > q
-            // subtract U[q][c] z_q (a[q] = 0 for c <= q); lane q then keeps z_q
-            int cf = lane;
-            asm volatile("" : "+v"(cf));
-#pragma unroll
-            for (int q = 0; q < kNB; ++q) {
-                const float zq = lanef(v * rinv, q);
-                v = fmaf(-a[q], zq, v);
-                v = cf == q ? zq : v;
-            }
-            z[k0 + lane] = v;
-            rhs[k0 + lane] = v;
-        }
+        if (wave == 0) tri_lower_solve64(H, P, k0, frz, z, lane);
         __syncthreads();
+        const int c0 = k0 + kNB;
+        const float* pan = H + (int64_t)k0 * P;
+        for (int j = c0 + 4 * tid; j < P; j += 4 * kST) {
+            f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll 16
+            for (int q = 0; q < kNB; ++q) {
+                const f32x4 u = *reinterpret_cast<const f32x4*>(pan + (int64_t)q * P + j);
+                const float zq = z[k0 + q];
+                acc += u * zq;
+            }
+            z[j] -= acc[0];
+            z[j + 1] -= acc[1];
+            z[j + 2] -= acc[2];
+            z[j + 3] -= acc[3];
+        }
     }
+    __syncthreads();
+    for (int j = tid; j < P; j += kST) rhs[j] = z[j];
 }
 
-// Blocked back substitution U x = z, then delta = -x.  Per 64-block (last to first): the
-// four waves form the 64 row dot products with the solved tail (16 rows per wave, four
-// 64-column chunks per pass: 64 loads in flight per lane), then wave 0 solves the 64 x 64
-// triangle with readlane broadcasts, branch-free.
-__global__ void __launch_bounds__(kCT) chol_back_kernel(
+__global__ void __launch_bounds__(kST) chol_back2_kernel(
     const float* __restrict__ Hall, int32_t P, const int32_t* __restrict__ fits,
-    const uint8_t* __restrict__ frozen_all, float* __restrict__ rhs_all,
+    const uint8_t* __restrict__ frozen_all, const float* __restrict__ rhs_all,
     float* __restrict__ delta_all) {
-    __shared__ float sD[kNB][kNB + 1];
-    __shared__ float part[kNB];
     __shared__ float x[kMaxP];
     const int fit = fits[blockIdx.x];
     const float* H = Hall + (int64_t)fit * P * P;
@@ -357,65 +385,27 @@ __global__ void __launch_bounds__(kCT) chol_back_kernel(
     const float* z = rhs_all + (int64_t)fit * P;
     float* delta = delta_all + (int64_t)fit * P;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int sub = tid & 15;                         // float4 slot of a 64-column row slab
+    for (int j = tid; j < P; j += kST) x[j] = z[j];
     const int nb = P / kNB;
     for (int kb = nb - 1; kb >= 0; --kb) {
         const int k0 = kb * kNB;
-        const int r0 = k0 + wave * (kNB / 4);
-        float acc[kNB / 4];
-#pragma unroll
-        for (int rr = 0; rr < kNB / 4; ++rr) acc[rr] = 0.0f;
-        int j = k0 + kNB + lane;
-        for (; j + 3 * 64 < P; j += 4 * 64) {
-            float h[4][kNB / 4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-#pragma unroll
-                for (int rr = 0; rr < kNB / 4; ++rr) h[u][rr] = H[(int64_t)(r0 + rr) * P + j + 64 * u];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const float xj = x[j + 64 * u];
-#pragma unroll
-                for (int rr = 0; rr < kNB / 4; ++rr) acc[rr] = fmaf(h[u][rr], xj, acc[rr]);
-            }
-        }
-        for (; j < P; j += 64) {
-            const float xj = x[j];
-#pragma unroll
-            for (int rr = 0; rr < kNB / 4; ++rr) acc[rr] = fmaf(H[(int64_t)(r0 + rr) * P + j], xj, acc[rr]);
-        }
-#pragma unroll
-        for (int rr = 0; rr < kNB / 4; ++rr) {
-            float v = acc[rr];
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-            if (lane == 0) part[wave * (kNB / 4) + rr] = v;
-        }
-        for (int e = tid; e < kNB * kNB; e += kCT) {
-            const int r = e / kNB, c = e % kNB;
-            sD[r][c] = (r <= c) ? H[(int64_t)(k0 + r) * P + k0 + c] : 0.0f;
-        }
         __syncthreads();
-        if (wave == 0) {
-            float v = z[k0 + lane] - part[lane];
-            const float rd = frz[k0 + lane] ? 0.0f : 1.0f / sD[lane][lane];
-            int l = lane;                            // opaque per block: the lane masks are
-            asm volatile("" : "+v"(l));              // not hoisted out of the kb loop (spills)
-            // this lane's row of U_kk, read once (sD is 0 below the diagonal, and lane q's
-            // own update at step q is overwritten by x_q, so no mask is needed)
-            float row[kNB];
-#pragma unroll
-            for (int q = 0; q < kNB; ++q) row[q] = sD[lane][q];
-#pragma unroll
-            for (int q = kNB - 1; q >= 0; --q) {
-                const float xq = lanef(v * rd, q);   // lane-local product, one broadcast
-                v = fmaf(-row[q], xq, v);
-                v = l == q ? xq : v;
-            }
-            x[k0 + lane] = v;
-        }
+        if (wave == 0) tri_upper_solve64(H, P, k0, frz, x, lane);
         __syncthreads();
+        const f32x4 xk = *reinterpret_cast<const f32x4*>(&x[k0 + 4 * sub]);
+        for (int r0 = 0; r0 < k0; r0 += kST / 16) {
+            const int r = r0 + (tid >> 4);
+            f32x4 u = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (r < k0) u = *reinterpret_cast<const f32x4*>(H + (int64_t)r * P + k0 + 4 * sub);
+            float d = u[0] * xk[0] + u[1] * xk[1] + u[2] * xk[2] + u[3] * xk[3];
+#pragma unroll
+            for (int o = 8; o > 0; o >>= 1) d += __shfl_xor(d, o, 16);
+            if (r < k0 && sub == 0) x[r] -= d;
+        }
     }
-    for (int j = tid; j < P; j += kCT) delta[j] = frz[j] ? 0.0f : -x[j];
+    __syncthreads();
+    for (int j = tid; j < P; j += kST) delta[j] = frz[j] ? 0.0f : -x[j];
 }
 
 }  // namespace sglm
@@ -445,11 +435,11 @@ static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t na
     int st = check_launch("chol_prep_kernel");
     if (st) return st;
     if (nrefac == 0) {                       // stored factors only: two triangular solves
-        chol_fwd_kernel<<<nact, kCT, 0, s>>>(H, P, fits, frozen, rhs);
-        st = check_launch("chol_fwd_kernel");
+        chol_fwd2_kernel<<<nact, kST, 0, s>>>(H, P, fits, frozen, rhs);
+        st = check_launch("chol_fwd2_kernel");
         if (st) return st;
-        chol_back_kernel<<<nact, kCT, 0, s>>>(H, P, fits, frozen, rhs, delta);
-        return check_launch("chol_back_kernel");
+        chol_back2_kernel<<<nact, kST, 0, s>>>(H, P, fits, frozen, rhs, delta);
+        return check_launch("chol_back2_kernel");
     }
     const int nb = P / kNB;
     // block steps in pairs: diag/panel kb, look-ahead update of block row kb+1 only,
@@ -476,8 +466,8 @@ static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t na
     }
     st = check_launch("chol block kernels");
     if (st) return st;
-    chol_back_kernel<<<nact, kCT, 0, s>>>(H, P, fits, frozen, rhs, delta);
-    return check_launch("chol_back_kernel");
+    chol_back2_kernel<<<nact, kST, 0, s>>>(H, P, fits, frozen, rhs, delta);
+    return check_launch("chol_back2_kernel");
 }
 
 extern "C" int sglm_chol_solve_ex(float* H, int32_t P, const int32_t* fits, int32_t nact,
