@@ -80,6 +80,18 @@ __device__ __forceinline__ void waitE(StepE& t) {
                  : "memory");
 }
 
+// all but the youngest 32 loads (two later steps of 16 loads each) have landed: the step
+// whose registers are tied here is complete (3-stage ring, two steps in flight)
+__device__ __forceinline__ void waitE32(StepE& t) {
+    asm volatile("s_waitcnt vmcnt(32)"
+                 : "+v"(t.b[0]), "+v"(t.b[1]), "+v"(t.b[2]), "+v"(t.b[3]), "+v"(t.a[0][0]),
+                   "+v"(t.a[0][1]), "+v"(t.a[0][2]), "+v"(t.a[0][3]), "+v"(t.a[1][0]),
+                   "+v"(t.a[1][1]), "+v"(t.a[1][2]), "+v"(t.a[1][3]), "+v"(t.a[2][0]),
+                   "+v"(t.a[2][1]), "+v"(t.a[2][2]), "+v"(t.a[2][3])
+                 :
+                 : "memory");
+}
+
 __device__ __forceinline__ void mmaE(const StepE& t, int h, f32x16 (&acc)[3][4]) {
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
@@ -113,23 +125,31 @@ eta_bits_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
 #pragma unroll
         for (int n = 0; n < 4; ++n) acc[pc][n] = (f32x16){};
 
-    StepE A, Bs;
+    // 3-stage register ring: the loads of step s+2 are issued before step s's MFMAs, so two
+    // steps' L2 round trips overlap the MFMA work (clamped duplicate loads at the tail)
+    StepE A, Bs, C;
+    const int last = nsteps - 1;
     loadE(A, pb, pa, ld, pstride, 0);
-    waitE(A);
-    int s = 0;
-    for (; s + 1 < nsteps; s += 2) {
-        loadE(Bs, pb, pa, ld, pstride, s + 1);
-        __builtin_amdgcn_sched_barrier(0);          // keep the prefetch ahead of the MFMAs
+    loadE(Bs, pb, pa, ld, pstride, 1 < last ? 1 : last);
+    for (int s = 0; s < nsteps; s += 3) {
+        loadE(C, pb, pa, ld, pstride, s + 2 < last ? s + 2 : last);
+        waitE32(A);
+        __builtin_amdgcn_sched_barrier(0);
         mmaE(A, h, acc);
-        __builtin_amdgcn_sched_barrier(0);          // ... and the wait behind them
-        waitE(Bs);
-        loadE(A, pb, pa, ld, pstride, s + 2 < nsteps ? s + 2 : nsteps - 1);
         __builtin_amdgcn_sched_barrier(0);
-        mmaE(Bs, h, acc);
+        loadE(A, pb, pa, ld, pstride, s + 3 < last ? s + 3 : last);
+        waitE32(Bs);
         __builtin_amdgcn_sched_barrier(0);
-        waitE(A);
+        if (s + 1 < nsteps) mmaE(Bs, h, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        loadE(Bs, pb, pa, ld, pstride, s + 4 < last ? s + 4 : last);
+        waitE32(C);
+        __builtin_amdgcn_sched_barrier(0);
+        if (s + 2 < nsteps) mmaE(C, h, acc);
+        __builtin_amdgcn_sched_barrier(0);
     }
-    if (s < nsteps) mmaE(A, h, acc);
+    waitE(A);
+    waitE(Bs);
 
 #pragma unroll
     for (int n = 0; n < 4; ++n)
