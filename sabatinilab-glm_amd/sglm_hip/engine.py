@@ -764,7 +764,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
 
 
 IRLS_GROUPS = int(__import__("os").environ.get("SGLM_IRLS_GROUPS", "2"))
-IRLS_GROUP_MIN = 24             # fits per group below which the batch is not split
+IRLS_GROUP_MIN = int(__import__("os").environ.get("SGLM_IRLS_GROUP_MIN", "24"))            # fits per group below which the batch is not split
 
 
 def _partition(reqs: List[FitReq], ngroups: int) -> List[List[int]]:
