@@ -192,6 +192,16 @@ int sglm_enet_cd_shared(const double* Q, int32_t p, const int32_t* qidx, int32_t
                         const double* q, const double* l1, const double* l2, int32_t max_sweeps,
                         double tol, double* w, int32_t* sweeps, sglm_stream_t stream);
 
+/* sglm_enet_cd_shared with several fits of one Q per workgroup: workgroup g solves fits
+ * wg_fits[g*fpw .. g*fpw+fpw) (-1 = empty slot), all on Q[wg_q[g]]; row j of Q is read once
+ * per coordinate step for all of them.  fpw must equal sglm_enet_cd_fits_per_wg(p) (>= 2;
+ * (2 fpw + 1) x p doubles of LDS).  Same outputs as sglm_enet_cd_shared (w [fit][p], sweeps). */
+int32_t sglm_enet_cd_fits_per_wg(int32_t p);
+int sglm_enet_cd_grouped(const double* Q, int32_t p, const int32_t* wg_fits, int32_t nwg,
+                         int32_t fpw, const int32_t* wg_q, const double* q, const double* l1,
+                         const double* l2, int32_t max_sweeps, double tol, double* w,
+                         int32_t* sweeps, sglm_stream_t stream);
+
 /* Development entries: a specific bf16 Gram variant (1 = register-staged, 2 = LDS-DMA
  * staged; sglm_syrk uses the default), same arguments as sglm_syrk. */
 int sglm_syrk_v1(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, const float* W,

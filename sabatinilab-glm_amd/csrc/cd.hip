@@ -183,9 +183,331 @@ __global__ void __launch_bounds__(kCDT) enet_cd_shared_kernel(
     if (tid == 0) sweeps_out[f] = sweep;
 }
 
+// Several fits of one shared Q per workgroup (C5: 1280 fits per mask).  The coordinate step
+// reads row j of Q once for all FPW fits (the row stream, not the arithmetic, bounds the dense
+// fits of a lambda path), each fit's decision runs on its own thread, and the fits' running
+// gradients hv and coefficients w live in dynamic LDS (2 x FPW x p doubles, plus Q's diagonal).  A fit that has
+// converged stops moving; the workgroup ends when all its fits have.
+template <int FPW>
+__global__ void __launch_bounds__(kCDT) enet_cd_multi_kernel(
+    const double* __restrict__ Qall, int32_t p, const int32_t* __restrict__ wg_fits,
+    const int32_t* __restrict__ wg_q, const double* __restrict__ qv,
+    const double* __restrict__ l1v, const double* __restrict__ l2v, int32_t max_sweeps,
+    double tol, double* __restrict__ wout, int32_t* __restrict__ sweeps_out) {
+    extern __shared__ double lds[];
+    double* hv = lds;                               // [FPW][p]
+    double* w = lds + (size_t)FPW * p;              // [FPW][p]
+    double* qd = lds + (size_t)2 * FPW * p;         // [p] diagonal of Q
+    __shared__ double s_d[2][FPW], s_maxdw[FPW], s_maxw[FPW];
+    __shared__ int s_act[FPW], s_nact;
+    const int tid = threadIdx.x;
+    const double* Q = Qall + (int64_t)wg_q[blockIdx.x] * p * p;
+    int f_me = -1;                                  // thread i < FPW owns fit slot i
+    double l1 = 0.0, l2 = 0.0;
+    if (tid < FPW) {
+        f_me = wg_fits[blockIdx.x * FPW + tid];
+        s_act[tid] = f_me >= 0;
+        if (f_me >= 0) { l1 = l1v[f_me]; l2 = l2v[f_me]; }
+    }
+    for (int i = 0; i < FPW; ++i) {
+        const int f = wg_fits[blockIdx.x * FPW + i];
+        for (int j = tid; j < p; j += kCDT) {
+            hv[i * p + j] = f >= 0 ? -qv[(int64_t)f * p + j] : 0.0;
+            w[i * p + j] = 0.0;
+        }
+    }
+    for (int j = tid; j < p; j += kCDT) qd[j] = Q[(int64_t)j * p + j];
+    if (tid == 0) {
+        int a = 0;
+        for (int i = 0; i < FPW; ++i) a += wg_fits[blockIdx.x * FPW + i] >= 0;
+        s_nact = a;
+    }
+    __syncthreads();
+    // row j+1 of Q is loaded into registers while coordinate j is decided and applied, so the
+    // global-load latency of the next row overlaps the barriers instead of following them
+    constexpr int kRowRegs = (kCDMaxP + kCDT - 1) / kCDT;
+    const int nr = (p + kCDT - 1) / kCDT;
+    double qn[kRowRegs];
+    int sweep = 0;
+    for (; sweep < max_sweeps && s_nact > 0; ++sweep) {
+        if (tid < FPW) { s_maxdw[tid] = 0.0; s_maxw[tid] = 0.0; }
+#pragma unroll
+        for (int r = 0; r < kRowRegs; ++r) {
+            const int k = tid + r * kCDT;
+            qn[r] = (r < nr && k < p) ? Q[k] : 0.0;
+        }
+        for (int j = 0; j < p; ++j) {
+            double qc[kRowRegs];
+#pragma unroll
+            for (int r = 0; r < kRowRegs; ++r) qc[r] = qn[r];
+            if (j + 1 < p) {
+                const double* Qn = Q + (int64_t)(j + 1) * p;
+#pragma unroll
+                for (int r = 0; r < kRowRegs; ++r) {
+                    const int k = tid + r * kCDT;
+                    if (r < nr && k < p) qn[r] = Qn[k];
+                }
+            }
+            if (tid < FPW) {
+                const double qjj = qd[j];
+                double d = 0.0;
+                if (s_act[tid] && qjj > 0.0) {
+                    double* wi = w + tid * p;
+                    const double wj = wi[j];
+                    const double rho = -(hv[tid * p + j] - qjj * wj);
+                    const double mag = fabs(rho) - l1;
+                    const double nw = mag > 0.0 ? copysign(mag, rho) / (qjj + l2) : 0.0;
+                    d = nw - wj;
+                    wi[j] = nw;
+                    s_maxdw[tid] = fmax(s_maxdw[tid], fabs(d));
+                    s_maxw[tid] = fmax(s_maxw[tid], fabs(nw));
+                }
+                s_d[j & 1][tid] = d;
+            }
+            __syncthreads();
+            double dv[FPW];
+            bool any = false;
+#pragma unroll
+            for (int i = 0; i < FPW; ++i) {
+                dv[i] = s_d[j & 1][i];
+                any |= dv[i] != 0.0;
+            }
+            if (any) {
+#pragma unroll
+                for (int r = 0; r < kRowRegs; ++r) {
+                    const int k = tid + r * kCDT;
+                    if (r < nr && k < p) {
+#pragma unroll
+                        for (int i = 0; i < FPW; ++i) hv[i * p + k] += qc[r] * dv[i];
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        __syncthreads();
+        if (tid < FPW && s_act[tid]) {
+            const double mdw = s_maxdw[tid], mw = s_maxw[tid];
+            if (mw == 0.0 || mdw <= tol * mw) {
+                s_act[tid] = 0;
+                sweeps_out[f_me] = sweep + 1;
+            }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int a = 0;
+            for (int i = 0; i < FPW; ++i) a += s_act[i];
+            s_nact = a;
+        }
+        __syncthreads();
+    }
+    if (tid < FPW && f_me >= 0 && s_act[tid]) sweeps_out[f_me] = sweep;
+    for (int i = 0; i < FPW; ++i) {
+        const int f = wg_fits[blockIdx.x * FPW + i];
+        if (f < 0) continue;
+        for (int j = tid; j < p; j += kCDT) wout[(int64_t)f * p + j] = w[i * p + j];
+    }
+}
+
+// Register-resident form (p <= kCDT * kRegRows): thread t owns coordinates k = t + kCDT r; it
+// holds those coordinates' running gradients hv, coefficients w and Q diagonal for all FPW
+// fits in registers.  Coordinate j's owner decides the FPW fits' moves on its own and
+// publishes them (double-buffered by j parity); after ONE barrier every thread folds row j of
+// Q (prefetched into registers one coordinate ahead) into its hv.  No LDS traffic on the
+// gradient, one barrier per coordinate.
+constexpr int kRegRows = 8;
+
+template <int FPW>
+__global__ void __launch_bounds__(kCDT) enet_cd_reg_kernel(
+    const double* __restrict__ Qall, int32_t p, const int32_t* __restrict__ wg_fits,
+    const int32_t* __restrict__ wg_q, const double* __restrict__ qv,
+    const double* __restrict__ l1v, const double* __restrict__ l2v, int32_t max_sweeps,
+    double tol, double* __restrict__ wout, int32_t* __restrict__ sweeps_out) {
+    __shared__ double s_d[2][FPW];
+    __shared__ double s_red[2][FPW][kCDT / 64];
+    __shared__ int s_act[FPW];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const double* Q = Qall + (int64_t)wg_q[blockIdx.x] * p * p;
+    int fit[FPW];
+    double l1[FPW], l2[FPW];
+#pragma unroll
+    for (int i = 0; i < FPW; ++i) {
+        fit[i] = wg_fits[blockIdx.x * FPW + i];
+        l1[i] = fit[i] >= 0 ? l1v[fit[i]] : 0.0;
+        l2[i] = fit[i] >= 0 ? l2v[fit[i]] : 0.0;
+    }
+    double hv[FPW][kRegRows], w[FPW][kRegRows], qdg[kRegRows], qn[kRegRows];
+#pragma unroll
+    for (int r = 0; r < kRegRows; ++r) {
+        const int k = tid + r * kCDT;
+        const bool ok = k < p;
+        qdg[r] = ok ? Q[(int64_t)k * p + k] : 0.0;
+#pragma unroll
+        for (int i = 0; i < FPW; ++i) {
+            hv[i][r] = (ok && fit[i] >= 0) ? -qv[(int64_t)fit[i] * p + k] : 0.0;
+            w[i][r] = 0.0;
+        }
+    }
+    bool act[FPW];
+#pragma unroll
+    for (int i = 0; i < FPW; ++i) act[i] = fit[i] >= 0;
+    int sweep = 0;
+    int sw_done[FPW];
+#pragma unroll
+    for (int i = 0; i < FPW; ++i) sw_done[i] = max_sweeps;
+    for (; sweep < max_sweeps; ++sweep) {
+        bool anyact = false;
+#pragma unroll
+        for (int i = 0; i < FPW; ++i) anyact |= act[i];
+        if (!anyact) break;
+        double mdw[FPW], mw[FPW];
+#pragma unroll
+        for (int i = 0; i < FPW; ++i) { mdw[i] = 0.0; mw[i] = 0.0; }
+#pragma unroll
+        for (int r = 0; r < kRegRows; ++r) {
+            const int k = tid + r * kCDT;
+            qn[r] = k < p ? Q[k] : 0.0;                       // row 0
+        }
+#pragma unroll
+        for (int rr = 0; rr < kRegRows; ++rr) {               // owner register of coordinate j
+            for (int t = 0; t < kCDT; ++t) {
+                const int j = t + rr * kCDT;
+                if (j >= p) break;                            // uniform
+                double qc[kRegRows];
+#pragma unroll
+                for (int r = 0; r < kRegRows; ++r) qc[r] = qn[r];
+                if (j + 1 < p) {
+                    const double* Qn = Q + (int64_t)(j + 1) * p;
+#pragma unroll
+                    for (int r = 0; r < kRegRows; ++r) {
+                        const int k = tid + r * kCDT;
+                        if (k < p) qn[r] = Qn[k];
+                    }
+                }
+                if (tid == t) {                               // the owner decides
+                    const double qjj = qdg[rr];
+#pragma unroll
+                    for (int i = 0; i < FPW; ++i) {
+                        double d = 0.0;
+                        if (act[i] && qjj > 0.0) {
+                            const double wj = w[i][rr];
+                            const double rho = -(hv[i][rr] - qjj * wj);
+                            const double mag = fabs(rho) - l1[i];
+                            const double nw = mag > 0.0 ? copysign(mag, rho) / (qjj + l2[i]) : 0.0;
+                            d = nw - wj;
+                            w[i][rr] = nw;
+                            mdw[i] = fmax(mdw[i], fabs(d));
+                            mw[i] = fmax(mw[i], fabs(nw));
+                        }
+                        s_d[j & 1][i] = d;
+                    }
+                }
+                __syncthreads();
+                double dv[FPW];
+                bool any = false;
+#pragma unroll
+                for (int i = 0; i < FPW; ++i) {
+                    dv[i] = s_d[j & 1][i];
+                    any |= dv[i] != 0.0;
+                }
+                if (any) {
+#pragma unroll
+                    for (int r = 0; r < kRegRows; ++r)
+#pragma unroll
+                        for (int i = 0; i < FPW; ++i) hv[i][r] = fma(qc[r], dv[i], hv[i][r]);
+                }
+            }
+        }
+        // per-fit convergence: block max of the sweep's max |dw| and max |w|
+#pragma unroll
+        for (int i = 0; i < FPW; ++i) {
+            double a = mdw[i], b = mw[i];
+            for (int o = 32; o > 0; o >>= 1) {
+                a = fmax(a, __shfl_xor(a, o, 64));
+                b = fmax(b, __shfl_xor(b, o, 64));
+            }
+            if (lane == 0) { s_red[0][i][wave] = a; s_red[1][i][wave] = b; }
+        }
+        __syncthreads();
+        if (tid < FPW && act[tid > FPW ? 0 : tid]) {
+            double a = 0.0, b = 0.0;
+            for (int v = 0; v < kCDT / 64; ++v) {
+                a = fmax(a, s_red[0][tid][v]);
+                b = fmax(b, s_red[1][tid][v]);
+            }
+            s_act[tid] = !(b == 0.0 || a <= tol * b);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < FPW; ++i) {
+            if (act[i] && !s_act[i]) sw_done[i] = sweep + 1;
+            act[i] = act[i] && s_act[i];
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < FPW; ++i) {
+        if (fit[i] < 0) continue;
+        if (tid == 0) sweeps_out[fit[i]] = sw_done[i];
+#pragma unroll
+        for (int r = 0; r < kRegRows; ++r) {
+            const int k = tid + r * kCDT;
+            if (k < p) wout[(int64_t)fit[i] * p + k] = w[i][r];
+        }
+    }
+}
+
+template <int FPW>
+static int launch_cd_multi(const double* Q, int32_t p, const int32_t* wg_fits, int32_t nwg,
+                           const int32_t* wg_q, const double* q, const double* l1,
+                           const double* l2, int32_t max_sweeps, double tol, double* w,
+                           int32_t* sweeps, hipStream_t s) {
+    const size_t lds = (size_t)(2 * FPW + 1) * p * sizeof(double);
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&enet_cd_multi_kernel<FPW>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+        set_error("enet_cd_multi_kernel: %zu bytes of LDS refused", lds);
+        return SGLM_EHIP;
+    }
+    enet_cd_multi_kernel<FPW><<<nwg, kCDT, lds, s>>>(Q, p, wg_fits, wg_q, q, l1, l2, max_sweeps,
+                                                   tol, w, sweeps);
+    return check_launch("enet_cd_multi_kernel");
+}
+
 }  // namespace sglm
 
 using namespace sglm;
+
+// fits per workgroup that the LDS holds ((2 fpw + 1) x p doubles within 160 KiB; 1 if none)
+extern "C" int32_t sglm_enet_cd_fits_per_wg(int32_t p) {
+    if (p <= kCDT * kRegRows) return 4;              // register-resident form
+    const int64_t row = (int64_t)p * sizeof(double);
+    for (int f : {8, 4, 2})
+        if ((2 * f + 1) * row <= 160 * 1024 - 1024) return f;
+    return 1;
+}
+
+extern "C" int sglm_enet_cd_grouped(const double* Q, int32_t p, const int32_t* wg_fits,
+                                    int32_t nwg, int32_t fpw, const int32_t* wg_q,
+                                    const double* q, const double* l1, const double* l2,
+                                    int32_t max_sweeps, double tol, double* w, int32_t* sweeps,
+                                    sglm_stream_t stream) {
+    if (nwg <= 0) return SGLM_OK;
+    if (!Q || !wg_fits || !wg_q || !q || !l1 || !l2 || !w || !sweeps || p <= 0 ||
+        fpw != sglm_enet_cd_fits_per_wg(p) || fpw < 2) {
+        set_error("sglm_enet_cd_grouped: bad args (p=%d fpw=%d)", p, fpw);
+        return SGLM_EINVAL;
+    }
+    hipStream_t s = as_stream(stream);
+    if (p <= kCDT * kRegRows && fpw >= 4) {          // register-resident form
+        enet_cd_reg_kernel<4><<<nwg, kCDT, 0, s>>>(Q, p, wg_fits, wg_q, q, l1, l2, max_sweeps,
+                                                   tol, w, sweeps);
+        return check_launch("enet_cd_reg_kernel");
+    }
+    switch (fpw) {
+        case 8: return launch_cd_multi<8>(Q, p, wg_fits, nwg, wg_q, q, l1, l2, max_sweeps, tol, w, sweeps, s);
+        case 4: return launch_cd_multi<4>(Q, p, wg_fits, nwg, wg_q, q, l1, l2, max_sweeps, tol, w, sweeps, s);
+        default: return launch_cd_multi<2>(Q, p, wg_fits, nwg, wg_q, q, l1, l2, max_sweeps, tol, w, sweeps, s);
+    }
+}
 
 extern "C" size_t sglm_enet_work_bytes(int32_t p, int32_t nact) {
     return (size_t)nact * (size_t)p * (size_t)p * sizeof(double);

@@ -46,6 +46,9 @@ SIGNATURES = {
     "sglm_center_gram": (C.c_int, [_vp, _i32, _i32, _vp, _i32, _i32, _vp, _vp]),
     "sglm_enet_cd_shared": (C.c_int, [_vp, _i32, _vp, _i32, _vp, _vp, _vp, _i32, C.c_double,
                                       _vp, _vp, _vp]),
+    "sglm_enet_cd_fits_per_wg": (_i32, [_i32]),
+    "sglm_enet_cd_grouped": (C.c_int, [_vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _i32,
+                                       C.c_double, _vp, _vp, _vp]),
     "sglm_syrk_v1": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
     "sglm_syrk_variant": (C.c_int, [_i32, _vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _vp,
                                     _vp]),

@@ -130,7 +130,7 @@ def solve(prob: E.Problem, grams: SharedGrams, fits: Sequence[dict], c: torch.Te
         cpv[sel_t] = cc[:, p]
         if center:
             gslot = torch.tensor([grams.slot[masks[i]] for i in sel], device=dev)
-            g = grams.H[gslot][:, :p, p].to(torch.float64)      # X^T m (upper: rows < p)
+            g = grams.H[:, :p, p][gslot].to(torch.float64)      # X^T m (upper: rows < p)
             n = torch.from_numpy(cnt[sel]).to(dev)
             gv[sel_t] = g
             q[sel_t] = cc[:, :p] - g * (cc[:, p] / n.clamp_min(1))[:, None]
@@ -141,9 +141,26 @@ def solve(prob: E.Problem, grams: SharedGrams, fits: Sequence[dict], c: torch.Te
     w = torch.empty((B, p), dtype=torch.float64, device=dev)
     sw = torch.empty(B, dtype=torch.int32, device=dev)
     max_sweeps = int(max(max(int(f["max_iter"]) for f in fits), 10000))
-    qidx_d = torch.from_numpy(qidx).to(dev)
-    _lib.call("sglm_enet_cd_shared", E._p(grams.Qt), p, E._p(qidx_d), B, E._p(q), E._p(l1),
-              E._p(l2), max_sweeps, CD_TOL, E._p(w), E._p(sw), E._stream())
+    fpw = int(_lib.query("sglm_enet_cd_fits_per_wg", p))
+    if fpw >= 2:
+        # fits sharing a Q go to the same workgroups, fpw at a time (padding slots -1)
+        wg_f, wg_q = [], []
+        for qv_ in np.unique(qidx):
+            fs = np.flatnonzero(qidx == qv_)
+            for c0 in range(0, fs.size, fpw):
+                chunk = np.full(fpw, -1, dtype=np.int32)
+                chunk[: min(fpw, fs.size - c0)] = fs[c0:c0 + fpw]
+                wg_f.append(chunk)
+                wg_q.append(int(qv_))
+        wgf_d = torch.from_numpy(np.concatenate(wg_f)).to(dev)
+        wgq_d = torch.from_numpy(np.array(wg_q, dtype=np.int32)).to(dev)
+        _lib.call("sglm_enet_cd_grouped", E._p(grams.Qt), p, E._p(wgf_d), len(wg_q), fpw,
+                  E._p(wgq_d), E._p(q), E._p(l1), E._p(l2), max_sweeps, CD_TOL, E._p(w),
+                  E._p(sw), E._stream())
+    else:
+        qidx_d = torch.from_numpy(qidx).to(dev)
+        _lib.call("sglm_enet_cd_shared", E._p(grams.Qt), p, E._p(qidx_d), B, E._p(q),
+                  E._p(l1), E._p(l2), max_sweeps, CD_TOL, E._p(w), E._p(sw), E._stream())
     fi = torch.tensor([bool(f["fit_intercept"]) for f in fits], device=dev)
     n = torch.from_numpy(cnt).to(dev)
     b = torch.where(fi & (n > 0), (cpv - (gv * w).sum(1)) / n.clamp_min(1), 0.0)
@@ -194,7 +211,7 @@ def cv_enet_path(X, Y, cv_idx, alphas: Sequence[float], l1_ratio: float = 0.5,
         masks += [tr, te]
     FULL = len(masks)
     masks.append(np.ones(n, np.uint8))
-    prob = E.Problem(design, [Y[:, r] for r in range(R)], masks)
+    prob = E.Problem(design, Y, masks)
     grams = SharedGrams(prob)
     grams.ensure(range(len(masks)))
     pairs = [(r, m) for r in range(R) for m in range(len(masks))]
@@ -210,10 +227,11 @@ def cv_enet_path(X, Y, cv_idx, alphas: Sequence[float], l1_ratio: float = 0.5,
                 keys.append((r, j, k))
     w, b, sw, conv = solve(prob, grams, fits, c, [ci[(r, f["mask"])] for (r, _, _), f in zip(keys, fits)])
     # ---- scores from Gram algebra: SS(mask) = y'My - 2 beta'c + beta' G beta (augmented)
-    Yd = torch.from_numpy(Y.T.copy()).to(dev)                    # R x n float64
     Md = prob.M[:, :n].to(torch.float64)
-    yyh = (Md @ (Yd * Yd).T).cpu().numpy()                       # F x R: sum m y^2
-    del Md, Yd
+    y2t = (prob.Yd64 * prob.Yd64).t().contiguous()              # R x n (a GEMM with a long
+    yyh = (Md @ y2t.t()).cpu().numpy()                           # K picks a fast kernel this
+    del y2t                                                      # way): F x R, sum m y^2
+    del Md
     cnt = np.array([float(prob.mask_count(m)) for m in range(len(masks))])
     c_p = c[:, p].cpu().numpy()                                  # sum m y per (r, m) pair
     beta = np.zeros((len(fits), design.P))

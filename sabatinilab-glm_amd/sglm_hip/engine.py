@@ -252,27 +252,55 @@ class Design:
 
 
 # ------------------------------------------------------------------------------ problem
+class _Columns:
+    """Read-only list view of the columns of an (n x R) array (host copies on access)."""
+
+    def __init__(self, a):
+        self.a = a
+
+    def __len__(self):
+        return self.a.shape[1]
+
+    def __getitem__(self, r):
+        return np.ascontiguousarray(self.a[:, r], dtype=np.float64)
+
+    def __iter__(self):
+        return (self[r] for r in range(len(self)))
+
+
 class Problem:
     """A design plus the response columns and row masks that a batch of fits refers to."""
 
-    def __init__(self, design: Design, ys: Sequence[np.ndarray], masks: Sequence[np.ndarray]):
+    def __init__(self, design: Design, ys, masks: Sequence[np.ndarray]):
+        """``ys``: a list of response vectors, or one (n x R) float64 array of R responses
+        (multi-response paths: uploaded once, transposed on the device; ``Yd64`` keeps the
+        float64 device copy)."""
         self.design = design
         n, ld, dev = design.n, design.ld, design.device
-        self.ys = [np.asarray(y, dtype=np.float64).reshape(-1) for y in ys]
         self.masks = [np.asarray(m, dtype=np.uint8).reshape(-1) for m in masks]
-        for y in self.ys:
-            if y.shape[0] != n:
-                raise ValueError(f"response length {y.shape[0]} != n_samples {n}")
         for m in self.masks:
             if m.shape[0] != n:
                 raise ValueError(f"mask length {m.shape[0]} != n_samples {n}")
-        Y = np.zeros((len(self.ys), ld), dtype=np.float32)
-        for r, y in enumerate(self.ys):
-            Y[r, :n] = y
+        self.Yd64 = None
+        if isinstance(ys, np.ndarray) and ys.ndim == 2:
+            if ys.shape[0] != n:
+                raise ValueError(f"response length {ys.shape[0]} != n_samples {n}")
+            self.ys = _Columns(ys)
+            self.Yd64 = torch.from_numpy(np.ascontiguousarray(ys, dtype=np.float64)).to(dev)
+            self.Y = torch.zeros((ys.shape[1], ld), dtype=torch.float32, device=dev)
+            self.Y[:, :n] = self.Yd64.t().float()
+        else:
+            self.ys = [np.asarray(y, dtype=np.float64).reshape(-1) for y in ys]
+            for y in self.ys:
+                if y.shape[0] != n:
+                    raise ValueError(f"response length {y.shape[0]} != n_samples {n}")
+            Y = np.zeros((len(self.ys), ld), dtype=np.float32)
+            for r, y in enumerate(self.ys):
+                Y[r, :n] = y
+            self.Y = torch.from_numpy(Y).to(dev)
         M = np.zeros((len(self.masks), ld), dtype=np.uint8)
         for f, m in enumerate(self.masks):
             M[f, :n] = m
-        self.Y = torch.from_numpy(Y).to(dev)
         self.M = torch.from_numpy(M).to(dev)
         self._stats = {}
         self._groups = None
