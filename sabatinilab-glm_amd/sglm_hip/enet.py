@@ -125,11 +125,12 @@ def solve(prob: E.Problem, grams: SharedGrams, fits: Sequence[dict], c: torch.Te
             continue
         qi = grams.centred([masks[i] for i in sel], center)
         qidx[sel] = qi
-        sel_t = torch.tensor(sel, device=dev)
-        cc = c[torch.tensor([cidx[i] for i in sel], device=dev)]
+        sel_t = torch.from_numpy(np.asarray(sel, dtype=np.int64)).to(dev)
+        cc = c[torch.from_numpy(np.asarray(cidx, dtype=np.int64)[sel]).to(dev)]
         cpv[sel_t] = cc[:, p]
         if center:
-            gslot = torch.tensor([grams.slot[masks[i]] for i in sel], device=dev)
+            gslot = torch.from_numpy(np.array([grams.slot[masks[i]] for i in sel],
+                                              dtype=np.int64)).to(dev)
             g = grams.H[:, :p, p][gslot].to(torch.float64)      # X^T m (upper: rows < p)
             n = torch.from_numpy(cnt[sel]).to(dev)
             gv[sel_t] = g
@@ -161,7 +162,7 @@ def solve(prob: E.Problem, grams: SharedGrams, fits: Sequence[dict], c: torch.Te
         qidx_d = torch.from_numpy(qidx).to(dev)
         _lib.call("sglm_enet_cd_shared", E._p(grams.Qt), p, E._p(qidx_d), B, E._p(q),
                   E._p(l1), E._p(l2), max_sweeps, CD_TOL, E._p(w), E._p(sw), E._stream())
-    fi = torch.tensor([bool(f["fit_intercept"]) for f in fits], device=dev)
+    fi = torch.from_numpy(np.array([bool(f["fit_intercept"]) for f in fits])).to(dev)
     n = torch.from_numpy(cnt).to(dev)
     b = torch.where(fi & (n > 0), (cpv - (gv * w).sum(1)) / n.clamp_min(1), 0.0)
     swh = sw.cpu().numpy()
