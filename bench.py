@@ -38,6 +38,7 @@ CONFIGS = {
     "c5": (1_000_000, 50, 20, 5, 20),
 }
 C5_RESPONSES = 64
+INIT_PASSES = 2
 
 
 def parse():
@@ -251,6 +252,12 @@ def main():
     def step(stats=None):
         return grid.run(design, s.y, cv_idx, objs, rolls, stats=stats)
 
+    # engine initialisation (part of setup, not a warmup step): the process's first two grids
+    # pay one-time HIP runtime / allocator costs (the second grid of a fresh process measured
+    # 20-30 ms slower than later ones on an 8-rank share), so two untimed passes run before the
+    # W warmup steps
+    for _ in range(INIT_PASSES):
+        step()
     for _ in range(a.warmup):
         step()
     stats = E.IrlsStats(record=True)
@@ -314,6 +321,7 @@ def main():
                 "distinct_hessians_per_grid": gram_fits / a.steps,
                 "kept_factor_fit_iters_per_grid": reused / a.steps,
                 "hess_reuse_tol": E.HESS_REUSE_TOL,
+                "init_passes_untimed": INIT_PASSES,
                 "grid_roofline_frac": alg_flop / elapsed / (world * PEAK_BF16_TFLOPS * 1e12),
                 "grid_roofline_note": "SURVEY.md 8(d): sum over fit-iterations of "
                                       "n p'(p'+1) + 4 n p' + p'^3/3 + 2 p'^2, / wall / "

@@ -250,6 +250,14 @@ int sglm_loss_trials(int32_t family, float power, int64_t n, int64_t ld, int32_t
                      const int32_t* fit_resp, const int32_t* fit_mask, const float* t,
                      int32_t T, double* out, void* work, sglm_stream_t stream);
 
+/* sglm_loss_trials plus dmax[k] = max over the rows of mask fit_mask[k] of |deta[k][i]| (B
+ * floats, zeroed by the call): the step's predictor drift per unit step length, returned with
+ * the trial losses so that the host needs one round trip per Newton iteration. */
+int sglm_loss_trials_max(int32_t family, float power, int64_t n, int64_t ld, int32_t B,
+                         const float* eta, const float* deta, const float* Y, const uint8_t* M,
+                         const int32_t* fit_resp, const int32_t* fit_mask, const float* t,
+                         int32_t T, double* out, float* dmax, void* work, sglm_stream_t stream);
+
 /* eta[k][i] += step[k] * deta[k][i]  (host-chosen step per fit, device array). */
 int sglm_eta_axpy(int64_t n, int64_t ld, int32_t B, const float* step, const float* deta,
                   float* eta, sglm_stream_t stream);

@@ -259,8 +259,10 @@ __global__ void __launch_bounds__(256) loss_trials_kernel(
     int32_t family, float power, int64_t n, int64_t ld, const float* __restrict__ eta,
     const float* __restrict__ deta, const float* __restrict__ Y, const uint8_t* __restrict__ M,
     const int32_t* __restrict__ fit_resp, const int32_t* __restrict__ fit_mask,
-    const float* __restrict__ tv, int32_t T, double* __restrict__ part) {
+    const float* __restrict__ tv, int32_t T, double* __restrict__ part,
+    float* __restrict__ dmax) {
     __shared__ double sh[4];
+    __shared__ float shm[4];
     const int k = blockIdx.y;
     const int32_t nchunks = gridDim.x;
     const float* e = eta + (int64_t)k * ld;
@@ -269,18 +271,28 @@ __global__ void __launch_bounds__(256) loss_trials_kernel(
     const uint8_t* m = M + (int64_t)fit_mask[k] * ld;
     double acc[kMaxTrials];
     for (int j = 0; j < kMaxTrials; ++j) acc[j] = 0.0;
+    float mx = 0.0f;
     const int64_t i0 = (int64_t)blockIdx.x * kRowChunk;
     const int64_t i1 = min(i0 + kRowChunk, n);
     for (int64_t i = i0 + threadIdx.x; i < i1; i += 256) {
         const double mi = (double)m[i];
         if (mi == 0.0) continue;
         const double yi = y[i], ei = e[i], di = d[i];
+        mx = fmaxf(mx, fabsf((float)di));
         for (int j = 0; j < T; ++j)
             acc[j] += mi * half_loss_d(family, (double)power, yi, ei + (double)tv[j] * di);
     }
     for (int j = 0; j < T; ++j) {
         const double s = block_sum_d(acc[j], sh);
         if (threadIdx.x == 0) part[((int64_t)k * T + j) * nchunks + blockIdx.x] = s;
+    }
+    if (dmax) {                 // max |d_eta| over the fit's rows (Hessian drift bound)
+        for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+        if ((threadIdx.x & 63) == 0) shm[threadIdx.x >> 6] = mx;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            atomicMax(reinterpret_cast<unsigned int*>(dmax + k),
+                      __float_as_uint(fmaxf(fmaxf(shm[0], shm[1]), fmaxf(shm[2], shm[3]))));
     }
 }
 
@@ -515,7 +527,30 @@ int sglm_loss_trials(int32_t family, float power, int64_t n, int64_t ld, int32_t
     (void)ld;
     const int32_t nc = row_chunks(n);
     hipStream_t s = as_stream(stream);
-    loss_trials_kernel<<<dim3((unsigned)nc, (unsigned)B), 256, 0, s>>>(family, power, n, ld, eta, deta, Y, M, fit_resp, fit_mask, t, T, (double*)work);
+    loss_trials_kernel<<<dim3((unsigned)nc, (unsigned)B), 256, 0, s>>>(family, power, n, ld, eta, deta, Y, M, fit_resp, fit_mask, t, T, (double*)work, nullptr);
+    int st = check_launch("loss_trials_kernel");
+    if (st) return st;
+    const int64_t rows = (int64_t)B * T;
+    reduce_chunks_d<<<grid1(rows, 256), 256, 0, s>>>((const double*)work, rows, nc, out);
+    return check_launch("reduce_chunks_d");
+}
+
+int sglm_loss_trials_max(int32_t family, float power, int64_t n, int64_t ld, int32_t B,
+                         const float* eta, const float* deta, const float* Y, const uint8_t* M,
+                         const int32_t* fit_resp, const int32_t* fit_mask, const float* t,
+                         int32_t T, double* out, float* dmax, void* work, sglm_stream_t stream) {
+    if (B <= 0) return SGLM_OK;
+    if (T < 1 || T > kMaxTrials || !eta || !deta || !Y || !M || !t || !out || !dmax || !work) {
+        set_error("sglm_loss_trials_max: bad args (T=%d)", T);
+        return SGLM_EINVAL;
+    }
+    const int32_t nc = row_chunks(n);
+    hipStream_t s = as_stream(stream);
+    if (hipMemsetAsync(dmax, 0, sizeof(float) * (size_t)B, s) != hipSuccess) {
+        set_error("sglm_loss_trials_max: hipMemsetAsync failed");
+        return SGLM_EHIP;
+    }
+    loss_trials_kernel<<<dim3((unsigned)nc, (unsigned)B), 256, 0, s>>>(family, power, n, ld, eta, deta, Y, M, fit_resp, fit_mask, t, T, (double*)work, dmax);
     int st = check_launch("loss_trials_kernel");
     if (st) return st;
     const int64_t rows = (int64_t)B * T;

@@ -61,6 +61,8 @@ SIGNATURES = {
     "sglm_rowsum_work_bytes": (_sz, [_i32, _i32, _i64]),
     "sglm_loss_trials": (C.c_int, [_i32, _f32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
                                    _vp, _i32, _vp, _vp, _vp]),
+    "sglm_loss_trials_max": (C.c_int, [_i32, _f32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp,
+                                       _vp, _vp, _i32, _vp, _vp, _vp, _vp]),
     "sglm_eta_axpy": (C.c_int, [_i64, _i64, _i32, _vp, _vp, _vp, _vp]),
     "sglm_eta_axpy_max": (C.c_int, [_i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "sglm_eta_pair_absmax": (C.c_int, [_i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),

@@ -479,6 +479,20 @@ def _gram_done():
     _GRAM_DONE[torch.cuda.current_device()] = ev
 
 
+_PINNED = {}
+
+
+def _pinned(tag, numel, dtype):
+    """Grow-only pinned host buffer per (group namespace, tag): page-locked allocation is slow,
+    so the per-iteration readback buffers are allocated once and reused (flat; callers view)."""
+    key = (getattr(_TLS, "ns", 0), tag, dtype)
+    t = _PINNED.get(key)
+    if t is None or t.numel() < numel:
+        t = torch.zeros(int(numel), dtype=dtype).pin_memory()
+        _PINNED[key] = t
+    return t[:numel]
+
+
 def _work(nbytes, dev, tag="main"):
     """Grow-only scratch buffer per (group namespace, device, tag); stream-ordered reuse only
     (each IRLS group thread has its own namespace and stream)."""
@@ -577,9 +591,16 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
     fit_resp = torch.from_numpy(fresp_h).to(dev)
     fit_mask = torch.from_numpy(fmask_h).to(dev)
     drift = np.full(B0, np.inf)         # predictor drift since each fit's Hessian was formed
+    # one host round trip per Newton iteration: the gradient, the step direction, the trial
+    # losses and the step's predictor drift come back together (pinned buffers, async copies)
     dmax_d = torch.zeros(B0, dtype=torch.float32, device=dev)
-    dmax_h = torch.zeros(B0, dtype=torch.float32).pin_memory()
-    dmax_pending = False
+    dmax_h = _pinned("dmax", B0, torch.float32)
+    g_h = _pinned("g", B0 * P, torch.float64).view(B0, P)
+    delta_h = _pinned("delta", B0 * P, torch.float32).view(B0, P)
+    L_h = _pinned("L", B0 * 8, torch.float64)
+    beta_pin = _pinned("beta", B0 * P, torch.float64).view(B0, P)
+    beta64_d = torch.zeros((B0, P), dtype=torch.float64, device=dev)
+    lamp_d = torch.from_numpy(lam[:, None] * penal).to(dev)        # lam * penalty mask
     gram_now = np.zeros(B0, dtype=bool)
     active = np.ones(B0, dtype=bool)
     n_iter = np.zeros(B0, dtype=np.int64)
@@ -621,21 +642,26 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         if act.size == 0:
             break
         if act.size <= COMPACT_FRAC * B and B - act.size >= COMPACT_MIN:
-            if dmax_pending:            # last step's drift, still in the old slot order
-                torch.cuda.current_stream().synchronize()
-                drift += dmax_h.numpy()[:B].astype(np.float64)
-                dmax_pending = False
             retire(np.flatnonzero(~active))
             m = int(act.size)
-            idx = torch.from_numpy(act).to(dev)
-            for t in (bf.eta, bf.frozen, bf.info, bf.H):
-                t[:m] = t[idx]
+            # in-place row moves, ascending (slot act[i] >= i is never a destination already
+            # written): no temporaries, so no allocator traffic inside the iteration loop
+            moves = [(i, int(s_)) for i, s_ in enumerate(act) if i != s_]
+            if moves:
+                dst = torch.from_numpy(np.array([a for a, _ in moves], dtype=np.int64)).to(dev)
+                src = torch.from_numpy(np.array([b for _, b in moves], dtype=np.int64)).to(dev)
+                for t in (bf.frozen, bf.info):
+                    t[dst] = t[src]      # small: one gather/scatter (sources read first)
+                for i, s_ in moves:
+                    bf.eta[i].copy_(bf.eta[s_])
+                    bf.H[i].copy_(bf.H[s_])
             (lam, penal, dsh, beta, drift, gram_now, active, n_iter, converged, prev_rel,
              max_iter, rows, fid, fresp_h, fmask_h) = (
                 x[act] for x in (lam, penal, dsh, beta, drift, gram_now, active, n_iter,
                                  converged, prev_rel, max_iter, rows, fid, fresp_h, fmask_h))
             reqs = [reqs[s_] for s_ in act]
             bf.dshift[:m].copy_(torch.from_numpy(dsh))
+            lamp_d = torch.from_numpy(lam[:, None] * penal).to(dev)
             fit_resp = torch.from_numpy(fresp_h).to(dev)
             fit_mask = torch.from_numpy(fmask_h).to(dev)
             bf.fit_mask = fmask_h
@@ -645,10 +671,11 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         _lib.call("sglm_link_update", fam, power, n, ld, B, _p(bf.eta), _p(prob.Y), _p(prob.M),
                   _p(fit_resp), _p(fit_mask), _p(bf.W), _p(bf.R), st)
         d.xtr(bf.R, B, bf.g)
-        g = bf.g[:B].cpu().numpy() + lam[:, None] * penal * beta
-        if dmax_pending:
-            drift += dmax_h.numpy()[:B].astype(np.float64)
-            dmax_pending = False
+        bnp = beta_pin.numpy()
+        bnp[:B] = beta
+        beta64_d[:B].copy_(beta_pin[:B], non_blocking=True)
+        torch.addcmul(bf.g[:B], lamp_d, beta64_d[:B], out=bf.gtot[:B])   # + lam * w
+        g_h[:B].copy_(bf.gtot[:B], non_blocking=True)
         t0 = tick("it_gradient", t0)
         # ---- Hessian
         if const_hess:
@@ -694,7 +721,6 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                 stats.gram_fits += int(uniq.size)
                 stats.reused += int(keep.size)
         t0 = tick("it_gram", t0)
-        bf.gtot[:B].copy_(torch.from_numpy(g))
         bf.delta[:B].zero_()
         if const_hess:
             order, nref = act, (0 if factored else act.size)
@@ -706,12 +732,19 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                   _p(bf.cwork), st)
         factored = True
         d.eta(bf.delta[:B], bf.deta)
-        delta = bf.delta[:B].cpu().numpy().astype(np.float64)
+        delta_h[:B].copy_(bf.delta[:B], non_blocking=True)
         t0 = tick("it_solve_eta", t0)
         # ---- line search
-        _lib.call("sglm_loss_trials", fam, power, n, ld, B, _p(bf.eta), _p(bf.deta), _p(prob.Y),
-                  _p(prob.M), _p(fit_resp), _p(fit_mask), _p(tv1), 5, _p(Ltr), _p(xtr_work), st)
-        L = Ltr[: B * 5].view(B, 5).cpu().numpy().copy()
+        _lib.call("sglm_loss_trials_max", fam, power, n, ld, B, _p(bf.eta), _p(bf.deta),
+                  _p(prob.Y), _p(prob.M), _p(fit_resp), _p(fit_mask), _p(tv1), 5, _p(Ltr),
+                  _p(dmax_d), _p(xtr_work), st)
+        L_h[: B * 5].copy_(Ltr[: B * 5], non_blocking=True)
+        dmax_h[:B].copy_(dmax_d[:B], non_blocking=True)
+        torch.cuda.current_stream().synchronize()              # the iteration's round trip
+        g = g_h[:B].numpy().copy()
+        delta = delta_h[:B].numpy().astype(np.float64)
+        L = L_h[: B * 5].numpy().reshape(B, 5).copy()
+        dmaxeta = dmax_h[:B].numpy().astype(np.float64)
         ts = np.array([0.0, 1.0, 0.5, 0.25, 0.125])
         gdir = np.sum(g * delta, axis=1)
         # penalty lam/2 |w + t d|^2 = lam/2 (A + 2 t Bq + t^2 C), vectorised over fits x trials
@@ -744,14 +777,10 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         t0 = tick("it_linesearch", t0)
         # ---- update
         beta += step[:, None] * delta
-        bf.beta[:B].copy_(torch.from_numpy(beta.astype(np.float32)))
-        step_d = torch.from_numpy(step.astype(np.float32)).to(dev)
-        _lib.call("sglm_eta_axpy_max", n, ld, B, _p(step_d), _p(bf.deta), _p(prob.M),
-                  _p(fit_mask), _p(bf.eta), _p(dmax_d), st)
         if not const_hess:
-            # read back with the next iteration's gradient sync (no extra stall here)
-            dmax_h[:B].copy_(dmax_d[:B], non_blocking=True)
-            dmax_pending = True
+            drift[act] += step[act] * dmaxeta[act]    # max_i |t d_eta_i| over the fit's rows
+        step_d = torch.from_numpy(step.astype(np.float32)).to(dev)
+        _lib.call("sglm_eta_axpy", n, ld, B, _p(step_d), _p(bf.deta), _p(bf.eta), st)
         n_iter[act] += 1
         if stats is not None:
             stats.newton_iters += 1

@@ -41,9 +41,13 @@ def main():
     grid.SHARD_PLAN = a.plan
     if a.all:
         per = []
+        import gc
         for r in range(a.world):
             sim = (r, a.world)
             grid.run(d, s.y, cv_idx, objs, [0] * nlam, simulate=sim)
+            if os.environ.get("SIM_GC_FREEZE", "1") == "1":
+                gc.collect()
+                gc.freeze()
             st = E.IrlsStats(record=True)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -55,8 +59,28 @@ def main():
                           "max_ms": max(q["wall_ms"] for q in per)}))
         return
     sim = (a.rank, a.world)
-    grid.run(d, s.y, cv_idx, objs, [0] * nlam, simulate=sim)
-    out = {}
+    for _ in range(int(os.environ.get("SIM_WARMUPS", "1"))):
+        grid.run(d, s.y, cv_idx, objs, [0] * nlam, simulate=sim)
+    import gc
+    if os.environ.get("SIM_GC_FREEZE", "1") == "1":
+        gc.collect()
+        gc.freeze()                  # long-lived objects out of the collector's scans
+    out = {"plain_repeats_ms": []}
+    for rep in range(3):
+        prof = None
+        if rep == 0 and os.environ.get("SIM_CPROFILE"):
+            import cProfile
+            prof = cProfile.Profile()
+            prof.enable()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        grid.run(d, s.y, cv_idx, objs, [0] * nlam, simulate=sim)
+        torch.cuda.synchronize()
+        out["plain_repeats_ms"].append(round((time.perf_counter() - t0) * 1e3, 2))
+        if prof is not None:
+            import pstats
+            prof.disable()
+            pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(25)
     for phases in (False, True):
         st = E.IrlsStats(record=True, trace_phases=phases)
         torch.cuda.synchronize()
