@@ -44,7 +44,8 @@ def main():
         import gc
         for r in range(a.world):
             sim = (r, a.world)
-            grid.run(d, s.y, cv_idx, objs, [0] * nlam, simulate=sim)
+            for _ in range(int(os.environ.get("SIM_WARMUPS", "2"))):
+                grid.run(d, s.y, cv_idx, objs, [0] * nlam, simulate=sim)
             if os.environ.get("SIM_GC_FREEZE", "1") == "1":
                 gc.collect()
                 gc.freeze()
@@ -59,7 +60,7 @@ def main():
                           "max_ms": max(q["wall_ms"] for q in per)}))
         return
     sim = (a.rank, a.world)
-    for _ in range(int(os.environ.get("SIM_WARMUPS", "1"))):
+    for _ in range(int(os.environ.get("SIM_WARMUPS", "2"))):
         grid.run(d, s.y, cv_idx, objs, [0] * nlam, simulate=sim)
     import gc
     if os.environ.get("SIM_GC_FREEZE", "1") == "1":
