@@ -371,6 +371,12 @@ class Problem:
             self._stats[key] = float(self.masks[int(mask)].sum(dtype=np.int64))
         return self._stats[key]
 
+    def seed_stats(self, resp: int, mask: int, cnt: float, sum_y: float):
+        """Provide (count, sum y) of a (response, mask) pair computed elsewhere (the grid's
+        batched float64 device statistics), so that mask_stats needs no host pass."""
+        self._stats[(resp, mask)] = (cnt, sum_y, sum_y / cnt if cnt else 0.0)
+        self._stats[("count", int(mask))] = cnt
+
     def mask_stats(self, resp: int, mask: int):
         """float64 (count, sum y, mean y) over a mask — host side, cached."""
         key = (resp, mask)

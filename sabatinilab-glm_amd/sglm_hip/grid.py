@@ -240,6 +240,9 @@ def run_multi(X, y, groups: Sequence[dict], score_method: str = "mse", coef0=Non
     prob = E.Problem(design, ys, masks)
     t0 = tick("setup_problem", t0)
     ms = _MaskStats(prob)
+    for i in mine:                           # the IRLS setup reads these, not host passes
+        _, _, _, m, r, _ = table[i]
+        prob.seed_stats(r, local[m], float(ms.cnt[local[m]]), float(ms.sy[local[m], r]))
     # sklearn's y-range check of the log-link fits (y >= 0 on the fit's rows, positive mean;
     # glm.py:231-235), on this rank's fits from the device mask statistics; the verdict is
     # shared (one int all-reduce) so that every rank raises together
