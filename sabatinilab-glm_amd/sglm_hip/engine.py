@@ -55,11 +55,11 @@ SYRK_CBITS = True              # ... and its row-compacted register-only form (v
 # factor holds by a factor in [e^-cD, e^cD] (c = max(1, |2 - power|)), which bounds the
 # contraction of the inexact-Newton step by e^cD - 1; the fixed point (exact gradient) is
 # unchanged.  0 disables reuse.
-HESS_REUSE_TOL = float(__import__("os").environ.get("SGLM_HESS_REUSE_TOL", "0.25"))
+HESS_REUSE_TOL = float(__import__("os").environ.get("SGLM_HESS_REUSE_TOL", "0.375"))
 # Hessian sharing: among fits of one (mask, response) that need a new Hessian, a fit whose
 # predictor is within HESS_SHARE_TOL (max over its mask rows) of another's is factored from
 # that fit's Gram, and starts its drift count at that distance (same bound as above).
-HESS_SHARE_TOL = float(__import__("os").environ.get("SGLM_HESS_SHARE_TOL", "0.25"))
+HESS_SHARE_TOL = float(__import__("os").environ.get("SGLM_HESS_SHARE_TOL", "0.375"))
 # Batch compaction: once at most COMPACT_FRAC of the batch is still iterating (and at least
 # COMPACT_MIN fits have stopped), the active fits are moved to the front slots.
 COMPACT_FRAC = float(__import__("os").environ.get("SGLM_COMPACT_FRAC", "0.75"))
@@ -801,7 +801,12 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         relv = (np.max(np.abs(step[act, None] * delta[act]), axis=1)
                 / (1.0 + np.max(np.abs(beta[act]), axis=1)))
         stepa = step[act]
-        stop = (stepa == 0.0) | (relv <= tol) | ((relv < 1e-4) & (relv >= 0.5 * prev_rel[act]))
+        # stagnation (the f32 noise floor): a step no better than half the previous one, judged
+        # only on steps taken with a fresh Hessian -- a kept factor contracts by up to
+        # e^(c D) - 1, which may legitimately exceed 1/2 (Gaussian: the exact Hessian, always)
+        fresh = gram_now[act] | const_hess
+        stop = ((stepa == 0.0) | (relv <= tol) |
+                ((relv < 1e-4) & (relv >= 0.5 * prev_rel[act]) & fresh))
         conv_now = stop & ((stepa != 0.0) | (relv <= tol) |
                            (np.max(np.abs(delta[act]), axis=1) < 1e-5))
         active[act[stop]] = False
