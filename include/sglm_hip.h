@@ -144,6 +144,10 @@ int sglm_pack_bits_rows(const uint16_t* Xb, int64_t ld, int32_t P, const int32_t
  * 1 bit per element instead of the bf16 design). */
 int sglm_compact_bits(const uint32_t* xbits, int64_t ld, int32_t P, const int32_t* rows,
                       int64_t nrows, uint32_t* out, sglm_stream_t stream);
+/* sglm_compact_bits from the row-major planes of sglm_pack_bits_t (rbits, [P/64][ld] x 8 B):
+ * identical output, one 64 x 64 bit-tile transpose (64 wave ballots) per wave. */
+int sglm_compact_rbits(const uint32_t* rbits, int64_t ld, int32_t P, const int32_t* rows,
+                       int64_t nrows, uint32_t* out, sglm_stream_t stream);
 
 /* Per-slot descriptor for Gram v6, 4 x int64 per slot: [0] device address of the slot's
  * compacted bit-plane design, [1] its row count, [2] device address of the slot's compact

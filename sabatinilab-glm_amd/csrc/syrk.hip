@@ -1093,6 +1093,42 @@ __global__ void __launch_bounds__(256) compact_bits_kernel(
     }
 }
 
+// Same output again, from the ROW-major planes (rbits[t][i] = the 64 predictor bits of row i,
+// predictors 64t..64t+63, fragment order): one wave per (64-row output block, 64-predictor
+// group).  Lane l loads the word pair of mask row k = 64 blk + src(l) (so that the ballots come
+// out in fragment order), then 64 ballots transpose the 64 x 64 bit tile: ballot j is
+// predictor j's 64-row word, kept by lane j, and the wave stores 64 consecutive predictors
+// (512 B).  One 8-byte load per row and 64 register ballots, instead of a gather of one bit
+// per (row, predictor) from the column-packed planes.
+__global__ void __launch_bounds__(256) compact_rbits_kernel(
+    const u32x2* __restrict__ rbits, int64_t ld, int32_t P, const int32_t* __restrict__ rows,
+    int64_t nrows, uint2* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wid = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+    const int64_t nblk = (nrows + 63) / 64;
+    const int32_t ng = P / 64;
+    const int64_t total = nblk * ng;
+    const int src = (lane & 32) | frag_bit_source(lane & 31);
+    for (int64_t g = wid; g < total; g += ((int64_t)gridDim.x * 256) >> 6) {
+        const int64_t blk = g / ng;
+        const int t = (int)(g % ng);
+        const int64_t k = blk * 64 + src;
+        u32x2 w = {0u, 0u};
+        if (k < nrows) w = rbits[(int64_t)t * ld + (rows ? (int64_t)rows[k] : k)];
+        uint32_t lo = 0u, hi = 0u;
+#pragma unroll
+        for (int j = 0; j < 64; ++j) {
+            const int rho = j & 31;
+            const int pos = 4 * (rho >> 3) + ((rho & 7) >> 1) + 16 * (rho & 1);
+            const uint32_t word = j < 32 ? w.x : w.y;
+            const unsigned long long m = __ballot((word >> pos) & 1u);
+            lo = lane == j ? (uint32_t)m : lo;
+            hi = lane == j ? (uint32_t)(m >> 32) : hi;
+        }
+        out[blk * P + (int64_t)t * 64 + lane] = make_uint2(lo, hi);
+    }
+}
+
 // compact bf16 weights: wbf(slot)[k] = bf16(W[fits[slot]][row(k)]) for k < rows, 0 to pad 64
 __global__ void __launch_bounds__(256) gather_w_kernel(const float* __restrict__ W, int64_t ld,
                                                        const int32_t* __restrict__ fits,
@@ -1138,6 +1174,22 @@ extern "C" int sglm_compact_bits(const uint32_t* xbits, int64_t ld, int32_t P,
     compact_bits_kernel<<<4096, 256, 0, as_stream(stream)>>>(xbits, ld, P, rows, nrows,
                                                               reinterpret_cast<uint2*>(out));
     return check_launch("compact_bits_kernel");
+}
+
+extern "C" int sglm_compact_rbits(const uint32_t* rbits, int64_t ld, int32_t P,
+                                  const int32_t* rows, int64_t nrows, uint32_t* out,
+                                  sglm_stream_t stream) {
+    if (!rbits || !out || nrows < 0 || ld % 64 || P % 64 || (!rows && nrows > ld)) {
+        set_error("sglm_compact_rbits: bad args");
+        return SGLM_EINVAL;
+    }
+    if (nrows == 0) return SGLM_OK;
+    const int64_t waves = (nrows + 63) / 64 * (P / 64);
+    const int64_t blocks = (waves + 3) / 4;
+    compact_rbits_kernel<<<(unsigned)(blocks < 16384 ? blocks : 16384), 256, 0,
+                           as_stream(stream)>>>(reinterpret_cast<const u32x2*>(rbits), ld, P,
+                                                rows, nrows, reinterpret_cast<uint2*>(out));
+    return check_launch("compact_rbits_kernel");
 }
 
 extern "C" int sglm_gather_w(const float* W, int64_t ld, const int32_t* fits, int32_t nact,

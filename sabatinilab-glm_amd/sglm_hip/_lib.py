@@ -35,6 +35,7 @@ SIGNATURES = {
     "sglm_syrk_bits": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp,
                                  _vp, _vp]),
     "sglm_pack_bits_rows": (C.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _vp, _vp]),
+    "sglm_compact_rbits": (C.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _vp]),
     "sglm_compact_bits": (C.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _vp]),
     "sglm_gather_w": (C.c_int, [_vp, _i64, _vp, _i32, _vp, _i64, _vp]),
     "sglm_syrk_cbits": (C.c_int, [_vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp]),

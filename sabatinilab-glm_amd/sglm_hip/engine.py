@@ -219,8 +219,12 @@ class Design:
         if self._cbits is None and self.xbits is not None:
             self._cbits = torch.empty(max(1, (self.n + 63) // 64) * self.P * 2,
                                       dtype=torch.int32, device=self.device)
-            _lib.call("sglm_compact_bits", _p(self.xbits), self.ld, self.P, None, self.n,
-                      _p(self._cbits), _stream())
+            if self.rbits is not None:
+                _lib.call("sglm_compact_rbits", _p(self.rbits), self.ld, self.P, None, self.n,
+                          _p(self._cbits), _stream())
+            else:
+                _lib.call("sglm_compact_bits", _p(self.xbits), self.ld, self.P, None, self.n,
+                          _p(self._cbits), _stream())
         return self._cbits
 
     def xtr(self, R, B, g_out, work=None):
@@ -353,7 +357,10 @@ class Problem:
                 return c
             bits = torch.empty(max(1, (nr + 63) // 64) * d.P * 2, dtype=torch.int32,
                                device=d.device)
-            if d.xbits is not None:
+            if d.rbits is not None:
+                _lib.call("sglm_compact_rbits", _p(d.rbits), d.ld, d.P, _p(rows_d), nr,
+                          _p(bits), _stream())
+            elif d.xbits is not None:
                 _lib.call("sglm_compact_bits", _p(d.xbits), d.ld, d.P, _p(rows_d), nr,
                           _p(bits), _stream())
             else:

@@ -470,8 +470,11 @@ def test_compact_bits_equals_pack_bits_rows(engine, torch_mod):
         _lib.call("sglm_pack_bits_rows", d.xb.data_ptr(), d.ld, d.P, rp, nr, a.data_ptr(),
                   flag.data_ptr(), 0)
         _lib.call("sglm_compact_bits", d.xbits.data_ptr(), d.ld, d.P, rp, nr, b.data_ptr(), 0)
+        c = torch.full((size,), 7, dtype=torch.int32, device="cuda")
+        _lib.call("sglm_compact_rbits", d.rbits.data_ptr(), d.ld, d.P, rp, nr, c.data_ptr(), 0)
         torch.cuda.synchronize()
         assert torch.equal(a, b)
+        assert torch.equal(a, c)          # the ballot transpose of the row-major planes
 
 
 def test_xtr_bits_matches_float64(engine, torch_mod):
