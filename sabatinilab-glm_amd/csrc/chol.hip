@@ -70,25 +70,29 @@ __device__ __forceinline__ float lanef(float v, int l) {
 }
 
 // rank-1 update of this lane's column by row q of U: a[i] -= U[q][i] * u for i > q, where
-// U[q][i] = lane i's u.  Chunks of 8 readlane + FMA pairs behind scheduling fences, so that the
-// scalar broadcasts are consumed as they are produced instead of all being hoisted (SGPR
-// spills).
+// U[q][i] = lane i's u; the same broadcasts carry the elimination into v (lane i's column of
+// the block inverse, see chol_diag_kernel): v[i] -= U[q][i] * x_q.  Chunks of 8 readlane + FMA
+// pairs behind scheduling fences, so that the scalar broadcasts are consumed as they are
+// produced instead of all being hoisted (SGPR spills).
 template <int Q>
-__device__ __forceinline__ void diag_rank1(float (&a)[kNB], float u) {
+__device__ __forceinline__ void diag_rank1(float (&a)[kNB], float (&v)[kNB], float u, float xq) {
 #pragma unroll
     for (int i0 = Q + 1; i0 < kNB; i0 += 8) {
         float sc[8];                                 // broadcasts first: the readlane ->
 #pragma unroll                                       // VALU hazard is covered by distance
         for (int i = i0; i < i0 + 8 && i < kNB; ++i) sc[i - i0] = lanef(u, i);
 #pragma unroll
-        for (int i = i0; i < i0 + 8 && i < kNB; ++i) a[i] = fmaf(-sc[i - i0], u, a[i]);
+        for (int i = i0; i < i0 + 8 && i < kNB; ++i) {
+            a[i] = fmaf(-sc[i - i0], u, a[i]);
+            v[i] = fmaf(-sc[i - i0], xq, v[i]);
+        }
         __builtin_amdgcn_sched_barrier(0);
     }
 }
 
 template <int Q>
-__device__ __forceinline__ void diag_steps(float (&a)[kNB], float& rinv, int c, float thr,
-                                           int& myfrz, int& dropped) {
+__device__ __forceinline__ void diag_steps(float (&a)[kNB], float (&v)[kNB], float& rinv, int c,
+                                           float thr, int& myfrz, int& dropped) {
     if constexpr (Q < kNB) {
         // the pivot test runs lane-locally (lane Q's a[Q] against its own threshold) and only
         // its verdict is broadcast: a broadcast of the loop-invariant threshold would be
@@ -104,14 +108,16 @@ __device__ __forceinline__ void diag_steps(float (&a)[kNB], float& rinv, int c, 
         const float u = c > Q ? a[Q] * r : 0.0f;     // row Q of U (0 for a dropped pivot)
         a[Q] = c == Q ? d : (c > Q ? u : a[Q]);
         rinv = c == Q ? r : rinv;                    // lane Q keeps 1 / U[Q][Q] (0 if dropped)
+        const float xq = v[Q] * r;                   // x_Q of lane c's unit right-hand side
+        v[Q] = xq;
         // row Q is final from here on: materialise it now, or its selects sink to the store
         // at the end and keep every step's masks and pivots live (SGPR spills)
-        asm volatile("" : "+v"(a[Q]), "+v"(rinv));
+        asm volatile("" : "+v"(a[Q]), "+v"(rinv), "+v"(v[Q]));
         const bool newly = drop && !was && c == Q;
         myfrz = newly ? 1 : myfrz;
         dropped = newly ? 1 : dropped;
-        diag_rank1<Q>(a, u);
-        diag_steps<Q + 1>(a, rinv, c, thr, myfrz, dropped);
+        diag_rank1<Q>(a, v, u, xq);
+        diag_steps<Q + 1>(a, v, rinv, c, thr, myfrz, dropped);
     }
 }
 
@@ -123,7 +129,8 @@ __device__ __forceinline__ void diag_steps(float (&a)[kNB], float& rinv, int c, 
 __global__ void __launch_bounds__(64) chol_diag_kernel(
     float* __restrict__ Hall, int32_t P, int32_t k0, const int32_t* __restrict__ fits,
     uint8_t* __restrict__ frozen_all, float* __restrict__ rhs_all,
-    const float* __restrict__ diag_all, int32_t* __restrict__ info, int32_t nrefac) {
+    const float* __restrict__ diag_all, int32_t* __restrict__ info, int32_t nrefac,
+    float* __restrict__ minv_all) {
     const int fit = fits[blockIdx.x];
     const bool refactor = (int)blockIdx.x < nrefac;
     float* H = Hall + (int64_t)fit * P * P;
@@ -146,12 +153,25 @@ __global__ void __launch_bounds__(64) chol_diag_kernel(
     if (refactor) {
         const float thr = 1e-6f * diag_all[(int64_t)fit * P + k0 + c];
         int dropped = 0;
-        diag_steps<0>(a, rinv, c, thr, myfrz, dropped);
+        // v: lane c's column of M = (U_kk^T)^-1 (rows of frozen coordinates zero), built by
+        // eliminating e_c alongside the factorisation -- the panel step's operator
+        float v[kNB];
+        {
+            int ci = c;
+            asm volatile("" : "+v"(ci));
+#pragma unroll
+            for (int r = 0; r < kNB; ++r) v[r] = r == ci ? 1.0f : 0.0f;
+        }
+        diag_steps<0>(a, v, rinv, c, thr, myfrz, dropped);
         if (dropped) atomicAdd(&info[fit], 1);
         frz[c] = (uint8_t)myfrz;
         // whole block: the strictly-lower part is never read (consumers use row <= column)
 #pragma unroll
         for (int r = 0; r < kNB; ++r) H[(int64_t)(k0 + r) * P + k0 + c] = a[r];
+        // row-major M[r][i] (lane i writes column i: coalesced rows)
+        float* mo = minv_all + (int64_t)blockIdx.x * kNB * kNB + c;
+#pragma unroll
+        for (int r = 0; r < kNB; ++r) mo[r * kNB] = v[r];
     } else {
         float ucc = 1.0f;                            // U[c][c] (selects: no dynamic index)
 #pragma unroll
@@ -174,58 +194,64 @@ __global__ void __launch_bounds__(64) chol_diag_kernel(
     rhs[c] = zc;
 }
 
-// Panel: columns j >= k0+NB in chunks of 256 per workgroup.
+// Panel: block row k0 of U for columns j >= k0+NB, X = M B (M from the diagonal step, B the
+// block row as the trailing updates left it) as a 64 x 64-tile GEMM on v_mfma_f32_32x32x2f32
+// (exact f32 products): one 64-column tile per workgroup, one 32 x 32 quadrant per wave, the
+// whole K = 64 operand set loaded up front (lower-triangular M: the upper row half stops at
+// K = 32).  The same pass applies the block to the right-hand side, rhs[j] -= sum_r X[r][j] z[r]
+// (z = the block's forward-solved rhs); kept-factor slots only do that with their stored rows.
 __global__ void __launch_bounds__(kCT) chol_panel_kernel(
     float* __restrict__ Hall, int32_t P, int32_t k0, const int32_t* __restrict__ fits,
-    const uint8_t* __restrict__ frozen_all, float* __restrict__ rhs_all, int32_t nrefac) {
-    __shared__ float sD[kNB][kNB + 1];
-    __shared__ float z[kNB];
-    __shared__ uint8_t fz[kNB];
-    const int fit = fits[blockIdx.x];
-    const bool refactor = (int)blockIdx.x < nrefac;
+    const float* __restrict__ minv_all, float* __restrict__ rhs_all, int32_t nrefac) {
+    __shared__ float zs[kNB];
+    __shared__ float sred[2][kNB];
+    const int slot = blockIdx.x;
+    const int fit = fits[slot];
+    const bool refactor = slot < nrefac;
     float* H = Hall + (int64_t)fit * P * P;
     float* rhs = rhs_all + (int64_t)fit * P;
-    const int tid = threadIdx.x;
-    for (int e = tid; e < kNB * kNB; e += kCT) {
-        const int r = e / kNB, c = e % kNB;
-        sD[r][c] = (r <= c) ? H[(int64_t)(k0 + r) * P + k0 + c] : 0.0f;
-    }
-    __shared__ float rd[kNB];
-    if (tid < kNB) {
-        z[tid] = rhs[k0 + tid];
-        fz[tid] = frozen_all[(int64_t)fit * P + k0 + tid];
-    }
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r32 = lane & 31, kh = lane >> 5;
+    const int rh = wave >> 1, ch = wave & 1;
+    const int j0 = k0 + kNB + blockIdx.y * kNB;        // P and k0 are multiples of 64
+    const int j = j0 + ch * 32 + r32;
+    if (tid < kNB) zs[tid] = rhs[k0 + tid];
+    float b[32];
+    const float* pb = H + (int64_t)(k0 + kh) * P + j;
+#pragma unroll
+    for (int u = 0; u < 32; ++u) b[u] = pb[(int64_t)(2 * u) * P];
     __syncthreads();
-    if (tid < kNB) rd[tid] = 1.0f / sD[tid][tid];
-    __syncthreads();
-    const int j = k0 + kNB + blockIdx.y * kCT + tid;
-    if (j >= P) return;
-    float x[kNB];
-#pragma unroll
-    for (int r = 0; r < kNB; ++r) x[r] = H[(int64_t)(k0 + r) * P + j];
-    if (refactor) {
-#pragma unroll
-        for (int c = 0; c < kNB; ++c) {
-            // four partial sums shorten the dependent FMA chain of the triangular solve
-            float v0 = x[c], v1 = 0.0f, v2 = 0.0f, v3 = 0.0f;
-#pragma unroll
-            for (int r = 0; r + 3 < c; r += 4) {
-                v0 -= sD[r][c] * x[r];
-                v1 -= sD[r + 1][c] * x[r + 1];
-                v2 -= sD[r + 2][c] * x[r + 2];
-                v3 -= sD[r + 3][c] * x[r + 3];
-            }
-#pragma unroll
-            for (int r = c & ~3; r < c; ++r) v0 -= sD[r][c] * x[r];
-            x[c] = fz[c] ? 0.0f : ((v0 + v1) + (v2 + v3)) * rd[c];
-        }
-#pragma unroll
-        for (int r = 0; r < kNB; ++r) H[(int64_t)(k0 + r) * P + j] = x[r];
-    }
     float s = 0.0f;
+    if (refactor) {
+        const float* pm = minv_all + (int64_t)slot * kNB * kNB + (rh * 32 + r32) * kNB + kh;
+        float m[32];
 #pragma unroll
-    for (int r = 0; r < kNB; ++r) s += x[r] * z[r];
-    rhs[j] -= s;
+        for (int u = 0; u < 32; ++u) m[u] = (rh || u < 16) ? pm[2 * u] : 0.0f;
+        f32x16 acc = {};
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(m[u], b[u], acc, 0, 0, 0);
+        if (rh) {
+#pragma unroll
+            for (int u = 16; u < 32; ++u)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(m[u], b[u], acc, 0, 0, 0);
+        }
+        __syncthreads();                             // every wave has consumed its B rows
+        // X[row i][col j]: reg q -> i = (q&3) + 8(q>>2) + 4*kh within the quadrant
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int i = rh * 32 + (q & 3) + 8 * (q >> 2) + 4 * kh;
+            H[(int64_t)(k0 + i) * P + j] = acc[q];
+            s = fmaf(acc[q], zs[i], s);
+        }
+    } else if (rh == 0) {
+#pragma unroll
+        for (int u = 0; u < 32; ++u) s = fmaf(b[u], zs[2 * u + kh], s);
+    }
+    s += __shfl_xor(s, 32, 64);
+    if (kh == 0) sred[rh][ch * 32 + r32] = s;
+    __syncthreads();
+    if (tid < kNB) rhs[j0 + tid] -= sred[0][tid] + sred[1][tid];
 }
 
 // Trailing update of the upper triangle with `kc` rows of U (64 or 128: two block steps
@@ -413,7 +439,7 @@ __global__ void __launch_bounds__(kST) chol_back2_kernel(
 using namespace sglm;
 
 extern "C" size_t sglm_chol_work_bytes(int32_t P, int32_t B) {
-    return (size_t)2 * (size_t)B * (size_t)P * sizeof(float);
+    return ((size_t)2 * (size_t)B * (size_t)P + (size_t)B * kNB * kNB) * sizeof(float);
 }
 
 // fits[0 .. nrefac) are factored, fits[nrefac .. nact) reuse the factor and frozen set a
@@ -431,6 +457,7 @@ static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t na
     }
     float* rhs = (float*)work;
     float* dg = rhs + (size_t)B * P;
+    float* minv = dg + (size_t)B * P;
     chol_prep_kernel<<<nact, kCT, 0, s>>>(H, P, fits, g, dshift, frozen, rhs, dg, info, nrefac);
     int st = check_launch("chol_prep_kernel");
     if (st) return st;
@@ -446,11 +473,12 @@ static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t na
     // diag/panel kb+1, then ONE rank-128 update of the remaining trailing matrix
     auto factor_step = [&](int kb) {
         const int k0 = kb * kNB;
-        chol_diag_kernel<<<nact, 64, 0, s>>>(H, P, k0, fits, frozen, rhs, dg, info, nrefac);
+        chol_diag_kernel<<<nact, 64, 0, s>>>(H, P, k0, fits, frozen, rhs, dg, info, nrefac,
+                                             minv);
         const int rem = P - k0 - kNB;
         if (rem > 0)
-            chol_panel_kernel<<<dim3(nact, (rem + kCT - 1) / kCT), kCT, 0, s>>>(H, P, k0, fits,
-                                                                               frozen, rhs, nrefac);
+            chol_panel_kernel<<<dim3(nact, rem / kNB), kCT, 0, s>>>(H, P, k0, fits, minv, rhs,
+                                                                    nrefac);
     };
     for (int kb = 0; kb < nb; kb += 2) {
         factor_step(kb);
