@@ -17,6 +17,8 @@
 // original diagonal) get delta = 0.  refactor = 0 reuses the factor and frozen set left in
 // H by a previous call (kept Hessians, constant-Hessian Gaussian refinement): only the two
 // triangular solves run (chol_fwd2 / chol_back2).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace sglm {
@@ -254,23 +256,22 @@ __global__ void __launch_bounds__(kCT) chol_panel_kernel(
     if (tid < kNB) rhs[j0 + tid] -= sred[0][tid] + sred[1][tid];
 }
 
-// Trailing update of the upper triangle with `kc` rows of U (64 or 128: two block steps
-// folded into one pass over the trailing matrix), blocks counted from s0; rowonly: just block
-// row s0 (the look-ahead row the next diagonal step needs).  One 64x64 tile per workgroup,
+// Trailing update of the upper triangle with `kc` rows of U (64 for a look-ahead band, up to
+// kLA*64 when a group of block steps is folded into one pass over the trailing matrix), blocks
+// counted from s0.  One 64x64 tile per workgroup,
 // one 32x32 quadrant per wave on v_mfma_f32_32x32x2f32 (exact f32 products, f32 accumulate),
 // operands loaded straight from the panel rows (L2-resident: grid x = tile, so one fit's
 // tiles run together), no LDS.  D[i][j] = sum_r U[k0+r][i] U[k0+r][j]; H[i][j] -= D.
 __global__ void __launch_bounds__(kCT) chol_update_kernel(float* __restrict__ Hall, int32_t P,
                                                           int32_t k0, int32_t kc, int32_t s0,
-                                                          int32_t rowonly,
                                                           const int32_t* __restrict__ fits) {
     const int fit = fits[blockIdx.y];
     float* H = Hall + (int64_t)fit * P * P;
     const int T = P / kNB - s0;
+    // tiles row by row from block (s0, s0): the grid size alone selects the whole trailing
+    // triangle or only its first few block rows (the look-ahead band)
     int t = blockIdx.x, bi = 0, bj;
-    if (rowonly) {
-        bj = t;
-    } else {
+    {
         int rowlen = T;
         while (t >= rowlen) { t -= rowlen; ++bi; --rowlen; }
         bj = bi + t;
@@ -442,6 +443,17 @@ extern "C" size_t sglm_chol_work_bytes(int32_t P, int32_t B) {
     return ((size_t)2 * (size_t)B * (size_t)P + (size_t)B * kNB * kNB) * sizeof(float);
 }
 
+// Look-ahead depth of the blocked factorisation (block steps per trailing sweep); the
+// SGLM_CHOL_LOOKAHEAD environment variable (1..8) overrides the default 4 for experiments.
+static int chol_lookahead() {
+    static const int la = [] {
+        const char* e = getenv("SGLM_CHOL_LOOKAHEAD");
+        const int v = e ? atoi(e) : 4;
+        return v >= 1 && v <= 8 ? v : 4;
+    }();
+    return la;
+}
+
 // fits[0 .. nrefac) are factored, fits[nrefac .. nact) reuse the factor and frozen set a
 // previous call left in H (engine.irls' kept Hessians): one launch chain for both, the
 // trailing updates over the refactored fits only.
@@ -469,8 +481,10 @@ static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t na
         return check_launch("chol_back2_kernel");
     }
     const int nb = P / kNB;
-    // block steps in pairs: diag/panel kb, look-ahead update of block row kb+1 only,
-    // diag/panel kb+1, then ONE rank-128 update of the remaining trailing matrix
+    // look-ahead depth kLA: block steps in groups of kLA; after step b only the band of block
+    // rows b+1 .. (end of the group) is updated with panel b (K = 64), and once per group ONE
+    // rank-(kLA*64) update of the rest of the trailing matrix -- the trailing matrix (the HBM
+    // read-modify-write that bounds the chain at large batches) is swept P/(kLA*64) times
     auto factor_step = [&](int kb) {
         const int k0 = kb * kNB;
         chol_diag_kernel<<<nact, 64, 0, s>>>(H, P, k0, fits, frozen, rhs, dg, info, nrefac,
@@ -480,17 +494,21 @@ static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t na
             chol_panel_kernel<<<dim3(nact, rem / kNB), kCT, 0, s>>>(H, P, k0, fits, minv, rhs,
                                                                     nrefac);
     };
-    for (int kb = 0; kb < nb; kb += 2) {
-        factor_step(kb);
-        if (kb + 1 >= nb) break;
-        if (nrefac > 0)
-            chol_update_kernel<<<dim3(nb - kb - 1, nrefac), kCT, 0, s>>>(H, P, kb * kNB, kNB,
-                                                                        kb + 1, 1, fits);
-        factor_step(kb + 1);
-        const int T = nb - kb - 2;
+    const int la = chol_lookahead();
+    for (int kb = 0; kb < nb; kb += la) {
+        const int ke = kb + la < nb ? kb + la : nb;            // group [kb, ke)
+        for (int b = kb; b < ke; ++b) {
+            factor_step(b);
+            const int nr = ke - 1 - b;                         // band rows b+1 .. ke-1
+            const int T = nb - b - 1;
+            if (nrefac > 0 && nr > 0)
+                chol_update_kernel<<<dim3(nr * T - nr * (nr - 1) / 2, nrefac), kCT, 0, s>>>(
+                    H, P, b * kNB, kNB, b + 1, fits);
+        }
+        const int T = nb - ke;
         if (nrefac > 0 && T > 0)
-            chol_update_kernel<<<dim3(T * (T + 1) / 2, nrefac), kCT, 0, s>>>(H, P, kb * kNB,
-                                                                            2 * kNB, kb + 2, 0, fits);
+            chol_update_kernel<<<dim3(T * (T + 1) / 2, nrefac), kCT, 0, s>>>(
+                H, P, kb * kNB, (ke - kb) * kNB, ke, fits);
     }
     st = check_launch("chol block kernels");
     if (st) return st;
