@@ -36,6 +36,8 @@ CONFIGS = {
     "small": (50_000, 10, 5, 5, 4),
     # C5: 64 responses x C4 design, Gaussian elastic-net lambda path (l1_ratio 0.5, 20 alphas)
     "c5": (1_000_000, 50, 20, 5, 20),
+    # session preprocessing (lynne_pp.preprocess_lynne): rows per session
+    "prep": (16_000_000, 0, 0, 0, 0),
 }
 C5_RESPONSES = 64
 INIT_PASSES = 2
@@ -214,6 +216,82 @@ def bench_c5(a):
         "cpu_baseline": cpu}))
 
 
+def bench_prep(a):
+    """lynne_pp.preprocess_lynne's arithmetic (sglm_prep_session) on a
+    16M-row synthetic session resident in HBM (9 float64 input columns -> 40 derived columns).
+    One step = one session.  Sessions are independent: with N ranks each rank preprocesses
+    its own session (weak scaling, no collective beyond the timing barrier)."""
+    import torch
+    import torch.distributed as dist
+    from sglm_hip import prep, synth
+    n = CONFIGS["prep"][0]
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    _, cols = synth.session(n, 100 + rank, 0.02, with_extra=False)
+    Xh = np.stack([cols[c].astype(np.float64) for c in prep.IN_COLS])
+    X = torch.from_numpy(Xh).cuda()
+    out = torch.empty((len(prep.OUT_COLS), n), dtype=torch.float64, device="cuda")
+    ws = prep.Workspace(n)
+    for _ in range(max(1, a.warmup)):
+        prep.session_columns_device(X, 7, out, ws)
+    stream = torch.cuda.current_stream()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(a.steps):
+        prep.session_columns_device(X, 7, out, ws)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = (time.perf_counter() - t0) / a.steps
+    call_ms = ev0.elapsed_time(ev1) / a.steps
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64,
+                         device="cuda" if a.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t[0])
+    if rank != 0:
+        return
+    # host DataFrame columns in, host columns out: the PCIe-inclusive rate (never `value`)
+    t1 = time.perf_counter()
+    prep.session_columns(Xh, 7)
+    pcie_s = time.perf_counter() - t1
+    bytes_per_row = 8 * (len(prep.IN_COLS) + len(prep.OUT_COLS))
+    achieved = bytes_per_row * n / (call_ms * 1e-3) / 1e9
+    cpu = None
+    if not a.no_cpu:
+        from oracle import prep_pandas
+        rows = 2_000_000
+        sub = {c: v[:rows] for c, v in cols.items()}
+        t2 = time.perf_counter()
+        prep_pandas.derived_columns(sub, 7)
+        dt = time.perf_counter() - t2
+        cpu = {"value": rows / dt, "unit": "session rows/s", "cores": 1, "kind": "port",
+               "sample": f"oracle/prep_pandas.py (the reference's pandas operations: shift, "
+                         f"bfill/ffill, cumsum, groupby transform/cumsum, diff) on the first "
+                         f"{rows} rows of the same session, {dt:.2f} s"}
+    print(json.dumps({
+        "metric": "session preprocessing rows/s (lynne_pp.preprocess_lynne derived columns)",
+        "value": n * world / el, "unit": "session rows/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": el * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": f"one {n}-row behaviour session per rank (9 float64 event "
+                               f"columns -> 40 derived columns, trial_shift_bounds 7)",
+                   "config_name": "prep", "rows": n,
+                   "pcie_inclusive_rows_per_s": n / pcie_s,
+                   "parallelism": f"one session per rank, {world} rank(s)"},
+        "roofline": {"bound": "hbm", "kernel": "sglm_prep_session (whole call: 7 row kernels + "
+                                               "9 chunked scans)",
+                     "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": achieved / PEAK_HBM_GBS, "traffic": None,
+                     "algorithmic_bytes_per_row": bytes_per_row, "avg_call_ms": call_ms},
+        "cpu_baseline": cpu}))
+
+
 def main():
     a = parse()
     import torch
@@ -228,8 +306,8 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group("gloo")
-    if a.config == "c5":
-        bench_c5(a)
+    if a.config in ("c5", "prep"):
+        (bench_c5 if a.config == "c5" else bench_prep)(a)
         if world > 1:
             dist.destroy_process_group()
         return

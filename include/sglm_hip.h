@@ -302,6 +302,49 @@ int sglm_enet_cd(const float* H, int32_t P, int32_t p, const int32_t* fits, int3
                  const int32_t* fit_intercept, int32_t max_sweeps, double tol, double* coef,
                  int32_t* sweeps, void* work, sglm_stream_t stream);
 
+
+/* --- session preprocessing (lynne_pp.preprocess_lynne, lynne_pp.py:217-249) -------------
+ * Input: SGLM_PREP_NIN float64 columns of n rows, column c at in + c * ld_in, in the order of
+ * enum sglm_prep_in (the renamed session columns of lynne_pp.rename_columns, :95-111).
+ * Output: SGLM_PREP_NOUT float64 columns, column c at out + c * ld_out, in the order of enum
+ * sglm_prep_out, which is the order in which the reference appends them:
+ *   define_trial_starts_ends (:20-44): event_col (cpn*1 | lpx*2 | rpx*2, zeros as NaN,
+ *     backward fill), trial_start_flag ((ev == 1) & (ev.shift(-1) != 1), shifted by -k),
+ *     nTrial (its NaN-skipping cumulative sum), event_col_end (lpx*2 | rpx*2 | start flag,
+ *     forward fill), trial_end_flag ((ece == 2) & (ece.shift(1) != 2) & (nTrial > 0), shifted
+ *     by +k), nEndTrial;  set_reward_flags (:113-125): r_trial / nr_trial from the per-trial
+ *     sum of r;  set_port_entry_exit_... (:127-158): r / nr products;  define_side_agnostic_
+ *     events (:160-180): left + right sums;  get_first_time_events (:182-215): nn, xx, the
+ *     first-transition indicators of the per-trial cumulative sums of nn, xx, cpn and the
+ *     nn / xx / r / nr products.
+ * k = trial_shift_bounds (any sign).  Rows whose shifted source lies outside [0, n) are NaN in
+ * the flag columns and the cumulative sums skip them (pandas skipna).  Exact for integer-
+ * valued event columns (indicator counts); per-trial sums of non-integer r are summed in
+ * chunk order.  `work`: sglm_prep_work_bytes(n) bytes.  n == 0 is a no-op. */
+enum sglm_prep_in {
+    SGLM_PREP_IN_CPN = 0, SGLM_PREP_IN_LPX, SGLM_PREP_IN_RPX, SGLM_PREP_IN_LPN, SGLM_PREP_IN_RPN,
+    SGLM_PREP_IN_R, SGLM_PREP_IN_NR, SGLM_PREP_IN_RL, SGLM_PREP_IN_LL, SGLM_PREP_NIN
+};
+enum sglm_prep_out {
+    SGLM_PREP_OUT_EVENT_COL = 0, SGLM_PREP_OUT_TRIAL_START_FLAG, SGLM_PREP_OUT_NTRIAL,
+    SGLM_PREP_OUT_EVENT_COL_END, SGLM_PREP_OUT_TRIAL_END_FLAG, SGLM_PREP_OUT_NENDTRIAL,
+    SGLM_PREP_OUT_R_TRIAL, SGLM_PREP_OUT_NR_TRIAL,
+    SGLM_PREP_OUT_RPXR, SGLM_PREP_OUT_RPXNR, SGLM_PREP_OUT_LPXR, SGLM_PREP_OUT_LPXNR,
+    SGLM_PREP_OUT_RPNR, SGLM_PREP_OUT_RPNNR, SGLM_PREP_OUT_LPNR, SGLM_PREP_OUT_LPNNR,
+    SGLM_PREP_OUT_SPN, SGLM_PREP_OUT_SPX, SGLM_PREP_OUT_SPNR, SGLM_PREP_OUT_SPNNR,
+    SGLM_PREP_OUT_SPXR, SGLM_PREP_OUT_SPXNR, SGLM_PREP_OUT_SL,
+    SGLM_PREP_OUT_NN, SGLM_PREP_OUT_XX,
+    SGLM_PREP_OUT_FT_NN, SGLM_PREP_OUT_FT_XX, SGLM_PREP_OUT_FT_LPN, SGLM_PREP_OUT_FT_RPN,
+    SGLM_PREP_OUT_FT_SPN, SGLM_PREP_OUT_FT_LPX, SGLM_PREP_OUT_FT_RPX, SGLM_PREP_OUT_FT_SPX,
+    SGLM_PREP_OUT_FT_CPN,
+    SGLM_PREP_OUT_FT_R_RPN, SGLM_PREP_OUT_FT_R_LPN, SGLM_PREP_OUT_FT_R_SPN,
+    SGLM_PREP_OUT_FT_NR_RPN, SGLM_PREP_OUT_FT_NR_LPN, SGLM_PREP_OUT_FT_NR_SPN,
+    SGLM_PREP_NOUT
+};
+size_t sglm_prep_work_bytes(int64_t n);
+int sglm_prep_session(const double* in, int64_t ld_in, int64_t n, int32_t k, double* out,
+                      int64_t ld_out, void* work, sglm_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

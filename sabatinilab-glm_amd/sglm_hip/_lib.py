@@ -72,6 +72,8 @@ SIGNATURES = {
     "sglm_enet_work_bytes": (_sz, [_i32, _i32]),
     "sglm_enet_cd": (C.c_int, [_vp, _i32, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _i32, C.c_double,
                                _vp, _vp, _vp, _vp]),
+    "sglm_prep_work_bytes": (_sz, [_i64]),
+    "sglm_prep_session": (C.c_int, [_vp, _i64, _i64, _i32, _vp, _i64, _vp, _vp]),
 }
 
 

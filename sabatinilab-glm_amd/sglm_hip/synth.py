@@ -73,3 +73,27 @@ def make(N, m, L, family="poisson", rho=0.02, seed=0, beta_scale=0.1, intercept=
     trial = np.arange(N) // 100
     return Synthetic(E=E, L=L, shifts=shifts, N=N, beta=beta, intercept=b, y=y,
                      trial=trial, family=family)
+
+
+SESSION_LONG_NAMES = {"cpn": "centerIn", "lpx": "leftOut", "rpx": "rightOut", "lpn": "leftIn",
+                      "rpn": "rightIn", "r": "reward", "nr": "noreward", "rl": "rightLick",
+                      "ll": "leftLick"}
+
+
+def session(n: int, seed: int, rate: float = 0.02, with_extra: bool = True):
+    """Seeded behaviour session with the long column names of the acquisition files: sparse
+    0/1 port entries/exits, licks and reward outcomes, a photometry trace and an 'Unnamed'
+    index column; center entries precede side exits so trials form."""
+    import pandas as pd
+    rng = np.random.default_rng(seed)
+    cols = {}
+    for short in ("cpn", "lpx", "rpx", "lpn", "rpn", "rl", "ll"):
+        cols[short] = (rng.random(n) < rate).astype(np.int64)
+    cols["r"] = (rng.random(n) < rate / 2).astype(np.int64)
+    cols["nr"] = (rng.random(n) < rate / 2).astype(np.int64)
+    df = pd.DataFrame({SESSION_LONG_NAMES[k]: v for k, v in cols.items()})
+    if with_extra:
+        df.insert(0, "Unnamed: 0", np.arange(n))
+        df["zscored green"] = rng.standard_normal(n)
+        df["centerOcc"] = (rng.random(n) < 0.3).astype(np.int64)
+    return df, cols
