@@ -10,156 +10,200 @@
 namespace sglm {
 namespace {
 
-constexpr int kPT = 256;          // threads per scan workgroup
-constexpr int kPR = 8;            // consecutive rows per thread
-constexpr int kPC = kPT * kPR;    // rows per scan chunk
+constexpr int kPT = 256;          // threads per scan workgroup (4 waves)
+constexpr int kPJ = 32;           // 64-row slabs per wave
+constexpr int kPW = 64 * kPJ;     // consecutive rows per wave (the scan unit)
 constexpr int kCT1 = 1024;        // carry-scan workgroup
 
 enum { OP_ADD = 0, OP_MAX = 1 };
 
-// Scan element: value plus a "segment starts here" bit.  ADD with heads is the segmented sum
-// (a head resets the running value), MAX ignores heads.  The operator is associative but not
-// commutative, so every reduction below keeps row order.
-struct Agg { double v; int h; };
+// Scan element over NC columns at once: values plus a "segment starts here" bit (shared by
+// the columns: they are segmented by the same key).  ADD with heads is the segmented sum (a
+// head resets the running values), MAX ignores heads.  The operator is associative but not
+// commutative, so every combination below keeps row order.
+template <int NC> struct Agg { double v[NC]; int h; };
 
-template <int OP> __device__ __forceinline__ Agg ident() {
-    return {OP == OP_MAX ? -INFINITY : 0.0, 0};
+template <int OP, int NC> __device__ __forceinline__ Agg<NC> ident() {
+    Agg<NC> a;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) a.v[c] = OP == OP_MAX ? -INFINITY : 0.0;
+    a.h = 0;
+    return a;
 }
-template <int OP> __device__ __forceinline__ Agg comb(Agg a, Agg b) {
-    if (OP == OP_MAX) return {fmax(a.v, b.v), 0};
-    return {b.h ? b.v : a.v + b.v, a.h | b.h};
+template <int OP, int NC> __device__ __forceinline__ Agg<NC> comb(const Agg<NC>& a,
+                                                                  const Agg<NC>& b) {
+    Agg<NC> r;
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+        r.v[c] = OP == OP_MAX ? fmax(a.v[c], b.v[c]) : (b.h ? b.v[c] : a.v[c] + b.v[c]);
+    r.h = OP == OP_MAX ? 0 : (a.h | b.h);
+    return r;
 }
-
-// Ordered exclusive scan over the NW waves of a workgroup; `total` = the workgroup aggregate.
-template <int OP, int NW>
-__device__ __forceinline__ Agg block_excl(Agg a, Agg* lds, Agg& total) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    Agg inc = a;
+template <int NC> __device__ __forceinline__ Agg<NC> shfl_up(const Agg<NC>& a, int o) {
+    Agg<NC> r;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) r.v[c] = __shfl_up(a.v[c], o, 64);
+    r.h = __shfl_up(a.h, o, 64);
+    return r;
+}
+template <int NC> __device__ __forceinline__ Agg<NC> shfl(const Agg<NC>& a, int l) {
+    Agg<NC> r;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) r.v[c] = __shfl(a.v[c], l, 64);
+    r.h = __shfl(a.h, l, 64);
+    return r;
+}
+template <int OP, int NC> __device__ __forceinline__ Agg<NC> wave_incl(Agg<NC> a) {
+    const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        Agg t;
-        t.v = __shfl_up(inc.v, o, 64);
-        t.h = __shfl_up(inc.h, o, 64);
-        if (lane >= o) inc = comb<OP>(t, inc);
+        const Agg<NC> t = shfl_up(a, o);
+        if (lane >= o) a = comb<OP, NC>(t, a);
     }
-    if (lane == 63) lds[w] = inc;
-    Agg up;
-    up.v = __shfl_up(inc.v, 1, 64);
-    up.h = __shfl_up(inc.h, 1, 64);
-    __syncthreads();
-    Agg wp = ident<OP>(), tot = ident<OP>();
-#pragma unroll
-    for (int i = 0; i < NW; ++i) {
-        if (i < w) wp = comb<OP>(wp, lds[i]);
-        tot = comb<OP>(tot, lds[i]);
-    }
-    total = tot;
-    return comb<OP>(wp, lane == 0 ? ident<OP>() : up);
+    return a;
 }
 
-// Logical row i of a scan in direction `rev` is physical row rev ? n-1-i : i.  A row's value
-// is x (NaN rows contribute the identity: pandas' skipna cumsum); with a key column a row is a
-// segment head when its key differs from the previous logical row's (NaN keys never match).
-template <int OP>
-__device__ __forceinline__ Agg load_elem(const double* __restrict__ x,
-                                         const double* __restrict__ key, int64_t n, int rev,
-                                         int64_t i, double& raw) {
-    const int64_t p = rev ? n - 1 - i : i;
-    raw = x[p];
-    Agg e = {isnan(raw) ? ident<OP>().v : raw, 0};
-    if (key) {
-        const int64_t q = rev ? p + 1 : p - 1;
-        e.h = (i == 0) || (key[p] != key[q]);
+struct ScanCols {
+    const double* x[3];    // inputs (NC used)
+    double* y[3];          // outputs (may alias x)
+    const double* key;     // segment key or nullptr
+    int64_t n;
+    int rev;
+};
+
+// Logical row i is physical row rev ? n-1-i : i.  NaN values contribute the identity and stay
+// NaN in the output (pandas' skipna cumsum); with a key, rows whose key is NaN are NaN (the
+// groupby drops them) and a row is a segment head when its key differs from the previous
+// logical row's.
+template <int OP, int NC>
+__device__ __forceinline__ Agg<NC> load_elem(const ScanCols& a, int64_t i, bool& nan_out) {
+    const int64_t p = a.rev ? a.n - 1 - i : i;
+    Agg<NC> e;
+    e.h = 0;
+    bool kn = false;
+    if (a.key) {
+        const double kp = a.key[p];
+        kn = isnan(kp);
+        e.h = (i == 0) || (kp != a.key[a.rev ? p + 1 : p - 1]);
+    }
+    nan_out = kn;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const double v = a.x[c][p];
+        const bool nn = kn || isnan(v);
+        e.v[c] = nn ? (OP == OP_MAX ? -INFINITY : 0.0) : v;
+        nan_out = nan_out || (NC == 1 && nn);
     }
     return e;
 }
 
-template <int OP>
-__global__ void __launch_bounds__(kPT) scan_reduce_kernel(const double* __restrict__ x,
-                                                          const double* __restrict__ key,
-                                                          int64_t n, int rev, Agg* agg) {
-    __shared__ Agg lds[kPT / 64];
-    const int64_t base = (int64_t)blockIdx.x * kPC + (int64_t)threadIdx.x * kPR;
-    Agg a = ident<OP>();
-    for (int j = 0; j < kPR; ++j) {
-        const int64_t i = base + j;
-        if (i < n) {
-            double raw;
-            a = comb<OP>(a, load_elem<OP>(x, key, n, rev, i, raw));
-        }
+// The scan unit is one wave: wave g owns rows [g*kPW, (g+1)*kPW) as kPJ slabs of 64
+// consecutive rows (lane = row within the slab: every load is coalesced), slabs chained in
+// order.  Pass 1 writes each wave's aggregate, one workgroup turns them into exclusive carries,
+// pass 2 rescans with the carry and writes -- no LDS, no barriers, few registers.
+template <int OP, int NC>
+__global__ void __launch_bounds__(kPT) scan_reduce_kernel(ScanCols a, Agg<NC>* agg) {
+    const int lane = threadIdx.x & 63;
+    const int64_t g = (int64_t)blockIdx.x * (kPT / 64) + (threadIdx.x >> 6);
+    const int64_t base = g * kPW + lane;
+    if (g * kPW >= a.n) return;
+    Agg<NC> run = ident<OP, NC>();
+#pragma unroll 8
+    for (int j = 0; j < kPJ; ++j) {
+        const int64_t i = base + j * 64;
+        bool nanr;
+        const Agg<NC> e = i < a.n ? load_elem<OP, NC>(a, i, nanr) : ident<OP, NC>();
+        run = comb<OP, NC>(run, shfl(wave_incl<OP, NC>(e), 63));
     }
-    Agg total;
-    block_excl<OP, kPT / 64>(a, lds, total);
-    if (threadIdx.x == 0) agg[blockIdx.x] = total;
+    if (lane == 0) agg[g] = run;
 }
 
-// One workgroup turns the chunk aggregates into exclusive carries, in place: thread t owns a
-// contiguous run of chunks, the runs are scanned in order across the workgroup.
-template <int OP>
-__global__ void __launch_bounds__(kCT1) scan_carry_kernel(Agg* agg, int64_t nchunks) {
-    __shared__ Agg lds[kCT1 / 64];
+// One workgroup turns the wave aggregates into exclusive carries, in place: thread t owns a
+// contiguous run of entries, the runs are chained in order across the workgroup.
+template <int OP, int NC>
+__global__ void __launch_bounds__(kCT1) scan_carry_kernel(Agg<NC>* agg, int64_t nchunks) {
+    __shared__ Agg<NC> lds[kCT1 / 64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t per = (nchunks + kCT1 - 1) / kCT1;
     const int64_t c0 = (int64_t)threadIdx.x * per;
     const int64_t c1 = c0 + per < nchunks ? c0 + per : nchunks;
-    Agg a = ident<OP>();
-    for (int64_t c = c0; c < c1; ++c) a = comb<OP>(a, agg[c]);
-    Agg total;
-    Agg run = block_excl<OP, kCT1 / 64>(a, lds, total);
-    for (int64_t c = c0; c < c1; ++c) {
-        const Agg v = agg[c];
-        agg[c] = run;
-        run = comb<OP>(run, v);
-    }
-}
-
-template <int OP>
-__global__ void __launch_bounds__(kPT) scan_apply_kernel(const double* __restrict__ x,
-                                                         const double* __restrict__ key,
-                                                         int64_t n, int rev,
-                                                         const Agg* __restrict__ carry,
-                                                         double* __restrict__ y) {
-    __shared__ Agg lds[kPT / 64];
-    const int64_t base = (int64_t)blockIdx.x * kPC + (int64_t)threadIdx.x * kPR;
-    Agg e[kPR];
-    double raw[kPR];
-    Agg a = ident<OP>();
+    // loads in groups of 8 issued together (independent), combined in order afterwards
+    constexpr int G = 8;
+    Agg<NC> a = ident<OP, NC>();
+    for (int64_t c = c0; c < c1; c += G) {
+        Agg<NC> v[G];
 #pragma unroll
-    for (int j = 0; j < kPR; ++j) {
-        const int64_t i = base + j;
-        if (i < n) {
-            e[j] = load_elem<OP>(x, key, n, rev, i, raw[j]);
-            a = comb<OP>(a, e[j]);
-        }
-    }
-    Agg total;
-    Agg run = comb<OP>(carry[blockIdx.x], block_excl<OP, kPT / 64>(a, lds, total));
+        for (int q = 0; q < G; ++q) v[q] = c + q < c1 ? agg[c + q] : ident<OP, NC>();
 #pragma unroll
-    for (int j = 0; j < kPR; ++j) {
-        const int64_t i = base + j;
-        if (i < n) {
-            run = comb<OP>(run, e[j]);
-            y[rev ? n - 1 - i : i] = isnan(raw[j]) ? raw[j] : run.v;
+        for (int q = 0; q < G; ++q) a = comb<OP, NC>(a, v[q]);
+    }
+    const Agg<NC> inc = wave_incl<OP, NC>(a);
+    Agg<NC> exc = shfl_up(inc, 1);
+    if (lane == 0) exc = ident<OP, NC>();
+    if (lane == 63) lds[w] = inc;
+    __syncthreads();
+    Agg<NC> wp = ident<OP, NC>();
+    for (int v = 0; v < w; ++v) wp = comb<OP, NC>(wp, lds[v]);
+    Agg<NC> run = comb<OP, NC>(wp, exc);
+    for (int64_t c = c0; c < c1; c += G) {
+        Agg<NC> v[G];
+#pragma unroll
+        for (int q = 0; q < G; ++q) v[q] = c + q < c1 ? agg[c + q] : ident<OP, NC>();
+#pragma unroll
+        for (int q = 0; q < G; ++q) {
+            if (c + q < c1) agg[c + q] = run;
+            run = comb<OP, NC>(run, v[q]);
         }
     }
 }
 
-inline int64_t nchunks_of(int64_t n) { return (n + kPC - 1) / kPC; }
-
-// y = inclusive scan of x (in place allowed): ADD (pandas cumsum, skipna) or MAX, forward or
-// backward, segmented by `key` when given (ADD only).
-int scan(int op, const double* x, const double* key, int64_t n, int rev, double* y, Agg* agg,
-         hipStream_t s) {
-    const int64_t nc = nchunks_of(n);
-    if (op == OP_ADD) {
-        scan_reduce_kernel<OP_ADD><<<nc, kPT, 0, s>>>(x, key, n, rev, agg);
-        scan_carry_kernel<OP_ADD><<<1, kCT1, 0, s>>>(agg, nc);
-        scan_apply_kernel<OP_ADD><<<nc, kPT, 0, s>>>(x, key, n, rev, agg, y);
-    } else {
-        scan_reduce_kernel<OP_MAX><<<nc, kPT, 0, s>>>(x, key, n, rev, agg);
-        scan_carry_kernel<OP_MAX><<<1, kCT1, 0, s>>>(agg, nc);
-        scan_apply_kernel<OP_MAX><<<nc, kPT, 0, s>>>(x, key, n, rev, agg, y);
+template <int OP, int NC>
+__global__ void __launch_bounds__(kPT) scan_apply_kernel(ScanCols a,
+                                                         const Agg<NC>* __restrict__ carry) {
+    const int lane = threadIdx.x & 63;
+    const int64_t g = (int64_t)blockIdx.x * (kPT / 64) + (threadIdx.x >> 6);
+    const int64_t base = g * kPW + lane;
+    if (g * kPW >= a.n) return;
+    Agg<NC> run = carry[g];
+#pragma unroll 8
+    for (int j = 0; j < kPJ; ++j) {
+        const int64_t i = base + j * 64;
+        bool nanr = true;
+        const Agg<NC> e = i < a.n ? load_elem<OP, NC>(a, i, nanr) : ident<OP, NC>();
+        const Agg<NC> inc = wave_incl<OP, NC>(e);
+        if (i < a.n) {
+            const Agg<NC> r = comb<OP, NC>(run, inc);
+            const int64_t p = a.rev ? a.n - 1 - i : i;
+            const bool kn = a.key && isnan(a.key[p]);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const double v = NC == 1 ? (nanr ? NAN : r.v[c])
+                                         : ((kn || isnan(a.x[c][p])) ? NAN : r.v[c]);
+                a.y[c][p] = v;
+            }
+        }
+        run = comb<OP, NC>(run, shfl(inc, 63));
     }
+}
+
+inline int64_t nwaves_of(int64_t n) { return (n + kPW - 1) / kPW; }
+
+// Inclusive scans of NC columns (in place allowed): ADD (pandas cumsum, skipna; segmented by
+// `key` when given) or MAX, forward or backward.
+template <int OP, int NC>
+int scan(const ScanCols& a, void* agg, hipStream_t s) {
+    const int64_t nw = nwaves_of(a.n);
+    const int64_t nb = (nw + kPT / 64 - 1) / (kPT / 64);
+    scan_reduce_kernel<OP, NC><<<nb, kPT, 0, s>>>(a, (Agg<NC>*)agg);
+    scan_carry_kernel<OP, NC><<<1, kCT1, 0, s>>>((Agg<NC>*)agg, nw);
+    scan_apply_kernel<OP, NC><<<nb, kPT, 0, s>>>(a, (const Agg<NC>*)agg);
     return check_launch("prep scan");
+}
+
+ScanCols cols1(const double* x, double* y, const double* key, int64_t n, int rev) {
+    ScanCols a = {};
+    a.x[0] = x; a.y[0] = y; a.key = key; a.n = n; a.rev = rev;
+    return a;
 }
 
 // ---- row kernels (one thread per row) ---------------------------------------------------
@@ -246,25 +290,14 @@ __global__ void prep_end_kernel(const double* __restrict__ ece_raw,
     end_flag[t] = f;
 }
 
-// r restricted to rows with a trial number (groupby drops NaN keys, lynne_pp.py:121).
-__global__ void prep_mask_r_kernel(const double* __restrict__ r,
-                                   const double* __restrict__ ntrial, int64_t n,
-                                   double* __restrict__ rm) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n) return;
-    rm[t] = isnan(ntrial[t]) ? NAN : r[t];
-}
-
 struct Out {  // output columns (SGLM_PREP_OUT_* order)
     double* c[SGLM_PREP_NOUT];
 };
 
 // Reward flags (per-trial sum of r = forward + backward segmented sums - r), port indicators,
-// side-agnostic sums, nn / xx (lynne_pp.py:121-123, 142-151, 170-178, 193-194); the per-trial
-// cumulative-sum inputs of nn, xx, cpn (NaN outside trials) go to s0..s2.
+// side-agnostic sums, nn / xx (lynne_pp.py:121-123, 142-151, 170-178, 193-194).
 __global__ void prep_rows_kernel(In in, const double* __restrict__ ntrial, int64_t n, Out o,
-                                 double* __restrict__ s0, double* __restrict__ s1,
-                                 double* __restrict__ s2) {
+                                 const double* __restrict__ s0, const double* __restrict__ s1) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
     const double r = in.r[t], nr = in.nr[t];
@@ -295,9 +328,6 @@ __global__ void prep_rows_kernel(In in, const double* __restrict__ ntrial, int64
     const double xx = (isnan(lpx) ? 0.0 : lpx) + (isnan(rpx) ? 0.0 : rpx);
     o.c[SGLM_PREP_OUT_NN][t] = nn;
     o.c[SGLM_PREP_OUT_XX][t] = xx;
-    s0[t] = has ? nn : NAN;
-    s1[t] = has ? xx : NAN;
-    s2[t] = has ? in.cpn[t] : NAN;
 }
 
 // ((cumsum == 1) * 1).diff(), negatives zeroed by multiplication (so -1 becomes -0.0, row 0
@@ -314,18 +344,21 @@ __global__ void prep_first_kernel(In in, const double* __restrict__ cs_nn,
                                   const double* __restrict__ cs_cpn, int64_t n, Out o) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
-    const double nn = o.c[SGLM_PREP_OUT_NN][t], xx = o.c[SGLM_PREP_OUT_XX][t];
-    const double spn = o.c[SGLM_PREP_OUT_SPN][t], spx = o.c[SGLM_PREP_OUT_SPX][t];
+    // nn, xx, spn, spx recomputed from the inputs (cheaper than re-reading the outputs)
+    const double lpn = in.lpn[t], rpn = in.rpn[t], lpx = in.lpx[t], rpx = in.rpx[t];
+    const double nn = (isnan(lpn) ? 0.0 : lpn) + (isnan(rpn) ? 0.0 : rpn);
+    const double xx = (isnan(lpx) ? 0.0 : lpx) + (isnan(rpx) ? 0.0 : rpx);
+    const double spn = rpn + lpn, spx = rpx + lpx;
     const double r = in.r[t], nr = in.nr[t];
     o.c[SGLM_PREP_OUT_FT_NN][t] = first_step(cs_nn, t);
     o.c[SGLM_PREP_OUT_FT_XX][t] = first_step(cs_xx, t);
     o.c[SGLM_PREP_OUT_FT_CPN][t] = first_step(cs_cpn, t);
-    const double ft_lpn = nn * in.lpn[t], ft_rpn = nn * in.rpn[t], ft_spn = nn * spn;
+    const double ft_lpn = nn * lpn, ft_rpn = nn * rpn, ft_spn = nn * spn;
     o.c[SGLM_PREP_OUT_FT_LPN][t] = ft_lpn;
     o.c[SGLM_PREP_OUT_FT_RPN][t] = ft_rpn;
     o.c[SGLM_PREP_OUT_FT_SPN][t] = ft_spn;
-    o.c[SGLM_PREP_OUT_FT_LPX][t] = xx * in.lpx[t];
-    o.c[SGLM_PREP_OUT_FT_RPX][t] = xx * in.rpx[t];
+    o.c[SGLM_PREP_OUT_FT_LPX][t] = xx * lpx;
+    o.c[SGLM_PREP_OUT_FT_RPX][t] = xx * rpx;
     o.c[SGLM_PREP_OUT_FT_SPX][t] = xx * spx;
     o.c[SGLM_PREP_OUT_FT_R_RPN][t] = ft_rpn * r;
     o.c[SGLM_PREP_OUT_FT_R_LPN][t] = ft_lpn * r;
@@ -342,7 +375,7 @@ using namespace sglm;
 
 extern "C" size_t sglm_prep_work_bytes(int64_t n) {
     if (n < 0) n = 0;
-    return (size_t)3 * (size_t)n * sizeof(double) + (size_t)nchunks_of(n) * sizeof(Agg) + 256;
+    return (size_t)3 * (size_t)n * sizeof(double) + (size_t)nwaves_of(n) * sizeof(Agg<3>) + 256;
 }
 
 extern "C" int sglm_prep_session(const double* in, int64_t ld_in, int64_t n, int32_t k,
@@ -363,7 +396,7 @@ extern "C" int sglm_prep_session(const double* in, int64_t ld_in, int64_t n, int
     double* T0 = (double*)work;
     double* T1 = T0 + n;
     double* T2 = T1 + n;
-    Agg* agg = (Agg*)(((uintptr_t)(T2 + n) + 63) & ~(uintptr_t)63);
+    void* agg = (void*)(((uintptr_t)(T2 + n) + 63) & ~(uintptr_t)63);
     const int bs = 256;
     const int64_t g = (n + bs - 1) / bs;
     double* ntrial = o.c[SGLM_PREP_OUT_NTRIAL];
@@ -372,23 +405,27 @@ extern "C" int sglm_prep_session(const double* in, int64_t ld_in, int64_t n, int
     int st;
     // trial starts: codes -> backward fill -> start flag -> cumulative sum (nTrial)
     prep_codes_kernel<<<g, bs, 0, s>>>(x, n, T0, T1);
-    if ((st = scan(OP_MAX, T1, nullptr, n, 1, T1, agg, s))) return st;
+    if ((st = scan<OP_MAX, 1>(cols1(T1, T1, nullptr, n, 1), agg, s))) return st;
     prep_start_kernel<<<g, bs, 0, s>>>(T0, T1, n, k, o.c[SGLM_PREP_OUT_EVENT_COL], flag);
-    if ((st = scan(OP_ADD, flag, nullptr, n, 0, ntrial, agg, s))) return st;
+    if ((st = scan<OP_ADD, 1>(cols1(flag, ntrial, nullptr, n, 0), agg, s))) return st;
     // trial ends: codes -> forward fill -> end flag -> cumulative sum (nEndTrial)
     prep_end_codes_kernel<<<g, bs, 0, s>>>(x, flag, n, T0, T1);
-    if ((st = scan(OP_MAX, T1, nullptr, n, 0, T1, agg, s))) return st;
+    if ((st = scan<OP_MAX, 1>(cols1(T1, T1, nullptr, n, 0), agg, s))) return st;
     prep_end_kernel<<<g, bs, 0, s>>>(T0, T1, ntrial, n, k, o.c[SGLM_PREP_OUT_EVENT_COL_END],
                                      eflag);
-    if ((st = scan(OP_ADD, eflag, nullptr, n, 0, o.c[SGLM_PREP_OUT_NENDTRIAL], agg, s)))
+    if ((st = scan<OP_ADD, 1>(cols1(eflag, o.c[SGLM_PREP_OUT_NENDTRIAL], nullptr, n, 0), agg,
+                              s)))
         return st;
-    // per-trial reward totals, indicators, per-trial cumulative sums, first-time events
-    prep_mask_r_kernel<<<g, bs, 0, s>>>(x.r, ntrial, n, T2);
-    if ((st = scan(OP_ADD, T2, ntrial, n, 0, T0, agg, s))) return st;
-    if ((st = scan(OP_ADD, T2, ntrial, n, 1, T1, agg, s))) return st;
-    prep_rows_kernel<<<g, bs, 0, s>>>(x, ntrial, n, o, T0, T1, T2);
-    for (double* T : {T0, T1, T2})
-        if ((st = scan(OP_ADD, T, ntrial, n, 0, T, agg, s))) return st;
+    // per-trial reward totals (forward + backward segmented sums), indicators
+    if ((st = scan<OP_ADD, 1>(cols1(x.r, T0, ntrial, n, 0), agg, s))) return st;
+    if ((st = scan<OP_ADD, 1>(cols1(x.r, T1, ntrial, n, 1), agg, s))) return st;
+    prep_rows_kernel<<<g, bs, 0, s>>>(x, ntrial, n, o, T0, T1);
+    // per-trial cumulative sums of nn, xx, cpn in one 3-column scan, then first-time events
+    ScanCols c3 = {};
+    c3.x[0] = o.c[SGLM_PREP_OUT_NN]; c3.x[1] = o.c[SGLM_PREP_OUT_XX]; c3.x[2] = x.cpn;
+    c3.y[0] = T0; c3.y[1] = T1; c3.y[2] = T2;
+    c3.key = ntrial; c3.n = n; c3.rev = 0;
+    if ((st = scan<OP_ADD, 3>(c3, agg, s))) return st;
     prep_first_kernel<<<g, bs, 0, s>>>(x, T0, T1, T2, n, o);
     return check_launch("prep_first_kernel");
 }
