@@ -40,6 +40,7 @@ CONFIGS = {
     "prep": (16_000_000, 0, 0, 0, 0),
 }
 C5_RESPONSES = 64
+PREP_SHIFT = 1     # er_refactored_from_scratch_cleanup.py:269 calls preprocess_lynne(df, trial_shift_bounds=1)
 INIT_PASSES = 2
 
 
@@ -233,7 +234,7 @@ def bench_prep(a):
     out = torch.empty((len(prep.OUT_COLS), n), dtype=torch.float64, device="cuda")
     ws = prep.Workspace(n)
     for _ in range(max(1, a.warmup)):
-        prep.session_columns_device(X, 7, out, ws)
+        prep.session_columns_device(X, PREP_SHIFT, out, ws)
     stream = torch.cuda.current_stream()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
@@ -242,7 +243,7 @@ def bench_prep(a):
     t0 = time.perf_counter()
     ev0.record(stream)
     for _ in range(a.steps):
-        prep.session_columns_device(X, 7, out, ws)
+        prep.session_columns_device(X, PREP_SHIFT, out, ws)
     ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -258,7 +259,7 @@ def bench_prep(a):
         return
     # host DataFrame columns in, host columns out: the PCIe-inclusive rate (never `value`)
     t1 = time.perf_counter()
-    prep.session_columns(Xh, 7)
+    prep.session_columns(Xh, PREP_SHIFT)
     pcie_s = time.perf_counter() - t1
     bytes_per_row = 8 * (len(prep.IN_COLS) + len(prep.OUT_COLS))
     achieved = bytes_per_row * n / (call_ms * 1e-3) / 1e9
@@ -268,7 +269,7 @@ def bench_prep(a):
         rows = 2_000_000
         sub = {c: v[:rows] for c, v in cols.items()}
         t2 = time.perf_counter()
-        prep_pandas.derived_columns(sub, 7)
+        prep_pandas.derived_columns(sub, PREP_SHIFT)
         dt = time.perf_counter() - t2
         cpu = {"value": rows / dt, "unit": "session rows/s", "cores": 1, "kind": "port",
                "sample": f"oracle/prep_pandas.py (the reference's pandas operations: shift, "
@@ -280,7 +281,7 @@ def bench_prep(a):
         "warmup": a.warmup, "ms_per_step": el * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": f"one {n}-row behaviour session per rank (9 float64 event "
-                               f"columns -> 40 derived columns, trial_shift_bounds 7)",
+                               f"columns -> 40 derived columns, trial_shift_bounds {PREP_SHIFT} as the drivers call it)",
                    "config_name": "prep", "rows": n,
                    "pcie_inclusive_rows_per_s": n / pcie_s,
                    "parallelism": f"one session per rank, {world} rank(s)"},

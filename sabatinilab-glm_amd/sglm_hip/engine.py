@@ -532,6 +532,11 @@ def syrk_splits(n_tiles_total: int, nsteps: int, cus: int = 256) -> int:
     return best
 
 
+# lower bound on the Gram v6 split-K factor (shorter-lived workgroups let the other IRLS
+# group's small kernels interleave with a Gram; experiment knob)
+SYRK6_MIN_SPLIT = int(__import__("os").environ.get("SGLM_SYRK6_MIN_SPLIT", "1"))
+
+
 def syrk6_splits(wgs1: int, nsteps: int, nact: int, P: int, slots: int = 1024) -> int:
     """Split-K factor for Gram v6: minimise (rounds of one-wave workgroups) x (workgroup
     time) + the split-K slab traffic (write + reduce-read of splits x nact x P^2 floats)."""
@@ -540,6 +545,8 @@ def syrk6_splits(wgs1: int, nsteps: int, nact: int, P: int, slots: int = 1024) -
     for s in (1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64):
         if s > max(1, nsteps // 8):
             break
+        if s < SYRK6_MIN_SPLIT and s < max(1, nsteps // 8):
+            continue
         t = math.ceil(wgs1 * s / slots) * math.ceil(nsteps / s) * t_step
         if s > 1:
             t += s * nact * P * P * 8.0 / 4e12

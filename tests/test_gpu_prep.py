@@ -26,7 +26,7 @@ def _stack(cols):
 
 
 @pytest.mark.parametrize("n,seed,k,rate", [
-    (3000, 0, 7, 0.02), (3000, 1, 0, 0.05), (2000, 2, -3, 0.03), (500, 3, 7, 0.2),
+    (3000, 0, 7, 0.02), (3000, 15, 1, 0.02), (3000, 1, 0, 0.05), (2000, 2, -3, 0.03), (500, 3, 7, 0.2),
     (6, 4, 7, 0.5), (1, 5, 7, 0.5), (400, 6, 7, 0.0), (2500, 7, 25, 0.01),
     # scan chunk boundaries (2048 rows per chunk) with trials spanning chunks
     (2047, 8, 7, 0.002), (2048, 9, 7, 0.002), (2049, 10, 7, 0.002), (20000, 11, 7, 0.0005),

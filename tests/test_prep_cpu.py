@@ -17,7 +17,7 @@ def _same(a, b):
 
 
 @pytest.mark.parametrize("n,seed,k,rate", [
-    (3000, 0, 7, 0.02), (3000, 1, 0, 0.05), (2000, 2, -3, 0.03), (500, 3, 7, 0.2),
+    (3000, 0, 7, 0.02), (3000, 15, 1, 0.02), (3000, 1, 0, 0.05), (2000, 2, -3, 0.03), (500, 3, 7, 0.2),
     (6, 4, 7, 0.5), (1, 5, 7, 0.5), (400, 6, 7, 0.0), (2500, 7, 25, 0.01),
 ])
 def test_oracle_matches_pandas_semantics(n, seed, k, rate):
