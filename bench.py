@@ -4,12 +4,15 @@ Workload (configs[3], the config the metric is quoted on; it fits one MI355X): P
 1M rows x 2000 time-shifted predictors (50 Bernoulli(0.02) events x 40 lags, synthetic per
 SURVEY.md §8(d)), 5 GroupShuffleSplit splits x 20 lambdas + 20 full refits = 120 fits.
 One step = one full CV grid (all 120 fits solved to convergence + scored).  With N ranks
-the 120 fits are dealt round-robin (strong scaling: the grid is fixed); results are
-all-gathered over RCCL once per grid.
+the 120 fits are cut into mask-major, row-cost-balanced shards (grid.shard_plan; strong
+scaling: the grid is fixed); results are all-gathered over RCCL once per grid.
 
-value = fit-iterations (sum over fits of Newton/IRLS iterations, all ranks) / wall time.
+value = CV-grid wall-clock (seconds per grid, max over ranks; lower is better).  The IRLS
+rates ride along in `config`: all fit-iterations / s, and the Gram-forming ones (fit-iterations
+whose own X^T W X was computed) / s.
 
-Usage: python bench.py [--gpus N --steps K --warmup W] ; N > 1 under torch.distributed.run.
+Usage: python bench.py [--gpus N --steps K --warmup W].  With N > 1 and no launcher it starts
+N rank processes itself (torch.distributed.run, 127.0.0.1) before touching the GPU.
 """
 from __future__ import annotations
 
@@ -51,8 +54,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--cpu-rows", type=int, default=200_000)
-    ap.add_argument("--sklearn-rows", type=int, default=100_000)
+    ap.add_argument("--cpu-rows", type=int, default=100_000,
+                    help="rows of the oracle Newton sample (secondary CPU figure)")
+    ap.add_argument("--sklearn-rows", type=int, default=100_000,
+                    help="rows of the reference-path (sklearn lbfgs fold loop) sample")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI) for real runs; gloo to rehearse several ranks "
                          "on fewer GPUs")
@@ -68,59 +73,87 @@ def dense_slice(s, rows):
     return X
 
 
-def cpu_baseline(s, n_rows_unit, rows, fit_iters_per_grid, sk_rows):
-    """Oracle (float64 numpy/LAPACK damped Newton) on a bounded slice of the same design, plus
-    scikit-learn called directly with the estimator the reference selects
-    (TweedieRegressor(power=1), backend/sglm.py:112-115): newton-cholesky (IRLS-equivalent)
-    and the reference's default lbfgs."""
-    from oracle import glm_ref
+def _cpu_model():
+    import platform
+    try:
+        with open("/proc/cpuinfo") as f:
+            return next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
+    except Exception:  # pragma: no cover
+        return platform.machine()
+
+
+def _blas_threads():
     try:
         from threadpoolctl import threadpool_info
-        cores = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+        return max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
     except Exception:  # pragma: no cover
-        cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+        return int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+
+
+def cpu_reference_grid(s, cv_idx, lams, rows, lam_sample=(0, 10, 19), fold_threads=4):
+    """The reference's CPU path on a row sample of the same design: for each sampled lambda,
+    cv_glm_single_params' work (backend/sglm_cv.py:106-181) -- the 5 split fits on
+    X[idx_train] copies dealt to 4 worker threads (:162-170), then the full refit -- with the
+    estimator backend/sglm.py:112-115 selects, sklearn TweedieRegressor(power=1, alpha),
+    default lbfgs / tol 1e-4 / max_iter 100.  sklearn is called directly: the reference
+    modules' import is denied.  Extrapolated to the 1M-row, 20-lambda grid:
+    x (20 / lambdas sampled) x (N / rows), labelled as such."""
+    import threading
+    from sklearn.linear_model import TweedieRegressor
     rows = min(rows, s.N)
     X = dense_slice(s, rows)
     y = s.y[:rows]
+    # the splits restricted to the sample's rows (the same trial-id splits)
+    sub = [(tr[tr < rows], te[te < rows]) for tr, te in cv_idx]
+    per_lam = []
+    iters = []
+    t_all = time.perf_counter()
+    for j in lam_sample:
+        alpha = float(lams[j])
+        t0 = time.perf_counter()
+        tasks = list(range(len(sub)))
+        lock = threading.Lock()
+
+        def worker():
+            while True:
+                with lock:
+                    if not tasks:
+                        return
+                    k = tasks.pop(0)
+                tr = sub[k][0]
+                m = TweedieRegressor(power=1, alpha=alpha).fit(X[tr], y[tr])
+                iters.append(int(m.n_iter_))
+        ths = [threading.Thread(target=worker) for _ in range(fold_threads)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        m = TweedieRegressor(power=1, alpha=alpha).fit(X, y)       # the full refit
+        iters.append(int(m.n_iter_))
+        per_lam.append(time.perf_counter() - t0)
+    sample_s = time.perf_counter() - t_all
+    grid_s = float(np.mean(per_lam)) * len(lams) * (s.N / rows)
+    return {"value": grid_s, "unit": "s per CV grid (extrapolated)", "cores": _blas_threads(),
+            "kind": "reference",
+            "sample": f"sklearn TweedieRegressor(power=1) lbfgs, reference fold loop (4 threads "
+                      f"+ refit), first {rows} rows x {s.p}, lambdas {list(lam_sample)} in "
+                      f"{sample_s:.1f} s (lbfgs iters {min(iters)}-{max(iters)}); "
+                      f"x{len(lams) / len(lam_sample):.2f} lambdas x{s.N / rows:.0f} rows",
+            "cpu": _cpu_model(), "nproc": os.cpu_count()}
+
+
+def cpu_port_iter(s, n_rows_unit, rows):
+    """Secondary: the float64 oracle's damped Newton (the IRLS restatement) per iteration,
+    scaled to 1M rows."""
+    from oracle import glm_ref
+    rows = min(rows, s.N)
+    X = dense_slice(s, rows)
     t0 = time.perf_counter()
-    _, _, iters = glm_ref.fit_tweedie_newton(X, y, 1e-2, 1.0, tol=1e-8, max_iter=50,
+    _, _, iters = glm_ref.fit_tweedie_newton(X, s.y[:rows], 1e-2, 1.0, tol=1e-8, max_iter=50,
                                              return_iters=True)
     dt = time.perf_counter() - t0
-    per_iter_unit = dt / max(iters, 1) * (n_rows_unit / rows)
-    out = {"value": 1.0 / per_iter_unit, "unit": "IRLS fit-iterations/s (1M-row unit)",
-           "cores": int(cores), "kind": "port",
-           "sample": f"oracle fp64 damped Newton (numpy/LAPACK), Poisson alpha=1e-2, {rows}x{s.p} "
-                     f"slice of the C4 design, {iters} iterations in {dt:.2f} s; per-iteration "
-                     f"time scaled x{n_rows_unit / rows:.2f} to 1M rows",
-           "grid_wall_s_extrapolated": fit_iters_per_grid * per_iter_unit}
-    del X
-    try:
-        import platform
-        from sklearn.linear_model import TweedieRegressor
-        sk_rows = min(sk_rows, s.N)
-        X = dense_slice(s, sk_rows)
-        y = s.y[:sk_rows]
-        model = platform.machine()
-        try:
-            with open("/proc/cpuinfo") as f:
-                model = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
-        except Exception:  # pragma: no cover
-            pass
-        sk = {"rows": sk_rows, "cpu": model, "nproc": os.cpu_count()}
-        for solver in ("newton-cholesky", "lbfgs"):
-            m = TweedieRegressor(power=1.0, alpha=1e-2, link="log", solver=solver, tol=1e-4,
-                                 max_iter=100)
-            t0 = time.perf_counter()
-            m.fit(X, y)
-            dt = time.perf_counter() - t0
-            it = int(m.n_iter_)
-            sk[solver] = {"n_iter": it, "fit_s": dt,
-                          "fit_s_1M_rows": dt * n_rows_unit / sk_rows,
-                          "iters_per_s_1M_rows": it / dt * sk_rows / n_rows_unit}
-        out["sklearn_direct"] = sk
-    except Exception as e:  # pragma: no cover - sklearn is part of the image
-        out["sklearn_direct"] = {"error": repr(e)}
-    return out
+    return {"iters_per_s_1M_rows": max(iters, 1) / dt * rows / n_rows_unit, "rows": rows,
+            "iters": int(iters), "s": round(dt, 2)}
 
 
 def pmc_traffic():
@@ -293,13 +326,71 @@ def bench_prep(a):
         "cpu_baseline": cpu}))
 
 
+def spawn_ranks(a):
+    """``--gpus N`` without a launcher: start N rank processes (torch.distributed.run, one per
+    GPU, rendezvous on 127.0.0.1) as CHILDREN before anything touches the GPU, and exit with
+    their status.  Under a launcher (WORLD_SIZE set) this returns and main() runs the rank."""
+    if a.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={a.gpus}", "--master-addr", "127.0.0.1", "--master-port",
+           str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
+
+
+def newton_distance(s, design, cv_idx, res, lams, checks):
+    """float64 distance |H^-1 g|_inf / max|beta| of a few fits of the last grid to the exact
+    minimiser, from the exact design on the device (torch float64; outside the timed region)."""
+    import torch
+    m = s.E.shape[1]
+    Ed = torch.from_numpy(s.E).cuda().to(torch.float64)
+    Xd = torch.empty((s.N, s.p + 1), dtype=torch.float64, device="cuda")
+    r0 = s.L - 1
+    for bi, sh in enumerate(s.shifts):
+        Xd[:, bi * m:(bi + 1) * m] = Ed[r0 - sh:r0 - sh + s.N]
+    Xd[:, s.p] = 1.0
+    yd = torch.from_numpy(s.y).cuda()
+    worst = 0.0
+    for j, k in checks:
+        r = res[j]
+        if k < 0:
+            coef, b, msk = r["refit_coef"], r["refit_intercept"], None
+        else:
+            coef, b, msk = r["cv_coefs"][:, k], r["cv_intercepts"][k], cv_idx[k][0]
+        w = torch.ones(s.N, dtype=torch.float64, device="cuda")
+        if msk is not None:
+            w.zero_()
+            w[torch.from_numpy(np.asarray(msk)).cuda()] = 1.0
+        beta = torch.from_numpy(np.r_[coef, b]).cuda()
+        mu = torch.exp(Xd @ beta)
+        pen = torch.full((s.p + 1,), float(lams[j]) * float(w.sum()), dtype=torch.float64,
+                         device="cuda")
+        pen[-1] = 0.0
+        g = Xd.t() @ (w * (mu - yd)) + pen * beta
+        H = Xd.t() @ (Xd * (w * mu)[:, None])
+        H.diagonal().add_(pen)
+        worst = max(worst, float(torch.linalg.solve(H, g).abs().max()) / float(beta[:-1].abs().max()))
+        del H
+    del Xd
+    torch.cuda.empty_cache()
+    return worst
+
+
 def main():
     a = parse()
+    spawn_ranks(a)
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but the launcher started {world} rank(s)")
     dev = local % max(1, torch.cuda.device_count())   # one rank per GPU; wraps only in rehearsals
     torch.cuda.set_device(dev)
     if world > 1:
@@ -355,79 +446,78 @@ def main():
     kflop = sum(nact_flop for _, _, _, nact_flop in stats.syrk_events)
     nlaunch = len(stats.syrk_events)
     t = torch.tensor([elapsed, float(stats.fit_iters), ktime, kflop, float(nlaunch),
-                      float(stats.gram_fits), stats.alg_flop, float(stats.reused)],
+                      float(stats.gram_fits), stats.alg_flop, float(stats.reused),
+                      float(stats.gram_fit_iters), float(stats.stops["stagnation"]),
+                      float(stats.stops["line_search_failed"] + stats.stops["max_iter"])],
                      dtype=torch.float64, device="cuda" if a.dist_backend == "nccl" else "cpu")
     if world > 1:
         mx = t.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         sm = t.clone()
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        elapsed, fit_iters = float(mx[0]), float(sm[1])
-        ktime, kflop, nlaunch = float(sm[2]), float(sm[3]), int(sm[4])
-        gram_fits, alg_flop, reused = float(sm[5]), float(sm[6]), float(sm[7])
-    else:
-        fit_iters = float(stats.fit_iters)
-        gram_fits, alg_flop = float(stats.gram_fits), stats.alg_flop
-        reused = float(stats.reused)
+        elapsed = float(mx[0])
+        t = sm
+    fit_iters, ktime, kflop, nlaunch = float(t[1]), float(t[2]), float(t[3]), int(t[4])
+    gram_fits, alg_flop, reused, gram_iters = float(t[5]), float(t[6]), float(t[7]), float(t[8])
+    stag, failed = int(t[9]), int(t[10])
     if rank == 0:
-        pa = s.p + 1
+        grid_s = elapsed / a.steps
         achieved = kflop / ktime / 1e12 if ktime > 0 else 0.0
         traffic, traffic_src = pmc_traffic()
+        conv = all(r["converged"] for r in res)
+        ndist = None
+        if world == 1 and a.config == "c4":
+            # float64 Newton distance of the lambda = 1e-4 split-0 fit and refit (parity spot
+            # check of the timed grid's output; tests/test_gpu_fullsize.py checks every fit)
+            ndist = newton_distance(s, design, cv_idx, res, lams, [(0, 0), (0, -1)])
         cpu = None
         if not a.no_cpu and world == 1:
-            cpu = cpu_baseline(s, s.N, a.cpu_rows, fit_iters / a.steps, a.sklearn_rows)
+            cpu = cpu_reference_grid(s, cv_idx, lams, a.sklearn_rows)
+            cpu["port_oracle_newton"] = cpu_port_iter(s, s.N, a.cpu_rows)
         out = {
             "metric": "IRLS iters/sec on 1M×2000 design mat; CV-grid wall-clock (5-fold×20 λ)",
-            "value": fit_iters / elapsed,
-            "unit": "IRLS fit-iterations/s",
+            "value": grid_s,
+            "unit": "s per CV grid (5 splits x 20 lambdas + 20 refits = 120 fits)",
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": elapsed / a.steps * 1e3,
-            "higher_is_better": True,
+            "ms_per_step": grid_s * 1e3,
+            "higher_is_better": False,
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic",
             "config": {
-                "workload": f"Poisson/log IRLS CV grid: {s.N} rows x {s.p} timeshifted predictors "
-                            f"({m} events x {len(s.shifts)} lags), {K} GroupShuffleSplit splits x "
-                            f"{nlam} lambdas + {nlam} refits = {nlam * (K + 1)} fits",
+                "workload": f"Poisson CV grid {s.N}x{s.p} ({m} events x {len(s.shifts)} lags), "
+                            f"{K} splits x {nlam} lambdas + refits",
                 "config_name": a.config,
-                "n_rows": s.N, "p": s.p, "fits": nlam * (K + 1),
-                "grid_wall_s": elapsed / a.steps,
+                "irls_fit_iters_per_s": fit_iters / elapsed,
+                "gram_forming_fit_iters_per_s": gram_iters / elapsed,
                 "fit_iters_per_grid": fit_iters / a.steps,
-                "distinct_hessians_per_grid": gram_fits / a.steps,
+                "gram_forming_fit_iters_per_grid": gram_iters / a.steps,
                 "kept_factor_fit_iters_per_grid": reused / a.steps,
-                "hess_reuse_tol": E.HESS_REUSE_TOL,
-                "init_passes_untimed": INIT_PASSES,
+                "computed_grams_per_grid": gram_fits / a.steps,
                 "grid_roofline_frac": alg_flop / elapsed / (world * PEAK_BF16_TFLOPS * 1e12),
-                "grid_roofline_note": "SURVEY.md 8(d): sum over fit-iterations of "
-                                      "n p'(p'+1) + 4 n p' + p'^3/3 + 2 p'^2, / wall / "
-                                      "(n_gpus x 2.5 PF)",
-                "setup_s": setup_s,
-                "parallelism": f"fits round-robin over {world} rank(s), RCCL all-gather of results",
+                "all_converged": bool(conv),
+                "stagnation_or_failed_stops": stag + failed,
+                "newton_dist_f64": ndist,
+                "setup_s": round(setup_s, 2),
+                "parallelism": f"fit shards over {world} rank(s), RCCL all-gather of results",
             },
             "roofline": {
                 "bound": "mfma",
-                "kernel": "syrk6_kernel (X^T diag(w) X over row-compacted bit-planes, v_mfma_f32_32x32x16_bf16)",
+                "kernel": "syrk6_kernel",
                 "achieved": achieved,
                 "peak": PEAK_BF16_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": achieved / PEAK_BF16_TFLOPS,
                 "traffic": traffic,
-                "traffic_unit": "bytes per launch (HBM/fabric, PMC)",
                 "traffic_source": traffic_src,
-                "algorithmic_flop_per_fit_iter": f"n_train*p'*(p'+1), p'={pa}",
                 "launches": nlaunch,
                 "avg_launch_ms": ktime / max(nlaunch, 1) * 1e3,
-                "per_launch": [[n_, round(e0.elapsed_time(e1), 2), round(f_ / e0.elapsed_time(e1) / 1e9, 1)]
-                               for e0, e1, n_, f_ in stats.syrk_events] if world == 1 else None,
             },
             "cpu_baseline": cpu,
         }
-        conv = all(r["converged"] for r in res)
-        out["config"]["all_converged"] = bool(conv)
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

@@ -69,6 +69,8 @@ struct ScanCols {
     const double* key;     // segment key or nullptr
     int64_t n;
     int rev;
+    int keep;              // NC == 1: rows with a NaN VALUE get the running total (rows with a
+                           // NaN key stay NaN) -- the per-trial totals need it
 };
 
 // Logical row i is physical row rev ? n-1-i : i.  NaN values contribute the identity and stay
@@ -177,7 +179,7 @@ __global__ void __launch_bounds__(kPT) scan_apply_kernel(ScanCols a,
             const bool kn = a.key && isnan(a.key[p]);
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
-                const double v = NC == 1 ? (nanr ? NAN : r.v[c])
+                const double v = NC == 1 ? ((nanr && !(a.keep && !kn)) ? NAN : r.v[c])
                                          : ((kn || isnan(a.x[c][p])) ? NAN : r.v[c]);
                 a.y[c][p] = v;
             }
@@ -200,9 +202,10 @@ int scan(const ScanCols& a, void* agg, hipStream_t s) {
     return check_launch("prep scan");
 }
 
-ScanCols cols1(const double* x, double* y, const double* key, int64_t n, int rev) {
+ScanCols cols1(const double* x, double* y, const double* key, int64_t n, int rev,
+               int keep = 0) {
     ScanCols a = {};
-    a.x[0] = x; a.y[0] = y; a.key = key; a.n = n; a.rev = rev;
+    a.x[0] = x; a.y[0] = y; a.key = key; a.n = n; a.rev = rev; a.keep = keep;
     return a;
 }
 
@@ -294,7 +297,9 @@ struct Out {  // output columns (SGLM_PREP_OUT_* order)
     double* c[SGLM_PREP_NOUT];
 };
 
-// Reward flags (per-trial sum of r = forward + backward segmented sums - r), port indicators,
+// Reward flags (per-trial sum of r = forward + backward segmented sums - r, NaN r counted as 0
+// as groupby().transform(sum) skips it; the scans carry their running totals through NaN-r
+// rows), port indicators,
 // side-agnostic sums, nn / xx (lynne_pp.py:121-123, 142-151, 170-178, 193-194).
 __global__ void prep_rows_kernel(In in, const double* __restrict__ ntrial, int64_t n, Out o,
                                  const double* __restrict__ s0, const double* __restrict__ s1) {
@@ -303,7 +308,8 @@ __global__ void prep_rows_kernel(In in, const double* __restrict__ ntrial, int64
     const double r = in.r[t], nr = in.nr[t];
     const double rpx = in.rpx[t], lpx = in.lpx[t], rpn = in.rpn[t], lpn = in.lpn[t];
     const bool has = !isnan(ntrial[t]);
-    const double tot = s0[t] + s1[t] - r;      // s0 = forward, s1 = backward segmented sums
+    // s0 = forward, s1 = backward segmented sums (NaN r rows hold the running totals)
+    const double tot = s0[t] + s1[t] - (isnan(r) ? 0.0 : r);
     o.c[SGLM_PREP_OUT_R_TRIAL][t] = (has && tot > 0.0) ? 1.0 : 0.0;
     o.c[SGLM_PREP_OUT_NR_TRIAL][t] = (has && tot <= 0.0) ? 1.0 : 0.0;
     const double rpxr = r * rpx, rpxnr = nr * rpx, lpxr = r * lpx, lpxnr = nr * lpx;
@@ -417,8 +423,8 @@ extern "C" int sglm_prep_session(const double* in, int64_t ld_in, int64_t n, int
                               s)))
         return st;
     // per-trial reward totals (forward + backward segmented sums), indicators
-    if ((st = scan<OP_ADD, 1>(cols1(x.r, T0, ntrial, n, 0), agg, s))) return st;
-    if ((st = scan<OP_ADD, 1>(cols1(x.r, T1, ntrial, n, 1), agg, s))) return st;
+    if ((st = scan<OP_ADD, 1>(cols1(x.r, T0, ntrial, n, 0, 1), agg, s))) return st;
+    if ((st = scan<OP_ADD, 1>(cols1(x.r, T1, ntrial, n, 1, 1), agg, s))) return st;
     prep_rows_kernel<<<g, bs, 0, s>>>(x, ntrial, n, o, T0, T1);
     // per-trial cumulative sums of nn, xx, cpn in one 3-column scan, then first-time events
     ScanCols c3 = {};

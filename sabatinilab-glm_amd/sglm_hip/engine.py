@@ -426,10 +426,15 @@ class IrlsStats:
     fit_iters: int = 0
     newton_iters: int = 0
     gram_fits: int = 0                                  # distinct Hessians formed
+    gram_fit_iters: int = 0     # fit-iterations whose own Gram was computed (Gram-forming)
     reused: int = 0                                     # fit-iterations that kept a factor
     alg_flop: float = 0.0       # SURVEY.md §8(d) F summed over fit-iterations
     trace_phases: bool = False                          # sync + time grid phases (tools)
     phases: dict = field(default_factory=dict)          # host wall seconds per phase
+    # why fits stopped (converged fits: tol + line_search_converged)
+    stops: dict = field(default_factory=lambda: dict.fromkeys(
+        ("tol", "stagnation", "line_search_converged", "line_search_failed", "max_iter",
+         "stale_factor_retry"), 0))
 
     def mark(self, name, t0):
         """Add the wall time since t0 (after a device sync) to phase `name`; returns now."""
@@ -698,6 +703,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         g_h[:B].copy_(bf.gtot[:B], non_blocking=True)
         t0 = tick("it_gradient", t0)
         # ---- Hessian
+        gram_comp = np.zeros(B, dtype=bool)     # fits whose Gram is computed this iteration
         if const_hess:
             gram_now[:] = not factored
             if not factored:
@@ -706,6 +712,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                     reps.setdefault(reqs[k].mask, k)
                 rep_idx = np.array(sorted(reps.values()), dtype=np.int32)
                 _syrk(d, bf, rep_idx, nsteps, ntile1, stats, st, exact=True, rows=rows)
+                gram_comp[rep_idx] = True
                 for k in act:
                     rk = reps[reqs[k].mask]
                     if rk != k:
@@ -733,6 +740,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                     dup.append((k, rk))
                     drift[k] = dist_k
             _syrk(d, bf, uniq, nsteps, ntile1, stats, st, rows=rows)
+            gram_comp[uniq] = True
             for k, rk in dup:
                 bf.H[k].copy_(bf.H[rk])
             gram_now[:] = False
@@ -805,29 +813,50 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         if stats is not None:
             stats.newton_iters += 1
             stats.fit_iters += int(act.size)
-            # SURVEY.md §8(d) F per fit-iteration; the Gram and factorisation terms only for
-            # fit-iterations that took a new Hessian (a kept factor costs two triangular solves)
+            # SURVEY.md §8(d) F per fit-iteration, charged for work actually done: the Gram
+            # term only where a Gram was computed (not for a Hessian shared from another fit),
+            # the factorisation where a new factor was formed (a kept factor costs the two
+            # triangular solves only)
             pa = float(p + 1)
             nr = rows[act]
-            newh = gram_now[act]
-            stats.alg_flop += float(np.sum(np.where(newh, nr * pa * (pa + 1) + pa ** 3 / 3, 0.0)
+            stats.alg_flop += float(np.sum(np.where(gram_comp[act], nr * pa * (pa + 1), 0.0)
+                                           + np.where(gram_now[act], pa ** 3 / 3, 0.0)
                                            + 4.0 * nr * pa + 2 * pa * pa))
-        relv = (np.max(np.abs(step[act, None] * delta[act]), axis=1)
-                / (1.0 + np.max(np.abs(beta[act]), axis=1)))
+            stats.gram_fit_iters += int(np.sum(gram_comp[act]))
+        scale = 1.0 + np.max(np.abs(beta[act]), axis=1)
+        relv = np.max(np.abs(step[act, None] * delta[act]), axis=1) / scale
+        prop = np.max(np.abs(delta[act]), axis=1) / scale      # the proposed Newton step
         stepa = step[act]
+        fresh = gram_now[act] | const_hess
+        ls_fail = stepa == 0.0
+        # a failed line search on a kept (stale) factor is not a verdict: the next iteration
+        # forms a fresh Hessian for that fit instead of stopping it
+        if not const_hess:
+            drift[act[ls_fail & ~fresh]] = np.inf
+        stop_tol = ~ls_fail & (relv <= tol)
         # stagnation (the f32 noise floor): a step no better than half the previous one, judged
         # only on steps taken with a fresh Hessian -- a kept factor contracts by up to
-        # e^(c D) - 1, which may legitimately exceed 1/2 (Gaussian: the exact Hessian, always)
-        fresh = gram_now[act] | const_hess
-        stop = ((stepa == 0.0) | (relv <= tol) |
-                ((relv < 1e-4) & (relv >= 0.5 * prev_rel[act]) & fresh))
-        conv_now = stop & ((stepa != 0.0) | (relv <= tol) |
-                           (np.max(np.abs(delta[act]), axis=1) < 1e-5))
+        # e^(c D) - 1, which may legitimately exceed 1/2 (Gaussian: the exact Hessian, always).
+        # It stops the fit but is NOT convergence: the fit is reported unconverged.
+        stop_stag = (~ls_fail & ~stop_tol & fresh & (relv < 1e-4)
+                     & (relv >= 0.5 * prev_rel[act]))
+        # a failed search on a fresh Hessian: converged only if the proposed step itself is
+        # within tol (the iterate already sits at the minimiser up to rounding)
+        stop_fail = ls_fail & fresh
+        stop = stop_tol | stop_stag | stop_fail
+        conv_now = stop_tol | (stop_fail & (prop <= tol))
         active[act[stop]] = False
         converged[act[stop]] = conv_now[stop]
         out_of_iters = ~stop & (n_iter[act] >= max_iter[act])
         active[act[out_of_iters]] = False
         prev_rel[act] = relv
+        if stats is not None:
+            stats.stops["tol"] += int(np.sum(stop_tol))
+            stats.stops["stagnation"] += int(np.sum(stop_stag))
+            stats.stops["line_search_converged"] += int(np.sum(stop_fail & (prop <= tol)))
+            stats.stops["line_search_failed"] += int(np.sum(stop_fail & (prop > tol)))
+            stats.stops["max_iter"] += int(np.sum(out_of_iters))
+            stats.stops["stale_factor_retry"] += int(np.sum(ls_fail & ~fresh))
         t0 = tick("it_update", t0)
 
     retire(np.arange(B))
@@ -941,8 +970,11 @@ def irls_scored(prob: Problem, reqs: List[FitReq], sets: np.ndarray,
             stats.fit_iters += sg.fit_iters
             stats.newton_iters = max(stats.newton_iters, sg.newton_iters)
             stats.gram_fits += sg.gram_fits
+            stats.gram_fit_iters += sg.gram_fit_iters
             stats.reused += sg.reused
             stats.alg_flop += sg.alg_flop
+            for k, v in sg.stops.items():
+                stats.stops[k] += v
             for k, v in sg.phases.items():
                 stats.phases[k] = stats.phases.get(k, 0.0) + v
     for s_ in {(d.device, g) for g in range(len(parts))}:

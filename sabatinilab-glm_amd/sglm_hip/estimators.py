@@ -97,9 +97,21 @@ class _EngineRegressor:
             return c, b
         return None, None
 
+    # Designs already resident for this estimator, keyed by id() of the host array they were
+    # packed from (set only for the duration of GLM.fit_set, which uses each of X / X_test
+    # two or three times; outside it every call packs its X, as sklearn does).
+    _resident = None
+
+    def _design(self, X):
+        res = self._resident
+        if res is not None and id(X) in res and res[id(X)][0] is X:
+            return res[id(X)][1]
+        return E.Design.from_host(_as2d(X))
+
     def fit(self, X, y, sample_weight=None):
         if sample_weight is not None:
             raise NotYetImplementedError("sample_weight is not used by the reference path")
+        Xh = X
         X = _as2d(X)
         y = np.asarray(y, dtype=np.float64).reshape(-1)
         if X.shape[0] != y.shape[0]:
@@ -107,7 +119,7 @@ class _EngineRegressor:
                              f"[{X.shape[0]}, {y.shape[0]}]")
         obj = self.objective()
         _check_y_range(obj.power if obj.family == E.FAM_TWEEDIE_LOG else 0, y)
-        d = E.Design.from_host(X)
+        d = self._design(Xh)
         prob = E.Problem(d, [y], [np.ones(X.shape[0], np.uint8)])
         c0, b0 = self._warm()
         if c0 is not None and c0.shape[0] != X.shape[1]:
@@ -130,11 +142,12 @@ class _EngineRegressor:
 
     def _linear_predictor(self, X):
         import torch
+        Xh = X
         X = _as2d(X)
         if X.shape[1] != self.coef_.shape[0]:
             raise ValueError(f"X has {X.shape[1]} features, but {type(self).__name__} is expecting "
                              f"{self.coef_.shape[0]} features as input.")
-        d = E.Design.from_host(X)
+        d = self._design(Xh)
         beta = np.zeros((1, d.P), dtype=np.float32)
         beta[0, : d.p] = self.coef_
         beta[0, d.p] = self.intercept_

@@ -167,6 +167,58 @@ def run(X, y, cv_idx, objectives: Sequence[Objective], rolls: Sequence[int],
     return out if simulate is not None else out[0]
 
 
+def plan_fits(groups: Sequence[dict], n: int):
+    """Host-side plan of a (multi-)grid, identical on every rank: the row-mask specs, per
+    group its ([(train, test)] mask ids, refit mask, holdout mask), the masks' row counts, the
+    fit table -- per group, (param j, split k) then refit (j, -1) as (group, j, k, fit mask,
+    response, second score mask) -- and the sorted roll list (responses)."""
+    specs, mkey = [], {}
+    dedup = len(groups) > 1                  # one grid's masks are distinct by construction
+
+    def add_spec(idx, multiplicity):
+        """idx: row indices (None = every row); multiplicity: repeats count (fold lists)."""
+        if dedup:                            # resplit grids share masks: dedup by content
+            a = _mask_array(idx, multiplicity, n)
+            k = a.tobytes()
+            if k not in mkey:
+                mkey[k] = len(specs)
+                specs.append((idx, multiplicity, a))
+            return mkey[k]
+        specs.append((idx, multiplicity, None))
+        return len(specs) - 1
+
+    gm = []
+    for g in groups:
+        splits = [(add_spec(tr, True), add_spec(te, True)) for tr, te in g["cv_idx"]]
+        refit = add_spec(g.get("refit_rows"), False)
+        hold = g.get("holdout_rows")
+        gm.append((splits, refit, -1 if hold is None else add_spec(hold, False)))
+    counts = [_mask_count(sp[0], sp[1], n) for sp in specs]
+    roll_list = sorted(set(int(r) for g in groups for r in g["rolls"]) | {0})
+    ridx = {r: i for i, r in enumerate(roll_list)}
+    table = []
+    for gi, g in enumerate(groups):
+        splits, refit, hold = gm[gi]
+        for j, (obj, roll) in enumerate(zip(g["objectives"], g["rolls"])):
+            for k, (tr, te) in enumerate(splits):
+                table.append((gi, j, k, tr, ridx[int(roll)], te))
+            table.append((gi, j, -1, refit, 0, hold))
+    return specs, gm, counts, table, roll_list
+
+
+def rank_share(plan, groups: Sequence[dict], rank: int, world: int):
+    """Fit-table indices rank ``rank`` of ``world`` solves (mask-major cost-balanced chunks)."""
+    specs, gm, counts, table, roll_list = plan
+    if world > 1 and SHARD_PLAN == "round_robin":
+        return shard_indices(len(table), rank, world)
+    if world > 1:
+        njs = [len(g["objectives"]) for g in groups]
+        keys = [(t[3], t[4], snake(t[1], njs[t[0]]), t[0], t[1]) for t in table]
+        costs = [counts[t[3]] for t in table]
+        return shard_plan(keys, costs, rank, world)
+    return list(range(len(table)))
+
+
 def run_multi(X, y, groups: Sequence[dict], score_method: str = "mse", coef0=None,
               intercept0=None, stats=None, shard=True, simulate=None):
     """Several CV grids over ONE resident design, solved as one batch (SURVEY.md §8(f) 2:
@@ -183,53 +235,12 @@ def run_multi(X, y, groups: Sequence[dict], score_method: str = "mse", coef0=Non
     y = np.asarray(y, dtype=np.float64).reshape(-1)
     if y.shape[0] != n:
         raise ValueError(f"y has {y.shape[0]} rows, X has {n}")
-    # ---- row masks: specs first (index lists), arrays only for the masks this rank uses
-    specs, mkey = [], {}
-    dedup = len(groups) > 1                  # one grid's masks are distinct by construction
-
-    def add_spec(idx, multiplicity):
-        """idx: row indices (None = every row); multiplicity: repeats count (fold lists)."""
-        if dedup:                            # resplit grids share masks: dedup by content
-            a = _mask_array(idx, multiplicity, n)
-            k = a.tobytes()
-            if k not in mkey:
-                mkey[k] = len(specs)
-                specs.append((idx, multiplicity, a))
-            return mkey[k]
-        specs.append((idx, multiplicity, None))
-        return len(specs) - 1
-
-    gm = []                                  # per group: ([(train, test)], refit, holdout)
-    for g in groups:
-        splits = [(add_spec(tr, True), add_spec(te, True)) for tr, te in g["cv_idx"]]
-        refit = add_spec(g.get("refit_rows"), False)
-        hold = g.get("holdout_rows")
-        gm.append((splits, refit, -1 if hold is None else add_spec(hold, False)))
-    counts = [_mask_count(sp[0], sp[1], n) for sp in specs]
-    t0 = tick("setup_masks", t0)
-    roll_list = sorted(set(int(r) for g in groups for r in g["rolls"]) | {0})
-    ridx = {r: i for i, r in enumerate(roll_list)}
-
-    # ---- fit table: per group, (param j, split k) then refit (j, -1)
-    table = []                               # (group, j, k, fit mask, resp, second score mask)
-    for gi, g in enumerate(groups):
-        splits, refit, hold = gm[gi]
-        for j, (obj, roll) in enumerate(zip(g["objectives"], g["rolls"])):
-            for k, (tr, te) in enumerate(splits):
-                table.append((gi, j, k, tr, ridx[int(roll)], te))
-            table.append((gi, j, -1, refit, 0, hold))
+    plan = plan_fits(groups, n)
+    specs, gm, counts, table, roll_list = plan
     t0 = tick("grid_setup", t0)
     dist = _dist() if shard and simulate is None else None
     rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (simulate or (0, 1))
-    if world > 1 and SHARD_PLAN == "round_robin":
-        mine = shard_indices(len(table), rank, world)
-    elif world > 1:
-        njs = [len(g["objectives"]) for g in groups]
-        keys = [(t[3], t[4], snake(t[1], njs[t[0]]), t[0], t[1]) for t in table]
-        costs = [counts[t[3]] for t in table]
-        mine = shard_plan(keys, costs, rank, world)
-    else:
-        mine = list(range(len(table)))
+    mine = rank_share(plan, groups, rank, world)
 
     # only the masks (and responses) of this rank's fits are built and uploaded
     used = sorted({table[i][3] for i in mine} | {table[i][5] for i in mine if table[i][5] >= 0})
@@ -316,7 +327,15 @@ def run_multi(X, y, groups: Sequence[dict], score_method: str = "mse", coef0=Non
         return results
     results = merge_results(results, dist)
 
-    # ---- assemble per-param dicts (reference key order, backend/sglm_cv.py:188-200)
+    out_all = assemble(groups, plan, results, p)
+    tick("assemble", t0)
+    return out_all
+
+
+def assemble(groups: Sequence[dict], plan, results: dict, p: int):
+    """Per-param result dicts (reference key order, backend/sglm_cv.py:188-200) of every group
+    from the merged per-fit results {table index: (coef, intercept, n_iter, converged, scores)}."""
+    specs, gm, counts, table, roll_list = plan
     out_all = []
     for gi, g in enumerate(groups):
         K = len(gm[gi][0])
@@ -367,7 +386,6 @@ def run_multi(X, y, groups: Sequence[dict], score_method: str = "mse", coef0=Non
                 d["refit_holdout_r2"], d["refit_holdout_neg_mse"] = hold_scores
             out.append(d)
         out_all.append(out)
-    tick("assemble", t0)
     return out_all
 
 

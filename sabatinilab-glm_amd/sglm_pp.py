@@ -57,7 +57,12 @@ def concat_end_crop_start(blanks: np.ndarray, X_to_shift: np.ndarray):
 def shifted_cols_to_pandas(X: pd.DataFrame, shifted_X: np.ndarray, shift_inx: list,
                            keep_non_inx: bool) -> pd.DataFrame:
     return_setup = X.copy()
-    return_setup.iloc[:, shift_inx] = shifted_X
+    # column-by-position replacement: the shifted column's dtype (float64 when NaN-filled)
+    # replaces the original, as iloc assignment upcast under the reference's pandas 1.1.3;
+    # an in-place iloc write into int columns is deprecated in pandas 2
+    shifted_X = np.asarray(shifted_X)
+    for q, col in enumerate(np.atleast_1d(shift_inx)):
+        return_setup.isetitem(int(col), shifted_X[:, q])
     if not keep_non_inx:
         return_setup = return_setup.iloc[:, shift_inx]
     return return_setup

@@ -10,6 +10,7 @@ Sources — never the reference code itself (its import/execution was denied, SU
   and the 4x3 matrix), rebuilt here from the same tiny numpy expressions.
 
 Usage: ``python tests/golden/make_golden.py`` -> tests/golden/*.npz / *.json
+       ``python tests/golden/make_golden.py api`` -> tests/golden/api.npz only
 """
 from __future__ import annotations
 
@@ -183,7 +184,49 @@ def cv_grid():
     return out
 
 
+def api_extras():
+    """Round-2 pins: Tweedie with an explicit power (GLM('Tweedie', power=1.5),
+    backend/sglm.py:116-117), sklearn's D^2 ``TweedieRegressor.score`` (what GLM.r2_score
+    returns for the Tweedie family, backend/sglm.py:184) on train and held-out rows, and a
+    warm-started fit (backend/sglm.py:91-92,134-140: coef_/intercept_ preset, warm_start)."""
+    out = {}
+    sp = synth.make(N=3000, m=4, L=5, family="poisson", rho=0.05, seed=10, beta_scale=0.3)
+    X, y = sp.dense_X(), sp.y
+    tr, te = np.arange(0, 2400), np.arange(2400, 3000)
+    out.update(api_X=X, api_y=y)
+    for key, power, a in (("tw15", 1.5, 0.05), ("pois", 1.0, 0.01), ("tw12", 1.2, 0.1)):
+        m = TweedieRegressor(power=power, alpha=a, solver="newton-cholesky", tol=1e-12,
+                             max_iter=1000).fit(X[tr], y[tr])
+        out[f"{key}_coef"] = m.coef_
+        out[f"{key}_b"] = np.array(m.intercept_)
+        out[f"{key}_d2_train"] = np.array(m.score(X[tr], y[tr]))
+        out[f"{key}_d2_test"] = np.array(m.score(X[te], y[te]))
+        out[f"{key}_alpha"] = np.array(a)
+        out[f"{key}_power"] = np.array(power)
+    # Gamma D^2 (power 2) on the gamma design
+    sg = synth.make(N=2000, m=3, L=3, family="gamma", rho=0.1, seed=20, beta_scale=0.2)
+    Xg = sg.dense_X()
+    mg = TweedieRegressor(power=2, alpha=0.05, solver="newton-cholesky", tol=1e-12,
+                          max_iter=1000).fit(Xg, sg.y)
+    out.update(gam_X=Xg, gam_y=sg.y, gam_coef=mg.coef_, gam_b=np.array(mg.intercept_),
+               gam_d2=np.array(mg.score(Xg, sg.y)))
+    # warm start: lbfgs from a preset (coef_, intercept_) reaches the same minimiser
+    w0 = np.full(X.shape[1], 0.05)
+    mw = TweedieRegressor(power=1, alpha=0.01, warm_start=True, solver="newton-cholesky",
+                          tol=1e-12, max_iter=1000)
+    mw.coef_, mw.intercept_ = w0.copy(), -0.5
+    mw.fit(X[tr], y[tr])
+    out.update(warm_w0=w0, warm_b0=np.array(-0.5), warm_coef=mw.coef_,
+               warm_b=np.array(mw.intercept_))
+    return out
+
+
 def main():
+    if sys.argv[1:] == ["api"]:            # round-2 fixture only (others unchanged)
+        np.savez_compressed(os.path.join(HERE, "api.npz"), **api_extras())
+        print("api fixture written")
+        return
+    np.savez_compressed(os.path.join(HERE, "api.npz"), **api_extras())
     np.savez_compressed(os.path.join(HERE, "timeshift_known.npz"), **timeshift_known_answers())
     f, meta = fits()
     np.savez_compressed(os.path.join(HERE, "fits.npz"), **f)

@@ -80,3 +80,93 @@ def test_shard_plan_mask_major_balanced():
                 assert min(lams) < nlam // 2 <= max(lams)
     assert [grid.snake(j, 5) for j in range(5)] == [0, 2, 4, 3, 1]
     assert sorted(grid.snake(j, 6) for j in range(6)) == list(range(6))
+
+
+def _grid_worker(rank, world, port, q):
+    """One rank of a sharded CV grid with the product's host plan (grid.plan_fits /
+    rank_share / merge_results / assemble); each rank's per-fit solves come from the float64
+    oracle, in the exact per-fit result format grid.run_multi gathers."""
+    import sys
+    import torch.distributed as dist
+    from conftest import PKG, ROOT
+    sys.path[:0] = [ROOT, PKG]
+    from oracle import glm_ref
+    from sglm_hip import engine as E, grid, synth
+    from sglm_hip.estimators import Objective
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    s = synth.make(N=1500, m=3, L=3, family="poisson", rho=0.1, seed=5, beta_scale=0.3)
+    X, y = s.dense_X(), s.y
+    rng = np.random.default_rng(1)
+    cv_idx = []
+    for _ in range(3):
+        perm = rng.permutation(s.N)
+        cv_idx.append((np.sort(perm[300:]), np.sort(perm[:300])))
+    alphas = [0.01, 0.1, 1.0]
+    groups = [{"cv_idx": cv_idx, "rolls": [0, 0, 0],
+               "objectives": [Objective("irls", E.FAM_TWEEDIE_LOG, 1.0, a, "n", True, 100)
+                              for a in alphas]}]
+    plan = grid.plan_fits(groups, s.N)
+    specs, gm, counts, table, roll_list = plan
+    mine = grid.rank_share(plan, groups, rank, world)
+    local = {}
+    for i in mine:
+        _, j, k, m, r, mt = table[i]
+        rows = np.arange(s.N) if k < 0 else cv_idx[k][0]
+        c, b = glm_ref.fit_tweedie_newton(X[rows], y[rows], alphas[j], 1.0)
+        sc = {}
+        if k >= 0:
+            te = cv_idx[k][1]
+            mu_tr = np.exp(X[rows] @ c + b)
+            mu_te = np.exp(X[te] @ c + b)
+            sc = {"train": -np.mean((y[rows] - mu_tr) ** 2), "test": -np.mean((y[te] - mu_te) ** 2),
+                  "ss_res": float(np.sum((y[te] - mu_te) ** 2)),
+                  "sst": float(np.sum((y[te] - y[te].mean()) ** 2)), "cnt_te": float(te.size)}
+        local[i] = (c, b, 1, True, sc)
+    merged = grid.merge_results(local, dist)
+    out = grid.assemble(groups, plan, merged, s.p)[0]
+    q.put((rank, sorted(mine), sorted(merged), out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_grid_plan_gather_assemble(world):
+    """shard_plan over real fit tables, merge_results over gloo, assemble into the
+    reference's per-param dicts: every rank ends with the same dicts, equal to the oracle's
+    unsharded cv_glm_mult_params (backend/sglm_cv.py:42-206)."""
+    import sys
+    from conftest import PKG, ROOT
+    sys.path[:0] = [ROOT, PKG]
+    from oracle import cv_ref
+    from sglm_hip import synth
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_grid_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    shares = [m for _, m, _, _ in outs]
+    assert sorted(i for m in shares for i in m) == list(range(12))
+    assert all(len(m) > 0 for m in shares)
+    s = synth.make(N=1500, m=3, L=3, family="poisson", rho=0.1, seed=5, beta_scale=0.3)
+    X, y = s.dense_X(), s.y
+    rng = np.random.default_rng(1)
+    cv_idx = []
+    for _ in range(3):
+        perm = rng.permutation(s.N)
+        cv_idx.append((np.sort(perm[300:]), np.sort(perm[:300])))
+    ref = cv_ref.cv_mult(X, y, cv_idx, [{"model_name": "Poisson", "alpha": a}
+                                        for a in (0.01, 0.1, 1.0)])["full_cv_results"]
+    for _, _, keys, out in outs:
+        assert keys == list(range(12))
+        for d, r in zip(out, ref):
+            np.testing.assert_allclose(d["cv_coefs"], r["cv_coefs"], rtol=0, atol=1e-10)
+            np.testing.assert_allclose(d["refit_coef"], r["coef"], rtol=0, atol=1e-10)
+            np.testing.assert_allclose(d["cv_scores_test"], r["cv_scores_test"], rtol=1e-12)
+            assert abs(d["cv_R2_score"] - r["cv_R2_score"]) < 1e-12
+            assert abs(d["cv_mse_score"] - r["cv_mse_score"]) < 1e-12 * r["cv_mse_score"]

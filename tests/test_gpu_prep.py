@@ -8,7 +8,7 @@ import pytest
 from oracle import prep_ref
 from oracle.prep_pandas import derived_columns
 from sglm_hip.synth import session as synth_session
-from test_prep_cpu import _same
+from test_prep_cpu import _same, with_nans
 
 pytestmark = pytest.mark.gpu
 
@@ -33,6 +33,22 @@ def _stack(cols):
 ])
 def test_session_columns_vs_oracle(prep, n, seed, k, rate):
     _, cols = synth_session(n, seed, rate)
+    D = prep.session_columns(_stack(cols), k)
+    ref = prep_ref.preprocess_columns(cols, k)
+    for j, name in enumerate(prep_ref.OUT_COLS):
+        assert _same(D[j], ref[name]), name
+
+
+@pytest.mark.parametrize("n,seed,k,names", [
+    (3000, 20, 7, ("r",)), (3000, 21, 1, ("r", "nr")),
+    (2500, 22, 7, ("r", "nr", "cpn", "lpx", "rpn", "ll")), (2049, 23, -3, ("cpn", "rpx", "lpn")),
+    (20000, 24, 7, ("r", "cpn")),
+])
+def test_session_columns_nan_inputs_vs_oracle(prep, n, seed, k, names):
+    """NaN samples in the event / reward columns (the per-trial reward total of a
+    NaN-r row must be the trial's skipna sum, as groupby('nTrial')['r'].transform(sum))."""
+    _, cols = synth_session(n, seed, 0.03 if n < 10000 else 0.002)
+    cols = with_nans(cols, seed, 0.02, names)
     D = prep.session_columns(_stack(cols), k)
     ref = prep_ref.preprocess_columns(cols, k)
     for j, name in enumerate(prep_ref.OUT_COLS):

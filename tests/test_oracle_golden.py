@@ -175,3 +175,34 @@ def test_c1_ols_oracle_vs_sklearn():
     sk = LinearRegression().fit(X[tr], s.y[tr])
     assert np.max(np.abs(c - sk.coef_)) <= 1e-9 * max(1.0, np.max(np.abs(sk.coef_)))
     assert abs(b - sk.intercept_) <= 1e-9 * max(1.0, abs(sk.intercept_))
+
+
+def test_d2_score_and_tweedie_power_pinned_to_sklearn(golden):
+    """glm_ref.r2_score's D^2 (GLM.r2_score for Tweedie, backend/sglm.py:184 -> sklearn
+    TweedieRegressor.score) and the explicit-power Tweedie fit (backend/sglm.py:116-117)
+    against sklearn 1.7.2 (tests/golden/make_golden.py::api_extras)."""
+    g = golden("api.npz")
+    X, y = g["api_X"], g["api_y"]
+    tr, te = np.arange(0, 2400), np.arange(2400, 3000)
+    for key in ("tw15", "pois", "tw12"):
+        power, a = float(g[f"{key}_power"]), float(g[f"{key}_alpha"])
+        c, b = glm_ref.fit_tweedie_newton(X[tr], y[tr], a, power)
+        assert np.max(np.abs(c - g[f"{key}_coef"])) < 1e-8 * max(1, np.max(np.abs(c))), key
+        assert abs(b - float(g[f"{key}_b"])) < 1e-8
+        spec = glm_ref.FitSpec("tweedie", alpha=a, power=power)
+        for rows, tag in ((tr, "train"), (te, "test")):
+            d2 = glm_ref.r2_score(spec, g[f"{key}_coef"], float(g[f"{key}_b"]), X[rows], y[rows])
+            assert abs(d2 - float(g[f"{key}_d2_{tag}"])) < 1e-12, (key, tag)
+    spec = glm_ref.FitSpec("tweedie", alpha=0.05, power=2.0)
+    d2 = glm_ref.r2_score(spec, g["gam_coef"], float(g["gam_b"]), g["gam_X"], g["gam_y"])
+    assert abs(d2 - float(g["gam_d2"])) < 1e-12
+
+
+def test_warm_start_oracle_reaches_the_same_minimiser(golden):
+    g = golden("api.npz")
+    X, y = g["api_X"], g["api_y"]
+    tr = np.arange(0, 2400)
+    c, b = glm_ref.fit_tweedie_newton(X[tr], y[tr], 0.01, 1.0,
+                                      coef0=np.r_[g["warm_w0"], float(g["warm_b0"])])
+    assert np.max(np.abs(c - g["warm_coef"])) < 1e-8
+    assert abs(b - float(g["warm_b"])) < 1e-8

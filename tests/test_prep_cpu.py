@@ -29,6 +29,29 @@ def test_oracle_matches_pandas_semantics(n, seed, k, rate):
         assert _same(got[name], ref[name]), name
 
 
+def with_nans(cols, seed, frac=0.01, names=("r", "nr", "cpn", "lpx", "rpn", "ll")):
+    """Float copies of the session columns with NaN at random rows of `names` (missing samples
+    in the acquisition files): pandas' skipna sums/cumsums and NaN-key groupby paths."""
+    rng = np.random.default_rng(seed)
+    out = {c: np.asarray(v, dtype=np.float64).copy() for c, v in cols.items()}
+    for c in names:
+        out[c][rng.random(out[c].size) < frac] = np.nan
+    return out
+
+
+@pytest.mark.parametrize("n,seed,k,names", [
+    (3000, 20, 7, ("r",)), (3000, 21, 1, ("r", "nr")), (2500, 22, 7, ("r", "nr", "cpn", "lpx", "rpn", "ll")),
+    (2049, 23, -3, ("cpn", "rpx", "lpn")),
+])
+def test_oracle_matches_pandas_with_nan_inputs(n, seed, k, names):
+    _, cols = synth_session(n, seed, 0.03)
+    cols = with_nans(cols, seed, 0.02, names)
+    ref = derived_columns(cols, k)
+    got = prep_ref.preprocess_columns(cols, k)
+    for name in prep_ref.OUT_COLS:
+        assert _same(got[name], ref[name]), name
+
+
 def test_oracle_columns_match_product_layout():
     import sglm_hip.prep as prep
     assert prep.IN_COLS == prep_ref.IN_COLS and prep.OUT_COLS == prep_ref.OUT_COLS
