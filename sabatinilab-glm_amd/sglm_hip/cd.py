@@ -23,7 +23,7 @@ def enet_batch(prob: E.Problem, objectives, reqs):
     from . import enet
     d = prob.design
     B, P, ld, p = len(reqs), d.P, d.ld, d.p
-    bf = E._BUF.get(B, P, ld, d.device)
+    bf = E._scratch().buf.get(B, P, ld, d.device)
     grams = enet.SharedGrams(prob)
     pairs = list(dict.fromkeys((r.resp, r.mask) for r in reqs))
     ci = {pm: i for i, pm in enumerate(pairs)}

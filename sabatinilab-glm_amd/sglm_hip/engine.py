@@ -473,11 +473,35 @@ class _Buffers:
         return self
 
 
-_BUF = _Buffers()
-_WORK = {}
-_TLS = threading.local()        # .ns: scratch namespace of an IRLS group thread (0 = main)
-_GROUP_BUF = {}                 # group -> _Buffers
-_GROUP_STREAM = {}              # (device, group) -> torch stream
+class _Scratch:
+    """Per-thread engine scratch: device work buffers, pinned readback buffers, the IRLS batch
+    buffers, and (for a thread that splits a batch into IRLS groups) its group threads'
+    scratch and streams.  The reference calls fit / fit_set from several threads at once
+    (backend/sglm_cv.py:162-170), so no two threads may share one."""
+
+    def __init__(self):
+        self.work = {}          # (device, tag) -> uint8 device buffer (grow-only)
+        self.pinned = {}        # (tag, dtype) -> pinned host buffer (grow-only)
+        self.buf = _Buffers()
+        self.groups = {}        # group -> _Scratch of that IRLS group's thread
+        self.streams = {}       # (device, group) -> torch stream
+
+
+_TLS = threading.local()        # .scratch: this thread's _Scratch
+_MAIN_SCRATCH = _Scratch()
+
+
+def _scratch() -> _Scratch:
+    """The calling thread's scratch: the main thread's lives for the process (so repeated
+    grids reuse their buffers), other threads get their own (freed with the thread); IRLS group
+    threads are handed their parent's persistent group scratch."""
+    s = getattr(_TLS, "scratch", None)
+    if s is None:
+        s = _MAIN_SCRATCH if threading.current_thread() is threading.main_thread() else _Scratch()
+        _TLS.scratch = s
+    return s
+
+
 _GRAM_LOCK = threading.Lock()   # orders the Gram launches of concurrent IRLS groups ...
 _GRAM_DONE = {}                 # device -> event after the last Gram enqueued (any stream)
 
@@ -497,29 +521,26 @@ def _gram_done():
     _GRAM_DONE[torch.cuda.current_device()] = ev
 
 
-_PINNED = {}
-
-
 def _pinned(tag, numel, dtype):
-    """Grow-only pinned host buffer per (group namespace, tag): page-locked allocation is slow,
+    """Grow-only pinned host buffer per (thread scratch, tag): page-locked allocation is slow,
     so the per-iteration readback buffers are allocated once and reused (flat; callers view)."""
-    key = (getattr(_TLS, "ns", 0), tag, dtype)
-    t = _PINNED.get(key)
+    pinned = _scratch().pinned
+    t = pinned.get((tag, dtype))
     if t is None or t.numel() < numel:
         t = torch.zeros(int(numel), dtype=dtype).pin_memory()
-        _PINNED[key] = t
+        pinned[(tag, dtype)] = t
     return t[:numel]
 
 
 def _work(nbytes, dev, tag="main"):
-    """Grow-only scratch buffer per (group namespace, device, tag); stream-ordered reuse only
-    (each IRLS group thread has its own namespace and stream)."""
+    """Grow-only scratch buffer per (thread scratch, device, tag); stream-ordered reuse only
+    (each thread that runs the engine has its own scratch)."""
     nbytes = max(int(nbytes), 16)
-    key = (getattr(_TLS, "ns", 0), dev, tag)
-    t = _WORK.get(key)
+    work = _scratch().work
+    t = work.get((dev, tag))
     if t is None or t.numel() < nbytes:
         t = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        _WORK[key] = t
+        work[(dev, tag)] = t
     return t
 
 
@@ -572,7 +593,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         raise ValueError("irls(): one loss family per batch")
     B0, P, ld, n, p = len(reqs), d.P, d.ld, d.n, d.p
     dev = d.device
-    bf = (bufs or _BUF).get(B0, P, ld, dev)
+    bf = (bufs or _scratch().buf).get(B0, P, ld, dev)
     st = _stream()
     log_link = fam == FAM_TWEEDIE_LOG
     reqs0 = list(reqs)
@@ -931,21 +952,24 @@ def irls_scored(prob: Problem, reqs: List[FitReq], sets: np.ndarray,
     main = torch.cuda.current_stream()
     out = [None] * len(parts)
     errs = []
+    parent = _scratch()
+    streams = []
+    for g in range(len(parts)):
+        key = (d.device, g)
+        if key not in parent.streams:
+            parent.streams[key] = torch.cuda.Stream(device=d.device)
+        streams.append(parent.streams[key])
 
     def run(g, idx):
         try:
-            _TLS.ns = g + 1
-            key = (d.device, g)
-            if key not in _GROUP_STREAM:
-                _GROUP_STREAM[key] = torch.cuda.Stream(device=d.device)
-            s = _GROUP_STREAM[key]
+            _TLS.scratch = parent.groups.setdefault(g, _Scratch())
+            s = streams[g]
             s.wait_stream(main)
             with torch.cuda.stream(s):
                 sg = None
                 if stats is not None:
                     sg = IrlsStats(record=stats.record, trace_phases=stats.trace_phases)
-                res, eta = irls(prob, [reqs[i] for i in idx], stats=sg,
-                                bufs=_GROUP_BUF.setdefault(g, _Buffers()))
+                res, eta = irls(prob, [reqs[i] for i in idx], stats=sg)
                 sums = score_sums(prob, fam, power, eta, [fresp[i] for i in idx], sets[idx])
             s.synchronize()
             out[g] = (res, sums, sg)
@@ -977,8 +1001,8 @@ def irls_scored(prob: Problem, reqs: List[FitReq], sets: np.ndarray,
                 stats.stops[k] += v
             for k, v in sg.phases.items():
                 stats.phases[k] = stats.phases.get(k, 0.0) + v
-    for s_ in {(d.device, g) for g in range(len(parts))}:
-        main.wait_stream(_GROUP_STREAM[s_])
+    for s_ in streams:
+        main.wait_stream(s_)
     return res, sums
 
 

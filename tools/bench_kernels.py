@@ -146,7 +146,7 @@ def main():
         for v in vs[1:]:
             res[f"maxrel_v{v}_vs_v{vs[0]}"] = float(((H[v][:, up] - a0).abs().max() / a0.abs().max()).item())
     if a.other:
-        bf = E._BUF.get(B, d.P, d.ld, "cuda")
+        bf = E._scratch().buf.get(B, d.P, d.ld, "cuda")
         bf.H.copy_(H[vs[-1]])
         dsh = torch.full((B, d.P), -1.0, dtype=torch.float32, device="cuda")
         dsh[:, : d.p] = 1e-2 * d.n
