@@ -91,14 +91,23 @@ class SharedGrams:
 
 
 def xty(prob: E.Problem, pairs: Sequence[tuple]) -> torch.Tensor:
-    """c[(r, m)] = X^T (m * y_r) (float64 [len(pairs)][P]; c[p] = sum m y)."""
+    """c[(r, m)] = X^T (m * y_r) (float64 [len(pairs)][P]; c[p] = sum m y).  y is split into
+    f32 high and low parts (two exact-product passes), so c carries float64 y, as the
+    reference's float64 ElasticNet does."""
     d = prob.design
     out = torch.empty((len(pairs), d.P), dtype=torch.float64, device=d.device)
+    ylo = prob.y_lo()
+    tmp = None if ylo is None else torch.empty((min(256, len(pairs)), d.P), dtype=torch.float64,
+                                               device=d.device)
     chunk = 256
     for s in range(0, len(pairs), chunk):
         pr = pairs[s:s + chunk]
         R = torch.stack([prob.M[m].to(torch.float32) * prob.Y[r] for r, m in pr])
         d.xtr(R, len(pr), out[s:s + len(pr)])
+        if ylo is not None:
+            R = torch.stack([prob.M[m].to(torch.float32) * ylo[r] for r, m in pr])
+            d.xtr(R, len(pr), tmp[:len(pr)])
+            out[s:s + len(pr)] += tmp[:len(pr)]
     return out
 
 

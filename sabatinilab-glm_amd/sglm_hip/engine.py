@@ -306,9 +306,24 @@ class Problem:
         for f, m in enumerate(self.masks):
             M[f, :n] = m
         self.M = torch.from_numpy(M).to(dev)
+        self._ylo = None
         self._stats = {}
         self._groups = None
         self._compact = {}
+
+    def y_lo(self):
+        """f32 residual y - f32(y) of the responses ([R][ld], or None when every y is exact in
+        f32, e.g. counts): X^T(m y) = X^T(m y_hi) + X^T(m y_lo) recovers the float64 sums."""
+        if self._ylo is None:
+            n, ld, dev = self.design.n, self.design.ld, self.design.device
+            if self.Yd64 is not None:
+                y64 = self.Yd64.t()
+            else:
+                y64 = torch.from_numpy(np.stack(self.ys)).to(dev)
+            lo = torch.zeros_like(self.Y)
+            lo[:, :n] = (y64 - self.Y[:, :n].double()).float()
+            self._ylo = lo if bool(lo.any()) else False
+        return self._ylo if self._ylo is not False else None
 
     def _group_lists(self):
         """Row lists for the masked v2/v3 Gram (non-binary designs): the 8-row groups of every

@@ -1,10 +1,16 @@
 # Round artifacts: PMC traffic of the Gram (separate FETCH/WRITE passes), the default bench line
-# (with CPU baseline), and the rocprofv3 kernel-trace summary of the same bench command.
+# (with CPU baseline), the rocprofv3 kernel-trace summary of the same bench command, and the
+# uncontended per-kernel costs (one IRLS group: no second stream competing for CUs).
+# Usage on the box: bash tools/gpu_profile.sh ROUND   (e.g. r02)
 set -e
 export TMPDIR=/tmp
+R=${1:-r02}
 O=gpurun_out/prof; mkdir -p $O
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu > $O/fetch.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu > $O/write.log 2>&1
-python tools/pmc_traffic.py $O/fetch $O/write profiles/r01_pmc_traffic.json > $O/pmc.log 2>&1
+python tools/pmc_traffic.py $O/fetch $O/write profiles/${R}_pmc_traffic.json > $O/pmc.log 2>&1
 timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu > $O/bench_prof.json 2> $O/kt.err
+SGLM_IRLS_GROUPS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt1 -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu > $O/bench_prof_g1.json 2> $O/kt1.err
+timeout -k 10 200 python tools/grid_phases.py > $O/phases_g2.json 2> $O/phases.err
+SGLM_IRLS_GROUPS=1 timeout -k 10 200 python tools/grid_phases.py > $O/phases_g1.json 2>> $O/phases.err
