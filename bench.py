@@ -448,7 +448,8 @@ def main():
     t = torch.tensor([elapsed, float(stats.fit_iters), ktime, kflop, float(nlaunch),
                       float(stats.gram_fits), stats.alg_flop, float(stats.reused),
                       float(stats.gram_fit_iters), float(stats.stops["stagnation"]),
-                      float(stats.stops["line_search_failed"] + stats.stops["max_iter"])],
+                      float(stats.stops["line_search_failed"] + stats.stops["max_iter"]),
+                      float(stats.aliased), float(stats.newton_iters)],
                      dtype=torch.float64, device="cuda" if a.dist_backend == "nccl" else "cpu")
     if world > 1:
         mx = t.clone()
@@ -460,6 +461,7 @@ def main():
     fit_iters, ktime, kflop, nlaunch = float(t[1]), float(t[2]), float(t[3]), int(t[4])
     gram_fits, alg_flop, reused, gram_iters = float(t[5]), float(t[6]), float(t[7]), float(t[8])
     stag, failed = int(t[9]), int(t[10])
+    aliased, newton_iters = float(t[11]), float(t[12])
     if rank == 0:
         grid_s = elapsed / a.steps
         achieved = kflop / ktime / 1e12 if ktime > 0 else 0.0
@@ -496,6 +498,8 @@ def main():
                 "fit_iters_per_grid": fit_iters / a.steps,
                 "gram_forming_fit_iters_per_grid": gram_iters / a.steps,
                 "kept_factor_fit_iters_per_grid": reused / a.steps,
+                "aliased_fit_iters_per_grid": aliased / a.steps,
+                "newton_iters_per_grid": newton_iters / a.steps,
                 "computed_grams_per_grid": gram_fits / a.steps,
                 "grid_roofline_frac": alg_flop / elapsed / (world * PEAK_BF16_TFLOPS * 1e12),
                 "all_converged": bool(conv),

@@ -246,6 +246,15 @@ int sglm_chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t nact
                           int32_t* info, uint8_t* frozen, int32_t B, void* work,
                           sglm_stream_t stream);
 
+/* Solves on the stored factor of ANOTHER slot (engine.irls cross-mask Hessian sharing: a CV
+ * split fit preconditioned by the full-data fit's Hessian at the same penalty, scaled by the
+ * row-count ratio).  For i < nact: delta[fits[i]] = -rscale[i] * F^-1 F^-T g[fits[i]] with F the
+ * factor a previous sglm_chol_solve_* call left in H[fsrc[i]] (its frozen set applies).
+ * Replaces nothing in the reference (sklearn re-factors per fold copy, _newton_solver.py). */
+int sglm_chol_solve_alias(const float* H, int32_t P, const int32_t* fits, const int32_t* fsrc,
+                          int32_t nact, const double* g, const float* rscale, float* delta,
+                          const uint8_t* frozen, int32_t B, void* work, sglm_stream_t stream);
+
 /* Line search: out[k][j] = sum_i M[m][i] * loss(y_i, eta_i + t[j] * deta_i) (float64),
  * for j < T, fits k < B.  `work`: sglm_rowsum_work_bytes(B, T, n). */
 size_t sglm_rowsum_work_bytes(int32_t B, int32_t T, int64_t n);

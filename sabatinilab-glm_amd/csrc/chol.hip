@@ -67,6 +67,20 @@ __global__ void __launch_bounds__(kCT) chol_prep_kernel(
     for (int j = tid; j < P; j += kCT) rhs[j] = frz[j] ? 0.0f : (float)g[j];
 }
 
+// Right-hand sides of fits solved on ANOTHER slot's factor (engine.irls cross-mask Hessian
+// sharing): rhs[fit] = g[fit] * rscale, zero on the factor's frozen coordinates.
+__global__ void __launch_bounds__(kCT) chol_alias_prep_kernel(
+    int32_t P, const int32_t* __restrict__ fits, const int32_t* __restrict__ fsrc,
+    const double* __restrict__ gall, const float* __restrict__ rscale,
+    const uint8_t* __restrict__ frozen_all, float* __restrict__ rhs_all) {
+    const int fit = fits[blockIdx.x];
+    const uint8_t* frz = frozen_all + (int64_t)fsrc[blockIdx.x] * P;
+    const double* g = gall + (int64_t)fit * P;
+    float* rhs = rhs_all + (int64_t)fit * P;
+    const double sc = (double)rscale[blockIdx.x];
+    for (int j = threadIdx.x; j < P; j += kCT) rhs[j] = frz[j] ? 0.0f : (float)(g[j] * sc);
+}
+
 __device__ __forceinline__ float lanef(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
@@ -367,11 +381,13 @@ __device__ __forceinline__ void tri_upper_solve64(const float* __restrict__ H, i
 
 __global__ void __launch_bounds__(kST) chol_fwd2_kernel(
     const float* __restrict__ Hall, int32_t P, const int32_t* __restrict__ fits,
-    const uint8_t* __restrict__ frozen_all, float* __restrict__ rhs_all) {
+    const int32_t* __restrict__ fsrc, const uint8_t* __restrict__ frozen_all,
+    float* __restrict__ rhs_all) {
     __shared__ float z[kMaxP];
     const int fit = fits[blockIdx.x];
-    const float* H = Hall + (int64_t)fit * P * P;
-    const uint8_t* frz = frozen_all + (int64_t)fit * P;
+    const int src = fsrc ? fsrc[blockIdx.x] : fit;    // slot holding the factor
+    const float* H = Hall + (int64_t)src * P * P;
+    const uint8_t* frz = frozen_all + (int64_t)src * P;
     float* rhs = rhs_all + (int64_t)fit * P;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     for (int j = tid; j < P; j += kST) z[j] = rhs[j];
@@ -403,12 +419,13 @@ __global__ void __launch_bounds__(kST) chol_fwd2_kernel(
 
 __global__ void __launch_bounds__(kST) chol_back2_kernel(
     const float* __restrict__ Hall, int32_t P, const int32_t* __restrict__ fits,
-    const uint8_t* __restrict__ frozen_all, const float* __restrict__ rhs_all,
-    float* __restrict__ delta_all) {
+    const int32_t* __restrict__ fsrc, const uint8_t* __restrict__ frozen_all,
+    const float* __restrict__ rhs_all, float* __restrict__ delta_all) {
     __shared__ float x[kMaxP];
     const int fit = fits[blockIdx.x];
-    const float* H = Hall + (int64_t)fit * P * P;
-    const uint8_t* frz = frozen_all + (int64_t)fit * P;
+    const int src = fsrc ? fsrc[blockIdx.x] : fit;
+    const float* H = Hall + (int64_t)src * P * P;
+    const uint8_t* frz = frozen_all + (int64_t)src * P;
     const float* z = rhs_all + (int64_t)fit * P;
     float* delta = delta_all + (int64_t)fit * P;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -474,10 +491,10 @@ static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t na
     int st = check_launch("chol_prep_kernel");
     if (st) return st;
     if (nrefac == 0) {                       // stored factors only: two triangular solves
-        chol_fwd2_kernel<<<nact, kST, 0, s>>>(H, P, fits, frozen, rhs);
+        chol_fwd2_kernel<<<nact, kST, 0, s>>>(H, P, fits, nullptr, frozen, rhs);
         st = check_launch("chol_fwd2_kernel");
         if (st) return st;
-        chol_back2_kernel<<<nact, kST, 0, s>>>(H, P, fits, frozen, rhs, delta);
+        chol_back2_kernel<<<nact, kST, 0, s>>>(H, P, fits, nullptr, frozen, rhs, delta);
         return check_launch("chol_back2_kernel");
     }
     const int nb = P / kNB;
@@ -512,7 +529,7 @@ static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t na
     }
     st = check_launch("chol block kernels");
     if (st) return st;
-    chol_back2_kernel<<<nact, kST, 0, s>>>(H, P, fits, frozen, rhs, delta);
+    chol_back2_kernel<<<nact, kST, 0, s>>>(H, P, fits, nullptr, frozen, rhs, delta);
     return check_launch("chol_back2_kernel");
 }
 
@@ -522,6 +539,31 @@ extern "C" int sglm_chol_solve_ex(float* H, int32_t P, const int32_t* fits, int3
                                   int32_t B, void* work, sglm_stream_t stream) {
     return chol_solve_mixed(H, P, fits, nact, refactor ? nact : 0, g, dshift, delta, info,
                             frozen, B, work, as_stream(stream));
+}
+
+// Solves on stored factors of other slots: for i < nact, fit = fits[i] solves
+// (H_src / rscale[i]) delta = -g, i.e. delta[fit] = -rscale[i] * F_src^-1 F_src^-T g[fit],
+// src = fsrc[i] (frozen set of src).  The factors must be complete (a previous call).
+extern "C" int sglm_chol_solve_alias(const float* H, int32_t P, const int32_t* fits,
+                                     const int32_t* fsrc, int32_t nact, const double* g,
+                                     const float* rscale, float* delta, const uint8_t* frozen,
+                                     int32_t B, void* work, sglm_stream_t stream) {
+    if (nact <= 0) return SGLM_OK;
+    if (!H || !fits || !fsrc || !g || !rscale || !delta || !frozen || !work || P % kNB ||
+        P > kMaxP || B < nact) {
+        set_error("sglm_chol_solve_alias: bad args (P=%d)", P);
+        return SGLM_EINVAL;
+    }
+    hipStream_t s = as_stream(stream);
+    float* rhs = (float*)work;
+    chol_alias_prep_kernel<<<nact, kCT, 0, s>>>(P, fits, fsrc, g, rscale, frozen, rhs);
+    int st = check_launch("chol_alias_prep_kernel");
+    if (st) return st;
+    chol_fwd2_kernel<<<nact, kST, 0, s>>>(H, P, fits, fsrc, frozen, rhs);
+    st = check_launch("chol_fwd2_kernel");
+    if (st) return st;
+    chol_back2_kernel<<<nact, kST, 0, s>>>(H, P, fits, fsrc, frozen, rhs, delta);
+    return check_launch("chol_back2_kernel");
 }
 
 extern "C" int sglm_chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t nact,

@@ -20,9 +20,6 @@
 //   * optional split-K over rows (blockIdx.y) into fixed-order f32 slabs.
 #include "common.h"
 
-#ifndef SGLM_SYRK_DEFAULT
-#define SGLM_SYRK_DEFAULT 2
-#endif
 
 namespace sglm {
 
@@ -39,129 +36,6 @@ __device__ __forceinline__ void tile_coords(int t, int nt, int& ti, int& tj) {
     int rowlen = nt;
     while (t >= rowlen) { t -= rowlen; ++ti; --rowlen; }
     tj = ti + t;
-}
-
-__global__ void __launch_bounds__(kThreads) syrk_kernel(
-    const uint16_t* __restrict__ Xb, int64_t ld, int32_t P, int64_t nsteps_total,
-    int64_t steps_per_split, const float* __restrict__ W, const int32_t* __restrict__ fits,
-    int32_t ntiles, float* __restrict__ H, float* __restrict__ slab, int32_t nact) {
-    extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-
-    const int nt = P / kBM;
-    const int tile = blockIdx.x % ntiles;
-    const int slot = blockIdx.x / ntiles;
-    const int split = blockIdx.y;
-    int ti, tj;
-    tile_coords(tile, nt, ti, tj);
-    const int fit = fits[slot];
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
-    const int wr = wave >> 2, wc = wave & 3;   // 2 x 4 waves
-    const int r = lane & 31, h = lane >> 5;
-
-    const int64_t step0 = (int64_t)split * steps_per_split;
-    int64_t step1 = step0 + steps_per_split;
-    if (step1 > nsteps_total) step1 = nsteps_total;
-    const int64_t nsteps = step1 - step0;
-
-    const uint16_t* XA = Xb + (int64_t)(ti * kBM) * ld;
-    const uint16_t* XB = Xb + (int64_t)(tj * kBM) * ld;
-    const float* w = W + (int64_t)fit * ld;
-
-    // staging assignment: chunk q = tid + 512u (u = 0, 1): predictor col = q >> 2, part = q & 3
-    const int c0 = tid >> 2, part = tid & 3;
-    const int c1 = c0 + 128;
-
-    uint4 ra0, ra1, rb0, rb1;
-    f32x4 w0, w1;
-
-    auto gload = [&](int64_t step) {
-        const int64_t i = step * kBK + part * 8;
-        ra0 = *reinterpret_cast<const uint4*>(XA + (int64_t)c0 * ld + i);
-        ra1 = *reinterpret_cast<const uint4*>(XA + (int64_t)c1 * ld + i);
-        rb0 = *reinterpret_cast<const uint4*>(XB + (int64_t)c0 * ld + i);
-        rb1 = *reinterpret_cast<const uint4*>(XB + (int64_t)c1 * ld + i);
-        w0 = *reinterpret_cast<const f32x4*>(w + i);
-        w1 = *reinterpret_cast<const f32x4*>(w + i + 4);
-    };
-    auto scale = [&](uint4 v) -> uint4 {
-        const uint32_t in[4] = {v.x, v.y, v.z, v.w};
-        uint32_t o[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float lo = __uint_as_float(in[q] << 16) * (q < 2 ? w0[2 * q] : w1[2 * q - 4]);
-            const float hi = __uint_as_float(in[q] & 0xffff0000u) * (q < 2 ? w0[2 * q + 1] : w1[2 * q - 3]);
-            const __bf16 blo = (__bf16)lo, bhi = (__bf16)hi;
-            o[q] = (uint32_t)__builtin_bit_cast(uint16_t, blo) |
-                   ((uint32_t)__builtin_bit_cast(uint16_t, bhi) << 16);
-        }
-        return make_uint4(o[0], o[1], o[2], o[3]);
-    };
-    auto swrite = [&](int stage) {
-        uint16_t* A = smem + stage * kStage;
-        uint16_t* Bp = A + kPanel;
-        *reinterpret_cast<uint4*>(A + c0 * kRow + part * 8) = ra0;
-        *reinterpret_cast<uint4*>(A + c1 * kRow + part * 8) = ra1;
-        *reinterpret_cast<uint4*>(Bp + c0 * kRow + part * 8) = scale(rb0);
-        *reinterpret_cast<uint4*>(Bp + c1 * kRow + part * 8) = scale(rb1);
-    };
-
-    f32x16 acc[4][2];
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < 2; ++n) acc[m][n] = (f32x16){};
-
-    if (nsteps > 0) {
-        gload(step0);
-        swrite(0);
-        __syncthreads();
-        for (int64_t s = 0; s < nsteps; ++s) {
-            const int stage = (int)(s & 1);
-            if (s + 1 < nsteps) gload(step0 + s + 1);
-            const uint16_t* A = smem + stage * kStage;
-            const uint16_t* Bp = A + kPanel;
-#pragma unroll
-            for (int ks = 0; ks < kBK / 16; ++ks) {
-                bf16x8 af[4], bfr[2];
-#pragma unroll
-                for (int m = 0; m < 4; ++m)
-                    af[m] = *reinterpret_cast<const bf16x8*>(
-                        A + (wr * 128 + m * 32 + r) * kRow + ks * 16 + h * 8);
-#pragma unroll
-                for (int n = 0; n < 2; ++n)
-                    bfr[n] = *reinterpret_cast<const bf16x8*>(
-                        Bp + (wc * 64 + n * 32 + r) * kRow + ks * 16 + h * 8);
-#pragma unroll
-                for (int m = 0; m < 4; ++m)
-#pragma unroll
-                    for (int n = 0; n < 2; ++n)
-                        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[m], bfr[n],
-                                                                            acc[m][n], 0, 0, 0);
-            }
-            if (s + 1 < nsteps) swrite(stage ^ 1);
-            __syncthreads();
-        }
-    }
-
-    // epilogue: D[row][col], reg j -> row (j&3) + 8(j>>2) + 4h, col r
-    float* out;
-    int64_t ldo = P;
-    if (slab) out = slab + ((int64_t)split * nact + slot) * (int64_t)P * P;
-    else out = H + (int64_t)fit * P * P;
-    const int64_t rbase = (int64_t)ti * kBM + wr * 128;
-    const int64_t cbase = (int64_t)tj * kBM + wc * 64;
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < 2; ++n)
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const int64_t row = rbase + m * 32 + (j & 3) + 8 * (j >> 2) + 4 * h;
-                const int64_t col = cbase + n * 32 + r;
-                out[row * ldo + col] = acc[m][n][j];
-            }
 }
 
 // Sum the split slabs (fixed order) into H for the upper-triangular tiles only.
@@ -190,51 +64,6 @@ extern "C" {
 size_t sglm_syrk_work_bytes(int32_t P, int32_t nact, int32_t splits) {
     if (splits <= 1) return 0;
     return (size_t)splits * (size_t)nact * (size_t)P * (size_t)P * sizeof(float);
-}
-
-int sglm_syrk_v1(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, const float* W,
-                 const int32_t* fits, int32_t nact, int32_t splits, float* H, void* work,
-                 sglm_stream_t stream) {
-    if (nact <= 0) return SGLM_OK;
-    if (!Xb || !W || !fits || !H || P % kBM || ld % kBK || n > ld || splits < 1 ||
-        (splits > 1 && !work)) {
-        set_error("sglm_syrk: bad args (P=%d ld=%lld n=%lld splits=%d)", P, (long long)ld,
-                  (long long)n, splits);
-        return SGLM_EINVAL;
-    }
-    const int nt = P / kBM;
-    const int ntiles = nt * (nt + 1) / 2;
-    const int64_t nsteps_total = (n + kBK - 1) / kBK;     // rows >= n carry w = 0
-    const int64_t sps = (nsteps_total + splits - 1) / splits;
-    const size_t lds = (size_t)2 * kStage * sizeof(uint16_t);
-    hipStream_t s = as_stream(stream);
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)syrk_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds);
-        attr_set = true;
-    }
-    dim3 grid((unsigned)(ntiles * nact), (unsigned)splits);
-    float* slab = splits > 1 ? (float*)work : nullptr;
-    syrk_kernel<<<grid, kThreads, lds, s>>>(Xb, ld, P, nsteps_total, sps, W, fits, ntiles, H,
-                                            slab, nact);
-    int st = check_launch("syrk_kernel");
-    if (st || splits == 1) return st;
-    const int64_t PP = (int64_t)P * P;
-    unsigned gx = (unsigned)((PP + 255) / 256 < 4096 ? (PP + 255) / 256 : 4096);
-    syrk_reduce<<<dim3(gx, (unsigned)nact), 256, 0, s>>>(slab, P, nact, splits, fits, H);
-    return check_launch("syrk_reduce");
-}
-
-int sglm_syrk_variant(int32_t variant, const uint16_t* Xb, int64_t ld, int32_t P, int64_t n,
-                      const float* W, const int32_t* fits, int32_t nact, int32_t splits,
-                      float* H, void* work, sglm_stream_t stream);
-
-int sglm_syrk(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, const float* W,
-              const int32_t* fits, int32_t nact, int32_t splits, float* H, void* work,
-              sglm_stream_t stream) {
-    return sglm_syrk_variant(SGLM_SYRK_DEFAULT, Xb, ld, P, n, W, fits, nact, splits, H, work,
-                             stream);
 }
 
 }  // extern "C"
@@ -546,14 +375,6 @@ extern "C" int sglm_syrk_masked(const uint16_t* Xb, int64_t ld, int32_t P, int64
                         group_count, stream);
 }
 
-extern "C" int sglm_syrk_variant(int32_t variant, const uint16_t* Xb, int64_t ld, int32_t P,
-                                 int64_t n, const float* W, const int32_t* fits, int32_t nact,
-                                 int32_t splits, float* H, void* work, sglm_stream_t stream) {
-    if (variant == 1) return sglm_syrk_v1(Xb, ld, P, n, W, fits, nact, splits, H, work, stream);
-    return syrk2_launch(Xb, ld, P, n, W, fits, nact, splits, H, work, nullptr, nullptr, nullptr,
-                        stream);
-}
-
 static int syrk2_launch(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, const float* W,
                         const int32_t* fits, int32_t nact, int32_t splits, float* H, void* work,
                         const int32_t* grp, const int64_t* grp_off, const int32_t* grp_cnt,
@@ -586,153 +407,7 @@ static int syrk2_launch(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, co
     return check_launch("syrk_reduce");
 }
 
-// ---------------------------------------------------------------------------------------
-// v3: bit-packed 0/1 designs.  Event designs (the reference's time-shifted indicators) are
-// stored as bit-planes Xbits[a][i/32] (1 bit per element: 256 MB at 1M x 2048, resident in
-// the Infinity Cache), which removes the fabric bandwidth bound of v2 (16x fewer bytes per
-// K-step).  Per K-step each thread loads one 32-bit word per panel (32 rows of one
-// predictor), expands it to 16-bit masks (0x0000 / 0xFFFF) in LDS; fragments become bf16
-// by one v_and per dword: A = mask & bf16(1.0), B = mask & bf16(w) pair.  The result is
-// bitwise identical to v2 (bf16(1 * w) == bf16(w)).
-// LDS rows: 64 rows x 2 B = 128 B + 16 B pad (36-dword stride: conflict-free ds_read_b128).
 namespace sglm {
-constexpr int k3Row = 144;                      // bytes per predictor row
-constexpr int k3Panel = 256 * k3Row;            // 36 KB
-constexpr int k3Stage = 2 * k3Panel + 256;      // A, B masks + w[64]
-
-__device__ __forceinline__ void expand_store(uint32_t word, char* dst) {
-    uint32_t o[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_sbfe((int)word, 2 * k, 1);
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_sbfe((int)word, 2 * k + 1, 1);
-        o[k] = (lo & 0x0000FFFFu) | (hi & 0xFFFF0000u);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-        *reinterpret_cast<uint4*>(dst + 16 * q) = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
-}
-
-__global__ void __launch_bounds__(512) syrk3_kernel(
-    const uint32_t* __restrict__ Xbits, int64_t ld, int32_t P, int64_t nsteps_total,
-    int32_t splits, const float* __restrict__ W, const int32_t* __restrict__ fits,
-    int32_t ntiles, float* __restrict__ H, float* __restrict__ slab, int32_t nact,
-    const int32_t* __restrict__ grp, const int64_t* __restrict__ grp_off,
-    const int32_t* __restrict__ grp_cnt) {
-    extern __shared__ __attribute__((aligned(16))) char sm3[];
-    const int nt = P / 256;
-    const int tile = blockIdx.x % ntiles;
-    const int slot = blockIdx.x / ntiles;
-    const int split = blockIdx.y;
-    int ti, tj;
-    tile_coords(tile, nt, ti, tj);
-    const bool diag = ti == tj;
-    const int fit = fits[slot];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wr = wave >> 2, wc = wave & 3;
-    const int r = lane & 31, h = lane >> 5;
-    // aligned 64-row blocks: step t of this fit covers block gl[8t] / 8 (identity if no list)
-    const int32_t* gl = grp ? grp + grp_off[fit] : nullptr;
-    const int64_t nblk = grp ? (int64_t)grp_cnt[fit] / 8 : nsteps_total;
-    const int64_t sps = (nblk + splits - 1) / splits;
-    const int64_t step0 = (int64_t)split * sps;
-    const int nsteps = (int)(min(step0 + sps, nblk) - step0 > 0 ? min(step0 + sps, nblk) - step0 : 0);
-    const int64_t wpc = ld / 32;                       // bit words per predictor
-    const int col = tid >> 1, half = tid & 1;          // staging: one word per panel
-    const uint32_t* BA = Xbits + (int64_t)(ti * 256 + col) * wpc + half;
-    const uint32_t* BB = Xbits + (int64_t)(tj * 256 + col) * wpc + half;
-    const float* w = W + (int64_t)fit * ld;
-    auto blk_of = [&](int t) -> int64_t {
-        return gl ? (int64_t)gl[(step0 + t) * 8] / 8 : step0 + t;
-    };
-
-    uint32_t ra = 0, rb = 0;
-    f32x4 rw = {};
-    auto gload = [&](int64_t blk) {
-        ra = BA[blk * 2];
-        if (!diag) rb = BB[blk * 2];
-        if (tid < 16) rw = *reinterpret_cast<const f32x4*>(w + blk * 64 + 4 * tid);
-    };
-    auto swrite = [&](int buf) {
-        char* base = sm3 + buf * k3Stage;
-        expand_store(ra, base + col * k3Row + half * 64);
-        if (!diag) expand_store(rb, base + k3Panel + col * k3Row + half * 64);
-        if (tid < 16) *reinterpret_cast<f32x4*>(base + 2 * k3Panel + 16 * tid) = rw;
-    };
-
-    f32x16 acc[4][2];
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < 2; ++n) acc[m][n] = (f32x16){};
-
-    if (nsteps > 0) {
-        int64_t bnext = blk_of(0);
-        gload(bnext);
-        swrite(0);
-        if (nsteps > 1) bnext = blk_of(1);
-        __syncthreads();
-        for (int s = 0; s < nsteps; ++s) {
-            const int cur = s & 1;
-            if (s + 1 < nsteps) {
-                gload(bnext);                              // in flight during the MFMAs
-                if (s + 2 < nsteps) bnext = blk_of(s + 2);
-            }
-            const char* A = sm3 + cur * k3Stage;
-            const char* Bp = diag ? A : A + k3Panel;
-            const float* wv = reinterpret_cast<const float*>(A + 2 * k3Panel);
-#pragma unroll
-            for (int ks = 0; ks < 4; ++ks) {
-                const int boff = 32 * ks + 16 * h;         // byte offset of rows 16ks+8h..+7
-                const f32x4 w0 = *reinterpret_cast<const f32x4*>(wv + 16 * ks + 8 * h);
-                const f32x4 w1 = *reinterpret_cast<const f32x4*>(wv + 16 * ks + 8 * h + 4);
-                uint32_t wp[4];
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    wp[j] = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)w0[2 * j]) |
-                            ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)w0[2 * j + 1]) << 16);
-                    wp[2 + j] = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)w1[2 * j]) |
-                                ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)w1[2 * j + 1]) << 16);
-                }
-                bf16x8 af[4], bfr[2];
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    uint4 mk = *reinterpret_cast<const uint4*>(A + (wr * 128 + m * 32 + r) * k3Row + boff);
-                    mk.x &= 0x3F803F80u; mk.y &= 0x3F803F80u; mk.z &= 0x3F803F80u; mk.w &= 0x3F803F80u;
-                    af[m] = __builtin_bit_cast(bf16x8, mk);
-                }
-#pragma unroll
-                for (int n = 0; n < 2; ++n) {
-                    uint4 mk = *reinterpret_cast<const uint4*>(Bp + (wc * 64 + n * 32 + r) * k3Row + boff);
-                    mk.x &= wp[0]; mk.y &= wp[1]; mk.z &= wp[2]; mk.w &= wp[3];
-                    bfr[n] = __builtin_bit_cast(bf16x8, mk);
-                }
-#pragma unroll
-                for (int m = 0; m < 4; ++m)
-#pragma unroll
-                    for (int n = 0; n < 2; ++n)
-                        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[m], bfr[n],
-                                                                            acc[m][n], 0, 0, 0);
-            }
-            if (s + 1 < nsteps) swrite(cur ^ 1);
-            __syncthreads();
-        }
-    }
-    float* out = slab ? slab + ((int64_t)split * nact + slot) * (int64_t)P * P
-                      : H + (int64_t)fit * P * P;
-    const int64_t rbase = (int64_t)ti * 256 + wr * 128;
-    const int64_t cbase = (int64_t)tj * 256 + wc * 64;
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < 2; ++n)
-#pragma unroll
-            for (int j = 0; j < 16; ++j)
-                out[(rbase + m * 32 + (j & 3) + 8 * (j >> 2) + 4 * h) * P + cbase + n * 32 + r] =
-                    acc[m][n][j];
-}
-
 // Bit-plane packing of a feature-major bf16 design: bit b of word q of predictor a is
 // (X[a][32q + b] != 0).  One wave per 64 rows: __ballot gives two words at once.  Sets
 // *nonbinary if any value is not exactly 0 or 1.
@@ -767,40 +442,6 @@ extern "C" int sglm_pack_bits(const uint16_t* Xb, int64_t ld, int32_t P, uint32_
     }
     pack_bits_kernel<<<2048, 256, 0, as_stream(stream)>>>(Xb, ld, P, bits, nonbinary);
     return check_launch("pack_bits_kernel");
-}
-
-extern "C" int sglm_syrk_bits(const uint32_t* Xbits, int64_t ld, int32_t P, int64_t n,
-                              const float* W, const int32_t* fits, int32_t nact, int32_t splits,
-                              float* H, void* work, const int32_t* row_groups,
-                              const int64_t* group_offset, const int32_t* group_count,
-                              sglm_stream_t stream) {
-    if (nact <= 0) return SGLM_OK;
-    if (!Xbits || !W || !fits || !H || P % 256 || ld % 256 || n > ld || splits < 1 ||
-        (splits > 1 && !work)) {
-        set_error("sglm_syrk_bits: bad args");
-        return SGLM_EINVAL;
-    }
-    const int nt = P / 256;
-    const int ntiles = nt * (nt + 1) / 2;
-    const int64_t nst = (n + 63) / 64;
-    const size_t lds = (size_t)2 * k3Stage;
-    hipStream_t s = as_stream(stream);
-    static bool attr3 = false;
-    if (!attr3) {
-        (void)hipFuncSetAttribute((const void*)syrk3_kernel,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr3 = true;
-    }
-    float* slab = splits > 1 ? (float*)work : nullptr;
-    syrk3_kernel<<<dim3((unsigned)(ntiles * nact), (unsigned)splits), 512, lds, s>>>(
-        Xbits, ld, P, nst, splits, W, fits, ntiles, H, slab, nact, row_groups, group_offset,
-        group_count);
-    int st = check_launch("syrk3_kernel");
-    if (st || splits == 1) return st;
-    const int64_t PP = (int64_t)P * P;
-    unsigned gx = (unsigned)((PP + 255) / 256 < 4096 ? (PP + 255) / 256 : 4096);
-    syrk_reduce<<<dim3(gx, (unsigned)nact), 256, 0, s>>>(slab, P, nact, splits, fits, H);
-    return check_launch("syrk_reduce");
 }
 
 // ---------------------------------------------------------------------------------------

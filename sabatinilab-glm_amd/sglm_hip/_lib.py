@@ -59,6 +59,8 @@ SIGNATURES = {
                                      _vp, _vp]),
     "sglm_chol_solve_mixed": (C.c_int, [_vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32,
                                         _vp, _vp]),
+    "sglm_chol_solve_alias": (C.c_int, [_vp, _i32, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _i32, _vp,
+                                        _vp]),
     "sglm_rowsum_work_bytes": (_sz, [_i32, _i32, _i64]),
     "sglm_loss_trials": (C.c_int, [_i32, _f32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
                                    _vp, _i32, _vp, _vp, _vp]),

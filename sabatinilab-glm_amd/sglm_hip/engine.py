@@ -60,6 +60,16 @@ HESS_REUSE_TOL = float(__import__("os").environ.get("SGLM_HESS_REUSE_TOL", "0.37
 # predictor is within HESS_SHARE_TOL (max over its mask rows) of another's is factored from
 # that fit's Gram, and starts its drift count at that distance (same bound as above).
 HESS_SHARE_TOL = float(__import__("os").environ.get("SGLM_HESS_SHARE_TOL", "0.375"))
+# Cross-mask Hessian sharing (log-link families): the fits of one penalty (alpha per row),
+# response and intercept setting -- a lambda's CV split fits and its full-data refit -- differ
+# only in their row masks.  A split fit k is solved on the factor of the member with the most
+# rows ("representative") scaled by the row-count ratio, c_k (G_rep + alpha n_rep I') =
+# c_k G_rep + alpha n_k I', while its predictor stays within XMASK_TOL (max over its rows) of
+# the representative's; the generalized eigenvalues of (H_k, c_k H_rep) measured at the
+# solutions of the C3 grid lie in [0.92, 1.10] (contraction <= 0.1).  A fit whose aliased
+# step fails the line search or contracts slowly leaves the family for good.  0 disables.
+HESS_XMASK_TOL = float(__import__("os").environ.get("SGLM_HESS_XMASK_TOL", "0.5"))
+XMASK_SLOW = 0.7                # aliased-step contraction above which a fit leaves its family
 # Batch compaction: once at most COMPACT_FRAC of the batch is still iterating (and at least
 # COMPACT_MIN fits have stopped), the active fits are moved to the front slots.
 COMPACT_FRAC = float(__import__("os").environ.get("SGLM_COMPACT_FRAC", "0.75"))
@@ -443,13 +453,14 @@ class IrlsStats:
     gram_fits: int = 0                                  # distinct Hessians formed
     gram_fit_iters: int = 0     # fit-iterations whose own Gram was computed (Gram-forming)
     reused: int = 0                                     # fit-iterations that kept a factor
+    aliased: int = 0            # fit-iterations solved on a family representative's factor
     alg_flop: float = 0.0       # SURVEY.md §8(d) F summed over fit-iterations
     trace_phases: bool = False                          # sync + time grid phases (tools)
     phases: dict = field(default_factory=dict)          # host wall seconds per phase
     # why fits stopped (converged fits: tol + line_search_converged)
     stops: dict = field(default_factory=lambda: dict.fromkeys(
         ("tol", "stagnation", "line_search_converged", "line_search_failed", "max_iter",
-         "stale_factor_retry"), 0))
+         "stale_factor_retry", "alias_dropped"), 0))
 
     def mark(self, name, t0):
         """Add the wall time since t0 (after a device sync) to phase `name`; returns now."""
@@ -683,6 +694,24 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
     ntile1 = (P // 256) * (P // 256 + 1) // 2
     rows = np.array([prob.mask_stats(r.resp, r.mask)[0] for r in reqs], dtype=np.float64)
     bf.prob, bf.fit_mask = prob, fmask_h
+    # cross-mask families (slot of the representative per slot, -1: none / is one)
+    xmask_tol = 0.0 if const_hess else HESS_XMASK_TOL / max(1.0, abs(2.0 - power))
+    repl = np.full(B0, -1, dtype=np.int64)
+    if xmask_tol > 0.0:
+        fams = {}
+        for k, r in enumerate(reqs):
+            key = _family_key(r, rows[k])
+            if key is not None:
+                fams.setdefault(key, []).append(k)
+        for members in fams.values():
+            if len(members) > 1:
+                rk = max(members, key=lambda k: (rows[k], -k))
+                for k in members:
+                    if k != rk:
+                        repl[k] = rk
+    alias = np.full(B0, -1, dtype=np.int64)     # slot whose factor the fit used this iteration
+    no_alias = np.zeros(B0, dtype=bool)
+    rscale_d = torch.zeros(B0, dtype=torch.float32, device=dev)
 
     def retire(slots):
         """Record the results of the fits in `slots` (they leave the batch or it ends)."""
@@ -702,12 +731,17 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         act = np.flatnonzero(active)
         if act.size == 0:
             break
-        if act.size <= COMPACT_FRAC * B and B - act.size >= COMPACT_MIN:
+        # slots to keep: the active fits and the representatives whose factors they may use
+        need = np.unique(repl[act][(repl[act] >= 0) & ~no_alias[act]])
+        kept = np.union1d(act, need) if need.size else act
+        if act.size <= COMPACT_FRAC * B and B - kept.size >= COMPACT_MIN:
             retire(np.flatnonzero(~active))
-            m = int(act.size)
-            # in-place row moves, ascending (slot act[i] >= i is never a destination already
+            m = int(kept.size)
+            remap = np.full(B, -1, dtype=np.int64)
+            remap[kept] = np.arange(m)
+            # in-place row moves, ascending (slot kept[i] >= i is never a destination already
             # written): no temporaries, so no allocator traffic inside the iteration loop
-            moves = [(i, int(s_)) for i, s_ in enumerate(act) if i != s_]
+            moves = [(i, int(s_)) for i, s_ in enumerate(kept) if i != s_]
             if moves:
                 dst = torch.from_numpy(np.array([a for a, _ in moves], dtype=np.int64)).to(dev)
                 src = torch.from_numpy(np.array([b for _, b in moves], dtype=np.int64)).to(dev)
@@ -717,17 +751,20 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                     bf.eta[i].copy_(bf.eta[s_])
                     bf.H[i].copy_(bf.H[s_])
             (lam, penal, dsh, beta, drift, gram_now, active, n_iter, converged, prev_rel,
-             max_iter, rows, fid, fresp_h, fmask_h) = (
-                x[act] for x in (lam, penal, dsh, beta, drift, gram_now, active, n_iter,
-                                 converged, prev_rel, max_iter, rows, fid, fresp_h, fmask_h))
-            reqs = [reqs[s_] for s_ in act]
+             max_iter, rows, fid, fresp_h, fmask_h, repl, alias, no_alias) = (
+                x[kept] for x in (lam, penal, dsh, beta, drift, gram_now, active, n_iter,
+                                  converged, prev_rel, max_iter, rows, fid, fresp_h, fmask_h,
+                                  repl, alias, no_alias))
+            repl = np.where(repl >= 0, remap[np.maximum(repl, 0)], -1)
+            alias = np.where(alias >= 0, remap[np.maximum(alias, 0)], -1)
+            reqs = [reqs[s_] for s_ in kept]
             bf.dshift[:m].copy_(torch.from_numpy(dsh))
             lamp_d = torch.from_numpy(lam[:, None] * penal).to(dev)
             fit_resp = torch.from_numpy(fresp_h).to(dev)
             fit_mask = torch.from_numpy(fmask_h).to(dev)
             bf.fit_mask = fmask_h
             B = m
-            act = np.arange(m)
+            act = np.flatnonzero(active)
             t0 = tick("it_compact", t0)
         _lib.call("sglm_link_update", fam, power, n, ld, B, _p(bf.eta), _p(prob.Y), _p(prob.M),
                   _p(fit_resp), _p(fit_mask), _p(bf.W), _p(bf.R), st)
@@ -758,9 +795,16 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
             # response and coefficients (every fit of a mask/response pair in the first
             # iteration, which starts from the intercept-only model).  Form each distinct
             # Hessian once and copy it.  Fits whose predictor drifted less than reuse_tol
-            # since their last Hessian keep its factor (no Gram, no factorisation).
-            keep = act[drift[act] <= reuse_tol]
-            form = act[drift[act] > reuse_tol]
+            # since their last Hessian keep its factor (no Gram, no factorisation).  Fits of a
+            # cross-mask family that hold no valid factor of their own are candidates for the
+            # representative's factor; their distance to it is measured first.
+            own_ok = drift[act] <= reuse_tol
+            cand = act[(repl[act] >= 0) & ~no_alias[act] & ~own_ok]
+            dist_c = (_pair_dist(bf, prob, np.stack([cand, repl[cand]], 1), n, ld, st)
+                      if cand.size else np.zeros(0))
+            rest = act[~np.isin(act, cand)]
+            keep = rest[drift[rest] <= reuse_tol]
+            form = rest[drift[rest] > reuse_tol]
             reps = {}
             dup = []
             for k in form:
@@ -775,7 +819,23 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                 for k, rk, dist_k in shared:
                     dup.append((k, rk))
                     drift[k] = dist_k
-            _syrk(d, bf, uniq, nsteps, ntile1, stats, st, rows=rows)
+            # candidates: alias while (distance to the representative) + (the representative's
+            # own drift after this iteration's decision) <= xmask_tol, else form their own
+            ok = dist_c + drift[repl[cand]] <= xmask_tol
+            ali = cand[ok]
+            fail = cand[~ok]
+            for k in fail:
+                key = (reqs[k].mask, reqs[k].resp, beta[k].tobytes())
+                rk = reps.setdefault(key, k)
+                if rk != k:
+                    dup.append((k, rk))
+                else:
+                    uniq = np.append(uniq, np.int32(k))
+            drift[fail] = 0.0
+            form = np.concatenate([form, fail])
+            alias[:] = -1
+            alias[ali] = repl[ali]
+            _syrk(d, bf, np.sort(uniq).astype(np.int32), nsteps, ntile1, stats, st, rows=rows)
             gram_comp[uniq] = True
             for k, rk in dup:
                 bf.H[k].copy_(bf.H[rk])
@@ -784,6 +844,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
             if stats is not None:
                 stats.gram_fits += int(uniq.size)
                 stats.reused += int(keep.size)
+                stats.aliased += int(ali.size)
         t0 = tick("it_gram", t0)
         bf.delta[:B].zero_()
         if const_hess:
@@ -794,6 +855,14 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         _lib.call("sglm_chol_solve_mixed", _p(bf.H), P, _p(fits_d), int(order.size), int(nref),
                   _p(bf.gtot), _p(bf.dshift), _p(bf.delta), _p(bf.info), _p(bf.frozen), B,
                   _p(bf.cwork), st)
+        if not const_hess and ali.size:
+            # the representatives' factors are complete: solve the aliased fits on them
+            src = repl[ali]
+            al_d = torch.from_numpy(np.stack([ali, src]).astype(np.int32)).to(dev)
+            rscale_d[:ali.size].copy_(torch.from_numpy((rows[src] / rows[ali]).astype(np.float32)))
+            _lib.call("sglm_chol_solve_alias", _p(bf.H), P, _p(al_d[0]), _p(al_d[1]),
+                      int(ali.size), _p(bf.gtot), _p(rscale_d), _p(bf.delta), _p(bf.frozen), B,
+                      _p(bf.cwork), st)
         factored = True
         d.eta(bf.delta[:B], bf.deta)
         delta_h[:B].copy_(bf.delta[:B], non_blocking=True)
@@ -869,6 +938,14 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         # forms a fresh Hessian for that fit instead of stopping it
         if not const_hess:
             drift[act[ls_fail & ~fresh]] = np.inf
+            # a fit whose step on the representative's factor failed, or contracted slowly,
+            # forms its own Hessians from here on
+            was_alias = alias[act] >= 0
+            slow = was_alias & (relv > XMASK_SLOW * prev_rel[act]) & (relv > tol)
+            drop = was_alias & (ls_fail | slow)
+            no_alias[act[drop]] = True
+            if stats is not None:
+                stats.stops["alias_dropped"] += int(np.sum(drop))
         stop_tol = ~ls_fail & (relv <= tol)
         # stagnation (the f32 noise floor): a step no better than half the previous one, judged
         # only on steps taken with a fresh Hessian -- a kept factor contracts by up to
@@ -914,10 +991,41 @@ IRLS_GROUPS = int(__import__("os").environ.get("SGLM_IRLS_GROUPS", "2"))
 IRLS_GROUP_MIN = int(__import__("os").environ.get("SGLM_IRLS_GROUP_MIN", "24"))            # fits per group below which the batch is not split
 
 
-def _partition(reqs: List[FitReq], ngroups: int) -> List[List[int]]:
-    """Fit indices per group: whole row masks go to the lighter group (fits of one mask share
-    their first Hessian and the lambda-path Hessian sharing); with fewer masks than groups the
-    largest mask's fits are dealt alternately in penalty order."""
+def _family_key(r: FitReq, rows: float):
+    """Cross-mask family of a fit (see HESS_XMASK_TOL): response, penalty per row, intercept."""
+    if r.lam > 0 and rows > 0:
+        return (r.resp, float("%.12g" % (r.lam / rows)), bool(r.fit_intercept))
+    return None
+
+
+GROUP_SPLIT = __import__("os").environ.get("SGLM_GROUP_SPLIT", "contig")
+
+
+def _partition(reqs: List[FitReq], ngroups: int, rows=None) -> List[List[int]]:
+    """Fit indices per group.  With cross-mask families (log link, HESS_XMASK_TOL > 0) the
+    unit is a family -- a penalty's split fits and refit, which share the refit's factor --
+    and the families, in penalty order, are cut into contiguous groups (lambda-neighbours share
+    Grams) or dealt in snake order (SGLM_GROUP_SPLIT=snake).  Otherwise whole row masks go to
+    the lighter group (fits of one mask share their first Hessian and the lambda-path Hessian
+    sharing); with fewer masks than groups the largest mask's fits are dealt alternately in
+    penalty order."""
+    if (rows is not None and HESS_XMASK_TOL > 0 and reqs[0].family == FAM_TWEEDIE_LOG):
+        fams = {}
+        for i, r in enumerate(reqs):
+            fams.setdefault(_family_key(r, rows[i]) or ("solo", i), []).append(i)
+        units = sorted(fams.values(), key=lambda u: (reqs[u[0]].lam / max(rows[u[0]], 1.0), u[0]))
+        if len(units) >= ngroups:
+            out = [[] for _ in range(ngroups)]
+            if GROUP_SPLIT == "snake":
+                for q, u in enumerate(units):
+                    g = q % (2 * ngroups)
+                    out[g if g < ngroups else 2 * ngroups - 1 - g] += u
+            else:
+                cut = np.linspace(0, len(units), ngroups + 1).round().astype(int)
+                for g in range(ngroups):
+                    for u in units[cut[g]:cut[g + 1]]:
+                        out[g] += u
+            return [sorted(o) for o in out if o]
     by_mask = {}
     for i, r in enumerate(reqs):
         by_mask.setdefault(r.mask, []).append(i)
@@ -950,7 +1058,8 @@ def irls_scored(prob: Problem, reqs: List[FitReq], sets: np.ndarray,
     fresp = [r.resp for r in reqs]
     # groups pay off when each still fills the chip with Gram work (C4 on one GPU: 120 fits);
     # a rank's share at 8 GPUs (~15 fits) runs as one group
-    parts = (_partition(reqs, ng) if ng > 1 and len(reqs) >= IRLS_GROUP_MIN * ng
+    rows = [prob.mask_stats(r.resp, r.mask)[0] for r in reqs]
+    parts = (_partition(reqs, ng, rows) if ng > 1 and len(reqs) >= IRLS_GROUP_MIN * ng
              else [list(range(len(reqs)))])
     if len(parts) == 1:
         res, eta = irls(prob, reqs, stats=stats)
@@ -1007,18 +1116,31 @@ def irls_scored(prob: Problem, reqs: List[FitReq], sets: np.ndarray,
         if stats is not None and sg is not None:
             stats.syrk_events += sg.syrk_events
             stats.fit_iters += sg.fit_iters
-            stats.newton_iters = max(stats.newton_iters, sg.newton_iters)
             stats.gram_fits += sg.gram_fits
             stats.gram_fit_iters += sg.gram_fit_iters
             stats.reused += sg.reused
+            stats.aliased += sg.aliased
             stats.alg_flop += sg.alg_flop
             for k, v in sg.stops.items():
                 stats.stops[k] += v
             for k, v in sg.phases.items():
                 stats.phases[k] = stats.phases.get(k, 0.0) + v
+    if stats is not None:       # the groups iterate concurrently: the batch's count is the max
+        stats.newton_iters += max(sg.newton_iters for _, _, sg in out if sg is not None)
     for s_ in streams:
         main.wait_stream(s_)
     return res, sums
+
+
+def _pair_dist(bf, prob, pairs, n, ld, st):
+    """max over the rows of fit a's mask of |eta_a - eta_b| for each (a, b) in pairs (host)."""
+    dev = bf.eta.device
+    pd_ = torch.from_numpy(np.ascontiguousarray(pairs, dtype=np.int32).reshape(-1)).to(dev)
+    fm = torch.from_numpy(np.asarray(bf.fit_mask, dtype=np.int32)).to(dev)
+    out = torch.empty(len(pairs), dtype=torch.float32, device=dev)
+    _lib.call("sglm_eta_pair_absmax", n, ld, len(pairs), _p(pd_), _p(prob.M), _p(fm),
+              _p(bf.eta), _p(out), st)
+    return out.cpu().numpy().astype(np.float64)
 
 
 def _share_grams(bf, prob, reqs, lam, uniq, tol, n, ld, st):
@@ -1035,13 +1157,7 @@ def _share_grams(bf, prob, reqs, lam, uniq, tol, n, ld, st):
         return uniq, []
     pairs = np.array([(c[i], c[i + 1]) for c in chains for i in range(len(c) - 1)],
                      dtype=np.int32)
-    dev = bf.eta.device
-    pd_ = torch.from_numpy(pairs.reshape(-1)).to(dev)
-    fm = torch.from_numpy(np.asarray(bf.fit_mask, dtype=np.int32)).to(dev)
-    out = torch.empty(len(pairs), dtype=torch.float32, device=dev)
-    _lib.call("sglm_eta_pair_absmax", n, ld, len(pairs), _p(pd_), _p(prob.M), _p(fm),
-              _p(bf.eta), _p(out), st)
-    dist = out.cpu().numpy().astype(np.float64)
+    dist = _pair_dist(bf, prob, pairs, n, ld, st)
     shared, drop, q = [], set(), 0
     for c in chains:
         rep, acc = c[0], 0.0

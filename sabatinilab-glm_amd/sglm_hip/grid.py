@@ -211,6 +211,21 @@ def rank_share(plan, groups: Sequence[dict], rank: int, world: int):
     specs, gm, counts, table, roll_list = plan
     if world > 1 and SHARD_PLAN == "round_robin":
         return shard_indices(len(table), rank, world)
+    units = {}
+    for i, t in enumerate(table):
+        units.setdefault((t[0], t[1]), []).append(i)
+    fam = (world > 1 and SHARD_PLAN == "mask_major" and E.HESS_XMASK_TOL > 0
+           and len(units) >= world
+           and all(o.kind == "irls" and o.family == E.FAM_TWEEDIE_LOG
+                   for g in groups for o in g["objectives"]))
+    if fam:
+        # whole parameters (a penalty's split fits + refit: one cross-mask family, solved on
+        # the refit's factor) per rank, in snake order of the penalty list, cut into
+        # contiguous runs of near-equal count
+        njs = [len(g["objectives"]) for g in groups]
+        order = sorted(units, key=lambda u: (snake(u[1], njs[u[0]]), u[0]))
+        cuts = np.linspace(0, len(order), world + 1).round().astype(int)
+        return sorted(i for u in order[cuts[rank]:cuts[rank + 1]] for i in units[u])
     if world > 1:
         njs = [len(g["objectives"]) for g in groups]
         keys = [(t[3], t[4], snake(t[1], njs[t[0]]), t[0], t[1]) for t in table]
