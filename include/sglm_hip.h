@@ -122,15 +122,6 @@ int sglm_syrk_masked(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, const
 int sglm_pack_bits(const uint16_t* Xb, int64_t ld, int32_t P, uint32_t* bits,
                    int32_t* nonbinary, sglm_stream_t stream);
 
-/* sglm_syrk(_masked) for a 0/1 design in bit-plane form (v3: 16x fewer bytes per K-step,
- * the 1M x 2048 design is 256 MB and stays in the Infinity Cache).  Row lists, when given,
- * must consist of whole aligned 64-row blocks (8 consecutive groups 8b..8b+7).  Bitwise
- * identical to sglm_syrk on the same design. */
-int sglm_syrk_bits(const uint32_t* Xbits, int64_t ld, int32_t P, int64_t n, const float* W,
-                   const int32_t* fits, int32_t nact, int32_t splits, float* H, void* work,
-                   const int32_t* row_groups, const int64_t* group_offset,
-                   const int32_t* group_count, sglm_stream_t stream);
-
 /* Row-compacted bit-plane design (Gram v6).  Output row k is X[.][rows[k]] (rows == NULL:
  * row k) for k < nrows, zero up to the next multiple of 64.  Layout K-step-major:
  * out[(blk * P + a) * 2 + {0,1}] = the two 32-row words of 64-row block blk of predictor a;
@@ -205,15 +196,6 @@ int sglm_enet_cd_grouped(const double* Q, int32_t p, const int32_t* wg_fits, int
                          int32_t fpw, const int32_t* wg_q, const double* q, const double* l1,
                          const double* l2, int32_t max_sweeps, double tol, double* w,
                          int32_t* sweeps, sglm_stream_t stream);
-
-/* Development entries: a specific bf16 Gram variant (1 = register-staged, 2 = LDS-DMA
- * staged; sglm_syrk uses the default), same arguments as sglm_syrk. */
-int sglm_syrk_v1(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, const float* W,
-                 const int32_t* fits, int32_t nact, int32_t splits, float* H, void* work,
-                 sglm_stream_t stream);
-int sglm_syrk_variant(int32_t variant, const uint16_t* Xb, int64_t ld, int32_t P, int64_t n,
-                      const float* W, const int32_t* fits, int32_t nact, int32_t splits,
-                      float* H, void* work, sglm_stream_t stream);
 
 /* Same contraction from the f32 design (v_mfma_f32_32x32x2_f32, exact f32 products) for
  * designs that are not bf16-exact, where the Gram itself must be accurate (coordinate
@@ -298,19 +280,6 @@ int sglm_score_sums(int32_t family, float power, int64_t n, int64_t ld, int32_t 
                     const float* eta, const float* Y, const uint8_t* M,
                     const int32_t* fit_resp, const int32_t* sets, double* out, void* work,
                     sglm_stream_t stream);
-
-/* Lasso / ElasticNet by Gram-space cyclic coordinate descent (float64), one workgroup per
- * fit in fits[].  H: the augmented Gram of sglm_syrk formed with W = mask (ones column at
- * index p); c[k]: X^T (m y) (sglm_xtr of R = m y); l1[k] = alpha rho n_k,
- * l2[k] = alpha (1 - rho) n_k.  Stops when max|dw| <= tol * max|w| over a sweep or after
- * max_sweeps.  coef[k][0..p) = w, coef[k][p] = intercept.  p <= 4096.
- * Replaces sklearn cd_fast.enet_coordinate_descent behind backend/sglm.py:106-110. */
-size_t sglm_enet_work_bytes(int32_t p, int32_t nact);
-int sglm_enet_cd(const float* H, int32_t P, int32_t p, const int32_t* fits, int32_t nact,
-                 const double* c, const double* l1, const double* l2,
-                 const int32_t* fit_intercept, int32_t max_sweeps, double tol, double* coef,
-                 int32_t* sweeps, void* work, sglm_stream_t stream);
-
 
 /* --- session preprocessing (lynne_pp.preprocess_lynne, lynne_pp.py:217-249) -------------
  * Input: SGLM_PREP_NIN float64 columns of n rows, column c at in + c * ld_in, in the order of

@@ -4,31 +4,20 @@
 // (backend/sglm.py:241): sklearn's X^T diag(h) X for newton-cholesky / the X^T X of Ridge's
 // cholesky (_ridge.py:201-213) and, for lbfgs, the 2 GEMVs per evaluation it stands in for.
 //
-// Geometry (gfx950):
-//   * one workgroup = one 256x256 output tile (ti <= tj, upper triangle) of one fit,
-//     512 threads = 8 waves in a 2 (rows) x 4 (cols) grid, each wave 128 x 64 =
-//     4 x 2 tiles of v_mfma_f32_32x32x16_bf16 (128 f32 accumulators per lane);
-//   * K loop over rows of X in steps of BK = 32 (two 16-deep MFMA sub-steps);
-//   * X is feature-major, so a tile's K-slice of predictor a is 64 contiguous bytes:
-//     A panel = X[a0..a0+255][i..i+31] (unscaled), B panel = w_i * X[b0..b0+255][i..i+31]
-//     (scaled once while staging, in registers, then rounded to bf16);
-//   * LDS: 2 stages x 2 panels x 256 predictors x 80-byte rows (64 B + 16 B pad);
-//     the 20-dword row stride makes the 16-lane ds_read_b128 groups conflict-free
-//     (5r mod 16 is a bijection);
-//   * register-staged double buffering: tile t+1's global loads are issued before the
-//     MFMAs of tile t and written to the other LDS stage after them; one barrier per step.
-//   * optional split-K over rows (blockIdx.y) into fixed-order f32 slabs.
+// Three forms, all v_mfma on gfx950, upper triangle by 256- (v2) or 128-blocks (v6, f32):
+//   * v6 (sglm_syrk_cbits): 0/1 event designs, per-mask row-compacted bit-planes expanded to
+//     bf16 in registers, one wave per 128x128 block, no LDS -- the C4 production path;
+//   * v2 (sglm_syrk / sglm_syrk_masked): any bf16 design, 256x256 tiles of 8 waves staged
+//     through LDS by LDS-DMA, optional 8-row-group lists that skip rows outside a mask;
+//   * f32 (sglm_syrk_f32): exact f32 products for designs that are not bf16-representable,
+//     where the Gram itself must be exact (coordinate descent, Gaussian closed forms).
+// Optional split-K over rows into fixed-order f32 slabs (deterministic).
 #include "common.h"
 
 
 namespace sglm {
 
-constexpr int kBM = 256;       // output tile edge
-constexpr int kBK = 32;        // rows of X per K-step
-constexpr int kThreads = 512;
-constexpr int kRow = 40;       // bf16 elements per LDS predictor row (32 + 8 pad) = 80 B
-constexpr int kPanel = kBM * kRow;          // elements per panel
-constexpr int kStage = 2 * kPanel;          // A + B
+constexpr int kBM = 256;       // v2 output tile edge (slab reduction granularity)
 
 __device__ __forceinline__ void tile_coords(int t, int nt, int& ti, int& tj) {
     // enumerate upper-triangular tiles row by row: (0,0),(0,1)..(0,nt-1),(1,1)...
@@ -356,11 +345,18 @@ __global__ void __launch_bounds__(512) syrk2_kernel(
 }
 }  // namespace sglm
 
-// Development entry: run a specific Gram kernel variant (1 = register-staged, 2 = LDS-DMA).
 static int syrk2_launch(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, const float* W,
                         const int32_t* fits, int32_t nact, int32_t splits, float* H, void* work,
                         const int32_t* grp, const int64_t* grp_off, const int32_t* grp_cnt,
                         sglm_stream_t stream);
+
+// All rows (w carries the mask): the v2 LDS-DMA kernel without row-group lists.
+extern "C" int sglm_syrk(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, const float* W,
+                         const int32_t* fits, int32_t nact, int32_t splits, float* H, void* work,
+                         sglm_stream_t stream) {
+    return syrk2_launch(Xb, ld, P, n, W, fits, nact, splits, H, work, nullptr, nullptr, nullptr,
+                        stream);
+}
 
 extern "C" int sglm_syrk_masked(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n,
                                 const float* W, const int32_t* fits, int32_t nact,
@@ -382,7 +378,7 @@ static int syrk2_launch(const uint16_t* Xb, int64_t ld, int32_t P, int64_t n, co
     if (nact <= 0) return SGLM_OK;
     if (!Xb || !W || !fits || !H || P % 256 || ld % 256 || n > ld || splits < 1 ||
         (splits > 1 && !work)) {
-        set_error("sglm_syrk_variant: bad args");
+        set_error("sglm_syrk: bad args");
         return SGLM_EINVAL;
     }
     const int nt = P / 256;

@@ -32,8 +32,6 @@ SIGNATURES = {
     "sglm_syrk_masked": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp,
                                    _vp, _vp]),
     "sglm_pack_bits": (C.c_int, [_vp, _i64, _i32, _vp, _vp, _vp]),
-    "sglm_syrk_bits": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp,
-                                 _vp, _vp]),
     "sglm_pack_bits_rows": (C.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _vp, _vp]),
     "sglm_compact_rbits": (C.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _vp]),
     "sglm_compact_bits": (C.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _vp]),
@@ -50,9 +48,6 @@ SIGNATURES = {
     "sglm_enet_cd_fits_per_wg": (_i32, [_i32]),
     "sglm_enet_cd_grouped": (C.c_int, [_vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _i32,
                                        C.c_double, _vp, _vp, _vp]),
-    "sglm_syrk_v1": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
-    "sglm_syrk_variant": (C.c_int, [_i32, _vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _vp,
-                                    _vp]),
     "sglm_syrk_f32": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
     "sglm_chol_work_bytes": (_sz, [_i32, _i32]),
     "sglm_chol_solve_ex": (C.c_int, [_vp, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _i32,
@@ -71,9 +66,6 @@ SIGNATURES = {
     "sglm_eta_pair_absmax": (C.c_int, [_i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "sglm_score_sums": (C.c_int, [_i32, _f32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
                                   _vp, _vp]),
-    "sglm_enet_work_bytes": (_sz, [_i32, _i32]),
-    "sglm_enet_cd": (C.c_int, [_vp, _i32, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _i32, C.c_double,
-                               _vp, _vp, _vp, _vp]),
     "sglm_prep_work_bytes": (_sz, [_i64]),
     "sglm_prep_session": (C.c_int, [_vp, _i64, _i64, _i32, _vp, _i64, _vp, _vp]),
 }

@@ -44,7 +44,6 @@ X_BF16, X_F32 = 0, 1
 COL_PAD = 256
 ROW_PAD = 256
 ARMIJO_SIGMA = 2.0 ** -11      # sklearn _newton_solver.py:214
-SYRK_BITS = True               # use the bit-plane Gram (v3) for 0/1 designs
 XTR_BITS = True                # X^T R on the MFMA from compacted bit-planes for 0/1 designs
 ETA_BITS = True                # eta on the MFMA from row-major bit-planes for 0/1 designs
 SYRK_CBITS = True              # ... and its row-compacted register-only form (v6) when fits
@@ -68,7 +67,7 @@ HESS_SHARE_TOL = float(__import__("os").environ.get("SGLM_HESS_SHARE_TOL", "0.37
 # the representative's; the generalized eigenvalues of (H_k, c_k H_rep) measured at the
 # solutions of the C3 grid lie in [0.92, 1.10] (contraction <= 0.1).  A fit whose aliased
 # step fails the line search or contracts slowly leaves the family for good.  0 disables.
-HESS_XMASK_TOL = float(__import__("os").environ.get("SGLM_HESS_XMASK_TOL", "0.5"))
+HESS_XMASK_TOL = float(__import__("os").environ.get("SGLM_HESS_XMASK_TOL", "0.75"))
 XMASK_SLOW = 0.7                # aliased-step contraction above which a fit leaves its family
 # Batch compaction: once at most COMPACT_FRAC of the batch is still iterating (and at least
 # COMPACT_MIN fits have stopped), the active fits are moved to the front slots.
@@ -1207,9 +1206,6 @@ def _syrk(d: Design, bf, fits: np.ndarray, nsteps: int, ntile1: int, stats, st, 
             gcnt = torch.from_numpy(prob.group_count[bf.fit_mask]).to(d.device)
             _lib.call("sglm_syrk_masked", _p(d.xb), d.ld, d.P, d.n, _p(bf.W), _p(fits_d), nact,
                       splits, _p(bf.H), _p(work), _p(prob.groups), _p(goff), _p(gcnt), st)
-        elif d.xbits is not None and SYRK_BITS:
-            _lib.call("sglm_syrk_bits", _p(d.xbits), d.ld, d.P, d.n, _p(bf.W), _p(fits_d),
-                      nact, splits, _p(bf.H), _p(work), None, None, None, st)
         else:
             _lib.call("sglm_syrk", _p(d.xb), d.ld, d.P, d.n, _p(bf.W), _p(fits_d), nact,
                       splits, _p(bf.H), _p(work), st)

@@ -298,44 +298,6 @@ def test_syrk_masked_row_groups(engine, torch_mod):
             assert torch.max(torch.abs(a - b)).item() <= 1e-6 * max(1.0, torch.max(torch.abs(a)).item()), (splits, k)
 
 
-def test_syrk_bits_bitwise_equal_to_bf16(engine, torch_mod):
-    """Bit-plane Gram (v3) == LDS-DMA bf16 Gram (v2), bitwise, plain and masked, with splits."""
-    torch = torch_mod
-    from sglm_hip import _lib, synth
-    s = synth.make(N=30000, m=13, L=6, rho=0.1, seed=14)
-    d = engine.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
-    assert d.xbits is not None
-    rng = np.random.default_rng(15)
-    masks = [np.repeat(rng.random(300) >= 0.25, 100).astype(np.uint8), np.ones(s.N, np.uint8)]
-    prob = engine.Problem(d, [s.y], masks)
-    B = 2
-    W = torch.zeros((B, d.ld), dtype=torch.float32, device="cuda")
-    for k in range(B):
-        W[k, : s.N] = torch.from_numpy(masks[k] * rng.random(s.N).astype(np.float32))
-    fits = torch.tensor([0, 1], dtype=torch.int32, device="cuda")
-    goff = torch.from_numpy(prob.group_offset).cuda()
-    gcnt = torch.from_numpy(prob.group_count).cuda()
-    up = torch.triu(torch.ones((d.P, d.P), dtype=torch.bool, device="cuda"))
-    for splits in (1, 3):
-        wk = torch.empty(max(_lib.query("sglm_syrk_work_bytes", d.P, B, splits), 16),
-                         dtype=torch.uint8, device="cuda")
-        Href = torch.zeros((B, d.P, d.P), dtype=torch.float32, device="cuda")
-        _lib.call("sglm_syrk_variant", 2, d.xb.data_ptr(), d.ld, d.P, d.n, W.data_ptr(),
-                  fits.data_ptr(), B, splits, Href.data_ptr(), wk.data_ptr(), 0)
-        for masked in (False, True):
-            Hb = torch.zeros_like(Href)
-            _lib.call("sglm_syrk_bits", d.xbits.data_ptr(), d.ld, d.P, d.n, W.data_ptr(),
-                      fits.data_ptr(), B, splits, Hb.data_ptr(), wk.data_ptr(),
-                      prob.groups.data_ptr() if masked else None,
-                      goff.data_ptr() if masked else None, gcnt.data_ptr() if masked else None, 0)
-            for k in range(B):
-                if masked:      # skipped blocks change the f32 summation order only
-                    err = torch.max(torch.abs(Hb[k][up] - Href[k][up])).item()
-                    assert err <= 1e-6 * torch.max(torch.abs(Href[k][up])).item(), (splits, k)
-                else:
-                    assert torch.equal(Hb[k][up], Href[k][up]), (splits, k)
-
-
 def _unpack_cbits(bits, P, nrows):
     """Host decode of the v6 compact layout -> (nrows, P) 0/1 matrix."""
     nblk = max(1, (nrows + 63) // 64)
@@ -402,7 +364,7 @@ def test_syrk_cbits_compacted_gram(engine, torch_mod):
     blk = np.triu(np.ones((d.P, d.P), dtype=bool))         # what the consumers read
     Href = torch.zeros((1, d.P, d.P), dtype=torch.float32, device="cuda")
     wk1 = torch.empty(16, dtype=torch.uint8, device="cuda")
-    _lib.call("sglm_syrk_variant", 2, d.xb.data_ptr(), d.ld, d.P, d.n, W.data_ptr(),
+    _lib.call("sglm_syrk", d.xb.data_ptr(), d.ld, d.P, d.n, W.data_ptr(),
               fits.data_ptr(), 1, 1, Href.data_ptr(), wk1.data_ptr(), 0)
     for splits in (1, 4):
         wk = torch.empty(max(_lib.query("sglm_syrk_work_bytes", d.P, B, splits), 16),
