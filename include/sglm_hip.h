@@ -84,13 +84,16 @@ int sglm_pack_design(const void* src, int32_t src_is_f64, int64_t n, int32_t p,
 int sglm_gemv_eta(const void* X, int32_t xtype, int64_t ld, int32_t P, int64_t n,
                   const float* beta, int32_t B, float* eta, sglm_stream_t stream);
 
-/* Link/variance update.  For fit k with response r = fit_resp[k], mask m = fit_mask[k]:
+/* Link/variance update over B fits: launch row q is fit slot k = slots[q] (q when slots is
+ * NULL).  With response r = fit_resp[k], mask m = fit_mask[k]:
  *   W[k][i] = M[m][i] * d2loss/deta2,   R[k][i] = M[m][i] * dloss/deta,   rows i < n.
- * Rows n <= i < ld are written as 0. */
+ * Rows n <= i < ld are written as 0.  R (f32 per slot) and Rp may each be NULL (not both):
+ * Rp receives R as three bf16 pieces hi + mid + lo == R, bf16 [3][Bp][ld] with
+ * Bp = ceil(B/32)*32, row q = launch row -- the operand of sglm_xtr_bits_packed. */
 int sglm_link_update(int32_t family, float power, int64_t n, int64_t ld, int32_t B,
-                     const float* eta, const float* Y, const uint8_t* M,
+                     const int32_t* slots, const float* eta, const float* Y, const uint8_t* M,
                      const int32_t* fit_resp, const int32_t* fit_mask, float* W, float* R,
-                     sglm_stream_t stream);
+                     void* Rp, sglm_stream_t stream);
 
 /* G[k][a] = sum_i X[a][i] * R[k][i] (float64 out; f32 MFMA partial sums, fixed-order
  * float64 reduction over row chunks).  `work`: sglm_xtr_work_bytes(P, B, n). */
@@ -160,12 +163,14 @@ int sglm_pack_bits_t(const uint16_t* Xb, int64_t ld, int32_t P, uint32_t* out,
                      int32_t* nonbinary, sglm_stream_t stream);
 
 /* eta[k] = X beta[k] (as sglm_gemv_eta) for a 0/1 design given as sglm_pack_bits_t planes:
- * beta split into three bf16 pieces (exact), bf16 MFMA with f32 accumulation.  Writes all
- * ld rows of eta (padding rows: 0).  work: sglm_eta_bits_work_bytes(P, B) bytes.
+ * beta split into three bf16 pieces (exact), bf16 MFMA with f32 accumulation, for the B slots
+ * k = slots[q] (q < B; all k < B when slots is NULL).  Writes all ld rows of eta (padding
+ * rows: 0).  work: sglm_eta_bits_work_bytes(P, B) bytes.
  * Replaces X @ coef (backend/sglm.py:347 -> sklearn glm.py:350). */
 size_t sglm_eta_bits_work_bytes(int32_t P, int32_t B);
 int sglm_gemv_eta_bits(const uint32_t* rbits, int64_t ld, int32_t P, const float* beta,
-                       int32_t B, float* eta, void* work, sglm_stream_t stream);
+                       int32_t B, const int32_t* slots, float* eta, void* work,
+                       sglm_stream_t stream);
 
 /* g[k] = X^T R[k] (as sglm_xtr, float64 out) for a 0/1 design given as its identity-row
  * compacted planes (sglm_compact_bits with rows = NULL, nrows = n): R split into three bf16
@@ -174,6 +179,14 @@ int sglm_gemv_eta_bits(const uint32_t* rbits, int64_t ld, int32_t P, const float
 size_t sglm_xtr_bits_work_bytes(int32_t P, int32_t B, int64_t ld);
 int sglm_xtr_bits(const uint32_t* cbits, int64_t ld, int32_t P, int64_t n, const float* R,
                   int32_t B, double* G, void* work, sglm_stream_t stream);
+
+/* sglm_xtr_bits with R already split into the packed bf16 pieces that sglm_link_update writes
+ * (Rp: [3][Bp][ld]): G[slots[q]] = X^T R_q for q < B (G[q] when slots is NULL).
+ * work: sglm_xtr_bits_packed_work_bytes(P, Bmax, ld), valid for every call with B <= Bmax. */
+size_t sglm_xtr_bits_packed_work_bytes(int32_t P, int32_t B, int64_t ld);
+int sglm_xtr_bits_packed(const uint32_t* cbits, int64_t ld, int32_t P, int64_t n,
+                         const void* Rp, int32_t B, const int32_t* slots, double* G,
+                         void* work, sglm_stream_t stream);
 
 /* Shared-Gram elastic net for many fits per mask (multi-response lambda paths):
  * sglm_center_gram: Q[m] (float64 p x p) = G_xx - g g^T / n (center) or G_xx from the
@@ -237,25 +250,27 @@ int sglm_chol_solve_alias(const float* H, int32_t P, const int32_t* fits, const 
                           int32_t nact, const double* g, const float* rscale, float* delta,
                           const uint8_t* frozen, int32_t B, void* work, sglm_stream_t stream);
 
-/* Line search: out[k][j] = sum_i M[m][i] * loss(y_i, eta_i + t[j] * deta_i) (float64),
- * for j < T, fits k < B.  `work`: sglm_rowsum_work_bytes(B, T, n). */
+/* Line search: out[q][j] = sum_i M[m][i] * loss(y_i, eta_i + t[j] * deta_i) (float64),
+ * for j < T, over fit slot k = slots[q] (q when slots is NULL), q < B.
+ * `work`: sglm_rowsum_work_bytes(B, T, n). */
 size_t sglm_rowsum_work_bytes(int32_t B, int32_t T, int64_t n);
 int sglm_loss_trials(int32_t family, float power, int64_t n, int64_t ld, int32_t B,
-                     const float* eta, const float* deta, const float* Y, const uint8_t* M,
+                     const int32_t* slots, const float* eta, const float* deta, const float* Y, const uint8_t* M,
                      const int32_t* fit_resp, const int32_t* fit_mask, const float* t,
                      int32_t T, double* out, void* work, sglm_stream_t stream);
 
-/* sglm_loss_trials plus dmax[k] = max over the rows of mask fit_mask[k] of |deta[k][i]| (B
+/* sglm_loss_trials plus dmax[q] = max over the rows of mask fit_mask[k] of |deta[k][i]| (B
  * floats, zeroed by the call): the step's predictor drift per unit step length, returned with
  * the trial losses so that the host needs one round trip per Newton iteration. */
 int sglm_loss_trials_max(int32_t family, float power, int64_t n, int64_t ld, int32_t B,
-                         const float* eta, const float* deta, const float* Y, const uint8_t* M,
+                         const int32_t* slots, const float* eta, const float* deta, const float* Y, const uint8_t* M,
                          const int32_t* fit_resp, const int32_t* fit_mask, const float* t,
                          int32_t T, double* out, float* dmax, void* work, sglm_stream_t stream);
 
-/* eta[k][i] += step[k] * deta[k][i]  (host-chosen step per fit, device array). */
-int sglm_eta_axpy(int64_t n, int64_t ld, int32_t B, const float* step, const float* deta,
-                  float* eta, sglm_stream_t stream);
+/* eta[k][i] += step[q] * deta[k][i], k = slots[q] (q when slots is NULL), q < B
+ * (host-chosen step per fit, device array). */
+int sglm_eta_axpy(int64_t n, int64_t ld, int32_t B, const int32_t* slots, const float* step,
+                  const float* deta, float* eta, sglm_stream_t stream);
 
 /* sglm_eta_axpy plus dmax[k] = max over the rows of mask fit_mask[k] of |step[k] d_eta[k][i]|
  * (B floats, zeroed by the call): the per-step drift of the linear predictor that bounds the

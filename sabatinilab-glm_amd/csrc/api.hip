@@ -127,32 +127,48 @@ __global__ void __launch_bounds__(256) eta_kernel(const TX* __restrict__ X, int6
 }
 
 // ------------------------------------------------------------------------------ link
+// Row y of the launch is fit slot k = slots[y] (all slots when slots is null).  W and the
+// optional f32 R are written per slot; Rp (optional) receives R as three bf16 pieces
+// hi + mid + lo == R in the packed operand layout of the gradient kernel, row y of each piece
+// plane (Bp rows per plane): the split is fused here instead of a separate pass over R.
 __global__ void __launch_bounds__(256) link_kernel(int32_t family, float power, int64_t n,
-                                                   int64_t ld, const float* __restrict__ eta,
+                                                   int64_t ld, const int32_t* __restrict__ slots,
+                                                   const float* __restrict__ eta,
                                                    const float* __restrict__ Y,
                                                    const uint8_t* __restrict__ M,
                                                    const int32_t* __restrict__ fit_resp,
                                                    const int32_t* __restrict__ fit_mask,
-                                                   float* __restrict__ W, float* __restrict__ R) {
-    const int k = blockIdx.y;
+                                                   float* __restrict__ W, float* __restrict__ R,
+                                                   __bf16* __restrict__ Rp, int32_t Bp) {
+    const int y = blockIdx.y;
+    const int k = slots ? slots[y] : y;
     const float* e = eta + (int64_t)k * ld;
-    const float* y = Y + (int64_t)fit_resp[k] * ld;
+    const float* yv = Y + (int64_t)fit_resp[k] * ld;
     const uint8_t* m = M + (int64_t)fit_mask[k] * ld;
     float* w = W + (int64_t)k * ld;
-    float* r = R + (int64_t)k * ld;
+    float* r = R ? R + (int64_t)k * ld : nullptr;
+    const int64_t plane = (int64_t)Bp * ld;
+    __bf16* rp = Rp ? Rp + (int64_t)y * ld : nullptr;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < ld;
          i += (int64_t)gridDim.x * 256) {
         float wi = 0.0f, ri = 0.0f;
         if (i < n) {
             const float mi = (float)m[i];
             if (mi != 0.0f) {
-                const LossOut o = half_loss(family, power, y[i], e[i]);
+                const LossOut o = half_loss(family, power, yv[i], e[i]);
                 wi = mi * o.h;
                 ri = mi * o.g;
             }
         }
         w[i] = wi;
-        r[i] = ri;
+        if (r) r[i] = ri;
+        if (rp) {
+            __bf16 hi, mid, lo;
+            split3(ri, hi, mid, lo);
+            rp[i] = hi;
+            rp[plane + i] = mid;
+            rp[2 * plane + i] = lo;
+        }
     }
 }
 
@@ -260,10 +276,11 @@ __global__ void __launch_bounds__(256) loss_trials_kernel(
     const float* __restrict__ deta, const float* __restrict__ Y, const uint8_t* __restrict__ M,
     const int32_t* __restrict__ fit_resp, const int32_t* __restrict__ fit_mask,
     const float* __restrict__ tv, int32_t T, double* __restrict__ part,
-    float* __restrict__ dmax) {
+    float* __restrict__ dmax, const int32_t* __restrict__ slots) {
     __shared__ double sh[4];
     __shared__ float shm[4];
-    const int k = blockIdx.y;
+    const int q = blockIdx.y;                       // output row
+    const int k = slots ? slots[q] : q;             // fit slot
     const int32_t nchunks = gridDim.x;
     const float* e = eta + (int64_t)k * ld;
     const float* d = deta + (int64_t)k * ld;
@@ -284,14 +301,14 @@ __global__ void __launch_bounds__(256) loss_trials_kernel(
     }
     for (int j = 0; j < T; ++j) {
         const double s = block_sum_d(acc[j], sh);
-        if (threadIdx.x == 0) part[((int64_t)k * T + j) * nchunks + blockIdx.x] = s;
+        if (threadIdx.x == 0) part[((int64_t)q * T + j) * nchunks + blockIdx.x] = s;
     }
     if (dmax) {                 // max |d_eta| over the fit's rows (Hessian drift bound)
         for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
         if ((threadIdx.x & 63) == 0) shm[threadIdx.x >> 6] = mx;
         __syncthreads();
         if (threadIdx.x == 0)
-            atomicMax(reinterpret_cast<unsigned int*>(dmax + k),
+            atomicMax(reinterpret_cast<unsigned int*>(dmax + q),
                       __float_as_uint(fmaxf(fmaxf(shm[0], shm[1]), fmaxf(shm[2], shm[3]))));
     }
 }
@@ -340,11 +357,12 @@ __global__ void __launch_bounds__(256) reduce_chunks_d(const double* __restrict_
 }
 
 __global__ void __launch_bounds__(256) eta_axpy_kernel(int64_t n, int64_t ld,
+                                                       const int32_t* __restrict__ slots,
                                                        const float* __restrict__ step,
                                                        const float* __restrict__ deta,
                                                        float* __restrict__ eta) {
-    const int k = blockIdx.y;
-    const float t = step[k];
+    const int k = slots ? slots[blockIdx.y] : blockIdx.y;
+    const float t = step[blockIdx.y];
     if (t == 0.0f) return;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * 256)
@@ -477,13 +495,15 @@ int sglm_gemv_eta(const void* X, int32_t xtype, int64_t ld, int32_t P, int64_t n
 }
 
 int sglm_link_update(int32_t family, float power, int64_t n, int64_t ld, int32_t B,
-                     const float* eta, const float* Y, const uint8_t* M,
+                     const int32_t* slots, const float* eta, const float* Y, const uint8_t* M,
                      const int32_t* fit_resp, const int32_t* fit_mask, float* W, float* R,
-                     sglm_stream_t stream) {
+                     void* Rp, sglm_stream_t stream) {
     if (B <= 0) return SGLM_OK;
-    if (!eta || !Y || !M || !fit_resp || !fit_mask || !W || !R) { set_error("sglm_link_update: null pointer"); return SGLM_EINVAL; }
+    if (!eta || !Y || !M || !fit_resp || !fit_mask || !W || (!R && !Rp)) { set_error("sglm_link_update: null pointer"); return SGLM_EINVAL; }
     dim3 grid(grid1(ld, 256, 1024), (unsigned)B);
-    link_kernel<<<grid, 256, 0, as_stream(stream)>>>(family, power, n, ld, eta, Y, M, fit_resp, fit_mask, W, R);
+    link_kernel<<<grid, 256, 0, as_stream(stream)>>>(family, power, n, ld, slots, eta, Y, M,
+                                                     fit_resp, fit_mask, W, R, (__bf16*)Rp,
+                                                     (B + 31) / 32 * 32);
     return check_launch("link_kernel");
 }
 
@@ -516,7 +536,7 @@ size_t sglm_rowsum_work_bytes(int32_t B, int32_t T, int64_t n) {
 }
 
 int sglm_loss_trials(int32_t family, float power, int64_t n, int64_t ld, int32_t B,
-                     const float* eta, const float* deta, const float* Y, const uint8_t* M,
+                     const int32_t* slots, const float* eta, const float* deta, const float* Y, const uint8_t* M,
                      const int32_t* fit_resp, const int32_t* fit_mask, const float* t,
                      int32_t T, double* out, void* work, sglm_stream_t stream) {
     if (B <= 0) return SGLM_OK;
@@ -527,7 +547,7 @@ int sglm_loss_trials(int32_t family, float power, int64_t n, int64_t ld, int32_t
     (void)ld;
     const int32_t nc = row_chunks(n);
     hipStream_t s = as_stream(stream);
-    loss_trials_kernel<<<dim3((unsigned)nc, (unsigned)B), 256, 0, s>>>(family, power, n, ld, eta, deta, Y, M, fit_resp, fit_mask, t, T, (double*)work, nullptr);
+    loss_trials_kernel<<<dim3((unsigned)nc, (unsigned)B), 256, 0, s>>>(family, power, n, ld, eta, deta, Y, M, fit_resp, fit_mask, t, T, (double*)work, nullptr, slots);
     int st = check_launch("loss_trials_kernel");
     if (st) return st;
     const int64_t rows = (int64_t)B * T;
@@ -536,7 +556,7 @@ int sglm_loss_trials(int32_t family, float power, int64_t n, int64_t ld, int32_t
 }
 
 int sglm_loss_trials_max(int32_t family, float power, int64_t n, int64_t ld, int32_t B,
-                         const float* eta, const float* deta, const float* Y, const uint8_t* M,
+                         const int32_t* slots, const float* eta, const float* deta, const float* Y, const uint8_t* M,
                          const int32_t* fit_resp, const int32_t* fit_mask, const float* t,
                          int32_t T, double* out, float* dmax, void* work, sglm_stream_t stream) {
     if (B <= 0) return SGLM_OK;
@@ -550,7 +570,7 @@ int sglm_loss_trials_max(int32_t family, float power, int64_t n, int64_t ld, int
         set_error("sglm_loss_trials_max: hipMemsetAsync failed");
         return SGLM_EHIP;
     }
-    loss_trials_kernel<<<dim3((unsigned)nc, (unsigned)B), 256, 0, s>>>(family, power, n, ld, eta, deta, Y, M, fit_resp, fit_mask, t, T, (double*)work, dmax);
+    loss_trials_kernel<<<dim3((unsigned)nc, (unsigned)B), 256, 0, s>>>(family, power, n, ld, eta, deta, Y, M, fit_resp, fit_mask, t, T, (double*)work, dmax, slots);
     int st = check_launch("loss_trials_kernel");
     if (st) return st;
     const int64_t rows = (int64_t)B * T;
@@ -558,12 +578,12 @@ int sglm_loss_trials_max(int32_t family, float power, int64_t n, int64_t ld, int
     return check_launch("reduce_chunks_d");
 }
 
-int sglm_eta_axpy(int64_t n, int64_t ld, int32_t B, const float* step, const float* deta,
-                  float* eta, sglm_stream_t stream) {
+int sglm_eta_axpy(int64_t n, int64_t ld, int32_t B, const int32_t* slots, const float* step,
+                  const float* deta, float* eta, sglm_stream_t stream) {
     if (B <= 0) return SGLM_OK;
     if (!step || !deta || !eta) { set_error("sglm_eta_axpy: null pointer"); return SGLM_EINVAL; }
     dim3 grid(grid1(n, 256, 1024), (unsigned)B);
-    eta_axpy_kernel<<<grid, 256, 0, as_stream(stream)>>>(n, ld, step, deta, eta);
+    eta_axpy_kernel<<<grid, 256, 0, as_stream(stream)>>>(n, ld, slots, step, deta, eta);
     return check_launch("eta_axpy_kernel");
 }
 

@@ -39,14 +39,17 @@ __global__ void __launch_bounds__(256) pack_bits_t_kernel(const uint16_t* __rest
     if (bad) atomicOr(nonbinary, 1);
 }
 
-// out[p][f][e] (p = 0,1,2: hi, mid, lo) for f < Bp, e < len; rows f >= B are zero
+// out[p][f][e] (p = 0,1,2: hi, mid, lo) for f < Bp, e < len; rows f >= B are zero; row f
+// holds source row rows[f] (f when rows is null)
 __global__ void __launch_bounds__(256) split3_kernel(const float* __restrict__ src, int64_t len,
                                                      int32_t B, int32_t Bp,
+                                                     const int32_t* __restrict__ rows,
                                                      __bf16* __restrict__ out) {
     const int64_t total = (int64_t)Bp * len;
     for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
          e += (int64_t)gridDim.x * 256) {
-        const float x = (e / len) < B ? src[e] : 0.0f;
+        const int64_t f = e / len;
+        const float x = f < B ? src[(rows ? (int64_t)rows[f] : f) * len + (e - f * len)] : 0.0f;
         __bf16 hi, mid, lo;
         split3(x, hi, mid, lo);
         out[e] = hi;
@@ -110,7 +113,8 @@ __device__ __forceinline__ void mmaE(const StepE& t, int h, f32x16 (&acc)[3][4])
 
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 eta_bits_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
-                const __bf16* __restrict__ Dp, int32_t Bp, int32_t B, float* __restrict__ eta) {
+                const __bf16* __restrict__ Dp, int32_t Bp, int32_t B,
+                const int32_t* __restrict__ slots, float* __restrict__ eta) {
     const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
     const int64_t row0 = (int64_t)blockIdx.x * 128;
     const int g = blockIdx.y;
@@ -157,7 +161,7 @@ eta_bits_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
         for (int j = 0; j < 16; ++j) {
             const int f = g * 32 + (j & 3) + 8 * (j >> 2) + 4 * h;
             if (f < B)
-                eta[(int64_t)f * ld + row0 + n * 32 + r] =
+                eta[(int64_t)(slots ? slots[f] : f) * ld + row0 + n * 32 + r] =
                     0.5f * ((acc[0][n][j] + acc[1][n][j]) + acc[2][n][j]);
         }
 }
@@ -165,48 +169,78 @@ eta_bits_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
 // ---------------------------------------------------------------------------------------
 // g = X^T R (the gradient, sklearn _linear_loss.py:266-330) on the MFMA for 0/1 designs.
 // A = the design's compacted bit-planes with identity rows ([ld/64][P] uint2, the Gram v6
-// layout, K = rows), B = R split into three bf16 pieces; one wave computes 128 predictors x
-// 32 fits (x 3 pieces) over one split-K slab of rows; slabs are reduced in float64 in a
-// fixed order.
+// layout, K = rows), B = R split into three bf16 pieces (exact products); one wave computes
+// kXT x 32 predictors x 32 fits over one split-K slab of rows; slabs are reduced in float64 in
+// a fixed order.  Two f32 accumulators per tile: the hi piece alone and mid + lo together
+// (the small pieces round at their own magnitude, so the sum keeps the accuracy of three
+// separate accumulators with two thirds of the registers; 8 tiles per wave still spill).
+// Workgroups are numbered so that the predictor panels of one (fit group, row slab) are
+// consecutive on one XCD (blocks are dealt round-robin over the 8 XCDs): the slab of R they
+// all read comes from that XCD's L2 instead of once per XCD from the fabric.
+constexpr int kXT = 4;              // 32-predictor tiles per wave
+
 struct StepX {
-    u32x2 a[4];          // predictor bits of the 4 tiles, one 64-row block
+    u32x2 a[kXT];        // predictor bits of the tiles, one 64-row block
     u32x4 b[3][4];       // piece x sub-step: 8 bf16 of this lane's fit
 };
 
-__device__ __forceinline__ void loadX(StepX& t, g_uint2* pa, g_uint4* pb, int32_t P,
-                                      int64_t pstride, int64_t s) {
+// Loads from a wave-uniform SGPR base + one per-lane offset + immediates (no per-lane address
+// registers): A tile m at +256 m bytes, R piece sub-step ks at +32 ks bytes.
+template <int M>
+__device__ __forceinline__ void loadA(u32x2 (&a)[kXT], uint64_t sb, uint32_t vo) {
+    a[M] = gld2s<M * 256>(sb, vo);
+    if constexpr (M + 1 < kXT) loadA<M + 1>(a, sb, vo);
+}
+template <int KS>
+__device__ __forceinline__ void loadB(u32x4 (&b)[4], uint64_t sb, uint32_t vo) {
+    b[KS] = gld4s<KS * 32>(sb, vo);
+    if constexpr (KS + 1 < 4) loadB<KS + 1>(b, sb, vo);
+}
+
+// step s: A bytes at abase + s * P * 8, piece pc of R at bbase + pc * plane + s * 128
+__device__ __forceinline__ void loadX(StepX& t, uint64_t abase, uint32_t avo, uint64_t bbase,
+                                      uint32_t bvo, uint64_t plane, int32_t P, int64_t s) {
+    loadA<0>(t.a, abase + (uint64_t)s * P * 8, avo);
 #pragma unroll
-    for (int m = 0; m < 4; ++m) t.a[m] = gld2(pa + s * P + 32 * m);
+    for (int pc = 0; pc < 3; ++pc) loadB<0>(t.b[pc], bbase + pc * plane + (uint64_t)s * 128, bvo);
+}
+
+// wait for every load in flight, then tie the step's registers (one empty asm per register,
+// after the wait, so no use of them can be scheduled before it)
+__device__ __forceinline__ void waitX(StepX& t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int m = 0; m < kXT; ++m) asm volatile("" : "+v"(t.a[m]));
 #pragma unroll
     for (int pc = 0; pc < 3; ++pc)
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) t.b[pc][ks] = gld4(pb + pc * pstride + s * 8 + 2 * ks);
+        for (int ks = 0; ks < 4; ++ks) asm volatile("" : "+v"(t.b[pc][ks]));
 }
 
-__device__ __forceinline__ void waitX(StepX& t) {
-    asm volatile("s_waitcnt vmcnt(0)"
-                 : "+v"(t.a[0]), "+v"(t.a[1]), "+v"(t.a[2]), "+v"(t.a[3]), "+v"(t.b[0][0]),
-                   "+v"(t.b[0][1]), "+v"(t.b[0][2]), "+v"(t.b[0][3]), "+v"(t.b[1][0]),
-                   "+v"(t.b[1][1]), "+v"(t.b[1][2]), "+v"(t.b[1][3]), "+v"(t.b[2][0]),
-                   "+v"(t.b[2][1]), "+v"(t.b[2][2]), "+v"(t.b[2][3])
-                 :
-                 : "memory");
-}
-
-__device__ __forceinline__ void mmaX(const StepX& t, int h, f32x16 (&acc)[4][3]) {
+__device__ __forceinline__ void mmaX(const StepX& t, int h, f32x16 (&ah)[kXT],
+                                     f32x16 (&al)[kXT]) {
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-        bf16x8 ax[4];
+        const bf16x8 b0 = __builtin_bit_cast(bf16x8, t.b[0][ks]);
+        const bf16x8 b1 = __builtin_bit_cast(bf16x8, t.b[1][ks]);
+        const bf16x8 b2 = __builtin_bit_cast(bf16x8, t.b[2][ks]);
 #pragma unroll
-        for (int m = 0; m < 4; ++m) ax[m] = frag_two(t.a[m], ks, h);
-#pragma unroll
-        for (int pc = 0; pc < 3; ++pc) {
-            const bf16x8 b = __builtin_bit_cast(bf16x8, t.b[pc][ks]);
-#pragma unroll
-            for (int m = 0; m < 4; ++m)
-                acc[m][pc] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ax[m], b, acc[m][pc], 0, 0, 0);
+        for (int m = 0; m < kXT; ++m) {
+            // expand one tile's bits right before its three MFMAs (a fence per tile keeps the
+            // compiler from hoisting all expansions: registers, not latency, are the limit)
+            const bf16x8 ax = frag_two(t.a[m], ks, h);
+            ah[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ax, b0, ah[m], 0, 0, 0);
+            al[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ax, b1, al[m], 0, 0, 0);
+            al[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ax, b2, al[m], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
         }
     }
+}
+
+// logical block id whose consecutive values share an XCD (blocks b and b + 8 do)
+__device__ __forceinline__ int xcd_logical(int w, int nwg) {
+    const int q = nwg / 8, r = nwg % 8, x = w % 8, l = w / 8;
+    return x < r ? x * (q + 1) + l : r * (q + 1) + (x - r) * q + l;
 }
 
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
@@ -214,66 +248,72 @@ xtr_bits_kernel(const u32x2* __restrict__ cbits, int64_t ld, int32_t P, int64_t 
                 const __bf16* __restrict__ Rp, int32_t Bp, int32_t B, int32_t splits,
                 float* __restrict__ part) {
     const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
-    const int pb = blockIdx.x, g = blockIdx.y, z = blockIdx.z;
+    const int npan = P / (32 * kXT), ngrp = Bp / 32;
+    const int L = xcd_logical(blockIdx.x, npan * ngrp * splits);
+    const int pn = L % npan, g = (L / npan) % ngrp, z = L / (npan * ngrp);
     const int64_t sps = (nblk + splits - 1) / splits;
     const int64_t blk0 = (int64_t)z * sps;
     const int64_t blk1 = min(blk0 + sps, nblk);
     const int nsteps = blk1 > blk0 ? (int)(blk1 - blk0) : 0;
-    g_uint2* pa = as_global<g_uint2>(cbits + blk0 * P + pb * 128 + r);
-    g_uint4* pbp = as_global<g_uint4>(Rp + (int64_t)(g * 32 + r) * ld + blk0 * 64 + 8 * h);
-    const int64_t pstride = (int64_t)Bp * ld / 8;
+    const uint64_t abase = (uint64_t)(cbits + blk0 * P);
+    const uint32_t avo = (uint32_t)((pn * (32 * kXT) + r) * 8);
+    const uint64_t bbase = (uint64_t)(Rp + blk0 * 64);
+    const uint32_t bvo = (uint32_t)(((int64_t)(g * 32 + r) * ld + 8 * h) * 2);
+    const uint64_t plane = (uint64_t)Bp * ld * 2;
 
-    f32x16 acc[4][3];
+    f32x16 ah[kXT], al[kXT];
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int pc = 0; pc < 3; ++pc) acc[m][pc] = (f32x16){};
-
+    for (int m = 0; m < kXT; ++m) {
+        ah[m] = (f32x16){};
+        al[m] = (f32x16){};
+    }
     if (nsteps > 0) {
         StepX A, Bs;
-        loadX(A, pa, pbp, P, pstride, 0);
+        loadX(A, abase, avo, bbase, bvo, plane, P, 0);
         waitX(A);
         int s = 0;
         for (; s + 1 < nsteps; s += 2) {
-            loadX(Bs, pa, pbp, P, pstride, s + 1);
+            loadX(Bs, abase, avo, bbase, bvo, plane, P, s + 1);
             __builtin_amdgcn_sched_barrier(0);
-            mmaX(A, h, acc);
+            mmaX(A, h, ah, al);
             __builtin_amdgcn_sched_barrier(0);
             waitX(Bs);
-            loadX(A, pa, pbp, P, pstride, s + 2 < nsteps ? s + 2 : nsteps - 1);
+            loadX(A, abase, avo, bbase, bvo, plane, P, s + 2 < nsteps ? s + 2 : nsteps - 1);
             __builtin_amdgcn_sched_barrier(0);
-            mmaX(Bs, h, acc);
+            mmaX(Bs, h, ah, al);
             __builtin_amdgcn_sched_barrier(0);
             waitX(A);
         }
-        if (s < nsteps) mmaX(A, h, acc);
+        if (s < nsteps) mmaX(A, h, ah, al);
     }
-    // D[row = predictor][col = fit piece]: lane r = fit, reg j -> predictor (j&3)+8(j>>2)+4h
+    // D[row = predictor][col = fit]: lane r = fit, reg j -> predictor (j&3)+8(j>>2)+4h
     const int f = g * 32 + r;
     if (f < B) {
-        float* out = part + ((int64_t)z * B + f) * P + pb * 128;
+        float* out = part + ((int64_t)z * B + f) * P + pn * (32 * kXT);
 #pragma unroll
-        for (int m = 0; m < 4; ++m)
+        for (int m = 0; m < kXT; ++m)
 #pragma unroll
             for (int j = 0; j < 16; ++j)
-                out[m * 32 + (j & 3) + 8 * (j >> 2) + 4 * h] =
-                    0.5f * ((acc[m][0][j] + acc[m][1][j]) + acc[m][2][j]);
+                out[m * 32 + (j & 3) + 8 * (j >> 2) + 4 * h] = 0.5f * (ah[m][j] + al[m][j]);
     }
 }
 
+// out[slots[f]][a] = sum over slabs z of part[z][f][a] (f = e / P), fixed order
 __global__ void __launch_bounds__(256) reduce_slabs_f64(const float* __restrict__ part,
-                                                        int64_t len, int32_t nz,
+                                                        int64_t len, int32_t nz, int32_t P,
+                                                        const int32_t* __restrict__ slots,
                                                         double* __restrict__ out) {
     for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < len;
          e += (int64_t)gridDim.x * 256) {
         double s = 0.0;
         for (int z = 0; z < nz; ++z) s += (double)part[(int64_t)z * len + e];
-        out[e] = s;
+        const int64_t f = e / P;
+        out[(slots ? (int64_t)slots[f] : f) * P + (e - f * P)] = s;
     }
 }
 
 static int xtr_bits_splits(int32_t P, int32_t B, int64_t nblk) {
-    const int tiles = (P / 128) * ((B + 31) / 32);
+    const int tiles = (P / (32 * kXT)) * ((B + 31) / 32);
     int s = (2048 + tiles - 1) / tiles;
     const int64_t cap = nblk / 32 > 1 ? nblk / 32 : 1;      // >= 32 K-steps per slab
     if (s > cap) s = (int)cap;
@@ -304,7 +344,8 @@ size_t sglm_eta_bits_work_bytes(int32_t P, int32_t B) {
 }
 
 int sglm_gemv_eta_bits(const uint32_t* rbits, int64_t ld, int32_t P, const float* beta,
-                       int32_t B, float* eta, void* work, sglm_stream_t stream) {
+                       int32_t B, const int32_t* slots, float* eta, void* work,
+                       sglm_stream_t stream) {
     if (B <= 0) return SGLM_OK;
     if (!rbits || !beta || !eta || !work || ld % 256 || P % 256) {
         set_error("sglm_gemv_eta_bits: bad args");
@@ -315,11 +356,11 @@ int sglm_gemv_eta_bits(const uint32_t* rbits, int64_t ld, int32_t P, const float
     __bf16* Dp = reinterpret_cast<__bf16*>(work);
     const int64_t total = (int64_t)Bp * P;
     split3_kernel<<<(unsigned)((total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048), 256, 0,
-                    s>>>(beta, P, B, Bp, Dp);
+                    s>>>(beta, P, B, Bp, slots, Dp);
     int st = check_launch("split3_kernel");
     if (st) return st;
     eta_bits_kernel<<<dim3((unsigned)(ld / 128), (unsigned)(Bp / 32)), 64, 0, s>>>(
-        reinterpret_cast<const u32x2*>(rbits), ld, P, Dp, Bp, B, eta);
+        reinterpret_cast<const u32x2*>(rbits), ld, P, Dp, Bp, B, slots, eta);
     return check_launch("eta_bits_kernel");
 }
 
@@ -345,17 +386,54 @@ int sglm_xtr_bits(const uint32_t* cbits, int64_t ld, int32_t P, int64_t n, const
     float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(work) + (size_t)3 * Bp * ld * 2);
     const int64_t total = (int64_t)Bp * ld;
     split3_kernel<<<(unsigned)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192), 256, 0,
-                    s>>>(R, ld, B, Bp, Rp);
+                    s>>>(R, ld, B, Bp, nullptr, Rp);
     int st = check_launch("split3_kernel");
     if (st) return st;
-    xtr_bits_kernel<<<dim3((unsigned)(P / 128), (unsigned)(Bp / 32), (unsigned)splits), 64, 0,
+    xtr_bits_kernel<<<(unsigned)((P / (32 * kXT)) * (Bp / 32) * splits), 64, 0,
                       s>>>(reinterpret_cast<const u32x2*>(cbits), ld, P, nblk, Rp, Bp, B, splits,
                            part);
     st = check_launch("xtr_bits_kernel");
     if (st) return st;
     const int64_t len = (int64_t)B * P;
     reduce_slabs_f64<<<(unsigned)((len + 255) / 256 < 4096 ? (len + 255) / 256 : 4096), 256, 0,
-                       s>>>(part, len, splits, G);
+                       s>>>(part, len, splits, P, nullptr, G);
+    return check_launch("reduce_slabs_f64");
+}
+
+// X^T R with R already in the packed three-piece operand layout ([3][Bp][ld] bf16, as
+// sglm_link_update writes it): G[slots[f]] (float64) for f < B.  `work`: the slab partials,
+// sglm_xtr_bits_packed_work_bytes(P, B, ld): enough for any call with at most B fits (fewer
+// fits take more row slabs, so the bound is the maximum over b <= B).
+size_t sglm_xtr_bits_packed_work_bytes(int32_t P, int32_t B, int64_t ld) {
+    size_t mx = 0;
+    for (int32_t b = 1; b <= B; ++b) {
+        const size_t w = (size_t)xtr_bits_splits(P, b, ld / 64) * b * P * sizeof(float);
+        mx = w > mx ? w : mx;
+    }
+    return mx;
+}
+
+int sglm_xtr_bits_packed(const uint32_t* cbits, int64_t ld, int32_t P, int64_t n,
+                         const void* Rp, int32_t B, const int32_t* slots, double* G, void* work,
+                         sglm_stream_t stream) {
+    if (B <= 0) return SGLM_OK;
+    if (!cbits || !Rp || !G || !work || ld % 256 || P % 256 || n > ld) {
+        set_error("sglm_xtr_bits_packed: bad args");
+        return SGLM_EINVAL;
+    }
+    const int32_t Bp = (B + 31) / 32 * 32;
+    const int64_t nblk = (n + 63) / 64;
+    const int splits = xtr_bits_splits(P, B, ld / 64);
+    hipStream_t s = as_stream(stream);
+    float* part = reinterpret_cast<float*>(work);
+    xtr_bits_kernel<<<(unsigned)((P / (32 * kXT)) * (Bp / 32) * splits), 64, 0,
+                      s>>>(reinterpret_cast<const u32x2*>(cbits), ld, P, nblk,
+                           reinterpret_cast<const __bf16*>(Rp), Bp, B, splits, part);
+    int st = check_launch("xtr_bits_kernel");
+    if (st) return st;
+    const int64_t len = (int64_t)B * P;
+    reduce_slabs_f64<<<(unsigned)((len + 255) / 256 < 4096 ? (len + 255) / 256 : 4096), 256, 0,
+                       s>>>(part, len, splits, P, slots, G);
     return check_launch("reduce_slabs_f64");
 }
 

@@ -24,7 +24,7 @@ SIGNATURES = {
                                    _i32, _vp, _vp]),
     "sglm_gemv_eta": (C.c_int, [_vp, _i32, _i64, _i32, _i64, _vp, _i32, _vp, _vp]),
     "sglm_link_update": (C.c_int, [_i32, _f32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
-                                   _vp, _vp]),
+                                   _vp, _vp, _vp, _vp]),
     "sglm_xtr_work_bytes": (_sz, [_i32, _i32, _i64]),
     "sglm_xtr": (C.c_int, [_vp, _i32, _i64, _i32, _i64, _vp, _i32, _vp, _vp, _vp]),
     "sglm_syrk_work_bytes": (_sz, [_i32, _i32, _i32]),
@@ -39,9 +39,11 @@ SIGNATURES = {
     "sglm_syrk_cbits": (C.c_int, [_vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp]),
     "sglm_pack_bits_t": (C.c_int, [_vp, _i64, _i32, _vp, _vp, _vp]),
     "sglm_eta_bits_work_bytes": (_sz, [_i32, _i32]),
-    "sglm_gemv_eta_bits": (C.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _vp, _vp]),
+    "sglm_gemv_eta_bits": (C.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _vp, _vp, _vp]),
     "sglm_xtr_bits_work_bytes": (_sz, [_i32, _i32, _i64]),
     "sglm_xtr_bits": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _i32, _vp, _vp, _vp]),
+    "sglm_xtr_bits_packed_work_bytes": (_sz, [_i32, _i32, _i64]),
+    "sglm_xtr_bits_packed": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _i32, _vp, _vp, _vp, _vp]),
     "sglm_center_gram": (C.c_int, [_vp, _i32, _i32, _vp, _i32, _i32, _vp, _vp]),
     "sglm_enet_cd_shared": (C.c_int, [_vp, _i32, _vp, _i32, _vp, _vp, _vp, _i32, C.c_double,
                                       _vp, _vp, _vp]),
@@ -58,10 +60,10 @@ SIGNATURES = {
                                         _vp]),
     "sglm_rowsum_work_bytes": (_sz, [_i32, _i32, _i64]),
     "sglm_loss_trials": (C.c_int, [_i32, _f32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
-                                   _vp, _i32, _vp, _vp, _vp]),
+                                   _vp, _vp, _i32, _vp, _vp, _vp]),
     "sglm_loss_trials_max": (C.c_int, [_i32, _f32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp,
-                                       _vp, _vp, _i32, _vp, _vp, _vp, _vp]),
-    "sglm_eta_axpy": (C.c_int, [_i64, _i64, _i32, _vp, _vp, _vp, _vp]),
+                                       _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp]),
+    "sglm_eta_axpy": (C.c_int, [_i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp]),
     "sglm_eta_axpy_max": (C.c_int, [_i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "sglm_eta_pair_absmax": (C.c_int, [_i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "sglm_score_sums": (C.c_int, [_i32, _f32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp,

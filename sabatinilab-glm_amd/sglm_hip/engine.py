@@ -44,6 +44,8 @@ X_BF16, X_F32 = 0, 1
 COL_PAD = 256
 ROW_PAD = 256
 ARMIJO_SIGMA = 2.0 ** -11      # sklearn _newton_solver.py:214
+# second round of line-search step lengths (the first: 1, 1/2, 1/4, 1/8)
+TV2 = np.array([0.0625, 0.03125, 0.015625, 0.0078125, 2.0 ** -10, 2.0 ** -14, 2.0 ** -20])
 XTR_BITS = True                # X^T R on the MFMA from compacted bit-planes for 0/1 designs
 ETA_BITS = True                # eta on the MFMA from row-major bit-planes for 0/1 designs
 SYRK_CBITS = True              # ... and its row-compacted register-only form (v6) when fits
@@ -69,10 +71,6 @@ HESS_SHARE_TOL = float(__import__("os").environ.get("SGLM_HESS_SHARE_TOL", "0.37
 # step fails the line search or contracts slowly leaves the family for good.  0 disables.
 HESS_XMASK_TOL = float(__import__("os").environ.get("SGLM_HESS_XMASK_TOL", "0.75"))
 XMASK_SLOW = 0.7                # aliased-step contraction above which a fit leaves its family
-# Batch compaction: once at most COMPACT_FRAC of the batch is still iterating (and at least
-# COMPACT_MIN fits have stopped), the active fits are moved to the front slots.
-COMPACT_FRAC = float(__import__("os").environ.get("SGLM_COMPACT_FRAC", "0.75"))
-COMPACT_MIN = 4
 
 
 def require_gpu():
@@ -249,15 +247,17 @@ class Design:
             _lib.call("sglm_xtr", _p(self.xg), self.xtype, self.ld, self.P, self.n, _p(R), B,
                       _p(g_out), _p(w), st)
 
-    def eta(self, beta_dev, out=None):
-        """eta[k] = X beta[k] for a (B, P) f32 device tensor."""
+    def eta(self, beta_dev, out=None, slots=None):
+        """eta[k] = X beta[k] for a (B, P) f32 device tensor; with ``slots`` (int32 device
+        tensor) only those rows k (the rest of ``out`` is left as is)."""
         B = beta_dev.shape[0]
         if out is None:
             out = torch.empty((B, self.ld), dtype=torch.float32, device=self.device)
         if self.rbits is not None and ETA_BITS:
-            work = _work(_lib.query("sglm_eta_bits_work_bytes", self.P, B), self.device, "eta")
-            _lib.call("sglm_gemv_eta_bits", _p(self.rbits), self.ld, self.P, _p(beta_dev), B,
-                      _p(out), _p(work), _stream())
+            nb = B if slots is None else int(slots.numel())
+            work = _work(_lib.query("sglm_eta_bits_work_bytes", self.P, nb), self.device, "eta")
+            _lib.call("sglm_gemv_eta_bits", _p(self.rbits), self.ld, self.P, _p(beta_dev), nb,
+                      _p(slots), _p(out), _p(work), _stream())
         else:
             _lib.call("sglm_gemv_eta", _p(self.xg), self.xtype, self.ld, self.P, self.n,
                       _p(beta_dev), B, _p(out), _stream())
@@ -557,6 +557,46 @@ def _pinned(tag, numel, dtype):
     return t[:numel]
 
 
+_NP2TORCH = {np.dtype(np.int32): torch.int32, np.dtype(np.int64): torch.int64,
+             np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64}
+
+
+class _Uploads:
+    """Asynchronous small host->device uploads for one IRLS thread.  A pageable ``.to(dev)``
+    synchronises the stream (the host then waits for every queued kernel, and the GPU idles
+    while the host prepares the next launches); arrays are instead staged in a pinned arena
+    and copied with non_blocking=True into a device arena.  The arena has two halves that
+    alternate at every stream synchronisation (``synced()``): a half is rewritten only after
+    a synchronisation that followed every copy out of it, and an upload stays valid until
+    the second synchronisation after it (kernels enqueued after the first may still read
+    it)."""
+
+    def __init__(self, dev, nbytes=1 << 20):
+        self.half = nbytes // 2
+        self.h = _pinned("up", nbytes, torch.uint8)
+        self.d = _work(nbytes, dev, "up")
+        self.dev = dev
+        self.base = 0
+        self.off = 0
+
+    def __call__(self, a, dtype=None):
+        a = np.ascontiguousarray(a if dtype is None else np.asarray(a).astype(dtype))
+        nb = a.nbytes
+        if self.off + nb > self.half:            # half full: a synchronous upload
+            return torch.from_numpy(a).to(self.dev)
+        o = self.base + self.off
+        self.h[o:o + nb].numpy()[:] = a.reshape(-1).view(np.uint8)
+        dst = self.d[o:o + nb]
+        dst.copy_(self.h[o:o + nb], non_blocking=True)
+        self.off += (nb + 255) // 256 * 256
+        return dst.view(_NP2TORCH[a.dtype]).view(a.shape)
+
+    def synced(self):
+        """Call right after a synchronisation of the stream the uploads are ordered on."""
+        self.base = self.half - self.base
+        self.off = 0
+
+
 def _work(nbytes, dev, tag="main"):
     """Grow-only scratch buffer per (thread scratch, device, tag); stream-ordered reuse only
     (each thread that runs the engine has its own scratch)."""
@@ -651,12 +691,9 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
     reuse_tol = 0.0 if const_hess else HESS_REUSE_TOL / max(1.0, abs(2.0 - power))
     share_tol = 0.0 if const_hess else min(HESS_SHARE_TOL / max(1.0, abs(2.0 - power)),
                                            reuse_tol)
-    # Device state is held per SLOT; slot s holds fit fid[s].  When enough fits have stopped,
-    # the batch is compacted to the active ones (their predictor, factor, frozen set and
-    # penalty rows move to the front), so the per-fit kernels of later iterations (link,
-    # gradient, eta, line search) run over the active fits only.
+    # Device state is held per SLOT (one per fit, fixed for the whole solve); every per-fit
+    # kernel takes the list of active slots, so stopped fits cost nothing and no state moves.
     B = B0
-    fid = np.arange(B0)
     fresp_h = np.array([r.resp for r in reqs], dtype=np.int32)
     fmask_h = np.array([r.mask for r in reqs], dtype=np.int32)
     fit_resp = torch.from_numpy(fresp_h).to(dev)
@@ -686,13 +723,12 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
     xtr_work = _work(max(_lib.query("sglm_xtr_work_bytes", P, B0, n),
                          _lib.query("sglm_rowsum_work_bytes", B0, 8, n)), dev)
     tv1 = torch.tensor([0.0, 1.0, 0.5, 0.25, 0.125], dtype=torch.float32, device=dev)
-    tv2 = torch.tensor([0.0625, 0.03125, 0.015625, 0.0078125, 2.0 ** -10, 2.0 ** -14, 2.0 ** -20],
-                       dtype=torch.float32, device=dev)
+    tv2 = torch.from_numpy(TV2.astype(np.float32)).to(dev)
     Ltr = torch.zeros(B0 * 8, dtype=torch.float64, device=dev)    # dense [B][T] per call
     nsteps = (n + 31) // 32
     ntile1 = (P // 256) * (P // 256 + 1) // 2
     rows = np.array([prob.mask_stats(r.resp, r.mask)[0] for r in reqs], dtype=np.float64)
-    bf.prob, bf.fit_mask = prob, fmask_h
+    bf.prob, bf.fit_mask, bf.fit_mask_d = prob, fmask_h, fit_mask
     # cross-mask families (slot of the representative per slot, -1: none / is one)
     xmask_tol = 0.0 if const_hess else HESS_XMASK_TOL / max(1.0, abs(2.0 - power))
     repl = np.full(B0, -1, dtype=np.int64)
@@ -710,64 +746,102 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                         repl[k] = rk
     alias = np.full(B0, -1, dtype=np.int64)     # slot whose factor the fit used this iteration
     no_alias = np.zeros(B0, dtype=bool)
-    rscale_d = torch.zeros(B0, dtype=torch.float32, device=dev)
 
-    def retire(slots):
-        """Record the results of the fits in `slots` (they leave the batch or it ends)."""
-        if slots.size == 0:
-            return
-        info_h = bf.info[:B].cpu().numpy()
-        f = fid[slots]
-        out_beta[f] = beta[slots]
-        out_iter[f] = n_iter[slots]
-        out_conv[f] = converged[slots]
-        out_info[f] = info_h[slots]
+    up = _Uploads(dev)
+    bf.up = up
+    pd_h = _pinned("pairdist", 4 * B0, torch.float32)
+
+    def hess_plan(act):
+        """Hessian decisions of the next iteration that need no device data, and one launch of
+        the max-row distances they depend on (copied back asynchronously): fits with a valid
+        factor keep it (drift <= reuse_tol); fits of a cross-mask family without one are
+        candidates for the representative's factor (distance to it); the rest form a new
+        Hessian -- once per distinct (mask, response, beta) -- and the distinct ones of one
+        (mask, response) may share along the lambda path (distances of neighbours)."""
+        own_ok = drift[act] <= reuse_tol
+        cand = act[(repl[act] >= 0) & ~no_alias[act] & ~own_ok]
+        rest = act[~np.isin(act, cand)]
+        keep = rest[drift[rest] <= reuse_tol]
+        form = rest[drift[rest] > reuse_tol]
+        reps, dup = {}, []
+        for k in form:
+            rk = reps.setdefault((reqs[k].mask, reqs[k].resp, beta[k].tobytes()), k)
+            if rk != k:
+                dup.append((k, rk))
+        uniq = np.array(sorted(reps.values()), dtype=np.int32)
+        chains = []
+        if share_tol > 0.0 and uniq.size > 1:
+            groups = {}
+            for k in uniq:
+                groups.setdefault((reqs[k].mask, reqs[k].resp), []).append(int(k))
+            chains = [sorted(g, key=lambda k: lam[k]) for g in groups.values() if len(g) > 1]
+        pairs = [(int(k), int(repl[k])) for k in cand]
+        pairs += [(c[i], c[i + 1]) for c in chains for i in range(len(c) - 1)]
+        ev = None
+        if pairs:
+            npair = len(pairs)
+            if npair > pd_h.numel():
+                raise RuntimeError("pair distance buffer too small")
+            pd_d = _pair_dist_async(bf, prob, np.array(pairs, dtype=np.int32), n, ld, st)
+            pd_h[:npair].copy_(pd_d, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        return dict(cand=cand, keep=keep, form=form, reps=reps, dup=dup, uniq=uniq,
+                    chains=chains, npairs=len(pairs), ev=ev)
+
+    def hess_finish(pl):
+        """Apply the distances of a plan: lambda-neighbour sharing, then aliasing of the
+        candidates whose distance to the representative plus the representative's own drift
+        after this iteration's decision stays <= xmask_tol (the others form their own)."""
+        if pl["ev"] is not None:
+            pl["ev"].synchronize()
+        dist = pd_h[:pl["npairs"]].numpy().astype(np.float64)
+        cand, keep, form, reps, dup, uniq = (pl[k] for k in ("cand", "keep", "form", "reps",
+                                                             "dup", "uniq"))
+        dist_c, dist_s = dist[:cand.size], dist[cand.size:]
+        drift[form] = 0.0
+        if pl["chains"]:
+            uniq, shared = _share_chains(uniq, pl["chains"], dist_s, share_tol)
+            for k, rk, dist_k in shared:
+                dup.append((k, rk))
+                drift[k] = dist_k
+        ok = dist_c + drift[repl[cand]] <= xmask_tol
+        ali, fail = cand[ok], cand[~ok]
+        for k in fail:
+            rk = reps.setdefault((reqs[k].mask, reqs[k].resp, beta[k].tobytes()), k)
+            if rk != k:
+                dup.append((k, rk))
+            else:
+                uniq = np.append(uniq, np.int32(k))
+        drift[fail] = 0.0
+        return keep, np.concatenate([form, fail]), uniq, dup, ali, fail
+    use_rp = d.xbits is not None and XTR_BITS      # R packed into the MFMA gradient operand
+    if use_rp:
+        rp_buf = _work(3 * pad_to(B0, 32) * ld * 2, dev, "rp")
+        gx_work = _work(_lib.query("sglm_xtr_bits_packed_work_bytes", P, B0, ld), dev, "xtr")
 
     import time
     tick = stats.mark if (stats is not None and stats.trace_phases) else (lambda name, t: t)
     t0 = tick("irls_setup", time.perf_counter())
+    plan = None
     for it in range(int(max_iter.max()) + 1):
+        # every per-fit kernel runs over the active slots only (slot lists): no compaction,
+        # so factors, predictors and the representatives' factors stay where they are
         act = np.flatnonzero(active)
-        if act.size == 0:
+        na = int(act.size)
+        if na == 0:
             break
-        # slots to keep: the active fits and the representatives whose factors they may use
-        need = np.unique(repl[act][(repl[act] >= 0) & ~no_alias[act]])
-        kept = np.union1d(act, need) if need.size else act
-        if act.size <= COMPACT_FRAC * B and B - kept.size >= COMPACT_MIN:
-            retire(np.flatnonzero(~active))
-            m = int(kept.size)
-            remap = np.full(B, -1, dtype=np.int64)
-            remap[kept] = np.arange(m)
-            # in-place row moves, ascending (slot kept[i] >= i is never a destination already
-            # written): no temporaries, so no allocator traffic inside the iteration loop
-            moves = [(i, int(s_)) for i, s_ in enumerate(kept) if i != s_]
-            if moves:
-                dst = torch.from_numpy(np.array([a for a, _ in moves], dtype=np.int64)).to(dev)
-                src = torch.from_numpy(np.array([b for _, b in moves], dtype=np.int64)).to(dev)
-                for t in (bf.frozen, bf.info):
-                    t[dst] = t[src]      # small: one gather/scatter (sources read first)
-                for i, s_ in moves:
-                    bf.eta[i].copy_(bf.eta[s_])
-                    bf.H[i].copy_(bf.H[s_])
-            (lam, penal, dsh, beta, drift, gram_now, active, n_iter, converged, prev_rel,
-             max_iter, rows, fid, fresp_h, fmask_h, repl, alias, no_alias) = (
-                x[kept] for x in (lam, penal, dsh, beta, drift, gram_now, active, n_iter,
-                                  converged, prev_rel, max_iter, rows, fid, fresp_h, fmask_h,
-                                  repl, alias, no_alias))
-            repl = np.where(repl >= 0, remap[np.maximum(repl, 0)], -1)
-            alias = np.where(alias >= 0, remap[np.maximum(alias, 0)], -1)
-            reqs = [reqs[s_] for s_ in kept]
-            bf.dshift[:m].copy_(torch.from_numpy(dsh))
-            lamp_d = torch.from_numpy(lam[:, None] * penal).to(dev)
-            fit_resp = torch.from_numpy(fresp_h).to(dev)
-            fit_mask = torch.from_numpy(fmask_h).to(dev)
-            bf.fit_mask = fmask_h
-            B = m
-            act = np.flatnonzero(active)
-            t0 = tick("it_compact", t0)
-        _lib.call("sglm_link_update", fam, power, n, ld, B, _p(bf.eta), _p(prob.Y), _p(prob.M),
-                  _p(fit_resp), _p(fit_mask), _p(bf.W), _p(bf.R), st)
-        d.xtr(bf.R, B, bf.g)
+        act_d = up(act, np.int32)
+        if use_rp:
+            _lib.call("sglm_link_update", fam, power, n, ld, na, _p(act_d), _p(bf.eta),
+                      _p(prob.Y), _p(prob.M), _p(fit_resp), _p(fit_mask), _p(bf.W), None,
+                      _p(rp_buf), st)
+            _lib.call("sglm_xtr_bits_packed", _p(d.cbits_full()), ld, P, n, _p(rp_buf), na,
+                      _p(act_d), _p(bf.g), _p(gx_work), st)
+        else:
+            _lib.call("sglm_link_update", fam, power, n, ld, B, None, _p(bf.eta), _p(prob.Y),
+                      _p(prob.M), _p(fit_resp), _p(fit_mask), _p(bf.W), _p(bf.R), None, st)
+            d.xtr(bf.R, B, bf.g)
         bnp = beta_pin.numpy()
         bnp[:B] = beta
         beta64_d[:B].copy_(beta_pin[:B], non_blocking=True)
@@ -790,48 +864,12 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                     if rk != k:
                         bf.H[k].copy_(bf.H[rk])
         else:
-            # Fits whose weights are bitwise identical have identical Hessians: same mask,
-            # response and coefficients (every fit of a mask/response pair in the first
-            # iteration, which starts from the intercept-only model).  Form each distinct
-            # Hessian once and copy it.  Fits whose predictor drifted less than reuse_tol
-            # since their last Hessian keep its factor (no Gram, no factorisation).  Fits of a
-            # cross-mask family that hold no valid factor of their own are candidates for the
-            # representative's factor; their distance to it is measured first.
-            own_ok = drift[act] <= reuse_tol
-            cand = act[(repl[act] >= 0) & ~no_alias[act] & ~own_ok]
-            dist_c = (_pair_dist(bf, prob, np.stack([cand, repl[cand]], 1), n, ld, st)
-                      if cand.size else np.zeros(0))
-            rest = act[~np.isin(act, cand)]
-            keep = rest[drift[rest] <= reuse_tol]
-            form = rest[drift[rest] > reuse_tol]
-            reps = {}
-            dup = []
-            for k in form:
-                key = (reqs[k].mask, reqs[k].resp, beta[k].tobytes())
-                rk = reps.setdefault(key, k)
-                if rk != k:
-                    dup.append((k, rk))
-            uniq = np.array(sorted(reps.values()), dtype=np.int32)
-            drift[form] = 0.0
-            if share_tol > 0.0 and uniq.size > 1:
-                uniq, shared = _share_grams(bf, prob, reqs, lam, uniq, share_tol, n, ld, st)
-                for k, rk, dist_k in shared:
-                    dup.append((k, rk))
-                    drift[k] = dist_k
-            # candidates: alias while (distance to the representative) + (the representative's
-            # own drift after this iteration's decision) <= xmask_tol, else form their own
-            ok = dist_c + drift[repl[cand]] <= xmask_tol
-            ali = cand[ok]
-            fail = cand[~ok]
-            for k in fail:
-                key = (reqs[k].mask, reqs[k].resp, beta[k].tobytes())
-                rk = reps.setdefault(key, k)
-                if rk != k:
-                    dup.append((k, rk))
-                else:
-                    uniq = np.append(uniq, np.int32(k))
-            drift[fail] = 0.0
-            form = np.concatenate([form, fail])
+            # decisions planned at the end of the previous iteration (their device distances are
+            # long computed): keep / form / share / alias (see _hess_plan)
+            if plan is None:
+                plan = hess_plan(act)
+            keep, form, uniq, dup, ali, fail = hess_finish(plan)
+            plan = None
             alias[:] = -1
             alias[ali] = repl[ali]
             _syrk(d, bf, np.sort(uniq).astype(np.int32), nsteps, ntile1, stats, st, rows=rows)
@@ -850,77 +888,83 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
             order, nref = act, (0 if factored else act.size)
         else:
             order, nref = np.concatenate([form, keep]), form.size
-        fits_d = torch.from_numpy(order.astype(np.int32)).to(dev)
+        fits_d = up(order, np.int32)
         _lib.call("sglm_chol_solve_mixed", _p(bf.H), P, _p(fits_d), int(order.size), int(nref),
                   _p(bf.gtot), _p(bf.dshift), _p(bf.delta), _p(bf.info), _p(bf.frozen), B,
                   _p(bf.cwork), st)
         if not const_hess and ali.size:
             # the representatives' factors are complete: solve the aliased fits on them
             src = repl[ali]
-            al_d = torch.from_numpy(np.stack([ali, src]).astype(np.int32)).to(dev)
-            rscale_d[:ali.size].copy_(torch.from_numpy((rows[src] / rows[ali]).astype(np.float32)))
+            al_d = up(np.stack([ali, src]), np.int32)
+            rscale_d = up(rows[src] / rows[ali], np.float32)
             _lib.call("sglm_chol_solve_alias", _p(bf.H), P, _p(al_d[0]), _p(al_d[1]),
                       int(ali.size), _p(bf.gtot), _p(rscale_d), _p(bf.delta), _p(bf.frozen), B,
                       _p(bf.cwork), st)
         factored = True
-        d.eta(bf.delta[:B], bf.deta)
+        d.eta(bf.delta, bf.deta, slots=act_d)
         delta_h[:B].copy_(bf.delta[:B], non_blocking=True)
         t0 = tick("it_solve_eta", t0)
-        # ---- line search
-        _lib.call("sglm_loss_trials_max", fam, power, n, ld, B, _p(bf.eta), _p(bf.deta),
-                  _p(prob.Y), _p(prob.M), _p(fit_resp), _p(fit_mask), _p(tv1), 5, _p(Ltr),
-                  _p(dmax_d), _p(xtr_work), st)
-        L_h[: B * 5].copy_(Ltr[: B * 5], non_blocking=True)
-        dmax_h[:B].copy_(dmax_d[:B], non_blocking=True)
+        # ---- line search (rows of L and dmax: active fits in slot order)
+        _lib.call("sglm_loss_trials_max", fam, power, n, ld, na, _p(act_d), _p(bf.eta),
+                  _p(bf.deta), _p(prob.Y), _p(prob.M), _p(fit_resp), _p(fit_mask), _p(tv1), 5,
+                  _p(Ltr), _p(dmax_d), _p(xtr_work), st)
+        L_h[: na * 5].copy_(Ltr[: na * 5], non_blocking=True)
+        dmax_h[:na].copy_(dmax_d[:na], non_blocking=True)
         torch.cuda.current_stream().synchronize()              # the iteration's round trip
-        g = g_h[:B].numpy().copy()
-        delta = delta_h[:B].numpy().astype(np.float64)
-        L = L_h[: B * 5].numpy().reshape(B, 5).copy()
-        dmaxeta = dmax_h[:B].numpy().astype(np.float64)
+        up.synced()
+        g = g_h[:B].numpy()[act]
+        delta = np.zeros((B, P))
+        delta[act] = delta_h[:B].numpy()[act]
+        L = L_h[: na * 5].numpy().reshape(na, 5).copy()
+        dmaxeta = dmax_h[:na].numpy().astype(np.float64)
         ts = np.array([0.0, 1.0, 0.5, 0.25, 0.125])
-        gdir = np.sum(g * delta, axis=1)
+        da = delta[act]
+        gdir = np.sum(g * da, axis=1)
         # penalty lam/2 |w + t d|^2 = lam/2 (A + 2 t Bq + t^2 C), vectorised over fits x trials
-        pb, pd_ = penal * beta, penal * delta
-        A_, B_, C_ = np.sum(pb * beta, 1), np.sum(pb * delta, 1), np.sum(pd_ * delta, 1)
+        pen_a, beta_a, lam_a = penal[act], beta[act], lam[act]
+        pb, pd_ = pen_a * beta_a, pen_a * da
+        A_, B_, C_ = np.sum(pb * beta_a, 1), np.sum(pb * da, 1), np.sum(pd_ * da, 1)
 
         def objectives(Lm, tv):
-            return Lm + 0.5 * lam[:, None] * (A_[:, None] + 2 * tv[None, :] * B_[:, None]
-                                              + tv[None, :] ** 2 * C_[:, None])
-        step = np.zeros(B)
-        obj = objectives(L, ts)[act]
-        ok = ((obj[:, 1:] - obj[:, :1] <= ARMIJO_SIGMA * ts[None, 1:] * gdir[act, None]) |
+            return Lm + 0.5 * lam_a[:, None] * (A_[:, None] + 2 * tv[None, :] * B_[:, None]
+                                                + tv[None, :] ** 2 * C_[:, None])
+        step_a = np.zeros(na)
+        obj = objectives(L, ts)
+        ok = ((obj[:, 1:] - obj[:, :1] <= ARMIJO_SIGMA * ts[None, 1:] * gdir[:, None]) |
               (np.abs(obj[:, 1:] - obj[:, :1]) <= 1e-13 * np.abs(obj[:, :1])))
         first = np.argmax(ok, axis=1)
-        hit = ok[np.arange(act.size), first]
-        step[act[hit]] = ts[1:][first[hit]]
-        need_more = act[~hit]
-        if need_more.size:
-            _lib.call("sglm_loss_trials", fam, power, n, ld, B, _p(bf.eta), _p(bf.deta),
-                      _p(prob.Y), _p(prob.M), _p(fit_resp), _p(fit_mask), _p(tv2), 7, _p(Ltr),
-                      _p(xtr_work), st)
-            L2 = Ltr[: B * 7].view(B, 7).cpu().numpy()
-            ts2 = tv2.cpu().numpy().astype(np.float64)
-            obj0 = objectives(L[:, :1], np.zeros(1))[need_more]
-            o2 = objectives(L2, ts2)[need_more]
-            ok2 = o2 - obj0 <= ARMIJO_SIGMA * ts2[None, :] * gdir[need_more, None]
+        hit = ok[np.arange(na), first]
+        step_a[hit] = ts[1:][first[hit]]
+        more = np.flatnonzero(~hit)                         # positions in act
+        if more.size:
+            sub_d = up(act[more], np.int32)
+            _lib.call("sglm_loss_trials", fam, power, n, ld, int(more.size), _p(sub_d),
+                      _p(bf.eta), _p(bf.deta), _p(prob.Y), _p(prob.M), _p(fit_resp),
+                      _p(fit_mask), _p(tv2), 7, _p(Ltr), _p(xtr_work), st)
+            L2 = Ltr[: more.size * 7].view(more.size, 7).cpu().numpy()
+            ts2 = TV2.astype(np.float32).astype(np.float64)
+            obj0 = objectives(L[:, :1], np.zeros(1))[more]
+            o2 = (L2 + 0.5 * lam_a[more, None] * (A_[more, None] + 2 * ts2[None, :] * B_[more, None]
+                                                  + ts2[None, :] ** 2 * C_[more, None]))
+            ok2 = o2 - obj0 <= ARMIJO_SIGMA * ts2[None, :] * gdir[more, None]
             f2 = np.argmax(ok2, axis=1)
-            h2 = ok2[np.arange(need_more.size), f2]
-            step[need_more[h2]] = ts2[f2[h2]]
+            h2 = ok2[np.arange(more.size), f2]
+            step_a[more[h2]] = ts2[f2[h2]]
         t0 = tick("it_linesearch", t0)
         # ---- update
-        beta += step[:, None] * delta
+        beta[act] += step_a[:, None] * da
         if not const_hess:
-            drift[act] += step[act] * dmaxeta[act]    # max_i |t d_eta_i| over the fit's rows
-        step_d = torch.from_numpy(step.astype(np.float32)).to(dev)
-        _lib.call("sglm_eta_axpy", n, ld, B, _p(step_d), _p(bf.deta), _p(bf.eta), st)
+            drift[act] += step_a * dmaxeta            # max_i |t d_eta_i| over the fit's rows
+        step_d = up(step_a, np.float32)
+        _lib.call("sglm_eta_axpy", n, ld, na, _p(act_d), _p(step_d), _p(bf.deta), _p(bf.eta), st)
         n_iter[act] += 1
         if stats is not None:
             stats.newton_iters += 1
-            stats.fit_iters += int(act.size)
+            stats.fit_iters += na
             # SURVEY.md §8(d) F per fit-iteration, charged for work actually done: the Gram
             # term only where a Gram was computed (not for a Hessian shared from another fit),
-            # the factorisation where a new factor was formed (a kept factor costs the two
-            # triangular solves only)
+            # the factorisation where a new factor was formed (a kept or aliased factor costs
+            # the two triangular solves only)
             pa = float(p + 1)
             nr = rows[act]
             stats.alg_flop += float(np.sum(np.where(gram_comp[act], nr * pa * (pa + 1), 0.0)
@@ -928,9 +972,9 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                                            + 4.0 * nr * pa + 2 * pa * pa))
             stats.gram_fit_iters += int(np.sum(gram_comp[act]))
         scale = 1.0 + np.max(np.abs(beta[act]), axis=1)
-        relv = np.max(np.abs(step[act, None] * delta[act]), axis=1) / scale
-        prop = np.max(np.abs(delta[act]), axis=1) / scale      # the proposed Newton step
-        stepa = step[act]
+        relv = np.max(np.abs(step_a[:, None] * da), axis=1) / scale
+        prop = np.max(np.abs(da), axis=1) / scale      # the proposed Newton step
+        stepa = step_a
         fresh = gram_now[act] | const_hess
         ls_fail = stepa == 0.0
         # a failed line search on a kept (stale) factor is not a verdict: the next iteration
@@ -969,10 +1013,17 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
             stats.stops["line_search_failed"] += int(np.sum(stop_fail & (prop > tol)))
             stats.stops["max_iter"] += int(np.sum(out_of_iters))
             stats.stops["stale_factor_retry"] += int(np.sum(ls_fail & ~fresh))
+        if not const_hess and active.any():
+            # the next iteration's Hessian decisions and their distances, enqueued behind
+            # this iteration's predictor update (read back without a stall next iteration)
+            plan = hess_plan(np.flatnonzero(active))
         t0 = tick("it_update", t0)
 
-    retire(np.arange(B))
-    bf.prob = bf.keep = None            # drop the compacted designs with the problem
+    out_beta[:] = beta
+    out_iter[:] = n_iter
+    out_conv[:] = converged
+    out_info[:] = bf.info[:B].cpu().numpy()
+    bf.prob = bf.keep = bf.up = bf.fit_mask_d = None   # drop the compacted designs with the problem
     # final linear predictor from the final coefficients, in request order (no accumulated
     # drift)
     bf.beta.copy_(torch.from_numpy(out_beta.astype(np.float32)))
@@ -1131,32 +1182,29 @@ def irls_scored(prob: Problem, reqs: List[FitReq], sets: np.ndarray,
     return res, sums
 
 
-def _pair_dist(bf, prob, pairs, n, ld, st):
-    """max over the rows of fit a's mask of |eta_a - eta_b| for each (a, b) in pairs (host)."""
+def _pair_dist_async(bf, prob, pairs, n, ld, st):
+    """Device float32 [len(pairs)]: max over the rows of fit a's mask of |eta_a - eta_b| for
+    each (a, b) in pairs (enqueued, not waited for)."""
     dev = bf.eta.device
-    pd_ = torch.from_numpy(np.ascontiguousarray(pairs, dtype=np.int32).reshape(-1)).to(dev)
-    fm = torch.from_numpy(np.asarray(bf.fit_mask, dtype=np.int32)).to(dev)
-    out = torch.empty(len(pairs), dtype=torch.float32, device=dev)
-    _lib.call("sglm_eta_pair_absmax", n, ld, len(pairs), _p(pd_), _p(prob.M), _p(fm),
+    upl = getattr(bf, "up", None)
+    pairs = np.ascontiguousarray(pairs, dtype=np.int32).reshape(-1)
+    pd_ = upl(pairs) if upl is not None else torch.from_numpy(pairs).to(dev)
+    fm = getattr(bf, "fit_mask_d", None)
+    if fm is None:
+        fm = torch.from_numpy(np.asarray(bf.fit_mask, dtype=np.int32)).to(dev)
+    out = torch.empty(pairs.size // 2, dtype=torch.float32, device=dev)
+    _lib.call("sglm_eta_pair_absmax", n, ld, pairs.size // 2, _p(pd_), _p(prob.M), _p(fm),
               _p(bf.eta), _p(out), st)
-    return out.cpu().numpy().astype(np.float64)
+    return out
 
 
-def _share_grams(bf, prob, reqs, lam, uniq, tol, n, ld, st):
-    """Approximate Hessian dedup.  Fits of one (mask, response) are ordered by penalty (the
-    lambda path: neighbours have the closest solutions); the max-row distances of consecutive
-    predictors are measured on the device, and a greedy chain lets each fit share the Gram of
-    the chain's representative while the summed distance (a bound on the true one, triangle
-    inequality) stays <= tol.  Returns (representatives, [(fit, rep, distance bound)])."""
-    groups = {}
-    for k in uniq:
-        groups.setdefault((reqs[k].mask, reqs[k].resp), []).append(int(k))
-    chains = [sorted(g, key=lambda k: lam[k]) for g in groups.values() if len(g) > 1]
-    if not chains:
-        return uniq, []
-    pairs = np.array([(c[i], c[i + 1]) for c in chains for i in range(len(c) - 1)],
-                     dtype=np.int32)
-    dist = _pair_dist(bf, prob, pairs, n, ld, st)
+def _share_chains(uniq, chains, dist, tol):
+    """Approximate Hessian dedup along the lambda path.  ``chains``: fits of one (mask,
+    response) ordered by penalty (neighbours have the closest solutions); ``dist``: the
+    max-row predictor distances of consecutive chain members.  A greedy chain lets each fit
+    share the Gram of the chain's representative while the summed distance (a bound on the
+    true one, triangle inequality) stays <= tol.  Returns (representatives, [(fit, rep,
+    distance bound)])."""
     shared, drop, q = [], set(), 0
     for c in chains:
         rep, acc = c[0], 0.0
@@ -1234,8 +1282,12 @@ def _syrk_cbits(d: Design, bf, prob: Problem, fits: np.ndarray, st, ev=None):
     desc = np.array([[c[0].data_ptr(), c[1], wc.data_ptr() + 2 * i * stride,
                       0 if c[2] is None else c[2].data_ptr()] for i, c in enumerate(cbs)],
                     dtype=np.int64)
-    desc_d = torch.from_numpy(desc).to(d.device)
-    fits_d = torch.from_numpy(fits.astype(np.int32)).to(d.device)
+    upl = getattr(bf, "up", None)
+    if upl is not None:
+        desc_d, fits_d = upl(desc), upl(fits, np.int32)
+    else:
+        desc_d = torch.from_numpy(desc).to(d.device)
+        fits_d = torch.from_numpy(fits.astype(np.int32)).to(d.device)
     nb = d.P // 128
     splits = syrk6_splits(nb * (nb + 1) // 2 * nact, max(1, (maxrows + 63) // 64), nact, d.P)
     wb = _lib.query("sglm_syrk_work_bytes", d.P, nact, splits)

@@ -361,11 +361,11 @@ def test_odd_shapes_vs_oracle(engine, n, p):
 
 
 def test_hessian_reuse_keeps_the_fixed_point(engine, monkeypatch):
-    """Hessian reuse / sharing (engine.HESS_REUSE_TOL, HESS_SHARE_TOL) only changes the
-    inexact-Newton contraction, not the minimiser, and batch compaction only the slot order: a
-    C3-shape 5-split x 20-lambda Poisson grid with the defaults matches the same grid with a
-    fresh Hessian every iteration and a fixed batch (1e-5 relative), converges everywhere, and actually kept factors; two lambdas are also
-    held to the float64 oracle."""
+    """Hessian reuse, lambda-neighbour sharing and cross-mask sharing (engine.HESS_REUSE_TOL,
+    HESS_SHARE_TOL, HESS_XMASK_TOL) only change the inexact-Newton contraction, not the
+    minimiser: a C3-shape 5-split x 20-lambda Poisson grid with the defaults matches the same
+    grid with a fresh own Hessian every iteration (1e-5 relative), converges everywhere, and
+    actually kept and aliased factors; two lambdas are also held to the float64 oracle."""
     import pandas as pd
     from sglm_hip import engine as E, folds, grid, synth
     from sglm_hip.estimators import Objective
@@ -378,13 +378,13 @@ def test_hessian_reuse_keeps_the_fixed_point(engine, monkeypatch):
     objs = [Objective("irls", E.FAM_TWEEDIE_LOG, 1.0, float(a), "n", True, 100) for a in lams]
     st = E.IrlsStats()
     fast = grid.run(d, s.y, cv_idx, objs, [0] * len(objs), stats=st)
-    assert st.reused > 0 and st.gram_fits < st.fit_iters
+    assert st.reused > 0 and st.aliased > 0 and st.gram_fits < st.fit_iters
     monkeypatch.setattr(E, "HESS_REUSE_TOL", 0.0)
     monkeypatch.setattr(E, "HESS_SHARE_TOL", 0.0)
-    monkeypatch.setattr(E, "COMPACT_FRAC", 0.0)        # and no batch compaction
+    monkeypatch.setattr(E, "HESS_XMASK_TOL", 0.0)
     st0 = E.IrlsStats()
     exact = grid.run(d, s.y, cv_idx, objs, [0] * len(objs), stats=st0)
-    assert st0.reused == 0
+    assert st0.reused == 0 and st0.aliased == 0
     for a, b in zip(fast, exact):
         assert rel(a["cv_coefs"], b["cv_coefs"]) < 1e-5
         assert rel(a["cv_intercepts"], b["cv_intercepts"]) < 1e-5

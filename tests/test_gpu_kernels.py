@@ -399,8 +399,17 @@ def test_eta_bits_matches_float64(engine, torch_mod):
     out = torch.full((B, d.ld), float("nan"), dtype=torch.float32, device="cuda")
     work = torch.empty(_lib.query("sglm_eta_bits_work_bytes", d.P, B), dtype=torch.uint8,
                        device="cuda")
-    _lib.call("sglm_gemv_eta_bits", d.rbits.data_ptr(), d.ld, d.P, bd.data_ptr(), B,
+    _lib.call("sglm_gemv_eta_bits", d.rbits.data_ptr(), d.ld, d.P, bd.data_ptr(), B, None,
               out.data_ptr(), work.data_ptr(), 0)
+    # a slot list computes exactly those rows (bitwise: each fit's column is independent) and
+    # leaves the others untouched
+    sl = torch.tensor([36, 0, 17, 5], dtype=torch.int32, device="cuda")
+    out_s = torch.full_like(out, float("nan"))
+    _lib.call("sglm_gemv_eta_bits", d.rbits.data_ptr(), d.ld, d.P, bd.data_ptr(), 4,
+              sl.data_ptr(), out_s.data_ptr(), work.data_ptr(), 0)
+    for k in (36, 0, 17, 5):
+        assert torch.equal(out_s[k], out[k]), k
+    assert torch.isnan(out_s[1]).all()
     ref_valu = torch.empty_like(out)
     _lib.call("sglm_gemv_eta", d.xb.data_ptr(), 0, d.ld, d.P, d.n, bd.data_ptr(), B,
               ref_valu.data_ptr(), 0)
@@ -467,3 +476,78 @@ def test_xtr_bits_matches_float64(engine, torch_mod):
     got = G.cpu().numpy()
     assert np.max(np.abs(got - ref) / np.maximum(scale, 1e-30)) < 2e-6
     assert np.max(np.abs(got - G2.cpu().numpy()) / np.maximum(scale, 1e-30)) < 4e-6
+
+
+def test_fused_link_gradient_and_slot_lists(engine, torch_mod):
+    """sglm_link_update writing R as packed bf16 pieces for a slot list, then
+    sglm_xtr_bits_packed scattering G to those slots == the unfused path (f32 R, split, X^T R);
+    the line-search sums over a slot list == the same rows of the all-slot call (bitwise)."""
+    torch = torch_mod
+    from sglm_hip import _lib, synth
+    s = synth.make(N=40000, m=12, L=4, rho=0.08, seed=71)
+    d = engine.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
+    rng = np.random.default_rng(72)
+    masks = [(rng.random(s.N) < 0.8).astype(np.uint8), np.ones(s.N, np.uint8)]
+    prob = engine.Problem(d, [s.y, np.roll(s.y, 7)], masks)
+    B = 40
+    fr = torch.from_numpy(rng.integers(0, 2, B).astype(np.int32)).cuda()
+    fm = torch.from_numpy(rng.integers(0, 2, B).astype(np.int32)).cuda()
+    eta = torch.zeros((B, d.ld), dtype=torch.float32, device="cuda")
+    eta[:, : s.N] = torch.from_numpy(rng.normal(-1.0, 0.5, (B, s.N)).astype(np.float32))
+    W = torch.zeros_like(eta)
+    R = torch.zeros_like(eta)
+    _lib.call("sglm_link_update", 1, 1.0, d.n, d.ld, B, None, eta.data_ptr(), prob.Y.data_ptr(),
+              prob.M.data_ptr(), fr.data_ptr(), fm.data_ptr(), W.data_ptr(), R.data_ptr(), None, 0)
+    G = torch.zeros((B, d.P), dtype=torch.float64, device="cuda")
+    w = torch.empty(_lib.query("sglm_xtr_bits_work_bytes", d.P, B, d.ld), dtype=torch.uint8,
+                    device="cuda")
+    _lib.call("sglm_xtr_bits", d.cbits_full().data_ptr(), d.ld, d.P, d.n, R.data_ptr(), B,
+              G.data_ptr(), w.data_ptr(), 0)
+    slots = np.array([3, 39, 0, 21, 22, 8, 30], dtype=np.int32)
+    sl = torch.from_numpy(slots).cuda()
+    ns = len(slots)
+    W2 = torch.full_like(W, float("nan"))
+    Rp = torch.empty(3 * 32 * d.ld, dtype=torch.bfloat16, device="cuda")
+    _lib.call("sglm_link_update", 1, 1.0, d.n, d.ld, ns, sl.data_ptr(), eta.data_ptr(),
+              prob.Y.data_ptr(), prob.M.data_ptr(), fr.data_ptr(), fm.data_ptr(), W2.data_ptr(),
+              None, Rp.data_ptr(), 0)
+    G2 = torch.full_like(G, float("nan"))
+    w2 = torch.empty(_lib.query("sglm_xtr_bits_packed_work_bytes", d.P, ns, d.ld),
+                     dtype=torch.uint8, device="cuda")
+    _lib.call("sglm_xtr_bits_packed", d.cbits_full().data_ptr(), d.ld, d.P, d.n, Rp.data_ptr(),
+              ns, sl.data_ptr(), G2.data_ptr(), w2.data_ptr(), 0)
+    X = d.xb.double().cpu().numpy()
+    scale = np.abs(R.double().cpu().numpy()) @ np.abs(X.T)
+    for k in slots:
+        assert torch.equal(W2[k], W[k]), k
+        err = np.abs(G2[k].cpu().numpy() - G[k].cpu().numpy()) / np.maximum(scale[k], 1e-30)
+        assert np.max(err) < 4e-6, k
+    assert torch.isnan(G2[1]).all() and torch.isnan(W2[1]).all()
+    # line-search sums and drift over a slot list
+    deta = torch.zeros_like(eta)
+    deta[:, : s.N] = torch.from_numpy(rng.normal(0, 0.1, (B, s.N)).astype(np.float32))
+    tv = torch.tensor([0.0, 1.0, 0.5, 0.25, 0.125], dtype=torch.float32, device="cuda")
+    wk = torch.empty(_lib.query("sglm_rowsum_work_bytes", B, 8, d.n), dtype=torch.uint8,
+                     device="cuda")
+    L = torch.zeros(B * 5, dtype=torch.float64, device="cuda")
+    dm = torch.zeros(B, dtype=torch.float32, device="cuda")
+    _lib.call("sglm_loss_trials_max", 1, 1.0, d.n, d.ld, B, None, eta.data_ptr(), deta.data_ptr(),
+              prob.Y.data_ptr(), prob.M.data_ptr(), fr.data_ptr(), fm.data_ptr(), tv.data_ptr(), 5,
+              L.data_ptr(), dm.data_ptr(), wk.data_ptr(), 0)
+    L2 = torch.zeros(ns * 5, dtype=torch.float64, device="cuda")
+    dm2 = torch.zeros(ns, dtype=torch.float32, device="cuda")
+    _lib.call("sglm_loss_trials_max", 1, 1.0, d.n, d.ld, ns, sl.data_ptr(), eta.data_ptr(),
+              deta.data_ptr(), prob.Y.data_ptr(), prob.M.data_ptr(), fr.data_ptr(), fm.data_ptr(),
+              tv.data_ptr(), 5, L2.data_ptr(), dm2.data_ptr(), wk.data_ptr(), 0)
+    Lh, L2h = L.view(B, 5).cpu().numpy(), L2.view(ns, 5).cpu().numpy()
+    assert np.array_equal(L2h, Lh[slots]) and np.array_equal(dm2.cpu().numpy(), dm.cpu().numpy()[slots])
+    # eta axpy over the slot list
+    st = torch.from_numpy(rng.random(ns).astype(np.float32)).cuda()
+    e2 = eta.clone()
+    _lib.call("sglm_eta_axpy", d.n, d.ld, ns, sl.data_ptr(), st.data_ptr(), deta.data_ptr(),
+              e2.data_ptr(), 0)
+    for q, k in enumerate(slots):
+        # (the kernel may contract to one FMA: compare to f32 rounding)
+        assert torch.allclose(e2[k, : s.N], eta[k, : s.N] + st[q] * deta[k, : s.N],
+                              rtol=1e-6, atol=1e-7), k
+    assert torch.equal(e2[1], eta[1])
