@@ -162,14 +162,17 @@ int sglm_syrk_cbits(const int64_t* desc, int32_t P, const int32_t* fits, int32_t
 int sglm_pack_bits_t(const uint16_t* Xb, int64_t ld, int32_t P, uint32_t* out,
                      int32_t* nonbinary, sglm_stream_t stream);
 
-/* eta[k] = X beta[k] (as sglm_gemv_eta) for a 0/1 design given as sglm_pack_bits_t planes:
- * beta split into three bf16 pieces (exact), bf16 MFMA with f32 accumulation, for the B slots
- * k = slots[q] (q < B; all k < B when slots is NULL).  Writes all ld rows of eta (padding
- * rows: 0).  work: sglm_eta_bits_work_bytes(P, B) bytes.
+/* eta[k] = X beta[k] (as sglm_gemv_eta) for a 0/1 design given as sglm_pack_bits_t planes,
+ * bf16 MFMA with f32 accumulation, for the B slots k = slots[q] (q < B; all k < B when slots
+ * is NULL).  exact = 1: beta split into three bf16 pieces (exact products).  exact = 0 (a
+ * Newton direction): beta[k] is rounded to bf16 IN PLACE and X times the rounded vector is
+ * computed (one piece, a third of the MFMA work) -- the caller steps with the rounded
+ * direction, so the predictor stays X beta.  Writes all ld rows of eta (padding rows: 0).
+ * work: sglm_eta_bits_work_bytes(P, B) bytes.
  * Replaces X @ coef (backend/sglm.py:347 -> sklearn glm.py:350). */
 size_t sglm_eta_bits_work_bytes(int32_t P, int32_t B);
-int sglm_gemv_eta_bits(const uint32_t* rbits, int64_t ld, int32_t P, const float* beta,
-                       int32_t B, const int32_t* slots, float* eta, void* work,
+int sglm_gemv_eta_bits(const uint32_t* rbits, int64_t ld, int32_t P, float* beta, int32_t B,
+                       const int32_t* slots, int32_t exact, float* eta, void* work,
                        sglm_stream_t stream);
 
 /* g[k] = X^T R[k] (as sglm_xtr, float64 out) for a 0/1 design given as its identity-row

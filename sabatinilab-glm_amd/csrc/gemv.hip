@@ -58,51 +58,70 @@ __global__ void __launch_bounds__(256) split3_kernel(const float* __restrict__ s
     }
 }
 
+// One-piece form of the operand for Newton directions: out[f][e] = bf16(src[rows[f]][e]) and
+// the source row is overwritten with that bf16 value, so the caller updates its coefficients
+// with exactly the direction whose X d the kernel computes (the predictor stays X beta).
+__global__ void __launch_bounds__(256) round1_kernel(float* __restrict__ src, int64_t len,
+                                                     int32_t B, int32_t Bp,
+                                                     const int32_t* __restrict__ rows,
+                                                     __bf16* __restrict__ out) {
+    const int64_t total = (int64_t)Bp * len;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * 256) {
+        const int64_t f = e / len;
+        __bf16 v = (__bf16)0.0f;
+        if (f < B) {
+            float* q = src + (rows ? (int64_t)rows[f] : f) * len + (e - f * len);
+            v = (__bf16)*q;
+            *q = (float)v;
+        }
+        out[e] = v;
+    }
+}
+
+template <int NP>
 struct StepE {
     u32x2 b[4];          // row bits of the 4 row tiles
-    u32x4 a[3][4];       // piece x sub-step: 8 bf16 of this lane's fit
+    u32x4 a[NP][4];      // piece x sub-step: 8 bf16 of this lane's fit
 };
 
-__device__ __forceinline__ void loadE(StepE& t, g_uint2* pb, g_uint4* pa, int64_t ld,
+template <int NP>
+__device__ __forceinline__ void loadE(StepE<NP>& t, g_uint2* pb, g_uint4* pa, int64_t ld,
                                       int64_t pstride, int s) {
 #pragma unroll
     for (int n = 0; n < 4; ++n) t.b[n] = gld2(pb + (int64_t)s * ld + 32 * n);
 #pragma unroll
-    for (int pc = 0; pc < 3; ++pc)
+    for (int pc = 0; pc < NP; ++pc)
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) t.a[pc][ks] = gld4(pa + pc * pstride + s * 8 + 2 * ks);
 }
 
-__device__ __forceinline__ void waitE(StepE& t) {
-    asm volatile("s_waitcnt vmcnt(0)"
-                 : "+v"(t.b[0]), "+v"(t.b[1]), "+v"(t.b[2]), "+v"(t.b[3]), "+v"(t.a[0][0]),
-                   "+v"(t.a[0][1]), "+v"(t.a[0][2]), "+v"(t.a[0][3]), "+v"(t.a[1][0]),
-                   "+v"(t.a[1][1]), "+v"(t.a[1][2]), "+v"(t.a[1][3]), "+v"(t.a[2][0]),
-                   "+v"(t.a[2][1]), "+v"(t.a[2][2]), "+v"(t.a[2][3])
-                 :
-                 : "memory");
+// wait until at most `keep` loads are in flight, then tie the step's registers
+template <int NP>
+__device__ __forceinline__ void waitE(StepE<NP>& t, bool all) {
+    if (all)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (NP == 3)
+        asm volatile("s_waitcnt vmcnt(32)" ::: "memory");      // two later steps of 16 loads
+    else
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");      // two later steps of 8 loads
+#pragma unroll
+    for (int n = 0; n < 4; ++n) asm volatile("" : "+v"(t.b[n]));
+#pragma unroll
+    for (int pc = 0; pc < NP; ++pc)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) asm volatile("" : "+v"(t.a[pc][ks]));
 }
 
-// all but the youngest 32 loads (two later steps of 16 loads each) have landed: the step
-// whose registers are tied here is complete (3-stage ring, two steps in flight)
-__device__ __forceinline__ void waitE32(StepE& t) {
-    asm volatile("s_waitcnt vmcnt(32)"
-                 : "+v"(t.b[0]), "+v"(t.b[1]), "+v"(t.b[2]), "+v"(t.b[3]), "+v"(t.a[0][0]),
-                   "+v"(t.a[0][1]), "+v"(t.a[0][2]), "+v"(t.a[0][3]), "+v"(t.a[1][0]),
-                   "+v"(t.a[1][1]), "+v"(t.a[1][2]), "+v"(t.a[1][3]), "+v"(t.a[2][0]),
-                   "+v"(t.a[2][1]), "+v"(t.a[2][2]), "+v"(t.a[2][3])
-                 :
-                 : "memory");
-}
-
-__device__ __forceinline__ void mmaE(const StepE& t, int h, f32x16 (&acc)[3][4]) {
+template <int NP>
+__device__ __forceinline__ void mmaE(const StepE<NP>& t, int h, f32x16 (&acc)[NP][4]) {
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
         bf16x8 bx[4];
 #pragma unroll
         for (int n = 0; n < 4; ++n) bx[n] = frag_two(t.b[n], ks, h);
 #pragma unroll
-        for (int pc = 0; pc < 3; ++pc) {
+        for (int pc = 0; pc < NP; ++pc) {
             const bf16x8 a = __builtin_bit_cast(bf16x8, t.a[pc][ks]);
 #pragma unroll
             for (int n = 0; n < 4; ++n)
@@ -111,6 +130,8 @@ __device__ __forceinline__ void mmaE(const StepE& t, int h, f32x16 (&acc)[3][4])
     }
 }
 
+// NP = 3: beta as three bf16 pieces (exact); NP = 1: one bf16 piece (a rounded direction)
+template <int NP>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 eta_bits_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
                 const __bf16* __restrict__ Dp, int32_t Bp, int32_t B,
@@ -123,46 +144,48 @@ eta_bits_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
     const int64_t pstride = (int64_t)Bp * P / 8;           // one piece plane, in uint4
     const int nsteps = P / 64;
 
-    f32x16 acc[3][4];
+    f32x16 acc[NP][4];
 #pragma unroll
-    for (int pc = 0; pc < 3; ++pc)
+    for (int pc = 0; pc < NP; ++pc)
 #pragma unroll
         for (int n = 0; n < 4; ++n) acc[pc][n] = (f32x16){};
 
     // 3-stage register ring: the loads of step s+2 are issued before step s's MFMAs, so two
     // steps' L2 round trips overlap the MFMA work (clamped duplicate loads at the tail)
-    StepE A, Bs, C;
+    StepE<NP> A, Bs, C;
     const int last = nsteps - 1;
     loadE(A, pb, pa, ld, pstride, 0);
     loadE(Bs, pb, pa, ld, pstride, 1 < last ? 1 : last);
     for (int s = 0; s < nsteps; s += 3) {
         loadE(C, pb, pa, ld, pstride, s + 2 < last ? s + 2 : last);
-        waitE32(A);
+        waitE(A, false);
         __builtin_amdgcn_sched_barrier(0);
         mmaE(A, h, acc);
         __builtin_amdgcn_sched_barrier(0);
         loadE(A, pb, pa, ld, pstride, s + 3 < last ? s + 3 : last);
-        waitE32(Bs);
+        waitE(Bs, false);
         __builtin_amdgcn_sched_barrier(0);
         if (s + 1 < nsteps) mmaE(Bs, h, acc);
         __builtin_amdgcn_sched_barrier(0);
         loadE(Bs, pb, pa, ld, pstride, s + 4 < last ? s + 4 : last);
-        waitE32(C);
+        waitE(C, false);
         __builtin_amdgcn_sched_barrier(0);
         if (s + 2 < nsteps) mmaE(C, h, acc);
         __builtin_amdgcn_sched_barrier(0);
     }
-    waitE(A);
-    waitE(Bs);
+    waitE(A, true);
+    waitE(Bs, true);
 
 #pragma unroll
     for (int n = 0; n < 4; ++n)
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             const int f = g * 32 + (j & 3) + 8 * (j >> 2) + 4 * h;
-            if (f < B)
-                eta[(int64_t)(slots ? slots[f] : f) * ld + row0 + n * 32 + r] =
-                    0.5f * ((acc[0][n][j] + acc[1][n][j]) + acc[2][n][j]);
+            if (f < B) {
+                float v = acc[0][n][j];
+                if constexpr (NP == 3) v = (v + acc[1][n][j]) + acc[2][n][j];
+                eta[(int64_t)(slots ? slots[f] : f) * ld + row0 + n * 32 + r] = 0.5f * v;
+            }
         }
 }
 
@@ -343,8 +366,8 @@ size_t sglm_eta_bits_work_bytes(int32_t P, int32_t B) {
     return (size_t)3 * (size_t)Bp * (size_t)P * 2;
 }
 
-int sglm_gemv_eta_bits(const uint32_t* rbits, int64_t ld, int32_t P, const float* beta,
-                       int32_t B, const int32_t* slots, float* eta, void* work,
+int sglm_gemv_eta_bits(const uint32_t* rbits, int64_t ld, int32_t P, float* beta,
+                       int32_t B, const int32_t* slots, int32_t exact, float* eta, void* work,
                        sglm_stream_t stream) {
     if (B <= 0) return SGLM_OK;
     if (!rbits || !beta || !eta || !work || ld % 256 || P % 256) {
@@ -355,12 +378,22 @@ int sglm_gemv_eta_bits(const uint32_t* rbits, int64_t ld, int32_t P, const float
     hipStream_t s = as_stream(stream);
     __bf16* Dp = reinterpret_cast<__bf16*>(work);
     const int64_t total = (int64_t)Bp * P;
-    split3_kernel<<<(unsigned)((total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048), 256, 0,
-                    s>>>(beta, P, B, Bp, slots, Dp);
-    int st = check_launch("split3_kernel");
-    if (st) return st;
-    eta_bits_kernel<<<dim3((unsigned)(ld / 128), (unsigned)(Bp / 32)), 64, 0, s>>>(
-        reinterpret_cast<const u32x2*>(rbits), ld, P, Dp, Bp, B, slots, eta);
+    const unsigned gs = (unsigned)((total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048);
+    const dim3 grid((unsigned)(ld / 128), (unsigned)(Bp / 32));
+    int st;
+    if (exact) {
+        split3_kernel<<<gs, 256, 0, s>>>(beta, P, B, Bp, slots, Dp);
+        st = check_launch("split3_kernel");
+        if (st) return st;
+        eta_bits_kernel<3><<<grid, 64, 0, s>>>(reinterpret_cast<const u32x2*>(rbits), ld, P, Dp,
+                                               Bp, B, slots, eta);
+    } else {
+        round1_kernel<<<gs, 256, 0, s>>>(beta, P, B, Bp, slots, Dp);
+        st = check_launch("round1_kernel");
+        if (st) return st;
+        eta_bits_kernel<1><<<grid, 64, 0, s>>>(reinterpret_cast<const u32x2*>(rbits), ld, P, Dp,
+                                               Bp, B, slots, eta);
+    }
     return check_launch("eta_bits_kernel");
 }
 

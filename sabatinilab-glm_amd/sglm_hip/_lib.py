@@ -39,7 +39,7 @@ SIGNATURES = {
     "sglm_syrk_cbits": (C.c_int, [_vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp]),
     "sglm_pack_bits_t": (C.c_int, [_vp, _i64, _i32, _vp, _vp, _vp]),
     "sglm_eta_bits_work_bytes": (_sz, [_i32, _i32]),
-    "sglm_gemv_eta_bits": (C.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _vp, _vp, _vp]),
+    "sglm_gemv_eta_bits": (C.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _i32, _vp, _vp, _vp]),
     "sglm_xtr_bits_work_bytes": (_sz, [_i32, _i32, _i64]),
     "sglm_xtr_bits": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _i32, _vp, _vp, _vp]),
     "sglm_xtr_bits_packed_work_bytes": (_sz, [_i32, _i32, _i64]),

@@ -247,9 +247,11 @@ class Design:
             _lib.call("sglm_xtr", _p(self.xg), self.xtype, self.ld, self.P, self.n, _p(R), B,
                       _p(g_out), _p(w), st)
 
-    def eta(self, beta_dev, out=None, slots=None):
+    def eta(self, beta_dev, out=None, slots=None, direction=False):
         """eta[k] = X beta[k] for a (B, P) f32 device tensor; with ``slots`` (int32 device
-        tensor) only those rows k (the rest of ``out`` is left as is)."""
+        tensor) only those rows k (the rest of ``out`` is left as is).  ``direction``: beta
+        holds Newton directions, which are rounded to bf16 in place (0/1 designs) and X times
+        the rounded directions is returned -- the caller must step with the rounded values."""
         B = beta_dev.shape[0]
         if out is None:
             out = torch.empty((B, self.ld), dtype=torch.float32, device=self.device)
@@ -257,7 +259,7 @@ class Design:
             nb = B if slots is None else int(slots.numel())
             work = _work(_lib.query("sglm_eta_bits_work_bytes", self.P, nb), self.device, "eta")
             _lib.call("sglm_gemv_eta_bits", _p(self.rbits), self.ld, self.P, _p(beta_dev), nb,
-                      _p(slots), _p(out), _p(work), _stream())
+                      _p(slots), int(not direction), _p(out), _p(work), _stream())
         else:
             _lib.call("sglm_gemv_eta", _p(self.xg), self.xtype, self.ld, self.P, self.n,
                       _p(beta_dev), B, _p(out), _stream())
@@ -901,7 +903,10 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                       int(ali.size), _p(bf.gtot), _p(rscale_d), _p(bf.delta), _p(bf.frozen), B,
                       _p(bf.cwork), st)
         factored = True
-        d.eta(bf.delta, bf.deta, slots=act_d)
+        # the directions are rounded to bf16 in place (X d on one MFMA piece); the step below
+        # uses the rounded values, so eta stays X beta and the fixed point (exact gradient) is
+        # unchanged -- the rounding only perturbs the Newton direction by 2^-9 relative
+        d.eta(bf.delta, bf.deta, slots=act_d, direction=True)
         delta_h[:B].copy_(bf.delta[:B], non_blocking=True)
         t0 = tick("it_solve_eta", t0)
         # ---- line search (rows of L and dmax: active fits in slot order)
@@ -1037,7 +1042,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
     return res, bf.eta
 
 
-IRLS_GROUPS = int(__import__("os").environ.get("SGLM_IRLS_GROUPS", "2"))
+IRLS_GROUPS = int(__import__("os").environ.get("SGLM_IRLS_GROUPS", "1"))
 IRLS_GROUP_MIN = int(__import__("os").environ.get("SGLM_IRLS_GROUP_MIN", "24"))            # fits per group below which the batch is not split
 
 

@@ -399,14 +399,14 @@ def test_eta_bits_matches_float64(engine, torch_mod):
     out = torch.full((B, d.ld), float("nan"), dtype=torch.float32, device="cuda")
     work = torch.empty(_lib.query("sglm_eta_bits_work_bytes", d.P, B), dtype=torch.uint8,
                        device="cuda")
-    _lib.call("sglm_gemv_eta_bits", d.rbits.data_ptr(), d.ld, d.P, bd.data_ptr(), B, None,
+    _lib.call("sglm_gemv_eta_bits", d.rbits.data_ptr(), d.ld, d.P, bd.data_ptr(), B, None, 1,
               out.data_ptr(), work.data_ptr(), 0)
     # a slot list computes exactly those rows (bitwise: each fit's column is independent) and
     # leaves the others untouched
     sl = torch.tensor([36, 0, 17, 5], dtype=torch.int32, device="cuda")
     out_s = torch.full_like(out, float("nan"))
     _lib.call("sglm_gemv_eta_bits", d.rbits.data_ptr(), d.ld, d.P, bd.data_ptr(), 4,
-              sl.data_ptr(), out_s.data_ptr(), work.data_ptr(), 0)
+              sl.data_ptr(), 1, out_s.data_ptr(), work.data_ptr(), 0)
     for k in (36, 0, 17, 5):
         assert torch.equal(out_s[k], out[k]), k
     assert torch.isnan(out_s[1]).all()
@@ -421,6 +421,18 @@ def test_eta_bits_matches_float64(engine, torch_mod):
     assert np.max(np.abs(got - ref) / np.maximum(scale, 1e-30)) < 2e-6
     assert not got[:, s.N + 1:].any()                     # padding rows are exactly 0
     assert np.max(np.abs(got - ref_valu.cpu().numpy()) / np.maximum(scale, 1e-30)) < 2e-6
+    # direction mode: the selected rows of beta are rounded to bf16 in place and X times the
+    # rounded rows is returned (one piece); other rows of beta are untouched
+    bd2 = bd.clone()
+    out_r = torch.full_like(out, float("nan"))
+    _lib.call("sglm_gemv_eta_bits", d.rbits.data_ptr(), d.ld, d.P, bd2.data_ptr(), 4,
+              sl.data_ptr(), 0, out_r.data_ptr(), work.data_ptr(), 0)
+    for k in (36, 0, 17, 5):
+        assert torch.equal(bd2[k], bd[k].to(torch.bfloat16).float()), k
+        rk = bd2[k].double().cpu().numpy() @ X
+        sk = np.abs(bd2[k].double().cpu().numpy()) @ np.abs(X)
+        assert np.max(np.abs(out_r[k].cpu().numpy() - rk) / np.maximum(sk, 1e-30)) < 2e-6, k
+    assert torch.equal(bd2[1], bd[1]) and torch.isnan(out_r[1]).all()
 
 
 def test_compact_bits_equals_pack_bits_rows(engine, torch_mod):
