@@ -253,6 +253,17 @@ int sglm_chol_solve_alias(const float* H, int32_t P, const int32_t* fits, const 
                           int32_t nact, const double* g, const float* rscale, float* delta,
                           const uint8_t* frozen, int32_t B, void* work, sglm_stream_t stream);
 
+/* Statistics of every (row mask, response) pair, one float64 pass: out[r][f][0..4] =
+ * { sum m, sum m (y - K[r]), sum m (y - K[r])^2, sum m c(y), min over m > 0 of y } with M
+ * [F][ldm] uint8 multiplicities, Y [R][n] float64, K a per-response shift (e.g. the mean of y),
+ * c the half-Tweedie loss constant of `power` (sklearn constant_to_optimal_zero; power < 0:
+ * not computed, 0).  The CV scores (R^2 / D^2 / mse, backend/sglm.py:150-184) and sklearn's
+ * y-range check need only these.  work: sglm_mask_stats_work_bytes(F, R, n). */
+size_t sglm_mask_stats_work_bytes(int32_t F, int32_t R, int64_t n);
+int sglm_mask_stats(const uint8_t* M, int64_t ldm, int32_t F, const double* Y, int32_t R,
+                    int64_t n, const double* K, double power, double* out, void* work,
+                    sglm_stream_t stream);
+
 /* Line search: out[q][j] = sum_i M[m][i] * loss(y_i, eta_i + t[j] * deta_i) (float64),
  * for j < T, over fit slot k = slots[q] (q when slots is NULL), q < B.
  * `work`: sglm_rowsum_work_bytes(B, T, n). */

@@ -425,6 +425,70 @@ __global__ void __launch_bounds__(256) eta_pair_absmax_kernel(
     }
 }
 
+// Statistics of every (mask f, response r) pair in one pass (float64, deterministic two-level
+// reduction): count = sum m, sum m (y - K_r), sum m (y - K_r)^2, min over m > 0 of y and, when
+// power >= 0, sum m c_power(y) with c the half-Tweedie loss constant (sklearn
+// constant_to_optimal_zero).  K_r is a per-response shift that keeps the centred sums exact.
+constexpr int kStat = 5;
+__device__ __forceinline__ double tweedie_const(double power, double y) {
+    if (power == 0.0) return -0.5 * y * y;
+    if (power == 1.0) return (y > 0.0 ? y * log(y) : 0.0) - y;
+    if (power == 2.0) return -log(y) - 1.0;
+    return pow(fmax(y, 0.0), 2.0 - power) / (1.0 - power) / (2.0 - power);
+}
+
+__global__ void __launch_bounds__(256) mask_stats_kernel(const uint8_t* __restrict__ M,
+                                                         const double* __restrict__ Y,
+                                                         const double* __restrict__ K,
+                                                         int64_t n, int64_t ldm, int32_t F,
+                                                         double power,
+                                                         double* __restrict__ part) {
+    __shared__ double sh[4];
+    const int f = blockIdx.y, r = blockIdx.z;
+    const uint8_t* m = M + (int64_t)f * ldm;
+    const double* y = Y + (int64_t)r * n;
+    const double kr = K[r];
+    double a[kStat - 1] = {0.0, 0.0, 0.0, 0.0};
+    double mn = INFINITY;
+    const int64_t i0 = (int64_t)blockIdx.x * kRowChunk;
+    const int64_t i1 = min(i0 + kRowChunk, n);
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += 256) {
+        const double w = (double)m[i];
+        if (w == 0.0) continue;
+        const double yi = y[i], d = yi - kr;
+        a[0] += w;
+        a[1] += w * d;
+        a[2] += w * d * d;
+        if (power >= 0.0) a[3] += w * tweedie_const(power, yi);
+        mn = fmin(mn, yi);
+    }
+    const int64_t nch = gridDim.x;
+    double* out = part + (((int64_t)r * F + f) * kStat) * nch + blockIdx.x;
+    for (int q = 0; q < kStat - 1; ++q) {
+        const double v = block_sum_d(a[q], sh);
+        if (threadIdx.x == 0) out[q * nch] = v;
+    }
+    for (int o = 32; o > 0; o >>= 1) mn = fmin(mn, __shfl_xor(mn, o, 64));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = mn;
+    __syncthreads();
+    if (threadIdx.x == 0) out[(kStat - 1) * nch] = fmin(fmin(sh[0], sh[1]), fmin(sh[2], sh[3]));
+}
+
+__global__ void __launch_bounds__(256) mask_stats_reduce(const double* __restrict__ part,
+                                                         int64_t rows, int32_t nch,
+                                                         double* __restrict__ out) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= rows) return;
+    const bool is_min = e % kStat == kStat - 1;
+    double s = is_min ? INFINITY : 0.0;
+    for (int c = 0; c < nch; ++c) {
+        const double v = part[e * nch + c];
+        s = is_min ? fmin(s, v) : s + v;
+    }
+    out[e] = s;
+}
+
 static unsigned grid1(int64_t work, int64_t per_block, unsigned cap = 8192) {
     int64_t g = (work + per_block - 1) / per_block;
     if (g < 1) g = 1;
@@ -621,6 +685,29 @@ int sglm_eta_pair_absmax(int64_t n, int64_t ld, int32_t npairs, const int32_t* p
     dim3 grid(grid1(n, 256, 256), (unsigned)npairs);
     eta_pair_absmax_kernel<<<grid, 256, 0, s>>>(n, ld, pairs, M, fit_mask, eta, out);
     return check_launch("eta_pair_absmax_kernel");
+}
+
+size_t sglm_mask_stats_work_bytes(int32_t F, int32_t R, int64_t n) {
+    return (size_t)F * R * kStat * row_chunks(n) * sizeof(double);
+}
+
+int sglm_mask_stats(const uint8_t* M, int64_t ldm, int32_t F, const double* Y, int32_t R,
+                    int64_t n, const double* K, double power, double* out, void* work,
+                    sglm_stream_t stream) {
+    if (F <= 0 || R <= 0) return SGLM_OK;
+    if (!M || !Y || !K || !out || !work || ldm < n) {
+        set_error("sglm_mask_stats: bad args");
+        return SGLM_EINVAL;
+    }
+    hipStream_t s = as_stream(stream);
+    const int32_t nc = row_chunks(n);
+    mask_stats_kernel<<<dim3((unsigned)nc, (unsigned)F, (unsigned)R), 256, 0, s>>>(
+        M, Y, K, n, ldm, F, power, (double*)work);
+    int st = check_launch("mask_stats_kernel");
+    if (st) return st;
+    const int64_t rows = (int64_t)R * F * kStat;
+    mask_stats_reduce<<<grid1(rows, 256), 256, 0, s>>>((const double*)work, rows, nc, out);
+    return check_launch("mask_stats_reduce");
 }
 
 int sglm_score_sums(int32_t family, float power, int64_t n, int64_t ld, int32_t B,

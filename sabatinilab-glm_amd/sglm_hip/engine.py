@@ -375,9 +375,10 @@ class Problem:
         c = self._compact.get(mask)
         if c is None:
             d = self.design
-            rows = np.flatnonzero(self.masks[mask] > 0).astype(np.int32)
-            nr = int(rows.size)
-            rows_d = None if nr == d.n else torch.from_numpy(rows).to(d.device)
+            nr = int(np.count_nonzero(self.masks[mask]))
+            # the mask's row list, built on the device (no host pass, no synchronising upload)
+            rows_d = None if nr == d.n else torch.nonzero_static(
+                self.M[mask, :d.n], size=nr).view(-1).to(torch.int32)
             if rows_d is None and d.xbits is not None:
                 c = self._compact[mask] = (d.cbits_full(), nr, None)
                 return c
@@ -687,7 +688,13 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                 beta[k, p] = ym
     bf.dshift.copy_(torch.from_numpy(dsh))
     bf.beta.copy_(torch.from_numpy(beta.astype(np.float32)))
-    d.eta(bf.beta, bf.eta)
+    if all(r.coef0 is None for r in reqs):
+        # intercept-only start: X beta is the intercept on every row (exactly, as the MFMA
+        # product of the ones column would give it)
+        bf.eta[:, :n].copy_(bf.beta[:, p:p + 1].expand(B0, n))
+        bf.eta[:, n:].zero_()
+    else:
+        d.eta(bf.beta, bf.eta)
 
     const_hess = fam == FAM_SQUARED
     reuse_tol = 0.0 if const_hess else HESS_REUSE_TOL / max(1.0, abs(2.0 - power))

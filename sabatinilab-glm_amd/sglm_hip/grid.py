@@ -33,48 +33,47 @@ from .estimators import Objective
 class _MaskStats:
     """float64 statistics of every (response, mask) pair that the scores and the y-range check
     need: count, mean, sum of squares about the mean, min y; per Tweedie power the summed
-    loss constant and null deviance.  Computed in one batched float64 pass on the device
-    (the reference computes them per fold on host copies, backend/sglm.py:150-184, 388-408)."""
+    loss constant and null deviance.  One pass of sglm_mask_stats over the device masks and
+    responses per power (the reference computes them per fold on host copies,
+    backend/sglm.py:150-184, 388-408)."""
 
     def __init__(self, prob: E.Problem):
         import torch
-        self.torch = torch
+        from . import _lib
+        self.torch, self._lib = torch, _lib
+        self.prob = prob
         n, dev = prob.design.n, prob.design.device
-        self.Md = prob.M[:, :n].to(torch.float64)                      # F x n multiplicities
-        self.Yd = torch.from_numpy(np.stack(prob.ys)).to(dev)           # R x n float64
-        cnt = self.Md.sum(1)
-        # elementwise row sums, not a matmul: an F x n x R float64 GEMM with R ~ 1 runs as a
-        # slow library DGEMM
-        sy = torch.stack([(self.Md * self.Yd[r][None, :]).sum(1)
-                          for r in range(self.Yd.shape[0])], dim=1)     # F x R
-        mean = torch.where(cnt[:, None] > 0, sy / cnt.clamp_min(1)[:, None], 0.0)
-        R = self.Yd.shape[0]
-        sst = torch.empty_like(sy)
-        ymin = torch.empty_like(sy)
-        for r in range(R):
-            dev_r = self.Yd[r][None, :] - mean[:, r][:, None]
-            sst[:, r] = (self.Md * dev_r * dev_r).sum(1)
-            ymin[:, r] = torch.where(self.Md > 0, self.Yd[r][None, :], torch.inf).amin(1)
-        self.cnt, self.sy, self.mean = cnt.cpu().numpy(), sy.cpu().numpy(), mean.cpu().numpy()
-        self.sst, self.ymin = sst.cpu().numpy(), ymin.cpu().numpy()
+        ys = np.stack(prob.ys)
+        self.F, self.R, self.n = prob.M.shape[0], ys.shape[0], n
+        self.K = ys.mean(axis=1)                         # per-response shift
+        self.Yd = torch.from_numpy(ys).to(dev)           # R x n float64
+        self.Kd = torch.from_numpy(self.K).to(dev)
+        self.work = torch.empty(_lib.query("sglm_mask_stats_work_bytes", self.F, self.R, n),
+                                dtype=torch.uint8, device=dev)
+        st = self._pass(-1.0)                             # [R][F][5]
+        cnt = st[0, :, 0]
+        a1, a2 = st[:, :, 1].T, st[:, :, 2].T             # F x R
+        safe = np.where(cnt > 0, cnt, 1.0)[:, None]
+        self.cnt = cnt
+        self.sy = a1 + self.K[None, :] * cnt[:, None]
+        self.mean = np.where(cnt[:, None] > 0, self.sy / safe, 0.0)
+        self.sst = np.maximum(a2 - a1 * a1 / safe, 0.0) * (cnt[:, None] > 0)
+        self.ymin = st[:, :, 4].T
         self.c = {}
         self._const = {}
+
+    def _pass(self, power):
+        torch, _lib, prob = self.torch, self._lib, self.prob
+        out = torch.empty((self.R, self.F, 5), dtype=torch.float64, device=self.Yd.device)
+        _lib.call("sglm_mask_stats", prob.M.data_ptr(), prob.M.shape[1], self.F,
+                  self.Yd.data_ptr(), self.R, self.n, self.Kd.data_ptr(), float(power),
+                  out.data_ptr(), self.work.data_ptr(), E._stream())
+        return out.cpu().numpy()
 
     def _consts(self, power):
         """Summed per-row loss constant of each (mask, response) for one Tweedie power."""
         if power not in self._const:
-            torch = self.torch
-            y = self.Yd
-            if power == 1:
-                c = torch.where(y > 0, torch.xlogy(y, y), 0.0) - y
-            elif power == 2:
-                c = -torch.log(y) - 1
-            else:
-                c = torch.pow(y.clamp_min(0), 2 - power) / (1 - power) / (2 - power)
-            out = np.empty((self.Md.shape[0], y.shape[0]))
-            for r in range(y.shape[0]):
-                out[:, r] = torch.where(self.Md > 0, self.Md * c[r][None, :], 0.0).sum(1).cpu().numpy()
-            self._const[power] = out
+            self._const[power] = self._pass(float(power))[:, :, 3].T      # F x R
         return self._const[power]
 
     def get(self, r, m, power=None):
