@@ -89,11 +89,13 @@ int sglm_gemv_eta(const void* X, int32_t xtype, int64_t ld, int32_t P, int64_t n
  *   W[k][i] = M[m][i] * d2loss/deta2,   R[k][i] = M[m][i] * dloss/deta,   rows i < n.
  * Rows n <= i < ld are written as 0.  R (f32 per slot) and Rp may each be NULL (not both):
  * Rp receives R as three bf16 pieces hi + mid + lo == R, bf16 [3][Bp][ld] with
- * Bp = ceil(B/32)*32, row q = launch row -- the operand of sglm_xtr_bits_packed. */
+ * Bp = ceil(B/32)*32, row q = launch row -- the operand of sglm_xtr_bits_packed.
+ * deta (optional, with step[q]): first eta[k] += step[q] * deta[k] (the previous Newton
+ * step's predictor update, fused), then the link on the updated eta. */
 int sglm_link_update(int32_t family, float power, int64_t n, int64_t ld, int32_t B,
-                     const int32_t* slots, const float* eta, const float* Y, const uint8_t* M,
+                     const int32_t* slots, float* eta, const float* Y, const uint8_t* M,
                      const int32_t* fit_resp, const int32_t* fit_mask, float* W, float* R,
-                     void* Rp, sglm_stream_t stream);
+                     void* Rp, const float* step, const float* deta, sglm_stream_t stream);
 
 /* G[k][a] = sum_i X[a][i] * R[k][i] (float64 out; f32 MFMA partial sums, fixed-order
  * float64 reduction over row chunks).  `work`: sglm_xtr_work_bytes(P, B, n). */

@@ -24,7 +24,7 @@ SIGNATURES = {
                                    _i32, _vp, _vp]),
     "sglm_gemv_eta": (C.c_int, [_vp, _i32, _i64, _i32, _i64, _vp, _i32, _vp, _vp]),
     "sglm_link_update": (C.c_int, [_i32, _f32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
-                                   _vp, _vp, _vp, _vp]),
+                                   _vp, _vp, _vp, _vp, _vp, _vp]),
     "sglm_xtr_work_bytes": (_sz, [_i32, _i32, _i64]),
     "sglm_xtr": (C.c_int, [_vp, _i32, _i64, _i32, _i64, _vp, _i32, _vp, _vp, _vp]),
     "sglm_syrk_work_bytes": (_sz, [_i32, _i32, _i32]),

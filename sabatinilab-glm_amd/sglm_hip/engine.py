@@ -636,7 +636,7 @@ def syrk6_splits(wgs1: int, nsteps: int, nact: int, P: int, slots: int = 1024) -
     time) + the split-K slab traffic (write + reduce-read of splits x nact x P^2 floats)."""
     t_step = 2048 / 2.4e9                     # 64 MFMA x 32 cycles per K-step
     best, best_t = 1, None
-    for s in (1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64):
+    for s in range(1, 65):              # every factor: whole rounds of the 1024 wave slots
         if s > max(1, nsteps // 8):
             break
         if s < SYRK6_MIN_SPLIT and s < max(1, nsteps // 8):
@@ -712,11 +712,13 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
     # losses and the step's predictor drift come back together (pinned buffers, async copies)
     dmax_d = torch.zeros(B0, dtype=torch.float32, device=dev)
     dmax_h = _pinned("dmax", B0, torch.float32)
-    g_h = _pinned("g", B0 * P, torch.float64).view(B0, P)
-    delta_h = _pinned("delta", B0 * P, torch.float32).view(B0, P)
     L_h = _pinned("L", B0 * 8, torch.float64)
-    beta_pin = _pinned("beta", B0 * P, torch.float64).view(B0, P)
-    beta64_d = torch.zeros((B0, P), dtype=torch.float64, device=dev)
+    # the coefficients live on the device (float64); the host sees per-fit scalars only
+    beta64_d = torch.from_numpy(beta).to(dev)
+    ts_all = torch.from_numpy(np.concatenate([[0.0, 1.0, 0.5, 0.25, 0.125],
+                                              TV2.astype(np.float32)])).to(dev)
+    # fits still at their common start (same mask and response => bitwise equal Hessians)
+    fresh_start = np.array([r.coef0 is None for r in reqs])
     lamp_d = torch.from_numpy(lam[:, None] * penal).to(dev)        # lam * penalty mask
     gram_now = np.zeros(B0, dtype=bool)
     active = np.ones(B0, dtype=bool)
@@ -774,7 +776,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         form = rest[drift[rest] > reuse_tol]
         reps, dup = {}, []
         for k in form:
-            rk = reps.setdefault((reqs[k].mask, reqs[k].resp, beta[k].tobytes()), k)
+            rk = reps.setdefault((reqs[k].mask, reqs[k].resp, -1 if fresh_start[k] else k), k)
             if rk != k:
                 dup.append((k, rk))
         uniq = np.array(sorted(reps.values()), dtype=np.int32)
@@ -817,7 +819,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         ok = dist_c + drift[repl[cand]] <= xmask_tol
         ali, fail = cand[ok], cand[~ok]
         for k in fail:
-            rk = reps.setdefault((reqs[k].mask, reqs[k].resp, beta[k].tobytes()), k)
+            rk = reps.setdefault((reqs[k].mask, reqs[k].resp, -1 if fresh_start[k] else k), k)
             if rk != k:
                 dup.append((k, rk))
             else:
@@ -833,6 +835,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
     tick = stats.mark if (stats is not None and stats.trace_phases) else (lambda name, t: t)
     t0 = tick("irls_setup", time.perf_counter())
     plan = None
+    linked = None           # slot list whose link (and predictor update) is already enqueued
     for it in range(int(max_iter.max()) + 1):
         # every per-fit kernel runs over the active slots only (slot lists): no compaction,
         # so factors, predictors and the representatives' factors stay where they are
@@ -840,22 +843,20 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         na = int(act.size)
         if na == 0:
             break
-        act_d = up(act, np.int32)
+        act_d = linked if linked is not None else up(act, np.int32)
         if use_rp:
-            _lib.call("sglm_link_update", fam, power, n, ld, na, _p(act_d), _p(bf.eta),
-                      _p(prob.Y), _p(prob.M), _p(fit_resp), _p(fit_mask), _p(bf.W), None,
-                      _p(rp_buf), st)
+            if linked is None:
+                _lib.call("sglm_link_update", fam, power, n, ld, na, _p(act_d), _p(bf.eta),
+                          _p(prob.Y), _p(prob.M), _p(fit_resp), _p(fit_mask), _p(bf.W), None,
+                          _p(rp_buf), None, None, st)
             _lib.call("sglm_xtr_bits_packed", _p(d.cbits_full()), ld, P, n, _p(rp_buf), na,
                       _p(act_d), _p(bf.g), _p(gx_work), st)
         else:
             _lib.call("sglm_link_update", fam, power, n, ld, B, None, _p(bf.eta), _p(prob.Y),
-                      _p(prob.M), _p(fit_resp), _p(fit_mask), _p(bf.W), _p(bf.R), None, st)
+                      _p(prob.M), _p(fit_resp), _p(fit_mask), _p(bf.W), _p(bf.R), None, None,
+                      None, st)
             d.xtr(bf.R, B, bf.g)
-        bnp = beta_pin.numpy()
-        bnp[:B] = beta
-        beta64_d[:B].copy_(beta_pin[:B], non_blocking=True)
         torch.addcmul(bf.g[:B], lamp_d, beta64_d[:B], out=bf.gtot[:B])   # + lam * w
-        g_h[:B].copy_(bf.gtot[:B], non_blocking=True)
         t0 = tick("it_gradient", t0)
         # ---- Hessian
         gram_comp = np.zeros(B, dtype=bool)     # fits whose Gram is computed this iteration
@@ -914,39 +915,50 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         # uses the rounded values, so eta stays X beta and the fixed point (exact gradient) is
         # unchanged -- the rounding only perturbs the Newton direction by 2^-9 relative
         d.eta(bf.delta, bf.deta, slots=act_d, direction=True)
-        delta_h[:B].copy_(bf.delta[:B], non_blocking=True)
+        # per-fit scalars of the line search and the stopping rule, reduced on the device
+        # over the coefficients (no B x P array crosses to the host): g.d, the penalty terms
+        # lam|w|^2, 2 lam w.d, lam|d|^2, max|d| and max|w + t d| for every trial step t
+        act_i = up(act, np.int64)
+        d64 = bf.delta.index_select(0, act_i).double()
+        b64 = beta64_d.index_select(0, act_i)
+        lp = lamp_d.index_select(0, act_i)
+        sc = torch.empty((na, 5 + ts_all.numel()), dtype=torch.float64, device=dev)
+        sc[:, 0] = (bf.gtot.index_select(0, act_i) * d64).sum(1)
+        sc[:, 1] = (lp * b64 * b64).sum(1)
+        sc[:, 2] = (lp * b64 * d64).sum(1)
+        sc[:, 3] = (lp * d64 * d64).sum(1)
+        sc[:, 4] = d64.abs().amax(1)
+        sc[:, 5:] = (b64[:, None, :] + ts_all[None, :, None] * d64[:, None, :]).abs().amax(2)
         t0 = tick("it_solve_eta", t0)
-        # ---- line search (rows of L and dmax: active fits in slot order)
+        # ---- line search (rows of L, dmax and sc: active fits in slot order)
         _lib.call("sglm_loss_trials_max", fam, power, n, ld, na, _p(act_d), _p(bf.eta),
                   _p(bf.deta), _p(prob.Y), _p(prob.M), _p(fit_resp), _p(fit_mask), _p(tv1), 5,
                   _p(Ltr), _p(dmax_d), _p(xtr_work), st)
         L_h[: na * 5].copy_(Ltr[: na * 5], non_blocking=True)
         dmax_h[:na].copy_(dmax_d[:na], non_blocking=True)
+        sc_h = _pinned("sc", na * sc.shape[1], torch.float64)
+        sc_h.copy_(sc.view(-1), non_blocking=True)
         torch.cuda.current_stream().synchronize()              # the iteration's round trip
         up.synced()
-        g = g_h[:B].numpy()[act]
-        delta = np.zeros((B, P))
-        delta[act] = delta_h[:B].numpy()[act]
         L = L_h[: na * 5].numpy().reshape(na, 5).copy()
         dmaxeta = dmax_h[:na].numpy().astype(np.float64)
+        scn = sc_h.numpy().reshape(na, -1).copy()
+        gdir, A_, B_, C_, maxd = scn[:, 0], scn[:, 1], scn[:, 2], scn[:, 3], scn[:, 4]
+        maxb = scn[:, 5:]                       # max|w + t d| for t in TS_ALL
         ts = np.array([0.0, 1.0, 0.5, 0.25, 0.125])
-        da = delta[act]
-        gdir = np.sum(g * da, axis=1)
-        # penalty lam/2 |w + t d|^2 = lam/2 (A + 2 t Bq + t^2 C), vectorised over fits x trials
-        pen_a, beta_a, lam_a = penal[act], beta[act], lam[act]
-        pb, pd_ = pen_a * beta_a, pen_a * da
-        A_, B_, C_ = np.sum(pb * beta_a, 1), np.sum(pb * da, 1), np.sum(pd_ * da, 1)
 
         def objectives(Lm, tv):
-            return Lm + 0.5 * lam_a[:, None] * (A_[:, None] + 2 * tv[None, :] * B_[:, None]
-                                                + tv[None, :] ** 2 * C_[:, None])
+            return Lm + 0.5 * (A_[:, None] + 2 * tv[None, :] * B_[:, None]
+                               + tv[None, :] ** 2 * C_[:, None])
         step_a = np.zeros(na)
+        tix = np.zeros(na, dtype=np.int64)      # index of the chosen step in TS_ALL
         obj = objectives(L, ts)
         ok = ((obj[:, 1:] - obj[:, :1] <= ARMIJO_SIGMA * ts[None, 1:] * gdir[:, None]) |
               (np.abs(obj[:, 1:] - obj[:, :1]) <= 1e-13 * np.abs(obj[:, :1])))
         first = np.argmax(ok, axis=1)
         hit = ok[np.arange(na), first]
         step_a[hit] = ts[1:][first[hit]]
+        tix[hit] = 1 + first[hit]
         more = np.flatnonzero(~hit)                         # positions in act
         if more.size:
             sub_d = up(act[more], np.int32)
@@ -956,19 +968,20 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
             L2 = Ltr[: more.size * 7].view(more.size, 7).cpu().numpy()
             ts2 = TV2.astype(np.float32).astype(np.float64)
             obj0 = objectives(L[:, :1], np.zeros(1))[more]
-            o2 = (L2 + 0.5 * lam_a[more, None] * (A_[more, None] + 2 * ts2[None, :] * B_[more, None]
-                                                  + ts2[None, :] ** 2 * C_[more, None]))
+            o2 = L2 + 0.5 * (A_[more, None] + 2 * ts2[None, :] * B_[more, None]
+                             + ts2[None, :] ** 2 * C_[more, None])
             ok2 = o2 - obj0 <= ARMIJO_SIGMA * ts2[None, :] * gdir[more, None]
             f2 = np.argmax(ok2, axis=1)
             h2 = ok2[np.arange(more.size), f2]
             step_a[more[h2]] = ts2[f2[h2]]
+            tix[more[h2]] = 5 + f2[h2]
         t0 = tick("it_linesearch", t0)
-        # ---- update
-        beta[act] += step_a[:, None] * da
+        # ---- update (coefficients on the device: w += t d)
+        st_d = up(step_a, np.float64)
+        beta64_d.index_add_(0, act_i, st_d[:, None] * d64)
         if not const_hess:
             drift[act] += step_a * dmaxeta            # max_i |t d_eta_i| over the fit's rows
-        step_d = up(step_a, np.float32)
-        _lib.call("sglm_eta_axpy", n, ld, na, _p(act_d), _p(step_d), _p(bf.deta), _p(bf.eta), st)
+        fresh_start[act[step_a != 0.0]] = False
         n_iter[act] += 1
         if stats is not None:
             stats.newton_iters += 1
@@ -983,9 +996,9 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                                            + np.where(gram_now[act], pa ** 3 / 3, 0.0)
                                            + 4.0 * nr * pa + 2 * pa * pa))
             stats.gram_fit_iters += int(np.sum(gram_comp[act]))
-        scale = 1.0 + np.max(np.abs(beta[act]), axis=1)
-        relv = np.max(np.abs(step_a[:, None] * da), axis=1) / scale
-        prop = np.max(np.abs(da), axis=1) / scale      # the proposed Newton step
+        scale = 1.0 + maxb[np.arange(na), tix]         # 1 + max|w| after the step
+        relv = step_a * maxd / scale
+        prop = maxd / scale                            # the proposed Newton step
         stepa = step_a
         fresh = gram_now[act] | const_hess
         ls_fail = stepa == 0.0
@@ -1025,13 +1038,30 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
             stats.stops["line_search_failed"] += int(np.sum(stop_fail & (prop > tol)))
             stats.stops["max_iter"] += int(np.sum(out_of_iters))
             stats.stops["stale_factor_retry"] += int(np.sum(ls_fail & ~fresh))
-        if not const_hess and active.any():
+        # predictor update eta += t d_eta: fused into the next iteration's link for the fits
+        # that continue (0/1 designs), a plain axpy for the others
+        linked = None
+        nxt = np.flatnonzero(active)
+        if use_rp and nxt.size:
+            cont = active[act]
+            done = np.flatnonzero(~cont & (step_a != 0.0))
+            if done.size:
+                _lib.call("sglm_eta_axpy", n, ld, int(done.size), _p(up(act[done], np.int32)),
+                          _p(up(step_a[done], np.float32)), _p(bf.deta), _p(bf.eta), st)
+            linked = up(nxt, np.int32)
+            _lib.call("sglm_link_update", fam, power, n, ld, int(nxt.size), _p(linked),
+                      _p(bf.eta), _p(prob.Y), _p(prob.M), _p(fit_resp), _p(fit_mask), _p(bf.W),
+                      None, _p(rp_buf), _p(up(step_a[cont], np.float32)), _p(bf.deta), st)
+        else:
+            _lib.call("sglm_eta_axpy", n, ld, na, _p(act_d), _p(up(step_a, np.float32)),
+                      _p(bf.deta), _p(bf.eta), st)
+        if not const_hess and nxt.size:
             # the next iteration's Hessian decisions and their distances, enqueued behind
             # this iteration's predictor update (read back without a stall next iteration)
-            plan = hess_plan(np.flatnonzero(active))
+            plan = hess_plan(nxt)
         t0 = tick("it_update", t0)
 
-    out_beta[:] = beta
+    out_beta[:] = beta64_d.cpu().numpy()
     out_iter[:] = n_iter
     out_conv[:] = converged
     out_info[:] = bf.info[:B].cpu().numpy()

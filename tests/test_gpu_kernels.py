@@ -509,7 +509,8 @@ def test_fused_link_gradient_and_slot_lists(engine, torch_mod):
     W = torch.zeros_like(eta)
     R = torch.zeros_like(eta)
     _lib.call("sglm_link_update", 1, 1.0, d.n, d.ld, B, None, eta.data_ptr(), prob.Y.data_ptr(),
-              prob.M.data_ptr(), fr.data_ptr(), fm.data_ptr(), W.data_ptr(), R.data_ptr(), None, 0)
+              prob.M.data_ptr(), fr.data_ptr(), fm.data_ptr(), W.data_ptr(), R.data_ptr(), None, None,
+              None, 0)
     G = torch.zeros((B, d.P), dtype=torch.float64, device="cuda")
     w = torch.empty(_lib.query("sglm_xtr_bits_work_bytes", d.P, B, d.ld), dtype=torch.uint8,
                     device="cuda")
@@ -522,7 +523,7 @@ def test_fused_link_gradient_and_slot_lists(engine, torch_mod):
     Rp = torch.empty(3 * 32 * d.ld, dtype=torch.bfloat16, device="cuda")
     _lib.call("sglm_link_update", 1, 1.0, d.n, d.ld, ns, sl.data_ptr(), eta.data_ptr(),
               prob.Y.data_ptr(), prob.M.data_ptr(), fr.data_ptr(), fm.data_ptr(), W2.data_ptr(),
-              None, Rp.data_ptr(), 0)
+              None, Rp.data_ptr(), None, None, 0)
     G2 = torch.full_like(G, float("nan"))
     w2 = torch.empty(_lib.query("sglm_xtr_bits_packed_work_bytes", d.P, ns, d.ld),
                      dtype=torch.uint8, device="cuda")
@@ -563,3 +564,19 @@ def test_fused_link_gradient_and_slot_lists(engine, torch_mod):
         assert torch.allclose(e2[k, : s.N], eta[k, : s.N] + st[q] * deta[k, : s.N],
                               rtol=1e-6, atol=1e-7), k
     assert torch.equal(e2[1], eta[1])
+    # link with the fused predictor update == axpy, then link
+    e3 = eta.clone()
+    W3 = torch.zeros_like(W)
+    Rp3 = torch.empty_like(Rp)
+    _lib.call("sglm_link_update", 1, 1.0, d.n, d.ld, ns, sl.data_ptr(), e3.data_ptr(),
+              prob.Y.data_ptr(), prob.M.data_ptr(), fr.data_ptr(), fm.data_ptr(), W3.data_ptr(),
+              None, Rp3.data_ptr(), st.data_ptr(), deta.data_ptr(), 0)
+    W4 = torch.zeros_like(W)
+    Rp4 = torch.empty_like(Rp)
+    _lib.call("sglm_link_update", 1, 1.0, d.n, d.ld, ns, sl.data_ptr(), e2.data_ptr(),
+              prob.Y.data_ptr(), prob.M.data_ptr(), fr.data_ptr(), fm.data_ptr(), W4.data_ptr(),
+              None, Rp4.data_ptr(), None, None, 0)
+    for k in slots:
+        assert torch.equal(e3[k], e2[k]) and torch.equal(W3[k], W4[k]), k
+    nb = 3 * 32 * d.ld
+    assert torch.equal(Rp3.view(3, 32, d.ld)[:, :ns], Rp4.view(3, 32, d.ld)[:, :ns])
