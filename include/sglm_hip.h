@@ -255,6 +255,18 @@ int sglm_chol_solve_alias(const float* H, int32_t P, const int32_t* fits, const 
                           int32_t nact, const double* g, const float* rscale, float* delta,
                           const uint8_t* frozen, int32_t B, void* work, sglm_stream_t stream);
 
+/* Per-fit scalars of a Newton step for the B fits k = slots[q], float64 (one workgroup per
+ * fit): out[q][0..5+T) = { g.d, sum lam w^2, sum lam w d, sum lam d^2, max|d|,
+ * max|w + t[j] d| for j < T } over the P coordinates of g[k] (float64), beta[k] (float64),
+ * delta[k] (f32), lamp[k] (float64 penalty row).  The Armijo test and the stopping rule of
+ * sklearn's Newton solver (_newton_solver.py:201-260) need only these.  T <= 16. */
+int sglm_step_scalars(int32_t P, int32_t B, const int32_t* slots, const double* g,
+                      const double* beta, const float* delta, const double* lamp,
+                      const double* t, int32_t T, double* out, sglm_stream_t stream);
+/* beta[k] += step[q] * delta[k] for k = slots[q], q < B (float64 coefficients). */
+int sglm_step_update(int32_t P, int32_t B, const int32_t* slots, const double* step,
+                     const float* delta, double* beta, sglm_stream_t stream);
+
 /* Statistics of every (row mask, response) pair, one float64 pass: out[r][f][0..4] =
  * { sum m, sum m (y - K[r]), sum m (y - K[r])^2, sum m c(y), min over m > 0 of y } with M
  * [F][ldm] uint8 multiplicities, Y [R][n] float64, K a per-response shift (e.g. the mean of y),

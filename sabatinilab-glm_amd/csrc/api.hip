@@ -520,6 +520,64 @@ __global__ void __launch_bounds__(256) mask_stats_reduce(const double* __restric
     out[e] = s;
 }
 
+// Per-fit scalars of a Newton step, one workgroup per active fit k = slots[q] (float64): the
+// directional derivative g.d, the penalty terms sum lam w^2, sum lam w d, sum lam d^2 (lam =
+// the fit's penalty row), max |d| and, for every trial step t[j], max |w + t[j] d| (the scale
+// of the stopping rule after that step).  out[q][0..5+T).
+constexpr int kMaxStepT = 16;
+__global__ void __launch_bounds__(256) step_scalars_kernel(
+    int32_t P, const int32_t* __restrict__ slots, const double* __restrict__ g,
+    const double* __restrict__ beta, const float* __restrict__ delta,
+    const double* __restrict__ lamp, const double* __restrict__ t, int32_t T,
+    double* __restrict__ out) {
+    __shared__ double sh[4];
+    const int q = blockIdx.x, k = slots[q];
+    const double* gk = g + (int64_t)k * P;
+    const double* bk = beta + (int64_t)k * P;
+    const float* dk = delta + (int64_t)k * P;
+    const double* lk = lamp + (int64_t)k * P;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0, md = 0.0;
+    double mb[kMaxStepT];
+    double tv[kMaxStepT];
+    for (int j = 0; j < T; ++j) { mb[j] = 0.0; tv[j] = t[j]; }
+    for (int a = threadIdx.x; a < P; a += 256) {
+        const double d = (double)dk[a], b = bk[a], l = lk[a];
+        s0 += gk[a] * d;
+        s1 += l * b * b;
+        s2 += l * b * d;
+        s3 += l * d * d;
+        md = fmax(md, fabs(d));
+        for (int j = 0; j < T; ++j) mb[j] = fmax(mb[j], fabs(b + tv[j] * d));
+    }
+    double* o = out + (int64_t)q * (5 + T);
+    double v;
+    v = block_sum_d(s0, sh); if (threadIdx.x == 0) o[0] = v;
+    v = block_sum_d(s1, sh); if (threadIdx.x == 0) o[1] = v;
+    v = block_sum_d(s2, sh); if (threadIdx.x == 0) o[2] = v;
+    v = block_sum_d(s3, sh); if (threadIdx.x == 0) o[3] = v;
+    for (int j = -1; j < T; ++j) {
+        double m = j < 0 ? md : mb[j];
+        for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_xor(m, off, 64));
+        __syncthreads();
+        if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) o[5 + j] = fmax(fmax(sh[0], sh[1]), fmax(sh[2], sh[3]));
+    }
+}
+
+// beta[k] += step[q] * delta[k] for k = slots[q] (float64 coefficients, f32 direction)
+__global__ void __launch_bounds__(256) step_update_kernel(int32_t P,
+                                                          const int32_t* __restrict__ slots,
+                                                          const double* __restrict__ step,
+                                                          const float* __restrict__ delta,
+                                                          double* __restrict__ beta) {
+    const int q = blockIdx.x, k = slots[q];
+    const double t = step[q];
+    if (t == 0.0) return;
+    for (int a = threadIdx.x; a < P; a += 256)
+        beta[(int64_t)k * P + a] += t * (double)delta[(int64_t)k * P + a];
+}
+
 static unsigned grid1(int64_t work, int64_t per_block, unsigned cap = 8192) {
     int64_t g = (work + per_block - 1) / per_block;
     if (g < 1) g = 1;
@@ -716,6 +774,30 @@ int sglm_eta_pair_absmax(int64_t n, int64_t ld, int32_t npairs, const int32_t* p
     dim3 grid(grid1(n, 256, 256), (unsigned)npairs);
     eta_pair_absmax_kernel<<<grid, 256, 0, s>>>(n, ld, pairs, M, fit_mask, eta, out);
     return check_launch("eta_pair_absmax_kernel");
+}
+
+int sglm_step_scalars(int32_t P, int32_t B, const int32_t* slots, const double* g,
+                      const double* beta, const float* delta, const double* lamp,
+                      const double* t, int32_t T, double* out, sglm_stream_t stream) {
+    if (B <= 0) return SGLM_OK;
+    if (!slots || !g || !beta || !delta || !lamp || !t || !out || T < 0 || T > kMaxStepT) {
+        set_error("sglm_step_scalars: bad args (T=%d, max %d)", T, kMaxStepT);
+        return SGLM_EINVAL;
+    }
+    step_scalars_kernel<<<(unsigned)B, 256, 0, as_stream(stream)>>>(P, slots, g, beta, delta,
+                                                                    lamp, t, T, out);
+    return check_launch("step_scalars_kernel");
+}
+
+int sglm_step_update(int32_t P, int32_t B, const int32_t* slots, const double* step,
+                     const float* delta, double* beta, sglm_stream_t stream) {
+    if (B <= 0) return SGLM_OK;
+    if (!slots || !step || !delta || !beta) {
+        set_error("sglm_step_update: null pointer");
+        return SGLM_EINVAL;
+    }
+    step_update_kernel<<<(unsigned)B, 256, 0, as_stream(stream)>>>(P, slots, step, delta, beta);
+    return check_launch("step_update_kernel");
 }
 
 size_t sglm_mask_stats_work_bytes(int32_t F, int32_t R, int64_t n) {

@@ -717,6 +717,8 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
     beta64_d = torch.from_numpy(beta).to(dev)
     ts_all = torch.from_numpy(np.concatenate([[0.0, 1.0, 0.5, 0.25, 0.125],
                                               TV2.astype(np.float32)])).to(dev)
+    nts = int(ts_all.numel())
+    sc_d = torch.empty(B0 * (5 + nts), dtype=torch.float64, device=dev)
     # fits still at their common start (same mask and response => bitwise equal Hessians)
     fresh_start = np.array([r.coef0 is None for r in reqs])
     lamp_d = torch.from_numpy(lam[:, None] * penal).to(dev)        # lam * penalty mask
@@ -918,17 +920,9 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         # per-fit scalars of the line search and the stopping rule, reduced on the device
         # over the coefficients (no B x P array crosses to the host): g.d, the penalty terms
         # lam|w|^2, 2 lam w.d, lam|d|^2, max|d| and max|w + t d| for every trial step t
-        act_i = up(act, np.int64)
-        d64 = bf.delta.index_select(0, act_i).double()
-        b64 = beta64_d.index_select(0, act_i)
-        lp = lamp_d.index_select(0, act_i)
-        sc = torch.empty((na, 5 + ts_all.numel()), dtype=torch.float64, device=dev)
-        sc[:, 0] = (bf.gtot.index_select(0, act_i) * d64).sum(1)
-        sc[:, 1] = (lp * b64 * b64).sum(1)
-        sc[:, 2] = (lp * b64 * d64).sum(1)
-        sc[:, 3] = (lp * d64 * d64).sum(1)
-        sc[:, 4] = d64.abs().amax(1)
-        sc[:, 5:] = (b64[:, None, :] + ts_all[None, :, None] * d64[:, None, :]).abs().amax(2)
+        sc = sc_d[: na * (5 + nts)]
+        _lib.call("sglm_step_scalars", P, na, _p(act_d), _p(bf.gtot), _p(beta64_d), _p(bf.delta),
+                  _p(lamp_d), _p(ts_all), nts, _p(sc), st)
         t0 = tick("it_solve_eta", t0)
         # ---- line search (rows of L, dmax and sc: active fits in slot order)
         _lib.call("sglm_loss_trials_max", fam, power, n, ld, na, _p(act_d), _p(bf.eta),
@@ -936,8 +930,8 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                   _p(Ltr), _p(dmax_d), _p(xtr_work), st)
         L_h[: na * 5].copy_(Ltr[: na * 5], non_blocking=True)
         dmax_h[:na].copy_(dmax_d[:na], non_blocking=True)
-        sc_h = _pinned("sc", na * sc.shape[1], torch.float64)
-        sc_h.copy_(sc.view(-1), non_blocking=True)
+        sc_h = _pinned("sc", sc.numel(), torch.float64)
+        sc_h.copy_(sc, non_blocking=True)
         torch.cuda.current_stream().synchronize()              # the iteration's round trip
         up.synced()
         L = L_h[: na * 5].numpy().reshape(na, 5).copy()
@@ -977,8 +971,8 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
             tix[more[h2]] = 5 + f2[h2]
         t0 = tick("it_linesearch", t0)
         # ---- update (coefficients on the device: w += t d)
-        st_d = up(step_a, np.float64)
-        beta64_d.index_add_(0, act_i, st_d[:, None] * d64)
+        _lib.call("sglm_step_update", P, na, _p(act_d), _p(up(step_a, np.float64)),
+                  _p(bf.delta), _p(beta64_d), st)
         if not const_hess:
             drift[act] += step_a * dmaxeta            # max_i |t d_eta_i| over the fit's rows
         fresh_start[act[step_a != 0.0]] = False

@@ -580,3 +580,37 @@ def test_fused_link_gradient_and_slot_lists(engine, torch_mod):
         assert torch.equal(e3[k], e2[k]) and torch.equal(W3[k], W4[k]), k
     nb = 3 * 32 * d.ld
     assert torch.equal(Rp3.view(3, 32, d.ld)[:, :ns], Rp4.view(3, 32, d.ld)[:, :ns])
+
+
+def test_step_scalars_and_update_vs_float64(engine, torch_mod):
+    """sglm_step_scalars (g.d, penalty terms, max|d|, max|w + t d| per trial step) and
+    sglm_step_update over a slot list vs float64 torch on the same inputs."""
+    torch = torch_mod
+    from sglm_hip import _lib
+    rng = np.random.default_rng(81)
+    B, P = 9, 512
+    g = torch.from_numpy(rng.normal(size=(B, P))).cuda()
+    w = torch.from_numpy(rng.normal(size=(B, P))).cuda()
+    d = torch.from_numpy(rng.normal(size=(B, P)).astype(np.float32)).cuda()
+    lp = torch.from_numpy(np.abs(rng.normal(size=(B, P)))).cuda()
+    t = torch.tensor([0.0, 1.0, 0.5, 0.25, 0.125, 0.0625, 2.0 ** -10], dtype=torch.float64,
+                     device="cuda")
+    slots = torch.tensor([7, 0, 3, 8], dtype=torch.int32, device="cuda")
+    T = t.numel()
+    out = torch.empty(4 * (5 + T), dtype=torch.float64, device="cuda")
+    _lib.call("sglm_step_scalars", P, 4, slots.data_ptr(), g.data_ptr(), w.data_ptr(),
+              d.data_ptr(), lp.data_ptr(), t.data_ptr(), T, out.data_ptr(), 0)
+    o = out.view(4, 5 + T).cpu().numpy()
+    for q, k in enumerate((7, 0, 3, 8)):
+        dk = d[k].double()
+        ref = [float((g[k] * dk).sum()), float((lp[k] * w[k] * w[k]).sum()),
+               float((lp[k] * w[k] * dk).sum()), float((lp[k] * dk * dk).sum()),
+               float(dk.abs().max())] + [float((w[k] + tj * dk).abs().max()) for tj in t.tolist()]
+        assert np.allclose(o[q], ref, rtol=1e-12, atol=1e-12), (k, o[q], ref)
+    step = torch.tensor([0.5, 0.0, 1.0, 0.25], dtype=torch.float64, device="cuda")
+    w2 = w.clone()
+    _lib.call("sglm_step_update", P, 4, slots.data_ptr(), step.data_ptr(), d.data_ptr(),
+              w2.data_ptr(), 0)
+    for q, k in enumerate((7, 0, 3, 8)):
+        assert torch.allclose(w2[k], w[k] + step[q] * d[k].double(), rtol=0, atol=1e-15)
+    assert torch.equal(w2[1], w[1])

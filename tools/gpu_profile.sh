@@ -1,6 +1,6 @@
 # Round artifacts: PMC traffic of the Gram (separate FETCH/WRITE passes), the default bench line
-# (with CPU baseline), the rocprofv3 kernel-trace summary of the same bench command, and the
-# uncontended per-kernel costs (one IRLS group: no second stream competing for CUs).
+# (with CPU baseline), the rocprofv3 kernel-trace summary of the same bench command, the C5 and
+# session-prep bench lines, and simulated 2/4/8-rank shares.
 # Usage on the box: bash tools/gpu_profile.sh ROUND   (e.g. r02)
 set -e
 export TMPDIR=/tmp
@@ -11,6 +11,8 @@ timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -
 python tools/pmc_traffic.py $O/fetch $O/write profiles/${R}_pmc_traffic.json > $O/pmc.log 2>&1
 timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu > $O/bench_prof.json 2> $O/kt.err
-SGLM_IRLS_GROUPS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt1 -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu > $O/bench_prof_g1.json 2> $O/kt1.err
-timeout -k 10 200 python tools/grid_phases.py > $O/phases_g2.json 2> $O/phases.err
-SGLM_IRLS_GROUPS=1 timeout -k 10 200 python tools/grid_phases.py > $O/phases_g1.json 2>> $O/phases.err
+timeout -k 10 300 python bench.py --config c5 > $O/bench_c5.json 2> $O/bench_c5.err
+timeout -k 10 300 python bench.py --config prep > $O/bench_prep.json 2> $O/bench_prep.err
+for w in 2 4 8; do
+  timeout -k 10 300 python -u tools/rank_sim.py --world $w --all > $O/rank$w.json 2> $O/rank$w.err
+done
