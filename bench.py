@@ -41,7 +41,10 @@ CONFIGS = {
     "c5": (1_000_000, 50, 20, 5, 20),
     # session preprocessing (lynne_pp.preprocess_lynne): rows per session
     "prep": (16_000_000, 0, 0, 0, 0),
+    # gen_signal_df.generate_signal_df: trials per session
+    "signal": (0, 0, 0, 0, 0),
 }
+SIGNAL_TRIALS = 60_000
 C5_RESPONSES = 64
 PREP_SHIFT = 1     # er_refactored_from_scratch_cleanup.py:269 calls preprocess_lynne(df, trial_shift_bounds=1)
 INIT_PASSES = 2
@@ -326,6 +329,114 @@ def bench_prep(a):
         "cpu_baseline": cpu}))
 
 
+def bench_signal(a):
+    """gen_signal_df.generate_signal_df's per-sample work on the device
+    (sglm_scatter_rows: the trial table aligned onto the signal, 31 columns; sglm_signal_trials:
+    nTrial / nEndTrial / diffTrialNums and the duplication row map) for one synthetic session
+    of SIGNAL_TRIALS trials, trial rows resident in HBM.  One step = one session; sessions are
+    independent (weak scaling).  The drop-in's whole call (host pandas table steps + these
+    kernels + the host row gather), host frames in and out, rides along in `config`."""
+    import torch
+    import torch.distributed as dist
+    import pandas as pd
+    from sglm.features import gen_signal_df as G
+    from sglm_hip import signal, synth
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    sig, table = synth.signal_session(SIGNAL_TRIALS, 200 + rank)
+    n = len(sig)
+    # trial rows per index column as the drop-in builds them (host table steps, untimed here)
+    df_t = G.generate_Ab_labels(table)
+    for b in G.BASIS_AA_COLS:
+        df_t[b] = (df_t["label"] == b).astype(np.float64)
+    df_t[G.TABLE_INDEX_COLUMNS] = G.matlab_indexing_to_python(df_t[G.TABLE_INDEX_COLUMNS])
+    df_t = G.replace_missed_center_out_indexes(df_t)
+    pieces, nc = [], 0
+    for col in G.TABLE_INDEX_COLUMNS:
+        tr = df_t[G.get_is_relevant_trial(df_t["hasAllPhotometryData"], df_t[col])]
+        pos = tr[col].to_numpy().astype(np.int64)
+        keep = pos < n
+        r = tr["wasRewarded"].to_numpy(dtype=np.float64)
+        vals = [np.ones_like(r), r, 1.0 - r]
+        if col in G._SIDE_COLS:
+            vals += [tr[b].to_numpy(dtype=np.float64) for b in G.BASIS_AA_COLS]
+        v = np.ascontiguousarray(np.stack(vals)[:, keep])
+        pieces.append((nc, torch.from_numpy(pos[keep]).cuda(), torch.from_numpy(v).cuda()))
+        nc += v.shape[0]
+    out = torch.empty((nc, n), dtype=torch.float64, device="cuda")
+    ws = signal.TrialWorkspace(n)
+    ci_row, so_row = pieces[0][0], pieces[3][0]
+
+    def step():
+        for c0, rd, vd in pieces:
+            signal.aligned_columns_device(n, rd, vd, out[c0:c0 + vd.shape[0]])
+        signal.trial_runs_device(out[ci_row], out[so_row], -20, 20, ws)
+
+    for _ in range(max(1, a.warmup)):
+        step()
+    stream = torch.cuda.current_stream()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(a.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = (time.perf_counter() - t0) / a.steps
+    call_ms = ev0.elapsed_time(ev1) / a.steps
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64,
+                         device="cuda" if a.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t[0])
+    if rank != 0:
+        return
+    n_out = signal.n_out(n, -20, int(ws.ncopies.item()))
+    nr = sum(int(rd.numel()) * (vd.shape[0] + 1) for _, rd, vd in pieces)
+    # NaN fill of every aligned column, the trial rows scattered (values + row index), the two
+    # flag columns read, three count columns written, the row map (int64 + u8) per output row
+    algo = 8 * nc * n + 8 * nr + 16 * n + 24 * n + 9 * n_out
+    achieved = algo / (call_ms * 1e-3) / 1e9
+    t1 = time.perf_counter()
+    full, _ = G.signal_frame(sig, table)
+    e2e_s = time.perf_counter() - t1
+    assert len(full) == n_out
+    cpu = None
+    if not a.no_cpu:
+        from oracle import signal_ref
+        trials = 3000
+        ssig, stab = synth.signal_session(trials, 200 + rank)
+        t2 = time.perf_counter()
+        signal_ref.signal_frame(ssig, stab)
+        dt = time.perf_counter() - t2
+        cpu = {"value": len(ssig) / dt, "unit": "signal rows/s", "cores": 1, "kind": "port",
+               "sample": f"oracle/signal_ref.py (the reference's pandas alignment, cumsum/shift "
+                         f"and per-trial duplication loop) on a {trials}-trial session of "
+                         f"{len(ssig)} rows, {dt:.2f} s"}
+    print(json.dumps({
+        "metric": "signal rows/s (gen_signal_df.generate_signal_df per-sample columns)",
+        "value": n * world / el, "unit": "signal rows/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": el * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": f"one {SIGNAL_TRIALS}-trial session per rank ({n} signal rows, "
+                               f"{nc} aligned columns, trial bounds -20 / +20, {n_out} output "
+                               f"rows)",
+                   "config_name": "signal", "rows": n,
+                   "dropin_host_frames_rows_per_s": n / e2e_s,
+                   "parallelism": f"one session per rank, {world} rank(s)"},
+        "roofline": {"bound": "hbm", "kernel": "sglm_scatter_rows x5 + sglm_signal_trials "
+                                               "(whole step: 17 launches)",
+                     "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": achieved / PEAK_HBM_GBS, "traffic": None,
+                     "algorithmic_bytes_per_step": algo, "avg_call_ms": call_ms},
+        "cpu_baseline": cpu}))
+
+
 def spawn_ranks(a):
     """``--gpus N`` without a launcher: start N rank processes (torch.distributed.run, one per
     GPU, rendezvous on 127.0.0.1) as CHILDREN before anything touches the GPU, and exit with
@@ -398,8 +509,8 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group("gloo")
-    if a.config in ("c5", "prep"):
-        (bench_c5 if a.config == "c5" else bench_prep)(a)
+    if a.config in ("c5", "prep", "signal"):
+        {"c5": bench_c5, "prep": bench_prep, "signal": bench_signal}[a.config](a)
         if world > 1:
             dist.destroy_process_group()
         return

@@ -324,6 +324,24 @@ int sglm_score_sums(int32_t family, float power, int64_t n, int64_t ld, int32_t 
                     const int32_t* fit_resp, const int32_t* sets, double* out, void* work,
                     sglm_stream_t stream);
 
+/* gen_signal_df.generate_signal_df (sglm/sglm/features/gen_signal_df.py:327-470).
+ * sglm_scatter_rows: out[c][i] = NaN for i < n, then out[c][rows[t]] = vals[c][t] for
+ * t < nrows with 0 <= rows[t] < n -- a trial-table column aligned onto the signal rows by index
+ * label (`signal_df[col] = df_t_tmp.set_index(col)[...]`, :416-427); rows must be distinct.
+ * sglm_signal_trials: nTrial = cumsum(center_in == 1).shift(k_before), nEndTrial =
+ * cumsum(side_out == 1).shift(k_after), diffTrialNums, and the output row map of the per-trial
+ * duplication loop (:437-458): src[q] = signal row of output row q, dup[q] = 1 for the copies
+ * (rows with diffTrialNums > 1 repeated ahead of their nTrial run with nTrial - 1); rows with
+ * a NaN nTrial are dropped.  Output rows = n - |k_before| (clamped) + *ncopies (device
+ * double).  src/dup need 2n entries; work: sglm_signal_trials_work_bytes(n). */
+int sglm_scatter_rows(int64_t n, const int64_t* rows, int64_t nrows, const double* vals,
+                      int32_t ncols, double* out, int64_t ld_out, sglm_stream_t stream);
+size_t sglm_signal_trials_work_bytes(int64_t n);
+int sglm_signal_trials(const double* center_in, const double* side_out, int64_t n,
+                       int64_t k_before, int64_t k_after, double* ntrial, double* nend,
+                       double* diff, int64_t* src, uint8_t* dup, double* ncopies, void* work,
+                       sglm_stream_t stream);
+
 /* --- session preprocessing (lynne_pp.preprocess_lynne, lynne_pp.py:217-249) -------------
  * Input: SGLM_PREP_NIN float64 columns of n rows, column c at in + c * ld_in, in the order of
  * enum sglm_prep_in (the renamed session columns of lynne_pp.rename_columns, :95-111).

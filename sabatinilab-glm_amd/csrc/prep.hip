@@ -374,10 +374,165 @@ __global__ void prep_first_kernel(In in, const double* __restrict__ cs_nn,
     o.c[SGLM_PREP_OUT_FT_NR_SPN][t] = ft_spn * nr;
 }
 
+// ---- gen_signal_df.generate_signal_df (sglm/sglm/features/gen_signal_df.py:327-470) ------
+// Trial-table values aligned onto the signal rows (pandas index alignment of
+// df_t_tmp.set_index(col)[...], :416-427): NaN everywhere, then out[c][rows[t]] = vals[c][t].
+__global__ void __launch_bounds__(256) fill_nan_kernel(double* __restrict__ out, int64_t ld,
+                                                       int32_t nc, int64_t n) {
+    const int c = blockIdx.y;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * 256)
+        out[(int64_t)c * ld + i] = NAN;
+}
+
+__global__ void __launch_bounds__(256) scatter_rows_kernel(const int64_t* __restrict__ rows,
+                                                           int64_t nr,
+                                                           const double* __restrict__ vals,
+                                                           int32_t nc, double* __restrict__ out,
+                                                           int64_t ld, int64_t n) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= nr) return;
+    const int64_t r = rows[t];
+    if (r < 0 || r >= n) return;                     // labels absent from the signal index
+    for (int c = 0; c < nc; ++c) out[(int64_t)c * ld + r] = vals[(int64_t)c * nr + t];
+}
+
+// trial start / end flags: ((~isna) & (x == 1)) * 1 (get_trial_start / get_trial_end, :251-281)
+__global__ void __launch_bounds__(256) sig_flags_kernel(const double* __restrict__ cin,
+                                                        const double* __restrict__ sout,
+                                                        int64_t n, double* __restrict__ fs,
+                                                        double* __restrict__ fe) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    fs[i] = cin[i] == 1.0 ? 1.0 : 0.0;
+    fe[i] = sout[i] == 1.0 ? 1.0 : 0.0;
+}
+
+__device__ __forceinline__ double shifted(const double* x, int64_t i, int64_t k, int64_t n) {
+    const int64_t j = i - k;                         // Series.shift(k): out[i] = in[i - k]
+    return j >= 0 && j < n ? x[j] : NAN;
+}
+
+// nTrial = cumsum(start).shift(kb), nEndTrial = cumsum(end).shift(ka), diffTrialNums, the
+// duplication flag F = diffTrialNums > 1 (:430-441) and each row's run-head index (nTrial
+// runs are contiguous: a cumulative count shifted)
+__global__ void __launch_bounds__(256) sig_shift_kernel(const double* __restrict__ cs,
+                                                        const double* __restrict__ ce,
+                                                        int64_t n, int64_t kb, int64_t ka,
+                                                        double* __restrict__ ntrial,
+                                                        double* __restrict__ nend,
+                                                        double* __restrict__ diff,
+                                                        double* __restrict__ F,
+                                                        double* __restrict__ head) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const double a = shifted(cs, i, kb, n), b = shifted(ce, i, ka, n);
+    const double prev = i > 0 ? shifted(cs, i - 1, kb, n) : NAN;
+    ntrial[i] = a;
+    nend[i] = b;
+    const double d = a - b;
+    diff[i] = d;
+    F[i] = d > 1.0 ? 1.0 : 0.0;
+    head[i] = (i == 0 || !(a == prev)) ? (double)i : -INFINITY;
+}
+
+// Output row map of the duplication loop (:437-458): per nTrial run (value v, in order), the
+// rows with F = 1 as copies (nTrial v - 1, dupe True), then the run itself; rows whose nTrial
+// is NaN are dropped.  G: inclusive cumsum of F; Fs / Fb: forward / backward cumsums of F within
+// the run; S: the run's first row.
+__global__ void __launch_bounds__(256) sig_map_kernel(const double* __restrict__ ntrial,
+                                                      const double* __restrict__ F,
+                                                      const double* __restrict__ G,
+                                                      const double* __restrict__ Fs,
+                                                      const double* __restrict__ Fb,
+                                                      const double* __restrict__ S, int64_t n,
+                                                      int64_t nan_lead,
+                                                      int64_t* __restrict__ src,
+                                                      uint8_t* __restrict__ dup) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n || isnan(ntrial[i])) return;
+    const int64_t f = (int64_t)F[i], fs = (int64_t)Fs[i];
+    const int64_t total = fs + (int64_t)Fb[i] - f;         // copies made in this run
+    const int64_t before = (int64_t)G[i] - fs;              // copies made in earlier runs
+    const int64_t pos = (i - nan_lead) + before + total;
+    src[pos] = i;
+    dup[pos] = 0;
+    if (f) {
+        const int64_t pd = ((int64_t)S[i] - nan_lead) + before + fs - 1;
+        src[pd] = i;
+        dup[pd] = 1;
+    }
+}
+
 }  // namespace
 }  // namespace sglm
 
 using namespace sglm;
+
+extern "C" int sglm_scatter_rows(int64_t n, const int64_t* rows, int64_t nrows,
+                                 const double* vals, int32_t ncols, double* out, int64_t ld_out,
+                                 sglm_stream_t stream) {
+    if (n <= 0 || ncols <= 0) return SGLM_OK;
+    if (!out || ld_out < n || (nrows > 0 && (!rows || !vals))) {
+        set_error("sglm_scatter_rows: bad args");
+        return SGLM_EINVAL;
+    }
+    hipStream_t s = as_stream(stream);
+    const int64_t g = (n + 255) / 256;
+    fill_nan_kernel<<<dim3((unsigned)(g < 4096 ? g : 4096), (unsigned)ncols), 256, 0, s>>>(
+        out, ld_out, ncols, n);
+    int st = check_launch("fill_nan_kernel");
+    if (st || nrows <= 0) return st;
+    scatter_rows_kernel<<<(unsigned)((nrows + 255) / 256), 256, 0, s>>>(rows, nrows, vals, ncols,
+                                                                       out, ld_out, n);
+    return check_launch("scatter_rows_kernel");
+}
+
+extern "C" size_t sglm_signal_trials_work_bytes(int64_t n) {
+    if (n < 0) n = 0;
+    return (size_t)7 * (size_t)n * sizeof(double) + (size_t)nwaves_of(n) * sizeof(Agg<1>) + 256;
+}
+
+extern "C" int sglm_signal_trials(const double* center_in, const double* side_out, int64_t n,
+                                  int64_t k_before, int64_t k_after, double* ntrial,
+                                  double* nend, double* diff, int64_t* src, uint8_t* dup,
+                                  double* ncopies, void* work, sglm_stream_t stream) {
+    if (n <= 0) return SGLM_OK;
+    if (!center_in || !side_out || !ntrial || !nend || !diff || !src || !dup || !ncopies ||
+        !work) {
+        set_error("sglm_signal_trials: null pointer");
+        return SGLM_EINVAL;
+    }
+    hipStream_t s = as_stream(stream);
+    double* T0 = (double*)work;                     // start flags -> cumsum
+    double* T1 = T0 + n;                            // end flags -> cumsum
+    double* F = T1 + n;
+    double* H = F + n;                              // head index -> run start (max scan)
+    double* G = H + n;
+    double* Fs = G + n;
+    double* Fb = Fs + n;
+    void* agg = (void*)(((uintptr_t)(Fb + n) + 63) & ~(uintptr_t)63);
+    const int64_t g = (n + 255) / 256;
+    int st;
+    sig_flags_kernel<<<g, 256, 0, s>>>(center_in, side_out, n, T0, T1);
+    if ((st = scan<OP_ADD, 1>(cols1(T0, T0, nullptr, n, 0), agg, s))) return st;
+    if ((st = scan<OP_ADD, 1>(cols1(T1, T1, nullptr, n, 0), agg, s))) return st;
+    sig_shift_kernel<<<g, 256, 0, s>>>(T0, T1, n, k_before, k_after, ntrial, nend, diff, F, H);
+    if ((st = scan<OP_ADD, 1>(cols1(F, G, nullptr, n, 0), agg, s))) return st;
+    if ((st = scan<OP_ADD, 1>(cols1(F, Fs, ntrial, n, 0), agg, s))) return st;
+    if ((st = scan<OP_ADD, 1>(cols1(F, Fb, ntrial, n, 1), agg, s))) return st;
+    if ((st = scan<OP_MAX, 1>(cols1(H, H, nullptr, n, 0), agg, s))) return st;
+    const int64_t lead = k_before > 0 ? (k_before < n ? k_before : n) : 0;
+    sig_map_kernel<<<g, 256, 0, s>>>(ntrial, F, G, Fs, Fb, H, n, lead, src, dup);
+    if ((st = check_launch("sig_map_kernel"))) return st;
+    // total copies = G[n-1]
+    if (hipMemcpyAsync(ncopies, G + (n - 1), sizeof(double), hipMemcpyDeviceToDevice, s) !=
+        hipSuccess) {
+        set_error("sglm_signal_trials: hipMemcpyAsync failed");
+        return SGLM_EHIP;
+    }
+    return SGLM_OK;
+}
 
 extern "C" size_t sglm_prep_work_bytes(int64_t n) {
     if (n < 0) n = 0;

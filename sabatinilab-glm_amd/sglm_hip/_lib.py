@@ -73,6 +73,10 @@ SIGNATURES = {
     "sglm_eta_pair_absmax": (C.c_int, [_i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "sglm_score_sums": (C.c_int, [_i32, _f32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
                                   _vp, _vp]),
+    "sglm_scatter_rows": (C.c_int, [_i64, _vp, _i64, _vp, _i32, _vp, _i64, _vp]),
+    "sglm_signal_trials_work_bytes": (_sz, [_i64]),
+    "sglm_signal_trials": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp,
+                                     _vp, _vp]),
     "sglm_prep_work_bytes": (_sz, [_i64]),
     "sglm_prep_session": (C.c_int, [_vp, _i64, _i64, _i32, _vp, _i64, _vp, _vp]),
 }

@@ -97,3 +97,63 @@ def session(n: int, seed: int, rate: float = 0.02, with_extra: bool = True):
         df["zscored green"] = rng.standard_normal(n)
         df["centerOcc"] = (rng.random(n) < 0.3).astype(np.int64)
     return df, cols
+
+
+def _ab_words(rew, left, right):
+    """The 'word' the acquisition pipeline stores per trial: previous trial rewarded 'A' / 'a'
+    (the first trial counts as rewarded), then this trial rewarded on the same side 'A', on
+    the other 'B', unrewarded same 'a', other 'b'."""
+    prev = lambda x: np.r_[True, x[:-1].astype(bool)]              # noqa: E731
+    same = (left == prev(left)) & (right == prev(right))
+    rw = rew.astype(bool)
+    first = np.where(prev(rew), "A", "a")
+    second = np.where(rw, np.where(same, "A", "B"), np.where(same, "a", "b"))
+    return np.char.add(first, second).astype(object)
+
+
+def signal_session(n_trials: int, seed: int, *, short_gap=0.3, missed_co=0.05,
+                   no_photometry=0.05, no_lick=0.1, nan_rows=0.03, past_end=2, signal_tail=40,
+                   channels=3):
+    """(signal_df, table_df) in the layout gen_signal_df.generate_signal_df reads: a behaviour
+    table of ``n_trials`` trials (MATLAB 1-based sample indices of center in/out, side in/out,
+    first lick; reward, choice, 'word') over a photometry signal.  A fraction of inter-trial
+    gaps is shorter than the default trial bounds (trials overlap, rows get duplicated), some
+    center outs are carried into the next trial's sample (the repair loop), some trials lack
+    photometry or a lick, some table rows carry NaN (dropped), and the last ``past_end``
+    trials lie beyond the recording (their indices match no signal row)."""
+    import pandas as pd
+    rng = np.random.default_rng(seed)
+    # per trial: center in, +1..5 center out, +2..10 side in, +0..3 first lick, +5..30 side out
+    d = np.stack([rng.integers(1, 6, n_trials), rng.integers(2, 11, n_trials),
+                  rng.integers(5, 31, n_trials), rng.integers(0, 4, n_trials)], axis=1)
+    gap = np.where(rng.random(n_trials) < short_gap, rng.integers(3, 18, n_trials),
+                   rng.integers(18, 80, n_trials))
+    span = d[:, 0] + d[:, 1] + d[:, 2] + gap
+    ci = 30 + np.r_[0, np.cumsum(span)[:-1]]
+    co = ci + d[:, 0]
+    si = co + d[:, 1]
+    so = si + d[:, 2]
+    fl = si + d[:, 3]
+    idx = np.stack([ci, co, si, so, fl], axis=1).astype(np.float64) + 1.0   # MATLAB 1-based
+    n_sig = int(idx[max(0, n_trials - past_end - 1), 3]) + signal_tail if n_trials else 50
+    carried = np.flatnonzero(rng.random(max(n_trials - 1, 0)) < missed_co)
+    idx[carried, 1] = idx[carried + 1, 1]
+    idx[rng.random(n_trials) < no_lick, 4] = 0.0
+    left = (rng.random(n_trials) < 0.5).astype(np.int64)
+    right = 1 - left
+    right[rng.random(n_trials) < 0.03] = 0                                  # no choice
+    rew = (rng.random(n_trials) < 0.6).astype(np.int64)
+    table = pd.DataFrame({c: idx[:, j] for j, c in enumerate(
+        ["photometryCenterInIndex", "photometryCenterOutIndex", "photometrySideInIndex",
+         "photometrySideOutIndex", "photometryFirstLickIndex"])})
+    table["hasAllPhotometryData"] = (rng.random(n_trials) >= no_photometry).astype(np.int64)
+    table["wasRewarded"] = rew
+    table["choseLeft"] = left
+    table["choseRight"] = right
+    table["word"] = _ab_words(rew, left, right)
+    rt = rng.random(n_trials)
+    rt[rng.random(n_trials) < nan_rows] = np.nan
+    table["reactionTime"] = rt
+    sig = pd.DataFrame({f"Ch{c + 1}": rng.standard_normal(n_sig) for c in range(channels)})
+    sig["timestamp"] = np.arange(n_sig) / 20.0
+    return sig, table
