@@ -245,6 +245,19 @@ int sglm_chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t nact
                           int32_t nrefac, const double* g, const float* dshift, float* delta,
                           int32_t* info, uint8_t* frozen, int32_t B, void* work,
                           sglm_stream_t stream);
+/* sglm_chol_solve_inv: factor fits[0 .. nrefac) as sglm_chol_solve_mixed does and form their
+ * explicit inverses M = U^-1 (Minv: B x P x P, upper triangle; frozen columns zero) by
+ * recursive doubling; then every fit q of the list solves on a stored inverse,
+ * delta[fits[q]] = -rscale[q] * M_f M_f^T g[fits[q]] with f = fsrc[q] (= fits[q] on its own
+ * factor, a representative's slot for a cross-mask alias), zero on f's frozen coordinates.
+ * tiles: ntiles x (start, count <= 32) runs of the list that share one f.  work:
+ * sglm_chol_work_bytes(P, B).  Replaces the per-iteration triangular solves (scipy
+ * cho_solve inside _newton_solver.py NewtonCholeskySolver.inner_solve). */
+int sglm_chol_solve_inv(float* H, float* Minv, int32_t P, const int32_t* fits,
+                        const int32_t* fsrc, const float* rscale, int32_t nact, int32_t nrefac,
+                        const int32_t* tiles, int32_t ntiles, const double* g,
+                        const float* dshift, float* delta, int32_t* info, uint8_t* frozen,
+                        int32_t B, void* work, sglm_stream_t stream);
 
 /* Solves on the stored factor of ANOTHER slot (engine.irls cross-mask Hessian sharing: a CV
  * split fit preconditioned by the full-data fit's Hessian at the same penalty, scaled by the
@@ -383,6 +396,18 @@ enum sglm_prep_out {
 size_t sglm_prep_work_bytes(int64_t n);
 int sglm_prep_session(const double* in, int64_t ld_in, int64_t n, int32_t k, double* out,
                       int64_t ld_out, void* work, sglm_stream_t stream);
+
+/* --- grid setup on the host (CPU, multithreaded; no device pointers) -------------------
+ * sglm_host_masks: row mask f (uint8, out + f * ld, zero past n) of a CV grid from its index
+ * list -- the fold selections of the reference's loop (backend/sglm_cv.py:107-110):
+ * SGLM_MASK_ALL every row (idx unused), SGLM_MASK_FOLD a fold list (0/1 when strictly
+ * increasing, else the multiplicity of each row; > 255 repeats is an error), SGLM_MASK_ROWS a
+ * row list (1 on every listed row).  nnz[f] = rows with a nonzero mask, sum[f] = the summed
+ * multiplicity (either may be NULL).  Rows outside [0, n) are an error. */
+enum { SGLM_MASK_ALL = 0, SGLM_MASK_FOLD = 1, SGLM_MASK_ROWS = 2 };
+int sglm_host_masks(int32_t nm, const int64_t* const* idx, const int64_t* len,
+                    const int32_t* kind, int64_t n, int64_t ld, uint8_t* out, int64_t* nnz,
+                    double* sum, int32_t nthreads);
 
 #ifdef __cplusplus
 }

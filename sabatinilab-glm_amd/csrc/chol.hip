@@ -146,7 +146,7 @@ __global__ void __launch_bounds__(64) chol_diag_kernel(
     float* __restrict__ Hall, int32_t P, int32_t k0, const int32_t* __restrict__ fits,
     uint8_t* __restrict__ frozen_all, float* __restrict__ rhs_all,
     const float* __restrict__ diag_all, int32_t* __restrict__ info, int32_t nrefac,
-    float* __restrict__ minv_all) {
+    float* __restrict__ minv_all, float* __restrict__ Mall) {
     const int fit = fits[blockIdx.x];
     const bool refactor = (int)blockIdx.x < nrefac;
     float* H = Hall + (int64_t)fit * P * P;
@@ -188,6 +188,14 @@ __global__ void __launch_bounds__(64) chol_diag_kernel(
         float* mo = minv_all + (int64_t)blockIdx.x * kNB * kNB + c;
 #pragma unroll
         for (int r = 0; r < kNB; ++r) mo[r * kNB] = v[r];
+        if (Mall) {
+            // the explicit inverse's diagonal block: M_kk = U_kk^-1, row c = this lane's v
+            // (v[r] = (U_kk^-T)[r][c]; zero below the diagonal and in frozen columns)
+            float* mr = Mall + (int64_t)fit * P * P + (int64_t)(k0 + c) * P + k0;
+#pragma unroll
+            for (int r = 0; r < kNB; r += 4)
+                *reinterpret_cast<f32x4*>(mr + r) = f32x4{v[r], v[r + 1], v[r + 2], v[r + 3]};
+        }
     } else {
         float ucc = 1.0f;                            // U[c][c] (selects: no dynamic index)
 #pragma unroll
@@ -452,12 +460,174 @@ __global__ void __launch_bounds__(kST) chol_back2_kernel(
     for (int j = tid; j < P; j += kST) delta[j] = frz[j] ? 0.0f : -x[j];
 }
 
+
+// ---- explicit inverse of the factor and the solves on it -----------------------------------
+// M = U^-1 (upper triangular, frozen / dropped-pivot columns zero), stored row-major per slot
+// in Mall.  The diagonal blocks come from chol_diag_kernel; the rest by recursive doubling over
+// aligned super-blocks [[A, B], [0, C]] of size 2s (s = 64, 128, ...):
+//     (U^-1)_AC = -M_A (B M_C),
+// two 64 x 64-tile GEMM launches per level (T = B M_C, then X = -M_A T), log2(P/64) levels.
+// A solve is then two GEMMs over the right-hand sides sharing a factor, Y = G M and
+// delta = -Y M^T -- full-chip launches instead of a 32-step substitution chain per solve.
+//
+// Wave tile: 32 x 32 on v_mfma_f32_32x32x2f32 (exact f32 products, f32 accumulation).  K is
+// consumed in chunks of 8 with the lane -> k assignment k = kc + 4 kh + u (u = 0..3) for both
+// operands, so a lane's A operands are 4 consecutive k of one row (one 16-byte load) and its
+// B operands 4 rows of one column (coalesced 128-byte rows across the 32 lanes).
+
+// one level of the recursive doubling; STEP 0: T = B M_C (scratch), STEP 1: X = -M_A T (into M)
+template <int STEP>
+__global__ void __launch_bounds__(kCT) chol_inv_level_kernel(const float* __restrict__ Hall,
+                                                             float* __restrict__ Mall,
+                                                             float* __restrict__ Tall,
+                                                             int32_t P, int32_t s,
+                                                             const int32_t* __restrict__ fits,
+                                                             int64_t tcap) {
+    const int fit = fits[blockIdx.y];
+    const float* H = Hall + (int64_t)fit * P * P;
+    float* M = Mall + (int64_t)fit * P * P;
+    const int sb = s / kNB;
+    int t = blockIdx.x;
+    const int pair = t / (sb * sb);
+    t -= pair * sb * sb;
+    const int ti = t / sb, tj = t - ti * sb;
+    const int a0 = 2 * s * pair, c0 = a0 + s;
+    const int cs = min(s, P - c0);
+    if (cs <= 0 || tj * kNB >= cs) return;
+    float* T = Tall + (int64_t)blockIdx.y * tcap + (int64_t)pair * s * s;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r32 = lane & 31, kh = lane >> 5;
+    const int i0 = ti * kNB + (wave >> 1) * 32;        // quadrant rows / cols (local)
+    const int j0 = tj * kNB + (wave & 1) * 32;
+    const float* pa;
+    const float* pb;
+    int64_t ldb;
+    int klo, khi;
+    if (STEP == 0) {                                   // A = U[a0 + i][c0 + k], B = M[c0 + k][c0 + j]
+        pa = H + (int64_t)(a0 + i0 + r32) * P + c0;
+        pb = M + (int64_t)c0 * P + c0 + j0 + r32;
+        ldb = P;
+        klo = 0;
+        khi = (tj + 1) * kNB;                          // M_C upper triangular
+    } else {                                           // A = M[a0 + i][a0 + k], B = T[k][j]
+        pa = M + (int64_t)(a0 + i0 + r32) * P + a0;
+        pb = T + j0 + r32;
+        ldb = s;
+        klo = ti * kNB;                                // M_A upper triangular
+        khi = s;
+    }
+    f32x16 acc = {};
+    for (int kc = klo; kc < khi; kc += 8) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(pa + kc + 4 * kh);
+        float b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) b[u] = pb[(int64_t)(kc + 4 * kh + u) * ldb];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[u], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int i = i0 + (q & 3) + 8 * (q >> 2) + 4 * kh, j = j0 + r32;
+        if (STEP == 0)
+            T[(int64_t)i * s + j] = acc[q];
+        else
+            M[(int64_t)(a0 + i) * P + c0 + j] = -acc[q];
+    }
+}
+
+// Solves on explicit inverses.  Tile t = rows [start, start + cnt) of the fit list (cnt <= 32,
+// one factor: slot fsrc[start]); blockIdx.x = a 32-wide output column block; the 4 waves split
+// K and reduce through LDS.  SECOND = false: Y[q][j] = sum_k G[q][k] M[k][j] with G = rscale *
+// g (float64 -> f32) zeroed on the factor's frozen coordinates.  SECOND = true:
+// delta[fit][i] = -sum_j Y[q][j] M[i][j], zero on frozen coordinates.
+template <bool SECOND>
+__global__ void __launch_bounds__(kCT) chol_inv_apply_kernel(
+    const float* __restrict__ Mall, int32_t P, const int32_t* __restrict__ fits,
+    const int32_t* __restrict__ fsrc, const float* __restrict__ rscale,
+    const int32_t* __restrict__ tiles, const double* __restrict__ gall,
+    const uint8_t* __restrict__ frozen_all, float* __restrict__ Y, float* __restrict__ delta_all) {
+    __shared__ float red[4][16 * 64];
+    const int start = tiles[2 * blockIdx.y], cnt = tiles[2 * blockIdx.y + 1];
+    const int src = fsrc[start];
+    const float* M = Mall + (int64_t)src * P * P;
+    const uint8_t* frz = frozen_all + (int64_t)src * P;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r32 = lane & 31, kh = lane >> 5;
+    const int c0 = blockIdx.x * 32;
+    const bool valid = r32 < cnt;
+    const int q = start + (valid ? r32 : 0);
+    f32x16 acc = {};
+    if (!SECOND) {
+        const double* g = gall + (int64_t)fits[q] * P;
+        const double sc = (double)rscale[q];
+        const float* pb = M + c0 + r32;
+        const int khi = (c0 / kNB + 1) * kNB;           // M upper triangular
+        for (int kc = 8 * wave; kc < khi; kc += 32) {
+            const int k = kc + 4 * kh;
+            const uint32_t fz = *reinterpret_cast<const uint32_t*>(frz + k);
+            float a[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                a[u] = (!valid || ((fz >> (8 * u)) & 0xff)) ? 0.0f : (float)(g[k + u] * sc);
+            float b[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) b[u] = pb[(int64_t)(k + u) * P];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[u], acc, 0, 0, 0);
+        }
+    } else {
+        const float* py = Y + (int64_t)q * P;
+        const float* pm = M + (int64_t)(c0 + r32) * P;
+        const int klo = (c0 / kNB) * kNB;               // M[i][j] = 0 for j < i
+        for (int kc = klo + 8 * wave; kc < P; kc += 32) {
+            const int k = kc + 4 * kh;
+            f32x4 a = *reinterpret_cast<const f32x4*>(py + k);
+            if (!valid) a = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+            const f32x4 b = *reinterpret_cast<const f32x4*>(pm + k);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[u], acc, 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[wave][r * 64 + lane] = acc[r];
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int o = threadIdx.x + kCT * m;            // (register r, lane l) of the quadrant
+        const float v = red[0][o] + red[1][o] + red[2][o] + red[3][o];
+        const int r = o >> 6, l = o & 63;
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), col = c0 + (l & 31);
+        if (row >= cnt) continue;
+        if (!SECOND)
+            Y[(int64_t)(start + row) * P + col] = v;
+        else
+            delta_all[(int64_t)fits[start + row] * P + col] = frz[col] ? 0.0f : -v;
+    }
+}
+
 }  // namespace sglm
 
 using namespace sglm;
 
+// recursive-doubling scratch per factored fit: the largest level's T blocks
+static int64_t inv_tcap(int32_t P) {
+    int64_t cap = 0;
+    for (int s = kNB; s < P; s *= 2) {
+        const int64_t pairs = (P - s + 2 * s - 1) / (2 * s);
+        const int64_t v = pairs * s * s;
+        cap = v > cap ? v : cap;
+    }
+    return cap;
+}
+
 extern "C" size_t sglm_chol_work_bytes(int32_t P, int32_t B) {
-    return ((size_t)2 * (size_t)B * (size_t)P + (size_t)B * kNB * kNB) * sizeof(float);
+    // rhs, original diagonal, diagonal-block inverses; for sglm_chol_solve_inv also Y (B x P)
+    // and the inversion scratch
+    return ((size_t)3 * (size_t)B * (size_t)P + (size_t)B * kNB * kNB +
+            (size_t)B * (size_t)inv_tcap(P)) * sizeof(float);
 }
 
 // Look-ahead depth of the blocked factorisation (block steps per trailing sweep); the
@@ -477,7 +647,7 @@ static int chol_lookahead() {
 static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t nact,
                             int32_t nrefac, const double* g, const float* dshift, float* delta,
                             int32_t* info, uint8_t* frozen, int32_t B, void* work,
-                            hipStream_t s) {
+                            hipStream_t s, float* Mall = nullptr) {
     if (nact <= 0) return SGLM_OK;
     if (!H || !fits || !g || !dshift || !delta || !info || !frozen || !work || P % kNB ||
         P > kMaxP || B < nact || nrefac < 0 || nrefac > nact) {
@@ -490,6 +660,7 @@ static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t na
     chol_prep_kernel<<<nact, kCT, 0, s>>>(H, P, fits, g, dshift, frozen, rhs, dg, info, nrefac);
     int st = check_launch("chol_prep_kernel");
     if (st) return st;
+    if (nrefac == 0 && Mall) return SGLM_OK;
     if (nrefac == 0) {                       // stored factors only: two triangular solves
         chol_fwd2_kernel<<<nact, kST, 0, s>>>(H, P, fits, nullptr, frozen, rhs);
         st = check_launch("chol_fwd2_kernel");
@@ -505,7 +676,7 @@ static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t na
     auto factor_step = [&](int kb) {
         const int k0 = kb * kNB;
         chol_diag_kernel<<<nact, 64, 0, s>>>(H, P, k0, fits, frozen, rhs, dg, info, nrefac,
-                                             minv);
+                                             minv, Mall);
         const int rem = P - k0 - kNB;
         if (rem > 0)
             chol_panel_kernel<<<dim3(nact, rem / kNB), kCT, 0, s>>>(H, P, k0, fits, minv, rhs,
@@ -529,6 +700,7 @@ static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t na
     }
     st = check_launch("chol block kernels");
     if (st) return st;
+    if (Mall) return SGLM_OK;                // the caller solves on the explicit inverses
     chol_back2_kernel<<<nact, kST, 0, s>>>(H, P, fits, nullptr, frozen, rhs, delta);
     return check_launch("chol_back2_kernel");
 }
@@ -572,4 +744,50 @@ extern "C" int sglm_chol_solve_mixed(float* H, int32_t P, const int32_t* fits, i
                                      void* work, sglm_stream_t stream) {
     return chol_solve_mixed(H, P, fits, nact, nrefac, g, dshift, delta, info, frozen, B, work,
                             as_stream(stream));
+}
+
+// Factor fits[0 .. nrefac) (penalty shift, frozen set, blocked Cholesky) and form their
+// explicit inverses M = U^-1 in Minv; then every fit of the list solves on a stored inverse:
+// delta[fits[q]] = -rscale[q] * M_f M_f^T g[fits[q]], f = fsrc[q] (fsrc[q] = fits[q] for a fit
+// on its own factor, the representative's slot for a cross-mask alias).  tiles: ntiles x
+// (start, count <= 32) runs of the list sharing one factor.
+extern "C" int sglm_chol_solve_inv(float* H, float* Minv, int32_t P, const int32_t* fits,
+                                   const int32_t* fsrc, const float* rscale, int32_t nact,
+                                   int32_t nrefac, const int32_t* tiles, int32_t ntiles,
+                                   const double* g, const float* dshift, float* delta,
+                                   int32_t* info, uint8_t* frozen, int32_t B, void* work,
+                                   sglm_stream_t stream) {
+    if (nact <= 0) return SGLM_OK;
+    if (!H || !Minv || !fits || !fsrc || !rscale || !tiles || ntiles <= 0 || !g || !delta ||
+        !frozen || !work || P % kNB || P > kMaxP || B < nact || nrefac < 0 || nrefac > nact ||
+        (nrefac > 0 && (!dshift || !info))) {
+        set_error("sglm_chol_solve_inv: bad args (P=%d, max %d)", P, kMaxP);
+        return SGLM_EINVAL;
+    }
+    hipStream_t s = as_stream(stream);
+    int st;
+    if (nrefac > 0) {
+        if ((st = chol_solve_mixed(H, P, fits, nrefac, nrefac, g, dshift, delta, info, frozen, B,
+                                   work, s, Minv)))
+            return st;
+        // work: rhs, original diagonal (B x P each), diagonal-block inverses (B x 64 x 64),
+        // Y (B x P), T (B x tcap)
+        float* T = (float*)work + (size_t)3 * B * P + (size_t)B * kNB * kNB;
+        const int64_t tcap = inv_tcap(P);
+        for (int sz = kNB; sz < P; sz *= 2) {
+            const int pairs = (P - sz + 2 * sz - 1) / (2 * sz);
+            const int sb = sz / kNB;
+            const dim3 grid((unsigned)(pairs * sb * sb), (unsigned)nrefac);
+            chol_inv_level_kernel<0><<<grid, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
+            chol_inv_level_kernel<1><<<grid, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
+        }
+        if ((st = check_launch("chol_inv_level_kernel"))) return st;
+    }
+    float* Y = (float*)work + (size_t)2 * B * P + (size_t)B * kNB * kNB;
+    const dim3 grid((unsigned)(P / 32), (unsigned)ntiles);
+    chol_inv_apply_kernel<false><<<grid, kCT, 0, s>>>(Minv, P, fits, fsrc, rscale, tiles, g,
+                                                       frozen, Y, delta);
+    chol_inv_apply_kernel<true><<<grid, kCT, 0, s>>>(Minv, P, fits, fsrc, rscale, tiles, g,
+                                                      frozen, Y, delta);
+    return check_launch("chol_inv_apply_kernel");
 }

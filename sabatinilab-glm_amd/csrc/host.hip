@@ -1,0 +1,128 @@
+// Host-side (CPU) helpers of the grid setup, multithreaded.
+//
+// sglm_host_masks: the per-fold row masks of a CV grid from their index lists, written
+// straight into the (pinned) upload buffer.  Replaces the per-fold `X[idx_train, :]` /
+// `y[idx_train]` selections of the reference's fold loop (backend/sglm_cv.py:107-110) as
+// one uint8 mask row per fold: 0/1 for a strictly increasing list (GroupShuffleSplit folds),
+// the multiplicity for a list with repeats (holdout resampling), 1 on every listed row for a
+// row list, all ones for "every row".  One thread per mask (a mask is ~1 MB of stores).
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "common.h"
+
+namespace {
+
+struct MaskJob {
+    const int64_t* idx;
+    int64_t len;
+    int32_t kind;
+    uint8_t* out;
+    int64_t n, ld;
+    int64_t nnz = 0;
+    double sum = 0.0;
+    int err = 0;            // 1: index out of range, 2: a row repeats > 255 times
+};
+
+void build_mask(MaskJob& j) {
+    uint8_t* m = j.out;
+    const int64_t n = j.n;
+    std::memset(m + n, 0, (size_t)(j.ld - n));
+    if (j.kind == SGLM_MASK_ALL) {
+        std::memset(m, 1, (size_t)n);
+        j.nnz = n;
+        j.sum = (double)n;
+        return;
+    }
+    std::memset(m, 0, (size_t)n);
+    const int64_t* idx = j.idx;
+    const int64_t L = j.len;
+    // one pass: every index in range, and whether the list is strictly increasing
+    bool bad = false, increasing = true;
+    int64_t prev = -1;
+    for (int64_t t = 0; t < L; ++t) {
+        const int64_t v = idx[t];
+        bad |= (uint64_t)v >= (uint64_t)n;
+        increasing &= v > prev;
+        prev = v;
+    }
+    if (bad) { j.err = 1; return; }
+    if (j.kind == SGLM_MASK_ROWS || increasing) {
+        for (int64_t t = 0; t < L; ++t) m[idx[t]] = 1;
+        if (increasing) {
+            j.nnz = L;
+            j.sum = (double)L;
+            return;
+        }
+        int64_t c = 0;
+        for (int64_t i = 0; i < n; ++i) c += m[i];
+        j.nnz = c;
+        j.sum = (double)c;
+        return;
+    }
+    // multiplicities (repeats)
+    for (int64_t t = 0; t < L; ++t) {
+        if (m[idx[t]] == 255) { j.err = 2; return; }
+        ++m[idx[t]];
+    }
+    int64_t c = 0;
+    for (int64_t i = 0; i < n; ++i) c += m[i] != 0;
+    j.nnz = c;
+    j.sum = (double)L;
+}
+
+}  // namespace
+
+using sglm::set_error;
+
+extern "C" int sglm_host_masks(int32_t nm, const int64_t* const* idx, const int64_t* len,
+                               const int32_t* kind, int64_t n, int64_t ld, uint8_t* out,
+                               int64_t* nnz, double* sum, int32_t nthreads) {
+    if (nm <= 0) return SGLM_OK;
+    if (!idx || !len || !kind || !out || n < 0 || ld < n) {
+        set_error("sglm_host_masks: bad args");
+        return SGLM_EINVAL;
+    }
+    std::vector<MaskJob> jobs((size_t)nm);
+    for (int32_t f = 0; f < nm; ++f) {
+        if (kind[f] != SGLM_MASK_ALL && kind[f] != SGLM_MASK_FOLD && kind[f] != SGLM_MASK_ROWS) {
+            set_error("sglm_host_masks: mask %d has unknown kind %d", f, kind[f]);
+            return SGLM_EINVAL;
+        }
+        if (kind[f] != SGLM_MASK_ALL && len[f] > 0 && !idx[f]) {
+            set_error("sglm_host_masks: mask %d has no index list", f);
+            return SGLM_EINVAL;
+        }
+        MaskJob& j = jobs[(size_t)f];
+        j.idx = idx[f];
+        j.len = kind[f] == SGLM_MASK_ALL ? 0 : len[f];
+        j.kind = kind[f];
+        j.out = out + (int64_t)f * ld;
+        j.n = n;
+        j.ld = ld;
+    }
+    int nt = nthreads > 0 ? nthreads : 1;
+    if (nt > nm) nt = nm;
+    std::vector<std::thread> pool;
+    pool.reserve((size_t)nt);
+    for (int w = 0; w < nt; ++w)
+        pool.emplace_back([&jobs, w, nt] {
+            for (size_t f = (size_t)w; f < jobs.size(); f += (size_t)nt) build_mask(jobs[f]);
+        });
+    for (auto& t : pool) t.join();
+    for (int32_t f = 0; f < nm; ++f) {
+        const MaskJob& j = jobs[(size_t)f];
+        if (j.err == 1) {
+            set_error("sglm_host_masks: mask %d lists a row outside [0, %lld)", f, (long long)n);
+            return SGLM_EINVAL;
+        }
+        if (j.err == 2) {
+            set_error("an index repeats more than 255 times in one split");
+            return SGLM_EINVAL;
+        }
+        if (nnz) nnz[f] = j.nnz;
+        if (sum) sum[f] = j.sum;
+    }
+    return SGLM_OK;
+}

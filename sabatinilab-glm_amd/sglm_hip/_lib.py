@@ -54,6 +54,8 @@ SIGNATURES = {
     "sglm_chol_work_bytes": (_sz, [_i32, _i32]),
     "sglm_chol_solve_ex": (C.c_int, [_vp, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _i32,
                                      _vp, _vp]),
+    "sglm_chol_solve_inv": (C.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _i32, _i32, _vp, _i32,
+                                      _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
     "sglm_chol_solve_mixed": (C.c_int, [_vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32,
                                         _vp, _vp]),
     "sglm_chol_solve_alias": (C.c_int, [_vp, _i32, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _i32, _vp,
@@ -73,6 +75,7 @@ SIGNATURES = {
     "sglm_eta_pair_absmax": (C.c_int, [_i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "sglm_score_sums": (C.c_int, [_i32, _f32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
                                   _vp, _vp]),
+    "sglm_host_masks": (C.c_int, [_i32, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _i32]),
     "sglm_scatter_rows": (C.c_int, [_i64, _vp, _i64, _vp, _i32, _vp, _i64, _vp]),
     "sglm_signal_trials_work_bytes": (_sz, [_i64]),
     "sglm_signal_trials": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp,

@@ -24,7 +24,9 @@ is reused by the refinement iterations.
 """
 from __future__ import annotations
 
+import ctypes
 import math
+import os
 import threading
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
@@ -71,6 +73,10 @@ HESS_SHARE_TOL = float(__import__("os").environ.get("SGLM_HESS_SHARE_TOL", "0.37
 # step fails the line search or contracts slowly leaves the family for good.  0 disables.
 HESS_XMASK_TOL = float(__import__("os").environ.get("SGLM_HESS_XMASK_TOL", "0.75"))
 XMASK_SLOW = 0.7                # aliased-step contraction above which a fit leaves its family
+# Newton solves on explicit factor inverses (sglm_chol_solve_inv: two full-chip GEMMs per
+# iteration over every fit, grouped by factor) instead of per-fit triangular substitution
+# chains; 0 restores sglm_chol_solve_mixed / sglm_chol_solve_alias.
+SOLVE_INV = __import__("os").environ.get("SGLM_SOLVE_INV", "1") == "1"
 
 
 def require_gpu():
@@ -267,6 +273,46 @@ class Design:
 
 
 # ------------------------------------------------------------------------------ problem
+# threads of the native host-side setup helpers (sglm_host_masks)
+HOST_THREADS = int(os.environ.get("SGLM_HOST_THREADS", "8"))
+
+
+def _np_ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def host_masks(specs, n: int, ld: int, out: Optional[np.ndarray] = None):
+    """uint8 row masks (nm x ld, zero past n) of mask specs (idx or None = every row,
+    multiplicity) by the multithreaded native builder (sglm_host_masks; host only, no GPU).
+    Returns (nnz, sums) per mask, and fills ``out`` (flat, >= nm * ld) or returns it as a
+    third value when ``out`` is None."""
+    nm = len(specs)
+    ret = out is None
+    if out is None:
+        out = np.empty(max(nm * ld, 1), dtype=np.uint8)
+    if out.dtype != np.uint8 or out.size < nm * ld or not out.flags.c_contiguous:
+        raise ValueError("out must be a contiguous uint8 array of >= nm * ld entries")
+    lists, kinds = [], np.empty(nm, dtype=np.int32)
+    for f, (idx, mult) in enumerate(specs):
+        if idx is None:
+            kinds[f] = 0                                       # SGLM_MASK_ALL
+            lists.append(None)
+        else:
+            kinds[f] = 1 if mult else 2                        # SGLM_MASK_FOLD / _ROWS
+            lists.append(np.ascontiguousarray(np.asarray(idx).reshape(-1), dtype=np.int64))
+    ptrs = (ctypes.c_void_p * max(nm, 1))(*[0 if a is None else a.ctypes.data for a in lists])
+    lens = np.array([0 if a is None else a.size for a in lists], dtype=np.int64)
+    nnz = np.zeros(nm, dtype=np.int64)
+    sums = np.zeros(nm, dtype=np.float64)
+    try:
+        _lib.call("sglm_host_masks", nm, ctypes.cast(ptrs, ctypes.c_void_p), _np_ptr(lens),
+                  _np_ptr(kinds), int(n), int(ld), _np_ptr(out), _np_ptr(nnz), _np_ptr(sums),
+                  HOST_THREADS)
+    except _lib.HipEngineError as e:
+        raise ValueError(str(e).split(": ", 1)[-1]) from None
+    return (nnz, sums, out[: nm * ld].reshape(nm, ld)) if ret else (nnz, sums)
+
+
 class _Columns:
     """Read-only list view of the columns of an (n x R) array (host copies on access)."""
 
@@ -292,10 +338,13 @@ class Problem:
         float64 device copy)."""
         self.design = design
         n, ld, dev = design.n, design.ld, design.device
-        self.masks = [np.asarray(m, dtype=np.uint8).reshape(-1) for m in masks]
-        for m in self.masks:
+        self._masks = [np.asarray(m, dtype=np.uint8).reshape(-1) for m in masks]
+        for m in self._masks:
             if m.shape[0] != n:
                 raise ValueError(f"mask length {m.shape[0]} != n_samples {n}")
+        self._nnz = None
+        self._y64r = None
+        self._rolled = None
         self.Yd64 = None
         if isinstance(ys, np.ndarray) and ys.ndim == 2:
             if ys.shape[0] != n:
@@ -322,15 +371,88 @@ class Problem:
         self._groups = None
         self._compact = {}
 
+    @classmethod
+    def from_index_lists(cls, design: Design, y, rolls: Sequence[int], specs):
+        """A CV grid's problem straight from its fold index lists (no host mask arrays): the
+        masks are built by the multithreaded native builder (sglm_host_masks) into a pinned
+        buffer and uploaded asynchronously; the responses ``np.roll(y, r)`` for r in ``rolls``
+        are formed on the device from one float64 upload.  ``specs``: per mask (idx or None =
+        every row, multiplicity) -- a fold list counts repeats, a row list marks rows."""
+        self = cls.__new__(cls)
+        self.design = design
+        n, ld, dev = design.n, design.ld, design.device
+        y = np.ascontiguousarray(np.asarray(y, dtype=np.float64).reshape(-1))
+        if y.shape[0] != n:
+            raise ValueError(f"response length {y.shape[0]} != n_samples {n}")
+        nm = len(specs)
+        buf = _pinned("problem_masks", max(nm * ld, 1), torch.uint8)
+        ev = _scratch().pinned.get(("problem_masks_ev", None))
+        if ev is not None:
+            ev.synchronize()                                   # the previous upload has read it
+        nnz, sums = host_masks(specs, n, ld, buf.numpy())
+        self.M = torch.empty((nm, ld), dtype=torch.uint8, device=dev)
+        self.M.view(-1).copy_(buf[: nm * ld], non_blocking=True)
+        yb = _pinned("problem_y", max(n, 1), torch.float64)
+        if ev is None:
+            ev = torch.cuda.Event()
+            _scratch().pinned[("problem_masks_ev", None)] = ev
+        yb[:n].copy_(torch.from_numpy(y))
+        yd = torch.empty(n, dtype=torch.float64, device=dev)
+        yd.copy_(yb[:n], non_blocking=True)
+        ev.record()
+        rolls = [int(r) for r in rolls]
+        self._y64r = torch.stack([torch.roll(yd, r) for r in rolls]) if rolls else yd[None, :0]
+        self.Y = torch.zeros((len(rolls), ld), dtype=torch.float32, device=dev)
+        self.Y[:, :n] = self._y64r.float()
+        self._masks = None
+        self._nnz = nnz
+        self._rolled = (y, rolls)
+        self.Yd64 = None
+        self._ylo = None
+        self._stats = {("count", f): float(sums[f]) for f in range(nm)}
+        self._groups = None
+        self._compact = {}
+        return self
+
+    @property
+    def masks(self):
+        """Host uint8 masks (a device copy when the problem was built from index lists)."""
+        if self._masks is None:
+            self._masks = list(self.M[:, : self.design.n].cpu().numpy())
+        return self._masks
+
+    @property
+    def ys(self):
+        if self._rolled is not None:
+            y, rolls = self._rolled
+            return [np.roll(y, r) for r in rolls]
+        return self._ys
+
+    @ys.setter
+    def ys(self, v):
+        self._ys = v
+
+    def y64_rows(self):
+        """The responses as one device float64 (R, n) array."""
+        if self._y64r is None:
+            if self.Yd64 is not None:
+                self._y64r = self.Yd64.t().contiguous()
+            else:
+                self._y64r = torch.from_numpy(np.stack(self.ys)).to(self.design.device)
+        return self._y64r
+
+    def mask_nnz(self, mask: int) -> int:
+        """Rows with a nonzero mask value."""
+        if self._nnz is not None:
+            return int(self._nnz[mask])
+        return int(np.count_nonzero(self.masks[mask]))
+
     def y_lo(self):
         """f32 residual y - f32(y) of the responses ([R][ld], or None when every y is exact in
         f32, e.g. counts): X^T(m y) = X^T(m y_hi) + X^T(m y_lo) recovers the float64 sums."""
         if self._ylo is None:
-            n, ld, dev = self.design.n, self.design.ld, self.design.device
-            if self.Yd64 is not None:
-                y64 = self.Yd64.t()
-            else:
-                y64 = torch.from_numpy(np.stack(self.ys)).to(dev)
+            n = self.design.n
+            y64 = self.y64_rows()
             lo = torch.zeros_like(self.Y)
             lo[:, :n] = (y64 - self.Y[:, :n].double()).float()
             self._ylo = lo if bool(lo.any()) else False
@@ -375,7 +497,7 @@ class Problem:
         c = self._compact.get(mask)
         if c is None:
             d = self.design
-            nr = int(np.count_nonzero(self.masks[mask]))
+            nr = self.mask_nnz(mask)
             # the mask's row list, built on the device (no host pass, no synchronising upload)
             rows_d = None if nr == d.n else torch.nonzero_static(
                 self.M[mask, :d.n], size=nr).view(-1).to(torch.int32)
@@ -490,6 +612,7 @@ class _Buffers:
             self.W = torch.zeros((B, ld), dtype=f32, device=dev)
             self.R = torch.zeros((B, ld), dtype=f32, device=dev)
             self.H = torch.empty((B, P, P), dtype=f32, device=dev)
+            self.Minv = torch.empty((B, P, P), dtype=f32, device=dev) if SOLVE_INV else None
             self.g = torch.zeros((B, P), dtype=torch.float64, device=dev)
             self.gtot = torch.zeros((B, P), dtype=torch.float64, device=dev)
             self.dshift = torch.zeros((B, P), dtype=f32, device=dev)
@@ -900,11 +1023,37 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
             order, nref = act, (0 if factored else act.size)
         else:
             order, nref = np.concatenate([form, keep]), form.size
-        fits_d = up(order, np.int32)
-        _lib.call("sglm_chol_solve_mixed", _p(bf.H), P, _p(fits_d), int(order.size), int(nref),
-                  _p(bf.gtot), _p(bf.dshift), _p(bf.delta), _p(bf.info), _p(bf.frozen), B,
-                  _p(bf.cwork), st)
-        if not const_hess and ali.size:
+        if SOLVE_INV:
+            # one list: factored and kept fits on their own inverses, then the aliased fits
+            # grouped by representative (tiles of <= 32 fits sharing one inverse)
+            al = ali[np.argsort(repl[ali], kind="stable")] if (not const_hess and ali.size) \
+                else np.zeros(0, dtype=np.int64)
+            src = repl[al]
+            lst = np.concatenate([order, al]).astype(np.int32)
+            fsrc = np.concatenate([order, src]).astype(np.int32)
+            rsc = np.concatenate([np.ones(order.size), rows[src] / rows[al]]).astype(np.float32)
+            tiles = [(q, 1) for q in range(order.size)]
+            q = order.size
+            while q < lst.size:
+                e = q
+                while e < lst.size and e - q < 32 and fsrc[e] == fsrc[q]:
+                    e += 1
+                tiles.append((q, e - q))
+                q = e
+            ints = up(np.concatenate([lst, fsrc, np.asarray(tiles, np.int32).reshape(-1)]),
+                      np.int32)
+            rsc_d = up(rsc, np.float32)
+            nl = int(lst.size)
+            _lib.call("sglm_chol_solve_inv", _p(bf.H), _p(bf.Minv), P, _p(ints),
+                      _p(ints[nl:]), _p(rsc_d), nl, int(nref), _p(ints[2 * nl:]), len(tiles),
+                      _p(bf.gtot), _p(bf.dshift), _p(bf.delta), _p(bf.info), _p(bf.frozen), B,
+                      _p(bf.cwork), st)
+        else:
+            fits_d = up(order, np.int32)
+            _lib.call("sglm_chol_solve_mixed", _p(bf.H), P, _p(fits_d), int(order.size),
+                      int(nref), _p(bf.gtot), _p(bf.dshift), _p(bf.delta), _p(bf.info),
+                      _p(bf.frozen), B, _p(bf.cwork), st)
+        if not SOLVE_INV and not const_hess and ali.size:
             # the representatives' factors are complete: solve the aliased fits on them
             src = repl[ali]
             al_d = up(np.stack([ali, src]), np.int32)

@@ -43,11 +43,10 @@ class _MaskStats:
         self.torch, self._lib = torch, _lib
         self.prob = prob
         n, dev = prob.design.n, prob.design.device
-        ys = np.stack(prob.ys)
-        self.F, self.R, self.n = prob.M.shape[0], ys.shape[0], n
-        self.K = ys.mean(axis=1)                         # per-response shift
-        self.Yd = torch.from_numpy(ys).to(dev)           # R x n float64
-        self.Kd = torch.from_numpy(self.K).to(dev)
+        self.Yd = prob.y64_rows()                        # R x n float64 (device)
+        self.F, self.R, self.n = prob.M.shape[0], self.Yd.shape[0], n
+        self.Kd = self.Yd.mean(dim=1)                    # per-response shift
+        self.K = self.Kd.cpu().numpy()
         self.work = torch.empty(_lib.query("sglm_mask_stats_work_bytes", self.F, self.R, n),
                                 dtype=torch.uint8, device=dev)
         st = self._pass(-1.0)                             # [R][F][5]
@@ -259,10 +258,8 @@ def run_multi(X, y, groups: Sequence[dict], score_method: str = "mse", coef0=Non
     # only the masks (and responses) of this rank's fits are built and uploaded
     used = sorted({table[i][3] for i in mine} | {table[i][5] for i in mine if table[i][5] >= 0})
     local = {mid: q for q, mid in enumerate(used)}
-    masks = [specs[mid][2] if specs[mid][2] is not None else
-             _mask_array(specs[mid][0], specs[mid][1], n) for mid in used]
-    ys = [np.roll(y, r) for r in roll_list]
-    prob = E.Problem(design, ys, masks)
+    prob = E.Problem.from_index_lists(design, y, roll_list,
+                                      [(specs[mid][0], specs[mid][1]) for mid in used])
     t0 = tick("setup_problem", t0)
     ms = _MaskStats(prob)
     for i in mine:                           # the IRLS setup reads these, not host passes

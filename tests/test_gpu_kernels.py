@@ -178,6 +178,69 @@ def test_chol_solve_matches_numpy(engine, torch_mod):
         assert rel(x3[k, : p + 1], -np.linalg.solve(M, g2[k, : p + 1])) < 1e-3, k
 
 
+@pytest.mark.parametrize("P,p,B", [(192, 150, 40), (2048, 1990, 4), (64, 40, 3)])
+def test_chol_solve_inv_vs_float64(engine, torch_mod, P, p, B):
+    """sglm_chol_solve_inv: factor + explicit inverse by recursive doubling (ragged P = 3 x 64
+    and the C4 P = 2048), solves on own, kept and aliased (rscale, frozen set of the source)
+    inverses in tiles of <= 32 fits, against float64 solves."""
+    torch = torch_mod
+    from sglm_hip import _lib
+    rng = np.random.default_rng(P)
+    H = np.zeros((B, P, P), np.float32)
+    for k in range(2):
+        A = rng.normal(size=(p + 400, p + 1))
+        H[k, : p + 1, : p + 1] = A.T @ A / 100.0
+    dsh = np.full((B, P), -1.0, np.float32)          # frozen padding
+    dsh[:, :p] = 0.5
+    dsh[:, p] = 0.0                                  # intercept: unpenalised
+    dsh[:, 7] = -1.0                                 # a frozen coordinate
+    g = rng.normal(size=(B, P))
+    Hd = torch.from_numpy(H).cuda()
+    Md = torch.empty_like(Hd)
+    gd = torch.from_numpy(g).cuda()
+    out = torch.full((B, P), np.nan, dtype=torch.float32, device="cuda")
+    info = torch.zeros(B, dtype=torch.int32, device="cuda")
+    frozen = torch.zeros((B, P), dtype=torch.uint8, device="cuda")
+    dshd = torch.from_numpy(dsh).cuda()
+    cw = torch.empty(_lib.query("sglm_chol_work_bytes", P, B), dtype=torch.uint8, device="cuda")
+
+    def solve(lst, fsrc, rsc, nref, tiles):
+        ints = torch.tensor(np.r_[lst, fsrc, np.asarray(tiles).reshape(-1)].astype(np.int32),
+                            device="cuda")
+        rs = torch.tensor(np.asarray(rsc, np.float32), device="cuda")
+        n = len(lst)
+        _lib.call("sglm_chol_solve_inv", Hd.data_ptr(), Md.data_ptr(), P, ints.data_ptr(),
+                  ints[n:].data_ptr(), rs.data_ptr(), n, nref, ints[2 * n:].data_ptr(),
+                  len(tiles), gd.data_ptr(), dshd.data_ptr(), out.data_ptr(), info.data_ptr(),
+                  frozen.data_ptr(), B, cw.data_ptr(), 0)
+        return out.cpu().numpy()
+
+    free = np.flatnonzero(dsh[0] >= 0)
+
+    def want(src, q, scale):
+        Mm = H[src].astype(np.float64)[np.ix_(free, free)] + np.diag(dsh[src, free])
+        x = np.zeros(P)
+        x[free] = -scale * np.linalg.solve(Mm, g[q, free])
+        return x
+
+    al = list(range(2, B))
+    rsc_al = list(rng.uniform(0.7, 1.3, size=len(al)))
+    lst = [0, 1] + al
+    fsrc = [0, 1] + [0] * len(al)
+    tiles = [(0, 1), (1, 1)] + [(2 + i, min(32, len(al) - i)) for i in range(0, len(al), 32)]
+    x = solve(lst, fsrc, [1.0, 1.0] + rsc_al, 2, tiles)
+    for q, src, sc in [(0, 0, 1.0), (1, 1, 1.0)] + list(zip(al, [0] * len(al), rsc_al)):
+        ref = want(src, q, sc)
+        assert rel(x[q], ref) < 1e-3, (q, rel(x[q], ref))
+        assert np.all(x[q, dsh[0] < 0] == 0)
+    # kept factors, new right-hand sides; an alias of slot 1
+    g[:] = rng.normal(size=(B, P))
+    gd.copy_(torch.from_numpy(g))
+    x = solve([1, 0, 2], [1, 0, 1], [1.0, 1.0, 0.9], 0, [(0, 1), (1, 1), (2, 1)])
+    for q, src, sc in ((1, 1, 1.0), (0, 0, 1.0), (2, 1, 0.9)):
+        assert rel(x[q], want(src, q, sc)) < 1e-3, q
+
+
 def _fit_one(engine, X, y, family, power, lam, fit_intercept=True):
     d = engine.Design.from_host(X)
     prob = engine.Problem(d, [y], [np.ones(len(y), np.uint8)])

@@ -110,3 +110,32 @@ def test_timeshift_fill_bits():
     assert fill_bits(np.nan, np.float64) == int(np.array(np.nan).view(np.uint64))
     assert fill_bits(0, np.int16) == 0
     assert fill_bits(-1, np.int32) == 0xFFFFFFFF
+
+
+def test_native_host_masks_vs_python():
+    """sglm_host_masks (host code of the library, no GPU) against the Python mask builders:
+    strictly increasing fold lists, fold lists with repeats (multiplicities), row lists with
+    duplicates, every-row masks; nnz / sums; the error cases."""
+    from sglm_hip import engine as E, folds, grid
+    rng = np.random.default_rng(0)
+    n, ld = 10_007, 10_048
+    inc = np.sort(rng.choice(n, 6000, replace=False))
+    rep = rng.integers(0, n, 9000)
+    rows = rng.integers(0, n, 3000)
+    specs = [(inc, True), (rep, True), (rows, False), (None, False), (inc[:0], True),
+             (list(inc[:10]), False)]
+    nnz, sums, M = E.host_masks(specs, n, ld)
+    for f, (idx, mult) in enumerate(specs):
+        want = grid._mask_array(idx, mult, n)
+        np.testing.assert_array_equal(M[f, :n], want)
+        assert not M[f, n:].any()
+        assert nnz[f] == np.count_nonzero(want)
+        assert sums[f] == want.sum(dtype=np.int64)
+        assert sums[f] == grid._mask_count(idx, mult, n)
+    np.testing.assert_array_equal(M[1, :n], folds.mask_from_idx(rep, n))
+    with pytest.raises(ValueError, match="255"):
+        E.host_masks([(np.zeros(256, np.int64), True)], n, ld)
+    with pytest.raises(ValueError, match="outside"):
+        E.host_masks([(np.array([3, n]), True)], n, ld)
+    with pytest.raises(ValueError, match="outside"):
+        E.host_masks([(np.array([-1, 3]), False)], n, ld)
