@@ -250,8 +250,9 @@ int sglm_chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t nact
  * recursive doubling; then every fit q of the list solves on a stored inverse,
  * delta[fits[q]] = -rscale[q] * M_f M_f^T g[fits[q]] with f = fsrc[q] (= fits[q] on its own
  * factor, a representative's slot for a cross-mask alias), zero on f's frozen coordinates.
- * tiles: ntiles x (start, count <= 32) runs of the list that share one f.  work:
- * sglm_chol_work_bytes(P, B).  Replaces the per-iteration triangular solves (scipy
+ * tiles: ntiles x (start, count <= 32) runs of the list that share one f.  ntiles = 0 only
+ * factors and inverts (g unused), nrefac = 0 only solves: the factorisation can run on
+ * another stream than the gradient and the solve.  work: sglm_chol_work_bytes(P, B).  Replaces the per-iteration triangular solves (scipy
  * cho_solve inside _newton_solver.py NewtonCholeskySolver.inner_solve). */
 int sglm_chol_solve_inv(float* H, float* Minv, int32_t P, const int32_t* fits,
                         const int32_t* fsrc, const float* rscale, int32_t nact, int32_t nrefac,

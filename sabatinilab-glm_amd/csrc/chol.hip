@@ -18,6 +18,9 @@
 // H by a previous call (kept Hessians, constant-Hessian Gaussian refinement): only the two
 // triangular solves run (chol_fwd2 / chol_back2).
 #include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
 
 #include "common.h"
 
@@ -26,6 +29,12 @@ namespace sglm {
 constexpr int kNB = 64;
 constexpr int kCT = 256;
 constexpr int kMaxP = 8192;
+
+// chol_diag.hip
+void launch_chol_diag(int nact, hipStream_t s, float* Hall, int32_t P, int32_t k0,
+                      const int32_t* fits, uint8_t* frozen_all, float* rhs_all,
+                      const float* diag_all, int32_t* info, int32_t nrefac, float* minv_all,
+                      float* Mall);
 
 // rhs/z/x scratch per fit lives in `work` (float, [B][P]); the original diagonal in
 // `work + B*P` (float, [B][P]); the dropped-pivot counter is info[].
@@ -38,7 +47,6 @@ __global__ void __launch_bounds__(kCT) chol_prep_kernel(
     const int fit = fits[blockIdx.x];
     const bool refactor = (int)blockIdx.x < nrefac;
     float* H = Hall + (int64_t)fit * P * P;
-    const double* g = gall + (int64_t)fit * P;
     const float* dsh = dshift_all + (int64_t)fit * P;
     uint8_t* frz = frozen_all + (int64_t)fit * P;
     float* rhs = rhs_all + (int64_t)fit * P;
@@ -51,20 +59,50 @@ __global__ void __launch_bounds__(kCT) chol_prep_kernel(
             const bool f = dsh[j] < 0.0f || !(d > 0.0f);
             frz[j] = f;
             dg[j] = f ? 1.0f : d;
-            if (!f) H[(int64_t)j * P + j] = d;
-        }
-        __syncthreads();
-        for (int j = 0; j < P; ++j) {
-            if (!frz[j]) continue;
-            for (int e = tid; e < P; e += kCT) {
-                if (e > j) H[(int64_t)j * P + e] = 0.0f;
-                if (e < j) H[(int64_t)e * P + j] = 0.0f;
-            }
-            if (tid == 0) H[(int64_t)j * P + j] = 1.0f;
+            H[(int64_t)j * P + j] = f ? 1.0f : d;
         }
     }
+    if (!gall) return;                      // solves on the explicit inverse read g themselves
+    const double* g = gall + (int64_t)fit * P;
     __syncthreads();
     for (int j = tid; j < P; j += kCT) rhs[j] = frz[j] ? 0.0f : (float)g[j];
+}
+
+// Frozen rows / columns of the refactored fits' upper triangles set to the identity's: one
+// 64 x 64 tile per workgroup (tiles of the upper triangle, row by row), nothing written where
+// neither the tile's rows nor its columns hold a frozen coordinate.
+__global__ void __launch_bounds__(kCT) chol_freeze_kernel(float* __restrict__ Hall, int32_t P,
+                                                          const int32_t* __restrict__ fits,
+                                                          const uint8_t* __restrict__ frozen_all) {
+    const int fit = fits[blockIdx.y];
+    float* H = Hall + (int64_t)fit * P * P;
+    const uint8_t* frz = frozen_all + (int64_t)fit * P;
+    int t = blockIdx.x, bi = 0;
+    {
+        int rowlen = P / kNB;
+        while (t >= rowlen) { t -= rowlen; ++bi; --rowlen; }
+    }
+    const int bj = bi + t;
+    __shared__ uint8_t fr[kNB], fc[kNB];
+    __shared__ int any;
+    const int tid = threadIdx.x;
+    if (tid == 0) any = 0;
+    __syncthreads();
+    if (tid < kNB) {
+        fr[tid] = frz[bi * kNB + tid];
+        if (fr[tid]) any = 1;
+    } else if (tid < 2 * kNB) {
+        fc[tid - kNB] = frz[bj * kNB + tid - kNB];
+        if (fc[tid - kNB]) any = 1;
+    }
+    __syncthreads();
+    if (!any) return;
+    const int c = tid & 63;
+    for (int r = tid >> 6; r < kNB; r += kCT / 64) {
+        const int i = bi * kNB + r, j = bj * kNB + c;
+        if (i > j || !(fr[r] | fc[c])) continue;
+        H[(int64_t)i * P + j] = i == j ? 1.0f : 0.0f;
+    }
 }
 
 // Right-hand sides of fits solved on ANOTHER slot's factor (engine.irls cross-mask Hessian
@@ -83,139 +121,6 @@ __global__ void __launch_bounds__(kCT) chol_alias_prep_kernel(
 
 __device__ __forceinline__ float lanef(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
-
-// rank-1 update of this lane's column by row q of U: a[i] -= U[q][i] * u for i > q, where
-// U[q][i] = lane i's u; the same broadcasts carry the elimination into v (lane i's column of
-// the block inverse, see chol_diag_kernel): v[i] -= U[q][i] * x_q.  Chunks of 8 readlane + FMA
-// pairs behind scheduling fences, so that the scalar broadcasts are consumed as they are
-// produced instead of all being hoisted (SGPR spills).
-template <int Q>
-__device__ __forceinline__ void diag_rank1(float (&a)[kNB], float (&v)[kNB], float u, float xq) {
-#pragma unroll
-    for (int i0 = Q + 1; i0 < kNB; i0 += 8) {
-        float sc[8];                                 // broadcasts first: the readlane ->
-#pragma unroll                                       // VALU hazard is covered by distance
-        for (int i = i0; i < i0 + 8 && i < kNB; ++i) sc[i - i0] = lanef(u, i);
-#pragma unroll
-        for (int i = i0; i < i0 + 8 && i < kNB; ++i) {
-            a[i] = fmaf(-sc[i - i0], u, a[i]);
-            v[i] = fmaf(-sc[i - i0], xq, v[i]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
-template <int Q>
-__device__ __forceinline__ void diag_steps(float (&a)[kNB], float (&v)[kNB], float& rinv, int c,
-                                           float thr, int& myfrz, int& dropped) {
-    if constexpr (Q < kNB) {
-        // the pivot test runs lane-locally (lane Q's a[Q] against its own threshold) and only
-        // its verdict is broadcast: a broadcast of the loop-invariant threshold would be
-        // hoisted for all 64 steps and spilled
-        const int verdict = (myfrz ? 2 : 0) | (a[Q] > thr ? 0 : 1);
-        const int vq = __builtin_amdgcn_readlane(verdict, Q);
-        const bool was = (vq & 2) != 0;
-        const bool drop = vq != 0;
-        // uniform pivot arithmetic: d = sqrt(piv) and its reciprocal from one v_rsq
-        const float piv = lanef(a[Q], Q);
-        const float r = drop ? 0.0f : __builtin_amdgcn_rsqf(piv);
-        const float d = drop ? 1.0f : piv * r;
-        const float u = c > Q ? a[Q] * r : 0.0f;     // row Q of U (0 for a dropped pivot)
-        a[Q] = c == Q ? d : (c > Q ? u : a[Q]);
-        rinv = c == Q ? r : rinv;                    // lane Q keeps 1 / U[Q][Q] (0 if dropped)
-        const float xq = v[Q] * r;                   // x_Q of lane c's unit right-hand side
-        v[Q] = xq;
-        // row Q is final from here on: materialise it now, or its selects sink to the store
-        // at the end and keep every step's masks and pivots live (SGPR spills)
-        asm volatile("" : "+v"(a[Q]), "+v"(rinv), "+v"(v[Q]));
-        const bool newly = drop && !was && c == Q;
-        myfrz = newly ? 1 : myfrz;
-        dropped = newly ? 1 : dropped;
-        diag_rank1<Q>(a, v, u, xq);
-        diag_steps<Q + 1>(a, v, rinv, c, thr, myfrz, dropped);
-    }
-}
-
-// One wave per fit: factor the diagonal block (refactor) and forward-solve the rhs block.
-// Lane c holds column c of the block in registers (a[r] = A[k0+r][k0+c]); step q reads the
-// pivot and row q of U with v_readlane (scalar broadcasts), so the whole 64-step
-// factorisation is register FMAs (entries below the diagonal are updated too and ignored),
-// branch-free: lane-dependent choices are selects, pivot decisions are wave-uniform.
-__global__ void __launch_bounds__(64) chol_diag_kernel(
-    float* __restrict__ Hall, int32_t P, int32_t k0, const int32_t* __restrict__ fits,
-    uint8_t* __restrict__ frozen_all, float* __restrict__ rhs_all,
-    const float* __restrict__ diag_all, int32_t* __restrict__ info, int32_t nrefac,
-    float* __restrict__ minv_all, float* __restrict__ Mall) {
-    const int fit = fits[blockIdx.x];
-    const bool refactor = (int)blockIdx.x < nrefac;
-    float* H = Hall + (int64_t)fit * P * P;
-    uint8_t* frz = frozen_all + (int64_t)fit * P + k0;
-    float* rhs = rhs_all + (int64_t)fit * P + k0;
-    const int c = threadIdx.x;
-    float a[kNB];
-    {
-        int cl = c;                                  // opaque copies of the lane index keep the
-        asm volatile("" : "+v"(cl));                 // load / store masks out of the steps' CSE
-#pragma unroll
-        for (int r = 0; r < kNB; ++r) {              // whole block (no branches), lower -> 0
-            const float v = H[(int64_t)(k0 + r) * P + k0 + c];
-            a[r] = r <= cl ? v : 0.0f;
-        }
-    }
-    int myfrz = frz[c];
-    // lane q: 1 / U[q][q] (0 for a frozen pivot) -- one VGPR, not 64 uniform SGPRs
-    float rinv = 0.0f;
-    if (refactor) {
-        const float thr = 1e-6f * diag_all[(int64_t)fit * P + k0 + c];
-        int dropped = 0;
-        // v: lane c's column of M = (U_kk^T)^-1 (rows of frozen coordinates zero), built by
-        // eliminating e_c alongside the factorisation -- the panel step's operator
-        float v[kNB];
-        {
-            int ci = c;
-            asm volatile("" : "+v"(ci));
-#pragma unroll
-            for (int r = 0; r < kNB; ++r) v[r] = r == ci ? 1.0f : 0.0f;
-        }
-        diag_steps<0>(a, v, rinv, c, thr, myfrz, dropped);
-        if (dropped) atomicAdd(&info[fit], 1);
-        frz[c] = (uint8_t)myfrz;
-        // whole block: the strictly-lower part is never read (consumers use row <= column)
-#pragma unroll
-        for (int r = 0; r < kNB; ++r) H[(int64_t)(k0 + r) * P + k0 + c] = a[r];
-        // row-major M[r][i] (lane i writes column i: coalesced rows)
-        float* mo = minv_all + (int64_t)blockIdx.x * kNB * kNB + c;
-#pragma unroll
-        for (int r = 0; r < kNB; ++r) mo[r * kNB] = v[r];
-        if (Mall) {
-            // the explicit inverse's diagonal block: M_kk = U_kk^-1, row c = this lane's v
-            // (v[r] = (U_kk^-T)[r][c]; zero below the diagonal and in frozen columns)
-            float* mr = Mall + (int64_t)fit * P * P + (int64_t)(k0 + c) * P + k0;
-#pragma unroll
-            for (int r = 0; r < kNB; r += 4)
-                *reinterpret_cast<f32x4*>(mr + r) = f32x4{v[r], v[r + 1], v[r + 2], v[r + 3]};
-        }
-    } else {
-        float ucc = 1.0f;                            // U[c][c] (selects: no dynamic index)
-#pragma unroll
-        for (int r = 0; r < kNB; ++r) ucc = r == c ? a[r] : ucc;
-        rinv = myfrz ? 0.0f : 1.0f / ucc;
-    }
-    // forward solve U_kk^T z = rhs_k, lane = row: step q needs 1/U[q][q] and U[q][c] (this
-    // lane's a[q]); z_q = 0 for a frozen coordinate (rinv 0)
-    float zc = rhs[c];
-    int cf = c;
-    asm volatile("" : "+v"(cf));                     // opaque copy: the factorisation's lane
-                                                     // masks are not CSE'd into 64 live pairs
-#pragma unroll
-    for (int q = 0; q < kNB; ++q) {
-        const float zq = lanef(zc, q) * lanef(rinv, q);
-        const float m = cf > q ? a[q] : 0.0f;
-        zc = fmaf(-m, zq, zc);
-        zc = cf == q ? zq : zc;
-    }
-    rhs[c] = zc;
 }
 
 // Panel: block row k0 of U for columns j >= k0+NB, X = M B (M from the diagonal step, B the
@@ -475,7 +380,10 @@ __global__ void __launch_bounds__(kST) chol_back2_kernel(
 // operands, so a lane's A operands are 4 consecutive k of one row (one 16-byte load) and its
 // B operands 4 rows of one column (coalesced 128-byte rows across the 32 lanes).
 
-// one level of the recursive doubling; STEP 0: T = B M_C (scratch), STEP 1: X = -M_A T (into M)
+// one level of the recursive doubling; STEP 0: T = B M_C (scratch), STEP 1: X = -M_A T (into M).
+// One 32 x 32 output quadrant per workgroup; its 4 waves split K in 64-wide blocks and reduce
+// through LDS (4x the workgroups and a quarter of the dependent K chain of one wave per quadrant:
+// the big levels have few tiles).
 template <int STEP>
 __global__ void __launch_bounds__(kCT) chol_inv_level_kernel(const float* __restrict__ Hall,
                                                              float* __restrict__ Mall,
@@ -483,11 +391,13 @@ __global__ void __launch_bounds__(kCT) chol_inv_level_kernel(const float* __rest
                                                              int32_t P, int32_t s,
                                                              const int32_t* __restrict__ fits,
                                                              int64_t tcap) {
+    __shared__ float red[4][16 * 64];
     const int fit = fits[blockIdx.y];
     const float* H = Hall + (int64_t)fit * P * P;
     float* M = Mall + (int64_t)fit * P * P;
     const int sb = s / kNB;
-    int t = blockIdx.x;
+    int t = blockIdx.x >> 2;
+    const int quad = blockIdx.x & 3;
     const int pair = t / (sb * sb);
     t -= pair * sb * sb;
     const int ti = t / sb, tj = t - ti * sb;
@@ -497,8 +407,8 @@ __global__ void __launch_bounds__(kCT) chol_inv_level_kernel(const float* __rest
     float* T = Tall + (int64_t)blockIdx.y * tcap + (int64_t)pair * s * s;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r32 = lane & 31, kh = lane >> 5;
-    const int i0 = ti * kNB + (wave >> 1) * 32;        // quadrant rows / cols (local)
-    const int j0 = tj * kNB + (wave & 1) * 32;
+    const int i0 = ti * kNB + (quad >> 1) * 32;        // quadrant rows / cols (local)
+    const int j0 = tj * kNB + (quad & 1) * 32;
     const float* pa;
     const float* pb;
     int64_t ldb;
@@ -517,22 +427,36 @@ __global__ void __launch_bounds__(kCT) chol_inv_level_kernel(const float* __rest
         khi = s;
     }
     f32x16 acc = {};
-    for (int kc = klo; kc < khi; kc += 8) {
-        const f32x4 a = *reinterpret_cast<const f32x4*>(pa + kc + 4 * kh);
-        float b[4];
+    // wave w: the 64-k blocks w, w + 4, ...; a block's 8 chunks load together
+    for (int kb = klo + kNB * wave; kb < khi; kb += 4 * kNB) {
+        f32x4 a[8];
+        float b[8][4];
+        const float* pbk = pb + (int64_t)(kb + 4 * kh) * ldb;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) b[u] = pb[(int64_t)(kc + 4 * kh + u) * ldb];
+        for (int v = 0; v < 8; ++v) {
+            a[v] = *reinterpret_cast<const f32x4*>(pa + kb + 8 * v + 4 * kh);
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[u], acc, 0, 0, 0);
+            for (int u = 0; u < 4; ++u) b[v][u] = pbk[(int64_t)(8 * v + u) * ldb];
+        }
+#pragma unroll
+        for (int v = 0; v < 8; ++v)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[v][u], b[v][u], acc, 0, 0, 0);
     }
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const int i = i0 + (q & 3) + 8 * (q >> 2) + 4 * kh, j = j0 + r32;
+    for (int r = 0; r < 16; ++r) red[wave][r * 64 + lane] = acc[r];
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int o = threadIdx.x + kCT * m;            // (register r, lane l) of the quadrant
+        const float v = red[0][o] + red[1][o] + red[2][o] + red[3][o];
+        const int r = o >> 6, l = o & 63;
+        const int i = i0 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), j = j0 + (l & 31);
         if (STEP == 0)
-            T[(int64_t)i * s + j] = acc[q];
+            T[(int64_t)i * s + j] = v;
         else
-            M[(int64_t)(a0 + i) * P + c0 + j] = -acc[q];
+            M[(int64_t)(a0 + i) * P + c0 + j] = -v;
     }
 }
 
@@ -563,32 +487,51 @@ __global__ void __launch_bounds__(kCT) chol_inv_apply_kernel(
         const double sc = (double)rscale[q];
         const float* pb = M + c0 + r32;
         const int khi = (c0 / kNB + 1) * kNB;           // M upper triangular
-        for (int kc = 8 * wave; kc < khi; kc += 32) {
-            const int k = kc + 4 * kh;
-            const uint32_t fz = *reinterpret_cast<const uint32_t*>(frz + k);
-            float a[4];
+        // wave w takes the 64-k blocks w, w + 4, ...; a block's 8 chunks load together
+        for (int kb = kNB * wave; kb < khi; kb += 4 * kNB) {
+            float a[8][4], b[8][4];
+            const float* pbk = pb + (int64_t)(kb + 4 * kh) * P;
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
-                a[u] = (!valid || ((fz >> (8 * u)) & 0xff)) ? 0.0f : (float)(g[k + u] * sc);
-            float b[4];
+            for (int v = 0; v < 8; ++v) {
+                const int k = kb + 8 * v + 4 * kh;
+                const uint32_t fz = *reinterpret_cast<const uint32_t*>(frz + k);
+                const double2 g01 = *reinterpret_cast<const double2*>(g + k);
+                const double2 g23 = *reinterpret_cast<const double2*>(g + k + 2);
+                a[v][0] = (float)(g01.x * sc);
+                a[v][1] = (float)(g01.y * sc);
+                a[v][2] = (float)(g23.x * sc);
+                a[v][3] = (float)(g23.y * sc);
+                const uint32_t keep = valid ? ~fz : 0u;        // a byte != 0: frozen
 #pragma unroll
-            for (int u = 0; u < 4; ++u) b[u] = pb[(int64_t)(k + u) * P];
+                for (int u = 0; u < 4; ++u) {
+                    if (((keep >> (8 * u)) & 0xff) != 0xff) a[v][u] = 0.0f;
+                    b[v][u] = pbk[(8 * v + u) * P];
+                }
+            }
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[u], acc, 0, 0, 0);
+            for (int v = 0; v < 8; ++v)
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[v][u], b[v][u], acc, 0, 0, 0);
         }
     } else {
         const float* py = Y + (int64_t)q * P;
         const float* pm = M + (int64_t)(c0 + r32) * P;
         const int klo = (c0 / kNB) * kNB;               // M[i][j] = 0 for j < i
-        for (int kc = klo + 8 * wave; kc < P; kc += 32) {
-            const int k = kc + 4 * kh;
-            f32x4 a = *reinterpret_cast<const f32x4*>(py + k);
-            if (!valid) a = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-            const f32x4 b = *reinterpret_cast<const f32x4*>(pm + k);
+        for (int kb = klo + kNB * wave; kb < P; kb += 4 * kNB) {
+            f32x4 a[8], b[8];
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[u], acc, 0, 0, 0);
+            for (int v = 0; v < 8; ++v) {
+                const int k = kb + 8 * v + 4 * kh;
+                a[v] = *reinterpret_cast<const f32x4*>(py + k);
+                if (!valid) a[v] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+                b[v] = *reinterpret_cast<const f32x4*>(pm + k);
+            }
+#pragma unroll
+            for (int v = 0; v < 8; ++v)
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[v][u], b[v][u], acc, 0, 0, 0);
         }
     }
 #pragma unroll
@@ -649,8 +592,8 @@ static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t na
                             int32_t* info, uint8_t* frozen, int32_t B, void* work,
                             hipStream_t s, float* Mall = nullptr) {
     if (nact <= 0) return SGLM_OK;
-    if (!H || !fits || !g || !dshift || !delta || !info || !frozen || !work || P % kNB ||
-        P > kMaxP || B < nact || nrefac < 0 || nrefac > nact) {
+    if (!H || !fits || (!g && !Mall) || !dshift || !delta || !info || !frozen || !work ||
+        P % kNB || P > kMaxP || B < nact || nrefac < 0 || nrefac > nact) {
         set_error("sglm_chol_solve: bad args (P=%d, max %d)", P, kMaxP);
         return SGLM_EINVAL;
     }
@@ -660,6 +603,12 @@ static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t na
     chol_prep_kernel<<<nact, kCT, 0, s>>>(H, P, fits, g, dshift, frozen, rhs, dg, info, nrefac);
     int st = check_launch("chol_prep_kernel");
     if (st) return st;
+    if (nrefac > 0) {
+        const int nb = P / kNB;
+        chol_freeze_kernel<<<dim3((unsigned)(nb * (nb + 1) / 2), (unsigned)nrefac), kCT, 0, s>>>(
+            H, P, fits, frozen);
+        if ((st = check_launch("chol_freeze_kernel"))) return st;
+    }
     if (nrefac == 0 && Mall) return SGLM_OK;
     if (nrefac == 0) {                       // stored factors only: two triangular solves
         chol_fwd2_kernel<<<nact, kST, 0, s>>>(H, P, fits, nullptr, frozen, rhs);
@@ -675,8 +624,7 @@ static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t na
     // read-modify-write that bounds the chain at large batches) is swept P/(kLA*64) times
     auto factor_step = [&](int kb) {
         const int k0 = kb * kNB;
-        chol_diag_kernel<<<nact, 64, 0, s>>>(H, P, k0, fits, frozen, rhs, dg, info, nrefac,
-                                             minv, Mall);
+        launch_chol_diag(nact, s, H, P, k0, fits, frozen, rhs, dg, info, nrefac, minv, Mall);
         const int rem = P - k0 - kNB;
         if (rem > 0)
             chol_panel_kernel<<<dim3(nact, rem / kNB), kCT, 0, s>>>(H, P, k0, fits, minv, rhs,
@@ -746,6 +694,99 @@ extern "C" int sglm_chol_solve_mixed(float* H, int32_t P, const int32_t* fits, i
                             as_stream(stream));
 }
 
+// The factorisation + inversion chain (~110 launches) of fits[0 .. n).
+static int factor_inv_launch(float* H, float* Minv, int32_t P, const int32_t* fits, int32_t n,
+                             const float* dshift, float* delta, int32_t* info, uint8_t* frozen,
+                             int32_t B, void* work, hipStream_t s) {
+    int st;
+    if ((st = chol_solve_mixed(H, P, fits, n, n, nullptr, dshift, delta, info, frozen, B, work, s,
+                               Minv)))
+        return st;
+    // work: rhs, original diagonal (B x P each), diagonal-block inverses (B x 64 x 64),
+    // Y (B x P), T (B x tcap)
+    float* T = (float*)work + (size_t)3 * B * P + (size_t)B * kNB * kNB;
+    const int64_t tcap = inv_tcap(P);
+    for (int sz = kNB; sz < P; sz *= 2) {
+        const int pairs = (P - sz + 2 * sz - 1) / (2 * sz);
+        const int sb = sz / kNB;
+        const dim3 grid((unsigned)(4 * pairs * sb * sb), (unsigned)n);
+        chol_inv_level_kernel<0><<<grid, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
+        chol_inv_level_kernel<1><<<grid, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
+    }
+    return check_launch("chol_inv_level_kernel");
+}
+
+// The chain is launch-bound on the host (~110 dependent launches, ~1.4 ms of enqueue against
+// ~1 ms of GPU time), so it is captured once per argument set into a HIP graph and replayed
+// (one launch).  Graphs are keyed by every pointer and size the chain bakes in; the caller
+// keeps `fits` in a stable buffer.  SGLM_CHOL_GRAPH=0 launches the chain directly.
+struct ChainKey {
+    const void *H, *Minv, *fits, *dshift, *delta, *info, *frozen, *work;
+    int32_t P, n, B, la;
+    bool operator<(const ChainKey& o) const {
+        return std::memcmp(this, &o, sizeof(ChainKey)) < 0;
+    }
+};
+
+static bool chol_graphs_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("SGLM_CHOL_GRAPH");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+static int factor_inv(float* H, float* Minv, int32_t P, const int32_t* fits, int32_t n,
+                      const float* dshift, float* delta, int32_t* info, uint8_t* frozen,
+                      int32_t B, void* work, hipStream_t s) {
+    if (!chol_graphs_enabled() || s == nullptr)      // the null stream cannot be captured
+        return factor_inv_launch(H, Minv, P, fits, n, dshift, delta, info, frozen, B, work, s);
+    static std::mutex mu;
+    static std::map<ChainKey, hipGraphExec_t> cache;
+    ChainKey key;
+    std::memset(&key, 0, sizeof(key));
+    key.H = H; key.Minv = Minv; key.fits = fits; key.dshift = dshift; key.delta = delta;
+    key.info = info; key.frozen = frozen; key.work = work;
+    key.P = P; key.n = n; key.B = B; key.la = chol_lookahead();
+    hipGraphExec_t exec = nullptr;
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        auto it = cache.find(key);
+        if (it != cache.end()) exec = it->second;
+    }
+    if (!exec) {
+        hipGraph_t graph = nullptr;
+        if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+            set_error("chol graph: hipStreamBeginCapture failed");
+            return SGLM_EHIP;
+        }
+        const int st = factor_inv_launch(H, Minv, P, fits, n, dshift, delta, info, frozen, B,
+                                         work, s);
+        const hipError_t ec = hipStreamEndCapture(s, &graph);
+        if (st) {
+            if (graph) (void)hipGraphDestroy(graph);
+            return st;
+        }
+        if (ec != hipSuccess || !graph) {
+            set_error("chol graph: hipStreamEndCapture failed");
+            return SGLM_EHIP;
+        }
+        const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        if (ei != hipSuccess) {
+            set_error("chol graph: hipGraphInstantiate failed");
+            return SGLM_EHIP;
+        }
+        std::lock_guard<std::mutex> lock(mu);
+        cache[key] = exec;
+    }
+    if (hipGraphLaunch(exec, s) != hipSuccess) {
+        set_error("chol graph: hipGraphLaunch failed");
+        return SGLM_EHIP;
+    }
+    return SGLM_OK;
+}
+
 // Factor fits[0 .. nrefac) (penalty shift, frozen set, blocked Cholesky) and form their
 // explicit inverses M = U^-1 in Minv; then every fit of the list solves on a stored inverse:
 // delta[fits[q]] = -rscale[q] * M_f M_f^T g[fits[q]], f = fsrc[q] (fsrc[q] = fits[q] for a fit
@@ -758,7 +799,7 @@ extern "C" int sglm_chol_solve_inv(float* H, float* Minv, int32_t P, const int32
                                    int32_t* info, uint8_t* frozen, int32_t B, void* work,
                                    sglm_stream_t stream) {
     if (nact <= 0) return SGLM_OK;
-    if (!H || !Minv || !fits || !fsrc || !rscale || !tiles || ntiles <= 0 || !g || !delta ||
+    if (!H || !Minv || !fits || (ntiles > 0 && (!fsrc || !rscale || !tiles || !g)) || !delta ||
         !frozen || !work || P % kNB || P > kMaxP || B < nact || nrefac < 0 || nrefac > nact ||
         (nrefac > 0 && (!dshift || !info))) {
         set_error("sglm_chol_solve_inv: bad args (P=%d, max %d)", P, kMaxP);
@@ -766,23 +807,10 @@ extern "C" int sglm_chol_solve_inv(float* H, float* Minv, int32_t P, const int32
     }
     hipStream_t s = as_stream(stream);
     int st;
-    if (nrefac > 0) {
-        if ((st = chol_solve_mixed(H, P, fits, nrefac, nrefac, g, dshift, delta, info, frozen, B,
-                                   work, s, Minv)))
-            return st;
-        // work: rhs, original diagonal (B x P each), diagonal-block inverses (B x 64 x 64),
-        // Y (B x P), T (B x tcap)
-        float* T = (float*)work + (size_t)3 * B * P + (size_t)B * kNB * kNB;
-        const int64_t tcap = inv_tcap(P);
-        for (int sz = kNB; sz < P; sz *= 2) {
-            const int pairs = (P - sz + 2 * sz - 1) / (2 * sz);
-            const int sb = sz / kNB;
-            const dim3 grid((unsigned)(pairs * sb * sb), (unsigned)nrefac);
-            chol_inv_level_kernel<0><<<grid, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
-            chol_inv_level_kernel<1><<<grid, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
-        }
-        if ((st = check_launch("chol_inv_level_kernel"))) return st;
-    }
+    if (nrefac > 0 && (st = factor_inv(H, Minv, P, fits, nrefac, dshift, delta, info, frozen, B,
+                                       work, s)))
+        return st;
+    if (ntiles <= 0) return SGLM_OK;         // factor + invert only (the solve comes later)
     float* Y = (float*)work + (size_t)2 * B * P + (size_t)B * kNB * kNB;
     const dim3 grid((unsigned)(P / 32), (unsigned)ntiles);
     chol_inv_apply_kernel<false><<<grid, kCT, 0, s>>>(Minv, P, fits, fsrc, rscale, tiles, g,

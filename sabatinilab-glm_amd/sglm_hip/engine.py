@@ -613,6 +613,8 @@ class _Buffers:
             self.R = torch.zeros((B, ld), dtype=f32, device=dev)
             self.H = torch.empty((B, P, P), dtype=f32, device=dev)
             self.Minv = torch.empty((B, P, P), dtype=f32, device=dev) if SOLVE_INV else None
+            # the factorisation chain's fit list (a stable address: the chain is a cached graph)
+            self.fact_fits = torch.zeros((B,), dtype=torch.int32, device=dev)
             self.g = torch.zeros((B, P), dtype=torch.float64, device=dev)
             self.gtot = torch.zeros((B, P), dtype=torch.float64, device=dev)
             self.dshift = torch.zeros((B, P), dtype=f32, device=dev)
@@ -670,6 +672,17 @@ def _gram_done():
     ev = torch.cuda.Event()
     ev.record()
     _GRAM_DONE[torch.cuda.current_device()] = ev
+
+
+def _side_stream():
+    """This thread's second stream on the current device (the factorisation chain, overlapped
+    with the gradient)."""
+    streams = _scratch().streams
+    key = (torch.cuda.current_device(), "chol")
+    sd = streams.get(key)
+    if sd is None:
+        sd = streams[key] = torch.cuda.Stream()
+    return sd
 
 
 def _pinned(tag, numel, dtype):
@@ -974,15 +987,21 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                 _lib.call("sglm_link_update", fam, power, n, ld, na, _p(act_d), _p(bf.eta),
                           _p(prob.Y), _p(prob.M), _p(fit_resp), _p(fit_mask), _p(bf.W), None,
                           _p(rp_buf), None, None, st)
-            _lib.call("sglm_xtr_bits_packed", _p(d.cbits_full()), ld, P, n, _p(rp_buf), na,
-                      _p(act_d), _p(bf.g), _p(gx_work), st)
         else:
             _lib.call("sglm_link_update", fam, power, n, ld, B, None, _p(bf.eta), _p(prob.Y),
                       _p(prob.M), _p(fit_resp), _p(fit_mask), _p(bf.W), _p(bf.R), None, None,
                       None, st)
-            d.xtr(bf.R, B, bf.g)
-        torch.addcmul(bf.g[:B], lamp_d, beta64_d[:B], out=bf.gtot[:B])   # + lam * w
-        t0 = tick("it_gradient", t0)
+
+        def _gradient():
+            """X^T R on the current stream, then + lam w (the Hessian step needs only W, so
+            its Grams go first and the new factorisations overlap this)."""
+            if use_rp:
+                _lib.call("sglm_xtr_bits_packed", _p(d.cbits_full()), ld, P, n, _p(rp_buf), na,
+                          _p(act_d), _p(bf.g), _p(gx_work), st)
+            else:
+                d.xtr(bf.R, B, bf.g)
+            torch.addcmul(bf.g[:B], lamp_d, beta64_d[:B], out=bf.gtot[:B])   # + lam * w
+
         # ---- Hessian
         gram_comp = np.zeros(B, dtype=bool)     # fits whose Gram is computed this iteration
         if const_hess:
@@ -1044,11 +1063,30 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                       np.int32)
             rsc_d = up(rsc, np.float32)
             nl = int(lst.size)
+            fact_done = None
+            if nref:
+                # factor + invert the new Hessians on a side stream while the gradient runs
+                side = _side_stream()
+                bf.fact_fits[:nref].copy_(ints[:nref])
+                ready = torch.cuda.Event()
+                ready.record()
+                side.wait_event(ready)
+                _lib.call("sglm_chol_solve_inv", _p(bf.H), _p(bf.Minv), P, _p(bf.fact_fits), None,
+                          None, int(nref), int(nref), None, 0, None, _p(bf.dshift), _p(bf.delta),
+                          _p(bf.info), _p(bf.frozen), B, _p(bf.cwork), side.cuda_stream)
+                fact_done = torch.cuda.Event()
+                fact_done.record(side)
+            _gradient()
+            t0 = tick("it_gradient", t0)
+            if fact_done is not None:
+                torch.cuda.current_stream().wait_event(fact_done)
             _lib.call("sglm_chol_solve_inv", _p(bf.H), _p(bf.Minv), P, _p(ints),
-                      _p(ints[nl:]), _p(rsc_d), nl, int(nref), _p(ints[2 * nl:]), len(tiles),
+                      _p(ints[nl:]), _p(rsc_d), nl, 0, _p(ints[2 * nl:]), len(tiles),
                       _p(bf.gtot), _p(bf.dshift), _p(bf.delta), _p(bf.info), _p(bf.frozen), B,
                       _p(bf.cwork), st)
         else:
+            _gradient()
+            t0 = tick("it_gradient", t0)
             fits_d = up(order, np.int32)
             _lib.call("sglm_chol_solve_mixed", _p(bf.H), P, _p(fits_d), int(order.size),
                       int(nref), _p(bf.gtot), _p(bf.dshift), _p(bf.delta), _p(bf.info),
