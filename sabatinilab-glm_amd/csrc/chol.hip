@@ -380,10 +380,9 @@ __global__ void __launch_bounds__(kST) chol_back2_kernel(
 // operands, so a lane's A operands are 4 consecutive k of one row (one 16-byte load) and its
 // B operands 4 rows of one column (coalesced 128-byte rows across the 32 lanes).
 
-// one level of the recursive doubling; STEP 0: T = B M_C (scratch), STEP 1: X = -M_A T (into M).
-// One 32 x 32 output quadrant per workgroup; its 4 waves split K in 64-wide blocks and reduce
-// through LDS (4x the workgroups and a quarter of the dependent K chain of one wave per quadrant:
-// the big levels have few tiles).
+// one level of the recursive doubling; STEP 0: T = B M_C (scratch), STEP 1: X = -M_A T (into M);
+// one 64 x 64 tile per workgroup, one 32 x 32 quadrant per wave over the whole K range (an
+// unrolled and a split-K variant both measured slower on the C4 chains)
 template <int STEP>
 __global__ void __launch_bounds__(kCT) chol_inv_level_kernel(const float* __restrict__ Hall,
                                                              float* __restrict__ Mall,
@@ -391,13 +390,11 @@ __global__ void __launch_bounds__(kCT) chol_inv_level_kernel(const float* __rest
                                                              int32_t P, int32_t s,
                                                              const int32_t* __restrict__ fits,
                                                              int64_t tcap) {
-    __shared__ float red[4][16 * 64];
     const int fit = fits[blockIdx.y];
     const float* H = Hall + (int64_t)fit * P * P;
     float* M = Mall + (int64_t)fit * P * P;
     const int sb = s / kNB;
-    int t = blockIdx.x >> 2;
-    const int quad = blockIdx.x & 3;
+    int t = blockIdx.x;
     const int pair = t / (sb * sb);
     t -= pair * sb * sb;
     const int ti = t / sb, tj = t - ti * sb;
@@ -407,8 +404,8 @@ __global__ void __launch_bounds__(kCT) chol_inv_level_kernel(const float* __rest
     float* T = Tall + (int64_t)blockIdx.y * tcap + (int64_t)pair * s * s;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r32 = lane & 31, kh = lane >> 5;
-    const int i0 = ti * kNB + (quad >> 1) * 32;        // quadrant rows / cols (local)
-    const int j0 = tj * kNB + (quad & 1) * 32;
+    const int i0 = ti * kNB + (wave >> 1) * 32;        // quadrant rows / cols (local)
+    const int j0 = tj * kNB + (wave & 1) * 32;
     const float* pa;
     const float* pb;
     int64_t ldb;
@@ -427,36 +424,22 @@ __global__ void __launch_bounds__(kCT) chol_inv_level_kernel(const float* __rest
         khi = s;
     }
     f32x16 acc = {};
-    // wave w: the 64-k blocks w, w + 4, ...; a block's 8 chunks load together
-    for (int kb = klo + kNB * wave; kb < khi; kb += 4 * kNB) {
-        f32x4 a[8];
-        float b[8][4];
-        const float* pbk = pb + (int64_t)(kb + 4 * kh) * ldb;
+    for (int kc = klo; kc < khi; kc += 8) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(pa + kc + 4 * kh);
+        float b[4];
 #pragma unroll
-        for (int v = 0; v < 8; ++v) {
-            a[v] = *reinterpret_cast<const f32x4*>(pa + kb + 8 * v + 4 * kh);
+        for (int u = 0; u < 4; ++u) b[u] = pb[(int64_t)(kc + 4 * kh + u) * ldb];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) b[v][u] = pbk[(int64_t)(8 * v + u) * ldb];
-        }
-#pragma unroll
-        for (int v = 0; v < 8; ++v)
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[v][u], b[v][u], acc, 0, 0, 0);
+        for (int u = 0; u < 4; ++u)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[u], acc, 0, 0, 0);
     }
 #pragma unroll
-    for (int r = 0; r < 16; ++r) red[wave][r * 64 + lane] = acc[r];
-    __syncthreads();
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        const int o = threadIdx.x + kCT * m;            // (register r, lane l) of the quadrant
-        const float v = red[0][o] + red[1][o] + red[2][o] + red[3][o];
-        const int r = o >> 6, l = o & 63;
-        const int i = i0 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), j = j0 + (l & 31);
+    for (int q = 0; q < 16; ++q) {
+        const int i = i0 + (q & 3) + 8 * (q >> 2) + 4 * kh, j = j0 + r32;
         if (STEP == 0)
-            T[(int64_t)i * s + j] = v;
+            T[(int64_t)i * s + j] = acc[q];
         else
-            M[(int64_t)(a0 + i) * P + c0 + j] = -v;
+            M[(int64_t)(a0 + i) * P + c0 + j] = -acc[q];
     }
 }
 
@@ -709,7 +692,7 @@ static int factor_inv_launch(float* H, float* Minv, int32_t P, const int32_t* fi
     for (int sz = kNB; sz < P; sz *= 2) {
         const int pairs = (P - sz + 2 * sz - 1) / (2 * sz);
         const int sb = sz / kNB;
-        const dim3 grid((unsigned)(4 * pairs * sb * sb), (unsigned)n);
+        const dim3 grid((unsigned)(pairs * sb * sb), (unsigned)n);
         chol_inv_level_kernel<0><<<grid, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
         chol_inv_level_kernel<1><<<grid, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
     }

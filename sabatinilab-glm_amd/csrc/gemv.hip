@@ -79,80 +79,89 @@ __global__ void __launch_bounds__(256) round1_kernel(float* __restrict__ src, in
     }
 }
 
-template <int NP>
+template <int NP, int NT>
 struct StepE {
-    u32x2 b[4];          // row bits of the 4 row tiles
+    u32x2 b[NT];         // row bits of the NT row tiles
     u32x4 a[NP][4];      // piece x sub-step: 8 bf16 of this lane's fit
 };
 
-template <int NP>
-__device__ __forceinline__ void loadE(StepE<NP>& t, g_uint2* pb, g_uint4* pa, int64_t ld,
+template <int NP, int NT>
+__device__ __forceinline__ void loadE(StepE<NP, NT>& t, g_uint2* pb, g_uint4* pa, int64_t ld,
                                       int64_t pstride, int s) {
 #pragma unroll
-    for (int n = 0; n < 4; ++n) t.b[n] = gld2(pb + (int64_t)s * ld + 32 * n);
+    for (int n = 0; n < NT; ++n) t.b[n] = gld2(pb + (int64_t)s * ld + 32 * n);
 #pragma unroll
     for (int pc = 0; pc < NP; ++pc)
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) t.a[pc][ks] = gld4(pa + pc * pstride + s * 8 + 2 * ks);
 }
 
-// wait until at most `keep` loads are in flight, then tie the step's registers
-template <int NP>
-__device__ __forceinline__ void waitE(StepE<NP>& t, bool all) {
+// wait until only the two later steps' loads (2 (NT + 4 NP)) are in flight, then tie the step's
+// registers
+template <int NP, int NT>
+__device__ __forceinline__ void waitE(StepE<NP, NT>& t, bool all) {
+    constexpr int kLater = 2 * (NT + 4 * NP);
     if (all)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if constexpr (NP == 3)
-        asm volatile("s_waitcnt vmcnt(32)" ::: "memory");      // two later steps of 16 loads
+    else if constexpr (kLater == 32)
+        asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    else if constexpr (kLater == 24)
+        asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else if constexpr (kLater == 16)
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     else
-        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");      // two later steps of 8 loads
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-    for (int n = 0; n < 4; ++n) asm volatile("" : "+v"(t.b[n]));
+    for (int n = 0; n < NT; ++n) asm volatile("" : "+v"(t.b[n]));
 #pragma unroll
     for (int pc = 0; pc < NP; ++pc)
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) asm volatile("" : "+v"(t.a[pc][ks]));
 }
 
-template <int NP>
-__device__ __forceinline__ void mmaE(const StepE<NP>& t, int h, f32x16 (&acc)[NP][4]) {
+template <int NP, int NT>
+__device__ __forceinline__ void mmaE(const StepE<NP, NT>& t, int h, f32x16 (&acc)[NP][NT]) {
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-        bf16x8 bx[4];
+        bf16x8 bx[NT];
 #pragma unroll
-        for (int n = 0; n < 4; ++n) bx[n] = frag_two(t.b[n], ks, h);
+        for (int n = 0; n < NT; ++n) bx[n] = frag_two(t.b[n], ks, h);
 #pragma unroll
         for (int pc = 0; pc < NP; ++pc) {
             const bf16x8 a = __builtin_bit_cast(bf16x8, t.a[pc][ks]);
 #pragma unroll
-            for (int n = 0; n < 4; ++n)
+            for (int n = 0; n < NT; ++n)
                 acc[pc][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bx[n], acc[pc][n], 0, 0, 0);
         }
     }
 }
 
-// NP = 3: beta as three bf16 pieces (exact); NP = 1: one bf16 piece (a rounded direction)
-template <int NP>
+// NP = 3: beta as three bf16 pieces (exact); NP = 1: one bf16 piece (a rounded direction).
+// One wave: 32 fits x 32 NT rows (NT = 8 for one piece: the direction pieces are re-read from
+// L2 by every wave, so a wave covering more rows halves that traffic; NT = 4 for three pieces,
+// whose 3 x 8 accumulator tiles fill the register file).
+template <int NP, int NT>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 eta_bits_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
                 const __bf16* __restrict__ Dp, int32_t Bp, int32_t B,
                 const int32_t* __restrict__ slots, float* __restrict__ eta) {
     const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
-    const int64_t row0 = (int64_t)blockIdx.x * 128;
+    const int64_t row0 = (int64_t)blockIdx.x * 32 * NT;
     const int g = blockIdx.y;
     g_uint2* pb = as_global<g_uint2>(rbits + row0 + r);
     g_uint4* pa = as_global<g_uint4>(Dp + (int64_t)(g * 32 + r) * P + 8 * h);
     const int64_t pstride = (int64_t)Bp * P / 8;           // one piece plane, in uint4
     const int nsteps = P / 64;
 
-    f32x16 acc[NP][4];
+    f32x16 acc[NP][NT];
 #pragma unroll
     for (int pc = 0; pc < NP; ++pc)
 #pragma unroll
-        for (int n = 0; n < 4; ++n) acc[pc][n] = (f32x16){};
+        for (int n = 0; n < NT; ++n) acc[pc][n] = (f32x16){};
 
     // 3-stage register ring: the loads of step s+2 are issued before step s's MFMAs, so two
     // steps' L2 round trips overlap the MFMA work (clamped duplicate loads at the tail)
-    StepE<NP> A, Bs, C;
+    StepE<NP, NT> A, Bs, C;
     const int last = nsteps - 1;
     loadE(A, pb, pa, ld, pstride, 0);
     loadE(Bs, pb, pa, ld, pstride, 1 < last ? 1 : last);
@@ -177,7 +186,7 @@ eta_bits_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
     waitE(Bs, true);
 
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
+    for (int n = 0; n < NT; ++n)
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             const int f = g * 32 + (j & 3) + 8 * (j >> 2) + 4 * h;
@@ -379,20 +388,19 @@ int sglm_gemv_eta_bits(const uint32_t* rbits, int64_t ld, int32_t P, float* beta
     __bf16* Dp = reinterpret_cast<__bf16*>(work);
     const int64_t total = (int64_t)Bp * P;
     const unsigned gs = (unsigned)((total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048);
-    const dim3 grid((unsigned)(ld / 128), (unsigned)(Bp / 32));
     int st;
     if (exact) {
         split3_kernel<<<gs, 256, 0, s>>>(beta, P, B, Bp, slots, Dp);
         st = check_launch("split3_kernel");
         if (st) return st;
-        eta_bits_kernel<3><<<grid, 64, 0, s>>>(reinterpret_cast<const u32x2*>(rbits), ld, P, Dp,
-                                               Bp, B, slots, eta);
+        eta_bits_kernel<3, 4><<<dim3((unsigned)(ld / 128), (unsigned)(Bp / 32)), 64, 0, s>>>(
+            reinterpret_cast<const u32x2*>(rbits), ld, P, Dp, Bp, B, slots, eta);
     } else {
         round1_kernel<<<gs, 256, 0, s>>>(beta, P, B, Bp, slots, Dp);
         st = check_launch("round1_kernel");
         if (st) return st;
-        eta_bits_kernel<1><<<grid, 64, 0, s>>>(reinterpret_cast<const u32x2*>(rbits), ld, P, Dp,
-                                               Bp, B, slots, eta);
+        eta_bits_kernel<1, 8><<<dim3((unsigned)(ld / 256), (unsigned)(Bp / 32)), 64, 0, s>>>(
+            reinterpret_cast<const u32x2*>(rbits), ld, P, Dp, Bp, B, slots, eta);
     }
     return check_launch("eta_bits_kernel");
 }
