@@ -35,6 +35,19 @@ void launch_chol_diag(int nact, hipStream_t s, float* Hall, int32_t P, int32_t k
                       const int32_t* fits, uint8_t* frozen_all, float* rhs_all,
                       const float* diag_all, int32_t* info, int32_t nrefac, float* minv_all,
                       float* Mall);
+void launch_chol_diag4(int nact, hipStream_t s, float* Hall, int32_t P, int32_t k0,
+                       const int32_t* fits, uint8_t* frozen_all, const float* diag_all,
+                       int32_t* info, float* minv_all, float* Mall);
+
+// Four-wave diagonal step (chol_diag4.hip) in the factor + inverse chain; SGLM_DIAG4=0 keeps
+// the single-wave kernel (comparison runs).
+static bool diag4() {
+    static const bool v = [] {
+        const char* e = getenv("SGLM_DIAG4");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
 
 // rhs/z/x scratch per fit lives in `work` (float, [B][P]); the original diagonal in
 // `work + B*P` (float, [B][P]); the dropped-pivot counter is info[].
@@ -189,6 +202,7 @@ __global__ void __launch_bounds__(kCT) chol_panel_kernel(
 // one 32x32 quadrant per wave on v_mfma_f32_32x32x2f32 (exact f32 products, f32 accumulate),
 // operands loaded straight from the panel rows (L2-resident: grid x = tile, so one fit's
 // tiles run together), no LDS.  D[i][j] = sum_r U[k0+r][i] U[k0+r][j]; H[i][j] -= D.
+template <bool PIPE>
 __global__ void __launch_bounds__(kCT) chol_update_kernel(float* __restrict__ Hall, int32_t P,
                                                           int32_t k0, int32_t kc, int32_t s0,
                                                           const int32_t* __restrict__ fits) {
@@ -210,16 +224,41 @@ __global__ void __launch_bounds__(kCT) chol_update_kernel(float* __restrict__ Ha
     const float* pa = H + (int64_t)(k0 + kh) * P + ci + r32;
     const float* pb = H + (int64_t)(k0 + kh) * P + cj + r32;
     f32x16 acc = {};
-    for (int r = 0; r < kc; r += 16) {
-        float av[8], bv[8];
+    if (!PIPE) {
+        for (int r = 0; r < kc; r += 16) {
+            float av[8], bv[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            av[u] = pa[(int64_t)(r + 2 * u) * P];
-            bv[u] = pb[(int64_t)(r + 2 * u) * P];
+            for (int u = 0; u < 8; ++u) {
+                av[u] = pa[(int64_t)(r + 2 * u) * P];
+                bv[u] = pb[(int64_t)(r + 2 * u) * P];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
         }
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
+    } else {
+        // two register stages of 16 rows (kc is a multiple of 64): the next stage's 16 loads
+        // are in flight while this stage's 8 MFMAs run
+        float a0[8], b0[8], a1[8], b1[8];
+#define SGLM_UPD_LOAD(A, B, R)                                                             \
+    _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                        \
+        A[u] = pa[(int64_t)((R) + 2 * u) * P];                                             \
+        B[u] = pb[(int64_t)((R) + 2 * u) * P];                                             \
+    }
+#define SGLM_UPD_MMA(A, B)                                                                 \
+    _Pragma("unroll") for (int u = 0; u < 8; ++u)                                          \
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(A[u], B[u], acc, 0, 0, 0);
+        SGLM_UPD_LOAD(a0, b0, 0)
+        for (int r = 0; r < kc; r += 32) {
+            SGLM_UPD_LOAD(a1, b1, r + 16)
+            SGLM_UPD_MMA(a0, b0)
+            if (r + 32 < kc) {
+                SGLM_UPD_LOAD(a0, b0, r + 32)
+            }
+            SGLM_UPD_MMA(a1, b1)
+        }
+#undef SGLM_UPD_LOAD
+#undef SGLM_UPD_MMA
     }
     // D[row i][col j]: reg q -> i = (q&3) + 8(q>>2) + 4*kh, j = r32
 #pragma unroll
@@ -383,7 +422,7 @@ __global__ void __launch_bounds__(kST) chol_back2_kernel(
 // one level of the recursive doubling; STEP 0: T = B M_C (scratch), STEP 1: X = -M_A T (into M);
 // one 64 x 64 tile per workgroup, one 32 x 32 quadrant per wave over the whole K range (an
 // unrolled and a split-K variant both measured slower on the C4 chains)
-template <int STEP>
+template <int STEP, bool PIPE>
 __global__ void __launch_bounds__(kCT) chol_inv_level_kernel(const float* __restrict__ Hall,
                                                              float* __restrict__ Mall,
                                                              float* __restrict__ Tall,
@@ -424,14 +463,43 @@ __global__ void __launch_bounds__(kCT) chol_inv_level_kernel(const float* __rest
         khi = s;
     }
     f32x16 acc = {};
-    for (int kc = klo; kc < khi; kc += 8) {
-        const f32x4 a = *reinterpret_cast<const f32x4*>(pa + kc + 4 * kh);
-        float b[4];
+    if (!PIPE) {
+        for (int kc = klo; kc < khi; kc += 8) {
+            const f32x4 a = *reinterpret_cast<const f32x4*>(pa + kc + 4 * kh);
+            float b[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) b[u] = pb[(int64_t)(kc + 4 * kh + u) * ldb];
+            for (int u = 0; u < 4; ++u) b[u] = pb[(int64_t)(kc + 4 * kh + u) * ldb];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[u], acc, 0, 0, 0);
+            for (int u = 0; u < 4; ++u)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[u], acc, 0, 0, 0);
+        }
+    } else {
+        // K in blocks of 32 through two register stages (klo and khi are multiples of 64):
+        // block b+1's 20 loads are in flight while block b's 16 MFMAs run, instead of every
+        // 4-MFMA chunk waiting out a full load latency
+        f32x4 a0[4], a1[4];
+        float b0[4][4], b1[4][4];
+#define SGLM_INV_LOAD(A, B, KC)                                                            \
+    _Pragma("unroll") for (int v = 0; v < 4; ++v) {                                        \
+        const int k = (KC) + 8 * v + 4 * kh;                                               \
+        A[v] = *reinterpret_cast<const f32x4*>(pa + k);                                    \
+        _Pragma("unroll") for (int u = 0; u < 4; ++u) B[v][u] = pb[(int64_t)(k + u) * ldb]; \
+    }
+#define SGLM_INV_MMA(A, B)                                                                 \
+    _Pragma("unroll") for (int v = 0; v < 4; ++v)                                          \
+        _Pragma("unroll") for (int u = 0; u < 4; ++u)                                      \
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(A[v][u], B[v][u], acc, 0, 0, 0);
+        SGLM_INV_LOAD(a0, b0, klo)
+        for (int kc = klo; kc < khi; kc += 64) {
+            SGLM_INV_LOAD(a1, b1, kc + 32)
+            SGLM_INV_MMA(a0, b0)
+            if (kc + 64 < khi) {
+                SGLM_INV_LOAD(a0, b0, kc + 64)
+            }
+            SGLM_INV_MMA(a1, b1)
+        }
+#undef SGLM_INV_LOAD
+#undef SGLM_INV_MMA
     }
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -567,6 +635,34 @@ static int chol_lookahead() {
     return la;
 }
 
+// Inversion levels with the two-stage register pipeline (default; 1.52 -> 1.42 ms per 1-fit
+// chain) or the one-chunk loop (SGLM_CHOL_PIPE=0, comparison runs).
+static bool inv_pipe() {
+    static const bool v = [] {
+        const char* e = getenv("SGLM_CHOL_PIPE");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
+// The two-stage update measured slower on the box (16.5 vs 13.3 us per launch at 3 fits), so
+// it is opt-in (SGLM_UPD_PIPE=1).
+static bool upd_pipe() {
+    static const bool v = [] {
+        const char* e = getenv("SGLM_UPD_PIPE");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
+static void launch_update(dim3 grid, hipStream_t s, float* H, int32_t P, int32_t k0, int32_t kc,
+                          int32_t s0, const int32_t* fits) {
+    if (upd_pipe())
+        chol_update_kernel<true><<<grid, kCT, 0, s>>>(H, P, k0, kc, s0, fits);
+    else
+        chol_update_kernel<false><<<grid, kCT, 0, s>>>(H, P, k0, kc, s0, fits);
+}
+
 // fits[0 .. nrefac) are factored, fits[nrefac .. nact) reuse the factor and frozen set a
 // previous call left in H (engine.irls' kept Hessians): one launch chain for both, the
 // trailing updates over the refactored fits only.
@@ -607,7 +703,10 @@ static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t na
     // read-modify-write that bounds the chain at large batches) is swept P/(kLA*64) times
     auto factor_step = [&](int kb) {
         const int k0 = kb * kNB;
-        launch_chol_diag(nact, s, H, P, k0, fits, frozen, rhs, dg, info, nrefac, minv, Mall);
+        if (Mall && nrefac == nact && diag4())
+            launch_chol_diag4(nact, s, H, P, k0, fits, frozen, dg, info, minv, Mall);
+        else
+            launch_chol_diag(nact, s, H, P, k0, fits, frozen, rhs, dg, info, nrefac, minv, Mall);
         const int rem = P - k0 - kNB;
         if (rem > 0)
             chol_panel_kernel<<<dim3(nact, rem / kNB), kCT, 0, s>>>(H, P, k0, fits, minv, rhs,
@@ -621,13 +720,13 @@ static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t na
             const int nr = ke - 1 - b;                         // band rows b+1 .. ke-1
             const int T = nb - b - 1;
             if (nrefac > 0 && nr > 0)
-                chol_update_kernel<<<dim3(nr * T - nr * (nr - 1) / 2, nrefac), kCT, 0, s>>>(
-                    H, P, b * kNB, kNB, b + 1, fits);
+                launch_update(dim3(nr * T - nr * (nr - 1) / 2, nrefac), s, H, P, b * kNB, kNB,
+                              b + 1, fits);
         }
         const int T = nb - ke;
         if (nrefac > 0 && T > 0)
-            chol_update_kernel<<<dim3(T * (T + 1) / 2, nrefac), kCT, 0, s>>>(
-                H, P, kb * kNB, (ke - kb) * kNB, ke, fits);
+            launch_update(dim3(T * (T + 1) / 2, nrefac), s, H, P, kb * kNB, (ke - kb) * kNB, ke,
+                          fits);
     }
     st = check_launch("chol block kernels");
     if (st) return st;
@@ -677,6 +776,7 @@ extern "C" int sglm_chol_solve_mixed(float* H, int32_t P, const int32_t* fits, i
                             as_stream(stream));
 }
 
+
 // The factorisation + inversion chain (~110 launches) of fits[0 .. n).
 static int factor_inv_launch(float* H, float* Minv, int32_t P, const int32_t* fits, int32_t n,
                              const float* dshift, float* delta, int32_t* info, uint8_t* frozen,
@@ -689,12 +789,18 @@ static int factor_inv_launch(float* H, float* Minv, int32_t P, const int32_t* fi
     // Y (B x P), T (B x tcap)
     float* T = (float*)work + (size_t)3 * B * P + (size_t)B * kNB * kNB;
     const int64_t tcap = inv_tcap(P);
+    const bool pipe = inv_pipe();
     for (int sz = kNB; sz < P; sz *= 2) {
         const int pairs = (P - sz + 2 * sz - 1) / (2 * sz);
         const int sb = sz / kNB;
         const dim3 grid((unsigned)(pairs * sb * sb), (unsigned)n);
-        chol_inv_level_kernel<0><<<grid, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
-        chol_inv_level_kernel<1><<<grid, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
+        if (pipe) {
+            chol_inv_level_kernel<0, true><<<grid, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
+            chol_inv_level_kernel<1, true><<<grid, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
+        } else {
+            chol_inv_level_kernel<0, false><<<grid, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
+            chol_inv_level_kernel<1, false><<<grid, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
+        }
     }
     return check_launch("chol_inv_level_kernel");
 }

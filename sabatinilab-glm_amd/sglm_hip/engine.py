@@ -77,6 +77,9 @@ XMASK_SLOW = 0.7                # aliased-step contraction above which a fit lea
 # iteration over every fit, grouped by factor) instead of per-fit triangular substitution
 # chains; 0 restores sglm_chol_solve_mixed / sglm_chol_solve_alias.
 SOLVE_INV = __import__("os").environ.get("SGLM_SOLVE_INV", "1") == "1"
+# where the factorisation chain runs: "side" (its own stream, overlapping the gradient),
+# "prio" (the same at high stream priority), "serial" (the main stream, before the gradient)
+CHOL_STREAM = __import__("os").environ.get("SGLM_CHOL_STREAM", "side")
 
 
 def require_gpu():
@@ -681,7 +684,9 @@ def _side_stream():
     key = (torch.cuda.current_device(), "chol")
     sd = streams.get(key)
     if sd is None:
-        sd = streams[key] = torch.cuda.Stream()
+        # high priority: the chain's small latency-bound launches are dispatched ahead of the
+        # gradient's workgroups as slots free up, instead of queueing behind a full-chip grid
+        sd = streams[key] = torch.cuda.Stream(priority=-1 if CHOL_STREAM == "prio" else 0)
     return sd
 
 
@@ -1064,7 +1069,12 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
             rsc_d = up(rsc, np.float32)
             nl = int(lst.size)
             fact_done = None
-            if nref:
+            if nref and CHOL_STREAM == "serial":
+                bf.fact_fits[:nref].copy_(ints[:nref])
+                _lib.call("sglm_chol_solve_inv", _p(bf.H), _p(bf.Minv), P, _p(bf.fact_fits), None,
+                          None, int(nref), int(nref), None, 0, None, _p(bf.dshift), _p(bf.delta),
+                          _p(bf.info), _p(bf.frozen), B, _p(bf.cwork), st)
+            elif nref:
                 # factor + invert the new Hessians on a side stream while the gradient runs
                 side = _side_stream()
                 bf.fact_fits[:nref].copy_(ints[:nref])
