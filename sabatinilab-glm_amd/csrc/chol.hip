@@ -511,6 +511,107 @@ __global__ void __launch_bounds__(kCT) chol_inv_level_kernel(const float* __rest
     }
 }
 
+// The same level with the 64 x 64 tile's operands staged through LDS (SGLM_INV_LDS=1): K in
+// blocks of 32, A [64][32] and B [32][64] loaded once per workgroup (the register variant has
+// every wave fetch its own 32 rows and 32 columns, so each operand crosses L2 twice), two LDS
+// buffers with the next block's global loads in registers while this block's 16 MFMAs per wave
+// run, one barrier per block.
+constexpr int kLA = 36;             // A row stride (floats): 16-byte aligned rows
+constexpr int kLB = 72;             // B row stride: the two k-halves of a wave on disjoint banks
+template <int STEP>
+__global__ void __launch_bounds__(kCT) chol_inv_level_lds_kernel(const float* __restrict__ Hall,
+                                                                 float* __restrict__ Mall,
+                                                                 float* __restrict__ Tall,
+                                                                 int32_t P, int32_t s,
+                                                                 const int32_t* __restrict__ fits,
+                                                                 int64_t tcap) {
+    __shared__ __attribute__((aligned(16))) float sa[2][64 * kLA];
+    __shared__ __attribute__((aligned(16))) float sb[2][32 * kLB];
+    const int fit = fits[blockIdx.y];
+    const float* H = Hall + (int64_t)fit * P * P;
+    float* M = Mall + (int64_t)fit * P * P;
+    const int nsb = s / kNB;
+    int t = blockIdx.x;
+    const int pair = t / (nsb * nsb);
+    t -= pair * nsb * nsb;
+    const int ti = t / nsb, tj = t - ti * nsb;
+    const int a0 = 2 * s * pair, c0 = a0 + s;
+    const int cs = min(s, P - c0);
+    if (cs <= 0 || tj * kNB >= cs) return;
+    float* T = Tall + (int64_t)blockIdx.y * tcap + (int64_t)pair * s * s;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r32 = lane & 31, kh = lane >> 5;
+    const int wr = wave >> 1, wc = wave & 1;
+    // global operand bases: A rows (64 of them, stride P), B rows k (stride ldb), 64 columns
+    const float* ga;
+    const float* gb;
+    int64_t ldb;
+    int klo, khi;
+    if (STEP == 0) {                                   // A = U[a0 + i][c0 + k], B = M[c0 + k][c0 + j]
+        ga = H + (int64_t)(a0 + ti * kNB) * P + c0;
+        gb = M + (int64_t)c0 * P + c0 + tj * kNB;
+        ldb = P;
+        klo = 0;
+        khi = (tj + 1) * kNB;
+    } else {                                           // A = M[a0 + i][a0 + k], B = T[k][j]
+        ga = M + (int64_t)(a0 + ti * kNB) * P + a0;
+        gb = T + tj * kNB;
+        ldb = s;
+        klo = ti * kNB;
+        khi = s;
+    }
+    // this thread's share of a block: A row tid>>2, k 8*(tid&3) .. +7; B row k = tid>>3,
+    // columns 8*(tid&7) .. +7
+    const int ar = tid >> 2, ak = 8 * (tid & 3);
+    const int bk = tid >> 3, bj = 8 * (tid & 7);
+    f32x4 ra0, ra1, rb0, rb1;
+    auto gload = [&](int kb) {
+        const float* pa = ga + (int64_t)ar * P + kb + ak;
+        ra0 = *reinterpret_cast<const f32x4*>(pa);
+        ra1 = *reinterpret_cast<const f32x4*>(pa + 4);
+        const float* pb = gb + (int64_t)(kb + bk) * ldb + bj;
+        rb0 = *reinterpret_cast<const f32x4*>(pb);
+        rb1 = *reinterpret_cast<const f32x4*>(pb + 4);
+    };
+    auto sstore = [&](int buf) {
+        *reinterpret_cast<f32x4*>(&sa[buf][ar * kLA + ak]) = ra0;
+        *reinterpret_cast<f32x4*>(&sa[buf][ar * kLA + ak + 4]) = ra1;
+        *reinterpret_cast<f32x4*>(&sb[buf][bk * kLB + bj]) = rb0;
+        *reinterpret_cast<f32x4*>(&sb[buf][bk * kLB + bj + 4]) = rb1;
+    };
+    f32x16 acc = {};
+    gload(klo);
+    sstore(0);
+    __syncthreads();
+    int cur = 0;
+    for (int kb = klo; kb < khi; kb += 32) {
+        const bool more = kb + 32 < khi;
+        if (more) gload(kb + 32);
+        const float* A = &sa[cur][(wr * 32 + r32) * kLA + 4 * kh];
+        const float* Bq = &sb[cur][(4 * kh) * kLB + wc * 32 + r32];
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const f32x4 a = *reinterpret_cast<const f32x4*>(A + 8 * kk);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], Bq[(8 * kk + u) * kLB], acc, 0,
+                                                           0, 0);
+        }
+        if (more) sstore(cur ^ 1);
+        __syncthreads();
+        cur ^= 1;
+    }
+    const int i0 = ti * kNB + wr * 32, j0 = tj * kNB + wc * 32;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int i = i0 + (q & 3) + 8 * (q >> 2) + 4 * kh, j = j0 + r32;
+        if (STEP == 0)
+            T[(int64_t)i * s + j] = acc[q];
+        else
+            M[(int64_t)(a0 + i) * P + c0 + j] = -acc[q];
+    }
+}
+
 // Solves on explicit inverses.  Tile t = rows [start, start + cnt) of the fit list (cnt <= 32,
 // one factor: slot fsrc[start]); blockIdx.x = a 32-wide output column block; the 4 waves split
 // K and reduce through LDS.  SECOND = false: Y[q][j] = sum_k G[q][k] M[k][j] with G = rscale *
@@ -641,6 +742,15 @@ static bool inv_pipe() {
     static const bool v = [] {
         const char* e = getenv("SGLM_CHOL_PIPE");
         return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
+// Inversion levels through LDS (chol_inv_level_lds_kernel), SGLM_INV_LDS=1.
+static bool inv_lds() {
+    static const bool v = [] {
+        const char* e = getenv("SGLM_INV_LDS");
+        return e && e[0] == '1';
     }();
     return v;
 }
@@ -794,7 +904,10 @@ static int factor_inv_launch(float* H, float* Minv, int32_t P, const int32_t* fi
         const int pairs = (P - sz + 2 * sz - 1) / (2 * sz);
         const int sb = sz / kNB;
         const dim3 grid((unsigned)(pairs * sb * sb), (unsigned)n);
-        if (pipe) {
+        if (inv_lds()) {
+            chol_inv_level_lds_kernel<0><<<grid, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
+            chol_inv_level_lds_kernel<1><<<grid, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
+        } else if (pipe) {
             chol_inv_level_kernel<0, true><<<grid, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
             chol_inv_level_kernel<1, true><<<grid, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
         } else {

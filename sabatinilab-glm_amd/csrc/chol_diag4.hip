@@ -25,75 +25,105 @@ static __global__ void __launch_bounds__(256) chol_diag4_kernel(
     float* __restrict__ Hall, int32_t P, int32_t k0, const int32_t* __restrict__ fits,
     uint8_t* __restrict__ frozen_all, const float* __restrict__ diag_all,
     int32_t* __restrict__ info, float* __restrict__ minv_all, float* __restrict__ Mall) {
-    __shared__ __attribute__((aligned(16))) float su[2][64];   // row Q of U, position (i&3)*16 + (i>>2)
-    __shared__ float sx[2][64];                                // row Q of V, by column
+    // per buffer and step h of the pair: the row multipliers U[Q+h][i] at position rpos(i)
+    // (row Q+1 zeroed in step 0's: the owner applied that term itself), the column multipliers
+    // U[Q+h][c] and V[Q+h][c] by column
+    __shared__ __attribute__((aligned(16))) float srow[2][2][64];
+    __shared__ float scol[2][2][64];
+    __shared__ float sx[2][2][64];
     __shared__ float sv[64][65];                               // V transposed (Mall row stores)
     const int fit = fits[blockIdx.x];
     float* H = Hall + (int64_t)fit * P * P;
     uint8_t* frz = frozen_all + (int64_t)fit * P + k0;
     const int c = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // register k of wave w holds row 8 (k >> 1) + 2 w + (k & 1)
     float a[16], v[16];
     {
         int cl = c;                                  // opaque lane index: the selects below are
         asm volatile("" : "+v"(cl));                 // not CSE'd into the steps
-        const float* col = H + (int64_t)(k0 + w) * P + k0 + c;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const float x = col[(int64_t)(4 * j) * P];
-            a[j] = 4 * j + w <= cl ? x : 0.0f;
-            v[j] = 4 * j + w == cl ? 1.0f : 0.0f;
+        for (int k = 0; k < 16; ++k) {
+            const int r = 8 * (k >> 1) + 2 * w + (k & 1);
+            const float x = H[(int64_t)(k0 + r) * P + k0 + c];
+            a[k] = r <= cl ? x : 0.0f;
+            v[k] = r == cl ? 1.0f : 0.0f;
         }
     }
     int myfrz = frz[c];
     const float thr = 1e-6f * diag_all[(int64_t)fit * P + k0 + c];
     int dropped = 0;
-    const int upos = (c & 3) * 16 + (c >> 2);
+    const int rpos = ((c >> 1) & 3) * 16 + 2 * (c >> 3) + (c & 1);
 #pragma unroll
-    for (int Q = 0; Q < 64; ++Q) {
-        const int buf = Q & 1;
-        if (w == (Q & 3)) {                          // wave-uniform: the owner of row Q
-            const int jq = Q >> 2;
-            const int verdict = (myfrz ? 2 : 0) | (a[jq] > thr ? 0 : 1);
-            const int vq = __builtin_amdgcn_readlane(verdict, Q);
-            const bool was = (vq & 2) != 0;
-            const bool drop = vq != 0;
-            const float piv = lane4f(a[jq], Q);
-            const float r = drop ? 0.0f : __builtin_amdgcn_rsqf(piv);
-            const float d = drop ? 1.0f : piv * r;
-            const float u = c > Q ? a[jq] * r : 0.0f;            // U[Q][c]
-            a[jq] = c == Q ? d : (c > Q ? u : a[jq]);
-            const float xq = v[jq] * r;                          // V[Q][c]
-            v[jq] = xq;
-            const bool newly = drop && !was && c == Q;
+    for (int Q = 0; Q < 64; Q += 2) {
+        const int buf = (Q >> 1) & 1;
+        if (w == ((Q >> 1) & 3)) {                   // wave-uniform: the owner of rows Q, Q+1
+            const int k = 2 * (Q >> 3);              // row Q in a[k], row Q+1 in a[k + 1]
+            // step Q
+            int verdict = (myfrz ? 2 : 0) | (a[k] > thr ? 0 : 1);
+            int vq = __builtin_amdgcn_readlane(verdict, Q);
+            bool drop = vq != 0;
+            bool newly = drop && (vq & 2) == 0 && c == Q;
+            float piv = lane4f(a[k], Q);
+            float r = drop ? 0.0f : __builtin_amdgcn_rsqf(piv);
+            float d = drop ? 1.0f : piv * r;
+            const float u0 = c > Q ? a[k] * r : 0.0f;            // U[Q][c]
+            a[k] = c == Q ? d : (c > Q ? u0 : a[k]);
+            const float x0 = v[k] * r;                           // V[Q][c]
+            v[k] = x0;
             myfrz = newly ? 1 : myfrz;
             dropped = newly ? 1 : dropped;
-            su[buf][upos] = u;
-            sx[buf][c] = xq;
+            // its term on row Q+1 (this wave's own row)
+            const float t = lane4f(u0, Q + 1);                  // U[Q][Q+1]
+            a[k + 1] = fmaf(-t, u0, a[k + 1]);
+            v[k + 1] = fmaf(-t, x0, v[k + 1]);
+            // step Q+1
+            verdict = (myfrz ? 2 : 0) | (a[k + 1] > thr ? 0 : 1);
+            vq = __builtin_amdgcn_readlane(verdict, Q + 1);
+            drop = vq != 0;
+            newly = drop && (vq & 2) == 0 && c == Q + 1;
+            piv = lane4f(a[k + 1], Q + 1);
+            r = drop ? 0.0f : __builtin_amdgcn_rsqf(piv);
+            d = drop ? 1.0f : piv * r;
+            const float u1 = c > Q + 1 ? a[k + 1] * r : 0.0f;    // U[Q+1][c]
+            a[k + 1] = c == Q + 1 ? d : (c > Q + 1 ? u1 : a[k + 1]);
+            const float x1 = v[k + 1] * r;                       // V[Q+1][c]
+            v[k + 1] = x1;
+            myfrz = newly ? 1 : myfrz;
+            dropped = newly ? 1 : dropped;
+            srow[buf][0][rpos] = c == Q + 1 ? 0.0f : u0;
+            srow[buf][1][rpos] = u1;
+            scol[buf][0][c] = u0;
+            scol[buf][1][c] = u1;
+            sx[buf][0][c] = x0;
+            sx[buf][1][c] = x1;
         }
         __syncthreads();
-        const float uc = su[buf][upos];
-        const float xc = sx[buf][c];
-        const f32x4* ur = reinterpret_cast<const f32x4*>(&su[buf][w * 16]);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const f32x4 ui = ur[q];                              // U[Q][4j + w], j = 4q..4q+3
+        for (int h = 0; h < 2; ++h) {
+            const float uc = scol[buf][h][c];
+            const float xc = sx[buf][h][c];
+            const f32x4* ur = reinterpret_cast<const f32x4*>(&srow[buf][h][w * 16]);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                a[4 * q + e] = fmaf(-ui[e], uc, a[4 * q + e]);
-                v[4 * q + e] = fmaf(-ui[e], xc, v[4 * q + e]);
+            for (int q = 0; q < 4; ++q) {
+                const f32x4 ui = ur[q];                          // U[Q+h][row of a[4q + e]]
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    a[4 * q + e] = fmaf(-ui[e], uc, a[4 * q + e]);
+                    v[4 * q + e] = fmaf(-ui[e], xc, v[4 * q + e]);
+                }
             }
         }
     }
     // whole block (the strictly-lower part is never read); M_kk row-major for the panel step
-    float* col = H + (int64_t)(k0 + w) * P + k0 + c;
-    float* mo = minv_all + (int64_t)blockIdx.x * 64 * 64 + (int64_t)w * 64 + c;
+    float* mo = minv_all + (int64_t)blockIdx.x * 64 * 64 + c;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        col[(int64_t)(4 * j) * P] = a[j];
-        mo[j * 4 * 64] = v[j];
-        sv[c][4 * j + w] = v[j];
+    for (int k = 0; k < 16; ++k) {
+        const int r = 8 * (k >> 1) + 2 * w + (k & 1);
+        H[(int64_t)(k0 + r) * P + k0 + c] = a[k];
+        mo[r * 64] = v[k];
+        sv[c][r] = v[k];
     }
-    if ((c & 3) == w) {                              // the owner of step c
+    if (((c >> 1) & 3) == w) {                       // the owner of step c
         frz[c] = (uint8_t)myfrz;
         if (dropped) atomicAdd(&info[fit], 1);
     }
