@@ -511,7 +511,7 @@ __global__ void __launch_bounds__(kCT) chol_inv_level_kernel(const float* __rest
     }
 }
 
-// The same level with the 64 x 64 tile's operands staged through LDS (SGLM_INV_LDS=1): K in
+// The same level with the 64 x 64 tile's operands staged through LDS (the default): K in
 // blocks of 32, A [64][32] and B [32][64] loaded once per workgroup (the register variant has
 // every wave fetch its own 32 rows and 32 columns, so each operand crosses L2 twice), two LDS
 // buffers with the next block's global loads in registers while this block's 16 MFMAs per wave
@@ -746,11 +746,13 @@ static bool inv_pipe() {
     return v;
 }
 
-// Inversion levels through LDS (chol_inv_level_lds_kernel), SGLM_INV_LDS=1.
+// Inversion levels through LDS (chol_inv_level_lds_kernel; default: 1-fit chain 1.22 -> 1.16 ms,
+// 3 fits 1.47 -> 1.33 ms, C4 grid 60-62 -> 58-59 ms on one box), SGLM_INV_LDS=0 for the
+// register variants.
 static bool inv_lds() {
     static const bool v = [] {
         const char* e = getenv("SGLM_INV_LDS");
-        return e && e[0] == '1';
+        return !(e && e[0] == '0');
     }();
     return v;
 }
