@@ -268,6 +268,73 @@ __global__ void __launch_bounds__(kCT) chol_update_kernel(float* __restrict__ Ha
     }
 }
 
+// The trailing update with both 64-column strips of the panel rows staged through LDS
+// (the default): K in blocks of 32 rows, each strip loaded once per workgroup with float4
+// row loads (the register variant has every wave fetch its own 32 columns of both strips, so
+// each crosses L2 twice, as scalar loads), two LDS buffers with the next block's loads in
+// registers during this block's 16 MFMAs per wave, one barrier per block.
+constexpr int kLU = 68;             // strip row stride (floats)
+__global__ void __launch_bounds__(kCT) chol_update_lds_kernel(float* __restrict__ Hall,
+                                                              int32_t P, int32_t k0, int32_t kc,
+                                                              int32_t s0,
+                                                              const int32_t* __restrict__ fits) {
+    __shared__ __attribute__((aligned(16))) float sa[2][32 * kLU];
+    __shared__ __attribute__((aligned(16))) float sb[2][32 * kLU];
+    const int fit = fits[blockIdx.y];
+    float* H = Hall + (int64_t)fit * P * P;
+    const int T = P / kNB - s0;
+    int t = blockIdx.x, bi = 0, bj;
+    {
+        int rowlen = T;
+        while (t >= rowlen) { t -= rowlen; ++bi; --rowlen; }
+        bj = bi + t;
+    }
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r32 = lane & 31, kh = lane >> 5;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int ca = (s0 + bi) * kNB, cb = (s0 + bj) * kNB;     // strip columns
+    const int lr = tid >> 3, lcol = 8 * (tid & 7);             // this thread's block share
+    const float* ga = H + (int64_t)(k0 + lr) * P + ca + lcol;
+    const float* gb = H + (int64_t)(k0 + lr) * P + cb + lcol;
+    f32x4 ra0, ra1, rb0, rb1;
+    auto gload = [&](int r) {
+        ra0 = *reinterpret_cast<const f32x4*>(ga + (int64_t)r * P);
+        ra1 = *reinterpret_cast<const f32x4*>(ga + (int64_t)r * P + 4);
+        rb0 = *reinterpret_cast<const f32x4*>(gb + (int64_t)r * P);
+        rb1 = *reinterpret_cast<const f32x4*>(gb + (int64_t)r * P + 4);
+    };
+    auto sstore = [&](int buf) {
+        *reinterpret_cast<f32x4*>(&sa[buf][lr * kLU + lcol]) = ra0;
+        *reinterpret_cast<f32x4*>(&sa[buf][lr * kLU + lcol + 4]) = ra1;
+        *reinterpret_cast<f32x4*>(&sb[buf][lr * kLU + lcol]) = rb0;
+        *reinterpret_cast<f32x4*>(&sb[buf][lr * kLU + lcol + 4]) = rb1;
+    };
+    f32x16 acc = {};
+    gload(0);
+    sstore(0);
+    __syncthreads();
+    int cur = 0;
+    for (int r = 0; r < kc; r += 32) {
+        const bool more = r + 32 < kc;
+        if (more) gload(r + 32);
+        const float* A = &sa[cur][kh * kLU + wr * 32 + r32];
+        const float* Bq = &sb[cur][kh * kLU + wc * 32 + r32];
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(A[2 * u * kLU], Bq[2 * u * kLU], acc, 0, 0,
+                                                       0);
+        if (more) sstore(cur ^ 1);
+        __syncthreads();
+        cur ^= 1;
+    }
+    const int ci = ca + wr * 32, cj = cb + wc * 32;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        float* h = &H[(int64_t)(ci + (q & 3) + 8 * (q >> 2) + 4 * kh) * P + cj + r32];
+        *h -= acc[q];
+    }
+}
+
 // Triangular solves on a stored factor, right-looking, one 1024-thread workgroup per fit: per
 // 64-block, wave 0 solves the 64 x 64 diagonal triangle (readlane broadcasts, branch-free),
 // then all 16 waves fold the solved block into the rest of the right-hand side, which stays in
@@ -767,9 +834,22 @@ static bool upd_pipe() {
     return v;
 }
 
+// Trailing updates through LDS (chol_update_lds_kernel; default: the same MFMA sequence as
+// the register kernel, so bitwise the same factor; 1-fit chain 1.19 -> 1.09 ms, C4 grid
+// 58.8-59.2 -> 58.0-58.2 ms in an alternating A/B), SGLM_UPD_LDS=0 for the register kernel.
+static bool upd_lds() {
+    static const bool v = [] {
+        const char* e = getenv("SGLM_UPD_LDS");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 static void launch_update(dim3 grid, hipStream_t s, float* H, int32_t P, int32_t k0, int32_t kc,
                           int32_t s0, const int32_t* fits) {
-    if (upd_pipe())
+    if (upd_lds())
+        chol_update_lds_kernel<<<grid, kCT, 0, s>>>(H, P, k0, kc, s0, fits);
+    else if (upd_pipe())
         chol_update_kernel<true><<<grid, kCT, 0, s>>>(H, P, k0, kc, s0, fits);
     else
         chol_update_kernel<false><<<grid, kCT, 0, s>>>(H, P, k0, kc, s0, fits);
