@@ -3,7 +3,7 @@
 set -e
 export TMPDIR=/tmp
 KV=${1:-SGLM_UPD_LDS=1}
-O=gpurun_out/ab2; mkdir -p $O
+O=gpurun_out/ab_${KV//[=.]/_}; mkdir -p $O
 timeout -k 10 120 python -u tools/chol_bench.py > $O/chain_base.json 2> $O/chain_base.err
 env $KV timeout -k 10 120 python -u tools/chol_bench.py > $O/chain_var.json 2> $O/chain_var.err
 env $KV timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/tests_var.log 2>&1
