@@ -241,6 +241,53 @@ def test_chol_solve_inv_vs_float64(engine, torch_mod, P, p, B):
         assert rel(x[q], want(src, q, sc)) < 1e-3, q
 
 
+@pytest.mark.parametrize("P", [128, 2048])
+def test_chol_inv_dropped_pivots(engine, torch_mod, P):
+    """Factor + inverse chain (four-wave diagonal step) on a Gram with exactly duplicated and
+    all-zero columns and no ridge: the dependent pivots fall below 1e-6 of their diagonal and
+    are dropped (counted in info, frozen), and the solve on the explicit inverse equals the
+    float64 solve restricted to the kept coordinates."""
+    torch = torch_mod
+    from sglm_hip import _lib
+    rng = np.random.default_rng(P + 7)
+    p = P - 9
+    A = rng.normal(size=(p + 300, p))
+    dup = [3, 70 % p, p - 2]                         # columns that copy their left neighbour
+    for j in dup:
+        A[:, j] = A[:, j - 1]
+    A[:, 5] = 0.0                                    # an all-zero column (frozen at prep)
+    H = np.zeros((1, P, P), np.float32)
+    H[0, :p, :p] = A.T @ A / 100.0
+    dsh = np.full((1, P), -1.0, np.float32)          # frozen padding
+    dsh[0, :p] = 0.0                                 # no ridge: duplicates are singular
+    g = rng.normal(size=(1, P))
+    Hd = torch.from_numpy(H).cuda()
+    Md = torch.empty_like(Hd)
+    gd = torch.from_numpy(g).cuda()
+    out = torch.full((1, P), np.nan, dtype=torch.float32, device="cuda")
+    info = torch.zeros(1, dtype=torch.int32, device="cuda")
+    frozen = torch.zeros((1, P), dtype=torch.uint8, device="cuda")
+    dshd = torch.from_numpy(dsh).cuda()
+    cw = torch.empty(_lib.query("sglm_chol_work_bytes", P, 1), dtype=torch.uint8, device="cuda")
+    ints = torch.tensor(np.array([0, 0, 0, 1], np.int32), device="cuda")   # fits, fsrc, tile
+    rs = torch.ones(1, dtype=torch.float32, device="cuda")
+    _lib.call("sglm_chol_solve_inv", Hd.data_ptr(), Md.data_ptr(), P, ints.data_ptr(),
+              ints[1:].data_ptr(), rs.data_ptr(), 1, 1, ints[2:].data_ptr(), 1, gd.data_ptr(),
+              dshd.data_ptr(), out.data_ptr(), info.data_ptr(), frozen.data_ptr(), 1,
+              cw.data_ptr(), 0)
+    x = out.cpu().numpy()[0]
+    frz = frozen.cpu().numpy()[0].astype(bool)
+    assert int(info.item()) == len(dup)              # the duplicates' pivots were dropped
+    assert frz[dup].all() and frz[5] and frz[p:].all()
+    keep = np.flatnonzero(~frz)
+    assert keep.size == p - len(dup) - 1
+    Hk = (A.T @ A / 100.0)[np.ix_(keep, keep)]
+    ref = np.zeros(P)
+    ref[keep] = -np.linalg.solve(Hk, g[0, keep])
+    assert np.all(x[frz] == 0)
+    assert rel(x, ref) < 1e-2, rel(x, ref)
+
+
 def _fit_one(engine, X, y, family, power, lam, fit_intercept=True):
     d = engine.Design.from_host(X)
     prob = engine.Problem(d, [y], [np.ones(len(y), np.uint8)])
