@@ -684,13 +684,17 @@ __global__ void __launch_bounds__(kCT) chol_inv_level_lds_kernel(const float* __
 // K and reduce through LDS.  SECOND = false: Y[q][j] = sum_k G[q][k] M[k][j] with G = rscale *
 // g (float64 -> f32) zeroed on the factor's frozen coordinates.  SECOND = true:
 // delta[fit][i] = -sum_j Y[q][j] M[i][j], zero on frozen coordinates.
-template <bool SECOND>
+// STAGE (first pass only, the default): each wave copies its 64 x 32 block of M into
+// LDS with eight float4 row loads per lane and reads the B operands from there, instead of 32
+// scalar column loads per lane from L2.
+template <bool SECOND, bool STAGE = false>
 __global__ void __launch_bounds__(kCT) chol_inv_apply_kernel(
     const float* __restrict__ Mall, int32_t P, const int32_t* __restrict__ fits,
     const int32_t* __restrict__ fsrc, const float* __restrict__ rscale,
     const int32_t* __restrict__ tiles, const double* __restrict__ gall,
     const uint8_t* __restrict__ frozen_all, float* __restrict__ Y, float* __restrict__ delta_all) {
     __shared__ float red[4][16 * 64];
+    __shared__ __attribute__((aligned(16))) float sm[STAGE ? 4 : 1][STAGE ? 64 * 32 : 4];
     const int start = tiles[2 * blockIdx.y], cnt = tiles[2 * blockIdx.y + 1];
     const int src = fsrc[start];
     const float* M = Mall + (int64_t)src * P * P;
@@ -710,6 +714,19 @@ __global__ void __launch_bounds__(kCT) chol_inv_apply_kernel(
         for (int kb = kNB * wave; kb < khi; kb += 4 * kNB) {
             float a[8][4], b[8][4];
             const float* pbk = pb + (int64_t)(kb + 4 * kh) * P;
+            if (STAGE) {
+                const float* src = M + (int64_t)kb * P + c0 + 4 * (lane & 7);
+                f32x4 tv[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    tv[i] = *reinterpret_cast<const f32x4*>(src + (int64_t)((lane >> 3) + 8 * i) * P);
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    *reinterpret_cast<f32x4*>(&sm[wave][((lane >> 3) + 8 * i) * 32 + 4 * (lane & 7)]) =
+                        tv[i];
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+            }
 #pragma unroll
             for (int v = 0; v < 8; ++v) {
                 const int k = kb + 8 * v + 4 * kh;
@@ -724,7 +741,8 @@ __global__ void __launch_bounds__(kCT) chol_inv_apply_kernel(
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     if (((keep >> (8 * u)) & 0xff) != 0xff) a[v][u] = 0.0f;
-                    b[v][u] = pbk[(8 * v + u) * P];
+                    b[v][u] = STAGE ? sm[wave][(8 * v + 4 * kh + u) * 32 + r32]
+                                    : pbk[(8 * v + u) * P];
                 }
             }
 #pragma unroll
@@ -732,6 +750,10 @@ __global__ void __launch_bounds__(kCT) chol_inv_apply_kernel(
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[v][u], b[v][u], acc, 0, 0, 0);
+            if (STAGE) {                             // this block's reads done before the next
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // block's writes
+                __builtin_amdgcn_wave_barrier();
+            }
         }
     } else {
         const float* py = Y + (int64_t)q * P;
@@ -830,6 +852,17 @@ static bool upd_pipe() {
     static const bool v = [] {
         const char* e = getenv("SGLM_UPD_PIPE");
         return e && e[0] == '1';
+    }();
+    return v;
+}
+
+// First inverse-solve pass with LDS-staged M blocks (chol_inv_apply_kernel<false, true>;
+// default: the same operands and MFMA order, C4 grid 59.6 / 57.2 -> 57.4 / 56.9 ms and the
+// 8-rank share 22.8 -> 21.9 ms in an alternating A/B), SGLM_APPLY_STAGE=0 for column loads.
+static bool apply_stage() {
+    static const bool v = [] {
+        const char* e = getenv("SGLM_APPLY_STAGE");
+        return !(e && e[0] == '0');
     }();
     return v;
 }
@@ -1097,8 +1130,12 @@ extern "C" int sglm_chol_solve_inv(float* H, float* Minv, int32_t P, const int32
     if (ntiles <= 0) return SGLM_OK;         // factor + invert only (the solve comes later)
     float* Y = (float*)work + (size_t)2 * B * P + (size_t)B * kNB * kNB;
     const dim3 grid((unsigned)(P / 32), (unsigned)ntiles);
-    chol_inv_apply_kernel<false><<<grid, kCT, 0, s>>>(Minv, P, fits, fsrc, rscale, tiles, g,
-                                                       frozen, Y, delta);
+    if (apply_stage())
+        chol_inv_apply_kernel<false, true><<<grid, kCT, 0, s>>>(Minv, P, fits, fsrc, rscale, tiles,
+                                                               g, frozen, Y, delta);
+    else
+        chol_inv_apply_kernel<false><<<grid, kCT, 0, s>>>(Minv, P, fits, fsrc, rscale, tiles, g,
+                                                           frozen, Y, delta);
     chol_inv_apply_kernel<true><<<grid, kCT, 0, s>>>(Minv, P, fits, fsrc, rscale, tiles, g,
                                                       frozen, Y, delta);
     return check_launch("chol_inv_apply_kernel");
