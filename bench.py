@@ -560,7 +560,8 @@ def main():
                       float(stats.gram_fits), stats.alg_flop, float(stats.reused),
                       float(stats.gram_fit_iters), float(stats.stops["stagnation"]),
                       float(stats.stops["line_search_failed"] + stats.stops["max_iter"]),
-                      float(stats.aliased), float(stats.newton_iters)],
+                      float(stats.aliased), float(stats.newton_iters), float(stats.shared),
+                  float(stats.roundtrips), stats.sync_wait_s],
                      dtype=torch.float64, device="cuda" if a.dist_backend == "nccl" else "cpu")
     if world > 1:
         mx = t.clone()
@@ -573,6 +574,7 @@ def main():
     gram_fits, alg_flop, reused, gram_iters = float(t[5]), float(t[6]), float(t[7]), float(t[8])
     stag, failed = int(t[9]), int(t[10])
     aliased, newton_iters = float(t[11]), float(t[12])
+    shared, roundtrips, sync_wait = float(t[13]), float(t[14]), float(t[15])
     if rank == 0:
         grid_s = elapsed / a.steps
         achieved = kflop / ktime / 1e12 if ktime > 0 else 0.0
@@ -598,7 +600,8 @@ def main():
             "higher_is_better": False,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "bf16 Hessian (w rounded to bf16, X exact 0/1) / exact-f32 gradient "
+                     "(3 bf16 pieces, f64 slab sums) / f64 coefficients and line search",
             "data": "synthetic",
             "config": {
                 "workload": f"Poisson CV grid {s.N}x{s.p} ({m} events x {len(s.shifts)} lags), "
@@ -610,6 +613,13 @@ def main():
                 "gram_forming_fit_iters_per_grid": gram_iters / a.steps,
                 "kept_factor_fit_iters_per_grid": reused / a.steps,
                 "aliased_fit_iters_per_grid": aliased / a.steps,
+                "lambda_shared_fit_iters_per_grid": shared / a.steps,
+                # host dependence of the number: round trips (stream synchronisations) per
+                # grid, and the host's own time per grid (wall minus the time it sat blocked
+                # in those synchronisations; summed over ranks when N > 1)
+                "host_roundtrips_per_grid": roundtrips / a.steps / max(world, 1),
+                "host_busy_ms_per_grid": (elapsed * (world if world > 1 else 1) - sync_wait)
+                                         / a.steps / max(world, 1) * 1e3,
                 "newton_iters_per_grid": newton_iters / a.steps,
                 "computed_grams_per_grid": gram_fits / a.steps,
                 "grid_roofline_frac": alg_flop / elapsed / (world * PEAK_BF16_TFLOPS * 1e12),

@@ -260,6 +260,14 @@ int sglm_chol_solve_inv(float* H, float* Minv, int32_t P, const int32_t* fits,
                         const float* dshift, float* delta, int32_t* info, uint8_t* frozen,
                         int32_t B, void* work, sglm_stream_t stream);
 
+/* The factor + inverse chain of sglm_chol_solve_inv is captured per argument set (device
+ * pointers, P, n, B) into a HIP graph and replayed.  The cache is a bounded LRU
+ * (SGLM_CHOL_GRAPH_CAP entries, default 32); an evicted executable is destroyed after its last
+ * replay completed.  _size reports the live entries; _clear destroys them all (call it before
+ * freeing buffers whose addresses a cached chain holds, if they may be reused later). */
+int32_t sglm_chol_graph_cache_size(void);
+int sglm_chol_graph_cache_clear(void);
+
 /* Solves on the stored factor of ANOTHER slot (engine.irls cross-mask Hessian sharing: a CV
  * split fit preconditioned by the full-data fit's Hessian at the same penalty, scaled by the
  * row-count ratio).  For i < nact: delta[fits[i]] = -rscale[i] * F^-1 F^-T g[fits[i]] with F the
@@ -272,9 +280,11 @@ int sglm_chol_solve_alias(const float* H, int32_t P, const int32_t* fits, const 
 /* Per-fit scalars of a Newton step for the B fits k = slots[q], float64 (one workgroup per
  * fit): out[q][0..5+T) = { g.d, sum lam w^2, sum lam w d, sum lam d^2, max|d|,
  * max|w + t[j] d| for j < T } over the P coordinates of g[k] (float64), beta[k] (float64),
- * delta[k] (f32), lamp[k] (float64 penalty row).  The Armijo test and the stopping rule of
- * sklearn's Newton solver (_newton_solver.py:201-260) need only these.  T <= 16. */
-int sglm_step_scalars(int32_t P, int32_t B, const int32_t* slots, const double* g,
+ * delta[k] (f32), lamp[k] (float64 penalty row); the max|w + t d| terms run over the first
+ * `ncoef` coordinates only (the coefficients without the intercept, the scale of the
+ * stopping rule; ncoef = P: all).  The Armijo test and the stopping rule of sklearn's Newton
+ * solver (_newton_solver.py:201-260) need only these.  T <= 16. */
+int sglm_step_scalars(int32_t P, int32_t ncoef, int32_t B, const int32_t* slots, const double* g,
                       const double* beta, const float* delta, const double* lamp,
                       const double* t, int32_t T, double* out, sglm_stream_t stream);
 /* beta[k] += step[q] * delta[k] for k = slots[q], q < B (float64 coefficients). */
@@ -404,7 +414,8 @@ int sglm_prep_session(const double* in, int64_t ld_in, int64_t n, int32_t k, dou
  * SGLM_MASK_ALL every row (idx unused), SGLM_MASK_FOLD a fold list (0/1 when strictly
  * increasing, else the multiplicity of each row; > 255 repeats is an error), SGLM_MASK_ROWS a
  * row list (1 on every listed row).  nnz[f] = rows with a nonzero mask, sum[f] = the summed
- * multiplicity (either may be NULL).  Rows outside [0, n) are an error. */
+ * multiplicity (either may be NULL).  An index in [-n, 0) names row idx + n (numpy fancy
+ * indexing, as X[idx_train] treats it); indices outside [-n, n) are an error. */
 enum { SGLM_MASK_ALL = 0, SGLM_MASK_FOLD = 1, SGLM_MASK_ROWS = 2 };
 int sglm_host_masks(int32_t nm, const int64_t* const* idx, const int64_t* len,
                     const int32_t* kind, int64_t n, int64_t ld, uint8_t* out, int64_t* nnz,

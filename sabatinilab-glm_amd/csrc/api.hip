@@ -526,7 +526,7 @@ __global__ void __launch_bounds__(256) mask_stats_reduce(const double* __restric
 // of the stopping rule after that step).  out[q][0..5+T).
 constexpr int kMaxStepT = 16;
 __global__ void __launch_bounds__(256) step_scalars_kernel(
-    int32_t P, const int32_t* __restrict__ slots, const double* __restrict__ g,
+    int32_t P, int32_t ncoef, const int32_t* __restrict__ slots, const double* __restrict__ g,
     const double* __restrict__ beta, const float* __restrict__ delta,
     const double* __restrict__ lamp, const double* __restrict__ t, int32_t T,
     double* __restrict__ out) {
@@ -547,7 +547,8 @@ __global__ void __launch_bounds__(256) step_scalars_kernel(
         s2 += l * b * d;
         s3 += l * d * d;
         md = fmax(md, fabs(d));
-        for (int j = 0; j < T; ++j) mb[j] = fmax(mb[j], fabs(b + tv[j] * d));
+        if (a < ncoef)
+            for (int j = 0; j < T; ++j) mb[j] = fmax(mb[j], fabs(b + tv[j] * d));
     }
     double* o = out + (int64_t)q * (5 + T);
     double v;
@@ -776,7 +777,7 @@ int sglm_eta_pair_absmax(int64_t n, int64_t ld, int32_t npairs, const int32_t* p
     return check_launch("eta_pair_absmax_kernel");
 }
 
-int sglm_step_scalars(int32_t P, int32_t B, const int32_t* slots, const double* g,
+int sglm_step_scalars(int32_t P, int32_t ncoef, int32_t B, const int32_t* slots, const double* g,
                       const double* beta, const float* delta, const double* lamp,
                       const double* t, int32_t T, double* out, sglm_stream_t stream) {
     if (B <= 0) return SGLM_OK;
@@ -784,8 +785,8 @@ int sglm_step_scalars(int32_t P, int32_t B, const int32_t* slots, const double* 
         set_error("sglm_step_scalars: bad args (T=%d, max %d)", T, kMaxStepT);
         return SGLM_EINVAL;
     }
-    step_scalars_kernel<<<(unsigned)B, 256, 0, as_stream(stream)>>>(P, slots, g, beta, delta,
-                                                                    lamp, t, T, out);
+    step_scalars_kernel<<<(unsigned)B, 256, 0, as_stream(stream)>>>(P, ncoef, slots, g, beta,
+                                                                    delta, lamp, t, T, out);
     return check_launch("step_scalars_kernel");
 }
 

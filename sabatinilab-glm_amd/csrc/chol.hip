@@ -1053,25 +1053,80 @@ static bool chol_graphs_enabled() {
     return on;
 }
 
+// Bounded LRU of instantiated chains.  Each entry keeps an event recorded after its latest
+// launch; an evicted (or cleared) executable is destroyed only after that event completed, so
+// a replay still in flight on any stream is never freed under it.  The reference's drivers
+// loop files x responses x runs (er_refactored_from_scratch_cleanup.py:261,388,393), and
+// every worker thread / reallocated buffer set is a new key: without a bound the cache would
+// grow by one ~110-node executable per key for the life of the process.
+namespace {
+struct ChainEntry {
+    hipGraphExec_t exec = nullptr;
+    hipEvent_t done = nullptr;
+    uint64_t used = 0;
+};
+std::mutex g_chain_mu;
+std::map<ChainKey, ChainEntry> g_chain_cache;
+uint64_t g_chain_tick = 0;
+
+int chain_cache_cap() {
+    static const int cap = [] {
+        const char* e = getenv("SGLM_CHOL_GRAPH_CAP");
+        const int v = e ? atoi(e) : 32;
+        return v > 0 ? v : 1;
+    }();
+    return cap;
+}
+
+void chain_entry_destroy(ChainEntry& e) {
+    if (e.done) {
+        (void)hipEventSynchronize(e.done);
+        (void)hipEventDestroy(e.done);
+    }
+    if (e.exec) (void)hipGraphExecDestroy(e.exec);
+    e.exec = nullptr;
+    e.done = nullptr;
+}
+
+// call with g_chain_mu held
+void chain_cache_evict_to(size_t keep) {
+    while (g_chain_cache.size() > keep) {
+        auto lru = g_chain_cache.begin();
+        for (auto it = g_chain_cache.begin(); it != g_chain_cache.end(); ++it)
+            if (it->second.used < lru->second.used) lru = it;
+        chain_entry_destroy(lru->second);
+        g_chain_cache.erase(lru);
+    }
+}
+}  // namespace
+
+extern "C" int32_t sglm_chol_graph_cache_size(void) {
+    std::lock_guard<std::mutex> lock(g_chain_mu);
+    return (int32_t)g_chain_cache.size();
+}
+
+extern "C" int sglm_chol_graph_cache_clear(void) {
+    std::lock_guard<std::mutex> lock(g_chain_mu);
+    chain_cache_evict_to(0);
+    return SGLM_OK;
+}
+
 static int factor_inv(float* H, float* Minv, int32_t P, const int32_t* fits, int32_t n,
                       const float* dshift, float* delta, int32_t* info, uint8_t* frozen,
                       int32_t B, void* work, hipStream_t s) {
     if (!chol_graphs_enabled() || s == nullptr)      // the null stream cannot be captured
         return factor_inv_launch(H, Minv, P, fits, n, dshift, delta, info, frozen, B, work, s);
-    static std::mutex mu;
-    static std::map<ChainKey, hipGraphExec_t> cache;
     ChainKey key;
     std::memset(&key, 0, sizeof(key));
     key.H = H; key.Minv = Minv; key.fits = fits; key.dshift = dshift; key.delta = delta;
     key.info = info; key.frozen = frozen; key.work = work;
     key.P = P; key.n = n; key.B = B; key.la = chol_lookahead();
-    hipGraphExec_t exec = nullptr;
-    {
-        std::lock_guard<std::mutex> lock(mu);
-        auto it = cache.find(key);
-        if (it != cache.end()) exec = it->second;
-    }
-    if (!exec) {
+    // the lock is held across capture and launch: a concurrent eviction must not destroy the
+    // entry between lookup and launch (captures are thread-local, so nothing else is stalled
+    // but other chains' host enqueue, which is short next to the chain itself)
+    std::lock_guard<std::mutex> lock(g_chain_mu);
+    auto it = g_chain_cache.find(key);
+    if (it == g_chain_cache.end()) {
         hipGraph_t graph = nullptr;
         if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) {
             set_error("chol graph: hipStreamBeginCapture failed");
@@ -1088,17 +1143,28 @@ static int factor_inv(float* H, float* Minv, int32_t P, const int32_t* fits, int
             set_error("chol graph: hipStreamEndCapture failed");
             return SGLM_EHIP;
         }
-        const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+        ChainEntry e;
+        const hipError_t ei = hipGraphInstantiate(&e.exec, graph, nullptr, nullptr, 0);
         (void)hipGraphDestroy(graph);
         if (ei != hipSuccess) {
             set_error("chol graph: hipGraphInstantiate failed");
             return SGLM_EHIP;
         }
-        std::lock_guard<std::mutex> lock(mu);
-        cache[key] = exec;
+        if (hipEventCreateWithFlags(&e.done, hipEventDisableTiming) != hipSuccess) {
+            (void)hipGraphExecDestroy(e.exec);
+            set_error("chol graph: hipEventCreate failed");
+            return SGLM_EHIP;
+        }
+        chain_cache_evict_to((size_t)chain_cache_cap() - 1);
+        it = g_chain_cache.emplace(key, e).first;
     }
-    if (hipGraphLaunch(exec, s) != hipSuccess) {
+    it->second.used = ++g_chain_tick;
+    if (hipGraphLaunch(it->second.exec, s) != hipSuccess) {
         set_error("chol graph: hipGraphLaunch failed");
+        return SGLM_EHIP;
+    }
+    if (hipEventRecord(it->second.done, s) != hipSuccess) {
+        set_error("chol graph: hipEventRecord failed");
         return SGLM_EHIP;
     }
     return SGLM_OK;

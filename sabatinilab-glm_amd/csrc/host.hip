@@ -38,18 +38,21 @@ void build_mask(MaskJob& j) {
     std::memset(m, 0, (size_t)n);
     const int64_t* idx = j.idx;
     const int64_t L = j.len;
+    // numpy fancy-indexing semantics (X[idx_train], backend/sglm_cv.py:107-110): an index in
+    // [-n, 0) names row idx + n
+    auto row = [n](int64_t v) { return v < 0 ? v + n : v; };
     // one pass: every index in range, and whether the list is strictly increasing
     bool bad = false, increasing = true;
     int64_t prev = -1;
     for (int64_t t = 0; t < L; ++t) {
-        const int64_t v = idx[t];
+        const int64_t v = row(idx[t]);
         bad |= (uint64_t)v >= (uint64_t)n;
         increasing &= v > prev;
         prev = v;
     }
     if (bad) { j.err = 1; return; }
     if (j.kind == SGLM_MASK_ROWS || increasing) {
-        for (int64_t t = 0; t < L; ++t) m[idx[t]] = 1;
+        for (int64_t t = 0; t < L; ++t) m[row(idx[t])] = 1;
         if (increasing) {
             j.nnz = L;
             j.sum = (double)L;
@@ -63,8 +66,9 @@ void build_mask(MaskJob& j) {
     }
     // multiplicities (repeats)
     for (int64_t t = 0; t < L; ++t) {
-        if (m[idx[t]] == 255) { j.err = 2; return; }
-        ++m[idx[t]];
+        const int64_t r = row(idx[t]);
+        if (m[r] == 255) { j.err = 2; return; }
+        ++m[r];
     }
     int64_t c = 0;
     for (int64_t i = 0; i < n; ++i) c += m[i] != 0;
@@ -114,7 +118,8 @@ extern "C" int sglm_host_masks(int32_t nm, const int64_t* const* idx, const int6
     for (int32_t f = 0; f < nm; ++f) {
         const MaskJob& j = jobs[(size_t)f];
         if (j.err == 1) {
-            set_error("sglm_host_masks: mask %d lists a row outside [0, %lld)", f, (long long)n);
+            set_error("sglm_host_masks: mask %d lists a row outside [-%lld, %lld)", f,
+                      (long long)n, (long long)n);
             return SGLM_EINVAL;
         }
         if (j.err == 2) {

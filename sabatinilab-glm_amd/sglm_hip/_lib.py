@@ -58,9 +58,11 @@ SIGNATURES = {
                                       _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
     "sglm_chol_solve_mixed": (C.c_int, [_vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32,
                                         _vp, _vp]),
+    "sglm_chol_graph_cache_size": (_i32, []),
+    "sglm_chol_graph_cache_clear": (C.c_int, []),
     "sglm_chol_solve_alias": (C.c_int, [_vp, _i32, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _i32, _vp,
                                         _vp]),
-    "sglm_step_scalars": (C.c_int, [_i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
+    "sglm_step_scalars": (C.c_int, [_i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
     "sglm_step_update": (C.c_int, [_i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     "sglm_mask_stats_work_bytes": (_sz, [_i32, _i32, _i64]),
     "sglm_mask_stats": (C.c_int, [_vp, _i64, _i32, _vp, _i32, _i64, _vp, C.c_double, _vp, _vp,

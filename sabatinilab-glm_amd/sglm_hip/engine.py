@@ -46,6 +46,8 @@ X_BF16, X_F32 = 0, 1
 COL_PAD = 256
 ROW_PAD = 256
 ARMIJO_SIGMA = 2.0 ** -11      # sklearn _newton_solver.py:214
+# stopping rule: max|t d| <= tol * max(max_j<p |w_j|, STOP_SCALE_FLOOR) (tol = 1e-6)
+STOP_SCALE_FLOOR = 1e-2
 # second round of line-search step lengths (the first: 1, 1/2, 1/4, 1/8)
 TV2 = np.array([0.0625, 0.03125, 0.015625, 0.0078125, 2.0 ** -10, 2.0 ** -14, 2.0 ** -20])
 XTR_BITS = True                # X^T R on the MFMA from compacted bit-planes for 0/1 designs
@@ -581,7 +583,10 @@ class IrlsStats:
     gram_fit_iters: int = 0     # fit-iterations whose own Gram was computed (Gram-forming)
     reused: int = 0                                     # fit-iterations that kept a factor
     aliased: int = 0            # fit-iterations solved on a family representative's factor
+    shared: int = 0             # fit-iterations on a lambda neighbour's Gram (own factor)
     alg_flop: float = 0.0       # SURVEY.md §8(d) F summed over fit-iterations
+    sync_wait_s: float = 0.0    # host time blocked in the per-iteration stream synchronisation
+    roundtrips: int = 0         # host<->device round trips (stream synchronisations) of the solve
     trace_phases: bool = False                          # sync + time grid phases (tools)
     phases: dict = field(default_factory=dict)          # host wall seconds per phase
     # why fits stopped (converged fits: tol + line_search_converged)
@@ -864,6 +869,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
     fresh_start = np.array([r.coef0 is None for r in reqs])
     lamp_d = torch.from_numpy(lam[:, None] * penal).to(dev)        # lam * penalty mask
     gram_now = np.zeros(B0, dtype=bool)
+    exact_h = np.zeros(B0, dtype=bool)     # Hessian = the fit's own Gram at its own predictor
     active = np.ones(B0, dtype=bool)
     n_iter = np.zeros(B0, dtype=np.int64)
     converged = np.zeros(B0, dtype=bool)
@@ -900,10 +906,18 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                         repl[k] = rk
     alias = np.full(B0, -1, dtype=np.int64)     # slot whose factor the fit used this iteration
     no_alias = np.zeros(B0, dtype=bool)
+    no_share = np.zeros(B0, dtype=bool)     # failed a step on a lambda neighbour's Hessian
 
     up = _Uploads(dev)
     bf.up = up
     pd_h = _pinned("pairdist", 4 * B0, torch.float32)
+
+    def hkey(k):
+        """Fits with equal keys have bitwise equal Hessians: one (mask, response) at the
+        common start -- which depends on the intercept setting (log(mean y) or 0) -- or the
+        fit itself once it has moved."""
+        return ((reqs[k].mask, reqs[k].resp, -1, bool(reqs[k].fit_intercept)) if fresh_start[k]
+                else (reqs[k].mask, reqs[k].resp, int(k)))
 
     def hess_plan(act):
         """Hessian decisions of the next iteration that need no device data, and one launch of
@@ -919,7 +933,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         form = rest[drift[rest] > reuse_tol]
         reps, dup = {}, []
         for k in form:
-            rk = reps.setdefault((reqs[k].mask, reqs[k].resp, -1 if fresh_start[k] else k), k)
+            rk = reps.setdefault(hkey(k), k)
             if rk != k:
                 dup.append((k, rk))
         uniq = np.array(sorted(reps.values()), dtype=np.int32)
@@ -927,7 +941,8 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         if share_tol > 0.0 and uniq.size > 1:
             groups = {}
             for k in uniq:
-                groups.setdefault((reqs[k].mask, reqs[k].resp), []).append(int(k))
+                if not no_share[k]:
+                    groups.setdefault((reqs[k].mask, reqs[k].resp), []).append(int(k))
             chains = [sorted(g, key=lambda k: lam[k]) for g in groups.values() if len(g) > 1]
         pairs = [(int(k), int(repl[k])) for k in cand]
         pairs += [(c[i], c[i + 1]) for c in chains for i in range(len(c) - 1)]
@@ -946,7 +961,12 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
     def hess_finish(pl):
         """Apply the distances of a plan: lambda-neighbour sharing, then aliasing of the
         candidates whose distance to the representative plus the representative's own drift
-        after this iteration's decision stays <= xmask_tol (the others form their own)."""
+        after this iteration's decision stays <= xmask_tol (the others form their own).
+        Every Hessian copy is resolved to a Hessian this iteration actually computes (a copy
+        of a fit that itself shares along the lambda chain follows the chain), and the copy's
+        drift is the summed distance along that path.  Returns (keep, form, uniq, copies,
+        aliased, failed candidates, exact): ``exact`` flags the fits whose Hessian is their
+        own Gram at their own predictor (computed, or an exact duplicate of one)."""
         if pl["ev"] is not None:
             pl["ev"].synchronize()
         dist = pd_h[:pl["npairs"]].numpy().astype(np.float64)
@@ -954,21 +974,28 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                                                              "dup", "uniq"))
         dist_c, dist_s = dist[:cand.size], dist[cand.size:]
         drift[form] = 0.0
+        src = {int(k): (int(rk), 0.0) for k, rk in dup}     # fit -> (source fit, distance)
         if pl["chains"]:
             uniq, shared = _share_chains(uniq, pl["chains"], dist_s, share_tol)
             for k, rk, dist_k in shared:
-                dup.append((k, rk))
-                drift[k] = dist_k
+                src[int(k)] = (int(rk), float(dist_k))
         ok = dist_c + drift[repl[cand]] <= xmask_tol
         ali, fail = cand[ok], cand[~ok]
         for k in fail:
-            rk = reps.setdefault((reqs[k].mask, reqs[k].resp, -1 if fresh_start[k] else k), k)
+            rk = reps.setdefault(hkey(k), k)
             if rk != k:
-                dup.append((k, rk))
+                src[int(k)] = (int(rk), 0.0)
             else:
                 uniq = np.append(uniq, np.int32(k))
         drift[fail] = 0.0
-        return keep, np.concatenate([form, fail]), uniq, dup, ali, fail
+        copies = _resolve_copies(src, uniq)
+        for k, _, dk in copies:
+            drift[k] = dk
+        copies = [(k, r) for k, r, _ in copies]
+        newh = np.concatenate([form, fail])
+        exact = np.zeros(B0, dtype=bool)
+        exact[newh] = drift[newh] == 0.0
+        return keep, newh, uniq, copies, ali, fail, exact
     use_rp = d.xbits is not None and XTR_BITS      # R packed into the MFMA gradient operand
     if use_rp:
         rp_buf = _work(3 * pad_to(B0, 32) * ld * 2, dev, "rp")
@@ -1027,7 +1054,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
             # long computed): keep / form / share / alias (see _hess_plan)
             if plan is None:
                 plan = hess_plan(act)
-            keep, form, uniq, dup, ali, fail = hess_finish(plan)
+            keep, form, uniq, dup, ali, fail, exact_h = hess_finish(plan)
             plan = None
             alias[:] = -1
             alias[ali] = repl[ali]
@@ -1041,6 +1068,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                 stats.gram_fits += int(uniq.size)
                 stats.reused += int(keep.size)
                 stats.aliased += int(ali.size)
+                stats.shared += int(np.sum(~exact_h[form]))
         t0 = tick("it_gram", t0)
         bf.delta[:B].zero_()
         if const_hess:
@@ -1118,7 +1146,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         # over the coefficients (no B x P array crosses to the host): g.d, the penalty terms
         # lam|w|^2, 2 lam w.d, lam|d|^2, max|d| and max|w + t d| for every trial step t
         sc = sc_d[: na * (5 + nts)]
-        _lib.call("sglm_step_scalars", P, na, _p(act_d), _p(bf.gtot), _p(beta64_d), _p(bf.delta),
+        _lib.call("sglm_step_scalars", P, p, na, _p(act_d), _p(bf.gtot), _p(beta64_d), _p(bf.delta),
                   _p(lamp_d), _p(ts_all), nts, _p(sc), st)
         t0 = tick("it_solve_eta", t0)
         # ---- line search (rows of L, dmax and sc: active fits in slot order)
@@ -1129,7 +1157,11 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         dmax_h[:na].copy_(dmax_d[:na], non_blocking=True)
         sc_h = _pinned("sc", sc.numel(), torch.float64)
         sc_h.copy_(sc, non_blocking=True)
+        t_sync = time.perf_counter()
         torch.cuda.current_stream().synchronize()              # the iteration's round trip
+        if stats is not None:
+            stats.sync_wait_s += time.perf_counter() - t_sync
+            stats.roundtrips += 1
         up.synced()
         L = L_h[: na * 5].numpy().reshape(na, 5).copy()
         dmaxeta = dmax_h[:na].numpy().astype(np.float64)
@@ -1156,7 +1188,11 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
             _lib.call("sglm_loss_trials", fam, power, n, ld, int(more.size), _p(sub_d),
                       _p(bf.eta), _p(bf.deta), _p(prob.Y), _p(prob.M), _p(fit_resp),
                       _p(fit_mask), _p(tv2), 7, _p(Ltr), _p(xtr_work), st)
+            t_sync = time.perf_counter()
             L2 = Ltr[: more.size * 7].view(more.size, 7).cpu().numpy()
+            if stats is not None:
+                stats.sync_wait_s += time.perf_counter() - t_sync
+                stats.roundtrips += 1
             ts2 = TV2.astype(np.float32).astype(np.float64)
             obj0 = objectives(L[:, :1], np.zeros(1))[more]
             o2 = L2 + 0.5 * (A_[more, None] + 2 * ts2[None, :] * B_[more, None]
@@ -1187,16 +1223,22 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
                                            + np.where(gram_now[act], pa ** 3 / 3, 0.0)
                                            + 4.0 * nr * pa + 2 * pa * pa))
             stats.gram_fit_iters += int(np.sum(gram_comp[act]))
-        scale = 1.0 + maxb[np.arange(na), tix]         # 1 + max|w| after the step
+        # the step is measured against the coefficients' own scale (max|w_j| over j < p after
+        # the step, the intercept excluded), floored at STOP_SCALE_FLOOR: the parity tests
+        # measure errors relative to max|coef|, so a fit with small coefficients (strong
+        # penalty) must converge in those units too
+        scale = np.maximum(maxb[np.arange(na), tix], STOP_SCALE_FLOOR)
         relv = step_a * maxd / scale
         prop = maxd / scale                            # the proposed Newton step
         stepa = step_a
-        fresh = gram_now[act] | const_hess
+        fresh = (gram_now[act] & exact_h[act]) | const_hess
         ls_fail = stepa == 0.0
-        # a failed line search on a kept (stale) factor is not a verdict: the next iteration
-        # forms a fresh Hessian for that fit instead of stopping it
+        # a failed line search on a kept (stale) factor, or on a Hessian shared from a lambda
+        # neighbour, is not a verdict: the next iteration forms a fresh Hessian of the fit's
+        # own instead of stopping it
         if not const_hess:
             drift[act[ls_fail & ~fresh]] = np.inf
+            no_share[act[ls_fail & gram_now[act] & ~exact_h[act]]] = True
             # a fit whose step on the representative's factor failed, or contracted slowly,
             # forms its own Hessians from here on
             was_alias = alias[act] >= 0
@@ -1403,6 +1445,9 @@ def irls_scored(prob: Problem, reqs: List[FitReq], sets: np.ndarray,
             stats.gram_fit_iters += sg.gram_fit_iters
             stats.reused += sg.reused
             stats.aliased += sg.aliased
+            stats.shared += sg.shared
+            stats.sync_wait_s += sg.sync_wait_s
+            stats.roundtrips += sg.roundtrips
             stats.alg_flop += sg.alg_flop
             for k, v in sg.stops.items():
                 stats.stops[k] += v
@@ -1428,6 +1473,27 @@ def _pair_dist_async(bf, prob, pairs, n, ld, st):
     out = torch.empty(pairs.size // 2, dtype=torch.float32, device=dev)
     _lib.call("sglm_eta_pair_absmax", n, ld, pairs.size // 2, _p(pd_), _p(prob.M), _p(fm),
               _p(bf.eta), _p(out), st)
+    return out
+
+
+def _resolve_copies(src, formed):
+    """Hessian copies of one iteration, each resolved to a Hessian that is actually computed.
+    ``src``: fit -> (source fit, distance) -- exact duplicates (distance 0), lambda-chain shares
+    and failed alias candidates; a source may itself be a copy (e.g. an exact duplicate of a
+    fit that was then shared along its lambda chain).  ``formed``: the fits whose Gram is
+    computed.  Returns [(fit, formed source, summed distance)], so every copy reads a
+    Hessian written this iteration, whatever order the copies run in."""
+    formed = set(int(u) for u in formed)
+    out = []
+    for k in src:
+        r, dk, hops = int(k), 0.0, 0
+        while r not in formed:
+            if r not in src or hops > len(src):
+                raise RuntimeError(f"Hessian copy of fit {k} does not reach a formed Hessian")
+            r, dd = src[r]
+            dk += dd
+            hops += 1
+        out.append((int(k), r, dk))
     return out
 
 

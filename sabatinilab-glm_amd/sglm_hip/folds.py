@@ -93,10 +93,21 @@ def trial_keys_codes(df, id_cols, package_style=False):
     return bucket.astype("category").cat.codes
 
 
+def wrap_indices(idx, n):
+    """int64 row indices with negative entries in [-n, 0) wrapped by + n, as the reference's
+    numpy fancy indexing ``X[idx_train]`` (backend/sglm_cv.py:107-110) treats them; anything
+    outside [-n, n) raises IndexError like numpy does."""
+    idx = np.asarray(idx, dtype=np.int64).reshape(-1)
+    if idx.size and (idx.min() < -n or idx.max() >= n):
+        bad = idx[(idx < -n) | (idx >= n)][0]
+        raise IndexError(f"index {bad} is out of bounds for axis 0 with size {n}")
+    return np.where(idx < 0, idx + n, idx)
+
+
 def mask_from_idx(idx, n):
     """Multiplicity mask (uint8, length n) of one index list: 0/1 for strictly increasing
     indices, counts for repeats (holdout resampling)."""
-    idx = np.asarray(idx, dtype=np.int64).reshape(-1)
+    idx = wrap_indices(idx, n)
     if idx.size and (idx[0] < 0 or idx[-1] >= n or not np.all(idx[1:] > idx[:-1])):
         m = np.bincount(idx, minlength=n)[:n]              # repeats (holdout resampling)
         if m.max(initial=0) > 255:

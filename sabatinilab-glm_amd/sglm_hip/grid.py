@@ -408,7 +408,7 @@ def _mask_array(idx, multiplicity, n):
     if multiplicity:
         return F.mask_from_idx(idx, n)
     m = np.zeros(n, np.uint8)
-    m[np.asarray(idx, dtype=np.int64).reshape(-1)] = 1
+    m[F.wrap_indices(idx, n)] = 1
     return m
 
 
@@ -416,7 +416,7 @@ def _mask_count(idx, multiplicity, n):
     """Row count of a spec (sum of multiplicities) without building the mask."""
     if idx is None:
         return float(n)
-    idx = np.asarray(idx).reshape(-1)
+    idx = F.wrap_indices(idx, n)
     return float(idx.size if multiplicity else np.unique(idx).size)
 
 

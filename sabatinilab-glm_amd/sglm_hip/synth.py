@@ -157,3 +157,84 @@ def signal_session(n_trials: int, seed: int, *, short_gap=0.3, missed_co=0.05,
     sig = pd.DataFrame({f"Ch{c + 1}": rng.standard_normal(n_sig) for c in range(channels)})
     sig["timestamp"] = np.arange(n_sig) / 20.0
     return sig, table
+
+
+def designmat_session(n_trials: int, seed: int, *, lead=7, no_cue=0.03, timeout=0.08,
+                      missing_trials=2, enlp_rate=0.25, lick_rate=0.06, cons_lick_rate=0.5,
+                      nan_clock=0.01, photo=("z_grnR", "z_grnL")):
+    """(timeseries, trials) in the layout pp_design_mat.make_design_mat reads, 50 Hz rows.
+
+    Per trial, in order: Cue (4 rows), ENL (8-40 rows; with probability ``enlp_rate`` a
+    penalised ENL repeated 1-3 times: ENLP / state_ENLP rows, nENL counting the ENL periods of
+    the trial), Select (5-30 rows), Consumption (10-60 rows, stateConsumption spanning Select
+    and Consumption), an ITI (5-20 rows).  iSpout is a spout id on lick rows (denser in
+    Consumption), NaN elsewhere; trial_clock is ms since the trial start (a few NaN).  ``lead``
+    rows before the first trial have NaN nTrial / nENL.  A fraction of trials lacks its cue
+    rows (``no_cue``; flagged by make_design_mat), timeouts carry NaN Reward and tSelection,
+    and the last ``missing_trials`` trial ids of the session are absent from the trial table
+    (unmapped keys).  Vectorised: sizes of millions of rows are cheap."""
+    import pandas as pd
+    rng = np.random.default_rng(seed)
+    T = int(n_trials)
+    L_cue = np.where(rng.random(T) < no_cue, 0, 4)
+    L_enl = rng.integers(8, 41, T)
+    n_enlp = np.where(rng.random(T) < enlp_rate, rng.integers(1, 4, T), 0)
+    L_enlp = n_enlp * rng.integers(6, 15, T)
+    L_sel = rng.integers(5, 31, T)
+    L_con = rng.integers(10, 61, T)
+    L_iti = rng.integers(5, 21, T)
+    phases = np.stack([L_cue, L_enl, L_enlp, L_sel, L_con, L_iti], 1)    # T x 6 row counts
+    per_trial = phases.sum(1)
+    n = int(lead + per_trial.sum())
+    trial_of_row = np.repeat(np.arange(T), per_trial)
+    start = np.r_[0, np.cumsum(per_trial)[:-1]]
+    pos = np.arange(n - lead) - np.repeat(start, per_trial)              # row within trial
+    bounds = np.cumsum(phases, 1)
+    b = bounds[trial_of_row]
+    phase = (pos[:, None] >= b).sum(1)                                    # 0..5
+    z = np.zeros(n)
+
+    def col(mask):
+        c = z.copy()
+        c[lead:] = mask.astype(np.float64)
+        return c
+    ts = {}
+    nt = np.full(n, np.nan)
+    nt[lead:] = trial_of_row + 1.0
+    ts["nTrial"] = nt
+    blk = np.full(n, np.nan)
+    blk[lead:] = (trial_of_row // 40).astype(np.float64)
+    ts["iBlock"] = blk
+    ts["Cue"] = col(phase == 0)
+    ts["ENL"] = col(phase == 1)
+    ts["ENLP"] = col(phase == 2)
+    ts["state_ENLP"] = col(phase == 2)
+    ts["Select"] = col(phase == 3)
+    ts["Consumption"] = col(phase == 4)
+    ts["stateConsumption"] = col((phase == 3) | (phase == 4))
+    # nENL: 1 in the first ENL, then one more per penalised repeat (equal-length chunks)
+    chunk = np.maximum(L_enlp // np.maximum(n_enlp, 1), 1)[trial_of_row]
+    rep = np.where(phase == 2, (pos - bounds[trial_of_row, 1]) // chunk + 2, 1)
+    ne = np.full(n, np.nan)
+    ne[lead:] = np.where(phase >= 3, 1 + n_enlp[trial_of_row], rep).astype(np.float64)
+    ts["nENL"] = ne
+    clock = np.full(n, np.nan)
+    clock[lead:] = pos * 20.0
+    clock[rng.random(n) < nan_clock] = np.nan
+    ts["trial_clock"] = clock
+    lick_p = np.full(n, lick_rate)
+    lick_p[lead:][phase == 4] = cons_lick_rate
+    sp = np.where(rng.random(n) < lick_p, rng.integers(1, 3, n).astype(np.float64), np.nan)
+    ts["iSpout"] = sp
+    for p in photo:
+        ts[p] = rng.standard_normal(n)
+    timeseries = pd.DataFrame(ts)
+    tsel = (L_cue + L_enl + L_enlp) * 20.0 + rng.integers(0, 200, T)
+    to = rng.random(T) < timeout
+    reward = np.where(to, np.nan, (rng.random(T) < 0.6).astype(np.float64))
+    tsel = np.where(to, np.nan, tsel)
+    h2 = rng.integers(0, 2, T).astype(np.float64)
+    keep = T - int(missing_trials)
+    trials = pd.DataFrame({"nTrial": np.arange(1, T + 1)[:keep], "tSelection": tsel[:keep],
+                           "Reward": reward[:keep], "h2": h2[:keep]})
+    return timeseries, trials

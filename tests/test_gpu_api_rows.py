@@ -15,6 +15,7 @@ import queue
 import threading
 
 import numpy as np
+import pandas as pd
 import pytest
 
 from oracle import cv_ref, glm_ref
@@ -164,3 +165,90 @@ def test_sglm_worker_threads_drain_fit_set_queue(engine, golden):
     t.start()
     t.join(timeout=60)
     assert not t.is_alive() and len(resp) == 2
+
+
+def test_poisson_grid_mixing_fit_intercept_vs_oracle(engine):
+    """The reference's own parameter grids vary 'fit_intercept' (backend/sglm.py:512); fits of
+    one fold that start at eta = log(mean y) and at eta = 0 are solved in ONE batch and must
+    not share a first Hessian.  Every fold fit, refit and score vs the oracle."""
+    import sglm_cv
+    import sglm_ez
+    from oracle import cv_ref
+    from sglm_hip import synth
+    s = synth.make(N=30_000, m=10, L=6, family="poisson", rho=0.05, seed=4, beta_scale=0.3)
+    X = s.dense_X()
+    np.random.seed(7)
+    cv_idx = sglm_ez.cv_idx_by_trial_id(pd.DataFrame({"nTrial": s.trial}),
+                                       trial_id_columns=["nTrial"], num_folds=3)
+    kws = sglm_cv.generate_mult_params({"alpha": [1e-3, 1e-1], "fit_intercept": [True, False]},
+                                       {"model_name": "Poisson"})
+    ref = cv_ref.cv_mult(X, s.y, cv_idx, [dict(k) for k in kws])
+    out = sglm_cv.cv_glm_mult_params(X, s.y, cv_idx, "Normal", kws)
+    for r, q in zip(out["full_cv_results"], ref["full_cv_results"]):
+        assert rel(r["cv_coefs"], q["cv_coefs"]) < 1e-4, r["glm_kwargs"]
+        assert np.max(np.abs(r["cv_intercepts"] - q["cv_intercepts"])) < 1e-4
+        assert rel(r["model"].coef_, q["coef"]) < 1e-4
+        assert np.max(np.abs(r["cv_scores_test"] - q["cv_scores_test"])) < 1e-6
+        if not r["glm_kwargs"].get("fit_intercept", True):
+            assert np.all(r["cv_intercepts"] == 0.0)
+
+
+def test_chain_graph_cache_is_bounded_and_survives_freed_buffers(engine):
+    """The factor + inverse chain graphs (csrc/chol.hip) are an LRU of at most
+    SGLM_CHOL_GRAPH_CAP (32) executables: two differently sized designs fitted back to back, the
+    first one's buffers freed, 40 distinct chain shapes -- the cache never exceeds the bound, a
+    clear empties it, and fits after it still match the oracle."""
+    import gc
+    import torch
+    import sglm
+    from sglm_hip import _lib, synth
+    lib = _lib.load()
+    lib.sglm_chol_graph_cache_clear()
+    assert lib.sglm_chol_graph_cache_size() == 0
+    fits = []
+    for N, m, L in ((20_000, 8, 5), (12_000, 5, 7)):
+        s = synth.make(N=N, m=m, L=L, family="poisson", rho=0.05, seed=N, beta_scale=0.3)
+        X = s.dense_X()
+        glm = sglm.GLM("Poisson", alpha=0.01)
+        glm.fit(X, s.y)
+        c, b = glm_ref.fit_tweedie_newton(X, s.y, 0.01, 1.0)
+        assert rel(glm.coef_, c) < TOL_POIS
+        fits.append((X, s.y))
+        del glm
+        gc.collect()
+        torch.cuda.empty_cache()
+    assert 1 <= lib.sglm_chol_graph_cache_size() <= 32
+    # 40 distinct chain shapes (n factored fits) through the C ABI on one stream
+    P, B = 64, 40
+    rng = np.random.default_rng(0)
+    A = rng.normal(size=(B, 200, P))
+    H = torch.from_numpy(np.einsum("bij,bik->bjk", A, A).astype(np.float32)).cuda()
+    Minv = torch.empty_like(H)
+    dsh = torch.zeros((B, P), dtype=torch.float32, device="cuda")
+    delta = torch.zeros((B, P), dtype=torch.float32, device="cuda")
+    info = torch.zeros(B, dtype=torch.int32, device="cuda")
+    frozen = torch.zeros((B, P), dtype=torch.uint8, device="cuda")
+    fl = torch.arange(B, dtype=torch.int32, device="cuda")
+    cw = torch.empty(_lib.query("sglm_chol_work_bytes", P, B), dtype=torch.uint8, device="cuda")
+    s_ = torch.cuda.Stream()
+    with torch.cuda.stream(s_):
+        for n in range(1, B + 1):
+            Hn = H.clone()
+            _lib.call("sglm_chol_solve_inv", Hn.data_ptr(), Minv.data_ptr(), P, fl.data_ptr(),
+                      None, None, n, n, None, 0, None, dsh.data_ptr(), delta.data_ptr(),
+                      info.data_ptr(), frozen.data_ptr(), B, cw.data_ptr(), s_.cuda_stream)
+            assert lib.sglm_chol_graph_cache_size() <= 32
+    s_.synchronize()
+    # the inverse of the last chain (all 40 fits) is right: U^-1 U^-T = H^-1
+    M = Minv.double().cpu().numpy()
+    Hh = H.double().cpu().numpy()
+    for k in (0, 39):
+        U = np.triu(M[k])
+        assert np.max(np.abs(U @ U.T @ Hh[k] - np.eye(P))) < 1e-3
+    assert lib.sglm_chol_graph_cache_clear() == 0
+    assert lib.sglm_chol_graph_cache_size() == 0
+    X, y = fits[0]
+    glm = sglm.GLM("Poisson", alpha=0.01)
+    glm.fit(X, y)
+    c, b = glm_ref.fit_tweedie_newton(X, y, 0.01, 1.0)
+    assert rel(glm.coef_, c) < TOL_POIS

@@ -1,18 +1,25 @@
 """Full-size parity at the BASELINE.json configs the bench runs (C4) and the C5 path at p=2000.
 
-C4 (configs[3]): Poisson/log, 1,000,000 rows x 2000 time-shifted 0/1 predictors (P = 2048),
-trial-id GroupShuffleSplit splits (seed 3), through ``grid.run`` exactly as bench.py calls it
-(bf16 bit-plane Gram, Hessian reuse/sharing at the default tolerances, two IRLS groups), at
-lambda in {1e-4, 1.0} x 5 splits + 2 refits = 12 fits.  Checks:
+C4 (configs[3]) -- EXACTLY the timed bench configuration: Poisson/log, 1,000,000 rows x 2000
+time-shifted 0/1 predictors (P = 2048), trial-id GroupShuffleSplit splits (seed 3), the 20
+lambdas np.logspace(-4, 1, 20) x (5 splits + refit) = 120 fits, through ``grid.run`` as
+bench.py calls it (bf16 bit-plane Gram, Hessian reuse, lambda-neighbour sharing and
+cross-mask aliasing at the default tolerances).  The reference's loop is
+cv_glm_single_params per lambda (backend/sglm_cv.py:42-206) with sklearn
+TweedieRegressor(power=1) (backend/sglm.py:112-115).  Checks:
 
-* every fit converged on the step criterion (no stagnation / line-search-failure stops);
+* every fit converged on the step criterion (no stagnation / line-search-failure stops), and
+  the grid actually exercised the lambda-neighbour sharing chain and cross-mask aliasing;
 * every fit's float64 Newton distance |H^-1 g|_inf to the minimiser, with g and H formed in
   float64 from the exact design on the device (torch float64, the property checker, not the
-  product), is <= 1e-5 of max|beta| -- ten times inside the north-star Poisson bar (1e-4);
-* one split fit and the refit at lambda = 1e-4 (the ill-conditioned end of the path) against
-  the float64 CPU oracle (oracle/glm_ref.fit_tweedie_newton, damped Newton to 1e-10) at 1e-4
-  relative -- the reference's estimator is sklearn TweedieRegressor(power=1)
-  (backend/sglm.py:112-115) inside cv_glm_single_params (backend/sglm_cv.py:42-206).
+  product), is <= 1e-5 of max|beta| -- ten times inside the north-star Poisson bar (1e-4) --
+  for ALL 120 fits;
+* against the float64 CPU oracle (oracle/glm_ref.fit_tweedie_newton, damped Newton to 1e-10)
+  at 1e-4 relative: split 0 and the refit at lambda index 0 (the ill-conditioned end), and the
+  split-0 fits at lambda index 5 and 12 (mid-path, where the sharing chain hands Hessians from
+  neighbour to neighbour);
+* the grid cut into 8 rank shares (grid.run(..., simulate=(r, 8)): each share solved as a rank
+  of an 8-GPU run solves it) merges to the unsharded grid at 1e-5.
 
 C5 (configs[4] path): Gaussian elastic net l1_ratio 0.5 through ``enet.cv_enet_path`` at
 p = 2000 (200k rows, 3 responses x 3 alphas x (5 splits + refit)), so the coordinate-descent
@@ -29,7 +36,7 @@ from oracle import glm_ref
 
 pytestmark = pytest.mark.gpu
 TOL_POIS, TOL_GAUSS = 1e-4, 1e-5
-LAMS_C4 = (1e-4, 1.0)
+LAMS_C4 = tuple(float(a) for a in np.logspace(-4, 1, 20))     # bench.py's grid
 
 
 def rel(a, b):
@@ -59,10 +66,14 @@ def _device_augmented(s, torch):
     return Xd
 
 
+def _objectives(E):
+    from sglm_hip.estimators import Objective
+    return [Objective("irls", E.FAM_TWEEDIE_LOG, 1.0, a, "n", True, 100) for a in LAMS_C4]
+
+
 @pytest.fixture(scope="module")
 def c4(engine):
     from sglm_hip import engine as E, folds, grid, synth
-    from sglm_hip.estimators import Objective
     t0 = time.time()
     s = synth.make(N=1_000_000, m=50, L=20, family="poisson", rho=0.02, seed=0)
     d = E.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
@@ -70,53 +81,61 @@ def c4(engine):
     codes = folds.trial_keys_codes(pd.DataFrame({"nTrial": s.trial}), ["nTrial"]).values
     np.random.seed(3)
     cv_idx = folds.cv_idx_from_bucket_ids(codes, num_folds=5)
-    objs = [Objective("irls", E.FAM_TWEEDIE_LOG, 1.0, a, "n", True, 100) for a in LAMS_C4]
     st = E.IrlsStats()
-    res = grid.run(d, s.y, cv_idx, objs, [0] * len(objs), stats=st)
-    print(f"c4 grid: {time.time() - t0:.1f} s, stops {st.stops}")
+    res = grid.run(d, s.y, cv_idx, _objectives(E), [0] * len(LAMS_C4), stats=st)
+    print(f"c4 grid: {time.time() - t0:.1f} s, stops {st.stops}, grams {st.gram_fits}, "
+          f"kept {st.reused}, shared {st.shared}, aliased {st.aliased}")
     return s, d, cv_idx, res, st
 
 
 def test_c4_grid_converged_on_step_criterion(c4):
     s, d, cv_idx, res, st = c4
+    assert len(res) == 20
     for r in res:
         assert r["converged"], r["n_iter"]
+        assert len(r["n_iter"]) == 6
     assert st.stops["stagnation"] == 0 and st.stops["line_search_failed"] == 0, st.stops
     assert st.stops["max_iter"] == 0, st.stops
+    # the timed configuration's approximate-Hessian paths all ran
+    assert st.shared > 0 and st.aliased > 0 and st.reused > 0, (st.shared, st.aliased, st.reused)
 
 
 def test_c4_newton_distance_float64_every_fit(c4):
-    """|H^-1 g|_inf <= 1e-5 max|beta| for all 12 fits, float64 on the device."""
+    """|H^-1 g|_inf <= 1e-5 max|beta| for all 120 fits, float64 on the device."""
     import torch
     s, d, cv_idx, res, st = c4
     Xd = _device_augmented(s, torch)
     yd = torch.from_numpy(s.y).cuda()
     n, pa = Xd.shape
-    worst = 0.0
+    masks = []
+    for k in range(5):
+        m = torch.zeros(n, dtype=torch.float64, device="cuda")
+        m[torch.from_numpy(np.asarray(cv_idx[k][0])).cuda()] = 1.0
+        masks.append(m)
+    masks.append(torch.ones(n, dtype=torch.float64, device="cuda"))
+    worst, checked = 0.0, 0
     for j, alpha in enumerate(LAMS_C4):
         r = res[j]
-        fits = [(cv_idx[k][0], r["cv_coefs"][:, k], r["cv_intercepts"][k]) for k in range(5)]
-        fits.append((None, r["refit_coef"], r["refit_intercept"]))
-        for rows, coef, b in fits:
-            m = torch.zeros(n, dtype=torch.float64, device="cuda")
-            if rows is None:
-                m.fill_(1.0)
-            else:
-                m[torch.from_numpy(np.asarray(rows)).cuda()] = 1.0
+        fits = [(r["cv_coefs"][:, k], r["cv_intercepts"][k]) for k in range(5)]
+        fits.append((r["refit_coef"], r["refit_intercept"]))
+        for k, (coef, b) in enumerate(fits):
+            m = masks[k]
             cnt = float(m.sum())
             beta = torch.from_numpy(np.r_[coef, b]).cuda()
-            mu = torch.exp(Xd @ beta)
+            wmu = m * torch.exp(Xd @ beta)
             pen = torch.full((pa,), alpha * cnt, dtype=torch.float64, device="cuda")
             pen[-1] = 0.0
-            g = Xd.t() @ (m * (mu - yd)) + pen * beta           # sum-objective gradient
-            H = Xd.t() @ (Xd * (m * mu)[:, None])
+            g = Xd.t() @ (wmu - m * yd) + pen * beta             # sum-objective gradient
+            H = Xd.t() @ (Xd * wmu[:, None])
             H.diagonal().add_(pen)
             step = torch.linalg.solve(H, g)
             dist = float(step.abs().max()) / float(beta[:-1].abs().max())
             worst = max(worst, dist)
-            assert dist <= 1e-5, (alpha, rows is None, dist)
-            del H, mu, g
-    print(f"c4 worst float64 Newton distance / max|beta|: {worst:.2e}")
+            checked += 1
+            assert dist <= 1e-5, (j, alpha, k, dist)
+            del H, wmu, g
+    assert checked == 120
+    print(f"c4 worst float64 Newton distance / max|beta| over 120 fits: {worst:.2e}")
 
 
 @pytest.fixture(scope="module")
@@ -125,16 +144,17 @@ def c4_host(c4):
     return _host_augmented(s)
 
 
-def test_c4_split_fit_vs_oracle(c4, c4_host):
-    """Split 0 at lambda = 1e-4 (800k train rows) vs the float64 oracle."""
+@pytest.mark.parametrize("j", [0, 5, 12])
+def test_c4_split_fit_vs_oracle(c4, c4_host, j):
+    """Split 0 (800k train rows) at lambda index j vs the float64 oracle."""
     s, d, cv_idx, res, st = c4
     tr = np.asarray(cv_idx[0][0])
     t0 = time.time()
-    c, b = glm_ref.fit_tweedie_newton(c4_host[tr], s.y[tr], LAMS_C4[0], 1.0, tol=1e-10,
+    c, b = glm_ref.fit_tweedie_newton(c4_host[tr], s.y[tr], LAMS_C4[j], 1.0, tol=1e-10,
                                       max_iter=50, augmented=True)
-    print(f"oracle split fit {time.time() - t0:.1f} s")
-    assert rel(res[0]["cv_coefs"][:, 0], c) < TOL_POIS
-    assert abs(res[0]["cv_intercepts"][0] - b) < TOL_POIS * max(1.0, abs(b))
+    print(f"oracle split fit (lambda {LAMS_C4[j]:.3g}) {time.time() - t0:.1f} s")
+    assert rel(res[j]["cv_coefs"][:, 0], c) < TOL_POIS
+    assert abs(res[j]["cv_intercepts"][0] - b) < TOL_POIS * max(1.0, abs(b))
 
 
 def test_c4_refit_vs_oracle(c4, c4_host):
@@ -146,6 +166,31 @@ def test_c4_refit_vs_oracle(c4, c4_host):
     print(f"oracle refit {time.time() - t0:.1f} s")
     assert rel(res[0]["refit_coef"], c) < TOL_POIS
     assert abs(res[0]["refit_intercept"] - b) < TOL_POIS * max(1.0, abs(b))
+
+
+def test_c4_eight_rank_shares_merge_to_the_unsharded_grid(c4):
+    """The timed grid cut into 8 rank shares, each solved exactly as a rank of the 8-GPU run
+    solves it, merged (grid.merge_results' input) and assembled == the unsharded grid."""
+    from sglm_hip import engine as E, grid
+    s, d, cv_idx, full, st = c4
+    objs = _objectives(E)
+    rolls = [0] * len(objs)
+    groups = [{"cv_idx": cv_idx, "objectives": objs, "rolls": rolls}]
+    plan = grid.plan_fits(groups, s.N)
+    merged, seen = {}, []
+    for r in range(8):
+        share = grid.run(d, s.y, cv_idx, objs, rolls, simulate=(r, 8))
+        assert sorted(share) == grid.rank_share(plan, groups, r, 8)
+        seen += list(share)
+        merged.update(share)
+    assert sorted(seen) == list(range(120))
+    out = grid.assemble(groups, plan, merged, s.p)[0]
+    for a, b in zip(out, full):
+        assert a["converged"] and b["converged"]
+        assert rel(a["cv_coefs"], b["cv_coefs"]) < 1e-5
+        assert rel(a["cv_intercepts"], b["cv_intercepts"]) < 1e-5
+        assert rel(a["refit_coef"], b["refit_coef"]) < 1e-5
+        assert np.max(np.abs(a["cv_scores_test"] - b["cv_scores_test"])) < 1e-6
 
 
 def test_chol_solve_p2048_lookahead_chain(engine):

@@ -708,9 +708,19 @@ def test_step_scalars_and_update_vs_float64(engine, torch_mod):
     slots = torch.tensor([7, 0, 3, 8], dtype=torch.int32, device="cuda")
     T = t.numel()
     out = torch.empty(4 * (5 + T), dtype=torch.float64, device="cuda")
-    _lib.call("sglm_step_scalars", P, 4, slots.data_ptr(), g.data_ptr(), w.data_ptr(),
+    _lib.call("sglm_step_scalars", P, P, 4, slots.data_ptr(), g.data_ptr(), w.data_ptr(),
               d.data_ptr(), lp.data_ptr(), t.data_ptr(), T, out.data_ptr(), 0)
     o = out.view(4, 5 + T).cpu().numpy()
+    nc = 300                                   # max|w + t d| over the first ncoef only
+    out2 = torch.empty_like(out)
+    _lib.call("sglm_step_scalars", P, nc, 4, slots.data_ptr(), g.data_ptr(), w.data_ptr(),
+              d.data_ptr(), lp.data_ptr(), t.data_ptr(), T, out2.data_ptr(), 0)
+    o2 = out2.view(4, 5 + T).cpu().numpy()
+    for q, k in enumerate((7, 0, 3, 8)):
+        dk = d[k, :nc].double()
+        assert np.allclose(o2[q, 5:], [float((w[k, :nc] + tj * dk).abs().max())
+                                       for tj in t.tolist()], rtol=1e-12, atol=1e-12)
+        assert np.array_equal(o2[q, :5], o[q, :5])
     for q, k in enumerate((7, 0, 3, 8)):
         dk = d[k].double()
         ref = [float((g[k] * dk).sum()), float((lp[k] * w[k] * w[k]).sum()),

@@ -138,4 +138,53 @@ def test_native_host_masks_vs_python():
     with pytest.raises(ValueError, match="outside"):
         E.host_masks([(np.array([3, n]), True)], n, ld)
     with pytest.raises(ValueError, match="outside"):
-        E.host_masks([(np.array([-1, 3]), False)], n, ld)
+        E.host_masks([(np.array([-n - 1, 3]), False)], n, ld)
+
+
+def test_negative_fold_indices_wrap_like_numpy():
+    """X[idx_train] (backend/sglm_cv.py:107-110) wraps indices in [-n, 0); the native mask
+    builder, the Python mask builders and the row counts do the same."""
+    from sglm_hip import engine as E, folds, grid
+    rng = np.random.default_rng(1)
+    n, ld = 5_003, 5_120
+    pos = np.sort(rng.choice(n, 2000, replace=False))
+    neg = pos - n                                            # the same rows, negative
+    mixed = np.where(rng.random(pos.size) < 0.5, pos, neg)   # unsorted once wrapped
+    rep = rng.integers(-n, n, 4000)
+    specs = [(neg, True), (mixed, True), (rep, True), (mixed, False)]
+    nnz, sums, M = E.host_masks(specs, n, ld)
+    want_rows = np.zeros(n, np.uint8)
+    want_rows[pos] = 1
+    for f, (idx, mult) in enumerate(specs):
+        want = np.zeros(n, np.int64)
+        np.add.at(want, np.asarray(idx) % n, 1)
+        if not mult:
+            want = (want > 0).astype(np.int64)
+        np.testing.assert_array_equal(M[f, :n], want)
+        np.testing.assert_array_equal(grid._mask_array(idx, mult, n), want)
+        assert sums[f] == want.sum() == grid._mask_count(idx, mult, n)
+        assert nnz[f] == np.count_nonzero(want)
+    np.testing.assert_array_equal(M[0, :n], want_rows)
+    np.testing.assert_array_equal(folds.mask_from_idx(neg, n), want_rows)
+    with pytest.raises(IndexError):
+        folds.wrap_indices([0, -n - 1], n)
+
+
+def test_hessian_copies_resolve_to_formed_hessians():
+    """engine._resolve_copies: an exact duplicate of a representative that is itself
+    shared along its lambda chain reads the chain representative's Hessian, with the chain
+    distance as its drift; order of the copy list does not matter."""
+    from sglm_hip import engine as E
+    # fit 3 duplicates 1 (same start); 1 is shared from 0 along the chain (dist .2); 5 from 1?
+    src = {3: (1, 0.0), 1: (0, 0.2), 4: (2, 0.0), 6: (4, 0.0)}
+    got = {k: (r, d) for k, r, d in E._resolve_copies(src, [0, 2, 7])}
+    assert got == {3: (0, 0.2), 1: (0, 0.2), 4: (2, 0.0), 6: (2, 0.0)}
+    with pytest.raises(RuntimeError):
+        E._resolve_copies({1: (5, 0.0)}, [0])
+    # uniq shares then fails back: a fit that is both formed and listed is its own source
+    assert E._resolve_copies({}, [0, 1]) == []
+    # the chain sharing of hess_finish: a chain 0 <- 1 <- 2 (greedy, summed distance)
+    keep, shared = E._share_chains(np.array([0, 1, 2], np.int32), [[0, 1, 2]],
+                                   np.array([0.1, 0.1]), 0.375)
+    assert keep.tolist() == [0] and [(k, r) for k, r, _ in shared] == [(1, 0), (2, 0)]
+    assert abs(shared[1][2] - 0.2) < 1e-12
