@@ -43,7 +43,12 @@ CONFIGS = {
     "prep": (16_000_000, 0, 0, 0, 0),
     # gen_signal_df.generate_signal_df: trials per session
     "signal": (0, 0, 0, 0, 0),
+    # pp_design_mat.make_design_mat: trials per session
+    "designmat": (0, 0, 0, 0, 0),
 }
+DM_TRIALS = 100_000                 # ~9.8M rows at 50 Hz (a ~54 h session, or a day's sessions)
+DM_CPU_TRIALS = 20_000              # the pandas sample (~2M rows, ~6 s)
+DM_INTERACTIONS = {"Reward": ["Consumption", "Cue"], "h2": ["Select"]}
 SIGNAL_TRIALS = 60_000
 C5_RESPONSES = 64
 PREP_SHIFT = 1     # er_refactored_from_scratch_cleanup.py:269 calls preprocess_lynne(df, trial_shift_bounds=1)
@@ -437,6 +442,97 @@ def bench_signal(a):
         "cpu_baseline": cpu}))
 
 
+def bench_designmat(a):
+    """pp_design_mat.make_design_mat (pp_design_mat.py:128-205) on a
+    synthetic DM_TRIALS-trial session resident in HBM (float64 columns), interactions Reward x
+    (Consumption, Cue) and h2 x Select, first licks of the consumption bouts.  One step = one
+    session's design matrix (grouping, heatmap columns, licks, counters, pulls, interactions,
+    flag) into one output block.  Sessions are independent: one per rank (weak scaling)."""
+    import contextlib
+    import io
+    import torch
+    import torch.distributed as dist
+    import pp_design_mat
+    from sglm_hip import designmat, synth
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    states = ["Select", "Consumption", "ENLP"]
+    ts, tr = synth.designmat_session(DM_TRIALS, 300 + rank)
+    n = len(ts)
+    tri = tr.set_index("nTrial").convert_dtypes()
+    cols, dts = designmat.upload(ts, states)
+
+    def step():
+        return designmat.design_matrix_device(cols, dts, n, tri, states, [1], DM_INTERACTIONS,
+                                              verbose=False)
+    for _ in range(max(1, a.warmup)):
+        res = step()
+    stream = torch.cuda.current_stream()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(a.steps):
+        res = step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = (time.perf_counter() - t0) / a.steps
+    call_ms = ev0.elapsed_time(ev1) / a.steps
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64,
+                         device="cuda" if a.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t[0])
+    if rank != 0:
+        return
+    K = len(res.names)
+    n_in = len([c for c in cols if c != "__order__"])
+    algo_row = 8 * (n_in + K)                # every input column read once, the matrix written
+    achieved = algo_row * n / el / 1e9
+    # the drop-in with host frames in and out (PCIe + pandas frame assembly), never `value`
+    t1 = time.perf_counter()
+    with contextlib.redirect_stdout(io.StringIO()):
+        pp_design_mat.make_design_mat(ts.copy(), tr, interactions=DM_INTERACTIONS)
+    e2e_s = time.perf_counter() - t1
+    cpu = None
+    if not a.no_cpu:
+        import warnings
+        from oracle import designmat_pandas
+        sts, str_ = synth.designmat_session(DM_CPU_TRIALS, 300 + rank)
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            t2 = time.perf_counter()
+            designmat_pandas.make_design_mat(sts, str_, interactions=DM_INTERACTIONS,
+                                             verbose=False)
+            dt = time.perf_counter() - t2
+        cpu = {"value": len(sts) / dt, "unit": "session rows/s", "cores": 1, "kind": "port",
+               "sample": f"oracle/designmat_pandas.py (the reference's pandas operations: "
+                         f"groupby cumcount / nth / first / sum, map, get_dummies) on a "
+                         f"{DM_CPU_TRIALS}-trial session of {len(sts)} rows, {dt:.2f} s"}
+    print(json.dumps({
+        "metric": "design-matrix rows/s (pp_design_mat.make_design_mat)",
+        "value": n * world / el, "unit": "session rows/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": el * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": f"one {DM_TRIALS}-trial session per rank ({n} rows, {n_in} "
+                               f"float64 input columns -> {K} design columns; interactions "
+                               f"{DM_INTERACTIONS}, nth_licks [1])",
+                   "config_name": "designmat", "rows": n, "columns": res.names,
+                   "dropin_host_frames_rows_per_s": n / e2e_s,
+                   "event_ms_per_step": call_ms,
+                   "parallelism": f"one session per rank, {world} rank(s)"},
+        "roofline": {"bound": "hbm", "kernel": "design_matrix_device (whole step: 2 groupings, "
+                                               "heatmap, licks, counters, pull, trial maps, flag)",
+                     "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": achieved / PEAK_HBM_GBS, "traffic": None,
+                     "algorithmic_bytes_per_row": algo_row, "avg_step_ms": el * 1e3},
+        "cpu_baseline": cpu}))
+
+
 def spawn_ranks(a):
     """``--gpus N`` without a launcher: start N rank processes (torch.distributed.run, one per
     GPU, rendezvous on 127.0.0.1) as CHILDREN before anything touches the GPU, and exit with
@@ -455,8 +551,9 @@ def spawn_ranks(a):
 
 
 def newton_distance(s, design, cv_idx, res, lams, checks):
-    """float64 distance |H^-1 g|_inf / max|beta| of a few fits of the last grid to the exact
-    minimiser, from the exact design on the device (torch float64; outside the timed region)."""
+    """float64 Newton distance of a few fits of the last grid to the exact minimiser,
+    max_j<p |(H^-1 g)_j| / max_j<p |beta_j| (the coefficients), from the exact design on the
+    device (torch float64; outside the timed region)."""
     import torch
     m = s.E.shape[1]
     Ed = torch.from_numpy(s.E).cuda().to(torch.float64)
@@ -485,7 +582,8 @@ def newton_distance(s, design, cv_idx, res, lams, checks):
         g = Xd.t() @ (w * (mu - yd)) + pen * beta
         H = Xd.t() @ (Xd * (w * mu)[:, None])
         H.diagonal().add_(pen)
-        worst = max(worst, float(torch.linalg.solve(H, g).abs().max()) / float(beta[:-1].abs().max()))
+        step = torch.linalg.solve(H, g)
+        worst = max(worst, float(step[:-1].abs().max()) / float(beta[:-1].abs().max()))
         del H
     del Xd
     torch.cuda.empty_cache()
@@ -509,8 +607,9 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group("gloo")
-    if a.config in ("c5", "prep", "signal"):
-        {"c5": bench_c5, "prep": bench_prep, "signal": bench_signal}[a.config](a)
+    if a.config in ("c5", "prep", "signal", "designmat"):
+        {"c5": bench_c5, "prep": bench_prep, "signal": bench_signal,
+         "designmat": bench_designmat}[a.config](a)
         if world > 1:
             dist.destroy_process_group()
         return

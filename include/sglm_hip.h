@@ -278,11 +278,11 @@ int sglm_chol_solve_alias(const float* H, int32_t P, const int32_t* fits, const 
                           const uint8_t* frozen, int32_t B, void* work, sglm_stream_t stream);
 
 /* Per-fit scalars of a Newton step for the B fits k = slots[q], float64 (one workgroup per
- * fit): out[q][0..5+T) = { g.d, sum lam w^2, sum lam w d, sum lam d^2, max|d|,
- * max|w + t[j] d| for j < T } over the P coordinates of g[k] (float64), beta[k] (float64),
- * delta[k] (f32), lamp[k] (float64 penalty row); the max|w + t d| terms run over the first
- * `ncoef` coordinates only (the coefficients without the intercept, the scale of the
- * stopping rule; ncoef = P: all).  The Armijo test and the stopping rule of sklearn's Newton
+ * fit): out[q][0..6+T) = { g.d, sum lam w^2, sum lam w d, sum lam d^2, max|d_a|,
+ * max|w_a + t[j] d_a| for j < T, max|d_b| } over the P coordinates of g[k] (float64), beta[k]
+ * (float64), delta[k] (f32), lamp[k] (float64 penalty row); a runs over the first `ncoef`
+ * coordinates (the coefficients), b over the rest (the intercept; padding is 0) -- the two
+ * scales of the stopping rule (ncoef = P: every coordinate in the a terms, max|d_b| = 0).  The Armijo test and the stopping rule of sklearn's Newton
  * solver (_newton_solver.py:201-260) need only these.  T <= 16. */
 int sglm_step_scalars(int32_t P, int32_t ncoef, int32_t B, const int32_t* slots, const double* g,
                       const double* beta, const float* delta, const double* lamp,
@@ -407,6 +407,68 @@ enum sglm_prep_out {
 size_t sglm_prep_work_bytes(int64_t n);
 int sglm_prep_session(const double* in, int64_t ld_in, int64_t n, int32_t k, double* out,
                       int64_t ld_out, void* work, sglm_stream_t stream);
+
+/* --- event design matrix (pp_design_mat.make_design_mat, pp_design_mat.py:6-205) --------
+ * Float64 session columns (a pandas float block) on the device.  A pandas groupby over a float
+ * key is a GROUPING here:
+ * sglm_group_rows: perm[0 .. m) = the rows whose key (and key2, when not NULL) is not NaN,
+ *   grouped by key value (lexicographic (key, key2)), row order kept within a group (pandas'
+ *   group and within-group order; NaN-key rows are dropped as groupby drops them);
+ *   seg[0 .. nseg] = group starts in perm plus m; counts = {m, nseg} (device int64).  The
+ *   ordering check synchronises the stream once; *sorted_out (host, may be NULL) reports
+ *   whether the keys were already ordered (stable partition) or were radix-sorted.  n < 2^31.
+ *   Replaces groupby('nTrial') / groupby(['nTrial', 'nENL']) (:52, 114-120, 171-175, 200).
+ * sglm_trial_lookup: tidx[i] = position of key[i] in the ascending, unique trial ids tkeys,
+ *   -1 when NaN or absent -- Series.map(trials[...]) (:93, 112, 123, 192).
+ * sglm_dm_heatmap: add_heatmap_columns (:108-126) into out (5 x ld_out): hm_t_cue_offset_to_sel
+ *   = tsel[tidx] (tidx NULL: NaN), hm_t_from_cue_onset, hm_t_from_cons_onset (trial_clock minus
+ *   the group's first non-null clock of its Cue == 1 / Consumption == 1 rows),
+ *   hm_t_sel_to_cons = (sum stateConsumption - sum Consumption) * 20, hm_t_cue_offset_to_cons.
+ *   Group sums run in a fixed order: exact for integer-valued state columns.
+ * sglm_dm_licks: Lick = ~isnan(iSpout) (from_spout) or the given Lick column; out[c] =
+ *   states[c] * Lick (classify_lick_state, :6-23); lick_out (may be NULL) gets Lick.  Host
+ *   arrays of device pointers, nstates <= 32.
+ * sglm_dm_counters: time_from_enl_onset = cumcount^2 / 5000 over the (ENL == 1 | Cue == 1)
+ *   rows of each nTrial group, time_from_enlp_onset over the state_ENLP == 1 rows of each
+ *   (nTrial, nENL) group (NaN on such rows with a NaN key, 0 elsewhere) (:167-172); cue_on (may
+ *   be NULL): 1 on each group's first Cue == 1 row (:175, 182-183).
+ * sglm_dm_pull: pull_lick_from_bout (:26-58) for positions nth[0 .. npull) in processing order:
+ *   cols[j] = 1 on the (nth - 1)-th (negative: from the end) bout == 1 row of each group, that
+ *   bout row set to 0.  npull <= 16; nth and cols are host arrays.
+ * sglm_trial_map: dst[dst_cols[c]][i] = (src_cols[c] < 0 ? 1 : src[src_cols[c]][i]) *
+ *   vals[val_cols[c]][tidx[i]] (NaN when tidx[i] < 0): event_interactions_dummies (:87-99)
+ *   and the flag's mapped isna (:192).  Index arrays on the device.
+ * sglm_zero_groups_flag: flag = 1 on every row of the groups whose listed columns sum to 0
+ *   (skipna) -- the trials without a cue dummy (:198-203); group_zero (may be NULL, >= nseg
+ *   bytes) gets 1 for those groups (the printed trials_without_dummies, :201-202). */
+size_t sglm_group_rows_work_bytes(int64_t n);
+int sglm_group_rows(const double* key, const double* key2, int64_t n, int64_t* perm,
+                    int64_t* seg, int64_t* counts, int32_t* sorted_out, void* work,
+                    sglm_stream_t stream);
+int sglm_trial_lookup(const double* key, int64_t n, const double* tkeys, int64_t nt,
+                      int32_t* tidx, sglm_stream_t stream);
+int sglm_dm_heatmap(const double* clock, const double* cue, const double* cons,
+                    const double* scons, int64_t n, const int64_t* perm, const int64_t* seg,
+                    const int64_t* counts, const int32_t* tidx, const double* tsel, double* out,
+                    int64_t ld_out, sglm_stream_t stream);
+int sglm_dm_licks(const double* lick_src, int32_t from_spout, const double* const* states,
+                  int32_t nstates, int64_t n, double* const* out, double* lick_out,
+                  sglm_stream_t stream);
+int sglm_dm_counters(const double* enl, const double* cue, const double* senlp, int64_t n,
+                     const int64_t* perm, const int64_t* seg, const int64_t* counts,
+                     const int64_t* perm2, const int64_t* seg2, const int64_t* counts2,
+                     double* tenl, double* tenlp, double* cue_on, sglm_stream_t stream);
+int sglm_dm_pull(double* bout, int64_t n, const int64_t* perm, const int64_t* seg,
+                 const int64_t* counts, const int32_t* nth, int32_t npull, double* const* cols,
+                 sglm_stream_t stream);
+int sglm_trial_map(int64_t n, const int32_t* tidx, const double* src, int64_t ld_src,
+                   const int32_t* src_cols, const double* vals, int64_t nt,
+                   const int32_t* val_cols, int32_t ncols, double* dst, int64_t ld_dst,
+                   const int32_t* dst_cols, sglm_stream_t stream);
+int sglm_zero_groups_flag(int64_t n, const int64_t* perm, const int64_t* seg,
+                          const int64_t* counts, const double* src, int64_t ld,
+                          const int32_t* cols, int32_t ncols, double* flag,
+                          uint8_t* group_zero, sglm_stream_t stream);
 
 /* --- grid setup on the host (CPU, multithreaded; no device pointers) -------------------
  * sglm_host_masks: row mask f (uint8, out + f * ld, zero past n) of a CV grid from its index

@@ -536,7 +536,7 @@ __global__ void __launch_bounds__(256) step_scalars_kernel(
     const double* bk = beta + (int64_t)k * P;
     const float* dk = delta + (int64_t)k * P;
     const double* lk = lamp + (int64_t)k * P;
-    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0, md = 0.0;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0, md = 0.0, mi = 0.0;
     double mb[kMaxStepT];
     double tv[kMaxStepT];
     for (int j = 0; j < T; ++j) { mb[j] = 0.0; tv[j] = t[j]; }
@@ -546,18 +546,18 @@ __global__ void __launch_bounds__(256) step_scalars_kernel(
         s1 += l * b * b;
         s2 += l * b * d;
         s3 += l * d * d;
-        md = fmax(md, fabs(d));
+        if (a < ncoef) md = fmax(md, fabs(d)); else mi = fmax(mi, fabs(d));
         if (a < ncoef)
             for (int j = 0; j < T; ++j) mb[j] = fmax(mb[j], fabs(b + tv[j] * d));
     }
-    double* o = out + (int64_t)q * (5 + T);
+    double* o = out + (int64_t)q * (6 + T);
     double v;
     v = block_sum_d(s0, sh); if (threadIdx.x == 0) o[0] = v;
     v = block_sum_d(s1, sh); if (threadIdx.x == 0) o[1] = v;
     v = block_sum_d(s2, sh); if (threadIdx.x == 0) o[2] = v;
     v = block_sum_d(s3, sh); if (threadIdx.x == 0) o[3] = v;
-    for (int j = -1; j < T; ++j) {
-        double m = j < 0 ? md : mb[j];
+    for (int j = -1; j <= T; ++j) {
+        double m = j < 0 ? md : (j < T ? mb[j] : mi);
         for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_xor(m, off, 64));
         __syncthreads();
         if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = m;

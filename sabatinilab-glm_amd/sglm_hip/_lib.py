@@ -77,6 +77,19 @@ SIGNATURES = {
     "sglm_eta_pair_absmax": (C.c_int, [_i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "sglm_score_sums": (C.c_int, [_i32, _f32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
                                   _vp, _vp]),
+    "sglm_group_rows_work_bytes": (_sz, [_i64]),
+    "sglm_group_rows": (C.c_int, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "sglm_trial_lookup": (C.c_int, [_vp, _i64, _vp, _i64, _vp, _vp]),
+    "sglm_dm_heatmap": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64,
+                                  _vp]),
+    "sglm_dm_licks": (C.c_int, [_vp, _i32, _vp, _i32, _i64, _vp, _vp, _vp]),
+    "sglm_dm_counters": (C.c_int, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                   _vp, _vp]),
+    "sglm_dm_pull": (C.c_int, [_vp, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
+    "sglm_trial_map": (C.c_int, [_i64, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _i32, _vp, _i64, _vp,
+                                 _vp]),
+    "sglm_zero_groups_flag": (C.c_int, [_i64, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp,
+                                        _vp]),
     "sglm_host_masks": (C.c_int, [_i32, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _i32]),
     "sglm_scatter_rows": (C.c_int, [_i64, _vp, _i64, _vp, _i32, _vp, _i64, _vp]),
     "sglm_signal_trials_work_bytes": (_sz, [_i64]),

@@ -47,7 +47,9 @@ COL_PAD = 256
 ROW_PAD = 256
 ARMIJO_SIGMA = 2.0 ** -11      # sklearn _newton_solver.py:214
 # stopping rule: max|t d| <= tol * max(max_j<p |w_j|, STOP_SCALE_FLOOR) (tol = 1e-6)
-STOP_SCALE_FLOOR = 1e-2
+STOP_SCALE_FLOOR = float(__import__("os").environ.get("SGLM_STOP_SCALE_FLOOR", "0.1"))
+# round-2 rule, for comparison runs: max|t d| <= tol * (1 + max|w|), intercept included
+STOP_LEGACY = __import__("os").environ.get("SGLM_STOP_RULE", "") == "legacy"
 # second round of line-search step lengths (the first: 1, 1/2, 1/4, 1/8)
 TV2 = np.array([0.0625, 0.03125, 0.015625, 0.0078125, 2.0 ** -10, 2.0 ** -14, 2.0 ** -20])
 XTR_BITS = True                # X^T R on the MFMA from compacted bit-planes for 0/1 designs
@@ -864,7 +866,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
     ts_all = torch.from_numpy(np.concatenate([[0.0, 1.0, 0.5, 0.25, 0.125],
                                               TV2.astype(np.float32)])).to(dev)
     nts = int(ts_all.numel())
-    sc_d = torch.empty(B0 * (5 + nts), dtype=torch.float64, device=dev)
+    sc_d = torch.empty(B0 * (6 + nts), dtype=torch.float64, device=dev)
     # fits still at their common start (same mask and response => bitwise equal Hessians)
     fresh_start = np.array([r.coef0 is None for r in reqs])
     lamp_d = torch.from_numpy(lam[:, None] * penal).to(dev)        # lam * penalty mask
@@ -1145,8 +1147,8 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         # per-fit scalars of the line search and the stopping rule, reduced on the device
         # over the coefficients (no B x P array crosses to the host): g.d, the penalty terms
         # lam|w|^2, 2 lam w.d, lam|d|^2, max|d| and max|w + t d| for every trial step t
-        sc = sc_d[: na * (5 + nts)]
-        _lib.call("sglm_step_scalars", P, p, na, _p(act_d), _p(bf.gtot), _p(beta64_d), _p(bf.delta),
+        sc = sc_d[: na * (6 + nts)]
+        _lib.call("sglm_step_scalars", P, P if STOP_LEGACY else p, na, _p(act_d), _p(bf.gtot), _p(beta64_d), _p(bf.delta),
                   _p(lamp_d), _p(ts_all), nts, _p(sc), st)
         t0 = tick("it_solve_eta", t0)
         # ---- line search (rows of L, dmax and sc: active fits in slot order)
@@ -1167,7 +1169,8 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         dmaxeta = dmax_h[:na].numpy().astype(np.float64)
         scn = sc_h.numpy().reshape(na, -1).copy()
         gdir, A_, B_, C_, maxd = scn[:, 0], scn[:, 1], scn[:, 2], scn[:, 3], scn[:, 4]
-        maxb = scn[:, 5:]                       # max|w + t d| for t in TS_ALL
+        maxb = scn[:, 5:5 + nts]                # max|w_j + t d_j| (j < p) for t in TS_ALL
+        maxdi = scn[:, 5 + nts]                 # |d| of the intercept
         ts = np.array([0.0, 1.0, 0.5, 0.25, 0.125])
 
         def objectives(Lm, tv):
@@ -1227,9 +1230,15 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         # the step, the intercept excluded), floored at STOP_SCALE_FLOOR: the parity tests
         # measure errors relative to max|coef|, so a fit with small coefficients (strong
         # penalty) must converge in those units too
-        scale = np.maximum(maxb[np.arange(na), tix], STOP_SCALE_FLOOR)
-        relv = step_a * maxd / scale
-        prop = maxd / scale                            # the proposed Newton step
+        if STOP_LEGACY:
+            scale = 1.0 + maxb[np.arange(na), tix]
+            prop = maxd / scale                        # the proposed Newton step
+        else:
+            # coefficients in units of their own scale, the intercept in absolute units (it
+            # is O(1) and its parity bar is absolute): the measures the parity tests apply
+            scale = np.maximum(maxb[np.arange(na), tix], STOP_SCALE_FLOOR)
+            prop = np.maximum(maxd / scale, maxdi)
+        relv = step_a * prop
         stepa = step_a
         fresh = (gram_now[act] & exact_h[act]) | const_hess
         ls_fail = stepa == 0.0

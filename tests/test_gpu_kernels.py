@@ -707,25 +707,28 @@ def test_step_scalars_and_update_vs_float64(engine, torch_mod):
                      device="cuda")
     slots = torch.tensor([7, 0, 3, 8], dtype=torch.int32, device="cuda")
     T = t.numel()
-    out = torch.empty(4 * (5 + T), dtype=torch.float64, device="cuda")
+    out = torch.empty(4 * (6 + T), dtype=torch.float64, device="cuda")
     _lib.call("sglm_step_scalars", P, P, 4, slots.data_ptr(), g.data_ptr(), w.data_ptr(),
               d.data_ptr(), lp.data_ptr(), t.data_ptr(), T, out.data_ptr(), 0)
-    o = out.view(4, 5 + T).cpu().numpy()
+    o = out.view(4, 6 + T).cpu().numpy()
     nc = 300                                   # max|w + t d| over the first ncoef only
     out2 = torch.empty_like(out)
     _lib.call("sglm_step_scalars", P, nc, 4, slots.data_ptr(), g.data_ptr(), w.data_ptr(),
               d.data_ptr(), lp.data_ptr(), t.data_ptr(), T, out2.data_ptr(), 0)
-    o2 = out2.view(4, 5 + T).cpu().numpy()
+    o2 = out2.view(4, 6 + T).cpu().numpy()
     for q, k in enumerate((7, 0, 3, 8)):
         dk = d[k, :nc].double()
-        assert np.allclose(o2[q, 5:], [float((w[k, :nc] + tj * dk).abs().max())
-                                       for tj in t.tolist()], rtol=1e-12, atol=1e-12)
-        assert np.array_equal(o2[q, :5], o[q, :5])
+        assert np.allclose(o2[q, 5:5 + T], [float((w[k, :nc] + tj * dk).abs().max())
+                                            for tj in t.tolist()], rtol=1e-12, atol=1e-12)
+        assert np.array_equal(o2[q, :4], o[q, :4])
+        assert o2[q, 4] == float(dk.abs().max())
+        assert o2[q, 5 + T] == float(d[k, nc:].double().abs().max())
     for q, k in enumerate((7, 0, 3, 8)):
         dk = d[k].double()
         ref = [float((g[k] * dk).sum()), float((lp[k] * w[k] * w[k]).sum()),
                float((lp[k] * w[k] * dk).sum()), float((lp[k] * dk * dk).sum()),
-               float(dk.abs().max())] + [float((w[k] + tj * dk).abs().max()) for tj in t.tolist()]
+               float(dk.abs().max())] + [float((w[k] + tj * dk).abs().max()) for tj in t.tolist()] \
+            + [0.0]
         assert np.allclose(o[q], ref, rtol=1e-12, atol=1e-12), (k, o[q], ref)
     step = torch.tensor([0.5, 0.0, 1.0, 0.25], dtype=torch.float64, device="cuda")
     w2 = w.clone()
