@@ -408,6 +408,24 @@ size_t sglm_prep_work_bytes(int64_t n);
 int sglm_prep_session(const double* in, int64_t ld_in, int64_t n, int32_t k, double* out,
                       int64_t ld_out, void* work, sglm_stream_t stream);
 
+/* --- gradient of a time-shifted event design ---------------------------------------------
+ * X[t, col(b, a)] = E[t + row0 - shifts[b], a] for a 0/1 event matrix E (m events, K lags;
+ * col = b*m + a for layout 0 (shift-major, sglm_ez.timeshift_cols), a*K + b for layout 1
+ * (event-major, setup_model_fit.timeshift_vals_by_dict)), the ones column at m*K:
+ * g[slots[q]][c] = sum_{t < n} X[t, c] R[slots[q]][t] (float64, c < P; columns past m*K zero)
+ * from the event occurrences: occ = every event's occurrence rows u of E, event-major and
+ * ascending; tbeg / tend [m][ntiles] = the occurrence index range of event a whose window
+ * [u - row0 + min(shifts), u - row0 + max(shifts)] meets design-row tile i (tiles of
+ * sglm_lag_tile_rows() rows, ntiles = ceil(n / that)).  m <= 64, K <= 256.  Replaces the
+ * X^T (y - mu) products of sklearn's gradient (_linear_loss.py:37-54) on the expanded design.
+ * work: sglm_lag_xtr_work_bytes(P, K, B, n) for up to B active fits. */
+int32_t sglm_lag_tile_rows(void);
+size_t sglm_lag_xtr_work_bytes(int32_t P, int32_t K, int32_t B, int64_t n);
+int sglm_lag_xtr(const int32_t* occ, const int32_t* tbeg, const int32_t* tend,
+                 const int32_t* shifts, int32_t m, int32_t K, int32_t layout, int64_t row0,
+                 int64_t n, int32_t P, const float* R, int64_t ld, const int32_t* slots,
+                 int32_t nact, double* g, void* work, sglm_stream_t stream);
+
 /* --- event design matrix (pp_design_mat.make_design_mat, pp_design_mat.py:6-205) --------
  * Float64 session columns (a pandas float block) on the device.  A pandas groupby over a float
  * key is a GROUPING here:

@@ -77,6 +77,10 @@ SIGNATURES = {
     "sglm_eta_pair_absmax": (C.c_int, [_i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "sglm_score_sums": (C.c_int, [_i32, _f32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
                                   _vp, _vp]),
+    "sglm_lag_tile_rows": (_i32, []),
+    "sglm_lag_xtr_work_bytes": (_sz, [_i32, _i32, _i32, _i64]),
+    "sglm_lag_xtr": (C.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i64, _i64, _i32, _vp, _i64,
+                               _vp, _i32, _vp, _vp, _vp]),
     "sglm_group_rows_work_bytes": (_sz, [_i64]),
     "sglm_group_rows": (C.c_int, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "sglm_trial_lookup": (C.c_int, [_vp, _i64, _vp, _i64, _vp, _vp]),

@@ -53,6 +53,8 @@ STOP_LEGACY = __import__("os").environ.get("SGLM_STOP_RULE", "") == "legacy"
 # second round of line-search step lengths (the first: 1, 1/2, 1/4, 1/8)
 TV2 = np.array([0.0625, 0.03125, 0.015625, 0.0078125, 2.0 ** -10, 2.0 ** -14, 2.0 ** -20])
 XTR_BITS = True                # X^T R on the MFMA from compacted bit-planes for 0/1 designs
+# X^T R of a time-shifted 0/1 event design (Design.from_events) from the event occurrences
+LAG_XTR = __import__("os").environ.get("SGLM_LAG_XTR", "0") == "1"
 ETA_BITS = True                # eta on the MFMA from row-major bit-planes for 0/1 designs
 SYRK_CBITS = True              # ... and its row-compacted register-only form (v6) when fits
                                # carry masks (the default path for event designs)
@@ -125,6 +127,7 @@ class Design:
         self.xbits = None      # uint32 bit-planes [P, ld/32] when the design is 0/1
         self.rbits = None      # row-major bit-planes [P/64][ld] x uint2 (MFMA eta) when 0/1
         self._cbits = None     # identity-row compacted planes [n/64][P] x uint2 (MFMA X^T R)
+        self.lag = None        # LagStructure of a time-shifted 0/1 event design (from_events)
         self.device = device
 
     @property
@@ -225,6 +228,8 @@ class Design:
         d.xb[p, :n] = 1.0
         if exact:
             d._pack_bits()
+            if d.xbits is not None and bool(((E == 0) | (E == 1)).all()):
+                d.lag = LagStructure.build(E, shifts, row0, n, event_major)
         if not exact:
             Ef = E.t().contiguous()
             d.xf = torch.zeros((d.P, d.ld), dtype=torch.float32, device=device)
@@ -277,6 +282,42 @@ class Design:
             _lib.call("sglm_gemv_eta", _p(self.xg), self.xtype, self.ld, self.P, self.n,
                       _p(beta_dev), B, _p(out), _stream())
         return out
+
+
+class LagStructure:
+    """A time-shifted 0/1 event design by its events (sglm_lag_xtr): X[t, col(b, a)] =
+    E[t + row0 - shifts[b], a].  occ = every event's occurrence rows of E, event-major and
+    ascending; tbeg / tend [m][ntiles] = the occurrence range of event a whose lag window meets
+    design-row tile i (tiles of sglm_lag_tile_rows() rows).  Built on the device once per
+    design."""
+
+    @classmethod
+    def build(cls, E, shifts, row0, n, event_major):
+        self = cls()
+        dev = E.device
+        N_raw, m = E.shape
+        sh = np.asarray(shifts, dtype=np.int64)
+        self.m, self.K = int(m), int(sh.size)
+        self.layout = 1 if event_major else 0
+        self.row0 = int(row0)
+        self.shifts = torch.from_numpy(sh.astype(np.int32)).to(dev)
+        nz = torch.nonzero(E.t() != 0)                       # (event, row), event-major order
+        ev, rows = nz[:, 0], nz[:, 1]
+        self.occ = rows.to(torch.int32).contiguous()
+        U = _lib.query("sglm_lag_tile_rows")
+        ntiles = (int(n) + U - 1) // U
+        big = np.int64(1) << 40
+        keys = ev.to(torch.int64) * big + rows.to(torch.int64)
+        t0 = torch.arange(ntiles, dtype=torch.int64, device=dev) * U
+        a = torch.arange(m, dtype=torch.int64, device=dev)[:, None] * big
+        lo = a + (t0 + row0 - int(sh.max()))[None, :]
+        hi = a + (t0 + U + row0 - int(sh.min()))[None, :]
+        self.tbeg = torch.searchsorted(keys, lo.reshape(-1)).to(torch.int32).contiguous()
+        self.tend = torch.searchsorted(keys, hi.reshape(-1)).to(torch.int32).contiguous()
+        self.ntiles = ntiles
+        if self.m > 64 or self.K > 256:
+            return None                                       # the kernel's bounds
+        return self
 
 
 # ------------------------------------------------------------------------------ problem
@@ -998,10 +1039,17 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         exact = np.zeros(B0, dtype=bool)
         exact[newh] = drift[newh] == 0.0
         return keep, newh, uniq, copies, ali, fail, exact
-    use_rp = d.xbits is not None and XTR_BITS      # R packed into the MFMA gradient operand
+    # the gradient: from the event occurrences for a time-shifted event design (sglm_lag_xtr,
+    # R in f32 by slot), else the bit-plane MFMA with R packed into its operand
+    use_lag = d.lag is not None and LAG_XTR
+    use_rp = d.xbits is not None and XTR_BITS and not use_lag
+    fused = use_rp or use_lag          # link fused with the previous step's predictor update
     if use_rp:
         rp_buf = _work(3 * pad_to(B0, 32) * ld * 2, dev, "rp")
         gx_work = _work(_lib.query("sglm_xtr_bits_packed_work_bytes", P, B0, ld), dev, "xtr")
+    if use_lag:
+        lag_work = _work(_lib.query("sglm_lag_xtr_work_bytes", P, d.lag.K, B0, n), dev, "xtr")
+    R_out, Rp_out = (_p(bf.R), None) if use_lag else (None, _p(rp_buf) if use_rp else None)
 
     import time
     tick = stats.mark if (stats is not None and stats.trace_phases) else (lambda name, t: t)
@@ -1016,11 +1064,11 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         if na == 0:
             break
         act_d = linked if linked is not None else up(act, np.int32)
-        if use_rp:
+        if fused:
             if linked is None:
                 _lib.call("sglm_link_update", fam, power, n, ld, na, _p(act_d), _p(bf.eta),
-                          _p(prob.Y), _p(prob.M), _p(fit_resp), _p(fit_mask), _p(bf.W), None,
-                          _p(rp_buf), None, None, st)
+                          _p(prob.Y), _p(prob.M), _p(fit_resp), _p(fit_mask), _p(bf.W), R_out,
+                          Rp_out, None, None, st)
         else:
             _lib.call("sglm_link_update", fam, power, n, ld, B, None, _p(bf.eta), _p(prob.Y),
                       _p(prob.M), _p(fit_resp), _p(fit_mask), _p(bf.W), _p(bf.R), None, None,
@@ -1029,7 +1077,12 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         def _gradient():
             """X^T R on the current stream, then + lam w (the Hessian step needs only W, so
             its Grams go first and the new factorisations overlap this)."""
-            if use_rp:
+            if use_lag:
+                lg = d.lag
+                _lib.call("sglm_lag_xtr", _p(lg.occ), _p(lg.tbeg), _p(lg.tend), _p(lg.shifts),
+                          lg.m, lg.K, lg.layout, lg.row0, n, P, _p(bf.R), ld, _p(act_d), na,
+                          _p(bf.g), _p(lag_work), st)
+            elif use_rp:
                 _lib.call("sglm_xtr_bits_packed", _p(d.cbits_full()), ld, P, n, _p(rp_buf), na,
                           _p(act_d), _p(bf.g), _p(gx_work), st)
             else:
@@ -1284,7 +1337,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
         # that continue (0/1 designs), a plain axpy for the others
         linked = None
         nxt = np.flatnonzero(active)
-        if use_rp and nxt.size:
+        if fused and nxt.size:
             cont = active[act]
             done = np.flatnonzero(~cont & (step_a != 0.0))
             if done.size:
@@ -1293,7 +1346,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[I
             linked = up(nxt, np.int32)
             _lib.call("sglm_link_update", fam, power, n, ld, int(nxt.size), _p(linked),
                       _p(bf.eta), _p(prob.Y), _p(prob.M), _p(fit_resp), _p(fit_mask), _p(bf.W),
-                      None, _p(rp_buf), _p(up(step_a[cont], np.float32)), _p(bf.deta), st)
+                      R_out, Rp_out, _p(up(step_a[cont], np.float32)), _p(bf.deta), st)
         else:
             _lib.call("sglm_eta_axpy", n, ld, na, _p(act_d), _p(up(step_a, np.float32)),
                       _p(bf.deta), _p(bf.eta), st)

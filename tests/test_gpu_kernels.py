@@ -737,3 +737,36 @@ def test_step_scalars_and_update_vs_float64(engine, torch_mod):
     for q, k in enumerate((7, 0, 3, 8)):
         assert torch.allclose(w2[k], w[k] + step[q] * d[k].double(), rtol=0, atol=1e-15)
     assert torch.equal(w2[1], w[1])
+
+
+@pytest.mark.parametrize("m,L,event_major,N", [(50, 20, False, 200_001), (7, 3, True, 13_000),
+                                               (17, 9, False, 6_144), (3, 1, False, 100)])
+def test_lag_xtr_vs_float64(engine, m, L, event_major, N):
+    """sglm_lag_xtr (X^T R from the event occurrences of a time-shifted design) against
+    float64 torch on the dense expansion: both layouts, m over and under 16 events (the two
+    register-accumulator variants), sizes off and on the tile boundary, a slot subset."""
+    import torch
+    from sglm_hip import _lib, engine as E, synth
+    s = synth.make(N=N, m=m, L=L, family="poisson", rho=0.05, seed=m + N)
+    d = E.Design.from_events(s.E, s.shifts, s.L - 1, s.N, event_major=event_major)
+    assert d.lag is not None
+    Xd = d.xb[: d.p + 1, : d.n].double().t().contiguous()           # dense (n, p + 1)
+    B = 9
+    rng = np.random.default_rng(3)
+    R = torch.zeros((B, d.ld), dtype=torch.float32, device="cuda")
+    R[:, : d.n] = torch.from_numpy(rng.normal(size=(B, d.n)).astype(np.float32)).cuda()
+    slots = torch.tensor([8, 0, 5, 3], dtype=torch.int32, device="cuda")
+    g = torch.full((B, d.P), 7.0, dtype=torch.float64, device="cuda")
+    lg = d.lag
+    work = torch.empty(_lib.query("sglm_lag_xtr_work_bytes", d.P, lg.K, B, d.n),
+                       dtype=torch.uint8, device="cuda")
+    _lib.call("sglm_lag_xtr", lg.occ.data_ptr(), lg.tbeg.data_ptr(), lg.tend.data_ptr(),
+              lg.shifts.data_ptr(), lg.m, lg.K, lg.layout, lg.row0, d.n, d.P, R.data_ptr(),
+              d.ld, slots.data_ptr(), 4, g.data_ptr(), work.data_ptr(), 0)
+    got = g.cpu().numpy()
+    for k in (8, 0, 5, 3):
+        ref = (Xd.t() @ R[k, : d.n].double()).cpu().numpy()
+        np.testing.assert_allclose(got[k, : d.p + 1], ref, rtol=1e-12, atol=1e-9)
+        assert np.all(got[k, d.p + 1:] == 0)
+    for k in (1, 2, 4, 6, 7):
+        assert np.all(got[k] == 7.0)                                   # untouched slots
