@@ -215,6 +215,19 @@ int sglm_enet_cd_grouped(const double* Q, int32_t p, const int32_t* wg_fits, int
                          const double* l2, int32_t max_sweeps, double tol, double* w,
                          int32_t* sweeps, sglm_stream_t stream);
 
+/* sglm_gram_ss: residual sums of squares of shared-Gram fits by Gram algebra (the C5 fold
+ * scores, backend/sglm.py:150-184 neg_mse / R^2 over a mask, without forming X beta):
+ * ss[q] = max(yy[q] - 2 beta_f . c[cidx[q]] + beta_f^T G beta_f, 0) for f = fits[q], with
+ * beta [*][P] float64 (augmented: intercept at p, pa = p + 1 coordinates used), G the f32 upper
+ * triangle H[grp_slot[g]] (P x P) of the group g holding q (fits sorted by group: group g is
+ * q in [grp_off[g], grp_off[g+1]), at most max_per_grp), c [*][P] float64 = X~^T (m y), yy =
+ * sum m y^2.  Float64 arithmetic; work: sglm_gram_ss_work_bytes(pa, nfit). */
+size_t sglm_gram_ss_work_bytes(int32_t pa, int32_t nfit);
+int sglm_gram_ss(const float* H, int32_t P, int32_t pa, const int32_t* grp_slot,
+                 const int32_t* grp_off, int32_t ngrp, int32_t max_per_grp, const int32_t* fits,
+                 int32_t nfit, const double* beta, const double* c, const int32_t* cidx,
+                 const double* yy, double* ss, void* work, sglm_stream_t stream);
+
 /* Same contraction from the f32 design (v_mfma_f32_32x32x2_f32, exact f32 products) for
  * designs that are not bf16-exact, where the Gram itself must be accurate (coordinate
  * descent, Gaussian closed forms).  128-tiles; work sized by sglm_syrk_work_bytes. */

@@ -451,3 +451,140 @@ extern "C" int sglm_enet_cd_shared(const double* Q, int32_t p, const int32_t* qi
                                                                 tol, w, sweeps);
     return check_launch("enet_cd_shared_kernel");
 }
+
+// ---- fold scores of shared-Gram fits by Gram algebra --------------------------------------
+// ss[f] = sum over the rows of a mask of (y - x~ beta_f)^2 = yy[f] - 2 beta_f.c[cidx[f]]
+//         + beta_f^T G beta_f, with G the mask's augmented Gram (f32 upper triangle, exact
+// integer counts for 0/1 designs), beta_f float64 over the pa = p + 1 active coordinates.
+// Quadratic part: workgroup = (row block of 32 rows of G, chunk of 256 fits of one Gram),
+// thread = fit; the block's G rows and the fits' beta columns are staged through LDS 32
+// columns at a time (beta rows loaded coalesced, read transposed), 32 float64 row
+// accumulators per thread; partials per row block, summed in a fixed order with the linear
+// term by one wave per fit.
+namespace sglm {
+namespace {
+constexpr int kQR = 32;           // G rows per workgroup
+constexpr int kQF = 256;          // fits per workgroup (one per thread)
+constexpr int kQC = 32;           // columns per staging step
+
+__global__ void __launch_bounds__(kQF) gram_quad_kernel(const float* __restrict__ H, int32_t P,
+                                                        int32_t pa,
+                                                        const int32_t* __restrict__ grp_slot,
+                                                        const int32_t* __restrict__ grp_off,
+                                                        const int32_t* __restrict__ fits,
+                                                        const double* __restrict__ beta,
+                                                        double* __restrict__ part,
+                                                        int32_t nfit) {
+    __shared__ float g[kQR][kQC + 1];
+    __shared__ double bt[kQF][kQC + 1];
+    __shared__ double brow[kQF][kQR + 1];
+    const int tid = threadIdx.x;
+    const int grp = blockIdx.z;
+    const int f0 = grp_off[grp] + blockIdx.y * kQF;
+    const int f1 = grp_off[grp + 1];
+    if (f0 >= f1) return;
+    const int nf = min(kQF, f1 - f0);
+    const int a0 = blockIdx.x * kQR;
+    if (a0 >= pa) return;
+    const float* G = H + (int64_t)grp_slot[grp] * P * P;
+    const bool on = tid < nf;
+    const int fit = on ? fits[f0 + tid] : 0;
+    // this block's beta rows (coordinates a0 .. a0 + 31 of every fit), read transposed
+    for (int e = tid; e < nf * kQR; e += kQF) {
+        const int ff = e / kQR, j = e - ff * kQR;
+        const int a = a0 + j;
+        brow[ff][j] = a < pa ? beta[(int64_t)fits[f0 + ff] * P + a] : 0.0;
+    }
+    double acc[kQR];
+#pragma unroll
+    for (int j = 0; j < kQR; ++j) acc[j] = 0.0;
+    for (int c0 = a0; c0 < pa; c0 += kQC) {
+        __syncthreads();
+        for (int e = tid; e < kQR * kQC; e += kQF) {
+            const int r = e / kQC, c = e - r * kQC;
+            const int a = a0 + r, b = c0 + c;
+            // strictly upper part only (b > a); the diagonal is added separately
+            g[r][c] = (a < pa && b < pa && b > a) ? G[(int64_t)a * P + b] : 0.0f;
+        }
+        for (int e = tid; e < nf * kQC; e += kQF) {
+            const int ff = e / kQC, c = e - ff * kQC;
+            const int b = c0 + c;
+            bt[ff][c] = b < pa ? beta[(int64_t)fits[f0 + ff] * P + b] : 0.0;
+        }
+        __syncthreads();
+        if (on) {
+#pragma unroll 4
+            for (int c = 0; c < kQC; ++c) {
+                const double bv = bt[tid][c];
+#pragma unroll
+                for (int j = 0; j < kQR; ++j) acc[j] = fma((double)g[j][c], bv, acc[j]);
+            }
+        }
+    }
+    if (!on) return;
+    double q = 0.0;
+#pragma unroll
+    for (int j = 0; j < kQR; ++j) {
+        const int a = a0 + j;
+        const double ba = brow[tid][j];
+        const double gaa = a < pa ? (double)G[(int64_t)a * P + a] : 0.0;
+        q += ba * (gaa * ba + 2.0 * acc[j]);
+    }
+    part[(int64_t)blockIdx.x * nfit + (f0 + tid)] = q;
+    (void)fit;
+}
+
+// one wave per fit: ss = max(yy - 2 beta.c + sum over row blocks of the quadratic part, 0)
+__global__ void __launch_bounds__(256) gram_quad_finish(const double* __restrict__ part,
+                                                        int32_t nblk, int32_t nfit,
+                                                        const int32_t* __restrict__ fits,
+                                                        const double* __restrict__ beta,
+                                                        const double* __restrict__ c,
+                                                        const int32_t* __restrict__ cidx,
+                                                        const double* __restrict__ yy,
+                                                        int32_t P, int32_t pa,
+                                                        double* __restrict__ ss) {
+    const int w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (w >= nfit) return;
+    const double* bf = beta + (int64_t)fits[w] * P;
+    const double* cf = c + (int64_t)cidx[w] * P;
+    double lin = 0.0;
+    for (int a = lane; a < pa; a += 64) lin = fma(bf[a], cf[a], lin);
+    for (int o = 32; o > 0; o >>= 1) lin += __shfl_xor(lin, o, 64);
+    if (lane == 0) {
+        double q = 0.0;
+        for (int k = 0; k < nblk; ++k) q += part[(int64_t)k * nfit + w];
+        const double v = yy[w] - 2.0 * lin + q;
+        ss[w] = v > 0.0 ? v : 0.0;
+    }
+}
+}  // namespace
+}  // namespace sglm
+
+extern "C" size_t sglm_gram_ss_work_bytes(int32_t pa, int32_t nfit) {
+    return (size_t)((pa + kQR - 1) / kQR) * (size_t)nfit * sizeof(double);
+}
+
+extern "C" int sglm_gram_ss(const float* H, int32_t P, int32_t pa, const int32_t* grp_slot,
+                            const int32_t* grp_off, int32_t ngrp, int32_t max_per_grp,
+                            const int32_t* fits, int32_t nfit, const double* beta,
+                            const double* c, const int32_t* cidx, const double* yy, double* ss,
+                            void* work, sglm_stream_t stream) {
+    if (nfit <= 0) return SGLM_OK;
+    if (!H || !grp_slot || !grp_off || !fits || !beta || !c || !cidx || !yy || !ss || !work ||
+        pa < 1 || pa > P || ngrp < 1 || ngrp > 65535 || max_per_grp < 1) {
+        set_error("sglm_gram_ss: bad args");
+        return SGLM_EINVAL;
+    }
+    hipStream_t s = as_stream(stream);
+    const int nblk = (pa + kQR - 1) / kQR;
+    dim3 grid((unsigned)nblk, (unsigned)((max_per_grp + kQF - 1) / kQF), (unsigned)ngrp);
+    gram_quad_kernel<<<grid, kQF, 0, s>>>(H, P, pa, grp_slot, grp_off, fits, beta,
+                                          (double*)work, nfit);
+    int st = check_launch("gram_quad_kernel");
+    if (st) return st;
+    gram_quad_finish<<<(unsigned)((nfit + 3) / 4), 256, 0, s>>>((const double*)work, nblk, nfit,
+                                                                fits, beta, c, cidx, yy, P, pa,
+                                                                ss);
+    return check_launch("gram_quad_finish");
+}

@@ -50,6 +50,9 @@ SIGNATURES = {
     "sglm_enet_cd_fits_per_wg": (_i32, [_i32]),
     "sglm_enet_cd_grouped": (C.c_int, [_vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _i32,
                                        C.c_double, _vp, _vp, _vp]),
+    "sglm_gram_ss_work_bytes": (_sz, [_i32, _i32]),
+    "sglm_gram_ss": (C.c_int, [_vp, _i32, _i32, _vp, _vp, _i32, _i32, _vp, _i32, _vp, _vp, _vp,
+                               _vp, _vp, _vp, _vp]),
     "sglm_syrk_f32": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
     "sglm_chol_work_bytes": (_sz, [_i32, _i32]),
     "sglm_chol_solve_ex": (C.c_int, [_vp, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _i32,

@@ -112,7 +112,7 @@ def xty(prob: E.Problem, pairs: Sequence[tuple]) -> torch.Tensor:
 
 
 def solve(prob: E.Problem, grams: SharedGrams, fits: Sequence[dict], c: torch.Tensor,
-          cidx: Sequence[int]):
+          cidx: Sequence[int], stats: Optional[dict] = None):
     """ElasticNet per fit dict {mask, alpha, l1_ratio, fit_intercept, max_iter} with
     c[cidx[f]] = X^T(m y) of its (response, mask).  Returns (w [B][p] f64, b [B] f64,
     sweeps [B] int, converged [B] bool) as host arrays."""
@@ -152,6 +152,10 @@ def solve(prob: E.Problem, grams: SharedGrams, fits: Sequence[dict], c: torch.Te
     sw = torch.empty(B, dtype=torch.int32, device=dev)
     max_sweeps = int(max(max(int(f["max_iter"]) for f in fits), 10000))
     fpw = int(_lib.query("sglm_enet_cd_fits_per_wg", p))
+    rec = stats is not None and stats.get("record")
+    if rec:                          # the roofline times the CD kernel alone (bench.py)
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
     if fpw >= 2:
         # fits sharing a Q go to the same workgroups, fpw at a time (padding slots -1)
         wg_f, wg_q = [], []
@@ -171,11 +175,32 @@ def solve(prob: E.Problem, grams: SharedGrams, fits: Sequence[dict], c: torch.Te
         qidx_d = torch.from_numpy(qidx).to(dev)
         _lib.call("sglm_enet_cd_shared", E._p(grams.Qt), p, E._p(qidx_d), B, E._p(q),
                   E._p(l1), E._p(l2), max_sweeps, CD_TOL, E._p(w), E._p(sw), E._stream())
+    if rec:
+        ev[1].record()
     fi = torch.from_numpy(np.array([bool(f["fit_intercept"]) for f in fits])).to(dev)
     n = torch.from_numpy(cnt).to(dev)
     b = torch.where(fi & (n > 0), (cpv - (gv * w).sum(1)) / n.clamp_min(1), 0.0)
     swh = sw.cpu().numpy()
+    if rec:
+        # algorithmic work of cyclic CD on a shared Q: every coordinate step reads one row of
+        # Q and updates the running gradient, 2p flop, so 2p^2 per sweep per fit (float64)
+        stats["cd_ms"] = stats.get("cd_ms", 0.0) + ev[0].elapsed_time(ev[1])
+        stats["cd_flop"] = stats.get("cd_flop", 0.0) + 2.0 * p * p * float(np.sum(swh))
     return w.cpu().numpy(), b.cpu().numpy(), swh, swh < max_sweeps
+
+
+def _mask_sum_y2(prob: E.Problem) -> np.ndarray:
+    """[F][R] float64 sum over each mask of m y^2 (sglm_mask_stats with a zero shift)."""
+    Y = prob.y64_rows()
+    F_, R = prob.M.shape[0], Y.shape[0]
+    n = prob.design.n
+    K0 = torch.zeros(R, dtype=torch.float64, device=Y.device)
+    out = torch.empty((R, F_, 5), dtype=torch.float64, device=Y.device)
+    work = torch.empty(_lib.query("sglm_mask_stats_work_bytes", F_, R, n), dtype=torch.uint8,
+                       device=Y.device)
+    _lib.call("sglm_mask_stats", E._p(prob.M), prob.M.shape[1], F_, E._p(Y), R, n, E._p(K0),
+              -1.0, E._p(out), E._p(work), E._stream())
+    return out[:, :, 2].t().cpu().numpy()
 
 
 def cv_enet_path(X, Y, cv_idx, alphas: Sequence[float], l1_ratio: float = 0.5,
@@ -235,31 +260,45 @@ def cv_enet_path(X, Y, cv_idx, alphas: Sequence[float], l1_ratio: float = 0.5,
                 fits.append({"mask": m, "alpha": float(al), "l1_ratio": float(l1_ratio),
                              "fit_intercept": fit_intercept, "max_iter": max_iter})
                 keys.append((r, j, k))
-    w, b, sw, conv = solve(prob, grams, fits, c, [ci[(r, f["mask"])] for (r, _, _), f in zip(keys, fits)])
-    # ---- scores from Gram algebra: SS(mask) = y'My - 2 beta'c + beta' G beta (augmented)
-    Md = prob.M[:, :n].to(torch.float64)
-    y2t = (prob.Yd64 * prob.Yd64).t().contiguous()              # R x n (a GEMM with a long
-    yyh = (Md @ y2t.t()).cpu().numpy()                           # K picks a fast kernel this
-    del y2t                                                      # way): F x R, sum m y^2
-    del Md
+    w, b, sw, conv = solve(prob, grams, fits, c,
+                           [ci[(r, f["mask"])] for (r, _, _), f in zip(keys, fits)], stats)
+    # ---- scores from Gram algebra: SS(mask) = y'My - 2 beta'c + beta' G beta (augmented),
+    # sum m y^2 per (mask, response) from the mask-statistics kernel, the rest from
+    # sglm_gram_ss over every (split fit, train / test mask) pair, grouped by mask
+    yyh = _mask_sum_y2(prob)                                     # F x R
     cnt = np.array([float(prob.mask_count(m)) for m in range(len(masks))])
     c_p = c[:, p].cpu().numpy()                                  # sum m y per (r, m) pair
     beta = np.zeros((len(fits), design.P))
     beta[:, :p] = w
     beta[:, p] = b
     betad = torch.from_numpy(beta).to(dev)
-    ss = np.zeros((len(fits), 2))                                # [train, test] per split fit
     kk = np.array([k for (_, _, k) in keys])
     rr = np.array([r for (r, _, _) in keys])
+    q_fit, q_cidx, q_yy, q_side, grp_off, grp_slot = [], [], [], [], [0], []
     for k in range(K):
         rows = np.flatnonzero(kk == k)
-        bt = betad[torch.from_numpy(rows).to(dev)]
         for side, mt in ((0, 2 * k), (1, 2 * k + 1)):
-            quad = ((bt @ grams.sym(mt)) * bt).sum(1)
-            cidx_t = torch.from_numpy(np.array([ci[(r, mt)] for r in rr[rows]])).to(dev)
-            lin = (bt * c[cidx_t]).sum(1)
-            yv = torch.from_numpy(yyh[mt, rr[rows]]).to(dev)
-            ss[rows, side] = (yv - 2 * lin + quad).clamp_min(0).cpu().numpy()
+            q_fit.append(rows)
+            q_cidx.append(np.array([ci[(r, mt)] for r in rr[rows]]))
+            q_yy.append(yyh[mt, rr[rows]])
+            q_side.append(np.full(rows.size, side))
+            grp_off.append(grp_off[-1] + rows.size)
+            grp_slot.append(grams.slot[mt])
+    ss = np.zeros((len(fits), 2))                                # [train, test] per split fit
+    if grp_slot:
+        qf = np.concatenate(q_fit)
+        ssd = torch.empty(qf.size, dtype=torch.float64, device=dev)
+        work = torch.empty(_lib.query("sglm_gram_ss_work_bytes", p + 1, int(qf.size)),
+                           dtype=torch.uint8, device=dev)
+        ints = torch.from_numpy(np.concatenate([qf, np.concatenate(q_cidx), grp_off, grp_slot])
+                                .astype(np.int32)).to(dev)
+        nq, ng = int(qf.size), len(grp_slot)
+        yyd = torch.from_numpy(np.concatenate(q_yy)).to(dev)
+        _lib.call("sglm_gram_ss", E._p(grams.H), design.P, p + 1, E._p(ints[2 * nq + ng + 1:]),
+                  E._p(ints[2 * nq:]), ng, int(np.max(np.diff(grp_off))), E._p(ints), nq,
+                  E._p(betad), E._p(c), E._p(ints[nq:]), E._p(yyd), E._p(ssd), E._p(work),
+                  E._stream())
+        ss[qf, np.concatenate(q_side)] = ssd.cpu().numpy()
     kpos = {key: i for i, key in enumerate(keys)}
     out = []
     for r in range(R):

@@ -252,3 +252,31 @@ def test_chain_graph_cache_is_bounded_and_survives_freed_buffers(engine):
     glm.fit(X, y)
     c, b = glm_ref.fit_tweedie_newton(X, y, 0.01, 1.0)
     assert rel(glm.coef_, c) < TOL_POIS
+
+
+def test_predict_reuses_the_packed_design_until_x_changes(engine):
+    """predict / score on the same array reuse its packed design (content digest), an array
+    changed in place is packed again (sklearn semantics), and a different estimator shares it."""
+    import time
+    import sglm
+    from sglm_hip import estimators as est, synth
+    s = synth.make(N=100_000, m=25, L=10, family="poisson", rho=0.02, seed=0)
+    X = s.dense_X()
+    est.clear_design_cache()
+    glm = sglm.GLM("Poisson", alpha=0.01)
+    glm.fit(X, s.y)
+    t0 = time.perf_counter()
+    p1 = glm.model.predict(X)
+    t1 = time.perf_counter()
+    p2 = glm.model.predict(X)
+    t2 = time.perf_counter()
+    print(f"predict: first {1e3 * (t1 - t0):.1f} ms, cached {1e3 * (t2 - t1):.1f} ms")
+    np.testing.assert_array_equal(p1, p2)
+    assert len(est._DESIGN_CACHE) >= 1
+    X[:, 0] = 1.0 - X[:, 0]                       # changed in place: packed again
+    p3 = glm.model.predict(X)
+    ref = np.exp(X @ glm.coef_ + glm.intercept_)
+    assert np.max(np.abs(p3 - ref) / ref) < 1e-5
+    assert np.max(np.abs(p3 - p1)) > 0
+    est.clear_design_cache()
+    assert len(est._DESIGN_CACHE) == 0
