@@ -679,6 +679,145 @@ __global__ void __launch_bounds__(kCT) chol_inv_level_lds_kernel(const float* __
     }
 }
 
+// The same level on 128 x 128 output tiles (levels with s >= 128 when enough fits fill the
+// chip): four waves of 64 x 64 (2 x 2 quadrants of v_mfma_f32_32x32x2f32), K in blocks of
+// 16 staged through double-buffered LDS (37 KB: static LDS stays under 64 KB) -- half the
+// operand traffic per flop of the 64 x 64 tile.  The triangles are bounded at 64-block granularity as in the 64 x 64 kernel: operand
+// elements of M in a strictly lower 64-block (never written) are zeroed while staging.
+constexpr int kT2 = 128;
+constexpr int kKB2 = 16;            // K block
+constexpr int kLA2 = 20;            // A [128][16] row stride (floats): 8 lanes of a b128 read
+                                    // on disjoint banks
+constexpr int kLB2 = 136;           // B [16][128] row stride: the k-halves on disjoint banks
+template <int STEP>
+__global__ void __launch_bounds__(kCT) chol_inv_level128_kernel(const float* __restrict__ Hall,
+                                                                float* __restrict__ Mall,
+                                                                float* __restrict__ Tall,
+                                                                int32_t P, int32_t s,
+                                                                const int32_t* __restrict__ fits,
+                                                                int64_t tcap) {
+    __shared__ __attribute__((aligned(16))) float sa[2][kT2 * kLA2];
+    __shared__ __attribute__((aligned(16))) float sb[2][kKB2 * kLB2];
+    const int fit = fits[blockIdx.y];
+    const float* H = Hall + (int64_t)fit * P * P;
+    float* M = Mall + (int64_t)fit * P * P;
+    const int nsb = s / kT2;
+    int t = blockIdx.x;
+    const int pair = t / (nsb * nsb);
+    t -= pair * nsb * nsb;
+    const int ti = t / nsb, tj = t - ti * nsb;
+    const int a0 = 2 * s * pair, c0 = a0 + s;
+    const int cs = min(s, P - c0);
+    if (cs <= 0 || tj * kT2 >= cs) return;
+    float* T = Tall + (int64_t)blockIdx.y * tcap + (int64_t)pair * s * s;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r32 = lane & 31, kh = lane >> 5;
+    const int wr = wave >> 1, wc = wave & 1;
+    const float* ga;
+    const float* gb;
+    int64_t ldb;
+    int klo, khi;
+    if (STEP == 0) {                                   // A = U[a0 + i][c0 + k], B = M[c0 + k][c0 + j]
+        ga = H + (int64_t)(a0 + ti * kT2) * P + c0;
+        gb = M + (int64_t)c0 * P + c0 + tj * kT2;
+        ldb = P;
+        klo = 0;
+        khi = (tj + 1) * kT2;
+    } else {                                           // A = M[a0 + i][a0 + k], B = T[k][j]
+        ga = M + (int64_t)(a0 + ti * kT2) * P + a0;
+        gb = T + tj * kT2;
+        ldb = s;
+        klo = ti * kT2;
+        khi = s;
+    }
+    // staging shares: A row tid >> 1, k 8 (tid & 1) .. +7; B row k = tid >> 4, columns
+    // 8 (tid & 15) .. +7
+    const int ar = tid >> 1, ak = 8 * (tid & 1);
+    const int bk = tid >> 4, bj = 8 * (tid & 15);
+    f32x4 ra[2], rb[2];
+    auto gload = [&](int kb) {
+        const float* pa = ga + (int64_t)ar * P + kb + ak;
+        const float* pb = gb + (int64_t)(kb + bk) * ldb + bj;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            ra[u] = *reinterpret_cast<const f32x4*>(pa + 4 * u);
+            rb[u] = *reinterpret_cast<const f32x4*>(pb + 4 * u);
+        }
+        if (STEP == 1) {
+            // A = M_A row ti*128 + ar, columns kb + ak + ..: zero where the column's 64-block
+            // lies left of the row's (a strictly lower 64-block of M)
+            const int rowb = (ti * kT2 + ar) >> 6;
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                if (((kb + ak + 4 * u) >> 6) < rowb) ra[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        } else {
+            // B = M_C row kb + bk, columns tj*128 + bj + ..: zero below the 64-block diagonal
+            const int rowb = (kb + bk) >> 6;
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                if (((tj * kT2 + bj + 4 * u) >> 6) < rowb) rb[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    auto sstore = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            *reinterpret_cast<f32x4*>(&sa[buf][ar * kLA2 + ak + 4 * u]) = ra[u];
+            *reinterpret_cast<f32x4*>(&sb[buf][bk * kLB2 + bj + 4 * u]) = rb[u];
+        }
+    };
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+        for (int qj = 0; qj < 2; ++qj) acc[qi][qj] = (f32x16){};
+    gload(klo);
+    sstore(0);
+    __syncthreads();
+    int cur = 0;
+    for (int kb = klo; kb < khi; kb += kKB2) {
+        const bool more = kb + kKB2 < khi;
+        if (more) gload(kb + kKB2);
+#pragma unroll
+        for (int kk = 0; kk < kKB2 / 8; ++kk) {
+            f32x4 a[2];
+#pragma unroll
+            for (int qi = 0; qi < 2; ++qi)
+                a[qi] = *reinterpret_cast<const f32x4*>(
+                    &sa[cur][(wr * 64 + qi * 32 + r32) * kLA2 + 4 * kh + 8 * kk]);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                float b[2];
+#pragma unroll
+                for (int qj = 0; qj < 2; ++qj)
+                    b[qj] = sb[cur][(4 * kh + 8 * kk + u) * kLB2 + wc * 64 + qj * 32 + r32];
+#pragma unroll
+                for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+                    for (int qj = 0; qj < 2; ++qj)
+                        acc[qi][qj] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[qi][u], b[qj],
+                                                                           acc[qi][qj], 0, 0, 0);
+            }
+        }
+        if (more) sstore(cur ^ 1);
+        __syncthreads();
+        cur ^= 1;
+    }
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+        for (int qj = 0; qj < 2; ++qj) {
+            const int i0 = ti * kT2 + wr * 64 + qi * 32, j0 = tj * kT2 + wc * 64 + qj * 32;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int i = i0 + (q & 3) + 8 * (q >> 2) + 4 * kh, j = j0 + r32;
+                if (STEP == 0)
+                    T[(int64_t)i * s + j] = acc[qi][qj][q];
+                else
+                    M[(int64_t)(a0 + i) * P + c0 + j] = -acc[qi][qj][q];
+            }
+        }
+}
+
 // Solves on explicit inverses.  Tile t = rows [start, start + cnt) of the fit list (cnt <= 32,
 // one factor: slot fsrc[start]); blockIdx.x = a 32-wide output column block; the 4 waves split
 // K and reduce through LDS.  SECOND = false: Y[q][j] = sum_k G[q][k] M[k][j] with G = rscale *
@@ -844,6 +983,14 @@ static bool inv_lds() {
         return !(e && e[0] == '0');
     }();
     return v;
+}
+
+// 128 x 128 inversion tiles on a level whose 128-tile grid has at least SGLM_INV128_WG
+// workgroups (0 = never; read per chain capture): fewer leave the chip underfilled.
+static bool inv128(int64_t wgs) {
+    const char* e = getenv("SGLM_INV128_WG");
+    const int64_t mn = e ? atoll(e) : 512;
+    return mn > 0 && wgs >= mn;
 }
 
 // The two-stage update measured slower on the box (16.5 vs 13.3 us per launch at 3 fits), so
@@ -1019,7 +1166,12 @@ static int factor_inv_launch(float* H, float* Minv, int32_t P, const int32_t* fi
         const int pairs = (P - sz + 2 * sz - 1) / (2 * sz);
         const int sb = sz / kNB;
         const dim3 grid((unsigned)(pairs * sb * sb), (unsigned)n);
-        if (inv_lds()) {
+        const int sb2 = sz / kT2;
+        if (sz >= kT2 && sz % kT2 == 0 && P % kT2 == 0 && inv128((int64_t)pairs * sb2 * sb2 * n)) {
+            const dim3 grid2((unsigned)(pairs * sb2 * sb2), (unsigned)n);
+            chol_inv_level128_kernel<0><<<grid2, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
+            chol_inv_level128_kernel<1><<<grid2, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
+        } else if (inv_lds()) {
             chol_inv_level_lds_kernel<0><<<grid, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
             chol_inv_level_lds_kernel<1><<<grid, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
         } else if (pipe) {

@@ -38,6 +38,7 @@ __device__ __forceinline__ uint64_t lanemask_lt(int lane) {
 struct Ord {          // ordering summary of a row range (valid rows only)
     uint64_t f1, f2, l1, l2;
     long long cnt;
+    long long heads;  // key changes within the range, its first valid row counted as one
     int ok;
 };
 
@@ -51,6 +52,7 @@ __device__ __forceinline__ Ord ord_comb(const Ord& a, const Ord& b) {
     Ord r;
     r.f1 = a.f1; r.f2 = a.f2; r.l1 = b.l1; r.l2 = b.l2;
     r.cnt = a.cnt + b.cnt;
+    r.heads = a.heads + b.heads - ((a.l1 == b.f1 && a.l2 == b.f2) ? 1 : 0);
     r.ok = a.ok && b.ok && lex_le(a.l1, a.l2, b.f1, b.f2);
     return r;
 }
@@ -63,7 +65,7 @@ __global__ void __launch_bounds__(kDmT) group_order_kernel(const double* __restr
                                                            Ord* __restrict__ part) {
     __shared__ Ord sh[kDmT];
     const int64_t r0 = ((int64_t)blockIdx.x * kDmT + threadIdx.x) * kOrdRows;
-    Ord o = {0, 0, 0, 0, 0, 1};
+    Ord o = {0, 0, 0, 0, 0, 0, 1};
     for (int j = 0; j < kOrdRows; ++j) {
         const int64_t i = r0 + j;
         if (i >= n) break;
@@ -71,7 +73,7 @@ __global__ void __launch_bounds__(kDmT) group_order_kernel(const double* __restr
         const bool v = !isnan(a) && !isnan(b);
         valid[i] = v;
         if (!v) continue;
-        Ord e = {key_bits(a), key_bits(b), key_bits(a), key_bits(b), 1, 1};
+        Ord e = {key_bits(a), key_bits(b), key_bits(a), key_bits(b), 1, 1, 1};
         o = ord_comb(o, e);
     }
     sh[threadIdx.x] = o;
@@ -83,14 +85,21 @@ __global__ void __launch_bounds__(kDmT) group_order_kernel(const double* __restr
     }
 }
 
+// Over the workgroup summaries in order: the verdict (ordered?, valid rows, groups) and per
+// block the exclusive offsets of its valid rows and group heads in the compacted order and
+// the last valid key before it (for the head test of its first valid row).
+struct BlockOff { long long v, h; uint64_t p1, p2; int has; };
+
 __global__ void __launch_bounds__(kDmT) group_order_final_kernel(const Ord* __restrict__ part,
                                                                  int64_t nb,
-                                                                 long long* __restrict__ res) {
+                                                                 long long* __restrict__ res,
+                                                                 BlockOff* __restrict__ off) {
     __shared__ Ord sh[kDmT];
     const int64_t per = (nb + kDmT - 1) / kDmT;
     const int64_t b0 = (int64_t)threadIdx.x * per;
-    Ord o = {0, 0, 0, 0, 0, 1};
-    for (int64_t b = b0; b < b0 + per && b < nb; ++b) o = ord_comb(o, part[b]);
+    const int64_t b1 = b0 + per < nb ? b0 + per : nb;
+    Ord o = {0, 0, 0, 0, 0, 0, 1};
+    for (int64_t b = b0; b < b1; ++b) o = ord_comb(o, part[b]);
     sh[threadIdx.x] = o;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -98,7 +107,123 @@ __global__ void __launch_bounds__(kDmT) group_order_final_kernel(const Ord* __re
         for (int t = 1; t < kDmT; ++t) r = ord_comb(r, sh[t]);
         res[0] = r.ok;
         res[1] = r.cnt;
+        res[2] = r.heads;
     }
+    // exclusive prefix of the runs before this thread's, then walk the run
+    Ord pre = {0, 0, 0, 0, 0, 0, 1};
+    for (int t = 0; t < (int)threadIdx.x; ++t) pre = ord_comb(pre, sh[t]);
+    for (int64_t b = b0; b < b1; ++b) {
+        const Ord& cur = part[b];
+        BlockOff bo;
+        bo.v = pre.cnt;
+        bo.h = pre.heads;
+        bo.has = pre.cnt > 0;
+        bo.p1 = pre.l1;
+        bo.p2 = pre.l2;
+        off[b] = bo;
+        pre = ord_comb(pre, cur);
+    }
+}
+
+// Stable compaction of an ORDERED key sequence: perm = the valid rows in row order, seg = the
+// positions in perm where the key changes (group starts); thread = 16 consecutive rows,
+// in-block prefix counts and "last valid key before me" by Hillis-Steele passes in LDS.
+__global__ void __launch_bounds__(kDmT) group_compact_kernel(const double* __restrict__ key,
+                                                             const double* __restrict__ key2,
+                                                             int64_t n,
+                                                             const BlockOff* __restrict__ off,
+                                                             int64_t* __restrict__ perm,
+                                                             int64_t* __restrict__ seg) {
+    __shared__ int cv[kDmT], ch[kDmT], hv[kDmT];
+    __shared__ uint64_t k1s[kDmT], k2s[kDmT];
+    const int tid = threadIdx.x;
+    const BlockOff bo = off[blockIdx.x];
+    const int64_t r0 = ((int64_t)blockIdx.x * kDmT + tid) * kOrdRows;
+    uint64_t a1[kOrdRows], a2[kOrdRows];
+    uint32_t vm = 0;
+    int nv = 0;
+    uint64_t l1 = 0, l2 = 0;
+#pragma unroll
+    for (int j = 0; j < kOrdRows; ++j) {
+        const int64_t i = r0 + j;
+        a1[j] = a2[j] = 0;
+        if (i < n) {
+            const double x = key[i], y = key2 ? key2[i] : 0.0;
+            if (!isnan(x) && !isnan(y)) {
+                vm |= 1u << j;
+                a1[j] = key_bits(x);
+                a2[j] = key_bits(y);
+                l1 = a1[j];
+                l2 = a2[j];
+                ++nv;
+            }
+        }
+    }
+    // nearest valid key before this thread's run: inclusive scan of (has, last key), shifted
+    hv[tid] = nv > 0;
+    k1s[tid] = l1;
+    k2s[tid] = l2;
+    cv[tid] = nv;
+    __syncthreads();
+    for (int o = 1; o < kDmT; o <<= 1) {
+        int h = 0, c = 0;
+        uint64_t x1 = 0, x2 = 0;
+        const bool take = tid >= o;
+        if (take) { h = hv[tid - o]; x1 = k1s[tid - o]; x2 = k2s[tid - o]; c = cv[tid - o]; }
+        __syncthreads();
+        if (take) {
+            if (!hv[tid] && h) { hv[tid] = 1; k1s[tid] = x1; k2s[tid] = x2; }
+            cv[tid] += c;
+        }
+        __syncthreads();
+    }
+    // exclusive: the values of thread tid - 1 (block prefix for thread 0)
+    int has_prev = tid > 0 ? hv[tid - 1] : 0;
+    uint64_t p1 = tid > 0 ? k1s[tid - 1] : 0, p2 = tid > 0 ? k2s[tid - 1] : 0;
+    if (!has_prev && bo.has) { has_prev = 1; p1 = bo.p1; p2 = bo.p2; }
+    const int vpre = tid > 0 ? cv[tid - 1] : 0;
+    // heads of this thread's run
+    int nh = 0;
+    {
+        int hp = has_prev;
+        uint64_t q1 = p1, q2 = p2;
+#pragma unroll
+        for (int j = 0; j < kOrdRows; ++j) {
+            if (vm >> j & 1u) {
+                if (!hp || a1[j] != q1 || a2[j] != q2) ++nh;
+                hp = 1; q1 = a1[j]; q2 = a2[j];
+            }
+        }
+    }
+    __syncthreads();
+    ch[tid] = nh;
+    __syncthreads();
+    for (int o = 1; o < kDmT; o <<= 1) {
+        const int c = tid >= o ? ch[tid - o] : 0;
+        __syncthreads();
+        ch[tid] += c;
+        __syncthreads();
+    }
+    const int hpre = tid > 0 ? ch[tid - 1] : 0;
+    int64_t pv = bo.v + vpre, ph = bo.h + hpre;
+    int hp = has_prev;
+    uint64_t q1 = p1, q2 = p2;
+#pragma unroll
+    for (int j = 0; j < kOrdRows; ++j) {
+        if (vm >> j & 1u) {
+            if (!hp || a1[j] != q1 || a2[j] != q2) seg[ph++] = pv;
+            perm[pv++] = r0 + j;
+            hp = 1; q1 = a1[j]; q2 = a2[j];
+        }
+    }
+}
+
+__global__ void group_finish2_kernel(int64_t* __restrict__ seg, const long long* __restrict__ res,
+                                     int64_t* __restrict__ counts) {
+    const long long m = res[1], g = res[2];
+    seg[g] = m;
+    counts[0] = m;
+    counts[1] = g;
 }
 
 // radix keys: the key's image, all ones when either key is NaN (those rows sort last)
@@ -447,6 +572,7 @@ inline unsigned groups_grid(int64_t n) {
 struct GroupWork {
     uint8_t* valid;
     Ord* part;
+    BlockOff* off;
     long long* res;
     int* nsel;
     uint64_t *ka, *kb;
@@ -475,6 +601,7 @@ GroupWork carve(void* work, int64_t n) {
     char* p = (char*)work;
     w.valid = (uint8_t*)p; p += align256((size_t)n);
     w.part = (Ord*)p; p += align256((size_t)(nb > 0 ? nb : 1) * sizeof(Ord));
+    w.off = (BlockOff*)p; p += align256((size_t)(nb > 0 ? nb : 1) * sizeof(BlockOff));
     w.res = (long long*)p; p += 256;
     w.nsel = (int*)p; p += 256;
     w.ka = (uint64_t*)p; p += align256((size_t)n * 8);
@@ -494,7 +621,8 @@ using namespace sglm;
 extern "C" size_t sglm_group_rows_work_bytes(int64_t n) {
     if (n < 0) n = 0;
     const int64_t nb = (n + (int64_t)kDmT * kOrdRows - 1) / ((int64_t)kDmT * kOrdRows);
-    return align256((size_t)n) + align256((size_t)(nb > 0 ? nb : 1) * sizeof(Ord)) + 512 +
+    return align256((size_t)n) + align256((size_t)(nb > 0 ? nb : 1) * sizeof(Ord)) +
+           align256((size_t)(nb > 0 ? nb : 1) * sizeof(BlockOff)) + 512 +
            4 * align256((size_t)n * 8) + cub_temp_bytes(n) + 256;
 }
 
@@ -518,10 +646,10 @@ extern "C" int sglm_group_rows(const double* key, const double* key2, int64_t n,
     GroupWork w = carve(work, n);
     const int64_t nb = (n + (int64_t)kDmT * kOrdRows - 1) / ((int64_t)kDmT * kOrdRows);
     group_order_kernel<<<(unsigned)nb, kDmT, 0, s>>>(key, key2, n, w.valid, w.part);
-    group_order_final_kernel<<<1, kDmT, 0, s>>>(w.part, nb, w.res);
+    group_order_final_kernel<<<1, kDmT, 0, s>>>(w.part, nb, w.res, w.off);
     int st = check_launch("group_order_kernel");
     if (st) return st;
-    long long res[2];
+    long long res[3];
     if (hipMemcpyAsync(res, w.res, sizeof(res), hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess) {
         set_error("sglm_group_rows: readback failed");
@@ -531,12 +659,10 @@ extern "C" int sglm_group_rows(const double* key, const double* key2, int64_t n,
     if (sorted_out) *sorted_out = (int32_t)res[0];
     size_t tb = w.temp_bytes;
     if (res[0]) {
-        // already grouped: the valid rows in row order (stable partition)
-        if (hipcub::DeviceSelect::Flagged(w.temp, tb, hipcub::CountingInputIterator<int64_t>(0),
-                                          w.valid, perm, w.nsel, (int)n, s) != hipSuccess) {
-            set_error("sglm_group_rows: DeviceSelect::Flagged failed");
-            return SGLM_EHIP;
-        }
+        // already grouped: the valid rows in row order and the group starts, one pass
+        group_compact_kernel<<<(unsigned)nb, kDmT, 0, s>>>(key, key2, n, w.off, perm, seg);
+        group_finish2_kernel<<<1, 1, 0, s>>>(seg, w.res, counts);
+        return check_launch("group_compact_kernel");
     } else {
         // stable LSD radix sort: by key2 first (if any), then by key; NaN rows last
         const unsigned g = rows_grid(n);

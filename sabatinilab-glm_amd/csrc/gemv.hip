@@ -330,6 +330,137 @@ xtr_bits_kernel(const u32x2* __restrict__ cbits, int64_t ld, int32_t P, int64_t 
     }
 }
 
+// Four panels per workgroup (256 predictors... 512 with kXT = 4: one panel per wave), the
+// three R pieces of the 32 fits staged through LDS once per 64-row step for all four waves:
+// R crosses L2 once per 512 predictors instead of once per 128 (xtr_bits_kernel), the A
+// operand (bit-planes) is per wave as before.  Same MFMA sequence per wave, so the same
+// partial sums bit for bit.  LDS: 2 buffers x 3 pieces x 32 fits x 144 B (a fit's 64-row
+// segment is 128 B; the 16-B pad spreads the 8 lanes of each ds_read_b128 pass over all banks).
+constexpr int kXW = 4;              // waves (panels) per workgroup
+constexpr int kRS = 144;            // LDS bytes per fit segment (128 + pad)
+
+__global__ void __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(1, 1)))
+xtr_bits4_kernel(const u32x2* __restrict__ cbits, int64_t ld, int32_t P, int64_t nblk,
+                 const __bf16* __restrict__ Rp, int32_t Bp, int32_t B, int32_t splits,
+                 float* __restrict__ part) {
+    __shared__ __attribute__((aligned(16))) char lds[2][3 * 32 * kRS];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int npan4 = P / (32 * kXT * kXW), ngrp = Bp / 32;
+    const int L = xcd_logical(blockIdx.x, npan4 * ngrp * splits);
+    const int pq = L % npan4, g = (L / npan4) % ngrp, z = L / (npan4 * ngrp);
+    const int pn = pq * kXW + wave;
+    const int64_t sps = (nblk + splits - 1) / splits;
+    const int64_t blk0 = (int64_t)z * sps;
+    const int64_t blk1 = min(blk0 + sps, nblk);
+    const int nsteps = blk1 > blk0 ? (int)(blk1 - blk0) : 0;
+    const uint64_t abase = (uint64_t)(cbits + blk0 * P);
+    const uint32_t avo = (uint32_t)((pn * (32 * kXT) + r) * 8);
+    // R staging: thread tid moves 16-B chunks c = tid + 256 j (j < 3) of the step's tile:
+    // piece c >> 8, fit (c >> 3) & 31, chunk c & 7 of that fit's 128-B row segment
+    const char* rb = reinterpret_cast<const char*>(Rp) + blk0 * 128;
+    const int64_t plane = (int64_t)Bp * ld * 2;
+    int64_t goff[3];
+    int loff[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const int c = tid + 256 * j;
+        const int pc = c >> 8, fit = (c >> 3) & 31, q = c & 7;
+        goff[j] = pc * plane + (int64_t)(g * 32 + fit) * ld * 2 + q * 16;
+        loff[j] = pc * 32 * kRS + fit * kRS + q * 16;
+    }
+    f32x16 ah[kXT], al[kXT];
+#pragma unroll
+    for (int m = 0; m < kXT; ++m) {
+        ah[m] = (f32x16){};
+        al[m] = (f32x16){};
+    }
+    if (nsteps > 0) {
+        u32x2 a0[kXT], a1[kXT];
+        u32x4 rv[3];
+        loadA<0>(a0, abase, avo);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) rv[j] = *reinterpret_cast<const u32x4*>(rb + goff[j]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int j = 0; j < 3; ++j) *reinterpret_cast<u32x4*>(&lds[0][loff[j]]) = rv[j];
+        __syncthreads();
+        // one step on A registers ac with the next step's loads into an: the loop is unrolled
+        // by two so the buffers never trade places through copies (an asm-loaded register
+        // copied before its s_waitcnt would copy stale data)
+        auto step = [&](u32x2 (&ac)[kXT], u32x2 (&an)[kXT], int s, int cur) {
+            const bool more = s + 1 < nsteps;
+            if (more) {
+                loadA<0>(an, abase + (uint64_t)(s + 1) * P * 8, avo);
+#pragma unroll
+                for (int j = 0; j < 3; ++j)
+                    rv[j] = *reinterpret_cast<const u32x4*>(rb + (int64_t)(s + 1) * 128 + goff[j]);
+            }
+#pragma unroll
+            for (int m = 0; m < kXT; ++m) asm volatile("" : "+v"(ac[m]));
+            const char* lb = &lds[cur][r * kRS + h * 16];
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) {
+                const bf16x8 b0 = __builtin_bit_cast(bf16x8,
+                    *reinterpret_cast<const u32x4*>(lb + 0 * 32 * kRS + 32 * ks));
+                const bf16x8 b1 = __builtin_bit_cast(bf16x8,
+                    *reinterpret_cast<const u32x4*>(lb + 1 * 32 * kRS + 32 * ks));
+                const bf16x8 b2 = __builtin_bit_cast(bf16x8,
+                    *reinterpret_cast<const u32x4*>(lb + 2 * 32 * kRS + 32 * ks));
+#pragma unroll
+                for (int m = 0; m < kXT; ++m) {
+                    const bf16x8 ax = frag_two(ac[m], ks, h);
+                    ah[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ax, b0, ah[m], 0, 0, 0);
+                    al[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ax, b1, al[m], 0, 0, 0);
+                    al[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ax, b2, al[m], 0, 0, 0);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            if (more) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+                for (int m = 0; m < kXT; ++m) asm volatile("" : "+v"(an[m]));
+#pragma unroll
+                for (int j = 0; j < 3; ++j)
+                    *reinterpret_cast<u32x4*>(&lds[cur ^ 1][loff[j]]) = rv[j];
+            }
+            __syncthreads();
+        };
+        int s = 0;
+        for (; s + 1 < nsteps; s += 2) {
+            step(a0, a1, s, 0);
+            step(a1, a0, s + 1, 1);
+        }
+        if (s < nsteps) step(a0, a1, s, 0);
+    }
+    const int f = g * 32 + r;
+    if (f < B) {
+        float* out = part + ((int64_t)z * B + f) * P + pn * (32 * kXT);
+#pragma unroll
+        for (int m = 0; m < kXT; ++m)
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                out[m * 32 + (j & 3) + 8 * (j >> 2) + 4 * h] = 0.5f * (ah[m][j] + al[m][j]);
+    }
+}
+
+// four-panel kernel when P % 512 == 0 unless SGLM_XTR4=0 (read per launch: tests switch it
+// inside one process).  C4 gradient at 120 fits: 1.87 -> 1.28 ms.
+static bool xtr4_on(int32_t P) {
+    const char* e = getenv("SGLM_XTR4");
+    return !(e && e[0] == '0') && P % (32 * kXT * kXW) == 0;
+}
+
+static void launch_xtr_bits(const u32x2* cbits, int64_t ld, int32_t P, int64_t nblk,
+                            const __bf16* Rp, int32_t Bp, int32_t B, int32_t splits, float* part,
+                            hipStream_t s) {
+    const unsigned tiles = (unsigned)((P / (32 * kXT)) * (Bp / 32) * splits);
+    if (xtr4_on(P))
+        xtr_bits4_kernel<<<tiles / kXW, 64 * kXW, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, B, splits,
+                                                          part);
+    else
+        xtr_bits_kernel<<<tiles, 64, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, B, splits, part);
+}
+
 // out[slots[f]][a] = sum over slabs z of part[z][f][a] (f = e / P), fixed order
 __global__ void __launch_bounds__(256) reduce_slabs_f64(const float* __restrict__ part,
                                                         int64_t len, int32_t nz, int32_t P,
@@ -430,9 +561,8 @@ int sglm_xtr_bits(const uint32_t* cbits, int64_t ld, int32_t P, int64_t n, const
                     s>>>(R, ld, B, Bp, nullptr, Rp);
     int st = check_launch("split3_kernel");
     if (st) return st;
-    xtr_bits_kernel<<<(unsigned)((P / (32 * kXT)) * (Bp / 32) * splits), 64, 0,
-                      s>>>(reinterpret_cast<const u32x2*>(cbits), ld, P, nblk, Rp, Bp, B, splits,
-                           part);
+    launch_xtr_bits(reinterpret_cast<const u32x2*>(cbits), ld, P, nblk, Rp, Bp, B, splits,
+                    part, s);
     st = check_launch("xtr_bits_kernel");
     if (st) return st;
     const int64_t len = (int64_t)B * P;
@@ -467,9 +597,8 @@ int sglm_xtr_bits_packed(const uint32_t* cbits, int64_t ld, int32_t P, int64_t n
     const int splits = xtr_bits_splits(P, B, ld / 64);
     hipStream_t s = as_stream(stream);
     float* part = reinterpret_cast<float*>(work);
-    xtr_bits_kernel<<<(unsigned)((P / (32 * kXT)) * (Bp / 32) * splits), 64, 0,
-                      s>>>(reinterpret_cast<const u32x2*>(cbits), ld, P, nblk,
-                           reinterpret_cast<const __bf16*>(Rp), Bp, B, splits, part);
+    launch_xtr_bits(reinterpret_cast<const u32x2*>(cbits), ld, P, nblk,
+                    reinterpret_cast<const __bf16*>(Rp), Bp, B, splits, part, s);
     int st = check_launch("xtr_bits_kernel");
     if (st) return st;
     const int64_t len = (int64_t)B * P;

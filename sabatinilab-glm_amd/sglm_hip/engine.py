@@ -46,7 +46,9 @@ X_BF16, X_F32 = 0, 1
 COL_PAD = 256
 ROW_PAD = 256
 ARMIJO_SIGMA = 2.0 ** -11      # sklearn _newton_solver.py:214
-# stopping rule: max|t d| <= tol * max(max_j<p |w_j|, STOP_SCALE_FLOOR) (tol = 1e-6)
+# stopping rule: max|t d| <= STOP_TOL * max(max_j<p |w_j|, STOP_SCALE_FLOOR) on the
+# coefficients, |t d| <= STOP_TOL on the intercept
+STOP_TOL = float(__import__("os").environ.get("SGLM_STOP_TOL", "1e-6"))
 STOP_SCALE_FLOOR = float(__import__("os").environ.get("SGLM_STOP_SCALE_FLOOR", "0.1"))
 # round-2 rule, for comparison runs: max|t d| <= tol * (1 + max|w|), intercept included
 STOP_LEGACY = __import__("os").environ.get("SGLM_STOP_RULE", "") == "legacy"
@@ -838,12 +840,13 @@ def syrk6_splits(wgs1: int, nsteps: int, nact: int, P: int, slots: int = 1024) -
     return best
 
 
-def irls(prob: Problem, reqs: List[FitReq], tol: float = 1e-6, stats: Optional[IrlsStats] = None,
-         bufs: Optional[_Buffers] = None):
+def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
+         stats: Optional[IrlsStats] = None, bufs: Optional[_Buffers] = None):
     """Run the batched damped-Newton (IRLS) solve; returns (results, final eta tensor)."""
     require_gpu()
     if not reqs:
         return [], None
+    tol = STOP_TOL if tol is None else float(tol)
     d = prob.design
     fam, power = reqs[0].family, float(reqs[0].power)
     if any(r.family != fam or float(r.power) != power for r in reqs):

@@ -241,6 +241,51 @@ def test_chol_solve_inv_vs_float64(engine, torch_mod, P, p, B):
         assert rel(x[q], want(src, q, sc)) < 1e-3, q
 
 
+@pytest.mark.parametrize("P,p,B", [(768, 700, 6), (2048, 1990, 5)])
+def test_chol_inv_many_fits_vs_float64(engine, torch_mod, P, p, B, monkeypatch):
+    """Factor + inverse chain on several fits of their own with the 128 x 128 inversion tiles
+    forced on every level s >= 128 (SGLM_INV128_WG=1: the ragged last level of P = 768, the
+    four 128-tile levels of P = 2048), each solve against its float64 solve."""
+    torch = torch_mod
+    monkeypatch.setenv("SGLM_INV128_WG", "1")
+    from sglm_hip import _lib
+    rng = np.random.default_rng(P + B)
+    H = np.zeros((B, P, P), np.float32)
+    for k in range(B):
+        A = rng.normal(size=(p + 300, p + 1))
+        H[k, : p + 1, : p + 1] = A.T @ A / 100.0
+    dsh = np.full((B, P), -1.0, np.float32)
+    dsh[:, :p] = rng.uniform(0.2, 1.0, size=(B, 1))
+    dsh[:, p] = 0.0
+    g = rng.normal(size=(B, P))
+    Hd = torch.from_numpy(H).cuda()
+    Md = torch.empty_like(Hd)
+    gd = torch.from_numpy(g).cuda()
+    out = torch.full((B, P), np.nan, dtype=torch.float32, device="cuda")
+    info = torch.zeros(B, dtype=torch.int32, device="cuda")
+    frozen = torch.zeros((B, P), dtype=torch.uint8, device="cuda")
+    dshd = torch.from_numpy(dsh).cuda()
+    cw = torch.empty(_lib.query("sglm_chol_work_bytes", P, B), dtype=torch.uint8, device="cuda")
+    lst = list(range(B))
+    tiles = [(q, 1) for q in range(B)]               # a tile shares one factor
+    ints = torch.tensor(np.r_[lst, lst, np.asarray(tiles).reshape(-1)].astype(np.int32),
+                        device="cuda")
+    rs = torch.ones(B, dtype=torch.float32, device="cuda")
+    _lib.call("sglm_chol_solve_inv", Hd.data_ptr(), Md.data_ptr(), P, ints.data_ptr(),
+              ints[B:].data_ptr(), rs.data_ptr(), B, B, ints[2 * B:].data_ptr(), B,
+              gd.data_ptr(), dshd.data_ptr(), out.data_ptr(), info.data_ptr(),
+              frozen.data_ptr(), B, cw.data_ptr(), 0)
+    x = out.cpu().numpy()
+    assert (info.cpu().numpy() == 0).all()
+    free = np.arange(p + 1)
+    for q in range(B):
+        Mm = H[q].astype(np.float64)[np.ix_(free, free)] + np.diag(dsh[q, free])
+        ref = np.zeros(P)
+        ref[free] = -np.linalg.solve(Mm, g[q, free])
+        assert rel(x[q], ref) < 1e-3, (q, rel(x[q], ref))
+        assert np.all(x[q, p + 1:] == 0)
+
+
 @pytest.mark.parametrize("P", [128, 2048])
 def test_chol_inv_dropped_pivots(engine, torch_mod, P):
     """Factor + inverse chain (four-wave diagonal step) on a Gram with exactly duplicated and
@@ -770,3 +815,28 @@ def test_lag_xtr_vs_float64(engine, m, L, event_major, N):
         assert np.all(got[k, d.p + 1:] == 0)
     for k in (1, 2, 4, 6, 7):
         assert np.all(got[k] == 7.0)                                   # untouched slots
+
+
+@pytest.mark.parametrize("B", [45, 7, 120])
+def test_xtr_bits_four_panel_kernel_vs_float64(engine, torch_mod, B, monkeypatch):
+    """The four-panel gradient kernel (xtr_bits4_kernel, R staged in LDS for 512 predictors;
+    taken on SGLM_XTR4=1 when P % 512 == 0) against float64 X^T R, ragged fit counts."""
+    torch = torch_mod
+    monkeypatch.setenv("SGLM_XTR4", "1")
+    from sglm_hip import _lib, synth
+    s = synth.make(N=40_000, m=50, L=5, rho=0.05, seed=B)
+    d = engine.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
+    assert d.P % 512 == 0
+    rng = np.random.default_rng(B)
+    R = np.zeros((B, d.ld), np.float32)
+    R[:, : s.N] = (rng.standard_normal((B, s.N)) * np.exp(rng.uniform(-6, 3, (B, 1)))).astype(np.float32)
+    Rd = torch.from_numpy(R).cuda()
+    G = torch.zeros((B, d.P), dtype=torch.float64, device="cuda")
+    w = torch.empty(_lib.query("sglm_xtr_bits_work_bytes", d.P, B, d.ld), dtype=torch.uint8,
+                    device="cuda")
+    _lib.call("sglm_xtr_bits", d.cbits_full().data_ptr(), d.ld, d.P, d.n, Rd.data_ptr(), B,
+              G.data_ptr(), w.data_ptr(), 0)
+    X = d.xb.double()
+    ref = (Rd.double() @ X.t()).cpu().numpy()
+    scale = (Rd.double().abs() @ X.abs().t()).cpu().numpy()
+    assert np.max(np.abs(G.cpu().numpy() - ref) / np.maximum(scale, 1e-30)) < 2e-6
