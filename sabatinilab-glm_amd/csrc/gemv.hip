@@ -475,12 +475,35 @@ __global__ void __launch_bounds__(256) reduce_slabs_f64(const float* __restrict_
     }
 }
 
-static int xtr_bits_splits(int32_t P, int32_t B, int64_t nblk) {
-    const int tiles = (P / (32 * kXT)) * ((B + 31) / 32);
-    int s = (2048 + tiles - 1) / tiles;
+// Row slabs of the gradient: the workgroup count is a multiple of the row-slab count, and
+// both kernels hold one wave per SIMD (256 four-wave workgroups, or 1024 one-wave workgroups,
+// resident at once), so the slab count minimises rounds x (K-steps per slab + a fixed cost
+// of ~8 steps per workgroup) -- a grid just over a multiple of the resident count would run a
+// nearly empty extra round.  four = the four-panel kernel.
+static int xtr_splits_for(int32_t P, int32_t B, int64_t nblk, bool four) {
+    const int64_t ngrp = (B + 31) / 32;
+    const int64_t wps = four ? (P / (32 * kXT * kXW)) * ngrp : (P / (32 * kXT)) * ngrp;
+    const int64_t resident = four ? 256 : 1024;
     const int64_t cap = nblk / 32 > 1 ? nblk / 32 : 1;      // >= 32 K-steps per slab
-    if (s > cap) s = (int)cap;
-    return s < 1 ? 1 : s;
+    int best = 1;
+    double bestc = 1e300;
+    for (int64_t s = 1; s <= cap && s <= 4096; ++s) {
+        const double c = (double)((wps * s + resident - 1) / resident) *
+                         ((double)((nblk + s - 1) / s) + 8.0);
+        if (c < bestc) {
+            bestc = c;
+            best = (int)s;
+        }
+    }
+    return best;
+}
+static int xtr_bits_splits(int32_t P, int32_t B, int64_t nblk) {
+    return xtr_splits_for(P, B, nblk, xtr4_on(P));
+}
+// workspace bound over both kernels (SGLM_XTR4 may change between the query and a launch)
+static size_t xtr_part_bytes(int32_t P, int32_t B, int64_t nblk) {
+    const int s = std::max(xtr_splits_for(P, B, nblk, false), xtr_splits_for(P, B, nblk, true));
+    return (size_t)s * B * P * sizeof(float);
 }
 
 }  // namespace sglm
@@ -539,8 +562,7 @@ int sglm_gemv_eta_bits(const uint32_t* rbits, int64_t ld, int32_t P, float* beta
 size_t sglm_xtr_bits_work_bytes(int32_t P, int32_t B, int64_t ld) {
     const int64_t Bp = ((int64_t)B + 31) / 32 * 32;
     const int64_t nblk = ld / 64;
-    const int splits = xtr_bits_splits(P, B, nblk);
-    return (size_t)3 * Bp * ld * 2 + (size_t)splits * B * P * sizeof(float);
+    return (size_t)3 * Bp * ld * 2 + xtr_part_bytes(P, B, nblk);
 }
 
 int sglm_xtr_bits(const uint32_t* cbits, int64_t ld, int32_t P, int64_t n, const float* R,
@@ -578,7 +600,7 @@ int sglm_xtr_bits(const uint32_t* cbits, int64_t ld, int32_t P, int64_t n, const
 size_t sglm_xtr_bits_packed_work_bytes(int32_t P, int32_t B, int64_t ld) {
     size_t mx = 0;
     for (int32_t b = 1; b <= B; ++b) {
-        const size_t w = (size_t)xtr_bits_splits(P, b, ld / 64) * b * P * sizeof(float);
+        const size_t w = xtr_part_bytes(P, b, ld / 64);
         mx = w > mx ? w : mx;
     }
     return mx;

@@ -772,21 +772,37 @@ class _Uploads:
         self.dev = dev
         self.base = 0
         self.off = 0
+        self.batch_at = None
 
     def __call__(self, a, dtype=None):
         a = np.ascontiguousarray(a if dtype is None else np.asarray(a).astype(dtype))
         nb = a.nbytes
         if self.off + nb > self.half:            # half full: a synchronous upload
+            self.flush()
             return torch.from_numpy(a).to(self.dev)
         o = self.base + self.off
         self.h[o:o + nb].numpy()[:] = a.reshape(-1).view(np.uint8)
         dst = self.d[o:o + nb]
-        dst.copy_(self.h[o:o + nb], non_blocking=True)
+        if self.batch_at is None:
+            dst.copy_(self.h[o:o + nb], non_blocking=True)
         self.off += (nb + 255) // 256 * 256
         return dst.view(_NP2TORCH[a.dtype]).view(a.shape)
 
+    def batch(self):
+        """Stage the next uploads without copying: ``flush()`` then moves them in ONE copy
+        (the returned device views must not be read by a launch before the flush)."""
+        self.flush()
+        self.batch_at = self.off
+
+    def flush(self):
+        if self.batch_at is not None and self.off > self.batch_at:
+            o0, o1 = self.base + self.batch_at, self.base + self.off
+            self.d[o0:o1].copy_(self.h[o0:o1], non_blocking=True)
+        self.batch_at = None
+
     def synced(self):
         """Call right after a synchronisation of the stream the uploads are ordered on."""
+        self.flush()
         self.base = self.half - self.base
         self.off = 0
 
@@ -1262,9 +1278,8 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
             step_a[more[h2]] = ts2[f2[h2]]
             tix[more[h2]] = 5 + f2[h2]
         t0 = tick("it_linesearch", t0)
-        # ---- update (coefficients on the device: w += t d)
-        _lib.call("sglm_step_update", P, na, _p(act_d), _p(up(step_a, np.float64)),
-                  _p(bf.delta), _p(beta64_d), st)
+        # ---- update (coefficients on the device: w += t d), launched below with the
+        # predictor update once the stopping decisions are made (one upload for all of them)
         if not const_hess:
             drift[act] += step_a * dmaxeta            # max_i |t d_eta_i| over the fit's rows
         fresh_start[act[step_a != 0.0]] = False
@@ -1340,19 +1355,31 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
         # that continue (0/1 designs), a plain axpy for the others
         linked = None
         nxt = np.flatnonzero(active)
+        up.batch()
+        step_d = up(step_a, np.float64)
         if fused and nxt.size:
             cont = active[act]
             done = np.flatnonzero(~cont & (step_a != 0.0))
             if done.size:
-                _lib.call("sglm_eta_axpy", n, ld, int(done.size), _p(up(act[done], np.int32)),
-                          _p(up(step_a[done], np.float32)), _p(bf.deta), _p(bf.eta), st)
+                done_d, tdone_d = up(act[done], np.int32), up(step_a[done], np.float32)
             linked = up(nxt, np.int32)
+            tcont_d = up(step_a[cont], np.float32)
+            up.flush()
+            _lib.call("sglm_step_update", P, na, _p(act_d), _p(step_d), _p(bf.delta),
+                      _p(beta64_d), st)
+            if done.size:
+                _lib.call("sglm_eta_axpy", n, ld, int(done.size), _p(done_d), _p(tdone_d),
+                          _p(bf.deta), _p(bf.eta), st)
             _lib.call("sglm_link_update", fam, power, n, ld, int(nxt.size), _p(linked),
                       _p(bf.eta), _p(prob.Y), _p(prob.M), _p(fit_resp), _p(fit_mask), _p(bf.W),
-                      R_out, Rp_out, _p(up(step_a[cont], np.float32)), _p(bf.deta), st)
+                      R_out, Rp_out, _p(tcont_d), _p(bf.deta), st)
         else:
-            _lib.call("sglm_eta_axpy", n, ld, na, _p(act_d), _p(up(step_a, np.float32)),
-                      _p(bf.deta), _p(bf.eta), st)
+            t32_d = up(step_a, np.float32)
+            up.flush()
+            _lib.call("sglm_step_update", P, na, _p(act_d), _p(step_d), _p(bf.delta),
+                      _p(beta64_d), st)
+            _lib.call("sglm_eta_axpy", n, ld, na, _p(act_d), _p(t32_d), _p(bf.deta),
+                      _p(bf.eta), st)
         if not const_hess and nxt.size:
             # the next iteration's Hessian decisions and their distances, enqueued behind
             # this iteration's predictor update (read back without a stall next iteration)
