@@ -986,10 +986,11 @@ static bool inv_lds() {
 }
 
 // 128 x 128 inversion tiles on a level whose 128-tile grid has at least SGLM_INV128_WG
-// workgroups (0 = never; read per chain capture): fewer leave the chip underfilled.
+// workgroups (read per chain capture).  Off by default: measured slower than the 64 x 64
+// LDS kernel at every fit count (C4 chain at 20 fits: 2.55 -> 2.64..2.69 ms).
 static bool inv128(int64_t wgs) {
     const char* e = getenv("SGLM_INV128_WG");
-    const int64_t mn = e ? atoll(e) : 512;
+    const int64_t mn = e ? atoll(e) : 0;
     return mn > 0 && wgs >= mn;
 }
 

@@ -198,6 +198,126 @@ eta_bits_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
         }
 }
 
+// Directions (one bf16 piece) with the direction tile staged in LDS: a workgroup of four
+// waves covers 256 rows (two 32-row tiles per wave) x 128 fits (four 32-fit groups), so each
+// expanded bit fragment feeds four MFMAs instead of one (eta_bits_kernel<1, 8>: eight VALU
+// per MFMA for the bit expansion, the limiter) and the direction crosses L2 once per 256 rows
+// for all four waves.  Same products and f32 accumulation order per (fit, row) as
+// eta_bits_kernel<1, NT>: bitwise equal results.
+constexpr int kEG = 4;              // 32-fit groups per workgroup
+constexpr int kENT = 2;             // 32-row tiles per wave
+constexpr int kEDS = 144;           // LDS bytes per fit segment (64 k x 2 B + pad)
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+eta_dir_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
+               const __bf16* __restrict__ Dp, int32_t Bp, int32_t B,
+               const int32_t* __restrict__ slots, float* __restrict__ eta) {
+    __shared__ __attribute__((aligned(16))) char lds[2][kEG * 32 * kEDS];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int64_t row0 = (int64_t)blockIdx.x * (4 * kENT * 32) + wave * (kENT * 32);
+    const int gb = blockIdx.y * kEG;
+    const int ng = min(kEG, Bp / 32 - gb);             // fit groups present (uniform)
+    const int nsteps = P / 64;
+    g_uint2* pb = as_global<g_uint2>(rbits + row0 + r);
+    // staging: 16-B chunk c = tid + 256 j (j < 4): fit c >> 3 of the 128, piece c & 7 of its
+    // 64-k segment
+    const char* dbase = reinterpret_cast<const char*>(Dp) + (int64_t)gb * 32 * P * 2;
+    int64_t goff[4];
+    int loff[4];
+    bool gl[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int c = tid + 256 * j, fit = c >> 3, q = c & 7;
+        goff[j] = (int64_t)fit * P * 2 + q * 16;
+        loff[j] = fit * kEDS + q * 16;
+        gl[j] = fit < ng * 32;
+    }
+    f32x16 acc[kEG][kENT];
+#pragma unroll
+    for (int gi = 0; gi < kEG; ++gi)
+#pragma unroll
+        for (int n = 0; n < kENT; ++n) acc[gi][n] = (f32x16){};
+    u32x2 b0[kENT], b1[kENT];
+    u32x4 dv[4];
+    auto gload = [&](u32x2 (&b)[kENT], int s) {
+#pragma unroll
+        for (int n = 0; n < kENT; ++n) b[n] = gld2(pb + (int64_t)s * ld + 32 * n);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (gl[j]) dv[j] = *reinterpret_cast<const u32x4*>(dbase + goff[j] + (int64_t)s * 128);
+    };
+    auto sstore = [&](int buf) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (gl[j]) *reinterpret_cast<u32x4*>(&lds[buf][loff[j]]) = dv[j];
+    };
+    gload(b0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int n = 0; n < kENT; ++n) asm volatile("" : "+v"(b0[n]));
+    sstore(0);
+    __syncthreads();
+    // unrolled by two so the bit registers never trade places through copies
+    auto step = [&](u32x2 (&bc)[kENT], u32x2 (&bn)[kENT], int s, int cur) {
+        const bool more = s + 1 < nsteps;
+        if (more) gload(bn, s + 1);
+        const char* lb = &lds[cur][r * kEDS + h * 16];
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            bf16x8 bx[kENT];
+#pragma unroll
+            for (int n = 0; n < kENT; ++n) bx[n] = frag_two(bc[n], ks, h);
+#pragma unroll
+            for (int gi = 0; gi < kEG; ++gi) {
+                if (gi < ng) {
+                    const bf16x8 a = __builtin_bit_cast(
+                        bf16x8, *reinterpret_cast<const u32x4*>(lb + gi * 32 * kEDS + 32 * ks));
+#pragma unroll
+                    for (int n = 0; n < kENT; ++n)
+                        acc[gi][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bx[n], acc[gi][n],
+                                                                             0, 0, 0);
+                }
+            }
+        }
+        if (more) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int n = 0; n < kENT; ++n) asm volatile("" : "+v"(bn[n]));
+            sstore(cur ^ 1);
+        }
+        __syncthreads();
+    };
+    int s = 0;
+    for (; s + 1 < nsteps; s += 2) {
+        step(b0, b1, s, 0);
+        step(b1, b0, s + 1, 1);
+    }
+    if (s < nsteps) step(b0, b1, s, 0);
+#pragma unroll
+    for (int gi = 0; gi < kEG; ++gi) {
+        if (gi >= ng) break;
+#pragma unroll
+        for (int n = 0; n < kENT; ++n)
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int f = (gb + gi) * 32 + (j & 3) + 8 * (j >> 2) + 4 * h;
+                if (f < B)
+                    eta[(int64_t)(slots ? slots[f] : f) * ld + row0 + n * 32 + r] =
+                        0.5f * acc[gi][n][j];
+            }
+    }
+}
+
+// the staged-direction kernel from four fit groups on (in one process on the C4 design:
+// 120 fits 0.80 vs 0.91 ms, 96 fits 0.65 vs 0.68, 70 fits 0.61 vs 0.59, 16 fits 0.32 vs
+// 0.16); SGLM_ETA_DIR=0 / 1 force it off / on (read per launch)
+static bool eta_dir_on(int32_t Bp) {
+    const char* e = getenv("SGLM_ETA_DIR");
+    if (e && e[0] == '0') return false;
+    if (e && e[0] == '1') return true;
+    return Bp / 32 >= 4;
+}
+
 // ---------------------------------------------------------------------------------------
 // g = X^T R (the gradient, sklearn _linear_loss.py:266-330) on the MFMA for 0/1 designs.
 // A = the design's compacted bit-planes with identity rows ([ld/64][P] uint2, the Gram v6
@@ -339,15 +459,22 @@ xtr_bits_kernel(const u32x2* __restrict__ cbits, int64_t ld, int32_t P, int64_t 
 constexpr int kXW = 4;              // waves (panels) per workgroup
 constexpr int kRS = 144;            // LDS bytes per fit segment (128 + pad)
 
+// NGW = 32-fit groups per workgroup: with two, every expanded bit fragment feeds six MFMAs
+// (three pieces x two groups) instead of three -- the bit expansion is VALU work that the
+// single MFMA stream of a one-wave-per-SIMD kernel cannot hide.
+template <int NGW>
 __global__ void __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(1, 1)))
 xtr_bits4_kernel(const u32x2* __restrict__ cbits, int64_t ld, int32_t P, int64_t nblk,
                  const __bf16* __restrict__ Rp, int32_t Bp, int32_t B, int32_t splits,
                  float* __restrict__ part) {
-    __shared__ __attribute__((aligned(16))) char lds[2][3 * 32 * kRS];
+    constexpr int kF = NGW * 32;                 // fits per workgroup
+    constexpr int kJ = 3 * NGW;                  // staging chunks per thread
+    __shared__ __attribute__((aligned(16))) char lds[2][3 * kF * kRS];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
-    const int npan4 = P / (32 * kXT * kXW), ngrp = Bp / 32;
-    const int L = xcd_logical(blockIdx.x, npan4 * ngrp * splits);
-    const int pq = L % npan4, g = (L / npan4) % ngrp, z = L / (npan4 * ngrp);
+    const int npan4 = P / (32 * kXT * kXW), ngrp = Bp / 32, ngrp2 = (ngrp + NGW - 1) / NGW;
+    const int L = xcd_logical(blockIdx.x, npan4 * ngrp2 * splits);
+    const int pq = L % npan4, g2 = (L / npan4) % ngrp2, z = L / (npan4 * ngrp2);
+    const int g0 = g2 * NGW, ngv = min(NGW, ngrp - g0);       // groups present (uniform)
     const int pn = pq * kXW + wave;
     const int64_t sps = (nblk + splits - 1) / splits;
     const int64_t blk0 = (int64_t)z * sps;
@@ -355,34 +482,37 @@ xtr_bits4_kernel(const u32x2* __restrict__ cbits, int64_t ld, int32_t P, int64_t
     const int nsteps = blk1 > blk0 ? (int)(blk1 - blk0) : 0;
     const uint64_t abase = (uint64_t)(cbits + blk0 * P);
     const uint32_t avo = (uint32_t)((pn * (32 * kXT) + r) * 8);
-    // R staging: thread tid moves 16-B chunks c = tid + 256 j (j < 3) of the step's tile:
-    // piece c >> 8, fit (c >> 3) & 31, chunk c & 7 of that fit's 128-B row segment
+    // R staging: thread tid moves 16-B chunks c = tid + 256 j of the step's tile: piece
+    // c / (256 NGW), fit (c >> 3) % kF, chunk c & 7 of that fit's 128-B row segment
     const char* rb = reinterpret_cast<const char*>(Rp) + blk0 * 128;
     const int64_t plane = (int64_t)Bp * ld * 2;
-    int64_t goff[3];
-    int loff[3];
+    // chunk j: piece j / NGW, fit (tid >> 3) + 32 (j % NGW) -- a per-thread base plus
+    // wave-uniform strides (kept in scalar registers)
+    const int64_t gbase = (int64_t)(g0 * 32 + (tid >> 3)) * ld * 2 + (tid & 7) * 16;
+    const int64_t gstep = (int64_t)32 * ld * 2;
+    const int lbase = (tid >> 3) * kRS + (tid & 7) * 16;
+    auto goff = [&](int j) { return gbase + (j / NGW) * plane + (j % NGW) * gstep; };
+    auto loff = [&](int j) { return lbase + ((j / NGW) * kF + 32 * (j % NGW)) * kRS; };
+    auto gl = [&](int j) { return (j % NGW) < ngv; };
+    f32x16 ah[NGW][kXT], al[NGW][kXT];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        const int c = tid + 256 * j;
-        const int pc = c >> 8, fit = (c >> 3) & 31, q = c & 7;
-        goff[j] = pc * plane + (int64_t)(g * 32 + fit) * ld * 2 + q * 16;
-        loff[j] = pc * 32 * kRS + fit * kRS + q * 16;
-    }
-    f32x16 ah[kXT], al[kXT];
+    for (int gi = 0; gi < NGW; ++gi)
 #pragma unroll
-    for (int m = 0; m < kXT; ++m) {
-        ah[m] = (f32x16){};
-        al[m] = (f32x16){};
-    }
+        for (int m = 0; m < kXT; ++m) {
+            ah[gi][m] = (f32x16){};
+            al[gi][m] = (f32x16){};
+        }
     if (nsteps > 0) {
         u32x2 a0[kXT], a1[kXT];
-        u32x4 rv[3];
+        u32x4 rv[kJ];
         loadA<0>(a0, abase, avo);
 #pragma unroll
-        for (int j = 0; j < 3; ++j) rv[j] = *reinterpret_cast<const u32x4*>(rb + goff[j]);
+        for (int j = 0; j < kJ; ++j)
+            if (gl(j)) rv[j] = *reinterpret_cast<const u32x4*>(rb + goff(j));
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-        for (int j = 0; j < 3; ++j) *reinterpret_cast<u32x4*>(&lds[0][loff[j]]) = rv[j];
+        for (int j = 0; j < kJ; ++j)
+            if (gl(j)) *reinterpret_cast<u32x4*>(&lds[0][loff(j)]) = rv[j];
         __syncthreads();
         // one step on A registers ac with the next step's loads into an: the loop is unrolled
         // by two so the buffers never trade places through copies (an asm-loaded register
@@ -392,36 +522,49 @@ xtr_bits4_kernel(const u32x2* __restrict__ cbits, int64_t ld, int32_t P, int64_t
             if (more) {
                 loadA<0>(an, abase + (uint64_t)(s + 1) * P * 8, avo);
 #pragma unroll
-                for (int j = 0; j < 3; ++j)
-                    rv[j] = *reinterpret_cast<const u32x4*>(rb + (int64_t)(s + 1) * 128 + goff[j]);
+                for (int j = 0; j < kJ; ++j)
+                    if (gl(j))
+                        rv[j] = *reinterpret_cast<const u32x4*>(rb + (int64_t)(s + 1) * 128 +
+                                                                goff(j));
             }
 #pragma unroll
             for (int m = 0; m < kXT; ++m) asm volatile("" : "+v"(ac[m]));
+            // per K-slice: the four tiles' expansions, then the MFMAs ordered by piece so that
+            // the two accumulations into al are 4 NGW MFMAs apart (each accumulator still sums
+            // b1 then b2 per slice: the same results bit for bit)
             const char* lb = &lds[cur][r * kRS + h * 16];
 #pragma unroll
             for (int ks = 0; ks < 4; ++ks) {
-                const bf16x8 b0 = __builtin_bit_cast(bf16x8,
-                    *reinterpret_cast<const u32x4*>(lb + 0 * 32 * kRS + 32 * ks));
-                const bf16x8 b1 = __builtin_bit_cast(bf16x8,
-                    *reinterpret_cast<const u32x4*>(lb + 1 * 32 * kRS + 32 * ks));
-                const bf16x8 b2 = __builtin_bit_cast(bf16x8,
-                    *reinterpret_cast<const u32x4*>(lb + 2 * 32 * kRS + 32 * ks));
+                bf16x8 ax[kXT];
 #pragma unroll
-                for (int m = 0; m < kXT; ++m) {
-                    const bf16x8 ax = frag_two(ac[m], ks, h);
-                    ah[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ax, b0, ah[m], 0, 0, 0);
-                    al[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ax, b1, al[m], 0, 0, 0);
-                    al[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ax, b2, al[m], 0, 0, 0);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
+                for (int m = 0; m < kXT; ++m) ax[m] = frag_two(ac[m], ks, h);
+#pragma unroll
+                for (int pc = 0; pc < 3; ++pc)
+#pragma unroll
+                    for (int gi = 0; gi < NGW; ++gi) {
+                        if (gi < ngv) {
+                            const bf16x8 b = __builtin_bit_cast(bf16x8,
+                                *reinterpret_cast<const u32x4*>(
+                                    lb + (pc * kF + gi * 32) * kRS + 32 * ks));
+#pragma unroll
+                            for (int m = 0; m < kXT; ++m) {
+                                if (pc == 0)
+                                    ah[gi][m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                                        ax[m], b, ah[gi][m], 0, 0, 0);
+                                else
+                                    al[gi][m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                                        ax[m], b, al[gi][m], 0, 0, 0);
+                            }
+                        }
+                    }
             }
             if (more) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
                 for (int m = 0; m < kXT; ++m) asm volatile("" : "+v"(an[m]));
 #pragma unroll
-                for (int j = 0; j < 3; ++j)
-                    *reinterpret_cast<u32x4*>(&lds[cur ^ 1][loff[j]]) = rv[j];
+                for (int j = 0; j < kJ; ++j)
+                    if (gl(j)) *reinterpret_cast<u32x4*>(&lds[cur ^ 1][loff(j)]) = rv[j];
             }
             __syncthreads();
         };
@@ -432,31 +575,51 @@ xtr_bits4_kernel(const u32x2* __restrict__ cbits, int64_t ld, int32_t P, int64_t
         }
         if (s < nsteps) step(a0, a1, s, 0);
     }
-    const int f = g * 32 + r;
-    if (f < B) {
-        float* out = part + ((int64_t)z * B + f) * P + pn * (32 * kXT);
 #pragma unroll
-        for (int m = 0; m < kXT; ++m)
+    for (int gi = 0; gi < NGW; ++gi) {
+        const int f = (g0 + gi) * 32 + r;
+        if (gi < ngv && f < B) {
+            float* out = part + ((int64_t)z * B + f) * P + pn * (32 * kXT);
 #pragma unroll
-            for (int j = 0; j < 16; ++j)
-                out[m * 32 + (j & 3) + 8 * (j >> 2) + 4 * h] = 0.5f * (ah[m][j] + al[m][j]);
+            for (int m = 0; m < kXT; ++m)
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    out[m * 32 + (j & 3) + 8 * (j >> 2) + 4 * h] =
+                        0.5f * (ah[gi][m][j] + al[gi][m][j]);
+        }
     }
 }
 
-// four-panel kernel when P % 512 == 0 unless SGLM_XTR4=0 (read per launch: tests switch it
-// inside one process).  C4 gradient at 120 fits: 1.87 -> 1.28 ms.
-static bool xtr4_on(int32_t P) {
-    const char* e = getenv("SGLM_XTR4");
-    return !(e && e[0] == '0') && P % (32 * kXT * kXW) == 0;
+// Gradient kernel per call (read per launch: tests switch it inside one process):
+//   2 = four-panel, two fit groups per workgroup -- an even group count (P % 512 == 0);
+//   0 = one-panel -- otherwise (an odd count leaves half-empty two-group workgroups, and the
+//       one-group four-panel kernel measured no faster than the one-panel kernel once the
+//       row slabs fill whole rounds: C4, 120 fits 1.20 / 1.46 / 1.43 ms, 70 fits
+//       1.19 / 1.13 / 1.08 ms for variants 2 / 1 / 0 in one process);
+//   1 = four-panel, one group -- only on request.
+// SGLM_XTR4=0 forces 0, SGLM_XTR_NGW=1 / 2 force 1 / 2 where P allows.
+static int xtr_variant(int32_t P, int32_t B) {
+    const int ngrp = (B + 31) / 32;
+    if (P % (32 * kXT * kXW) != 0) return 0;
+    const char* e4 = getenv("SGLM_XTR4");
+    if (e4 && e4[0] == '0') return 0;
+    const char* e = getenv("SGLM_XTR_NGW");
+    if (e && e[0] == '1') return 1;
+    if (e && e[0] == '2') return ngrp >= 2 ? 2 : 1;
+    return (ngrp >= 2 && ngrp % 2 == 0) ? 2 : 0;
 }
 
 static void launch_xtr_bits(const u32x2* cbits, int64_t ld, int32_t P, int64_t nblk,
                             const __bf16* Rp, int32_t Bp, int32_t B, int32_t splits, float* part,
                             hipStream_t s) {
+    const int v = xtr_variant(P, B);
     const unsigned tiles = (unsigned)((P / (32 * kXT)) * (Bp / 32) * splits);
-    if (xtr4_on(P))
-        xtr_bits4_kernel<<<tiles / kXW, 64 * kXW, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, B, splits,
-                                                          part);
+    const unsigned wgs4 = (unsigned)((P / (32 * kXT * kXW)) * ((Bp / 32 + v - 1) / (v ? v : 1)) *
+                                     splits);
+    if (v == 2)
+        xtr_bits4_kernel<2><<<wgs4, 64 * kXW, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, B, splits, part);
+    else if (v == 1)
+        xtr_bits4_kernel<1><<<wgs4, 64 * kXW, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, B, splits, part);
     else
         xtr_bits_kernel<<<tiles, 64, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, B, splits, part);
 }
@@ -480,10 +643,11 @@ __global__ void __launch_bounds__(256) reduce_slabs_f64(const float* __restrict_
 // resident at once), so the slab count minimises rounds x (K-steps per slab + a fixed cost
 // of ~8 steps per workgroup) -- a grid just over a multiple of the resident count would run a
 // nearly empty extra round.  four = the four-panel kernel.
-static int xtr_splits_for(int32_t P, int32_t B, int64_t nblk, bool four) {
+static int xtr_splits_for(int32_t P, int32_t B, int64_t nblk, int variant) {
     const int64_t ngrp = (B + 31) / 32;
-    const int64_t wps = four ? (P / (32 * kXT * kXW)) * ngrp : (P / (32 * kXT)) * ngrp;
-    const int64_t resident = four ? 256 : 1024;
+    const int64_t wps = variant ? (P / (32 * kXT * kXW)) * ((ngrp + variant - 1) / variant)
+                                : (P / (32 * kXT)) * ngrp;
+    const int64_t resident = variant ? 256 : 1024;
     const int64_t cap = nblk / 32 > 1 ? nblk / 32 : 1;      // >= 32 K-steps per slab
     int best = 1;
     double bestc = 1e300;
@@ -498,11 +662,12 @@ static int xtr_splits_for(int32_t P, int32_t B, int64_t nblk, bool four) {
     return best;
 }
 static int xtr_bits_splits(int32_t P, int32_t B, int64_t nblk) {
-    return xtr_splits_for(P, B, nblk, xtr4_on(P));
+    return xtr_splits_for(P, B, nblk, xtr_variant(P, B));
 }
-// workspace bound over both kernels (SGLM_XTR4 may change between the query and a launch)
+// workspace bound over every variant (the switches may change between the query and a launch)
 static size_t xtr_part_bytes(int32_t P, int32_t B, int64_t nblk) {
-    const int s = std::max(xtr_splits_for(P, B, nblk, false), xtr_splits_for(P, B, nblk, true));
+    const int s = std::max(xtr_splits_for(P, B, nblk, 0),
+                           std::max(xtr_splits_for(P, B, nblk, 1), xtr_splits_for(P, B, nblk, 2)));
     return (size_t)s * B * P * sizeof(float);
 }
 
@@ -553,8 +718,13 @@ int sglm_gemv_eta_bits(const uint32_t* rbits, int64_t ld, int32_t P, float* beta
         round1_kernel<<<gs, 256, 0, s>>>(beta, P, B, Bp, slots, Dp);
         st = check_launch("round1_kernel");
         if (st) return st;
-        eta_bits_kernel<1, 8><<<dim3((unsigned)(ld / 256), (unsigned)(Bp / 32)), 64, 0, s>>>(
-            reinterpret_cast<const u32x2*>(rbits), ld, P, Dp, Bp, B, slots, eta);
+        if (eta_dir_on(Bp))
+            eta_dir_kernel<<<dim3((unsigned)(ld / 256), (unsigned)((Bp / 32 + kEG - 1) / kEG)),
+                             256, 0, s>>>(reinterpret_cast<const u32x2*>(rbits), ld, P, Dp, Bp,
+                                          B, slots, eta);
+        else
+            eta_bits_kernel<1, 8><<<dim3((unsigned)(ld / 256), (unsigned)(Bp / 32)), 64, 0, s>>>(
+                reinterpret_cast<const u32x2*>(rbits), ld, P, Dp, Bp, B, slots, eta);
     }
     return check_launch("eta_bits_kernel");
 }

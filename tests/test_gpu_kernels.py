@@ -590,6 +590,42 @@ def test_eta_bits_matches_float64(engine, torch_mod):
     assert torch.equal(bd2[1], bd[1]) and torch.isnan(out_r[1]).all()
 
 
+@pytest.mark.parametrize("B", [100, 33, 7])
+def test_eta_dir_kernel_equals_per_group_kernel(engine, torch_mod, B, monkeypatch):
+    """Direction products through the LDS-staged kernel (eta_dir_kernel: 128 fits x 256 rows
+    per workgroup, ragged fit groups) equal the per-group kernel bit for bit and X d in
+    float64 to f32 accuracy, through a slot list."""
+    torch = torch_mod
+    from sglm_hip import _lib, synth
+    s = synth.make(N=20000, m=30, L=6, rho=0.05, seed=B)
+    d = engine.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
+    rng = np.random.default_rng(B)
+    nb = B + 5
+    beta = (rng.standard_normal((nb, d.P)) * np.exp(rng.uniform(-8, 3, (nb, d.P)))).astype(np.float32)
+    beta[:, d.p + 1:] = 0.0
+    slots = rng.permutation(nb)[:B].astype(np.int32)
+    sl = torch.from_numpy(slots).cuda()
+    work = torch.empty(_lib.query("sglm_eta_bits_work_bytes", d.P, B), dtype=torch.uint8,
+                       device="cuda")
+    outs = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("SGLM_ETA_DIR", v)
+        bd = torch.from_numpy(beta).cuda()
+        out = torch.full((nb, d.ld), float("nan"), dtype=torch.float32, device="cuda")
+        _lib.call("sglm_gemv_eta_bits", d.rbits.data_ptr(), d.ld, d.P, bd.data_ptr(), B,
+                  sl.data_ptr(), 0, out.data_ptr(), work.data_ptr(), 0)
+        outs[v] = (out.cpu().numpy(), bd.cpu().numpy())
+    got, br = outs["1"]
+    assert np.array_equal(got, outs["0"][0], equal_nan=True)
+    X = d.xb.double().cpu().numpy()
+    for k in slots[:12]:
+        ref = br[k].astype(np.float64) @ X
+        sc = np.abs(br[k].astype(np.float64)) @ np.abs(X)
+        assert np.max(np.abs(got[k] - ref) / np.maximum(sc, 1e-30)) < 2e-6, k
+    untouched = np.setdiff1d(np.arange(nb), slots)
+    assert np.isnan(got[untouched]).all()
+
+
 def test_compact_bits_equals_pack_bits_rows(engine, torch_mod):
     """Compaction from the 1-bit planes == compaction from the bf16 design, bit for bit."""
     torch = torch_mod
@@ -817,12 +853,14 @@ def test_lag_xtr_vs_float64(engine, m, L, event_major, N):
         assert np.all(got[k] == 7.0)                                   # untouched slots
 
 
-@pytest.mark.parametrize("B", [45, 7, 120])
-def test_xtr_bits_four_panel_kernel_vs_float64(engine, torch_mod, B, monkeypatch):
-    """The four-panel gradient kernel (xtr_bits4_kernel, R staged in LDS for 512 predictors;
-    taken on SGLM_XTR4=1 when P % 512 == 0) against float64 X^T R, ragged fit counts."""
+@pytest.mark.parametrize("B,ngw", [(45, "2"), (7, "1"), (120, "2"), (70, "1"), (70, "2"),
+                                   (120, "1")])
+def test_xtr_bits_four_panel_kernel_vs_float64(engine, torch_mod, B, ngw, monkeypatch):
+    """The four-panel gradient kernel (xtr_bits4_kernel, R staged in LDS for 512 predictors,
+    one or two 32-fit groups per workgroup, forced by SGLM_XTR_NGW; P % 512 == 0) against
+    float64 X^T R, ragged fit counts and a half-empty last workgroup (70 fits, two groups)."""
     torch = torch_mod
-    monkeypatch.setenv("SGLM_XTR4", "1")
+    monkeypatch.setenv("SGLM_XTR_NGW", ngw)
     from sglm_hip import _lib, synth
     s = synth.make(N=40_000, m=50, L=5, rho=0.05, seed=B)
     d = engine.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
