@@ -198,58 +198,61 @@ eta_bits_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
         }
 }
 
-// Directions (one bf16 piece) with the direction tile staged in LDS: a workgroup of four
-// waves covers 256 rows (two 32-row tiles per wave) x 128 fits (four 32-fit groups), so each
-// expanded bit fragment feeds four MFMAs instead of one (eta_bits_kernel<1, 8>: eight VALU
-// per MFMA for the bit expansion, the limiter) and the direction crosses L2 once per 256 rows
-// for all four waves.  Same products and f32 accumulation order per (fit, row) as
-// eta_bits_kernel<1, NT>: bitwise equal results.
-constexpr int kEG = 4;              // 32-fit groups per workgroup
+// eta on the MFMA with the coefficient tile staged in LDS: a workgroup of four waves covers
+// 256 rows (two 32-row tiles per wave) x NG 32-fit groups, so each expanded bit fragment feeds
+// NP x NG MFMAs instead of NP (eta_bits_kernel<1, 8>: eight VALU per MFMA for the bit
+// expansion, the limiter) and the coefficients cross L2 once per 256 rows for all four waves.
+// NP = 1: Newton directions rounded to one bf16 piece, 4 groups (the same products and f32
+// accumulation order per (fit, row) as eta_bits_kernel<1, NT>: bitwise equal results).
+// NP = 3: exact coefficients as three bf16 pieces, 2 groups, a hi accumulator and a mid + lo
+// accumulator per tile (as the gradient kernel).
 constexpr int kENT = 2;             // 32-row tiles per wave
 constexpr int kEDS = 144;           // LDS bytes per fit segment (64 k x 2 B + pad)
 
+template <int NP, int NG>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 eta_dir_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
                const __bf16* __restrict__ Dp, int32_t Bp, int32_t B,
                const int32_t* __restrict__ slots, float* __restrict__ eta) {
-    __shared__ __attribute__((aligned(16))) char lds[2][kEG * 32 * kEDS];
+    constexpr int kF = NG * 32;                  // fits per workgroup
+    constexpr int kJ = NP * NG;                  // staging chunks per thread
+    constexpr int kA = NP == 1 ? 1 : 2;          // accumulator sets
+    __shared__ __attribute__((aligned(16))) char lds[2][NP * kF * kEDS];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
     const int64_t row0 = (int64_t)blockIdx.x * (4 * kENT * 32) + wave * (kENT * 32);
-    const int gb = blockIdx.y * kEG;
-    const int ng = min(kEG, Bp / 32 - gb);             // fit groups present (uniform)
+    const int gb = blockIdx.y * NG;
+    const int ng = min(NG, Bp / 32 - gb);              // fit groups present (uniform)
     const int nsteps = P / 64;
     g_uint2* pb = as_global<g_uint2>(rbits + row0 + r);
-    // staging: 16-B chunk c = tid + 256 j (j < 4): fit c >> 3 of the 128, piece c & 7 of its
-    // 64-k segment
-    const char* dbase = reinterpret_cast<const char*>(Dp) + (int64_t)gb * 32 * P * 2;
-    int64_t goff[4];
-    int loff[4];
-    bool gl[4];
+    // staging: chunk j of this thread = piece j / NG, fit (tid >> 3) + 32 (j % NG), 16-B
+    // piece tid & 7 of that fit's 64-k segment
+    const char* dbase = reinterpret_cast<const char*>(Dp) +
+                        ((int64_t)(gb * 32 + (tid >> 3)) * P) * 2 + (tid & 7) * 16;
+    const int64_t pstride = (int64_t)Bp * P * 2;
+    const int lbase = (tid >> 3) * kEDS + (tid & 7) * 16;
+    auto goff = [&](int j) { return (j / NG) * pstride + (int64_t)(32 * (j % NG)) * P * 2; };
+    auto loff = [&](int j) { return lbase + ((j / NG) * kF + 32 * (j % NG)) * kEDS; };
+    auto gl = [&](int j) { return (j % NG) < ng; };
+    f32x16 acc[kA][NG][kENT];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int c = tid + 256 * j, fit = c >> 3, q = c & 7;
-        goff[j] = (int64_t)fit * P * 2 + q * 16;
-        loff[j] = fit * kEDS + q * 16;
-        gl[j] = fit < ng * 32;
-    }
-    f32x16 acc[kEG][kENT];
+    for (int a = 0; a < kA; ++a)
 #pragma unroll
-    for (int gi = 0; gi < kEG; ++gi)
+        for (int gi = 0; gi < NG; ++gi)
 #pragma unroll
-        for (int n = 0; n < kENT; ++n) acc[gi][n] = (f32x16){};
+            for (int n = 0; n < kENT; ++n) acc[a][gi][n] = (f32x16){};
     u32x2 b0[kENT], b1[kENT];
-    u32x4 dv[4];
+    u32x4 dv[kJ];
     auto gload = [&](u32x2 (&b)[kENT], int s) {
 #pragma unroll
         for (int n = 0; n < kENT; ++n) b[n] = gld2(pb + (int64_t)s * ld + 32 * n);
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-            if (gl[j]) dv[j] = *reinterpret_cast<const u32x4*>(dbase + goff[j] + (int64_t)s * 128);
+        for (int j = 0; j < kJ; ++j)
+            if (gl(j)) dv[j] = *reinterpret_cast<const u32x4*>(dbase + goff(j) + (int64_t)s * 128);
     };
     auto sstore = [&](int buf) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-            if (gl[j]) *reinterpret_cast<u32x4*>(&lds[buf][loff[j]]) = dv[j];
+        for (int j = 0; j < kJ; ++j)
+            if (gl(j)) *reinterpret_cast<u32x4*>(&lds[buf][loff(j)]) = dv[j];
     };
     gload(b0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -268,16 +271,25 @@ eta_dir_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
 #pragma unroll
             for (int n = 0; n < kENT; ++n) bx[n] = frag_two(bc[n], ks, h);
 #pragma unroll
-            for (int gi = 0; gi < kEG; ++gi) {
-                if (gi < ng) {
-                    const bf16x8 a = __builtin_bit_cast(
-                        bf16x8, *reinterpret_cast<const u32x4*>(lb + gi * 32 * kEDS + 32 * ks));
+            for (int pc = 0; pc < NP; ++pc)
 #pragma unroll
-                    for (int n = 0; n < kENT; ++n)
-                        acc[gi][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bx[n], acc[gi][n],
-                                                                             0, 0, 0);
+                for (int gi = 0; gi < NG; ++gi) {
+                    if (gi < ng) {
+                        const bf16x8 a = __builtin_bit_cast(bf16x8,
+                            *reinterpret_cast<const u32x4*>(lb + (pc * kF + gi * 32) * kEDS +
+                                                            32 * ks));
+                        const int as = pc == 0 ? 0 : 1;
+#pragma unroll
+                        for (int n = 0; n < kENT; ++n) {
+                            if (NP == 1 || as == 0)
+                                acc[0][gi][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                                    a, bx[n], acc[0][gi][n], 0, 0, 0);
+                            else
+                                acc[kA - 1][gi][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                                    a, bx[n], acc[kA - 1][gi][n], 0, 0, 0);
+                        }
+                    }
                 }
-            }
         }
         if (more) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -294,16 +306,18 @@ eta_dir_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
     }
     if (s < nsteps) step(b0, b1, s, 0);
 #pragma unroll
-    for (int gi = 0; gi < kEG; ++gi) {
+    for (int gi = 0; gi < NG; ++gi) {
         if (gi >= ng) break;
 #pragma unroll
         for (int n = 0; n < kENT; ++n)
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 const int f = (gb + gi) * 32 + (j & 3) + 8 * (j >> 2) + 4 * h;
-                if (f < B)
-                    eta[(int64_t)(slots ? slots[f] : f) * ld + row0 + n * 32 + r] =
-                        0.5f * acc[gi][n][j];
+                if (f < B) {
+                    const float v = NP == 1 ? acc[0][gi][n][j]
+                                            : acc[0][gi][n][j] + acc[kA - 1][gi][n][j];
+                    eta[(int64_t)(slots ? slots[f] : f) * ld + row0 + n * 32 + r] = 0.5f * v;
+                }
             }
     }
 }
@@ -316,6 +330,14 @@ static bool eta_dir_on(int32_t Bp) {
     if (e && e[0] == '0') return false;
     if (e && e[0] == '1') return true;
     return Bp / 32 >= 4;
+}
+
+// the staged kernel for exact coefficients (three pieces) at every fit count -- one kernel, so
+// a fit's eta is bitwise the same whatever else is in the call -- unless
+// SGLM_ETA_EXACT_STAGED=0 (read per launch)
+static bool eta_exact_staged(int32_t) {
+    const char* e = getenv("SGLM_ETA_EXACT_STAGED");
+    return !(e && e[0] == '0');
 }
 
 // ---------------------------------------------------------------------------------------
@@ -712,16 +734,21 @@ int sglm_gemv_eta_bits(const uint32_t* rbits, int64_t ld, int32_t P, float* beta
         split3_kernel<<<gs, 256, 0, s>>>(beta, P, B, Bp, slots, Dp);
         st = check_launch("split3_kernel");
         if (st) return st;
-        eta_bits_kernel<3, 4><<<dim3((unsigned)(ld / 128), (unsigned)(Bp / 32)), 64, 0, s>>>(
-            reinterpret_cast<const u32x2*>(rbits), ld, P, Dp, Bp, B, slots, eta);
+        if (eta_exact_staged(Bp))
+            eta_dir_kernel<3, 2><<<dim3((unsigned)(ld / 256), (unsigned)((Bp / 32 + 1) / 2)),
+                                   256, 0, s>>>(reinterpret_cast<const u32x2*>(rbits), ld, P,
+                                                Dp, Bp, B, slots, eta);
+        else
+            eta_bits_kernel<3, 4><<<dim3((unsigned)(ld / 128), (unsigned)(Bp / 32)), 64, 0, s>>>(
+                reinterpret_cast<const u32x2*>(rbits), ld, P, Dp, Bp, B, slots, eta);
     } else {
         round1_kernel<<<gs, 256, 0, s>>>(beta, P, B, Bp, slots, Dp);
         st = check_launch("round1_kernel");
         if (st) return st;
         if (eta_dir_on(Bp))
-            eta_dir_kernel<<<dim3((unsigned)(ld / 256), (unsigned)((Bp / 32 + kEG - 1) / kEG)),
-                             256, 0, s>>>(reinterpret_cast<const u32x2*>(rbits), ld, P, Dp, Bp,
-                                          B, slots, eta);
+            eta_dir_kernel<1, 4><<<dim3((unsigned)(ld / 256), (unsigned)((Bp / 32 + 3) / 4)),
+                                   256, 0, s>>>(reinterpret_cast<const u32x2*>(rbits), ld, P,
+                                                Dp, Bp, B, slots, eta);
         else
             eta_bits_kernel<1, 8><<<dim3((unsigned)(ld / 256), (unsigned)(Bp / 32)), 64, 0, s>>>(
                 reinterpret_cast<const u32x2*>(rbits), ld, P, Dp, Bp, B, slots, eta);

@@ -88,6 +88,33 @@ SOLVE_INV = __import__("os").environ.get("SGLM_SOLVE_INV", "1") == "1"
 # where the factorisation chain runs: "side" (its own stream, overlapping the gradient),
 # "prio" (the same at high stream priority), "serial" (the main stream, before the gradient)
 CHOL_STREAM = __import__("os").environ.get("SGLM_CHOL_STREAM", "side")
+# SGLM_GRAM_PIPE=1: Grams computed one source at a time with each group's factorisation chain
+# started right behind its Gram.  Off by default: the per-group chains are latency-bound
+# (~1.1 ms each at 1-3 fits against 2.6 ms for one chain of 20), so the side stream carried
+# 28.6 instead of 12.1 ms per C4 grid and more of it was exposed (11.4 vs 7.1 ms)
+GRAM_PIPE = __import__("os").environ.get("SGLM_GRAM_PIPE", "0") == "1"
+
+
+def _gram_groups(form, uniq, dup):
+    """The fits that form a new Hessian this iteration grouped by the Gram they take it from,
+    [(source, fits)] with the source first in its group, sources in ascending order; None when
+    there is a single source or a formed fit's source is not among the computed Grams."""
+    if len(uniq) < 2:
+        return None
+    src = {int(k): int(k) for k in uniq}
+    for k, rk in dup:
+        src[int(k)] = int(rk)
+    groups = {int(r): [int(r)] for r in uniq}
+    for k in form:
+        k = int(k)
+        r = src.get(k)
+        if r is None or r not in groups:
+            return None
+        if k != r:
+            groups[r].append(k)
+    if sum(len(g) for g in groups.values()) != len(form):
+        return None
+    return [(r, np.asarray(groups[r], dtype=np.int64)) for r in sorted(groups)]
 
 
 def require_gpu():
@@ -1110,6 +1137,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
 
         # ---- Hessian
         gram_comp = np.zeros(B, dtype=bool)     # fits whose Gram is computed this iteration
+        pipe_groups = None
         if const_hess:
             gram_now[:] = not factored
             if not factored:
@@ -1132,10 +1160,19 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
             plan = None
             alias[:] = -1
             alias[ali] = repl[ali]
-            _syrk(d, bf, np.sort(uniq).astype(np.int32), nsteps, ntile1, stats, st, rows=rows)
+            pipe_groups = _gram_groups(form, uniq, dup) if (
+                GRAM_PIPE and SOLVE_INV and CHOL_STREAM != "serial") else None
+            if pipe_groups is None:
+                _syrk(d, bf, np.sort(uniq).astype(np.int32), nsteps, ntile1, stats, st,
+                      rows=rows)
+                for k, rk in dup:
+                    bf.H[k].copy_(bf.H[rk])
+            else:
+                # Grams one source at a time, each group's factorisation chain started on the
+                # side stream as soon as its Gram is done (below): the chains overlap the next
+                # Grams instead of all waiting for the last one
+                form = np.concatenate([g for _, g in pipe_groups]).astype(form.dtype)
             gram_comp[uniq] = True
-            for k, rk in dup:
-                bf.H[k].copy_(bf.H[rk])
             gram_now[:] = False
             gram_now[form] = True
             if stats is not None:
@@ -1177,19 +1214,44 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
                           None, int(nref), int(nref), None, 0, None, _p(bf.dshift), _p(bf.delta),
                           _p(bf.info), _p(bf.frozen), B, _p(bf.cwork), st)
             elif nref:
-                # factor + invert the new Hessians on a side stream while the gradient runs
+                # factor + invert the new Hessians on a side stream while the gradient runs.
+                # Everything the main stream does first (the Grams one source at a time with
+                # pipelining, then the gradient) is enqueued BEFORE the chains: a chain's graph
+                # launch holds the host for ~1-2 ms (one submission per node), and the main
+                # stream must not wait behind it
                 side = _side_stream()
                 bf.fact_fits[:nref].copy_(ints[:nref])
-                ready = torch.cuda.Event()
-                ready.record()
-                side.wait_event(ready)
-                _lib.call("sglm_chol_solve_inv", _p(bf.H), _p(bf.Minv), P, _p(bf.fact_fits), None,
-                          None, int(nref), int(nref), None, 0, None, _p(bf.dshift), _p(bf.delta),
-                          _p(bf.info), _p(bf.frozen), B, _p(bf.cwork), side.cuda_stream)
+                chains = []
+                if pipe_groups is not None:
+                    off = 0
+                    dsrc = dict(dup)
+                    for r, grp in pipe_groups:
+                        _syrk(d, bf, np.array([r], dtype=np.int32), nsteps, ntile1, stats, st,
+                              rows=rows)
+                        for k in grp:
+                            if int(k) != int(r):
+                                bf.H[int(k)].copy_(bf.H[int(dsrc[int(k)])])
+                        ready = torch.cuda.Event()
+                        ready.record()
+                        chains.append((ready, off, int(len(grp))))
+                        off += int(len(grp))
+                else:
+                    ready = torch.cuda.Event()
+                    ready.record()
+                    chains.append((ready, 0, int(nref)))
+                _gradient()
+                t0 = tick("it_gradient", t0)
+                for ready, off, ng in chains:
+                    side.wait_event(ready)
+                    _lib.call("sglm_chol_solve_inv", _p(bf.H), _p(bf.Minv), P,
+                              _p(bf.fact_fits[off:]), None, None, ng, ng, None, 0, None,
+                              _p(bf.dshift), _p(bf.delta), _p(bf.info), _p(bf.frozen), B,
+                              _p(bf.cwork), side.cuda_stream)
                 fact_done = torch.cuda.Event()
                 fact_done.record(side)
-            _gradient()
-            t0 = tick("it_gradient", t0)
+            if fact_done is None:
+                _gradient()
+                t0 = tick("it_gradient", t0)
             if fact_done is not None:
                 torch.cuda.current_stream().wait_event(fact_done)
             _lib.call("sglm_chol_solve_inv", _p(bf.H), _p(bf.Minv), P, _p(ints),

@@ -4,6 +4,7 @@ compared inside one process, alternating rounds, medians reported.
 
 python tools/ab_micro.py eta|xtr [B,...] : C4 design (1M x 2000 event design), HIP events.
   eta : direction products sglm_gemv_eta_bits (SGLM_ETA_DIR=1 vs 0)
+  eta3: exact (three-piece) products (SGLM_ETA_EXACT_STAGED=1 vs 0)
   xtr : gradient sglm_xtr_bits_packed (SGLM_XTR_NGW=2 vs 1, SGLM_XTR4=0 one-panel)
 """
 import os
@@ -16,6 +17,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "sabatinilab-glm_amd")]
 
 VARIANTS = {
     "eta": [("dir", {"SGLM_ETA_DIR": "1"}), ("group", {"SGLM_ETA_DIR": "0"})],
+    "eta3": [("staged", {"SGLM_ETA_EXACT_STAGED": "1"}), ("group", {"SGLM_ETA_EXACT_STAGED": "0"})],
     "xtr": [("ngw2", {"SGLM_XTR4": "1", "SGLM_XTR_NGW": "2"}),
             ("ngw1", {"SGLM_XTR4": "1", "SGLM_XTR_NGW": "1"}),
             ("panel1", {"SGLM_XTR4": "0", "SGLM_XTR_NGW": "1"})],
@@ -33,7 +35,7 @@ def main():
     for B in sizes:
         rng = np.random.default_rng(B)
         slots = torch.arange(B, dtype=torch.int32, device="cuda")
-        if what == "eta":
+        if what in ("eta", "eta3"):
             beta = torch.from_numpy(rng.normal(size=(B, d.P)).astype(np.float32)).cuda()
             out = torch.zeros((B, d.ld), dtype=torch.float32, device="cuda")
             work = torch.empty(_lib.query("sglm_eta_bits_work_bytes", d.P, B),
@@ -41,7 +43,8 @@ def main():
 
             def fn():
                 _lib.call("sglm_gemv_eta_bits", d.rbits.data_ptr(), d.ld, d.P, beta.data_ptr(),
-                          B, slots.data_ptr(), 0, out.data_ptr(), work.data_ptr(), st)
+                          B, slots.data_ptr(), int(what == "eta3"), out.data_ptr(),
+                          work.data_ptr(), st)
         else:
             Bp = (B + 31) // 32 * 32
             rp = torch.zeros((3, Bp, d.ld), dtype=torch.bfloat16, device="cuda")

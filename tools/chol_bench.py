@@ -2,12 +2,14 @@
 (development tool): P = 2048, p = 2000, n representatives per call as the IRLS forms them.
 
 python tools/chol_bench.py [--n 1 3] [--reps 20] : prints JSON {n: ms per call} timed with HIP
-events on the launch stream (H restored from a copy before each call, outside the events).
+events on the launch stream (H restored from a copy before each call, outside the events), and
+the host time of the call itself (the captured graph's launch).
 """
 import argparse
 import json
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -46,24 +48,28 @@ def main():
                          device="cuda")
         fits = torch.arange(n, dtype=torch.int32, device="cuda")
         st = torch.cuda.current_stream().cuda_stream
-        times = []
+        times, host = [], []
         for rep in range(a.reps + 3):
             Hd.copy_(H0)
             info.zero_()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
+            h0 = time.perf_counter()
             _lib.call("sglm_chol_solve_inv", Hd.data_ptr(), Md.data_ptr(), P, fits.data_ptr(),
                       None, None, n, n, None, 0, None, dshd.data_ptr(), delta.data_ptr(),
                       info.data_ptr(), frozen.data_ptr(), n, cw.data_ptr(), st)
+            h1 = time.perf_counter()
             e1.record()
             torch.cuda.synchronize()
             if rep >= 3:
                 times.append(e0.elapsed_time(e1))
+                host.append((h1 - h0) * 1e3)
         # accuracy of the inverse: |U M - I| on the free block of fit 0
         U = np.triu(Hd[0].cpu().numpy()[: p + 1, : p + 1].astype(np.float64))
         M = np.triu(Md[0].cpu().numpy()[: p + 1, : p + 1].astype(np.float64))
         err = float(np.abs(U @ M - np.eye(p + 1)).max())
         out[n] = {"ms_median": float(np.median(times)), "ms_min": float(np.min(times)),
+                  "host_ms_median": float(np.median(host)),
                   "inv_err": err, "dropped": int(info.sum().item())}
     print(json.dumps(out))
 

@@ -1,6 +1,7 @@
 # Round artifacts: PMC traffic of the Gram (separate FETCH/WRITE passes), the default bench line
 # (with CPU baseline), the rocprofv3 kernel-trace summary of the same bench command, the C5,
-# session-prep and signal bench lines, and simulated 2/4/8-rank shares.  Everything lands under
+# session-prep, signal and design-matrix bench lines, a 2-rank gloo rehearsal of the sharded
+# bench on the one GPU, and simulated 2/4/8-rank shares.  Everything lands under
 # gpurun_out/prof (merged back by gpurun); copy what is judged into profiles/ afterwards.
 # Usage on the box: bash tools/gpu_profile.sh ROUND   (e.g. r02)
 set -e
@@ -16,6 +17,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt 
 timeout -k 10 300 python bench.py --config c5 > $O/bench_c5.json 2> $O/bench_c5.err
 timeout -k 10 300 python bench.py --config prep > $O/bench_prep.json 2> $O/bench_prep.err
 timeout -k 10 300 python bench.py --config signal > $O/bench_signal.json 2> $O/bench_signal.err
+timeout -k 10 300 python bench.py --config designmat > $O/bench_designmat.json 2> $O/bench_designmat.err
+timeout -k 10 400 python bench.py --gpus 2 --dist-backend gloo --no-cpu > $O/bench_g2_gloo.json 2> $O/bench_g2_gloo.err
 for w in 2 4 8; do
   timeout -k 10 300 python -u tools/rank_sim.py --world $w --all > $O/rank$w.json 2> $O/rank$w.err
 done
