@@ -462,9 +462,22 @@ __global__ void __launch_bounds__(256) eta_pair_absmax_kernel(
     const float* eb = eta + (int64_t)b * ld;
     const uint8_t* m = M + (int64_t)fit_mask[a] * ld;
     float mx = 0.0f;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * 256)
-        if (m[i]) mx = fmaxf(mx, fabsf(ea[i] - eb[i]));
+    // four consecutive rows per thread (4-byte mask / 16-byte eta loads; rows 16-byte aligned)
+    for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < n;
+         i += (int64_t)gridDim.x * 1024) {
+        if (i + 4 <= n) {
+            const uint32_t m4 = *reinterpret_cast<const uint32_t*>(m + i);
+            if (m4 == 0u) continue;
+            const f32x4 a4 = *reinterpret_cast<const f32x4*>(ea + i);
+            const f32x4 b4 = *reinterpret_cast<const f32x4*>(eb + i);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if ((m4 >> (8 * j)) & 0xffu) mx = fmaxf(mx, fabsf(a4[j] - b4[j]));
+        } else {
+            for (int64_t q2 = i; q2 < n; ++q2)
+                if (m[q2]) mx = fmaxf(mx, fabsf(ea[q2] - eb[q2]));
+        }
+    }
     for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
     __shared__ float sh[4];
     if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = mx;

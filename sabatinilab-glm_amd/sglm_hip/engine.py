@@ -89,10 +89,15 @@ SOLVE_INV = __import__("os").environ.get("SGLM_SOLVE_INV", "1") == "1"
 # "prio" (the same at high stream priority), "serial" (the main stream, before the gradient)
 CHOL_STREAM = __import__("os").environ.get("SGLM_CHOL_STREAM", "side")
 # SGLM_GRAM_PIPE=1: Grams computed one source at a time with each group's factorisation chain
-# started right behind its Gram.  Off by default: the per-group chains are latency-bound
+# started right behind its Gram -- measured slower: the per-group chains are latency-bound
 # (~1.1 ms each at 1-3 fits against 2.6 ms for one chain of 20), so the side stream carried
-# 28.6 instead of 12.1 ms per C4 grid and more of it was exposed (11.4 vs 7.1 ms)
-GRAM_PIPE = __import__("os").environ.get("SGLM_GRAM_PIPE", "0") == "1"
+# 28.6 instead of 12.1 ms per C4 grid and more of it was exposed (11.4 vs 7.1 ms).
+# SGLM_GRAM_PIPE=0: one Gram launch, then one chain.
+# SGLM_GRAM_PIPE=2: the sources in two batches -- one Gram launch and one chain per batch, the
+# first batch's chain overlapping the second batch's Grams -- also measured slower (C4 grid
+# 62.3 / 63.1 / 62.3 ms against 59.7 / 60.2 / 59.3 ms unpipelined, alternating on one box).
+# Default 0.
+GRAM_PIPE = int(__import__("os").environ.get("SGLM_GRAM_PIPE", "0") or 0)
 
 
 def _gram_groups(form, uniq, dup):
@@ -666,10 +671,14 @@ class IrlsStats:
         ("tol", "stagnation", "line_search_converged", "line_search_failed", "max_iter",
          "stale_factor_retry", "alias_dropped"), 0))
 
+    host_phases: bool = False   # host (enqueue) seconds per phase, no device syncs (tools)
+
     def mark(self, name, t0):
-        """Add the wall time since t0 (after a device sync) to phase `name`; returns now."""
+        """Add the wall time since t0 to phase `name` (after a device sync when trace_phases:
+        device + host time; without it the host's own time); returns now."""
         import time
-        torch.cuda.synchronize()
+        if self.trace_phases:
+            torch.cuda.synchronize()
         t = time.perf_counter()
         self.phases[name] = self.phases.get(name, 0.0) + (t - t0)
         return t
@@ -1098,7 +1107,8 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
     R_out, Rp_out = (_p(bf.R), None) if use_lag else (None, _p(rp_buf) if use_rp else None)
 
     import time
-    tick = stats.mark if (stats is not None and stats.trace_phases) else (lambda name, t: t)
+    tick = stats.mark if (stats is not None and (stats.trace_phases or stats.host_phases)) \
+        else (lambda name, t: t)
     t0 = tick("irls_setup", time.perf_counter())
     plan = None
     linked = None           # slot list whose link (and predictor update) is already enqueued
@@ -1161,7 +1171,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
             alias[:] = -1
             alias[ali] = repl[ali]
             pipe_groups = _gram_groups(form, uniq, dup) if (
-                GRAM_PIPE and SOLVE_INV and CHOL_STREAM != "serial") else None
+                GRAM_PIPE > 0 and SOLVE_INV and CHOL_STREAM != "serial") else None
             if pipe_groups is None:
                 _syrk(d, bf, np.sort(uniq).astype(np.int32), nsteps, ntile1, stats, st,
                       rows=rows)
@@ -1225,16 +1235,24 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
                 if pipe_groups is not None:
                     off = 0
                     dsrc = dict(dup)
-                    for r, grp in pipe_groups:
-                        _syrk(d, bf, np.array([r], dtype=np.int32), nsteps, ntile1, stats, st,
-                              rows=rows)
-                        for k in grp:
-                            if int(k) != int(r):
-                                bf.H[int(k)].copy_(bf.H[int(dsrc[int(k)])])
+                    if GRAM_PIPE == 1:                 # one source per batch
+                        batches = [[g] for g in pipe_groups]
+                    else:                              # two batches, the larger first
+                        h = (len(pipe_groups) + 1) // 2
+                        batches = [pipe_groups[:h], pipe_groups[h:]]
+                    for bt in batches:
+                        srcs = np.array(sorted(int(r) for r, _ in bt), dtype=np.int32)
+                        _syrk(d, bf, srcs, nsteps, ntile1, stats, st, rows=rows)
+                        nb_ = 0
+                        for r, grp in bt:
+                            for k in grp:
+                                if int(k) != int(r):
+                                    bf.H[int(k)].copy_(bf.H[int(dsrc[int(k)])])
+                            nb_ += int(len(grp))
                         ready = torch.cuda.Event()
                         ready.record()
-                        chains.append((ready, off, int(len(grp))))
-                        off += int(len(grp))
+                        chains.append((ready, off, nb_))
+                        off += nb_
                 else:
                     ready = torch.cuda.Event()
                     ready.record()
@@ -1571,7 +1589,8 @@ def irls_scored(prob: Problem, reqs: List[FitReq], sets: np.ndarray,
             with torch.cuda.stream(s):
                 sg = None
                 if stats is not None:
-                    sg = IrlsStats(record=stats.record, trace_phases=stats.trace_phases)
+                    sg = IrlsStats(record=stats.record, trace_phases=stats.trace_phases,
+                                   host_phases=stats.host_phases)
                 res, eta = irls(prob, [reqs[i] for i in idx], stats=sg)
                 sums = score_sums(prob, fam, power, eta, [fresp[i] for i in idx], sets[idx])
             s.synchronize()

@@ -416,8 +416,13 @@ def _mask_count(idx, multiplicity, n):
     """Row count of a spec (sum of multiplicities) without building the mask."""
     if idx is None:
         return float(n)
-    idx = F.wrap_indices(idx, n)
-    return float(idx.size if multiplicity else np.unique(idx).size)
+    if multiplicity:
+        # a fold list counts every entry: only the range check (numpy's IndexError), no wrap
+        a = np.asarray(idx).reshape(-1)
+        if a.size and (a.min() < -n or a.max() >= n):
+            F.wrap_indices(a, n)                             # raises with numpy's message
+        return float(a.size)
+    return float(np.unique(F.wrap_indices(idx, n)).size)
 
 
 def _score(method, obj: Objective, sums, st):

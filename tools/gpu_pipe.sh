@@ -3,10 +3,8 @@
 set -e
 export TMPDIR=/tmp
 O=gpurun_out/${1:-pipe}; mkdir -p $O
-timeout -k 10 200 python -u tools/chol_bench.py --n 1 6 20 --reps 10 > $O/chain_host.json 2> $O/chain_host.err
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_gpu_fullsize.py tests/test_gpu_api.py tests/test_gpu_kernels.py > $O/tests.log 2>&1
-for v in 1 0 1 0; do
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_gpu_fullsize.py tests/test_gpu_api.py > $O/tests.log 2>&1
+for v in 2 0 2 0 2 0; do
   SGLM_GRAM_PIPE=$v timeout -k 10 300 python bench.py --steps 5 --warmup 1 --no-cpu >> $O/bench_$v.json 2>> $O/bench_$v.err
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu > $O/kt.json 2> $O/kt.err
-timeout -k 10 300 python -u tools/ab_micro.py eta3 120,70,40,16 > $O/ab_eta3.log 2>&1

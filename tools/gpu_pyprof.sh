@@ -13,3 +13,5 @@ import pstats
 p = pstats.Stats('$O/bench.prof')
 p.sort_stats('cumulative').print_stats(60)
 " > $O/cumtime.txt
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu > $O/kt.json 2> $O/kt.err
+timeout -k 10 300 python bench.py --steps 5 --warmup 1 --no-cpu > $O/bench_plain.json 2> $O/bench_plain.err

@@ -82,6 +82,11 @@ def main():
             import pstats
             prof.disable()
             pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(25)
+    st = E.IrlsStats(record=True, host_phases=True)
+    grid.run(d, s.y, cv_idx, objs, [0] * nlam, stats=st, simulate=sim)
+    torch.cuda.synchronize()
+    out["host_phases_ms"] = {k: round(v * 1e3, 2) for k, v in st.phases.items()}
+    out["host_sync_wait_ms"] = round(st.sync_wait_s * 1e3, 2)
     for phases in (False, True):
         st = E.IrlsStats(record=True, trace_phases=phases)
         torch.cuda.synchronize()
