@@ -665,7 +665,11 @@ def main():
     N, m, L, K, nlam = CONFIGS[a.config]
     t_setup = time.perf_counter()
     s = synth.make(N=N, m=m, L=L, family="poisson", rho=0.02, seed=0)
-    design = E.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
+    # N > 1: each rank expands only its slab of the rows (row-sharded grid, comm.py), or the
+    # whole design when the grid is sharded by fits (SGLM_SHARD=fits)
+    rows_mode = world > 1 and grid.SHARD_MODE == "rows"
+    slab = grid.rank_slab(s.N, rank, world) if rows_mode else None
+    design = E.Design.from_events(s.E, s.shifts, s.L - 1, s.N, slab=slab)
     codes = folds.trial_keys_codes(__import__("pandas").DataFrame({"nTrial": s.trial}), ["nTrial"]).values
     np.random.seed(3)
     cv_idx = folds.cv_idx_from_bucket_ids(codes, num_folds=K)
@@ -715,6 +719,12 @@ def main():
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         elapsed = float(mx[0])
         t = sm
+        if rows_mode:
+            # every rank runs every fit: the fit / Newton / Gram counts and the algorithmic
+            # flop are the same on all ranks (not disjoint shares); the Gram launches, their
+            # time and flop and the host waits are per rank
+            for q in (1, 5, 6, 7, 8, 9, 10, 11, 12, 13):
+                t[q] /= world
     fit_iters, ktime, kflop, nlaunch = float(t[1]), float(t[2]), float(t[3]), int(t[4])
     gram_fits, alg_flop, reused, gram_iters = float(t[5]), float(t[6]), float(t[7]), float(t[8])
     stag, failed = int(t[9]), int(t[10])
@@ -772,7 +782,10 @@ def main():
                 "stagnation_or_failed_stops": stag + failed,
                 "newton_dist_f64": ndist,
                 "setup_s": round(setup_s, 2),
-                "parallelism": f"fit shards over {world} rank(s), RCCL all-gather of results",
+                "parallelism": (f"row slabs over {world} ranks: RCCL all-reduce of the slab "
+                                f"Grams, gradients, trial losses and directions" if rows_mode
+                                else f"fit shards over {world} rank(s), RCCL all-gather of "
+                                     f"results"),
             },
             "roofline": {
                 "bound": "mfma",

@@ -122,6 +122,14 @@ def _gram_groups(form, uniq, dup):
     return [(r, np.asarray(groups[r], dtype=np.int64)) for r in sorted(groups)]
 
 
+def _slab_info(slab, n: int):
+    """(start, stop, n) of a row slab, checked against n rows."""
+    s0, s1 = int(slab[0]), int(slab[1])
+    if not 0 <= s0 < s1 <= int(n):
+        raise ValueError(f"row slab {slab} outside 0..{n}")
+    return s0, s1, int(n)
+
+
 def require_gpu():
     """Raise unless the HIP engine can run (library present AND a ROCm device visible)."""
     _lib.load()
@@ -162,6 +170,8 @@ class Design:
         self.rbits = None      # row-major bit-planes [P/64][ld] x uint2 (MFMA eta) when 0/1
         self._cbits = None     # identity-row compacted planes [n/64][P] x uint2 (MFMA X^T R)
         self.lag = None        # LagStructure of a time-shifted 0/1 event design (from_events)
+        self.slab = None       # (start, stop, n_total): rows [start, stop) of an n_total-row
+        #                        design (one rank's share of a row-sharded solve, comm.py)
         self.device = device
 
     @property
@@ -174,13 +184,18 @@ class Design:
         return self.xf if self.xf is not None else self.xb
 
     @classmethod
-    def from_host(cls, X, device="cuda"):
-        """Pack a host (n x p) array / DataFrame (row-major) into HBM."""
+    def from_host(cls, X, device="cuda", slab=None):
+        """Pack a host (n x p) array / DataFrame (row-major) into HBM; ``slab`` = (start,
+        stop) packs only those rows (a rank's share of a row-sharded solve)."""
         if hasattr(X, "values") and not isinstance(X, np.ndarray):
             X = X.values
         X = np.asarray(X)
         if X.ndim == 1:
             X = X.reshape(-1, 1)
+        info = None
+        if slab is not None:
+            info = _slab_info(slab, X.shape[0])
+            X = X[info[0]:info[1]]
         if X.dtype not in (np.float32, np.float64):
             X = X.astype(np.float64)
         X = np.ascontiguousarray(X)
@@ -188,6 +203,7 @@ class Design:
         d = cls(n, p, device, zero=False)
         src = torch.from_numpy(X).to(device)
         d._pack(src, is_f64=X.dtype == np.float64, rs=p, cs=1)
+        d.slab = info
         return d
 
     @classmethod
@@ -229,7 +245,7 @@ class Design:
 
     @classmethod
     def from_events(cls, E, shifts: Sequence[int], row0: int, n: int, device="cuda",
-                    event_major=False):
+                    event_major=False, slab=None):
         """Expand base events E (N_raw x m) into lag columns directly on the device.
 
         Output column (shift block b, event a) = E[t + row0 - shifts[b], a] for rows
@@ -237,9 +253,14 @@ class Design:
         102-123) after the NaN-row drop (row0 = max positive shift), or event-major when
         ``event_major`` (setup_model_fit.timeshift_vals_by_dict, lag order as given).
         Source rows outside E can only occur if row0/n exceed the valid window; they are
-        filled with 0.
+        filled with 0.  ``slab`` = (start, stop): only rows [start, stop) of the n-row design
+        (a rank's share of a row-sharded solve, comm.py).
         """
         require_gpu()
+        info = None
+        if slab is not None:
+            info = _slab_info(slab, n)
+            row0, n = row0 + info[0], info[1] - info[0]
         if isinstance(E, np.ndarray):
             E = torch.from_numpy(np.ascontiguousarray(E, dtype=np.float32))
         E = E.to(device=device, dtype=torch.float32)
@@ -270,6 +291,7 @@ class Design:
             _lib.call("sglm_timeshift_expand", _p(Ef), N_raw, 1, N_raw, _p(cols_d), _p(sh_d),
                       p, _p(d.xf), n, 1, d.ld, row0, 4, 0, _stream())
             d.xf[p, :n] = 1.0
+        d.slab = info
         return d
 
     def cbits_full(self):
@@ -463,32 +485,46 @@ class Problem:
         self = cls.__new__(cls)
         self.design = design
         n, ld, dev = design.n, design.ld, design.device
+        # a slab design (row-sharded solve): the index lists address all n_total rows; the
+        # masks and responses are cut to the slab, the mask counts stay global
+        s0, s1, ntot = design.slab if design.slab is not None else (0, n, n)
         y = np.ascontiguousarray(np.asarray(y, dtype=np.float64).reshape(-1))
-        if y.shape[0] != n:
-            raise ValueError(f"response length {y.shape[0]} != n_samples {n}")
+        if y.shape[0] != ntot:
+            raise ValueError(f"response length {y.shape[0]} != n_samples {ntot}")
         nm = len(specs)
         buf = _pinned("problem_masks", max(nm * ld, 1), torch.uint8)
         ev = _scratch().pinned.get(("problem_masks_ev", None))
         if ev is not None:
             ev.synchronize()                                   # the previous upload has read it
-        nnz, sums = host_masks(specs, n, ld, buf.numpy())
+        if design.slab is None:
+            nnz, sums = host_masks(specs, n, ld, buf.numpy())
+        else:
+            ldt = pad_to(ntot + 1, ROW_PAD)
+            full = np.empty(max(nm * ldt, 1), dtype=np.uint8)
+            _, sums = host_masks(specs, ntot, ldt, full)
+            full = full[: nm * ldt].reshape(nm, ldt)
+            bm = buf.numpy()[: nm * ld].reshape(nm, ld)
+            bm[:, :n] = full[:, s0:s1]
+            bm[:, n:] = 0
+            nnz = np.count_nonzero(bm[:, :n], axis=1).astype(np.int64)
         self.M = torch.empty((nm, ld), dtype=torch.uint8, device=dev)
         self.M.view(-1).copy_(buf[: nm * ld], non_blocking=True)
-        yb = _pinned("problem_y", max(n, 1), torch.float64)
+        yb = _pinned("problem_y", max(ntot, 1), torch.float64)
         if ev is None:
             ev = torch.cuda.Event()
             _scratch().pinned[("problem_masks_ev", None)] = ev
-        yb[:n].copy_(torch.from_numpy(y))
-        yd = torch.empty(n, dtype=torch.float64, device=dev)
-        yd.copy_(yb[:n], non_blocking=True)
+        yb[:ntot].copy_(torch.from_numpy(y))
+        yd = torch.empty(ntot, dtype=torch.float64, device=dev)
+        yd.copy_(yb[:ntot], non_blocking=True)
         ev.record()
         rolls = [int(r) for r in rolls]
-        self._y64r = torch.stack([torch.roll(yd, r) for r in rolls]) if rolls else yd[None, :0]
+        self._y64r = (torch.stack([torch.roll(yd, r)[s0:s1] for r in rolls]) if rolls
+                      else yd[None, :0])
         self.Y = torch.zeros((len(rolls), ld), dtype=torch.float32, device=dev)
         self.Y[:, :n] = self._y64r.float()
         self._masks = None
         self._nnz = nnz
-        self._rolled = (y, rolls)
+        self._rolled = (y, rolls, s0, s1)
         self.Yd64 = None
         self._ylo = None
         self._stats = {("count", f): float(sums[f]) for f in range(nm)}
@@ -506,8 +542,8 @@ class Problem:
     @property
     def ys(self):
         if self._rolled is not None:
-            y, rolls = self._rolled
-            return [np.roll(y, r) for r in rolls]
+            y, rolls, s0, s1 = self._rolled
+            return [np.roll(y, r)[s0:s1] for r in rolls]
         return self._ys
 
     @ys.setter
@@ -788,7 +824,8 @@ def _pinned(tag, numel, dtype):
 
 
 _NP2TORCH = {np.dtype(np.int32): torch.int32, np.dtype(np.int64): torch.int64,
-             np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64}
+             np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64,
+             np.dtype(np.uint8): torch.uint8}
 
 
 class _Uploads:
@@ -893,8 +930,12 @@ def syrk6_splits(wgs1: int, nsteps: int, nact: int, P: int, slots: int = 1024) -
 
 
 def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
-         stats: Optional[IrlsStats] = None, bufs: Optional[_Buffers] = None):
-    """Run the batched damped-Newton (IRLS) solve; returns (results, final eta tensor)."""
+         stats: Optional[IrlsStats] = None, bufs: Optional[_Buffers] = None, comm=None):
+    """Run the batched damped-Newton (IRLS) solve; returns (results, final eta tensor).
+
+    ``comm`` (sglm_hip.comm.RowComm / SimComm): the problem holds one slab of the rows of a
+    row-sharded solve; sums over rows are all-reduced, maxima over rows max-reduced, and the
+    new factorisations are dealt over the ranks (see comm.py)."""
     require_gpu()
     if not reqs:
         return [], None
@@ -986,6 +1027,20 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
     nsteps = (n + 31) // 32
     ntile1 = (P // 256) * (P // 256 + 1) // 2
     rows = np.array([prob.mask_stats(r.resp, r.mask)[0] for r in reqs], dtype=np.float64)
+    # rows of the Grams this process computes (its slab's rows of each mask in a row-sharded
+    # solve; ``rows`` stays the fit's global count: penalty scale, alias ratios, flop count)
+    gram_rows = rows if comm is None else np.array([float(prob.mask_nnz(r.mask)) for r in reqs])
+    # row-sharded solve: the rank holding each slot's current factor, and whether the new
+    # factorisations are dealt over the ranks (explicit-inverse solves only)
+    dist_f = comm is not None and comm.distribute and SOLVE_INV
+    fowner = np.zeros(B0, dtype=np.int64)
+    rot = 0
+
+    def sum_hess(idx):
+        """The slab Grams of a row-sharded solve summed over the ranks (one all-reduce each)."""
+        if comm is not None:
+            for k in np.asarray(idx).reshape(-1):
+                comm.sum_(bf.H[int(k)])
     bf.prob, bf.fit_mask, bf.fit_mask_d = prob, fmask_h, fit_mask
     # cross-mask families (slot of the representative per slot, -1: none / is one)
     xmask_tol = 0.0 if const_hess else HESS_XMASK_TOL / max(1.0, abs(2.0 - power))
@@ -1050,6 +1105,8 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
             if npair > pd_h.numel():
                 raise RuntimeError("pair distance buffer too small")
             pd_d = _pair_dist_async(bf, prob, np.array(pairs, dtype=np.int32), n, ld, st)
+            if comm is not None:
+                comm.max_(pd_d)
             pd_h[:npair].copy_(pd_d, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record()
@@ -1143,6 +1200,8 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
                           _p(act_d), _p(bf.g), _p(gx_work), st)
             else:
                 d.xtr(bf.R, B, bf.g)
+            if comm is not None:
+                comm.sum_(bf.g[:B])
             torch.addcmul(bf.g[:B], lamp_d, beta64_d[:B], out=bf.gtot[:B])   # + lam * w
 
         # ---- Hessian
@@ -1155,7 +1214,8 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
                 for k in act:
                     reps.setdefault(reqs[k].mask, k)
                 rep_idx = np.array(sorted(reps.values()), dtype=np.int32)
-                _syrk(d, bf, rep_idx, nsteps, ntile1, stats, st, exact=True, rows=rows)
+                _syrk(d, bf, rep_idx, nsteps, ntile1, stats, st, exact=True, rows=gram_rows)
+                sum_hess(rep_idx)
                 gram_comp[rep_idx] = True
                 for k in act:
                     rk = reps[reqs[k].mask]
@@ -1171,10 +1231,11 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
             alias[:] = -1
             alias[ali] = repl[ali]
             pipe_groups = _gram_groups(form, uniq, dup) if (
-                GRAM_PIPE > 0 and SOLVE_INV and CHOL_STREAM != "serial") else None
+                GRAM_PIPE > 0 and SOLVE_INV and CHOL_STREAM != "serial" and comm is None) else None
             if pipe_groups is None:
                 _syrk(d, bf, np.sort(uniq).astype(np.int32), nsteps, ntile1, stats, st,
-                      rows=rows)
+                      rows=gram_rows)
+                sum_hess(uniq)
                 for k, rk in dup:
                     bf.H[k].copy_(bf.H[rk])
             else:
@@ -1202,6 +1263,18 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
             al = ali[np.argsort(repl[ali], kind="stable")] if (not const_hess and ali.size) \
                 else np.zeros(0, dtype=np.int64)
             src = repl[al]
+            if dist_f:
+                # row-sharded: this iteration's new factorisations dealt over the ranks; a
+                # rank factors and solves only on the factors it holds (its directions are
+                # summed with the other ranks' below)
+                fowner[order[:nref]] = comm.owners(int(nref), rot)
+                rot += int(nref)
+                mine_f = fowner == comm.rank
+                fo, ko = order[:nref], order[nref:]
+                fo, ko = fo[mine_f[fo]], ko[mine_f[ko]]
+                order, nref = np.concatenate([fo, ko]), int(fo.size)
+                sel = mine_f[src]
+                al, src = al[sel], src[sel]
             lst = np.concatenate([order, al]).astype(np.int32)
             fsrc = np.concatenate([order, src]).astype(np.int32)
             rsc = np.concatenate([np.ones(order.size), rows[src] / rows[al]]).astype(np.float32)
@@ -1242,7 +1315,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
                         batches = [pipe_groups[:h], pipe_groups[h:]]
                     for bt in batches:
                         srcs = np.array(sorted(int(r) for r, _ in bt), dtype=np.int32)
-                        _syrk(d, bf, srcs, nsteps, ntile1, stats, st, rows=rows)
+                        _syrk(d, bf, srcs, nsteps, ntile1, stats, st, rows=gram_rows)
                         nb_ = 0
                         for r, grp in bt:
                             for k in grp:
@@ -1272,10 +1345,15 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
                 t0 = tick("it_gradient", t0)
             if fact_done is not None:
                 torch.cuda.current_stream().wait_event(fact_done)
-            _lib.call("sglm_chol_solve_inv", _p(bf.H), _p(bf.Minv), P, _p(ints),
-                      _p(ints[nl:]), _p(rsc_d), nl, 0, _p(ints[2 * nl:]), len(tiles),
-                      _p(bf.gtot), _p(bf.dshift), _p(bf.delta), _p(bf.info), _p(bf.frozen), B,
-                      _p(bf.cwork), st)
+            if nl:
+                _lib.call("sglm_chol_solve_inv", _p(bf.H), _p(bf.Minv), P, _p(ints),
+                          _p(ints[nl:]), _p(rsc_d), nl, 0, _p(ints[2 * nl:]), len(tiles),
+                          _p(bf.gtot), _p(bf.dshift), _p(bf.delta), _p(bf.info), _p(bf.frozen),
+                          B, _p(bf.cwork), st)
+            if comm is not None and (dist_f or not comm.distribute):
+                owned = np.zeros(B0, dtype=np.uint8)
+                owned[lst] = 1
+                comm.directions_(bf.delta[:B], up(owned, np.uint8))
         else:
             _gradient()
             t0 = tick("it_gradient", t0)
@@ -1307,6 +1385,9 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
         _lib.call("sglm_loss_trials_max", fam, power, n, ld, na, _p(act_d), _p(bf.eta),
                   _p(bf.deta), _p(prob.Y), _p(prob.M), _p(fit_resp), _p(fit_mask), _p(tv1), 5,
                   _p(Ltr), _p(dmax_d), _p(xtr_work), st)
+        if comm is not None:
+            comm.sum_(Ltr[: na * 5])
+            comm.max_(dmax_d[:na])
         L_h[: na * 5].copy_(Ltr[: na * 5], non_blocking=True)
         dmax_h[:na].copy_(dmax_d[:na], non_blocking=True)
         sc_h = _pinned("sc", sc.numel(), torch.float64)
@@ -1343,6 +1424,8 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
             _lib.call("sglm_loss_trials", fam, power, n, ld, int(more.size), _p(sub_d),
                       _p(bf.eta), _p(bf.deta), _p(prob.Y), _p(prob.M), _p(fit_resp),
                       _p(fit_mask), _p(tv2), 7, _p(Ltr), _p(xtr_work), st)
+            if comm is not None:
+                comm.sum_(Ltr[: more.size * 7])
             t_sync = time.perf_counter()
             L2 = Ltr[: more.size * 7].view(more.size, 7).cpu().numpy()
             if stats is not None:
@@ -1469,7 +1552,14 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
     out_beta[:] = beta64_d.cpu().numpy()
     out_iter[:] = n_iter
     out_conv[:] = converged
-    out_info[:] = bf.info[:B].cpu().numpy()
+    if dist_f:
+        # a factor's dropped-pivot count lives on the rank that formed it
+        inf = bf.info[:B].clone()
+        inf[torch.from_numpy(fowner != comm.rank).to(dev)] = 0
+        comm.sum_owned_(inf)
+        out_info[:] = inf.cpu().numpy()
+    else:
+        out_info[:] = bf.info[:B].cpu().numpy()
     bf.prob = bf.keep = bf.up = bf.fit_mask_d = None   # drop the compacted designs with the problem
     # final linear predictor from the final coefficients, in request order (no accumulated
     # drift)
@@ -1544,7 +1634,7 @@ def _partition(reqs: List[FitReq], ngroups: int, rows=None) -> List[List[int]]:
 
 
 def irls_scored(prob: Problem, reqs: List[FitReq], sets: np.ndarray,
-                stats: Optional[IrlsStats] = None, ngroups: Optional[int] = None):
+                stats: Optional[IrlsStats] = None, ngroups: Optional[int] = None, comm=None):
     """IRLS + score sums for a batch, as ``ngroups`` independent fit groups, each driven by
     its own host thread on its own HIP stream.  A group's latency-bound phases (the blocked
     Cholesky chain, the host decisions between iterations) then run while another group's
@@ -1557,10 +1647,10 @@ def irls_scored(prob: Problem, reqs: List[FitReq], sets: np.ndarray,
     # a rank's share at 8 GPUs (~15 fits) runs as one group
     rows = [prob.mask_stats(r.resp, r.mask)[0] for r in reqs]
     parts = (_partition(reqs, ng, rows) if ng > 1 and len(reqs) >= IRLS_GROUP_MIN * ng
-             else [list(range(len(reqs)))])
+             and comm is None else [list(range(len(reqs)))])
     if len(parts) == 1:
-        res, eta = irls(prob, reqs, stats=stats)
-        return res, score_sums(prob, fam, power, eta, fresp, sets)
+        res, eta = irls(prob, reqs, stats=stats, comm=comm)
+        return res, score_sums(prob, fam, power, eta, fresp, sets, comm=comm)
     d = prob.design
     # shared lazily-built state, built once here before the threads start
     for r in reqs:
@@ -1778,8 +1868,9 @@ def _syrk_cbits(d: Design, bf, prob: Problem, fits: np.ndarray, st, ev=None):
 
 
 def score_sums(prob: Problem, family: int, power: float, eta, fit_resp: Sequence[int],
-               sets: np.ndarray) -> np.ndarray:
-    """[B, 2, 2] float64: per fit and set (train, test): sum m (y - mu)^2, sum m loss."""
+               sets: np.ndarray, comm=None) -> np.ndarray:
+    """[B, 2, 2] float64: per fit and set (train, test): sum m (y - mu)^2, sum m loss
+    (summed over the ranks' slabs of a row-sharded solve when ``comm`` is given)."""
     d = prob.design
     B = len(fit_resp)
     dev = d.device
@@ -1789,4 +1880,6 @@ def score_sums(prob: Problem, family: int, power: float, eta, fit_resp: Sequence
     work = _work(_lib.query("sglm_rowsum_work_bytes", B, 4, d.n), dev)
     _lib.call("sglm_score_sums", family, float(power), d.n, d.ld, B, _p(eta), _p(prob.Y),
               _p(prob.M), _p(fr), _p(sd), _p(out), _p(work), _stream())
+    if comm is not None:
+        comm.sum_(out)
     return out.cpu().numpy().reshape(B, 2, 2)

@@ -21,6 +21,7 @@ all-gathered (one RCCL collective over xGMI at the end).
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -37,15 +38,22 @@ class _MaskStats:
     responses per power (the reference computes them per fold on host copies,
     backend/sglm.py:150-184, 388-408)."""
 
-    def __init__(self, prob: E.Problem):
+    def __init__(self, prob: E.Problem, comm=None):
         import torch
         from . import _lib
         self.torch, self._lib = torch, _lib
         self.prob = prob
+        self.comm = comm
         n, dev = prob.design.n, prob.design.device
         self.Yd = prob.y64_rows()                        # R x n float64 (device)
         self.F, self.R, self.n = prob.M.shape[0], self.Yd.shape[0], n
-        self.Kd = self.Yd.mean(dim=1)                    # per-response shift
+        if comm is None:
+            self.Kd = self.Yd.mean(dim=1)                # per-response shift
+        else:                                            # the global mean over all slabs
+            tot = self.Yd.sum(dim=1)
+            comm.sum_(tot)
+            d = prob.design
+            self.Kd = tot / float(d.n if d.slab is None else d.slab[2])
         self.K = self.Kd.cpu().numpy()
         self.work = torch.empty(_lib.query("sglm_mask_stats_work_bytes", self.F, self.R, n),
                                 dtype=torch.uint8, device=dev)
@@ -67,6 +75,12 @@ class _MaskStats:
         _lib.call("sglm_mask_stats", prob.M.data_ptr(), prob.M.shape[1], self.F,
                   self.Yd.data_ptr(), self.R, self.n, self.Kd.data_ptr(), float(power),
                   out.data_ptr(), self.work.data_ptr(), E._stream())
+        if self.comm is not None:
+            # counts, centred sums and loss constants add over the slabs; min y is a minimum
+            sums, ymin = out[:, :, :4].contiguous(), out[:, :, 4].contiguous()
+            self.comm.sum_(sums)
+            self.comm.min_(ymin)
+            out = torch.cat([sums, ymin[:, :, None]], dim=2)
         return out.cpu().numpy()
 
     def _consts(self, power):
@@ -110,6 +124,27 @@ def _dist():
 
 
 SHARD_PLAN = "mask_major"                    # or "round_robin" (comparison runs)
+# "rows": a process group splits the rows of the grid (every rank runs every fit on its slab,
+# sums all-reduced; comm.py) -- the default for log-link IRLS grids; "fits": whole fits (cross-
+# mask families) per rank with one all-gather of the results
+SHARD_MODE = os.environ.get("SGLM_SHARD", "rows")
+
+
+def rank_slab(n: int, rank: Optional[int] = None, world: Optional[int] = None):
+    """Rows [start, stop) of a rank's slab of an n-row design in a row-sharded grid (the
+    current process group's rank / world by default)."""
+    from .comm import row_slab
+    if rank is None or world is None:
+        d = _dist()
+        rank, world = (d.get_rank(), d.get_world_size()) if d else (0, 1)
+    return row_slab(n, rank, world)
+
+
+def row_sharded(groups=None) -> bool:
+    """True when a grid run now (process group of > 1 rank) splits rows, not fits."""
+    if _dist() is None or SHARD_MODE != "rows":
+        return False
+    return groups is None or all(o.kind == "irls" for g in groups for o in g["objectives"])
 
 
 def shard_indices(total: int, rank: int, world: int):
@@ -158,6 +193,8 @@ def run(X, y, cv_idx, objectives: Sequence[Objective], rolls: Sequence[int],
         simulate=None):
     """Return one result dict per objective (reference key set minus glm_kwargs/model).
 
+    ``simulate=comm.SimComm`` (development only): one rank's slab of a row-sharded grid
+    (or, with ``SimComm.recorder()`` and the full design, the recording it replays).
     ``simulate=(rank, world)`` (development only) solves just that rank's share without a
     process group and returns the raw per-fit results instead of the assembled dicts."""
     out = run_multi(X, y, [{"cv_idx": cv_idx, "objectives": objectives, "rolls": rolls}],
@@ -243,17 +280,43 @@ def run_multi(X, y, groups: Sequence[dict], score_method: str = "mse", coef0=Non
     import time
     tick = stats.mark if (stats is not None and stats.trace_phases) else (lambda name, t: t)
     t0 = tick("-", time.perf_counter())
-    design = X if isinstance(X, E.Design) else E.Design.from_host(X)
-    n, p = design.n, design.p
+    from .comm import RowComm, SimComm, row_slab
+    dist = _dist() if shard and simulate is None else None
+    irls_only = all(o.kind == "irls" for g in groups for o in g["objectives"])
+    comm = None
+    if isinstance(simulate, SimComm):
+        comm = simulate                          # one rank of a row-sharded solve, simulated
+    elif (dist is not None and SHARD_MODE == "rows" and irls_only
+          and not (isinstance(X, E.Design) and X.slab is None)):
+        # host X is packed per slab here; a device Design must already be this rank's slab
+        # (Design.from_events / from_host with slab=grid.rank_slab(n)) -- a full Design in a
+        # process group is sharded by fits instead
+        comm = RowComm(dist)
+    if isinstance(X, E.Design):
+        design = X
+    else:
+        design = E.Design.from_host(X, slab=None if comm is None else row_slab(
+            np.asarray(X).shape[0], comm.rank, comm.world))
+    if design.slab is not None and comm is None:
+        raise ValueError("a slab design needs a row-sharded process group (or a SimComm)")
+    if comm is not None and comm.world > 1 and (design.slab is None or row_slab(
+            design.slab[2], comm.rank, comm.world) != tuple(design.slab[:2])):
+        raise ValueError(f"design slab {design.slab} is not rank {comm.rank}/{comm.world}'s "
+                         "row slab (grid.rank_slab)")
+    n = design.n if design.slab is None else design.slab[2]
+    p = design.p
     y = np.asarray(y, dtype=np.float64).reshape(-1)
     if y.shape[0] != n:
         raise ValueError(f"y has {y.shape[0]} rows, X has {n}")
     plan = plan_fits(groups, n)
     specs, gm, counts, table, roll_list = plan
     t0 = tick("grid_setup", t0)
-    dist = _dist() if shard and simulate is None else None
-    rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (simulate or (0, 1))
-    mine = rank_share(plan, groups, rank, world)
+    if comm is not None:
+        # row-sharded: every rank runs every fit over its slab of the rows
+        mine = list(range(len(table)))
+    else:
+        rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (simulate or (0, 1))
+        mine = rank_share(plan, groups, rank, world)
 
     # only the masks (and responses) of this rank's fits are built and uploaded
     used = sorted({table[i][3] for i in mine} | {table[i][5] for i in mine if table[i][5] >= 0})
@@ -261,7 +324,7 @@ def run_multi(X, y, groups: Sequence[dict], score_method: str = "mse", coef0=Non
     prob = E.Problem.from_index_lists(design, y, roll_list,
                                       [(specs[mid][0], specs[mid][1]) for mid in used])
     t0 = tick("setup_problem", t0)
-    ms = _MaskStats(prob)
+    ms = _MaskStats(prob, comm)
     for i in mine:                           # the IRLS setup reads these, not host passes
         _, _, _, m, r, _ = table[i]
         prob.seed_stats(r, local[m], float(ms.cnt[local[m]]), float(ms.sy[local[m], r]))
@@ -274,7 +337,7 @@ def run_multi(X, y, groups: Sequence[dict], score_method: str = "mse", coef0=Non
         if groups[table[i][0]]["objectives"][table[i][1]].family == E.FAM_TWEEDIE_LOG:
             st_ = ms.get(r, local[m])
             bad |= int(bool(st_["cnt"]) and (st_["ymin"] < 0 or st_["mean"] <= 0))
-    if dist is not None:
+    if dist is not None and comm is None:
         import torch
         flag = torch.tensor([bad], dtype=torch.int32,
                             device="cuda" if dist.get_backend() == "nccl" else "cpu")
@@ -313,7 +376,7 @@ def run_multi(X, y, groups: Sequence[dict], score_method: str = "mse", coef0=Non
             sums = E.score_sums(prob, E.FAM_SQUARED, 0.0, eta, [table[i][4] for i in idxs],
                                 sets)
         else:
-            res, sums = E.irls_scored(prob, reqs, sets, stats=stats)
+            res, sums = E.irls_scored(prob, reqs, sets, stats=stats, comm=comm)
         t0 = tick("solve", t0)
         for q, i in enumerate(idxs):
             rr = res[q]
@@ -336,7 +399,8 @@ def run_multi(X, y, groups: Sequence[dict], score_method: str = "mse", coef0=Non
     t0 = tick("score_sums", t0)
     if simulate is not None:
         return results
-    results = merge_results(results, dist)
+    if comm is None:
+        results = merge_results(results, dist)
 
     out_all = assemble(groups, plan, results, p)
     tick("assemble", t0)

@@ -5,7 +5,9 @@ Every rank: the C3-shape design (Poisson 100k x 500, 5 trial-id splits, 20 lambd
 from the same seeds, ``grid.run`` inside an initialised process group -- so the product's
 own path runs: rank_share -> the rank's batched IRLS on the device -> the y-range all-reduce
 -> grid.merge_results (all_gather_object) -> assemble.  Rank 0 writes the assembled result to
-argv[1] (npz).  All ranks may share one GPU (rehearsal of the N-GPU run on one card)."""
+argv[1] (npz).  All ranks may share one GPU (rehearsal of the N-GPU run on one card).
+argv[3] = "fits" (whole fits per rank, full design on every rank) or "rows" (every rank
+expands only its row slab and runs every fit on it; sums over rows all-reduced, comm.py)."""
 import os
 import sys
 
@@ -18,6 +20,7 @@ import pandas as pd  # noqa: E402
 
 def main():
     out_path, backend = sys.argv[1], sys.argv[2]
+    mode = sys.argv[3] if len(sys.argv) > 3 else "fits"
     import torch
     import torch.distributed as dist
     local = int(os.environ["LOCAL_RANK"])
@@ -28,8 +31,10 @@ def main():
         dist.init_process_group("gloo")
     from sglm_hip import engine as E, folds, grid, synth
     from sglm_hip.estimators import Objective
+    grid.SHARD_MODE = mode
     s = synth.make(N=100_000, m=25, L=10, family="poisson", rho=0.02, seed=0)
-    d = E.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
+    slab = grid.rank_slab(s.N) if mode == "rows" else None
+    d = E.Design.from_events(s.E, s.shifts, s.L - 1, s.N, slab=slab)
     codes = folds.trial_keys_codes(pd.DataFrame({"nTrial": s.trial}), ["nTrial"]).values
     np.random.seed(3)
     cv_idx = folds.cv_idx_from_bucket_ids(codes, num_folds=5)
@@ -37,7 +42,8 @@ def main():
     objs = [Objective("irls", E.FAM_TWEEDIE_LOG, 1.0, float(a), "n", True, 100) for a in lams]
     groups = [{"cv_idx": cv_idx, "objectives": objs, "rolls": [0] * len(objs)}]
     plan = grid.plan_fits(groups, s.N)
-    mine = grid.rank_share(plan, groups, dist.get_rank(), dist.get_world_size())
+    mine = (list(range(len(plan[3]))) if mode == "rows"
+            else grid.rank_share(plan, groups, dist.get_rank(), dist.get_world_size()))
     res = grid.run(d, s.y, cv_idx, objs, [0] * len(objs), score_method="r2")
     shares = [None] * dist.get_world_size()
     dist.all_gather_object(shares, mine)

@@ -188,3 +188,23 @@ def test_hessian_copies_resolve_to_formed_hessians():
                                    np.array([0.1, 0.1]), 0.375)
     assert keep.tolist() == [0] and [(k, r) for k, r, _ in shared] == [(1, 0), (2, 0)]
     assert abs(shared[1][2] - 0.2) < 1e-12
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 1000, 100_000, 1_000_000])
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_row_slabs_cover_the_rows(n, world):
+    """Row-sharded grids (sglm_hip/comm.py): the slabs of all ranks tile [0, n) in order,
+    inner boundaries on 64-row blocks, sizes within one block of n / world."""
+    from sglm_hip.comm import row_slab
+    if n < world:
+        with pytest.raises(ValueError):
+            row_slab(n, 0, world)
+        return
+    sl = [row_slab(n, r, world) for r in range(world)]
+    assert sl[0][0] == 0 and sl[-1][1] == n
+    assert all(a[1] == b[0] for a, b in zip(sl, sl[1:]))
+    assert all(e > s for s, e in sl)
+    if n >= 64 * world:
+        assert all(b[0] % 64 == 0 for b in sl[1:])
+    if n >= 64 * world:
+        assert all(abs((e - s) - n / world) <= 64 for s, e in sl)

@@ -4,6 +4,12 @@ python tools/rank_sim.py --world 8 [--rank R | --all] [--plan mask_major|round_r
 solves one rank's share of the C4 grid (grid.shard_plan) after a warm-up, with device syncs
 at phase boundaries, and prints the phase breakdown; --all times every rank and reports the
 max over ranks (what an N-GPU grid's wall-clock follows).
+
+--mode rows: the row-sharded grid (sglm_hip/comm.py).  One recording of the unsharded grid
+keeps every collective's global value and every iteration's directions (SimComm.recorder);
+each rank's slab design is then expanded alone and timed replaying it: the slab's own work,
+its share of the factorisations, the collectives' results copied in.  The collectives are
+NOT timed (no process group): their count and bytes per grid are reported.
 """
 import argparse
 import json
@@ -24,6 +30,7 @@ def main():
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--all", action="store_true")
     ap.add_argument("--plan", default="mask_major")
+    ap.add_argument("--mode", default="fits", choices=["fits", "rows"])
     a = ap.parse_args()
     import bench
     import pandas as pd
@@ -39,6 +46,58 @@ def main():
     objs = [Objective("irls", E.FAM_TWEEDIE_LOG, 1.0, float(al), "n", True, 100)
             for al in np.logspace(-4, 1, nlam)]
     grid.SHARD_PLAN = a.plan
+    if a.mode == "rows":
+        from sglm_hip.comm import SimComm, row_slab
+        import gc
+        rec = SimComm.recorder()
+        grid.run(d, s.y, cv_idx, objs, [0] * nlam, simulate=rec)
+        del d
+        gc.collect()
+        torch.cuda.empty_cache()
+        per = []
+        ranks = list(range(a.world)) if a.all else [a.rank]
+        for r in ranks:
+            dr = E.Design.from_events(s.E, s.shifts, s.L - 1, s.N,
+                                      slab=row_slab(s.N, r, a.world))
+            for _ in range(int(os.environ.get("SIM_WARMUPS", "2"))):
+                grid.run(dr, s.y, cv_idx, objs, [0] * nlam, simulate=rec.replay(r, a.world))
+            gc.collect()
+            st = E.IrlsStats(record=True)
+            rp = rec.replay(r, a.world)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            res = grid.run(dr, s.y, cv_idx, objs, [0] * nlam, stats=st, simulate=rp)
+            torch.cuda.synchronize()
+            per.append({"rank": r, "rows": list(dr.slab), "wall_ms": round(
+                (time.perf_counter() - t0) * 1e3, 2), "fits": len(res),
+                "fit_iters": st.fit_iters, "newton_iters": st.newton_iters,
+                "gram_fits": st.gram_fits, "gram_ms": round(sum(
+                    e0.elapsed_time(e1) for e0, e1, _, _ in st.syrk_events), 2),
+                "collectives": rp.calls, "collective_mb": round(rp.bytes / 2 ** 20, 1)})
+            if r == ranks[0] and os.environ.get("SIM_CPROFILE"):
+                import cProfile
+                import pstats
+                prof = cProfile.Profile()
+                prof.enable()
+                grid.run(dr, s.y, cv_idx, objs, [0] * nlam, simulate=rec.replay(r, a.world))
+                torch.cuda.synchronize()
+                prof.disable()
+                ps = pstats.Stats(prof, stream=sys.stderr)
+                ps.sort_stats("tottime").print_stats(45)
+                ps.sort_stats("cumulative").print_stats(60)
+            if r == ranks[0]:
+                # phase breakdown of the first rank (device syncs at phase boundaries)
+                st = E.IrlsStats(record=True, trace_phases=True)
+                grid.run(dr, s.y, cv_idx, objs, [0] * nlam, stats=st,
+                         simulate=rec.replay(r, a.world))
+                per[-1]["phases_ms"] = {k: round(v * 1e3, 2) for k, v in st.phases.items()}
+            del dr
+            gc.collect()
+            torch.cuda.empty_cache()
+        print(json.dumps({"mode": "rows", "world": a.world, "per_rank": per,
+                          "max_ms": max(q["wall_ms"] for q in per),
+                          "note": "collectives not timed (one GPU, no process group)"}))
+        return
     if a.all:
         per = []
         import gc
