@@ -439,6 +439,28 @@ int sglm_lag_xtr(const int32_t* occ, const int32_t* tbeg, const int32_t* tend,
                  int64_t n, int32_t P, const float* R, int64_t ld, const int32_t* slots,
                  int32_t nact, double* g, void* work, sglm_stream_t stream);
 
+/* sglm_xtr_prefer(1): this thread's following sglm_xtr_bits / _packed calls use the
+ * one-fit-group four-panel gradient kernel (fewer registers per lane, so work on another
+ * stream -- the factorisation chain -- can share the SIMDs); -1 restores the automatic choice. */
+int sglm_xtr_prefer(int32_t variant);
+
+/* --- Gram of a time-shifted event design at a constant weight ---------------------------
+ * H[fits[q]] = bf16(W[fits[q] * ldw]) * X^T X (f32, the 128-blocks I <= J of the P x P upper
+ * triangle; other entries untouched) over design rows t < n of the design above (layout 0 / 1,
+ * the ones column at m*K, zero padding to P), from the occurrences: occ / ev_off (event-major
+ * ascending rows, segment offsets [m + 1]), ebits = [m][nwords] occurrence bitmap of E (bit
+ * v & 31 of word v >> 5, n_raw rows), smin / smax = min / max of shifts (span <= 2048).  The
+ * Hessian of every all-rows fit at its intercept-only start (constant weight on every row):
+ * the first Newton iteration's Gram of engine.irls, which replaces the first cho_solve
+ * Hessian of sklearn's NewtonCholeskySolver on the expanded design (_newton_solver.py,
+ * backend/sglm.py:112-115).  work: sglm_lag_gram_work_bytes(m, smin, smax). */
+size_t sglm_lag_gram_work_bytes(int32_t m, int32_t smin, int32_t smax);
+int sglm_lag_gram(const int32_t* occ, const int32_t* ev_off, const uint32_t* ebits,
+                  int64_t nwords, const int32_t* shifts, int32_t m, int32_t K, int32_t layout,
+                  int32_t smin, int32_t smax, int64_t row0, int64_t n, int64_t n_raw, int32_t P,
+                  const float* W, int64_t ldw, const int32_t* fits, int32_t nfits, float* H,
+                  void* work, sglm_stream_t stream);
+
 /* --- event design matrix (pp_design_mat.make_design_mat, pp_design_mat.py:6-205) --------
  * Float64 session columns (a pandas float block) on the device.  A pandas groupby over a float
  * key is a GROUPING here:

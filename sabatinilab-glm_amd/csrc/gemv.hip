@@ -484,8 +484,11 @@ constexpr int kRS = 144;            // LDS bytes per fit segment (128 + pad)
 // NGW = 32-fit groups per workgroup: with two, every expanded bit fragment feeds six MFMAs
 // (three pieces x two groups) instead of three -- the bit expansion is VALU work that the
 // single MFMA stream of a one-wave-per-SIMD kernel cannot hide.
-template <int NGW>
-__global__ void __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(1, 1)))
+// WPE = waves per SIMD: 2 (one fit group, <= 256 registers per lane) doubles the loads in
+// flight of the latency-bound small batches, at the price of the SIMD room a concurrent
+// factorisation chain needs.
+template <int NGW, int WPE = 1>
+__global__ void __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 xtr_bits4_kernel(const u32x2* __restrict__ cbits, int64_t ld, int32_t P, int64_t nblk,
                  const __bf16* __restrict__ Rp, int32_t Bp, int32_t B, int32_t splits,
                  float* __restrict__ part) {
@@ -620,15 +623,23 @@ xtr_bits4_kernel(const u32x2* __restrict__ cbits, int64_t ld, int32_t P, int64_t
 //       1.19 / 1.13 / 1.08 ms for variants 2 / 1 / 0 in one process);
 //   1 = four-panel, one group -- only on request.
 // SGLM_XTR4=0 forces 0, SGLM_XTR_NGW=1 / 2 force 1 / 2 where P allows.
+// sglm_xtr_prefer(1) (per thread) asks for the one-group four-panel kernel: 262 registers
+// per lane leave room on every SIMD for the factorisation chain's waves (the two-group kernel
+// holds all 512), so a chain running beside the gradient progresses instead of waiting for it.
+static thread_local int t_xtr_prefer = -1;
 static int xtr_variant(int32_t P, int32_t B) {
     const int ngrp = (B + 31) / 32;
     if (P % (32 * kXT * kXW) != 0) return 0;
+    if (t_xtr_prefer == 1) return 1;
+    const char* e3 = getenv("SGLM_XTR_WPE2");
+    const bool wpe2 = !(e3 && e3[0] == '0');
     const char* e4 = getenv("SGLM_XTR4");
     if (e4 && e4[0] == '0') return 0;
     const char* e = getenv("SGLM_XTR_NGW");
     if (e && e[0] == '1') return 1;
     if (e && e[0] == '2') return ngrp >= 2 ? 2 : 1;
-    return (ngrp >= 2 && ngrp % 2 == 0) ? 2 : 0;
+    if (ngrp >= 2 && ngrp % 2 == 0) return 2;
+    return wpe2 ? 3 : 0;
 }
 
 static void launch_xtr_bits(const u32x2* cbits, int64_t ld, int32_t P, int64_t nblk,
@@ -636,9 +647,13 @@ static void launch_xtr_bits(const u32x2* cbits, int64_t ld, int32_t P, int64_t n
                             hipStream_t s) {
     const int v = xtr_variant(P, B);
     const unsigned tiles = (unsigned)((P / (32 * kXT)) * (Bp / 32) * splits);
-    const unsigned wgs4 = (unsigned)((P / (32 * kXT * kXW)) * ((Bp / 32 + v - 1) / (v ? v : 1)) *
+    const int ngw = v == 2 ? 2 : 1;
+    const unsigned wgs4 = (unsigned)((P / (32 * kXT * kXW)) * ((Bp / 32 + ngw - 1) / ngw) *
                                      splits);
-    if (v == 2)
+    if (v == 3)
+        xtr_bits4_kernel<1, 2><<<wgs4, 64 * kXW, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, B, splits,
+                                                         part);
+    else if (v == 2)
         xtr_bits4_kernel<2><<<wgs4, 64 * kXW, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, B, splits, part);
     else if (v == 1)
         xtr_bits4_kernel<1><<<wgs4, 64 * kXW, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, B, splits, part);
@@ -667,9 +682,10 @@ __global__ void __launch_bounds__(256) reduce_slabs_f64(const float* __restrict_
 // nearly empty extra round.  four = the four-panel kernel.
 static int xtr_splits_for(int32_t P, int32_t B, int64_t nblk, int variant) {
     const int64_t ngrp = (B + 31) / 32;
-    const int64_t wps = variant ? (P / (32 * kXT * kXW)) * ((ngrp + variant - 1) / variant)
+    const int ngw = variant == 2 ? 2 : 1;
+    const int64_t wps = variant ? (P / (32 * kXT * kXW)) * ((ngrp + ngw - 1) / ngw)
                                 : (P / (32 * kXT)) * ngrp;
-    const int64_t resident = variant ? 256 : 1024;
+    const int64_t resident = variant == 3 ? 512 : variant ? 256 : 1024;
     const int64_t cap = nblk / 32 > 1 ? nblk / 32 : 1;      // >= 32 K-steps per slab
     int best = 1;
     double bestc = 1e300;
@@ -688,7 +704,7 @@ static int xtr_bits_splits(int32_t P, int32_t B, int64_t nblk) {
 }
 // workspace bound over every variant (the switches may change between the query and a launch)
 static size_t xtr_part_bytes(int32_t P, int32_t B, int64_t nblk) {
-    const int s = std::max(xtr_splits_for(P, B, nblk, 0),
+    const int s = std::max(std::max(xtr_splits_for(P, B, nblk, 0), xtr_splits_for(P, B, nblk, 3)),
                            std::max(xtr_splits_for(P, B, nblk, 1), xtr_splits_for(P, B, nblk, 2)));
     return (size_t)s * B * P * sizeof(float);
 }
@@ -698,6 +714,11 @@ static size_t xtr_part_bytes(int32_t P, int32_t B, int64_t nblk) {
 using namespace sglm;
 
 extern "C" {
+
+int sglm_xtr_prefer(int32_t variant) {
+    t_xtr_prefer = variant == 1 ? 1 : -1;
+    return SGLM_OK;
+}
 
 int sglm_pack_bits_t(const uint16_t* Xb, int64_t ld, int32_t P, uint32_t* out,
                      int32_t* nonbinary, sglm_stream_t stream) {

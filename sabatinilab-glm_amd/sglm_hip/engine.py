@@ -88,6 +88,13 @@ SOLVE_INV = __import__("os").environ.get("SGLM_SOLVE_INV", "1") == "1"
 # where the factorisation chain runs: "side" (its own stream, overlapping the gradient),
 # "prio" (the same at high stream priority), "serial" (the main stream, before the gradient)
 CHOL_STREAM = __import__("os").environ.get("SGLM_CHOL_STREAM", "side")
+# gradient kernel that co-resides with the factorisation chain in iterations that form factors
+XTR_COCHAIN = __import__("os").environ.get("SGLM_XTR_COCHAIN", "1") == "1"
+# constant-weight Grams of lagged event designs from the event cross-correlations
+LAG_GRAM = __import__("os").environ.get("SGLM_LAG_GRAM", "1") == "1"
+# concurrent factorisation chains for a batch of >= CHOL_SPLIT_MIN new factorisations
+CHOL_SPLIT = int(__import__("os").environ.get("SGLM_CHOL_SPLIT", "2"))
+CHOL_SPLIT_MIN = int(__import__("os").environ.get("SGLM_CHOL_SPLIT_MIN", "6"))
 # SGLM_GRAM_PIPE=1: Grams computed one source at a time with each group's factorisation chain
 # started right behind its Gram -- measured slower: the per-group chains are latency-bound
 # (~1.1 ms each at 1-3 fits against 2.6 ms for one chain of 20), so the side stream carried
@@ -373,6 +380,20 @@ class LagStructure:
         self.ntiles = ntiles
         if self.m > 64 or self.K > 256:
             return None                                       # the kernel's bounds
+        # for the constant-weight Gram (sglm_lag_gram): event segments of occ and the
+        # occurrence bitmap [m][nwords] (bit v & 31 of word v >> 5)
+        self.n, self.n_raw = int(n), int(N_raw)
+        self.smin, self.smax = int(sh.min()), int(sh.max())
+        cnt = torch.bincount(ev, minlength=m)
+        self.ev_off = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev),
+                                 torch.cumsum(cnt, 0)]).to(torch.int32).contiguous()
+        self.nwords = (int(N_raw) + 31) // 32
+        nzb = torch.nn.functional.pad((E.t() != 0).to(torch.int32),
+                                      (0, self.nwords * 32 - int(N_raw))).view(m, self.nwords, 32)
+        bits = torch.zeros((m, self.nwords), dtype=torch.int32, device=dev)
+        for b in range(32):
+            bits |= nzb[:, :, b] << b
+        self.ebits = bits.contiguous()
         return self
 
 
@@ -697,6 +718,8 @@ class IrlsStats:
     reused: int = 0                                     # fit-iterations that kept a factor
     aliased: int = 0            # fit-iterations solved on a family representative's factor
     shared: int = 0             # fit-iterations on a lambda neighbour's Gram (own factor)
+    lag_grams: int = 0          # Grams from the event cross-correlations (sglm_lag_gram)
+    chain_host_s: float = 0.0   # host time spent enqueueing the factorisation chains
     alg_flop: float = 0.0       # SURVEY.md §8(d) F summed over fit-iterations
     sync_wait_s: float = 0.0    # host time blocked in the per-iteration stream synchronisation
     roundtrips: int = 0         # host<->device round trips (stream synchronisations) of the solve
@@ -747,8 +770,20 @@ class _Buffers:
             self.info = torch.zeros((B,), dtype=torch.int32, device=dev)
             self.cwork = torch.empty(_lib.query("sglm_chol_work_bytes", P, B), dtype=torch.uint8,
                                      device=dev)
+            self._cwork = {0: self.cwork}
+            self._P, self._B, self._dev = P, B, dev
             self.key = key
         return self
+
+    def chol_work(self, j):
+        """Work buffer of the j-th concurrent factorisation chain (the chain's scratch is
+        indexed by list position, so concurrent chains need their own)."""
+        w = self._cwork.get(j)
+        if w is None:
+            w = self._cwork[j] = torch.empty(_lib.query("sglm_chol_work_bytes", self._P,
+                                                        self._B), dtype=torch.uint8,
+                                             device=self._dev)
+        return w
 
 
 class _Scratch:
@@ -799,11 +834,12 @@ def _gram_done():
     _GRAM_DONE[torch.cuda.current_device()] = ev
 
 
-def _side_stream():
-    """This thread's second stream on the current device (the factorisation chain, overlapped
-    with the gradient)."""
+def _side_stream(j: int = 0):
+    """This thread's j-th side stream on the current device (the factorisation chains,
+    overlapped with the gradient)."""
     streams = _scratch().streams
-    key = (torch.cuda.current_device(), "chol")
+    key = (torch.cuda.current_device(), "chol") if j == 0 else (torch.cuda.current_device(),
+                                                                 "chol", j)
     sd = streams.get(key)
     if sd is None:
         # high priority: the chain's small latency-bound launches are dispatched ahead of the
@@ -1033,6 +1069,14 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
     # row-sharded solve: the rank holding each slot's current factor, and whether the new
     # factorisations are dealt over the ranks (explicit-inverse solves only)
     dist_f = comm is not None and comm.distribute and SOLVE_INV
+    # fits whose mask is every row with multiplicity 1 (the refits): a constant weight at the
+    # start, so the first Gram can come from the event cross-correlations (sglm_lag_gram)
+    ntot = d.n if d.slab is None else d.slab[2]
+    mall = {m: prob.mask_nnz(m) == d.n and prob.mask_count(m) == ntot
+            for m in set(int(r.mask) for r in reqs)}
+    all_rows = np.array([mall[int(r.mask)] for r in reqs])
+    use_lag_gram = (LAG_GRAM and d.lag is not None and getattr(d.lag, "ebits", None) is not None
+                    and d.lag.smax - d.lag.smin <= 2048)
     fowner = np.zeros(B0, dtype=np.int64)
     rot = 0
 
@@ -1196,8 +1240,15 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
                           lg.m, lg.K, lg.layout, lg.row0, n, P, _p(bf.R), ld, _p(act_d), na,
                           _p(bf.g), _p(lag_work), st)
             elif use_rp:
+                # a factorisation chain runs beside this gradient: the kernel variant that
+                # leaves it room on the SIMDs (sglm_xtr_prefer)
+                cochain = XTR_COCHAIN and nref > 0 and SOLVE_INV and CHOL_STREAM != "serial"
+                if cochain:
+                    _lib.call("sglm_xtr_prefer", 1)
                 _lib.call("sglm_xtr_bits_packed", _p(d.cbits_full()), ld, P, n, _p(rp_buf), na,
                           _p(act_d), _p(bf.g), _p(gx_work), st)
+                if cochain:
+                    _lib.call("sglm_xtr_prefer", -1)
             else:
                 d.xtr(bf.R, B, bf.g)
             if comm is not None:
@@ -1233,8 +1284,16 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
             pipe_groups = _gram_groups(form, uniq, dup) if (
                 GRAM_PIPE > 0 and SOLVE_INV and CHOL_STREAM != "serial" and comm is None) else None
             if pipe_groups is None:
-                _syrk(d, bf, np.sort(uniq).astype(np.int32), nsteps, ntile1, stats, st,
-                      rows=gram_rows)
+                # fits at their start on an all-rows mask have one weight on every row: their
+                # Gram is w X^T X, from the event cross-correlations for a lagged event design
+                lagg = np.array([k for k in uniq if fresh_start[k] and all_rows[k]],
+                                dtype=np.int32) if use_lag_gram else np.zeros(0, np.int32)
+                if lagg.size:
+                    _lag_gram(d, bf, lagg, st)
+                    if stats is not None:
+                        stats.lag_grams += int(lagg.size)
+                _syrk(d, bf, np.sort(np.setdiff1d(uniq, lagg)).astype(np.int32), nsteps,
+                      ntile1, stats, st, rows=gram_rows)
                 sum_hess(uniq)
                 for k, rk in dup:
                     bf.H[k].copy_(bf.H[rk])
@@ -1329,15 +1388,33 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
                 else:
                     ready = torch.cuda.Event()
                     ready.record()
-                    chains.append((ready, 0, int(nref)))
+                    # the chain is latency-bound (~0.9 ms fixed + ~0.23 ms per representative
+                    # at P = 2048): a large batch runs as CHOL_SPLIT concurrent chains, each on
+                    # its own side stream with its own work buffer
+                    nsplit = CHOL_SPLIT if nref >= CHOL_SPLIT_MIN else 1
+                    cuts = np.linspace(0, int(nref), nsplit + 1).round().astype(int)
+                    chains += [(ready, int(cuts[j]), int(cuts[j + 1] - cuts[j]))
+                               for j in range(nsplit) if cuts[j + 1] > cuts[j]]
                 _gradient()
                 t0 = tick("it_gradient", t0)
-                for ready, off, ng in chains:
-                    side.wait_event(ready)
+                dones = []
+                for j, (ready, off, ng) in enumerate(chains):
+                    sd = side if (pipe_groups is not None or j == 0) else _side_stream(j)
+                    sd.wait_event(ready)
+                    t_ch = time.perf_counter()
                     _lib.call("sglm_chol_solve_inv", _p(bf.H), _p(bf.Minv), P,
                               _p(bf.fact_fits[off:]), None, None, ng, ng, None, 0, None,
                               _p(bf.dshift), _p(bf.delta), _p(bf.info), _p(bf.frozen), B,
-                              _p(bf.cwork), side.cuda_stream)
+                              _p(bf.chol_work(j if pipe_groups is None else 0)),
+                              sd.cuda_stream)
+                    if stats is not None:
+                        stats.chain_host_s += time.perf_counter() - t_ch
+                    if sd is not side:
+                        ev_ = torch.cuda.Event()
+                        ev_.record(sd)
+                        dones.append(ev_)
+                for ev_ in dones:
+                    side.wait_event(ev_)
                 fact_done = torch.cuda.Event()
                 fact_done.record(side)
             if fact_done is None:
@@ -1780,6 +1857,20 @@ def _share_chains(uniq, chains, dist, tol):
                 rep, acc = c[i], 0.0
     keep = np.array([k for k in uniq if int(k) not in drop], dtype=np.int32)
     return keep, shared
+
+
+def _lag_gram(d: Design, bf, fits: np.ndarray, st):
+    """H[k] = w_k X^T X for fits at a constant weight over every row (sglm_lag_gram: event
+    cross-correlations instead of the MFMA Gram)."""
+    lg = d.lag
+    work = _work(_lib.query("sglm_lag_gram_work_bytes", lg.m, lg.smin, lg.smax), d.device,
+                 "laggram")
+    upl = getattr(bf, "up", None)
+    fits = np.ascontiguousarray(fits, dtype=np.int32)
+    fits_d = upl(fits, np.int32) if upl is not None else torch.from_numpy(fits).to(d.device)
+    _lib.call("sglm_lag_gram", _p(lg.occ), _p(lg.ev_off), _p(lg.ebits), lg.nwords,
+              _p(lg.shifts), lg.m, lg.K, lg.layout, lg.smin, lg.smax, lg.row0, lg.n, lg.n_raw,
+              d.P, _p(bf.W), d.ld, _p(fits_d), int(fits.size), _p(bf.H), _p(work), st)
 
 
 def _syrk(d: Design, bf, fits: np.ndarray, nsteps: int, ntile1: int, stats, st, exact=False,

@@ -878,3 +878,83 @@ def test_xtr_bits_four_panel_kernel_vs_float64(engine, torch_mod, B, ngw, monkey
     ref = (Rd.double() @ X.t()).cpu().numpy()
     scale = (Rd.double().abs() @ X.abs().t()).cpu().numpy()
     assert np.max(np.abs(G.cpu().numpy() - ref) / np.maximum(scale, 1e-30)) < 2e-6
+
+
+@pytest.mark.parametrize("shifts,event_major,row0,slab", [
+    (list(range(-5, 10)), False, 9, None),          # contiguous lags, shift-major
+    ([0, 2, 3, 7, -4], True, 7, None),              # scattered lags, event-major
+    (list(range(0, 40)), False, 0, None),           # rows past the start of E (zero)
+    (list(range(-3, 12)), False, 11, (3000, 11000)),  # a row slab of a row-sharded solve
+])
+def test_lag_gram_equals_the_dense_gram(engine, torch_mod, shifts, event_major, row0, slab):
+    """sglm_lag_gram (event cross-correlations) against the float64 X^T X of the expanded
+    design: bf16(w) * count exactly on the 128-blocks I <= J of every listed fit, other fits and
+    the lower blocks untouched."""
+    torch = torch_mod
+    from sglm_hip import _lib
+    E_ = engine
+    rng = np.random.default_rng(len(shifts) + row0)
+    n_raw, m = 12_000, 7
+    Ev = (rng.random((n_raw, m)) < 0.05).astype(np.float32)
+    Ev[:40, 2] = 1.0                                 # occurrences at both ends of the window
+    Ev[-40:, 5] = 1.0
+    n = n_raw - (max(shifts) - min(shifts)) - 3
+    d = E_.Design.from_events(Ev, shifts, row0, n, event_major=event_major, slab=slab)
+    assert d.lag is not None and d.lag.ebits is not None
+    nloc = d.n
+    X = d.xb[:, :nloc].double()
+    G = (X @ X.t()).cpu().numpy()
+    B, P = 3, d.P
+    W = torch.zeros((B, d.ld), dtype=torch.float32, device="cuda")
+    W[:, 0] = torch.tensor([0.7318, 1.0, 2.5e-3])
+    H = torch.full((B, P, P), float("nan"), dtype=torch.float32, device="cuda")
+    fits = torch.tensor([0, 2], dtype=torch.int32, device="cuda")
+    lg = d.lag
+    work = torch.empty(_lib.query("sglm_lag_gram_work_bytes", lg.m, lg.smin, lg.smax),
+                       dtype=torch.uint8, device="cuda")
+    _lib.call("sglm_lag_gram", lg.occ.data_ptr(), lg.ev_off.data_ptr(), lg.ebits.data_ptr(),
+              lg.nwords, lg.shifts.data_ptr(), lg.m, lg.K, lg.layout, lg.smin, lg.smax, lg.row0,
+              lg.n, lg.n_raw, P, W.data_ptr(), d.ld, fits.data_ptr(), 2, H.data_ptr(),
+              work.data_ptr(), 0)
+    torch.cuda.synchronize()
+    Hh = H.cpu().numpy()
+    blk = np.arange(P) // 128
+    upper = blk[:, None] <= blk[None, :]
+    for k in (0, 2):
+        w = np.float32(torch.tensor(float(W[k, 0])).to(torch.bfloat16).float().item())
+        want = (w * G.astype(np.float32)).astype(np.float32)
+        assert np.array_equal(Hh[k][upper], want[upper]), k
+        assert np.isnan(Hh[k][~upper]).all()
+    assert np.isnan(Hh[1]).all()
+
+
+def test_grid_first_gram_from_event_correlations(engine):
+    """The C3-shape grid takes its first (constant-weight) Gram from sglm_lag_gram and reaches
+    the same fits as with the MFMA Gram (the first Hessian differs only by f32 rounding; the
+    fixed point is the exact gradient's)."""
+    import pandas as pd
+    from sglm_hip import folds, grid, synth
+    from sglm_hip.estimators import Objective
+    E_ = engine
+    s = synth.make(N=100_000, m=25, L=10, family="poisson", rho=0.02, seed=0)
+    d = E_.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
+    codes = folds.trial_keys_codes(pd.DataFrame({"nTrial": s.trial}), ["nTrial"]).values
+    np.random.seed(3)
+    cv_idx = folds.cv_idx_from_bucket_ids(codes, num_folds=5)
+    objs = [Objective("irls", E_.FAM_TWEEDIE_LOG, 1.0, float(a), "n", True, 100)
+            for a in np.logspace(-4, 1, 6)]
+    st = E_.IrlsStats()
+    a = grid.run(d, s.y, cv_idx, objs, [0] * 6, stats=st)
+    assert st.lag_grams >= 1
+    old = E_.LAG_GRAM
+    try:
+        E_.LAG_GRAM = False
+        st2 = E_.IrlsStats()
+        b = grid.run(d, s.y, cv_idx, objs, [0] * 6, stats=st2)
+        assert st2.lag_grams == 0
+    finally:
+        E_.LAG_GRAM = old
+    for x, y in zip(a, b):
+        assert x["converged"] and y["converged"]
+        assert rel(x["cv_coefs"], y["cv_coefs"]) < 1e-5
+        assert rel(x["refit_coef"], y["refit_coef"]) < 1e-5

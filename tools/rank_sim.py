@@ -140,7 +140,9 @@ def main():
         if prof is not None:
             import pstats
             prof.disable()
-            pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(25)
+            ps = pstats.Stats(prof, stream=sys.stderr)
+            ps.sort_stats("tottime").print_stats(40)
+            ps.sort_stats("cumulative").print_stats(50)
     st = E.IrlsStats(record=True, host_phases=True)
     grid.run(d, s.y, cv_idx, objs, [0] * nlam, stats=st, simulate=sim)
     torch.cuda.synchronize()
