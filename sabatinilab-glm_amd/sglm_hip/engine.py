@@ -88,6 +88,8 @@ SOLVE_INV = __import__("os").environ.get("SGLM_SOLVE_INV", "1") == "1"
 # where the factorisation chain runs: "side" (its own stream, overlapping the gradient),
 # "prio" (the same at high stream priority), "serial" (the main stream, before the gradient)
 CHOL_STREAM = __import__("os").environ.get("SGLM_CHOL_STREAM", "side")
+# gradient enqueued before the Hessian decisions' device wait when no Hessian is planned
+GRAD_FIRST = __import__("os").environ.get("SGLM_GRAD_FIRST", "1") == "1"
 # gradient kernel that co-resides with the factorisation chain in iterations that form factors
 XTR_COCHAIN = __import__("os").environ.get("SGLM_XTR_COCHAIN", "1") == "1"
 # constant-weight Grams of lagged event designs from the event cross-correlations
@@ -987,29 +989,49 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
     log_link = fam == FAM_TWEEDIE_LOG
     reqs0 = list(reqs)
 
+    # the per-fit penalty rows, start coefficients and index arrays are built on the device from
+    # per-fit scalars staged through the pinned upload arena (a pageable upload of each [B][P]
+    # array would synchronise the stream several times before the first kernel)
+    up = _Uploads(dev)
     lam = np.array([float(r.lam) for r in reqs])
-    penal = np.zeros((B0, P), dtype=np.float64)
-    penal[:, :p] = 1.0
-    dsh = np.full((B0, P), -1.0, dtype=np.float32)
-    dsh[:, :p] = lam[:, None]
-    beta = np.zeros((B0, P), dtype=np.float64)
+    icpt = np.zeros(B0)
+    warm = any(r.coef0 is not None for r in reqs)
+    beta = np.zeros((B0, P), dtype=np.float64) if warm else None
     for k, r in enumerate(reqs):
-        if r.fit_intercept:
-            dsh[k, p] = 0.0
         if r.coef0 is not None:
             beta[k, :p] = r.coef0
-            beta[k, p] = (r.intercept0 or 0.0) if r.fit_intercept else 0.0
+            icpt[k] = (r.intercept0 or 0.0) if r.fit_intercept else 0.0
         elif r.fit_intercept:
             cnt, s, ym = prob.mask_stats(r.resp, r.mask)
             if log_link:
                 if ym <= 0:
                     raise ValueError("Some value(s) of y are out of the valid range of the loss")
-                beta[k, p] = math.log(ym)
+                icpt[k] = math.log(ym)
             else:
-                beta[k, p] = ym
-    bf.dshift.copy_(torch.from_numpy(dsh))
-    bf.beta.copy_(torch.from_numpy(beta.astype(np.float32)))
-    if all(r.coef0 is None for r in reqs):
+                icpt[k] = ym
+    fi = np.array([1.0 if r.fit_intercept else 0.0 for r in reqs])
+    fresp_h = np.array([r.resp for r in reqs], dtype=np.int32)
+    fmask_h = np.array([r.mask for r in reqs], dtype=np.int32)
+    ts_h = np.concatenate([[0.0, 1.0, 0.5, 0.25, 0.125], TV2.astype(np.float32)])
+    scal = up(np.concatenate([lam, icpt, fi, ts_h]), np.float64)
+    ints = up(np.concatenate([fresp_h, fmask_h]), np.int32)
+    lam_d, icpt_d, fi_d = scal[:B0], scal[B0:2 * B0], scal[2 * B0:3 * B0]
+    # ridge shift per coordinate (lam on the predictors, 0 on a fitted intercept, -1 = frozen:
+    # the intercept of fit_intercept=False and the padding columns)
+    bf.dshift.fill_(-1.0)
+    bf.dshift[:B0, :p] = lam_d[:, None]
+    bf.dshift[:B0, p] = fi_d - 1.0
+    # the coefficients live on the device (float64); the host sees per-fit scalars only
+    if warm:
+        beta[:, p] = icpt
+        beta64_d = torch.from_numpy(beta).to(dev)
+    else:
+        beta64_d = torch.zeros((B0, P), dtype=torch.float64, device=dev)
+        beta64_d[:, p] = icpt_d
+    bf.beta[:B0].copy_(beta64_d)
+    lamp_d = torch.zeros((B0, P), dtype=torch.float64, device=dev)      # lam * penalty mask
+    lamp_d[:, :p] = lam_d[:, None]
+    if not warm:
         # intercept-only start: X beta is the intercept on every row (exactly, as the MFMA
         # product of the ones column would give it)
         bf.eta[:, :n].copy_(bf.beta[:, p:p + 1].expand(B0, n))
@@ -1024,25 +1046,22 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
     # Device state is held per SLOT (one per fit, fixed for the whole solve); every per-fit
     # kernel takes the list of active slots, so stopped fits cost nothing and no state moves.
     B = B0
-    fresp_h = np.array([r.resp for r in reqs], dtype=np.int32)
-    fmask_h = np.array([r.mask for r in reqs], dtype=np.int32)
-    fit_resp = torch.from_numpy(fresp_h).to(dev)
-    fit_mask = torch.from_numpy(fmask_h).to(dev)
+    fit_resp = torch.empty(B0, dtype=torch.int32, device=dev)
+    fit_resp.copy_(ints[:B0])
+    fit_mask = torch.empty(B0, dtype=torch.int32, device=dev)
+    fit_mask.copy_(ints[B0:])
     drift = np.full(B0, np.inf)         # predictor drift since each fit's Hessian was formed
     # one host round trip per Newton iteration: the gradient, the step direction, the trial
     # losses and the step's predictor drift come back together (pinned buffers, async copies)
     dmax_d = torch.zeros(B0, dtype=torch.float32, device=dev)
     dmax_h = _pinned("dmax", B0, torch.float32)
     L_h = _pinned("L", B0 * 8, torch.float64)
-    # the coefficients live on the device (float64); the host sees per-fit scalars only
-    beta64_d = torch.from_numpy(beta).to(dev)
-    ts_all = torch.from_numpy(np.concatenate([[0.0, 1.0, 0.5, 0.25, 0.125],
-                                              TV2.astype(np.float32)])).to(dev)
+    ts_all = torch.empty(ts_h.size, dtype=torch.float64, device=dev)
+    ts_all.copy_(scal[3 * B0:])
     nts = int(ts_all.numel())
     sc_d = torch.empty(B0 * (6 + nts), dtype=torch.float64, device=dev)
     # fits still at their common start (same mask and response => bitwise equal Hessians)
     fresh_start = np.array([r.coef0 is None for r in reqs])
-    lamp_d = torch.from_numpy(lam[:, None] * penal).to(dev)        # lam * penalty mask
     gram_now = np.zeros(B0, dtype=bool)
     exact_h = np.zeros(B0, dtype=bool)     # Hessian = the fit's own Gram at its own predictor
     active = np.ones(B0, dtype=bool)
@@ -1057,8 +1076,8 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
     factored = False
     xtr_work = _work(max(_lib.query("sglm_xtr_work_bytes", P, B0, n),
                          _lib.query("sglm_rowsum_work_bytes", B0, 8, n)), dev)
-    tv1 = torch.tensor([0.0, 1.0, 0.5, 0.25, 0.125], dtype=torch.float32, device=dev)
-    tv2 = torch.from_numpy(TV2.astype(np.float32)).to(dev)
+    tv1 = ts_all[:5].float()
+    tv2 = ts_all[5:].float()
     Ltr = torch.zeros(B0 * 8, dtype=torch.float64, device=dev)    # dense [B][T] per call
     nsteps = (n + 31) // 32
     ntile1 = (P // 256) * (P // 256 + 1) // 2
@@ -1105,7 +1124,6 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
     no_alias = np.zeros(B0, dtype=bool)
     no_share = np.zeros(B0, dtype=bool)     # failed a step on a lambda neighbour's Hessian
 
-    up = _Uploads(dev)
     bf.up = up
     pd_h = _pinned("pairdist", 4 * B0, torch.float32)
 
@@ -1231,9 +1249,14 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
                       _p(prob.M), _p(fit_resp), _p(fit_mask), _p(bf.W), _p(bf.R), None, None,
                       None, st)
 
-        def _gradient():
+        grad_done = [False]
+
+        def _gradient(cochain_ok=True):
             """X^T R on the current stream, then + lam w (the Hessian step needs only W, so
-            its Grams go first and the new factorisations overlap this)."""
+            its Grams go first and the new factorisations overlap this).  Once per iteration."""
+            if grad_done[0]:
+                return
+            grad_done[0] = True
             if use_lag:
                 lg = d.lag
                 _lib.call("sglm_lag_xtr", _p(lg.occ), _p(lg.tbeg), _p(lg.tend), _p(lg.shifts),
@@ -1242,7 +1265,8 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
             elif use_rp:
                 # a factorisation chain runs beside this gradient: the kernel variant that
                 # leaves it room on the SIMDs (sglm_xtr_prefer)
-                cochain = XTR_COCHAIN and nref > 0 and SOLVE_INV and CHOL_STREAM != "serial"
+                cochain = (cochain_ok and XTR_COCHAIN and nref > 0 and SOLVE_INV
+                           and CHOL_STREAM != "serial")
                 if cochain:
                     _lib.call("sglm_xtr_prefer", 1)
                 _lib.call("sglm_xtr_bits_packed", _p(d.cbits_full()), ld, P, n, _p(rp_buf), na,
@@ -1277,6 +1301,10 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
             # long computed): keep / form / share / alias (see _hess_plan)
             if plan is None:
                 plan = hess_plan(act)
+            if GRAD_FIRST and plan["form"].size == 0 and plan["npairs"] and SOLVE_INV:
+                # no Hessian is certain to be formed: the gradient goes ahead of the wait for
+                # the pair distances (a failed alias candidate's Gram then follows it)
+                _gradient(cochain_ok=False)
             keep, form, uniq, dup, ali, fail, exact_h = hess_finish(plan)
             plan = None
             alias[:] = -1
