@@ -67,6 +67,8 @@ def parse():
                     help="rows of the oracle Newton sample (secondary CPU figure)")
     ap.add_argument("--sklearn-rows", type=int, default=100_000,
                     help="rows of the reference-path (sklearn lbfgs fold loop) sample")
+    ap.add_argument("--shard", default=None, choices=["fits", "rows"],
+                    help="N > 1: whole fits per rank (default) or row slabs (sglm_hip/comm.py)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI) for real runs; gloo to rehearse several ranks "
                          "on fewer GPUs")
@@ -667,6 +669,8 @@ def main():
     s = synth.make(N=N, m=m, L=L, family="poisson", rho=0.02, seed=0)
     # N > 1: each rank expands only its slab of the rows (row-sharded grid, comm.py), or the
     # whole design when the grid is sharded by fits (SGLM_SHARD=fits)
+    if a.shard:
+        grid.SHARD_MODE = a.shard
     rows_mode = world > 1 and grid.SHARD_MODE == "rows"
     slab = grid.rank_slab(s.N, rank, world) if rows_mode else None
     design = E.Design.from_events(s.E, s.shifts, s.L - 1, s.N, slab=slab)

@@ -1654,7 +1654,10 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
             plan = hess_plan(nxt)
         t0 = tick("it_update", t0)
 
-    out_beta[:] = beta64_d.cpu().numpy()
+    # final linear predictor from the final coefficients, in request order (no accumulated
+    # drift), enqueued before the readbacks so the host's one wait covers it
+    bf.beta[:B0].copy_(beta64_d)
+    d.eta(bf.beta, bf.eta)
     out_iter[:] = n_iter
     out_conv[:] = converged
     if dist_f:
@@ -1662,14 +1665,12 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
         inf = bf.info[:B].clone()
         inf[torch.from_numpy(fowner != comm.rank).to(dev)] = 0
         comm.sum_owned_(inf)
-        out_info[:] = inf.cpu().numpy()
     else:
-        out_info[:] = bf.info[:B].cpu().numpy()
+        inf = bf.info[:B]
+    outs = torch.cat([beta64_d.reshape(-1), inf.to(torch.float64)]).cpu().numpy()
+    out_beta[:] = outs[: B0 * P].reshape(B0, P)
+    out_info[:] = outs[B0 * P:].astype(np.int64)
     bf.prob = bf.keep = bf.up = bf.fit_mask_d = None   # drop the compacted designs with the problem
-    # final linear predictor from the final coefficients, in request order (no accumulated
-    # drift)
-    bf.beta.copy_(torch.from_numpy(out_beta.astype(np.float32)))
-    d.eta(bf.beta, bf.eta)
     res = []
     for k, r in enumerate(reqs0):
         res.append(FitResult(coef=out_beta[k, :p].copy(),

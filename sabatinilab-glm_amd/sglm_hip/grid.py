@@ -124,10 +124,13 @@ def _dist():
 
 
 SHARD_PLAN = "mask_major"                    # or "round_robin" (comparison runs)
-# "rows": a process group splits the rows of the grid (every rank runs every fit on its slab,
-# sums all-reduced; comm.py) -- the default for log-link IRLS grids; "fits": whole fits (cross-
-# mask families) per rank with one all-gather of the results
-SHARD_MODE = os.environ.get("SGLM_SHARD", "rows")
+# "fits" (default): whole fits (cross-mask families) per rank with one all-gather of the
+# results; "rows": a process group splits the rows of the grid (every rank runs every fit on
+# its slab, sums all-reduced; comm.py).  Simulated C4 shares at 2 / 4 / 8 ranks are equal within
+# 1 ms before the row mode's ~60 collectives per grid (profiles/r03_rank_shares*.json), so the
+# mode without a data-path collective is the default and the row mode is opt-in
+# (SGLM_SHARD=rows) -- it is balanced by construction and its floor is one slab's latency.
+SHARD_MODE = os.environ.get("SGLM_SHARD", "fits")
 
 
 def rank_slab(n: int, rank: Optional[int] = None, world: Optional[int] = None):

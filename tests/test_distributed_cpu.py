@@ -170,3 +170,61 @@ def test_sharded_grid_plan_gather_assemble(world):
             np.testing.assert_allclose(d["cv_scores_test"], r["cv_scores_test"], rtol=1e-12)
             assert abs(d["cv_R2_score"] - r["cv_R2_score"]) < 1e-12
             assert abs(d["cv_mse_score"] - r["cv_mse_score"]) < 1e-12 * r["cv_mse_score"]
+
+
+def _rowcomm_worker(rank, world, port, q):
+    import sys
+    import torch
+    import torch.distributed as dist
+    from conftest import PKG, ROOT
+    sys.path[:0] = [ROOT, PKG]
+    from sglm_hip.comm import RowComm, row_slab
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    c = RowComm(dist)
+    # slab partials of a Gram-like sum, a maximum and a minimum over rows
+    n = 1000
+    s0, s1 = row_slab(n, rank, world)
+    rows = torch.arange(s0, s1, dtype=torch.float64)
+    g = torch.stack([rows.sum(), (rows ** 2).sum()])
+    c.sum_(g)
+    mx = torch.tensor([rows.max().item()], dtype=torch.float32)
+    c.max_(mx)
+    mn = torch.tensor([rows.min().item()], dtype=torch.float64)
+    c.min_(mn)
+    # round-robin factorisation owners, then directions combined by one sum
+    own = c.owners(7, 3)
+    delta = torch.zeros((7, 4), dtype=torch.float32)
+    for k in range(7):
+        if own[k] == rank:
+            delta[k] = float(k + 1)
+    c.directions_(delta)
+    q.put((rank, g.tolist(), float(mx), float(mn), own.tolist(), delta[:, 0].tolist(),
+           c.calls))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_row_sharded_collectives(world):
+    """comm.RowComm over a gloo group: slab sums / maxima / minima equal the whole-row values
+    on every rank, the factorisation owners agree and cover every rank, and the directions
+    each owner solved reach every rank (the others add zeros) -- the collectives of the
+    row-sharded grid (engine.irls with comm=RowComm)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rowcomm_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n = 1000
+    for rank, g, mx, mn, own, d0, calls in out:
+        assert g == [float(sum(range(n))), float(sum(i * i for i in range(n)))]
+        assert mx == n - 1 and mn == 0
+        assert own == [(k + 3) % world for k in range(7)]
+        assert d0 == [float(k + 1) for k in range(7)]
+        assert calls == 4
