@@ -1,7 +1,7 @@
 # Round artifacts: PMC traffic of the Gram (separate FETCH/WRITE passes), the default bench line
 # (with CPU baseline), the rocprofv3 kernel-trace summary of the same bench command, the C5,
 # session-prep, signal and design-matrix bench lines, a 2-rank gloo rehearsal of the sharded
-# bench on the one GPU, and simulated 2/4/8-rank shares.  Everything lands under
+# bench on the one GPU (fit and row sharding), and simulated 2/4/8-rank shares of both modes.  Everything lands under
 # gpurun_out/prof (merged back by gpurun); copy what is judged into profiles/ afterwards.
 # Usage on the box: bash tools/gpu_profile.sh ROUND   (e.g. r02)
 set -e
@@ -21,4 +21,6 @@ timeout -k 10 300 python bench.py --config designmat > $O/bench_designmat.json 2
 timeout -k 10 400 python bench.py --gpus 2 --dist-backend gloo --no-cpu > $O/bench_g2_gloo.json 2> $O/bench_g2_gloo.err
 for w in 2 4 8; do
   timeout -k 10 300 python -u tools/rank_sim.py --world $w --all > $O/rank$w.json 2> $O/rank$w.err
+  timeout -k 10 300 python -u tools/rank_sim.py --mode rows --world $w --all > $O/rows$w.json 2> $O/rows$w.err
 done
+timeout -k 10 400 python bench.py --gpus 2 --dist-backend gloo --shard rows --no-cpu > $O/bench_g2_gloo_rows.json 2> $O/bench_g2_gloo_rows.err
