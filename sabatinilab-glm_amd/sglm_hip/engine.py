@@ -94,8 +94,10 @@ GRAD_FIRST = __import__("os").environ.get("SGLM_GRAD_FIRST", "1") == "1"
 XTR_COCHAIN = __import__("os").environ.get("SGLM_XTR_COCHAIN", "1") == "1"
 # constant-weight Grams of lagged event designs from the event cross-correlations
 LAG_GRAM = __import__("os").environ.get("SGLM_LAG_GRAM", "1") == "1"
-# concurrent factorisation chains for a batch of >= CHOL_SPLIT_MIN new factorisations
-CHOL_SPLIT = int(__import__("os").environ.get("SGLM_CHOL_SPLIT", "2"))
+# concurrent factorisation chains for a batch of >= CHOL_SPLIT_MIN new factorisations (off: the
+# second chain of a split measured no gain -- in the C4 kernel trace it starts only as the
+# first one ends -- tools/grid_ab.py split2 vs split1 56.2 / 56.2 ms)
+CHOL_SPLIT = int(__import__("os").environ.get("SGLM_CHOL_SPLIT", "1"))
 CHOL_SPLIT_MIN = int(__import__("os").environ.get("SGLM_CHOL_SPLIT_MIN", "6"))
 # SGLM_GRAM_PIPE=1: Grams computed one source at a time with each group's factorisation chain
 # started right behind its Gram -- measured slower: the per-group chains are latency-bound
@@ -1162,10 +1164,17 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
         pairs = [(int(k), int(repl[k])) for k in cand]
         pairs += [(c[i], c[i + 1]) for c in chains for i in range(len(c) - 1)]
         ev = None
-        if pairs:
+        if pairs and len(pairs) > pd_h.numel():
+            raise RuntimeError("pair distance buffer too small")
+        if pairs and not warm and all(fresh_start[a] and fresh_start[b]
+                                      and prob.mask_count(reqs[a].mask) > 0 for a, b in pairs):
+            # both fits still at their intercept-only start: eta is one constant per fit, so
+            # the max-row distance is |f32(b_a) - f32(b_b)| (what the kernel would compute)
+            ic32 = icpt.astype(np.float32)
+            pa = np.array(pairs, dtype=np.int64)
+            pd_h[:len(pairs)].copy_(torch.from_numpy(np.abs(ic32[pa[:, 0]] - ic32[pa[:, 1]])))
+        elif pairs:
             npair = len(pairs)
-            if npair > pd_h.numel():
-                raise RuntimeError("pair distance buffer too small")
             pd_d = _pair_dist_async(bf, prob, np.array(pairs, dtype=np.int32), n, ld, st)
             if comm is not None:
                 comm.max_(pd_d)
