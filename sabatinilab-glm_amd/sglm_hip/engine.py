@@ -1096,7 +1096,10 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
     mall = {m: prob.mask_nnz(m) == d.n and prob.mask_count(m) == ntot
             for m in set(int(r.mask) for r in reqs)}
     all_rows = np.array([mall[int(r.mask)] for r in reqs])
-    use_lag_gram = (LAG_GRAM and d.lag is not None and getattr(d.lag, "ebits", None) is not None
+    # the weight m * h(y, eta) is one constant on such a mask only when h does not depend on y:
+    # the Poisson log link (h = exp(eta)); Gamma / Tweedie's h carries y on every row
+    use_lag_gram = (LAG_GRAM and fam == FAM_TWEEDIE_LOG and power == 1.0 and d.lag is not None
+                    and getattr(d.lag, "ebits", None) is not None
                     and d.lag.smax - d.lag.smin <= 2048)
     fowner = np.zeros(B0, dtype=np.int64)
     rot = 0

@@ -958,3 +958,25 @@ def test_grid_first_gram_from_event_correlations(engine):
         assert x["converged"] and y["converged"]
         assert rel(x["cv_coefs"], y["cv_coefs"]) < 1e-5
         assert rel(x["refit_coef"], y["refit_coef"]) < 1e-5
+
+
+def test_lag_gram_only_for_constant_weights(engine):
+    """Gamma / Tweedie weights carry y on every row (h = y e^-eta for power 2) even at a
+    constant eta: their first Gram must stay the MFMA Gram over the rows."""
+    import pandas as pd
+    from sglm_hip import folds, grid, synth
+    from sglm_hip.estimators import Objective
+    E_ = engine
+    s = synth.make(N=50_000, m=10, L=8, family="poisson", rho=0.05, seed=4)
+    y = s.y + 0.5                                        # strictly positive (Gamma's range)
+    d = E_.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
+    codes = folds.trial_keys_codes(pd.DataFrame({"nTrial": s.trial}), ["nTrial"]).values
+    np.random.seed(5)
+    cv_idx = folds.cv_idx_from_bucket_ids(codes, num_folds=3)
+    for power in (2.0, 1.5):
+        objs = [Objective("irls", E_.FAM_TWEEDIE_LOG, power, float(a), "n", True, 100)
+                for a in (1e-3, 1e-1)]
+        st = E_.IrlsStats()
+        a = grid.run(d, y, cv_idx, objs, [0, 0], stats=st)
+        assert st.lag_grams == 0, power
+        assert all(r["converged"] for r in a)
