@@ -205,7 +205,7 @@ def run(X, y, cv_idx, objectives: Sequence[Objective], rolls: Sequence[int],
     return out if simulate is not None else out[0]
 
 
-def plan_fits(groups: Sequence[dict], n: int):
+def plan_fits(groups: Sequence[dict], n: int, check: bool = True):
     """Host-side plan of a (multi-)grid, identical on every rank: the row-mask specs, per
     group its ([(train, test)] mask ids, refit mask, holdout mask), the masks' row counts, the
     fit table -- per group, (param j, split k) then refit (j, -1) as (group, j, k, fit mask,
@@ -231,7 +231,7 @@ def plan_fits(groups: Sequence[dict], n: int):
         refit = add_spec(g.get("refit_rows"), False)
         hold = g.get("holdout_rows")
         gm.append((splits, refit, -1 if hold is None else add_spec(hold, False)))
-    counts = [_mask_count(sp[0], sp[1], n) for sp in specs]
+    counts = [_mask_count(sp[0], sp[1], n, check) for sp in specs]
     roll_list = sorted(set(int(r) for g in groups for r in g["rolls"]) | {0})
     ridx = {r: i for i, r in enumerate(roll_list)}
     table = []
@@ -311,7 +311,11 @@ def run_multi(X, y, groups: Sequence[dict], score_method: str = "mse", coef0=Non
     y = np.asarray(y, dtype=np.float64).reshape(-1)
     if y.shape[0] != n:
         raise ValueError(f"y has {y.shape[0]} rows, X has {n}")
-    plan = plan_fits(groups, n)
+    # one process builds every mask (no process group, or a row-sharded one): the mask builder
+    # checks the fold indices; ranks that build only their own masks check all of them here so
+    # that a bad index raises on every rank together
+    single = dist is None or comm is not None
+    plan = plan_fits(groups, n, check=not single)
     specs, gm, counts, table, roll_list = plan
     t0 = tick("grid_setup", t0)
     if comm is not None:
@@ -324,8 +328,13 @@ def run_multi(X, y, groups: Sequence[dict], score_method: str = "mse", coef0=Non
     # only the masks (and responses) of this rank's fits are built and uploaded
     used = sorted({table[i][3] for i in mine} | {table[i][5] for i in mine if table[i][5] >= 0})
     local = {mid: q for q, mid in enumerate(used)}
-    prob = E.Problem.from_index_lists(design, y, roll_list,
-                                      [(specs[mid][0], specs[mid][1]) for mid in used])
+    try:
+        prob = E.Problem.from_index_lists(design, y, roll_list,
+                                          [(specs[mid][0], specs[mid][1]) for mid in used])
+    except ValueError as e:
+        if single and "outside" in str(e):
+            raise IndexError(str(e)) from None         # numpy's X[idx] error type
+        raise
     t0 = tick("setup_problem", t0)
     ms = _MaskStats(prob, comm)
     for i in mine:                           # the IRLS setup reads these, not host passes
@@ -479,14 +488,16 @@ def _mask_array(idx, multiplicity, n):
     return m
 
 
-def _mask_count(idx, multiplicity, n):
-    """Row count of a spec (sum of multiplicities) without building the mask."""
+def _mask_count(idx, multiplicity, n, check=True):
+    """Row count of a spec (sum of multiplicities) without building the mask.  ``check`` =
+    False leaves a fold list's range check to the mask builder (one process builds every mask
+    of the grid: sglm_host_masks checks each index while it writes the row)."""
     if idx is None:
         return float(n)
     if multiplicity:
         # a fold list counts every entry: only the range check (numpy's IndexError), no wrap
         a = np.asarray(idx).reshape(-1)
-        if a.size and (a.min() < -n or a.max() >= n):
+        if check and a.size and (a.min() < -n or a.max() >= n):
             F.wrap_indices(a, n)                             # raises with numpy's message
         return float(a.size)
     return float(np.unique(F.wrap_indices(idx, n)).size)

@@ -980,3 +980,18 @@ def test_lag_gram_only_for_constant_weights(engine):
         a = grid.run(d, y, cv_idx, objs, [0, 0], stats=st)
         assert st.lag_grams == 0, power
         assert all(r["converged"] for r in a)
+
+
+def test_grid_bad_fold_index_raises_index_error(engine):
+    """A fold list naming a row outside [-n, n) raises IndexError, as the reference's
+    X[idx_train] does (the mask builder checks it when the grid is one process)."""
+    from sglm_hip import grid, synth
+    from sglm_hip.estimators import Objective
+    E_ = engine
+    s = synth.make(N=5_000, m=4, L=3, family="poisson", rho=0.05, seed=2)
+    d = E_.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
+    tr = np.arange(0, 4000)
+    te = np.arange(4000, s.N + 1)                       # one past the last row
+    objs = [Objective("irls", E_.FAM_TWEEDIE_LOG, 1.0, 1e-2, "n", True, 100)]
+    with pytest.raises(IndexError):
+        grid.run(d, s.y, [(tr, te)], objs, [0])
