@@ -622,7 +622,7 @@ xtr_bits4_kernel(const u32x2* __restrict__ cbits, int64_t ld, int32_t P, int64_t
 //       row slabs fill whole rounds: C4, 120 fits 1.20 / 1.46 / 1.43 ms, 70 fits
 //       1.19 / 1.13 / 1.08 ms for variants 2 / 1 / 0 in one process);
 //   1 = four-panel, one group -- only on request.
-// SGLM_XTR4=0 forces 0, SGLM_XTR_NGW=1 / 2 force 1 / 2 where P allows.
+// SGLM_XTR4=0 forces 0, SGLM_XTR_NGW=1 / 2 / 3 force 1 / 2 / 3 where P allows.
 // sglm_xtr_prefer(1) (per thread) asks for the one-group four-panel kernel: 262 registers
 // per lane leave room on every SIMD for the factorisation chain's waves (the two-group kernel
 // holds all 512), so a chain running beside the gradient progresses instead of waiting for it.
@@ -638,6 +638,7 @@ static int xtr_variant(int32_t P, int32_t B) {
     const char* e = getenv("SGLM_XTR_NGW");
     if (e && e[0] == '1') return 1;
     if (e && e[0] == '2') return ngrp >= 2 ? 2 : 1;
+    if (e && e[0] == '3') return 3;
     if (ngrp >= 2 && ngrp % 2 == 0) return 2;
     return wpe2 ? 3 : 0;
 }
