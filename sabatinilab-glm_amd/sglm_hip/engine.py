@@ -735,6 +735,7 @@ class IrlsStats:
          "stale_factor_retry", "alias_dropped"), 0))
 
     host_phases: bool = False   # host (enqueue) seconds per phase, no device syncs (tools)
+    iter_log: Optional[list] = None     # per Newton iteration: a dict of counts (tools)
 
     def mark(self, name, t0):
         """Add the wall time since t0 to phase `name` (after a device sync when trace_phases:
@@ -1623,6 +1624,15 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
         converged[act[stop]] = conv_now[stop]
         out_of_iters = ~stop & (n_iter[act] >= max_iter[act])
         active[act[out_of_iters]] = False
+        if stats is not None and stats.iter_log is not None:
+            stats.iter_log.append(dict(
+                it=it, active=int(na), keep=int(0 if const_hess else keep.size),
+                alias=int(0 if const_hess else ali.size), form=int(nref if not dist_f else -1),
+                grams=int(gram_comp.sum()), stop_tol=int(stop_tol.sum()),
+                ls_fail=int(ls_fail.sum()), step1=int(np.sum(step_a == 1.0)),
+                rel_max=float(relv.max()), rel_med=float(np.median(relv)),
+                lam_active=[float(lam[k]) for k in act[~stop]][:40],
+                rate=[float(x) for x in (relv / np.maximum(prev_rel[act], 1e-300))[~stop]][:40]))
         prev_rel[act] = relv
         if stats is not None:
             stats.stops["tol"] += int(np.sum(stop_tol))
