@@ -290,6 +290,39 @@ int sglm_chol_solve_alias(const float* H, int32_t P, const int32_t* fits, const 
                           int32_t nact, const double* g, const float* rscale, float* delta,
                           const uint8_t* frozen, int32_t B, void* work, sglm_stream_t stream);
 
+/* --- float64 factorisation, exact rank decisions, minimum-norm projection --------------
+ * The reference's OLS is LinearRegression -> scipy.linalg.lstsq (backend/sglm.py:96-101 ->
+ * sklearn linear_model/_base.py:701), float64, minimum-norm on a rank-deficient design; its
+ * unpenalised Poisson (TweedieRegressor alpha = 0, lbfgs from 0, backend/sglm.py:112-115) stays
+ * in the row space of X.  These three calls replace that arithmetic:
+ * sglm_chol64_factor: U[f] (float64 [nf][P][P], upper) = Cholesky of the f32 upper triangle
+ *   H[hsrc[f]] plus the float64 penalty row lamp[dsrc[f]] on the diagonal (lamp NULL: dshift);
+ *   coordinates with dshift[dsrc[f]][j] < 0 are excluded (state 2), zero diagonals are zero
+ *   columns (state 3), a pivot whose Schur complement is <= tol * its diagonal is DEPENDENT
+ *   (state 1: its row of U zeroed, U_jj = 1, its column above the diagonal kept); state 0 =
+ *   kept.  nulls[f][0 .. counts[2f]) = the dependent coordinates (ascending), counts[2f + 1] =
+ *   dependent + zero columns.  work: sglm_chol64_work_bytes(P, nf).  P % 64 == 0, P <= 8192.
+ * sglm_chol64_solve: delta[fits[q]] = -U_f^-1 U_f^-T g[fits[q]] (f32 out) on the kept
+ *   coordinates of f = fsrc[q], 0 elsewhere (g float64 [*][P]).
+ * sglm_chol64_minnorm: for each fit k = fits[q] on factor f = fsrc[q]: beta[k] (float64 [*][P])
+ *   -= N (N_w^T N_w)^-1 N_w^T beta[k], N = the null vectors e_d - U_KK^-1 U[K][d] of f's
+ *   dependent coordinates, N_w their first pw coordinates (the coefficients, without the
+ *   intercept): the minimum-norm point of the fit's solution set, fitted values unchanged on
+ *   the factor's rows.  work: sglm_chol64_minnorm_work_bytes(P, nf). */
+size_t sglm_chol64_work_bytes(int32_t P, int32_t nf);
+int sglm_chol64_factor(const float* H, int32_t P, const int32_t* hsrc, const float* dshift,
+                       const double* lamp, const int32_t* dsrc, int32_t nf, double tol,
+                       double* U, uint8_t* state, int32_t* nulls, int32_t* counts, void* work,
+                       sglm_stream_t stream);
+int sglm_chol64_solve(const double* U, int32_t P, const uint8_t* state, const int32_t* fits,
+                      const int32_t* fsrc, int32_t nq, const double* g, float* delta,
+                      sglm_stream_t stream);
+size_t sglm_chol64_minnorm_work_bytes(int32_t P, int32_t nf);
+int sglm_chol64_minnorm(const double* U, int32_t P, int32_t pw, const uint8_t* state,
+                        const int32_t* nulls, const int32_t* counts, int32_t nf,
+                        const int32_t* fits, const int32_t* fsrc, int32_t nfit, double* beta,
+                        void* work, sglm_stream_t stream);
+
 /* Per-fit scalars of a Newton step for the B fits k = slots[q], float64 (one workgroup per
  * fit): out[q][0..6+T) = { g.d, sum lam w^2, sum lam w d, sum lam d^2, max|d_a|,
  * max|w_a + t[j] d_a| for j < T, max|d_b| } over the P coordinates of g[k] (float64), beta[k]

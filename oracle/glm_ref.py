@@ -195,6 +195,34 @@ def weighted_gram(Xa, h, chunk=65536):
     return np.triu(H) + np.triu(H, 1).T
 
 
+def null_space(Xa):
+    """Orthonormal basis of null(Xa) (float64): right singular vectors whose singular value
+    is below lstsq's cut-off max(n, p) eps sigma_max (sklearn _base.py:699-701); for tall
+    designs the eigenvectors of Xa^T Xa below the squared cut-off."""
+    n, pa = Xa.shape
+    cut = max(n, pa) * np.finfo(np.float64).eps
+    if n * pa <= 5e7:
+        _, sv, vt = np.linalg.svd(Xa, full_matrices=False)
+        return vt[sv <= cut * sv[0]].T
+    ev, V = np.linalg.eigh(Xa.T @ Xa)
+    return V[:, ev <= max(cut * cut, 1e-13) * ev[-1]]
+
+
+def min_norm(Xa, coef, fit_intercept):
+    """The minimum-|w| point (w: the coefficients, not the intercept) of the solution set
+    coef + null(Xa): lstsq's answer on a rank-deficient design (centred lstsq = min |w| over
+    the same set), and the limit of lbfgs from w = 0, which stays in the row space."""
+    live = np.flatnonzero(np.any(Xa != 0.0, axis=0))    # all-zero columns keep their 0
+    N = null_space(Xa[:, live])
+    if N.shape[1] == 0:
+        return coef
+    nw = live.size - 1 if (fit_intercept and live[-1] == Xa.shape[1] - 1) else live.size
+    c = np.linalg.lstsq(N[:nw], coef[live[:nw]], rcond=None)[0]
+    out = coef.copy()
+    out[live] -= N @ c
+    return out
+
+
 def fit_tweedie_newton(X, y, alpha, power, link="auto", fit_intercept=True,
                        tol=1e-12, max_iter=200, coef0=None, return_iters=False,
                        augmented=False):
@@ -204,7 +232,8 @@ def fit_tweedie_newton(X, y, alpha, power, link="auto", fit_intercept=True,
     constants beta = 1/2, sigma = 2^-11 (_newton_solver.py:214).  Stops when the Newton
     step is below ``tol * (1 + |coef|_inf)`` or ``max|grad| <= tol`` (criterion 1 of
     _newton_solver.py:323-330).  Rank-deficient Hessians (alpha = 0 with all-zero
-    columns) fall back to the minimum-norm Newton step.  ``augmented``: X already carries
+    columns) fall back to the minimum-norm Newton step, and an unpenalised fit ends at the
+    minimum-norm point of its solution set (``min_norm``).  ``augmented``: X already carries
     the intercept's ones column as its LAST column (large designs: no hstack copy).
     """
     y = np.asarray(y, dtype=np.float64)
@@ -260,6 +289,8 @@ def fit_tweedie_newton(X, y, alpha, power, link="auto", fit_intercept=True,
         eta = eta + t * d_eta
         if np.max(np.abs(t * step)) <= tol * (1 + np.max(np.abs(coef))):
             break
+    if alpha == 0.0:
+        coef = min_norm(Xa, coef, fit_intercept)
     if fit_intercept:
         out = coef[:-1].copy(), float(coef[-1])
     else:
@@ -277,10 +308,18 @@ def fit_enet_cd(X, y, alpha, l1_ratio, fit_intercept=True, tol=1e-12, max_iter=1
         Xc, yc = X - xm, y - ym
     else:
         xm, ym, Xc, yc = np.zeros(p), 0.0, X, y
+    w = fit_enet_cd_gram(Xc.T @ Xc, Xc.T @ yc, n, alpha, l1_ratio, tol, max_iter)
+    return w, float(ym - xm @ w) if fit_intercept else 0.0
+
+
+def fit_enet_cd_gram(G, c, n, alpha, l1_ratio, tol=1e-12, max_iter=100000):
+    """The cyclic coordinate descent of ``fit_enet_cd`` given the (centred) Gram G = Xc^T Xc
+    and c = Xc^T yc of n rows (cd_fast's precomputed-Gram form); returns w."""
+    G = np.asarray(G, dtype=np.float64)
+    c = np.asarray(c, dtype=np.float64)
+    p = G.shape[0]
     l1 = alpha * l1_ratio * n
     l2 = alpha * (1.0 - l1_ratio) * n
-    G = Xc.T @ Xc
-    c = Xc.T @ yc
     w = np.zeros(p)
     q = -c.copy()          # = G w - c
     diag = np.diag(G).copy()
@@ -299,7 +338,7 @@ def fit_enet_cd(X, y, alpha, l1_ratio, fit_intercept=True, tol=1e-12, max_iter=1
             wmax = max(wmax, abs(new))
         if wmax == 0.0 or dmax / wmax < tol:
             break
-    return w, float(ym - xm @ w) if fit_intercept else 0.0
+    return w
 
 
 def fit(spec: FitSpec, X, y, tight=True):

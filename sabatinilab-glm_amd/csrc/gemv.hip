@@ -703,6 +703,16 @@ static int xtr_splits_for(int32_t P, int32_t B, int64_t nblk, int variant) {
 static int xtr_bits_splits(int32_t P, int32_t B, int64_t nblk) {
     return xtr_splits_for(P, B, nblk, xtr_variant(P, B));
 }
+// sglm_xtr_bits keeps every row slab at <= 1024 K-steps (65,536 rows): integer-valued R pieces
+// with |piece| <= 128 (the digit planes of enet.xty) then sum EXACTLY in the f32 accumulators
+// (|2 x 128 x 65536| = 2^24 with the 2.0 operand encoding), and the float64 slab reduction is
+// exact too
+constexpr int64_t kExactSlabSteps = 1024;
+static int xtr_bits_splits_capped(int32_t P, int32_t B, int64_t nblk) {
+    const int s = xtr_bits_splits(P, B, nblk);
+    const int64_t lo = (nblk + kExactSlabSteps - 1) / kExactSlabSteps;
+    return (int64_t)s < lo ? (int)lo : s;
+}
 // workspace bound over every variant (the switches may change between the query and a launch)
 static size_t xtr_part_bytes(int32_t P, int32_t B, int64_t nblk) {
     const int s = std::max(std::max(xtr_splits_for(P, B, nblk, 0), xtr_splits_for(P, B, nblk, 3)),
@@ -781,7 +791,10 @@ int sglm_gemv_eta_bits(const uint32_t* rbits, int64_t ld, int32_t P, float* beta
 size_t sglm_xtr_bits_work_bytes(int32_t P, int32_t B, int64_t ld) {
     const int64_t Bp = ((int64_t)B + 31) / 32 * 32;
     const int64_t nblk = ld / 64;
-    return (size_t)3 * Bp * ld * 2 + xtr_part_bytes(P, B, nblk);
+    const int64_t lo = (nblk + kExactSlabSteps - 1) / kExactSlabSteps;
+    const size_t floor_bytes = (size_t)lo * B * P * sizeof(float);
+    const size_t part = xtr_part_bytes(P, B, nblk);
+    return (size_t)3 * Bp * ld * 2 + (part > floor_bytes ? part : floor_bytes);
 }
 
 int sglm_xtr_bits(const uint32_t* cbits, int64_t ld, int32_t P, int64_t n, const float* R,
@@ -793,7 +806,7 @@ int sglm_xtr_bits(const uint32_t* cbits, int64_t ld, int32_t P, int64_t n, const
     }
     const int32_t Bp = (B + 31) / 32 * 32;
     const int64_t nblk = (n + 63) / 64;
-    const int splits = xtr_bits_splits(P, B, ld / 64);
+    const int splits = xtr_bits_splits_capped(P, B, ld / 64);
     hipStream_t s = as_stream(stream);
     __bf16* Rp = reinterpret_cast<__bf16*>(work);
     float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(work) + (size_t)3 * Bp * ld * 2);

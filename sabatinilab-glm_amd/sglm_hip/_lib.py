@@ -65,6 +65,13 @@ SIGNATURES = {
     "sglm_chol_graph_cache_clear": (C.c_int, []),
     "sglm_chol_solve_alias": (C.c_int, [_vp, _i32, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _i32, _vp,
                                         _vp]),
+    "sglm_chol64_work_bytes": (_sz, [_i32, _i32]),
+    "sglm_chol64_factor": (C.c_int, [_vp, _i32, _vp, _vp, _vp, _vp, _i32, C.c_double, _vp, _vp,
+                                     _vp, _vp, _vp, _vp]),
+    "sglm_chol64_solve": (C.c_int, [_vp, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp]),
+    "sglm_chol64_minnorm_work_bytes": (_sz, [_i32, _i32]),
+    "sglm_chol64_minnorm": (C.c_int, [_vp, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _vp,
+                                      _vp, _vp]),
     "sglm_step_scalars": (C.c_int, [_i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
     "sglm_step_update": (C.c_int, [_i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     "sglm_mask_stats_work_bytes": (_sz, [_i32, _i32, _i64]),

@@ -114,6 +114,14 @@ CHOL_SPLIT_MIN = int(__import__("os").environ.get("SGLM_CHOL_SPLIT_MIN", "6"))
 # 62.3 / 63.1 / 62.3 ms against 59.7 / 60.2 / 59.3 ms unpipelined, alternating on one box).
 # Default 0.
 GRAM_PIPE = int(__import__("os").environ.get("SGLM_GRAM_PIPE", "0") or 0)
+# Rank decisions of unpenalised fits (float64 factor of the exact mask Gram, sglm_chol64_factor):
+# a pivot whose Schur complement is <= tol * its diagonal is a dependent column.  The Gram of a
+# 0/1 design is exact (integer counts in f32), so tol only has to clear float64 elimination
+# noise (~1e-16 relative; a full-rank design would need cond(X^T X) > 1e9 to be truncated); the
+# f32-accumulated Gram of a real-valued design carries ~1e-7 relative noise, so dependence there
+# is judged at the f32 factor's former threshold.
+RANK_TOL_EXACT = float(__import__("os").environ.get("SGLM_RANK_TOL_EXACT", "1e-9"))
+RANK_TOL_F32 = float(__import__("os").environ.get("SGLM_RANK_TOL_F32", "1e-6"))
 
 
 def _gram_groups(form, uniq, dup):
@@ -728,6 +736,7 @@ class IrlsStats:
     aliased: int = 0            # fit-iterations solved on a family representative's factor
     shared: int = 0             # fit-iterations on a lambda neighbour's Gram (own factor)
     lag_grams: int = 0          # Grams from the event cross-correlations (sglm_lag_gram)
+    rank_grams: int = 0         # exact mask Grams for the rank decisions of unpenalised fits
     chain_host_s: float = 0.0   # host time spent enqueueing the factorisation chains
     aa_fit_iters: int = 0       # fit-iterations whose direction took the secant correction
     alg_flop: float = 0.0       # SURVEY.md §8(d) F summed over fit-iterations
@@ -1149,6 +1158,56 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
     bf.up = up
     pd_h = _pinned("pairdist", 4 * B0, torch.float32)
 
+    # float64 factors (sglm_chol64_factor) with exact rank decisions: every squared-loss fit
+    # solves on the factor of its (mask, penalty, intercept) -- the reference's closed forms
+    # run in float64 (lstsq / cholesky, sklearn _base.py:701, _ridge.py:201-213) -- and an
+    # unpenalised log-link fit takes its dependent columns from the float64 factor of its mask's
+    # exact Gram (null(X~^T W X~) = null(X~^T M X~) for W > 0).  Unpenalised fits end at the
+    # minimum-norm point of their solution set (lstsq; lbfgs from 0 stays in the row space).
+    lam0 = lam == 0.0
+    f64, fkey = None, np.full(B0, -1, dtype=np.int64)
+    if const_hess:
+        mrep = {}
+        for k, r in enumerate(reqs):
+            mrep.setdefault(int(r.mask), k)
+        keys, k_h, k_d = {}, [], []
+        # the unpenalised fits' factors first: the minimum-norm pass needs only those
+        for k in np.argsort(~lam0, kind="stable"):
+            r = reqs[k]
+            key = (int(r.mask), float(r.lam), bool(r.fit_intercept))
+            if key not in keys:
+                keys[key] = len(k_h)
+                k_h.append(mrep[int(r.mask)])
+                k_d.append(k)
+            fkey[k] = keys[key]
+        # a persistent copy: an upload-arena view is only valid until the second sync after it
+        fkey_d = torch.empty(B0, dtype=torch.int32, device=dev)
+        fkey_d.copy_(up(fkey, np.int32))
+    elif lam0.any():
+        keys, k_h = {}, []
+        for k in np.flatnonzero(lam0):
+            key = (int(reqs[k].mask), bool(reqs[k].fit_intercept))
+            if key not in keys:
+                keys[key] = len(k_h)
+                k_h.append(int(k))
+            fkey[k] = keys[key]
+        k_h = np.asarray(k_h, dtype=np.int32)
+        # the exact mask Gram of each (W = the mask's multiplicities; the first link update
+        # overwrites W)
+        kh_d = up(k_h, np.int64)
+        bf.W[kh_d] = prob.M[up(fmask_h[k_h], np.int64)].float()
+        _syrk(d, bf, k_h, nsteps, ntile1, None, st, exact=True, rows=gram_rows)
+        sum_hess(k_h)
+        f64 = _Factor64(d, bf, k_h, k_h, lamp_d, st)
+        sel = np.flatnonzero(lam0)
+        sel_d = up(sel, np.int64)
+        stt = f64.state[up(fkey[sel], np.int64)]
+        frz = (stt == 1) | (stt == 3)
+        ds = bf.dshift[sel_d]
+        bf.dshift[sel_d] = torch.where(frz, torch.full_like(ds, -1.0), ds)
+        if stats is not None:
+            stats.rank_grams += int(k_h.size)
+
     def hkey(k):
         """Fits with equal keys have bitwise equal Hessians: one (mask, response) at the
         common start -- which depends on the intercept setting (log(mean y) or 0) -- or the
@@ -1321,10 +1380,9 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
                 _syrk(d, bf, rep_idx, nsteps, ntile1, stats, st, exact=True, rows=gram_rows)
                 sum_hess(rep_idx)
                 gram_comp[rep_idx] = True
-                for k in act:
-                    rk = reps[reqs[k].mask]
-                    if rk != k:
-                        bf.H[k].copy_(bf.H[rk])
+                # one float64 factor per (mask, penalty, intercept), from its mask's Gram
+                f64 = _Factor64(d, bf, np.asarray([reps[reqs[k].mask] for k in k_d]),
+                                np.asarray(k_d), lamp_d, st)
         else:
             # decisions planned at the end of the previous iteration (their device distances are
             # long computed): keep / form / share / alias (see _hess_plan)
@@ -1370,10 +1428,15 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
         t0 = tick("it_gram", t0)
         bf.delta[:B].zero_()
         if const_hess:
-            order, nref = act, (0 if factored else act.size)
-        else:
+            # the float64 step on the fit's own (mask, penalty) factor; with the exact gradient
+            # one refinement pass absorbs the f32 / bf16 roundings of the step
+            order, nref = act, 0
+            _gradient()
+            t0 = tick("it_gradient", t0)
+            _lib.call("sglm_chol64_solve", _p(f64.U), P, _p(f64.state), _p(act_d),
+                      _p(fkey_d[act_d.long()]), na, _p(bf.gtot), _p(bf.delta), st)
+        elif SOLVE_INV:
             order, nref = np.concatenate([form, keep]), form.size
-        if SOLVE_INV:
             # one list: factored and kept fits on their own inverses, then the aliased fits
             # grouped by representative (tiles of <= 32 fits sharing one inverse)
             al = ali[np.argsort(repl[ali], kind="stable")] if (not const_hess and ali.size) \
@@ -1489,6 +1552,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
                 owned[lst] = 1
                 comm.directions_(bf.delta[:B], up(owned, np.uint8))
         else:
+            order, nref = np.concatenate([form, keep]), form.size
             _gradient()
             t0 = tick("it_gradient", t0)
             fits_d = up(order, np.int32)
@@ -1721,6 +1785,11 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
             plan = hess_plan(nxt)
         t0 = tick("it_update", t0)
 
+    # unpenalised fits: the minimum-norm point of the solution set (lstsq's answer on a
+    # rank-deficient design; the fitted values on the fit's rows are unchanged)
+    if f64 is not None:
+        pf = np.flatnonzero(lam0 & (fkey >= 0))
+        f64.minnorm(d, bf, pf, fkey[pf], beta64_d, st)
     # final linear predictor from the final coefficients, in request order (no accumulated
     # drift), enqueued before the readbacks so the host's one wait covers it
     bf.beta[:B0].copy_(beta64_d)
@@ -1734,9 +1803,17 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
         comm.sum_owned_(inf)
     else:
         inf = bf.info[:B]
-    outs = torch.cat([beta64_d.reshape(-1), inf.to(torch.float64)]).cpu().numpy()
+    parts = [beta64_d.reshape(-1), inf.to(torch.float64)]
+    if f64 is not None:
+        parts.append(f64.counts[:, 1].to(torch.float64))
+    outs = torch.cat(parts).cpu().numpy()
     out_beta[:] = outs[: B0 * P].reshape(B0, P)
-    out_info[:] = outs[B0 * P:].astype(np.int64)
+    out_info[:] = outs[B0 * P:B0 * P + B0].astype(np.int64)
+    if f64 is not None:
+        # coordinates the float64 factor found dependent or zero
+        cnt = outs[B0 * P + B0:].astype(np.int64)
+        has = fkey >= 0
+        out_info[has] = np.maximum(0 if const_hess else out_info[has], cnt[fkey[has]])
     bf.prob = bf.keep = bf.up = bf.fit_mask_d = None   # drop the compacted designs with the problem
     res = []
     for k, r in enumerate(reqs0):
@@ -1967,6 +2044,44 @@ def _lag_gram(d: Design, bf, fits: np.ndarray, st):
     _lib.call("sglm_lag_gram", _p(lg.occ), _p(lg.ev_off), _p(lg.ebits), lg.nwords,
               _p(lg.shifts), lg.m, lg.K, lg.layout, lg.smin, lg.smax, lg.row0, lg.n, lg.n_raw,
               d.P, _p(bf.W), d.ld, _p(fits_d), int(fits.size), _p(bf.H), _p(work), st)
+
+
+class _Factor64:
+    """Float64 factors of Grams (sglm_chol64_factor): U [nf][P][P], coordinate states, the
+    dependent coordinates and their counts, all on the device."""
+
+    def __init__(self, d: Design, bf, hsrc, dsrc, lamp_d, st):
+        P, dev = d.P, d.device
+        nf = len(hsrc)
+        self.nf = nf
+        self.U = torch.empty((nf, P, P), dtype=torch.float64, device=dev)
+        self.state = torch.empty((nf, P), dtype=torch.uint8, device=dev)
+        self.nulls = torch.empty((nf, P), dtype=torch.int32, device=dev)
+        self.counts = torch.zeros((nf, 2), dtype=torch.int32, device=dev)
+        upl = getattr(bf, "up", None)
+        idx = np.concatenate([np.asarray(hsrc), np.asarray(dsrc)]).astype(np.int32)
+        idx_d = upl(idx, np.int32) if upl is not None else torch.from_numpy(idx).to(dev)
+        work = _work(_lib.query("sglm_chol64_work_bytes", P, nf), dev, "chol64")
+        tol = RANK_TOL_EXACT if d.xbits is not None else RANK_TOL_F32
+        _lib.call("sglm_chol64_factor", _p(bf.H), P, _p(idx_d[:nf]), _p(bf.dshift), _p(lamp_d),
+                  _p(idx_d[nf:]), nf, tol, _p(self.U), _p(self.state), _p(self.nulls),
+                  _p(self.counts), _p(work), st)
+
+    def minnorm(self, d: Design, bf, fits, fsrc, beta64_d, st):
+        """beta[fits[q]] <- the minimum-norm point of its solution set on factor fsrc[q] (the
+        factors 0 .. max(fsrc) take part)."""
+        if len(fits) == 0:
+            return
+        nf = int(np.max(fsrc)) + 1
+        upl = getattr(bf, "up", None)
+        idx = np.concatenate([np.asarray(fits), np.asarray(fsrc)]).astype(np.int32)
+        idx_d = upl(idx, np.int32) if upl is not None else torch.from_numpy(idx).to(d.device)
+        nq = len(fits)
+        work = _work(_lib.query("sglm_chol64_minnorm_work_bytes", d.P, nf), d.device,
+                     "minnorm")
+        _lib.call("sglm_chol64_minnorm", _p(self.U), d.P, d.p, _p(self.state), _p(self.nulls),
+                  _p(self.counts), nf, _p(idx_d[:nq]), _p(idx_d[nq:]), nq, _p(beta64_d),
+                  _p(work), st)
 
 
 def _syrk(d: Design, bf, fits: np.ndarray, nsteps: int, ntile1: int, stats, st, exact=False,

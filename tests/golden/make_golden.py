@@ -11,6 +11,7 @@ Sources — never the reference code itself (its import/execution was denied, SU
 
 Usage: ``python tests/golden/make_golden.py`` -> tests/golden/*.npz / *.json
        ``python tests/golden/make_golden.py api`` -> tests/golden/api.npz only
+       ``python tests/golden/make_golden.py rank`` -> tests/golden/rank.npz only
 """
 from __future__ import annotations
 
@@ -107,6 +108,70 @@ def fits():
     olr = LinearRegression().fit(Xr, yn)
     out.update(olsr_X=Xr, olsr_coef=olr.coef_, olsr_b=np.array(olr.intercept_))
     return out, meta
+
+
+def _lag_X(E, L, N):
+    """Shift-major lag expansion of synth.Synthetic.dense_X (shifts [0] + [-L..-1] + [1..L-1])."""
+    return synth.Synthetic(E=E, L=L, shifts=synth.shift_list(L), N=N, beta=None, intercept=0.0,
+                           y=None, trial=None, family="gaussian").dense_X()
+
+
+def rank_cases():
+    """Round-4 pins of lstsq's minimum-norm answer (backend/sglm.py:96-101 -> sklearn
+    _base.py:701) and of unpenalised Poisson lbfgs from w = 0 (backend/sglm.py:112-115):
+    * dup: C1 shape (10k x 100, 10 events x lags -5..4) with event 9 a copy of event 2 (ten
+      duplicated lag columns) and event 5 never occurring (ten zero columns) -> LinearRegression;
+    * ill: a full-rank 0/1 lag design with cond(X~^T X~) ~ 7e6: two slow state indicators
+      (runs of 2000-5000 rows) that differ on one row, plus a sparse event, lags -15..14 ->
+      LinearRegression (a float32 factor cannot resolve it);
+    * pdup: Poisson 3000 x 41 with a duplicated column, alpha = 0, lbfgs at tol 1e-12.
+    Events are stored bit-packed; the tests rebuild X with the same expansion."""
+    out = {}
+    s = synth.make(N=10000, m=10, L=5, family="gaussian", rho=0.05, seed=7)
+    E = s.E.copy()
+    E[:, 9] = E[:, 2]
+    E[:, 5] = 0.0
+    X = _lag_X(E, 5, 10000)
+    rng = np.random.default_rng(71)
+    y = X @ rng.normal(0, 0.3, X.shape[1]) + 0.5 + rng.normal(0, 1, X.shape[0])
+    ols = LinearRegression().fit(X, y)
+    out.update(dup_E=np.packbits(E.astype(np.uint8), axis=0), dup_shape=np.array(E.shape),
+               dup_L=np.array(5), dup_N=np.array(10000), dup_y=y, dup_coef=ols.coef_,
+               dup_b=np.array(ols.intercept_))
+    # ill-conditioned, full rank
+    rng = np.random.default_rng(5)
+    L, N = 15, 100000
+    Nr = N + 2 * L - 1
+
+    def runs(lo, hi):
+        x = np.zeros(Nr)
+        t, v = 0, int(rng.integers(0, 2))
+        while t < Nr:
+            n_ = int(rng.integers(lo, hi))
+            x[t:t + n_] = v
+            v, t = 1 - v, t + n_
+        return x
+    e1 = runs(2000, 5000)
+    e2 = e1.copy()
+    e2[Nr // 3] = 1 - e2[Nr // 3]
+    E = np.stack([e1, e2, (rng.random(Nr) < 0.05).astype(float)], 1).astype(np.float32)
+    X = _lag_X(E, L, N)
+    beta = rng.normal(0, 0.5, X.shape[1])
+    y = np.round((X @ beta + 0.3 + rng.normal(0, 1, N)) * 4096) / 4096
+    Xt = np.hstack([X, np.ones((N, 1))])
+    ev = np.linalg.eigvalsh(Xt.T @ Xt)
+    ols = LinearRegression().fit(X, y)
+    out.update(ill_E=np.packbits(E.astype(np.uint8), axis=0), ill_shape=np.array(E.shape),
+               ill_L=np.array(L), ill_N=np.array(N), ill_y=y, ill_coef=ols.coef_,
+               ill_b=np.array(ols.intercept_), ill_cond=np.array(ev[-1] / ev[0]))
+    # Poisson, duplicated column, alpha = 0: lbfgs from 0 keeps the duplicates equal
+    sp = synth.make(N=3000, m=4, L=5, family="poisson", rho=0.05, seed=10, beta_scale=0.3)
+    Xp = np.hstack([sp.dense_X(), sp.dense_X()[:, [5]]])
+    tp = TweedieRegressor(power=1, alpha=0.0, tol=1e-12, max_iter=100000).fit(Xp, sp.y)
+    out.update(pdup_X=np.packbits(Xp.astype(np.uint8), axis=0), pdup_shape=np.array(Xp.shape),
+               pdup_y=sp.y, pdup_coef=tp.coef_, pdup_b=np.array(tp.intercept_),
+               pdup_niter=np.array(tp.n_iter_))
+    return out
 
 
 def folds():
@@ -226,7 +291,12 @@ def main():
         np.savez_compressed(os.path.join(HERE, "api.npz"), **api_extras())
         print("api fixture written")
         return
+    if sys.argv[1:] == ["rank"]:           # round-4 fixture only (others unchanged)
+        np.savez_compressed(os.path.join(HERE, "rank.npz"), **rank_cases())
+        print("rank fixture written")
+        return
     np.savez_compressed(os.path.join(HERE, "api.npz"), **api_extras())
+    np.savez_compressed(os.path.join(HERE, "rank.npz"), **rank_cases())
     np.savez_compressed(os.path.join(HERE, "timeshift_known.npz"), **timeshift_known_answers())
     f, meta = fits()
     np.savez_compressed(os.path.join(HERE, "fits.npz"), **f)

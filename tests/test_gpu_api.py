@@ -54,15 +54,18 @@ def test_glm_all_families_vs_golden(engine, golden):
 
 
 def test_glm_rank_deficient_ols(engine, golden):
-    """Duplicate + all-zero column, alpha = 0: the engine freezes the zero column and the
-    dropped duplicate pivot; predictions match the min-norm lstsq fit (coefficients of the
-    duplicated pair are not unique — parity is on the fitted values)."""
+    """Duplicate + all-zero column, alpha = 0: the COEFFICIENTS equal lstsq's minimum-norm
+    solution (sklearn _base.py:701; the duplicated pair splits the weight equally), the zero
+    column's coefficient is 0, and the fitted values match."""
     import sglm
     g = golden("fits.npz")
     X, y = g["olsr_X"], g["gau_y"]
     glm = sglm.GLM("Normal", alpha=0)
     glm.fit(X, y)
+    assert rel(glm.coef_, g["olsr_coef"]) < TOL_GAUSS
+    assert abs(glm.intercept_ - float(g["olsr_b"])) < TOL_GAUSS * max(1, abs(float(g["olsr_b"])))
     assert glm.coef_[7] == 0.0
+    assert abs(glm.coef_[2] - glm.coef_[6]) < 1e-9
     pred_ref = X @ g["olsr_coef"] + float(g["olsr_b"])
     assert rel(glm.predict(X), pred_ref) < 1e-5
 

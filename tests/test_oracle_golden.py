@@ -206,3 +206,37 @@ def test_warm_start_oracle_reaches_the_same_minimiser(golden):
                                       coef0=np.r_[g["warm_w0"], float(g["warm_b0"])])
     assert np.max(np.abs(c - g["warm_coef"])) < 1e-8
     assert abs(b - float(g["warm_b"])) < 1e-8
+
+
+# ------------------------------------------------------------------ rank deficiency (round 4)
+def rank_design(g, key):
+    """X of a rank.npz case, rebuilt from its bit-packed events with the fixture's expansion."""
+    from sglm_hip import synth
+    if key == "pdup":
+        sh = tuple(g["pdup_shape"])
+        return np.unpackbits(g["pdup_X"], axis=0)[: sh[0]].astype(np.float64)
+    sh = tuple(g[f"{key}_shape"])
+    E = np.unpackbits(g[f"{key}_E"], axis=0)[: sh[0]].astype(np.float32)
+    L, N = int(g[f"{key}_L"]), int(g[f"{key}_N"])
+    return synth.Synthetic(E=E, L=L, shifts=synth.shift_list(L), N=N, beta=None, intercept=0.0,
+                           y=None, trial=None, family="gaussian").dense_X()
+
+
+def test_rank_fixtures_pin_the_oracle(golden):
+    """lstsq's minimum-norm OLS on a duplicated-event lag design and on a cond ~7e6 full-rank
+    0/1 design, and unpenalised Poisson lbfgs from 0 with a duplicated column: the oracle
+    (glm_ref.fit_ols / fit_tweedie_newton) reproduces sklearn's answers."""
+    g = golden("rank.npz")
+    X = rank_design(g, "dup")
+    c, b = glm_ref.fit_ols(X, g["dup_y"])
+    assert rel(c, g["dup_coef"]) < 1e-9 and abs(b - float(g["dup_b"])) < 1e-9
+    for bi in range(10):                       # event 9 duplicates event 2: equal split
+        assert abs(c[bi * 10 + 2] - c[bi * 10 + 9]) < 1e-12
+        assert abs(c[bi * 10 + 5]) < 1e-12     # event 5 never occurs
+    X = rank_design(g, "ill")
+    assert 1e6 < float(g["ill_cond"]) < 1e8
+    c, b = glm_ref.fit_ols(X, g["ill_y"])
+    assert rel(c, g["ill_coef"]) < 1e-8
+    X = rank_design(g, "pdup")
+    c, b = glm_ref.fit_tweedie_newton(X, g["pdup_y"], 0.0, 1.0)
+    assert rel(c, g["pdup_coef"]) < 1e-6 and abs(c[5] - c[-1]) < 1e-12
