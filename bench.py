@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-dropin", action="store_true",
+                    help="skip the drop-in production-flow leg (dropin_grid_s)")
     ap.add_argument("--cpu-rows", type=int, default=100_000,
                     help="rows of the oracle Newton sample (secondary CPU figure)")
     ap.add_argument("--sklearn-rows", type=int, default=100_000,
@@ -598,6 +600,52 @@ def spawn_ranks(a):
     sys.exit(subprocess.call(cmd))
 
 
+def dropin_frame(s):
+    """The host event DataFrame the reference's production flow starts from
+    (er_refactored_from_scratch_cleanup.py:421-452): the N_raw rows of the 50 float64 event
+    columns, nTrial, and the response (NaN on the rows the lag expansion cannot fill)."""
+    import pandas as pd
+    Nr, m = s.E.shape
+    r0 = s.L - 1
+    ev = [f"e{a}" for a in range(m)]
+    df = pd.DataFrame(s.E.astype(np.float64), columns=ev)
+    t = np.arange(Nr)
+    df.insert(0, "nTrial", ((t - r0) // 100).astype(np.float64))
+    y = np.full(Nr, np.nan)
+    y[r0:r0 + s.N] = s.y
+    df["y"] = y
+    return df, ev
+
+
+def dropin_grid(df, ev, L, K, lams):
+    """The drop-in flow timed end to end: sglm_ez.timeshift_cols (lags -L..L-1) -> the NaN-row
+    filter -> cv_idx_by_trial_id (seed 3) -> sglm_ez.simple_cv_fit over the 20 Poisson alphas.
+    Returns (result dict, per-phase seconds)."""
+    import contextlib
+    import io
+    import torch
+    import sglm_ez
+    ph = {}
+    t = time.perf_counter()
+    dfrel = sglm_ez.timeshift_cols(df, ev, neg_order=-L, pos_order=L - 1)
+    xcols = sglm_ez.add_timeshifts_to_col_list(ev, ev, neg_order=-L, pos_order=L - 1)
+    ph["timeshift_cols"] = time.perf_counter() - t
+    t = time.perf_counter()
+    dfrel = dfrel[dfrel[["nTrial"] + xcols + ["y"]].isna().sum(axis=1) == 0]
+    ph["nan_filter"] = time.perf_counter() - t
+    t = time.perf_counter()
+    np.random.seed(3)
+    cv_idx = sglm_ez.cv_idx_by_trial_id(dfrel, trial_id_columns=["nTrial"], num_folds=K)
+    ph["folds"] = time.perf_counter() - t
+    t = time.perf_counter()
+    kws = [{"model_name": "Poisson", "alpha": float(al)} for al in lams]
+    with contextlib.redirect_stdout(io.StringIO()):       # the reference prints per parameter
+        out = sglm_ez.simple_cv_fit(dfrel[xcols], dfrel["y"], cv_idx, kws, model_type="Normal")
+    torch.cuda.synchronize()
+    ph["simple_cv_fit"] = time.perf_counter() - t
+    return out[4], ph
+
+
 def newton_distance(s, design, cv_idx, res, lams, checks):
     """float64 Newton distance of a few fits of the last grid to the exact minimiser,
     max_j<p |(H^-1 g)_j| / max_j<p |beta_j| (the coefficients), from the exact design on the
@@ -744,6 +792,30 @@ def main():
             # float64 Newton distance of the lambda = 1e-4 split-0 fit and refit (parity spot
             # check of the timed grid's output; tests/test_gpu_fullsize.py checks every fit)
             ndist = newton_distance(s, design, cv_idx, res, lams, [(0, 0), (0, -1)])
+        dropin = None
+        if world == 1 and a.config in ("c3", "c4") and not a.no_dropin:
+            # the production flow through the drop-in API from a host event DataFrame (the
+            # design stays on the device: sglm_hip.lagframe), one warm pass then timed passes
+            df, ev = dropin_frame(s)
+            dropin_grid(df, ev, L, K, lams)
+            walls, phs = [], []
+            for _ in range(3):
+                torch.cuda.synchronize()
+                t_d = time.perf_counter()
+                dres, ph = dropin_grid(df, ev, L, K, lams)
+                walls.append(time.perf_counter() - t_d)
+                phs.append(ph)
+            q = int(np.argmin(walls))
+            diff = max(float(np.max(np.abs(r["model"].coef_ - g["refit_coef"])) /
+                             max(float(np.max(np.abs(g["refit_coef"]))), 1e-30))
+                       for r, g in zip(dres["full_cv_results"], res))
+            dropin = {"dropin_grid_s": walls[q], "dropin_grid_s_runs": walls,
+                      "dropin_over_grid": walls[q] / grid_s,
+                      "dropin_phases_ms": {k: v * 1e3 for k, v in phs[q].items()},
+                      "dropin_refit_coef_max_rel_vs_grid": diff,
+                      "dropin_flow": "host event DataFrame (float64, N_raw rows) -> "
+                                     "sglm_ez.timeshift_cols -> isna().sum(axis=1) == 0 row "
+                                     "filter -> cv_idx_by_trial_id -> simple_cv_fit"}
         cpu = None
         if not a.no_cpu and world == 1:
             cpu = cpu_reference_grid(s, cv_idx, lams, a.sklearn_rows)
@@ -785,6 +857,7 @@ def main():
                 "all_converged": bool(conv),
                 "stagnation_or_failed_stops": stag + failed,
                 "newton_dist_f64": ndist,
+                **(dropin or {}),
                 "setup_s": round(setup_s, 2),
                 "parallelism": (f"row slabs over {world} ranks: RCCL all-reduce of the slab "
                                 f"Grams, gradients, trial losses and directions" if rows_mode

@@ -65,6 +65,16 @@ int sglm_timeshift_expand(const void* src, int64_t n_src, int64_t rs_src, int64_
                           int64_t row0, int32_t elem_size, uint64_t fill_bits,
                           sglm_stream_t stream);
 
+/* sglm_timeshift_expand with a row list: out(t, j) = src(rows[t] - shift[j], src_col[j]) when
+ * that source row lies in [0, n_src), else fill_bits (rows: device int64 [n_out]) -- the rows
+ * a lagged DataFrame keeps after its NaN / holdout filters (sglm_hip.lagframe), expanded
+ * without the intermediate frame the reference materialises (backend/sglm_pp.py:58-103). */
+int sglm_timeshift_gather(const void* src, int64_t n_src, int64_t rs_src, int64_t cs_src,
+                          const int32_t* src_col, const int32_t* shift, int32_t ncols_out,
+                          void* out, int64_t n_out, int64_t rs_out, int64_t cs_out,
+                          const int64_t* rows, int32_t elem_size, uint64_t fill_bits,
+                          sglm_stream_t stream);
+
 /* Pack a row-major (n x p) f32/f64 design (strides in elements) into the feature-major
  * layout: Xb (bf16, required), Xf (f32, optional/nullable), ones column at a = p when
  * add_ones, zero padding to (P, ld).  *inexact (device int32, caller-zeroed) is set to 1
@@ -74,6 +84,13 @@ int sglm_timeshift_expand(const void* src, int64_t n_src, int64_t rs_src, int64_
 int sglm_pack_design(const void* src, int32_t src_is_f64, int64_t n, int32_t p,
                      int64_t rs, int64_t cs, int32_t add_ones, uint16_t* Xb, float* Xf,
                      int64_t ld, int32_t P, int32_t* inexact, sglm_stream_t stream);
+
+/* sglm_pack_design for one chunk of a chunked upload: source rows 0 .. n go to design rows
+ * dst0 .. dst0 + n (dst0 a multiple of 64); only the 64-row tiles of the chunk are written
+ * (rows past the chunk inside its last tile as zero: chunks go in ascending order). */
+int sglm_pack_design_rows(const void* src, int32_t src_is_f64, int64_t n, int32_t p, int64_t rs,
+                          int64_t cs, int32_t add_ones, uint16_t* Xb, float* Xf, int64_t ld,
+                          int32_t P, int64_t dst0, int32_t* inexact, sglm_stream_t stream);
 
 /* --- IRLS inner step (one batched Newton iteration over B fits) -------------------------
  * Replaces the per-fit solver iterations inside self.model.fit (backend/sglm.py:241):
@@ -568,6 +585,13 @@ enum { SGLM_MASK_ALL = 0, SGLM_MASK_FOLD = 1, SGLM_MASK_ROWS = 2 };
 int sglm_host_masks(int32_t nm, const int64_t* const* idx, const int64_t* len,
                     const int32_t* kind, int64_t n, int64_t ld, uint8_t* out, int64_t* nnz,
                     double* sum, int32_t nthreads);
+
+/* Threaded host copies into pinned staging buffers (chunked uploads): sglm_host_copy copies
+ * nbytes; sglm_host_gather_cols copies ncols columns of nrows elements of elem bytes (host
+ * pointers src[c]) to dst column-major.  Host only, no device pointers. */
+int sglm_host_copy(void* dst, const void* src, int64_t nbytes, int32_t nthreads);
+int sglm_host_gather_cols(const void* const* src, int32_t ncols, int64_t nrows, int32_t elem,
+                          void* dst, int32_t nthreads);
 
 #ifdef __cplusplus
 }

@@ -29,17 +29,20 @@ int check_launch(const char* what) {
 // One output column per blockIdx.y (grid-strided), rows grid-strided over x.  For the
 // feature-major engine layout (rs = 1) both the read of the source column segment and the
 // write of the output column are contiguous: the lag expansion is a shifted memcpy.
+// rows (nullable): output row t reads source row rows[t] - shift instead of t + row0 - shift
+// (a row selection of the lagged frame, sglm_timeshift_gather).
 template <typename T>
 __global__ void __launch_bounds__(256) timeshift_kernel(
     const T* __restrict__ src, int64_t n_src, int64_t rs_src, int64_t cs_src,
     const int32_t* __restrict__ src_col, const int32_t* __restrict__ shift, int32_t ncols,
-    T* __restrict__ out, int64_t n_out, int64_t rs_out, int64_t cs_out, int64_t row0, T fill) {
+    T* __restrict__ out, int64_t n_out, int64_t rs_out, int64_t cs_out, int64_t row0, T fill,
+    const int64_t* __restrict__ rows) {
     for (int j = blockIdx.y; j < ncols; j += gridDim.y) {
         const int64_t c = src_col[j];
         const int64_t s = shift[j];
         for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n_out;
              t += (int64_t)gridDim.x * blockDim.x) {
-            const int64_t r = t + row0 - s;
+            const int64_t r = (rows ? rows[t] : t + row0) - s;
             out[t * rs_out + j * cs_out] =
                 (r >= 0 && r < n_src) ? src[r * rs_src + c * cs_src] : fill;
         }
@@ -48,10 +51,13 @@ __global__ void __launch_bounds__(256) timeshift_kernel(
 
 // ------------------------------------------------------------------------------ pack
 // 64x64 LDS transpose: row-major f32/f64 source -> feature-major bf16 (+ f32).
+// dst0: first destination row (a 64-aligned chunk of a chunked upload); src row i goes to
+// destination row dst0 + i, and only the tiles covering the chunk are written.
 template <typename TS>
 __global__ void __launch_bounds__(256) pack_kernel(
     const TS* __restrict__ src, int64_t n, int32_t p, int64_t rs, int64_t cs, int32_t add_ones,
-    uint16_t* __restrict__ Xb, float* __restrict__ Xf, int64_t ld, int32_t* inexact) {
+    uint16_t* __restrict__ Xb, float* __restrict__ Xf, int64_t ld, int32_t* inexact,
+    int64_t dst0 = 0) {
     __shared__ float tile[64][65];
     const int64_t i0 = (int64_t)blockIdx.x * 64;
     const int32_t a0 = blockIdx.y * 64;
@@ -76,7 +82,7 @@ __global__ void __launch_bounds__(256) pack_kernel(
         const float v = tile[tx][c];
         const __bf16 hb = (__bf16)v;
         bad |= ((float)hb != v);
-        const int64_t off = (int64_t)(a0 + c) * ld + i0 + tx;
+        const int64_t off = (int64_t)(a0 + c) * ld + dst0 + i0 + tx;
         Xb[off] = __builtin_bit_cast(uint16_t, hb);
         if (Xf) Xf[off] = v;
     }
@@ -627,11 +633,39 @@ extern "C" {
 const char* sglm_last_error(void) { return g_err; }
 int sglm_version(void) { return 1; }
 
+static int timeshift_launch(const void* src, int64_t n_src, int64_t rs_src, int64_t cs_src,
+                            const int32_t* src_col, const int32_t* shift, int32_t ncols_out,
+                            void* out, int64_t n_out, int64_t rs_out, int64_t cs_out,
+                            int64_t row0, int32_t elem_size, uint64_t fill_bits,
+                            const int64_t* rows, sglm_stream_t stream);
+
 int sglm_timeshift_expand(const void* src, int64_t n_src, int64_t rs_src, int64_t cs_src,
                           const int32_t* src_col, const int32_t* shift, int32_t ncols_out,
                           void* out, int64_t n_out, int64_t rs_out, int64_t cs_out,
                           int64_t row0, int32_t elem_size, uint64_t fill_bits,
                           sglm_stream_t stream) {
+    return timeshift_launch(src, n_src, rs_src, cs_src, src_col, shift, ncols_out, out, n_out,
+                            rs_out, cs_out, row0, elem_size, fill_bits, nullptr, stream);
+}
+
+int sglm_timeshift_gather(const void* src, int64_t n_src, int64_t rs_src, int64_t cs_src,
+                          const int32_t* src_col, const int32_t* shift, int32_t ncols_out,
+                          void* out, int64_t n_out, int64_t rs_out, int64_t cs_out,
+                          const int64_t* rows, int32_t elem_size, uint64_t fill_bits,
+                          sglm_stream_t stream) {
+    if (n_out > 0 && ncols_out > 0 && !rows) {
+        set_error("sglm_timeshift_gather: null row list");
+        return SGLM_EINVAL;
+    }
+    return timeshift_launch(src, n_src, rs_src, cs_src, src_col, shift, ncols_out, out, n_out,
+                            rs_out, cs_out, 0, elem_size, fill_bits, rows, stream);
+}
+
+static int timeshift_launch(const void* src, int64_t n_src, int64_t rs_src, int64_t cs_src,
+                            const int32_t* src_col, const int32_t* shift, int32_t ncols_out,
+                            void* out, int64_t n_out, int64_t rs_out, int64_t cs_out,
+                            int64_t row0, int32_t elem_size, uint64_t fill_bits,
+                            const int64_t* rows, sglm_stream_t stream) {
     if (ncols_out <= 0 || n_out <= 0) return SGLM_OK;
     if (!src || !out || !src_col || !shift || n_src < 0) {
         set_error("sglm_timeshift_expand: null pointer or negative size");
@@ -640,13 +674,32 @@ int sglm_timeshift_expand(const void* src, int64_t n_src, int64_t rs_src, int64_
     dim3 grid(grid1(n_out, 256, 1024), (unsigned)(ncols_out < 32768 ? ncols_out : 32768));
     hipStream_t s = as_stream(stream);
     switch (elem_size) {
-        case 1: timeshift_kernel<uint8_t><<<grid, 256, 0, s>>>((const uint8_t*)src, n_src, rs_src, cs_src, src_col, shift, ncols_out, (uint8_t*)out, n_out, rs_out, cs_out, row0, (uint8_t)fill_bits); break;
-        case 2: timeshift_kernel<uint16_t><<<grid, 256, 0, s>>>((const uint16_t*)src, n_src, rs_src, cs_src, src_col, shift, ncols_out, (uint16_t*)out, n_out, rs_out, cs_out, row0, (uint16_t)fill_bits); break;
-        case 4: timeshift_kernel<uint32_t><<<grid, 256, 0, s>>>((const uint32_t*)src, n_src, rs_src, cs_src, src_col, shift, ncols_out, (uint32_t*)out, n_out, rs_out, cs_out, row0, (uint32_t)fill_bits); break;
-        case 8: timeshift_kernel<uint64_t><<<grid, 256, 0, s>>>((const uint64_t*)src, n_src, rs_src, cs_src, src_col, shift, ncols_out, (uint64_t*)out, n_out, rs_out, cs_out, row0, (uint64_t)fill_bits); break;
+        case 1: timeshift_kernel<uint8_t><<<grid, 256, 0, s>>>((const uint8_t*)src, n_src, rs_src, cs_src, src_col, shift, ncols_out, (uint8_t*)out, n_out, rs_out, cs_out, row0, (uint8_t)fill_bits, rows); break;
+        case 2: timeshift_kernel<uint16_t><<<grid, 256, 0, s>>>((const uint16_t*)src, n_src, rs_src, cs_src, src_col, shift, ncols_out, (uint16_t*)out, n_out, rs_out, cs_out, row0, (uint16_t)fill_bits, rows); break;
+        case 4: timeshift_kernel<uint32_t><<<grid, 256, 0, s>>>((const uint32_t*)src, n_src, rs_src, cs_src, src_col, shift, ncols_out, (uint32_t*)out, n_out, rs_out, cs_out, row0, (uint32_t)fill_bits, rows); break;
+        case 8: timeshift_kernel<uint64_t><<<grid, 256, 0, s>>>((const uint64_t*)src, n_src, rs_src, cs_src, src_col, shift, ncols_out, (uint64_t*)out, n_out, rs_out, cs_out, row0, (uint64_t)fill_bits, rows); break;
         default: set_error("sglm_timeshift_expand: elem_size %d not in {1,2,4,8}", elem_size); return SGLM_EINVAL;
     }
     return check_launch("timeshift_kernel");
+}
+
+int sglm_pack_design_rows(const void* src, int32_t src_is_f64, int64_t n, int32_t p, int64_t rs,
+                          int64_t cs, int32_t add_ones, uint16_t* Xb, float* Xf, int64_t ld,
+                          int32_t P, int64_t dst0, int32_t* inexact, sglm_stream_t stream) {
+    if (n <= 0) return SGLM_OK;
+    if (!Xb || !inexact || (p > 0 && !src)) { set_error("sglm_pack_design_rows: null pointer"); return SGLM_EINVAL; }
+    if (ld % 64 || P % 64 || dst0 % 64 || dst0 < 0 || dst0 + n > ld || P < p + (add_ones ? 1 : 0)) {
+        set_error("sglm_pack_design_rows: bad rows dst0=%lld n=%lld ld=%lld", (long long)dst0,
+                  (long long)n, (long long)ld);
+        return SGLM_EINVAL;
+    }
+    dim3 grid((unsigned)((n + 63) / 64), (unsigned)(P / 64));
+    hipStream_t s = as_stream(stream);
+    if (src_is_f64)
+        pack_kernel<double><<<grid, 256, 0, s>>>((const double*)src, n, p, rs, cs, add_ones, Xb, Xf, ld, inexact, dst0);
+    else
+        pack_kernel<float><<<grid, 256, 0, s>>>((const float*)src, n, p, rs, cs, add_ones, Xb, Xf, ld, inexact, dst0);
+    return check_launch("pack_kernel");
 }
 
 int sglm_pack_design(const void* src, int32_t src_is_f64, int64_t n, int32_t p, int64_t rs,

@@ -6,6 +6,7 @@
 // one uint8 mask row per fold: 0/1 for a strictly increasing list (GroupShuffleSplit folds),
 // the multiplicity for a list with repeats (holdout resampling), 1 on every listed row for a
 // row list, all ones for "every row".  One thread per mask (a mask is ~1 MB of stores).
+#include <algorithm>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -129,5 +130,46 @@ extern "C" int sglm_host_masks(int32_t nm, const int64_t* const* idx, const int6
         if (nnz) nnz[f] = j.nnz;
         if (sum) sum[f] = j.sum;
     }
+    return SGLM_OK;
+}
+
+// Threaded host copies for the chunked uploads (engine.Design.from_host, the lagged frames of
+// sglm_pp.timeshift_multiple): a pageable numpy buffer is copied into a pinned staging buffer
+// by `nthreads` threads so that the DMA engine reads page-locked memory at full PCIe rate
+// (torch's pageable .to(device) is one staged, single-threaded copy).
+// sglm_host_copy: dst[0 .. nbytes) = src[0 .. nbytes).
+// sglm_host_gather_cols: dst[c * nrows * elem .. ) = column c (src[c], nrows contiguous
+//   elements of elem bytes) for c < ncols -- the event columns of a DataFrame, column-major.
+extern "C" int sglm_host_copy(void* dst, const void* src, int64_t nbytes, int32_t nthreads) {
+    if (nbytes <= 0) return SGLM_OK;
+    if (!dst || !src) { sglm::set_error("sglm_host_copy: null pointer"); return SGLM_EINVAL; }
+    const int nt = nthreads > 1 ? (int)std::min<int64_t>(nthreads, (nbytes >> 22) + 1) : 1;
+    const int64_t per = (nbytes + nt - 1) / nt;
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t) {
+        const int64_t a = (int64_t)t * per, b = std::min<int64_t>(nbytes, a + per);
+        if (a >= b) break;
+        th.emplace_back([=] {
+            std::memcpy((char*)dst + a, (const char*)src + a, (size_t)(b - a));
+        });
+    }
+    for (auto& x : th) x.join();
+    return SGLM_OK;
+}
+
+extern "C" int sglm_host_gather_cols(const void* const* src, int32_t ncols, int64_t nrows,
+                                     int32_t elem, void* dst, int32_t nthreads) {
+    if (ncols <= 0 || nrows <= 0) return SGLM_OK;
+    if (!src || !dst || elem <= 0) { sglm::set_error("sglm_host_gather_cols: bad args"); return SGLM_EINVAL; }
+    for (int c = 0; c < ncols; ++c)
+        if (!src[c]) { sglm::set_error("sglm_host_gather_cols: null column %d", c); return SGLM_EINVAL; }
+    const int nt = std::max(1, std::min<int>(nthreads, ncols));
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([=] {
+            for (int c = t; c < ncols; c += nt)
+                std::memcpy((char*)dst + (size_t)c * nrows * elem, src[c], (size_t)nrows * elem);
+        });
+    for (auto& x : th) x.join();
     return SGLM_OK;
 }

@@ -156,7 +156,7 @@ class GLM():
     def predict(self, X: Union[np.ndarray, pd.DataFrame]) -> np.ndarray:
         if type(X) == pd.DataFrame:
             X = X.values
-        return self.model.predict(X)
+        return self.model.predict(X)          # a lagged frame (sglm_hip.lagframe) stays resident
 
     def log_likelihood(self, prediction, truth) -> float:
         """backend/sglm.py:349-385 (Gaussian only, as in the reference)."""

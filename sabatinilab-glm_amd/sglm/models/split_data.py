@@ -54,7 +54,9 @@ def holdout_splits(dfrel_setup, id_cols=['nTrial_filenum'], perc_holdout=0.2):
 
 def cv_idx_by_trial_id(X, y=None, trial_id_columns=[], num_folds=5, test_size=None):
     """split_data.py:124-157 (package key scheme)."""
-    X = pd.DataFrame(X)
+    from sglm_hip.lagframe import LagFrame
+    if not isinstance(X, LagFrame):
+        X = pd.DataFrame(X)
     bucket_ids = _folds.trial_keys_codes(X, trial_id_columns, package_style=True)
     return cv_idx_from_bucket_ids(bucket_ids, X, y=y, num_folds=num_folds, test_size=test_size)
 

@@ -49,6 +49,9 @@ class SGLM_worker():
 
 
 def _values(a):
+    from sglm_hip.lagframe import LagFrame
+    if isinstance(a, LagFrame):
+        return a.design()                      # resident lagged frame: its device design
     return a.values if hasattr(a, "values") and not isinstance(a, np.ndarray) else a
 
 

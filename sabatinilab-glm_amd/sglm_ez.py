@@ -16,6 +16,7 @@ import sglm_
 import sglm_cv
 import sglm_pp
 from sglm_hip import folds as _folds
+from sglm_hip.lagframe import LagFrame
 
 
 def timeshift_cols_by_signal_length(X, cols_to_shift, neg_order=0, pos_order=1, trial_id='nTrial',
@@ -51,7 +52,8 @@ def add_timeshifts_by_sl_to_col_list(all_cols, shifted_cols, sft_orders):
 
 
 def timeshift_cols(X, cols_to_shift, neg_order=0, pos_order=1):
-    """backend/sglm_ez.py:102-123 — shifts [0] + neg..-1 + 1..pos in one kernel launch."""
+    """backend/sglm_ez.py:102-123 — shifts [0] + neg..-1 + 1..pos.  A DataFrame comes back as
+    a device-resident lagged frame (sglm_hip.lagframe.LagFrame, see sglm_pp.timeshift_multiple)."""
     col_nums = sglm_pp.get_column_nums(X, cols_to_shift)
     return sglm_pp.timeshift_multiple(X, shift_inx=col_nums,
                                       shift_amt_list=[0] + list(range(neg_order, 0)) +
@@ -69,7 +71,7 @@ def add_timeshifts_to_col_list(all_cols, shifted_cols, neg_order=0, pos_order=1)
 def fit_GLM(X, y, model_name='Gaussian', *args, **kwargs):
     """backend/sglm_ez.py:149-171."""
     glm = sglm_.GLM(model_name, *args, **kwargs)
-    glm.fit(X.values, y.values)
+    glm.fit(X if isinstance(X, LagFrame) else X.values, y.values)
     return glm
 
 
@@ -123,7 +125,8 @@ def holdout_split_by_trial_id(X, y=None, id_cols=['nTrial', 'iBlock'], strat_col
 
 def cv_idx_by_trial_id(X, y=None, trial_id_columns=[], num_folds=5, test_size=None):
     """backend/sglm_ez.py:311-343 — bit-exact with the reference's GroupShuffleSplit."""
-    X = pd.DataFrame(X)
+    if not isinstance(X, LagFrame):
+        X = pd.DataFrame(X)
     bucket_ids = _folds.trial_keys_codes(X, trial_id_columns)
     return sglm_pp.cv_idx_from_bucket_ids(bucket_ids, X, y=y, num_folds=num_folds,
                                           test_size=test_size)
@@ -131,7 +134,8 @@ def cv_idx_by_trial_id(X, y=None, trial_id_columns=[], num_folds=5, test_size=No
 
 def simple_cv_fit(X, y, cv_idx, glm_kwarg_lst, model_type='Normal', verbose=0, score_method='mse'):
     """backend/sglm_ez.py:347-389."""
-    Xv = X.values if hasattr(X, "values") and not isinstance(X, np.ndarray) else X
+    Xv = X if isinstance(X, LagFrame) else (
+        X.values if hasattr(X, "values") and not isinstance(X, np.ndarray) else X)
     yv = y.values if hasattr(y, "values") and not isinstance(y, np.ndarray) else y
     cv_results = sglm_cv.cv_glm_mult_params(Xv, yv, cv_idx, model_type, glm_kwarg_lst,
                                             verbose=verbose, score_method=score_method)
@@ -207,7 +211,8 @@ def holdout_resplit_cv(X, y, id_df, glm_kwarg_lst, num_runs=3, id_cols=('nTrial'
     groups = [{"cv_idx": [(setup[tr], setup[te]) for tr, te in cv_idx],
                "objectives": objectives, "rolls": rolls, "refit_rows": setup,
                "holdout_rows": np.flatnonzero(hold)} for hold, setup, cv_idx in runs]
-    Xv = X.values if hasattr(X, "values") and not isinstance(X, np.ndarray) else X
+    Xv = X.design() if isinstance(X, LagFrame) else (
+        X.values if hasattr(X, "values") and not isinstance(X, np.ndarray) else X)
     yv = np.asarray(y.values if hasattr(y, "values") else y, dtype=np.float64).reshape(-1)
     res = _grid.run_multi(Xv, yv, groups, score_method=score_method)
     out = []

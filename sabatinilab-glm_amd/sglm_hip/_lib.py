@@ -20,8 +20,12 @@ SIGNATURES = {
     "sglm_version": (C.c_int, []),
     "sglm_timeshift_expand": (C.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _i32, _vp, _i64, _i64,
                                         _i64, _i64, _i32, _u64, _vp]),
+    "sglm_timeshift_gather": (C.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _i32, _vp, _i64, _i64,
+                                        _i64, _vp, _i32, _u64, _vp]),
     "sglm_pack_design": (C.c_int, [_vp, _i32, _i64, _i32, _i64, _i64, _i32, _vp, _vp, _i64,
                                    _i32, _vp, _vp]),
+    "sglm_pack_design_rows": (C.c_int, [_vp, _i32, _i64, _i32, _i64, _i64, _i32, _vp, _vp, _i64,
+                                        _i32, _i64, _vp, _vp]),
     "sglm_gemv_eta": (C.c_int, [_vp, _i32, _i64, _i32, _i64, _vp, _i32, _vp, _vp]),
     "sglm_link_update": (C.c_int, [_i32, _f32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
                                    _vp, _vp, _vp, _vp, _vp, _vp]),
@@ -109,6 +113,8 @@ SIGNATURES = {
     "sglm_zero_groups_flag": (C.c_int, [_i64, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp,
                                         _vp]),
     "sglm_host_masks": (C.c_int, [_i32, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _i32]),
+    "sglm_host_copy": (C.c_int, [_vp, _vp, _i64, _i32]),
+    "sglm_host_gather_cols": (C.c_int, [_vp, _i32, _i64, _i32, _vp, _i32]),
     "sglm_scatter_rows": (C.c_int, [_i64, _vp, _i64, _vp, _i32, _vp, _i64, _vp]),
     "sglm_signal_trials_work_bytes": (_sz, [_i64]),
     "sglm_signal_trials": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp,

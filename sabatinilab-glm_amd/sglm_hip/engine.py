@@ -225,9 +225,108 @@ class Design:
         X = np.ascontiguousarray(X)
         n, p = X.shape
         d = cls(n, p, device, zero=False)
-        src = torch.from_numpy(X).to(device)
-        d._pack(src, is_f64=X.dtype == np.float64, rs=p, cs=1)
+        d._pack_chunked(X)
         d.slab = info
+        return d
+
+    def _pack_chunked(self, X: np.ndarray):
+        """Upload a row-major host array in row chunks of <= UPLOAD_CHUNK_BYTES: each chunk is
+        copied by HOST_THREADS threads into one of two pinned staging buffers (sglm_host_copy),
+        moved by an asynchronous copy, and packed into the design's rows (sglm_pack_design_rows)
+        -- no pageable multi-GB .to(device), and the host copy of chunk k + 1 overlaps the DMA
+        and pack of chunk k.  A design that is not bf16-exact is packed again with its f32 copy
+        (the first chunk's check catches it before the rest is uploaded once for nothing)."""
+        n, p = X.shape
+        dev, is64 = self.device, X.dtype == np.float64
+        item = X.itemsize
+        rows = max(64, (UPLOAD_CHUNK_BYTES // max(1, p * item)) // 64 * 64)
+        rows = min(rows, pad_to(max(n, 1), 64))
+        tdt = torch.float64 if is64 else torch.float32
+        hbuf = [_pinned(f"h2d{i}", rows * p, tdt) for i in range(2)]
+        dbuf = [_work(rows * p * item, dev, f"h2d{i}") for i in range(2)]
+        evs = [None, None]
+        flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        n64 = pad_to(n, 64)
+        if n64 < self.ld:
+            self.xb[:, n64:].zero_()
+        st = _stream()
+
+        def run(xf, first_only):
+            for k, r0 in enumerate(range(0, n, rows)):
+                c = min(rows, n - r0)
+                b = k % 2
+                if evs[b] is not None:
+                    evs[b].synchronize()          # the DMA out of this staging buffer is done
+                _lib.call("sglm_host_copy", hbuf[b].data_ptr(), X[r0:r0 + c].ctypes.data,
+                          c * p * item, HOST_THREADS)
+                dst = dbuf[b][: c * p * item]
+                dst.copy_(hbuf[b][: c * p].view(torch.uint8), non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+                evs[b] = ev
+                _lib.call("sglm_pack_design_rows", dst.data_ptr(), int(is64), c, p, p, 1, 1,
+                          _p(self.xb), _p(xf), self.ld, self.P, r0, _p(flag), st)
+                if first_only:
+                    return
+        if n == 0:
+            return
+        run(None, True)
+        if not int(flag.item()):
+            run(None, False)
+        if int(flag.item()):
+            self.xf = torch.empty((self.P, self.ld), dtype=torch.float32, device=dev)
+            if n64 < self.ld:
+                self.xf[:, n64:].zero_()
+            run(self.xf, False)
+        else:
+            self._pack_bits()
+        for ev in evs:
+            if ev is not None:
+                ev.synchronize()                      # the staging buffers are reusable
+
+    @classmethod
+    def from_lagged(cls, Ecm, cols, shifts, r0: int, n: int, rows=None, device="cuda"):
+        """A design whose column j is source column cols[j] lagged by shifts[j]:
+        X[t, j] = Ecm[cols[j], row(t) - shifts[j]] with row(t) = r0 + t (rows None) or rows[t]
+        (a device int64 row list).  Ecm: device float64 [m][N] source columns (NaN-free on
+        every row read).  A contiguous, canonical shift-major (or event-major) 0/1 layout goes
+        through from_events (LagStructure: event-correlation Gram and gradient); anything else
+        is expanded / gathered column by column (sglm_timeshift_expand / _gather)."""
+        require_gpu()
+        cols = np.asarray(cols, dtype=np.int64)
+        shifts = np.asarray(shifts, dtype=np.int64)
+        m = int(Ecm.shape[0])
+        if rows is None:
+            for major in (False, True):
+                lay = _canonical_lags(cols, shifts, m, major)
+                if lay is not None:
+                    ev, sl = lay
+                    E = Ecm[torch.from_numpy(ev).to(Ecm.device)].t()
+                    return cls.from_events(E, sl, r0, n, device=device, event_major=major)
+        p = int(cols.size)
+        d = cls(n, p, device, zero=True)
+        c_d = torch.from_numpy(cols.astype(np.int32)).to(device)
+        s_d = torch.from_numpy(shifts.astype(np.int32)).to(device)
+        N = int(Ecm.shape[1])
+        Eb = Ecm.to(torch.bfloat16).contiguous()
+        exact = bool(torch.equal(Eb.double(), Ecm))
+
+        def expand(src, out, elem):
+            if rows is None:
+                _lib.call("sglm_timeshift_expand", _p(src), N, 1, N, _p(c_d), _p(s_d), p,
+                          _p(out), n, 1, d.ld, int(r0), elem, 0, _stream())
+            else:
+                _lib.call("sglm_timeshift_gather", _p(src), N, 1, N, _p(c_d), _p(s_d), p,
+                          _p(out), n, 1, d.ld, _p(rows), elem, 0, _stream())
+        expand(Eb, d.xb, 2)
+        d.xb[p, :n] = 1.0
+        if exact:
+            d._pack_bits()
+        else:
+            Ef = Ecm.to(torch.float32).contiguous()
+            d.xf = torch.zeros((d.P, d.ld), dtype=torch.float32, device=device)
+            expand(Ef, d.xf, 4)
+            d.xf[p, :n] = 1.0
         return d
 
     @classmethod
@@ -364,6 +463,31 @@ class Design:
         return out
 
 
+def _canonical_lags(cols, shifts, m, event_major):
+    """(events, shift list) when the (column, shift) pairs are every event x every shift in
+    the shift-major (col = b * m' + a) or event-major (col = a * K + b) order, else None."""
+    p = cols.size
+    if p == 0:
+        return None
+    if event_major:
+        ev = cols[np.r_[0, np.flatnonzero(np.diff(cols) != 0) + 1]]
+        K = p // max(1, ev.size)
+        if ev.size * K != p:
+            return None
+        sl = shifts[:K]
+        ok = (np.array_equal(cols, np.repeat(ev, K)) and np.array_equal(shifts, np.tile(sl, ev.size)))
+    else:
+        K = int(np.sum(cols == cols[0]))
+        mm = p // max(1, K)
+        if mm * K != p:
+            return None
+        ev, sl = cols[:mm], shifts[::mm]
+        ok = (np.array_equal(cols, np.tile(ev, K)) and np.array_equal(shifts, np.repeat(sl, mm)))
+    if not ok or len(set(ev.tolist())) != ev.size or len(set(sl.tolist())) != sl.size:
+        return None
+    return ev, [int(x) for x in sl]
+
+
 class LagStructure:
     """A time-shifted 0/1 event design by its events (sglm_lag_xtr): X[t, col(b, a)] =
     E[t + row0 - shifts[b], a].  occ = every event's occurrence rows of E, event-major and
@@ -415,8 +539,10 @@ class LagStructure:
 
 
 # ------------------------------------------------------------------------------ problem
-# threads of the native host-side setup helpers (sglm_host_masks)
+# threads of the native host-side setup helpers (sglm_host_masks, sglm_host_copy)
 HOST_THREADS = int(os.environ.get("SGLM_HOST_THREADS", "8"))
+# row-chunk size of the pinned host->device design upload (Design.from_host)
+UPLOAD_CHUNK_BYTES = int(os.environ.get("SGLM_UPLOAD_CHUNK_BYTES", str(256 << 20)))
 
 
 def _np_ptr(a: np.ndarray) -> int:

@@ -56,6 +56,11 @@ def _check_y_range(power: float, y: np.ndarray):
 
 
 def _as2d(X):
+    from .lagframe import LagFrame
+    if isinstance(X, LagFrame):             # device-resident lagged frame: no host values
+        if len(X.shape) != 2:
+            raise ValueError("Expected 2D array")
+        return X
     if hasattr(X, "values") and not isinstance(X, np.ndarray):
         X = X.values
     X = np.asarray(X)
@@ -154,6 +159,9 @@ class _EngineRegressor:
         res = self._resident
         if res is not None and id(X) in res and res[id(X)][0] is X:
             return res[id(X)][1]
+        from .lagframe import LagFrame
+        if isinstance(X, LagFrame):
+            return X.design()
         return _cached_design(_as2d(X))
 
     def fit(self, X, y, sample_weight=None):

@@ -1,0 +1,585 @@
+"""Lagged DataFrames whose lag columns stay on the device (the production flow, resident).
+
+The reference's production driver (er_refactored_from_scratch_cleanup.py:421-452) runs
+
+    dfrel, X_cols_sftd = timeshift_vals(dfrel, X_cols, neg, pos)     # sglm_ez.timeshift_cols
+    dfrel = dfrel[(dfrel[cols + X_cols_sftd + [y]].isna().sum(axis=1) == 0) & ...]
+    dfrel_setup, dfrel_holdout = holdout_splits(dfrel, ...)          # .loc[bool mask]
+    kfold_cv_idx = sglm_ez.cv_idx_by_trial_id(dfrel_setup, ['nTrial'], ...)
+    X_setup, y_setup = dfrel_setup[X_cols_sftd], dfrel_setup[y_col]
+    sglm_ez.simple_cv_fit(X_setup, y_setup, kfold_cv_idx, ...)        # X.values -> sklearn
+
+where ``timeshift_multiple`` (backend/sglm_pp.py:58-103) materialises N x (m K) float64 values
+(16 GB at 1M x 2000) only for the NaN filter to read them and the fit to copy them again.
+
+``LagFrame`` is that frame without the materialisation: the source columns live on the device
+(float64, column-major), every lag column is the spec (source column, shift), and row
+selections are position lists.  The operations of the flow above are answered from the specs:
+column / row selections are bookkeeping, ``isna().sum(axis=1)`` counts the out-of-range and
+NaN source cells of each row on the device, id columns are host Series, and ``simple_cv_fit`` /
+``GLM.fit`` / ``predict`` build their design straight from the device sources
+(``engine.Design.from_lagged``: the event-correlation Gram and gradient when the rows are
+contiguous and the columns are the canonical lag layout).  Anything else -- ``.values``,
+printing, arithmetic, any other pandas method -- materialises exactly the values the reference
+would have held (``to_pandas()``), so the frame behaves as the reference's DataFrame.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+import pandas as pd
+
+from . import _lib
+
+NAN = float("nan")
+
+
+class LagSource:
+    """The frame a lagged frame was made from (host, never modified) and the device float64
+    copies of the columns the lag columns read (uploaded once, on first use)."""
+
+    def __init__(self, base: pd.DataFrame):
+        self.base = base
+        self.N = len(base)
+        self._dev = {}           # column name -> row of self._E
+        self._E = None
+        self._hasnan = {}        # column name -> holds a NaN cell
+        self.cast = {}           # base column name -> dtype of its shift-0 copy in the frame
+
+    def device(self, names):
+        """Device float64 [rows][N] holding the named base columns (uploaded once, NaN kept),
+        and the device int64 row index of each name."""
+        import ctypes
+        import torch
+        from .engine import HOST_THREADS, _pinned, require_gpu
+        require_gpu()
+        need = [c for c in dict.fromkeys(names) if c not in self._dev]
+        if need:
+            N, m = self.N, len(need)
+            new = torch.empty((m, N), dtype=torch.float64, device="cuda")
+            # column groups of <= 64 MB through two pinned stages: the threaded host gather of
+            # group g + 1 overlaps the DMA of group g
+            per = max(1, (64 << 20) // max(1, 8 * N))
+            stages = [_pinned(f"lagsrc{i}", max(1, per * N), torch.float64) for i in range(2)]
+            evs = [None, None]
+            for g, c0 in enumerate(range(0, m, per)):
+                grp = need[c0:c0 + per]
+                b = g % 2
+                if evs[b] is not None:
+                    evs[b].synchronize()
+                arrs = [np.ascontiguousarray(self.base[c].to_numpy(dtype=np.float64,
+                                                                   na_value=NAN))
+                        for c in grp]
+                ptrs = (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+                _lib.call("sglm_host_gather_cols", ctypes.cast(ptrs, ctypes.c_void_p),
+                          len(arrs), N, 8, stages[b].data_ptr(), HOST_THREADS)
+                new[c0:c0 + len(grp)].view(-1).copy_(stages[b][: len(grp) * N],
+                                                     non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+                evs[b] = ev
+            for ev in evs:
+                if ev is not None:
+                    ev.synchronize()
+            base = 0 if self._E is None else self._E.shape[0]
+            self._E = new if self._E is None else torch.cat([self._E, new])
+            has = torch.isnan(new).any(1).cpu().numpy()
+            for i, c in enumerate(need):
+                self._dev[c] = base + i
+                self._hasnan[c] = bool(has[i])
+        idx = torch.tensor([self._dev[c] for c in names], dtype=torch.int64, device="cuda")
+        return self._E, idx
+
+    def has_nan(self, name) -> bool:
+        """Whether an uploaded column holds a NaN cell."""
+        return self._hasnan[name]
+
+
+class LagFrame:
+    """A DataFrame-like view: columns ``cols`` (names), each either a base column of
+    ``src.base`` (``spec[c] = (name, 0, False)``), a lag column (``spec[c] = (source name,
+    shift, True)``: value at frame row r = base[name] at row r - shift, NaN outside), or a column
+    assigned to this frame (``overlay``); rows = positions into the base (None = all)."""
+
+    def __init__(self, src: LagSource, cols, spec, rows: Optional[np.ndarray] = None,
+                 index: Optional[pd.Index] = None, overlay: Optional[dict] = None):
+        self._src = src
+        self._cols = list(cols)
+        self._spec = spec
+        self._rows = rows
+        self._index = index
+        self._overlay = overlay if overlay is not None else {}
+        self._design = None
+
+    # ------------------------------------------------------------------ construction
+    @classmethod
+    def from_shifts(cls, X: pd.DataFrame, shift_inx, shift_amt_list, unshifted_keep_all=True):
+        """The frame ``sglm_pp.timeshift_multiple(X, shift_inx, shift_amt_list)`` returns
+        (backend/sglm_pp.py:58-103, 436-486): per shift s in order, s == 0 -> every column
+        (``unshifted_keep_all``) or the shifted ones, else the shifted columns renamed
+        ``f"{col}_{s}"``.  None when the names would not be unique (materialise instead)."""
+        inx = list(range(X.shape[1])) if len(shift_inx) == 0 else list(shift_inx)
+        names = [X.columns[i] for i in inx]
+        cols, spec = [], {}
+        for s in shift_amt_list:
+            if s == 0:
+                keep = list(X.columns) if unshifted_keep_all else names
+                for c in keep:
+                    cols.append(c)
+                    spec[c] = (c, 0, False)
+            else:
+                for c in names:
+                    nm = f"{c}_{s}"
+                    cols.append(nm)
+                    spec[nm] = (c, int(s), True)
+        if len(set(cols)) != len(cols) or not X.columns.is_unique:
+            return None
+        src = LagSource(X)
+        if 0 in list(shift_amt_list):
+            # the shift-0 block writes np.asarray(X)[:, inx] back into the selected columns
+            # (sglm_pp.shifted_cols_to_pandas): they take the frame's common value dtype
+            common = np.asarray(X.iloc[:0]).dtype
+            for c in names:
+                if X[c].dtype != common:
+                    src.cast[c] = common
+        return cls(src, cols, spec)
+
+    # ------------------------------------------------------------------ shape / labels
+    @property
+    def columns(self):
+        return pd.Index(self._cols)
+
+    @property
+    def index(self):
+        if self._index is None:
+            b = self._src.base.index
+            self._index = b if self._rows is None else b[self._rows]
+        return self._index
+
+    @property
+    def shape(self):
+        return (self._nrows(), len(self._cols))
+
+    def _nrows(self):
+        return self._src.N if self._rows is None else int(self._rows.size)
+
+    def __len__(self):
+        return self._nrows()
+
+    @property
+    def ndim(self):
+        return 2
+
+    @property
+    def size(self):
+        return self._nrows() * len(self._cols)
+
+    @property
+    def empty(self):
+        return self.size == 0
+
+    @property
+    def dtypes(self):
+        b = self._src.base
+        return pd.Series([self._overlay[c].dtype if c in self._overlay else
+                          (np.dtype(np.float64) if self._spec[c][2] else
+                           self._src.cast.get(c, b[self._spec[c][0]].dtype))
+                          for c in self._cols], index=self.columns, dtype=object)
+
+    def keys(self):
+        return self.columns
+
+    def __iter__(self):
+        return iter(self._cols)
+
+    def __contains__(self, c):
+        return c in self._spec or c in self._overlay
+
+    def positions(self):
+        """Row positions into the base frame (int64)."""
+        return np.arange(self._src.N, dtype=np.int64) if self._rows is None else self._rows
+
+    # ------------------------------------------------------------------ derived frames
+    def _derive(self, cols=None, rows=None, index=None, keep_rows=True):
+        ov = self._overlay
+        if rows is not None:
+            ov = {k: v[rows] for k, v in ov.items()}
+            base_rows = self.positions()[rows]
+        else:
+            base_rows = self._rows
+        cols = self._cols if cols is None else list(cols)
+        ov = {k: v for k, v in ov.items() if k in cols}
+        return LagFrame(self._src, cols, self._spec, base_rows,
+                        index if index is not None else (self._index if rows is None else None),
+                        dict(ov))
+
+    def _take(self, pos):
+        return self._derive(rows=np.asarray(pos, dtype=np.int64))
+
+    def _bool_rows(self, mask):
+        if isinstance(mask, pd.Series):
+            if not mask.index.equals(self.index):
+                mask = mask.reindex(self.index)
+            mask = mask.to_numpy(dtype=bool, na_value=False)
+        mask = np.asarray(mask, dtype=bool).reshape(-1)
+        if mask.size != self._nrows():
+            raise ValueError(f"Item wrong length {mask.size} instead of {self._nrows()}.")
+        return self._take(np.flatnonzero(mask))
+
+    def _check_cols(self, cols):
+        missing = [c for c in cols if c not in self._spec and c not in self._overlay]
+        if missing:
+            raise KeyError(f"{missing} not in index")
+
+    def __getitem__(self, key):
+        if isinstance(key, str) or (np.isscalar(key) and not isinstance(key, (bool, np.bool_))):
+            return self._series(key)
+        if isinstance(key, slice):
+            return self._take(np.arange(self._nrows())[key])
+        if isinstance(key, LagFrame):
+            raise TypeError("boolean frames as keys are not supported on a lagged frame")
+        arr = key if isinstance(key, (pd.Series, pd.Index, np.ndarray)) else np.asarray(key)
+        if getattr(arr, "dtype", None) is not None and arr.dtype == bool:
+            return self._bool_rows(key)
+        cols = list(key)
+        self._check_cols(cols)
+        if all(c not in self._overlay and not self._spec[c][2] for c in cols):
+            return self._base_frame(cols)               # id / response columns: a real frame
+        return self._derive(cols=cols)
+
+    def __setitem__(self, name, value):
+        n = self._nrows()
+        if isinstance(value, pd.Series):
+            value = value.reindex(self.index).to_numpy()
+        elif np.isscalar(value):
+            value = np.full(n, value)
+        value = np.asarray(value)
+        if value.shape[0] != n:
+            raise ValueError(f"Length of values ({value.shape[0]}) does not match length of "
+                             f"index ({n})")
+        self._overlay[name] = value
+        if name not in self._cols:
+            self._cols.append(name)
+        self._design = None
+
+    @property
+    def loc(self):
+        return _Loc(self)
+
+    @property
+    def iloc(self):
+        return _ILoc(self)
+
+    def copy(self, deep=True):
+        return LagFrame(self._src, self._cols, self._spec, self._rows, self._index,
+                        {k: v.copy() for k, v in self._overlay.items()})
+
+    def reset_index(self, drop=False, **kw):
+        if drop and not kw:
+            return LagFrame(self._src, self._cols, self._spec, self._rows,
+                            pd.RangeIndex(self._nrows()), dict(self._overlay))
+        return getattr(self.to_pandas(), "reset_index")(drop=drop, **kw)
+
+    def drop(self, labels=None, axis=0, columns=None, **kw):
+        if columns is None and axis in (1, "columns"):
+            columns, labels = labels, None
+        if columns is not None and labels is None and not kw:
+            drop = [columns] if isinstance(columns, str) else list(columns)
+            self._check_cols(drop)
+            return self._derive(cols=[c for c in self._cols if c not in set(drop)])
+        return self.to_pandas().drop(labels=labels, axis=axis, columns=columns, **kw)
+
+    # ------------------------------------------------------------------ missing values
+    def isna(self):
+        return _LagNA(self)
+
+    isnull = isna
+
+    def notna(self):
+        return _LagNA(self, negate=True)
+
+    notnull = notna
+
+    def dropna(self, axis=0, how="any", subset=None, inplace=False, **kw):
+        if axis not in (0, "index") or inplace or kw:
+            return self.to_pandas().dropna(axis=axis, how=how, subset=subset, inplace=inplace,
+                                           **kw)
+        cols = self._cols if subset is None else list(subset)
+        cnt = self.nan_counts(cols)
+        keep = cnt == 0 if how == "any" else cnt < len(cols)
+        return self._take(np.flatnonzero(keep))
+
+    def nan_counts(self, cols=None) -> np.ndarray:
+        """Per row of this frame, the number of NaN cells among ``cols`` (default: all): lag
+        columns from the device (a lag cell is NaN when its source row is outside the base or
+        the source cell is NaN), base and assigned columns on the host."""
+        import torch
+        cols = self._cols if cols is None else list(cols)
+        self._check_cols(cols)
+        n = self._nrows()
+        cnt = np.zeros(n, dtype=np.int64)
+        lag = {}
+        for c in cols:
+            if c in self._overlay:
+                cnt += pd.isna(self._overlay[c]).astype(np.int64)
+            elif self._spec[c][2]:
+                nm, s, _ = self._spec[c]
+                lag.setdefault(s, []).append(nm)
+            else:
+                cnt += self._src.base[self._spec[c][0]].isna().to_numpy()[self.positions()] \
+                    .astype(np.int64)
+        if lag:
+            cnt += self._lag_nan_counts(lag)
+        return cnt
+
+    def _lag_nan_counts(self, lag) -> np.ndarray:
+        """NaN lag cells per row; ``lag``: shift -> source names (one per lag column).  A
+        cell is NaN when its source row u - s is outside the base (counted on the host from
+        the edge rows only) or its source cell is NaN (device, for sources that hold any)."""
+        import torch
+        N = self._src.N
+        pos = self.positions()
+        n = pos.size
+        out = np.zeros(n, dtype=np.int64)
+        sh = np.array(sorted(lag), dtype=np.int64)
+        w = np.array([len(lag[s]) for s in sh], dtype=np.int64)
+        smin, smax = int(sh[0]), int(sh[-1])
+        edge = np.flatnonzero((pos < max(smax, 0)) | (pos >= N + min(smin, 0)))
+        if edge.size:
+            u = pos[edge]
+            cw = np.r_[0, np.cumsum(w)]
+            # shifts s > u (source row u - s < 0) plus shifts s <= u - N (u - s >= N)
+            gt = cw[-1] - cw[np.searchsorted(sh, u, side="right")]
+            le = cw[np.searchsorted(sh, u - N, side="right")]
+            out[edge] = gt + le
+        names = sorted({nm for v in lag.values() for nm in v}, key=str)
+        self._src.device(names)
+        if not any(self._src.has_nan(nm) for nm in names):
+            return out
+        E, idx = self._src.device(names)
+        row_of = {nm: int(r) for nm, r in zip(names, idx.tolist())}
+        pos_d = torch.from_numpy(pos).to("cuda")
+        acc = torch.zeros(n, dtype=torch.int64, device="cuda")
+        for s, nms in lag.items():
+            nn = [x for x in nms if self._src.has_nan(x)]
+            if not nn:
+                continue
+            rws = torch.tensor([row_of[x] for x in nn], dtype=torch.int64, device="cuda")
+            per_row = torch.isnan(E[rws]).sum(0)                 # NaN sources per base row
+            u = pos_d - int(s)
+            inside = (u >= 0) & (u < N)
+            acc += torch.where(inside, per_row[u.clamp(0, N - 1)], torch.zeros_like(u))
+        return out + acc.cpu().numpy()
+
+    # ------------------------------------------------------------------ values
+    def _series(self, name) -> pd.Series:
+        if name in self._overlay:
+            return pd.Series(self._overlay[name], index=self.index, name=name)
+        if name not in self._spec:
+            raise KeyError(name)
+        src, s, lag = self._spec[name]
+        if not lag:
+            return pd.Series(self._base_values(src), index=self.index, name=name)
+        return pd.Series(self._lag_values([name])[:, 0], index=self.index, name=name)
+
+    def _base_values(self, name) -> np.ndarray:
+        v = self._src.base[name].to_numpy()
+        if self._rows is not None:
+            v = v[self._rows]
+        elif v.base is not None or not v.flags.owndata:
+            v = v.copy()
+        cast = self._src.cast.get(name)
+        return v if cast is None else v.astype(cast)
+
+    def _base_frame(self, cols):
+        return pd.DataFrame({c: self._base_values(self._spec[c][0]) for c in cols},
+                            index=self.index, columns=cols)
+
+    def _lag_values(self, names, rows=None) -> np.ndarray:
+        """float64 host [n][len(names)] of lag columns, expanded on the device."""
+        import torch
+        from .timeshift import fill_bits
+        srcs = [self._spec[c][0] for c in names]
+        E, idx = self._src.device(sorted(set(srcs), key=str))
+        rowmap = {nm: int(r) for nm, r in zip(sorted(set(srcs), key=str), idx.tolist())}
+        cols_d = torch.tensor([rowmap[x] for x in srcs], dtype=torch.int32, device="cuda")
+        sh_d = torch.tensor([self._spec[c][1] for c in names], dtype=torch.int32, device="cuda")
+        pos = self.positions() if rows is None else self.positions()[rows]
+        pos_d = torch.from_numpy(np.ascontiguousarray(pos, dtype=np.int64)).to("cuda")
+        k, n, N = len(names), int(pos.size), self._src.N
+        out = torch.empty((n, k), dtype=torch.float64, device="cuda")
+        _lib.call("sglm_timeshift_gather", E.data_ptr(), N, 1, N, cols_d.data_ptr(),
+                  sh_d.data_ptr(), k, out.data_ptr(), n, k, 1, pos_d.data_ptr(), 8,
+                  fill_bits(NAN, np.float64), torch.cuda.current_stream().cuda_stream)
+        return out.cpu().numpy()
+
+    def to_pandas(self) -> pd.DataFrame:
+        """The DataFrame the reference would hold (every value materialised on the host)."""
+        b = self._src.base
+        pos = self.positions()
+        lag = [c for c in self._cols if c not in self._overlay and self._spec[c][2]]
+        lv = self._lag_values(lag) if lag else None
+        li = {c: i for i, c in enumerate(lag)}
+        data = {}
+        for c in self._cols:
+            if c in self._overlay:
+                data[c] = self._overlay[c]
+            elif c in li:
+                data[c] = lv[:, li[c]]
+            else:
+                data[c] = self._base_values(self._spec[c][0])
+        return pd.DataFrame(data, index=self.index, columns=self._cols)
+
+    def to_numpy(self, dtype=None, copy=False, na_value=None):
+        a = self.to_pandas().to_numpy(dtype=dtype)
+        return a
+
+    @property
+    def values(self):
+        return self.to_numpy()
+
+    def __array__(self, dtype=None, copy=None):
+        a = self.to_numpy()
+        return a if dtype is None else a.astype(dtype)
+
+    def head(self, n=5):
+        return self._take(np.arange(min(n, self._nrows()))).to_pandas()
+
+    def tail(self, n=5):
+        k = self._nrows()
+        return self._take(np.arange(max(0, k - n), k)).to_pandas()
+
+    def __repr__(self):
+        k, m = self.shape
+        if k <= 10:
+            return repr(self.to_pandas())
+        ht = self._take(np.r_[np.arange(5), np.arange(k - 5, k)]).to_pandas()
+        with pd.option_context("display.max_rows", 9, "display.min_rows", 9,
+                               "display.show_dimensions", False):
+            body = repr(ht)
+        return f"{body}\n\n[{k} rows x {m} columns]"
+
+    def __getattr__(self, name):
+        if name.startswith("_"):
+            raise AttributeError(name)
+        if name in self._spec or name in self._overlay:
+            return self._series(name)
+        return getattr(self.to_pandas(), name)
+
+    # ------------------------------------------------------------------ device design
+    def design(self):
+        """engine.Design of this frame's values (every column numeric, no NaN cell), built from
+        the device sources: lag and base columns alike are (source, shift) pairs."""
+        if self._design is not None:
+            return self._design
+        from .engine import Design
+        if self._overlay:
+            self._design = Design.from_host(self.to_numpy(dtype=np.float64))
+            return self._design
+        bad = self.nan_counts()
+        if bad.any():
+            raise ValueError("Input X contains NaN.")
+        srcs = [self._spec[c][0] for c in self._cols]
+        names = sorted(set(srcs), key=str)
+        E, idx = self._src.device(names)
+        Esub = E[idx]
+        if any(self._src.has_nan(nm) for nm in names):
+            Esub = Esub.nan_to_num(0.0)        # NaN source cells are never read (checked above)
+        at = {nm: i for i, nm in enumerate(names)}
+        cols = np.array([at[x] for x in srcs], dtype=np.int64)
+        shifts = np.array([self._spec[c][1] for c in self._cols], dtype=np.int64)
+        pos = self.positions()
+        n = int(pos.size)
+        if n and pos[-1] - pos[0] == n - 1 and np.all(np.diff(pos) == 1):
+            d = Design.from_lagged(Esub, cols, shifts, int(pos[0]), n)
+        else:
+            import torch
+            rows_d = torch.from_numpy(np.ascontiguousarray(pos, dtype=np.int64)).to("cuda")
+            d = Design.from_lagged(Esub, cols, shifts, 0, n, rows=rows_d)
+        self._design = d
+        return d
+
+
+class _LagNA:
+    """``frame.isna()`` (``negate``: ``notna()``) answered from the NaN counts per row."""
+
+    def __init__(self, frame: LagFrame, negate: bool = False):
+        self.frame = frame
+        self.negate = negate
+
+    def sum(self, axis=0, **kw):
+        if axis in (1, "columns") and not kw:
+            c = self.frame.nan_counts()
+            if self.negate:
+                c = len(self.frame._cols) - c
+            return pd.Series(c, index=self.frame.index)
+        return getattr(self._real(), "sum")(axis=axis, **kw)
+
+    def any(self, axis=0, **kw):
+        if axis in (1, "columns") and not kw:
+            c = self.frame.nan_counts()
+            full = len(self.frame._cols)
+            return pd.Series((c < full) if self.negate else (c > 0), index=self.frame.index)
+        return getattr(self._real(), "any")(axis=axis, **kw)
+
+    def all(self, axis=0, **kw):
+        if axis in (1, "columns") and not kw:
+            c = self.frame.nan_counts()
+            full = len(self.frame._cols)
+            return pd.Series((c == 0) if self.negate else (c == full), index=self.frame.index)
+        return getattr(self._real(), "all")(axis=axis, **kw)
+
+    def _real(self):
+        df = self.frame.to_pandas()
+        return df.notna() if self.negate else df.isna()
+
+    def __getattr__(self, name):
+        return getattr(self._real(), name)
+
+    def __repr__(self):
+        return repr(self._real())
+
+
+class _Loc:
+    def __init__(self, frame):
+        self.f = frame
+
+    def __getitem__(self, key):
+        f = self.f
+        if isinstance(key, tuple):
+            rk, ck = key
+            out = self[rk] if not (isinstance(rk, slice) and rk == slice(None)) else f
+            if isinstance(out, LagFrame):
+                return out[ck]
+            return out.loc[:, ck]
+        arr = key if isinstance(key, (pd.Series, np.ndarray, pd.Index)) else None
+        if arr is not None and arr.dtype == bool:
+            return f._bool_rows(key)
+        if isinstance(key, slice):
+            sl = f.index.slice_indexer(key.start, key.stop, key.step)
+            return f._take(np.arange(len(f))[sl])
+        labels = [key] if np.isscalar(key) else list(key)
+        pos = f.index.get_indexer(labels)
+        if (pos < 0).any():
+            raise KeyError(f"{[l for l, q in zip(labels, pos) if q < 0]} not in index")
+        out = f._take(pos)
+        return out.to_pandas().iloc[0] if np.isscalar(key) else out
+
+
+class _ILoc:
+    def __init__(self, frame):
+        self.f = frame
+
+    def __getitem__(self, key):
+        f = self.f
+        if isinstance(key, tuple):
+            rk, ck = key
+            out = self[rk] if not (isinstance(rk, slice) and rk == slice(None)) else f
+            cols = np.asarray(f._cols, dtype=object)[ck]
+            if isinstance(out, LagFrame):
+                return out[list(np.atleast_1d(cols))] if not np.isscalar(cols) else out[cols]
+            return out.iloc[:, ck]
+        if np.isscalar(key):
+            return f._take(np.array([int(key)])).to_pandas().iloc[0]
+        return f._take(np.arange(len(f))[key])

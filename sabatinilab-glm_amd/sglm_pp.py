@@ -20,7 +20,12 @@ import pandas as pd
 import scipy.signal  # noqa: F401  (reference imports it; kept for API parity)
 
 from sglm_hip import folds as _folds
+from sglm_hip.lagframe import LagFrame
 from sglm_hip.timeshift import shift_columns as _shift_columns
+
+# timeshift_multiple on a DataFrame returns a device-resident LagFrame (SGLM_LAGFRAME=0: the
+# materialised DataFrame)
+LAGFRAME = __import__("os").environ.get("SGLM_LAGFRAME", "1") == "1"
 
 
 # ----------------------------------------------------------------------------- helpers
@@ -103,7 +108,24 @@ def timeshift(X, shift_inx=[], shift_amt=1, keep_non_inx=False, dct=None, fill_v
 
 def timeshift_multiple(X, shift_inx=[], shift_amt_list=[-1, 0, 1], unshifted_keep_all=True,
                        fill_value=np.nan):
-    """backend/sglm_pp.py:58-103: all shifts in one kernel launch, shift-major blocks."""
+    """backend/sglm_pp.py:58-103: all shifts in one kernel launch, shift-major blocks.
+
+    A DataFrame input with the reference's NaN fill returns a ``LagFrame``
+    (sglm_hip.lagframe): the same columns, index and values, with the lag columns kept as
+    (source column, shift) specs over a device copy of the shifted columns instead of a
+    materialised N x (m K) float64 block -- the NaN filter, the trial-id folds and the fits of
+    the production flow read them there; any other use materialises them (``to_pandas()``).
+    SGLM_LAGFRAME=0 returns the materialised DataFrame."""
+    if isinstance(X, LagFrame):
+        X = X.to_pandas()
+    if (type(X) == pd.DataFrame and LAGFRAME and isinstance(fill_value, float)
+            and np.isnan(fill_value)
+            and len(shift_amt_list) > 0):
+        inx = list(range(X.shape[1])) if len(shift_inx) == 0 else list(shift_inx)
+        if all(pd.api.types.is_numeric_dtype(X.dtypes.iloc[i]) for i in inx):
+            lf = LagFrame.from_shifts(X, shift_inx, shift_amt_list, unshifted_keep_all)
+            if lf is not None:
+                return lf
     npX = np.asarray(get_numpy_version(X))
     inx = list(range(npX.shape[1])) if len(shift_inx) == 0 else list(shift_inx)
     nz = [s for s in shift_amt_list if s != 0]

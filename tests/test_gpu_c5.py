@@ -10,7 +10,7 @@ The reference runs one simple_cv_fit per response (er_refactored_from_scratch_cl
   |c_j - a(1-rho) w_j - a rho sign(w_j)| (w_j != 0) and max(|c_j| - a rho, 0) (w_j = 0), relative
   to a rho, <= 1e-6; mean residual <= 1e-7 (intercept).  The residuals of all 64 responses of
   one (mask, alpha) are one float64 GEMM pair on the device against the dense float64 design.
-* Two mid-path fits (split 0 and the refit at alphas 6 and 10) equal the oracle's cyclic CD
+* Two mid-path fits (split 0 and the refit at alphas 4 and 7 of the 9 with a non-empty support) equal the oracle's cyclic CD
   (oracle/glm_ref.fit_enet_cd_gram on the float64 centred Gram of the same rows) at 1e-5.
 """
 import time
@@ -111,7 +111,7 @@ def test_c5_full_size_every_fit_kkt(c5_full):
 
 
 def test_c5_full_size_mid_path_vs_oracle(c5_full):
-    """Split 0 and the refit at alphas[6] and alphas[10], responses 0 and 63, against the
+    """Split 0 and the refit at alphas[4] and alphas[7], responses 0 and 63, against the
     oracle's cyclic CD on the float64 centred Gram of the same rows."""
     import torch
     s, Y, cv_idx, alphas, out, st, Xd = c5_full
@@ -127,7 +127,7 @@ def test_c5_full_size_mid_path_vs_oracle(c5_full):
             yr = torch.from_numpy(Y[rows, r] if rows is not None else Y[:, r]).cuda()
             ym = float(yr.mean())
             c = (Xc.t() @ (yr - ym)).cpu().numpy()
-            for j in (6, 10):
+            for j in (4, 7):
                 w = glm_ref.fit_enet_cd_gram(G, c, nr, float(alphas[j]), 0.5)
                 b = ym - float(Xm.cpu().numpy() @ w)
                 res = out[r][j]
