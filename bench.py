@@ -839,6 +839,9 @@ def main():
                             f"{K} splits x {nlam} lambdas + refits",
                 "config_name": a.config,
                 "irls_fit_iters_per_s": fit_iters / elapsed,
+                "irls_fit_iters_counted": "fit-iterations incl. aliased / kept-factor ones "
+                                          "(those forming their own Gram: "
+                                          "gram_forming_fit_iters_per_s)",
                 "gram_forming_fit_iters_per_s": gram_iters / elapsed,
                 "fit_iters_per_grid": fit_iters / a.steps,
                 "gram_forming_fit_iters_per_grid": gram_iters / a.steps,

@@ -588,10 +588,15 @@ int sglm_host_masks(int32_t nm, const int64_t* const* idx, const int64_t* len,
 
 /* Threaded host copies into pinned staging buffers (chunked uploads): sglm_host_copy copies
  * nbytes; sglm_host_gather_cols copies ncols columns of nrows elements of elem bytes (host
- * pointers src[c]) to dst column-major.  Host only, no device pointers. */
+ * pointers src[c], element strides stride[c], NULL = contiguous) to dst column-major.  Host only, no device pointers. */
 int sglm_host_copy(void* dst, const void* src, int64_t nbytes, int32_t nthreads);
-int sglm_host_gather_cols(const void* const* src, int32_t ncols, int64_t nrows, int32_t elem,
-                          void* dst, int32_t nthreads);
+int sglm_host_gather_cols(const void* const* src, const int64_t* stride, int32_t ncols,
+                          int64_t nrows, int32_t elem, void* dst, int32_t nthreads);
+/* sglm_host_pack_bits_cols: float64 columns (src[c], element stride stride[c]) as bit-planes,
+ * bit r of bits[c * ceil(nrows / 32) + r / 32] = (value == 1.0); binary[c] = 1 when every
+ * value is 0.0 or 1.0.  The 0/1 event columns of a lagged frame cross PCIe as bits. */
+int sglm_host_pack_bits_cols(const void* const* src, const int64_t* stride, int32_t ncols,
+                             int64_t nrows, uint32_t* bits, uint8_t* binary, int32_t nthreads);
 
 #ifdef __cplusplus
 }

@@ -21,6 +21,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <vector>
 
 #include "common.h"
 
@@ -1220,6 +1221,7 @@ struct ChainEntry {
 };
 std::mutex g_chain_mu;
 std::map<ChainKey, ChainEntry> g_chain_cache;
+std::vector<ChainEntry> g_chain_pending;   // evicted, destroyed once their last replay is done
 uint64_t g_chain_tick = 0;
 
 int chain_cache_cap() {
@@ -1241,15 +1243,36 @@ void chain_entry_destroy(ChainEntry& e) {
     e.done = nullptr;
 }
 
-// call with g_chain_mu held
+// call with g_chain_mu held: evicted entries go to the pending list (no synchronisation
+// under the lock -- a chain's stream may sit behind an all-reduce of a row-sharded solve)
 void chain_cache_evict_to(size_t keep) {
     while (g_chain_cache.size() > keep) {
         auto lru = g_chain_cache.begin();
         for (auto it = g_chain_cache.begin(); it != g_chain_cache.end(); ++it)
             if (it->second.used < lru->second.used) lru = it;
-        chain_entry_destroy(lru->second);
+        g_chain_pending.push_back(lru->second);
         g_chain_cache.erase(lru);
     }
+}
+
+// call WITHOUT g_chain_mu: destroy the pending entries whose last replay has completed (all of
+// them, waiting for each, when `wait`)
+void chain_pending_reap(bool wait) {
+    std::vector<ChainEntry> done;
+    {
+        std::lock_guard<std::mutex> lock(g_chain_mu);
+        for (size_t i = 0; i < g_chain_pending.size();) {
+            ChainEntry& e = g_chain_pending[i];
+            if (wait || !e.done || hipEventQuery(e.done) == hipSuccess) {
+                done.push_back(e);
+                e = g_chain_pending.back();
+                g_chain_pending.pop_back();
+            } else {
+                ++i;
+            }
+        }
+    }
+    for (auto& e : done) chain_entry_destroy(e);
 }
 }  // namespace
 
@@ -1259,16 +1282,31 @@ extern "C" int32_t sglm_chol_graph_cache_size(void) {
 }
 
 extern "C" int sglm_chol_graph_cache_clear(void) {
-    std::lock_guard<std::mutex> lock(g_chain_mu);
-    chain_cache_evict_to(0);
+    {
+        std::lock_guard<std::mutex> lock(g_chain_mu);
+        chain_cache_evict_to(0);
+    }
+    chain_pending_reap(true);
     return SGLM_OK;
 }
+
+static int factor_inv_cached(float* H, float* Minv, int32_t P, const int32_t* fits, int32_t n,
+                             const float* dshift, float* delta, int32_t* info, uint8_t* frozen,
+                             int32_t B, void* work, hipStream_t s);
 
 static int factor_inv(float* H, float* Minv, int32_t P, const int32_t* fits, int32_t n,
                       const float* dshift, float* delta, int32_t* info, uint8_t* frozen,
                       int32_t B, void* work, hipStream_t s) {
     if (!chol_graphs_enabled() || s == nullptr)      // the null stream cannot be captured
         return factor_inv_launch(H, Minv, P, fits, n, dshift, delta, info, frozen, B, work, s);
+    const int st = factor_inv_cached(H, Minv, P, fits, n, dshift, delta, info, frozen, B, work, s);
+    chain_pending_reap(false);                        // evicted chains that finished, unlocked
+    return st;
+}
+
+static int factor_inv_cached(float* H, float* Minv, int32_t P, const int32_t* fits, int32_t n,
+                             const float* dshift, float* delta, int32_t* info, uint8_t* frozen,
+                             int32_t B, void* work, hipStream_t s) {
     ChainKey key;
     std::memset(&key, 0, sizeof(key));
     key.H = H; key.Minv = Minv; key.fits = fits; key.dshift = dshift; key.delta = delta;

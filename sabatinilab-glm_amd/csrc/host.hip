@@ -138,8 +138,9 @@ extern "C" int sglm_host_masks(int32_t nm, const int64_t* const* idx, const int6
 // by `nthreads` threads so that the DMA engine reads page-locked memory at full PCIe rate
 // (torch's pageable .to(device) is one staged, single-threaded copy).
 // sglm_host_copy: dst[0 .. nbytes) = src[0 .. nbytes).
-// sglm_host_gather_cols: dst[c * nrows * elem .. ) = column c (src[c], nrows contiguous
-//   elements of elem bytes) for c < ncols -- the event columns of a DataFrame, column-major.
+// sglm_host_gather_cols: dst[c * nrows * elem .. ) = column c (src[c], nrows elements of elem
+//   bytes, stride[c] elements apart; stride NULL: contiguous) for c < ncols -- the event
+//   columns of a DataFrame (a row-major block's columns are strided), column-major.
 extern "C" int sglm_host_copy(void* dst, const void* src, int64_t nbytes, int32_t nthreads) {
     if (nbytes <= 0) return SGLM_OK;
     if (!dst || !src) { sglm::set_error("sglm_host_copy: null pointer"); return SGLM_EINVAL; }
@@ -157,19 +158,88 @@ extern "C" int sglm_host_copy(void* dst, const void* src, int64_t nbytes, int32_
     return SGLM_OK;
 }
 
-extern "C" int sglm_host_gather_cols(const void* const* src, int32_t ncols, int64_t nrows,
-                                     int32_t elem, void* dst, int32_t nthreads) {
+extern "C" int sglm_host_gather_cols(const void* const* src, const int64_t* stride,
+                                     int32_t ncols, int64_t nrows, int32_t elem, void* dst,
+                                     int32_t nthreads) {
     if (ncols <= 0 || nrows <= 0) return SGLM_OK;
     if (!src || !dst || elem <= 0) { sglm::set_error("sglm_host_gather_cols: bad args"); return SGLM_EINVAL; }
     for (int c = 0; c < ncols; ++c)
         if (!src[c]) { sglm::set_error("sglm_host_gather_cols: null column %d", c); return SGLM_EINVAL; }
-    const int nt = std::max(1, std::min<int>(nthreads, ncols));
+    // threads own row ranges; inside a range of 2048 rows every column is copied in turn, so
+    // the columns of one row-major block (stride > 1) read the same cache lines back to back
+    const int64_t chunk = 2048;
+    const int64_t nchunks = (nrows + chunk - 1) / chunk;
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(nthreads, nchunks));
     std::vector<std::thread> th;
     for (int t = 0; t < nt; ++t)
         th.emplace_back([=] {
-            for (int c = t; c < ncols; c += nt)
-                std::memcpy((char*)dst + (size_t)c * nrows * elem, src[c], (size_t)nrows * elem);
+            for (int64_t q = t; q < nchunks; q += nt) {
+                const int64_t r0 = q * chunk, r1 = std::min(nrows, r0 + chunk);
+                for (int c = 0; c < ncols; ++c) {
+                    const int64_t st = stride ? stride[c] : 1;
+                    char* out = (char*)dst + ((size_t)c * nrows + r0) * elem;
+                    const char* in = (const char*)src[c] + (size_t)r0 * st * elem;
+                    if (st == 1) {
+                        std::memcpy(out, in, (size_t)(r1 - r0) * elem);
+                    } else if (elem == 8) {
+                        const uint64_t* a = (const uint64_t*)in;
+                        uint64_t* b = (uint64_t*)out;
+                        for (int64_t r = 0; r < r1 - r0; ++r) b[r] = a[r * st];
+                    } else {
+                        for (int64_t r = 0; r < r1 - r0; ++r)
+                            std::memcpy(out + r * elem, in + r * st * elem, (size_t)elem);
+                    }
+                }
+            }
         });
     for (auto& x : th) x.join();
+    return SGLM_OK;
+}
+
+// sglm_host_pack_bits_cols: for each column (float64, src[c] with element stride stride[c]),
+// bit r of bits[c * nwords + r / 32] = (value == 1.0), and binary[c] = 1 when every value is
+// 0.0 or 1.0 (a NaN, -0.0 is 0.0, or any other value clears it) -- a 0/1 event column crosses
+// PCIe as 1 bit per row instead of 8 bytes.  Threads own 2048-row ranges; nwords = ceil(nrows
+// / 32).
+extern "C" int sglm_host_pack_bits_cols(const void* const* src, const int64_t* stride,
+                                        int32_t ncols, int64_t nrows, uint32_t* bits,
+                                        uint8_t* binary, int32_t nthreads) {
+    if (ncols <= 0 || nrows <= 0) return SGLM_OK;
+    if (!src || !bits || !binary) { sglm::set_error("sglm_host_pack_bits_cols: bad args"); return SGLM_EINVAL; }
+    const int64_t nwords = (nrows + 31) / 32;
+    const int64_t chunk = 2048;
+    const int64_t nchunks = (nrows + chunk - 1) / chunk;
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(nthreads, nchunks));
+    std::vector<std::vector<uint8_t>> bad(nt, std::vector<uint8_t>(ncols, 0));
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([=, &bad] {
+            for (int64_t q = t; q < nchunks; q += nt) {
+                const int64_t r0 = q * chunk, r1 = std::min(nrows, r0 + chunk);
+                for (int c = 0; c < ncols; ++c) {
+                    const int64_t st = stride ? stride[c] : 1;
+                    const double* in = (const double*)src[c];
+                    uint32_t* out = bits + (size_t)c * nwords;
+                    uint8_t b = 0;
+                    for (int64_t w0 = r0; w0 < r1; w0 += 32) {
+                        uint32_t word = 0;
+                        const int64_t e = std::min<int64_t>(32, r1 - w0);
+                        for (int64_t k = 0; k < e; ++k) {
+                            const double v = in[(w0 + k) * st];
+                            word |= (uint32_t)(v == 1.0) << k;
+                            b |= (uint8_t)!(v == 0.0 || v == 1.0);
+                        }
+                        out[w0 / 32] = word;
+                    }
+                    bad[t][c] |= b;
+                }
+            }
+        });
+    for (auto& x : th) x.join();
+    for (int c = 0; c < ncols; ++c) {
+        uint8_t b = 0;
+        for (int t = 0; t < nt; ++t) b |= bad[t][c];
+        binary[c] = !b;
+    }
     return SGLM_OK;
 }

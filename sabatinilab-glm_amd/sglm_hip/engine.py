@@ -671,6 +671,7 @@ class Problem:
             bm[:, :n] = full[:, s0:s1]
             bm[:, n:] = 0
             nnz = np.count_nonzero(bm[:, :n], axis=1).astype(np.int64)
+            local = bm[:, :n].sum(axis=1, dtype=np.int64).astype(np.float64)
         self.M = torch.empty((nm, ld), dtype=torch.uint8, device=dev)
         self.M.view(-1).copy_(buf[: nm * ld], non_blocking=True)
         yb = _pinned("problem_y", max(ntot, 1), torch.float64)
@@ -692,6 +693,8 @@ class Problem:
         self.Yd64 = None
         self._ylo = None
         self._stats = {("count", f): float(sums[f]) for f in range(nm)}
+        # the slab's own multiplicity sums (the counts above stay global)
+        self._local_count = None if design.slab is None else local
         self._groups = None
         self._compact = {}
         return self
@@ -722,6 +725,12 @@ class Problem:
             else:
                 self._y64r = torch.from_numpy(np.stack(self.ys)).to(self.design.device)
         return self._y64r
+
+    def mask_local_count(self, mask: int) -> float:
+        """Sum of a mask's multiplicities over this process's rows (its slab's share in a
+        row-sharded solve, else mask_count)."""
+        lc = getattr(self, "_local_count", None)
+        return float(lc[mask]) if lc is not None else self.mask_count(mask)
 
     def mask_nnz(self, mask: int) -> int:
         """Rows with a nonzero mask value."""
@@ -1235,8 +1244,17 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
     # fits whose mask is every row with multiplicity 1 (the refits): a constant weight at the
     # start, so the first Gram can come from the event cross-correlations (sglm_lag_gram)
     ntot = d.n if d.slab is None else d.slab[2]
-    mall = {m: prob.mask_nnz(m) == d.n and prob.mask_count(m) == ntot
-            for m in set(int(r.mask) for r in reqs)}
+    # every row of this process with multiplicity exactly 1 (nnz == n and the local sum == n;
+    # a slab's rows can repeat while the global sum still equals the global row count) ...
+    umask = sorted(set(int(r.mask) for r in reqs))
+    mall = {m: prob.mask_nnz(m) == d.n and prob.mask_local_count(m) == d.n
+            and prob.mask_count(m) == ntot for m in umask}
+    if comm is not None and umask:
+        # ... on EVERY rank (min-reduced: all ranks take the same first-Gram decision)
+        flag = torch.tensor([1 if mall[m] else 0 for m in umask], dtype=torch.int32,
+                            device=dev)
+        comm.min_(flag)
+        mall = dict(zip(umask, (flag.cpu().numpy() > 0).tolist()))
     all_rows = np.array([mall[int(r.mask)] for r in reqs])
     # the weight m * h(y, eta) is one constant on such a mask only when h does not depend on y:
     # the Poisson log link (h = exp(eta)); Gamma / Tweedie's h carries y on every row
@@ -1252,6 +1270,10 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
     if use_aa:
         aa_raw = torch.zeros((B0, P), dtype=torch.float32, device=dev)
         aa_used = torch.zeros((B0, P), dtype=torch.float32, device=dev)
+        # per slot, this iteration's raw direction size (max |f_j|, j < p; |f_p|) where the
+        # correction ran: convergence is also judged on the raw Newton step
+        aa_rm = torch.zeros((B0, 2), dtype=torch.float32, device=dev)
+        aa_rm_h = _pinned("aa_rm", 2 * B0, torch.float32)
     aa_t = np.zeros(B0)
     aa_key = np.full(B0, -1, dtype=np.int64)
     fepoch = np.zeros(B0, dtype=np.int64)
@@ -1483,10 +1505,12 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
                            and CHOL_STREAM != "serial")
                 if cochain:
                     _lib.call("sglm_xtr_prefer", 1)
-                _lib.call("sglm_xtr_bits_packed", _p(d.cbits_full()), ld, P, n, _p(rp_buf), na,
-                          _p(act_d), _p(bf.g), _p(gx_work), st)
-                if cochain:
-                    _lib.call("sglm_xtr_prefer", -1)
+                try:
+                    _lib.call("sglm_xtr_bits_packed", _p(d.cbits_full()), ld, P, n, _p(rp_buf),
+                              na, _p(act_d), _p(bf.g), _p(gx_work), st)
+                finally:
+                    if cochain:
+                        _lib.call("sglm_xtr_prefer", -1)
             else:
                 d.xtr(bf.R, B, bf.g)
             if comm is not None:
@@ -1701,6 +1725,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
             key_now = src_now * 1_000_000 + fepoch[src_now]
             aa_idx = up(act, np.int64)
             raw = bf.delta[aa_idx]                     # this iteration's raw directions
+            aa_rm.zero_()
             sel = np.flatnonzero((aa_key[act] == key_now) & ~gram_now[act] & (aa_t[act] > 0))
             if sel.size:
                 # d = f - gamma (dbeta + df), gamma = df.f / df.df (f: raw direction, df its
@@ -1716,6 +1741,8 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
                 gdn = (bf.gtot[aa_idx[sel_d]].float() * dnew).sum(1)
                 good = (den > 1e-12 * (f * f).sum(1)) & (gam >= -2.0) & (gam <= 0.5) & (gdn < 0)
                 bf.delta[aa_idx[sel_d]] = torch.where(good[:, None], dnew, f)
+                aa_rm[aa_idx[sel_d], 0] = f[:, :p].abs().amax(1)
+                aa_rm[aa_idx[sel_d], 1] = f[:, p].abs()
                 if stats is not None:
                     stats.aa_fit_iters += int(sel.size)
             aa_raw[aa_idx] = raw
@@ -1742,6 +1769,8 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
         dmax_h[:na].copy_(dmax_d[:na], non_blocking=True)
         sc_h = _pinned("sc", sc.numel(), torch.float64)
         sc_h.copy_(sc, non_blocking=True)
+        if use_aa:
+            aa_rm_h.copy_(aa_rm.view(-1), non_blocking=True)
         t_sync = time.perf_counter()
         torch.cuda.current_stream().synchronize()              # the iteration's round trip
         if stats is not None:
@@ -1826,6 +1855,12 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
             scale = np.maximum(maxb[np.arange(na), tix], STOP_SCALE_FLOOR)
             prop = np.maximum(maxd / scale, maxdi)
         relv = step_a * prop
+        if use_aa:
+            # a secant-corrected step can be small while the raw Newton step is not
+            # (cancellation in f - gamma (dbeta + df)): such a fit is not converged
+            rm = aa_rm_h.numpy().reshape(B0, 2)[act].astype(np.float64)
+            rawp = np.maximum(rm[:, 0] / scale, rm[:, 1])
+            relv = np.maximum(relv, rawp)
         stepa = step_a
         fresh = (gram_now[act] & exact_h[act]) | const_hess
         ls_fail = stepa == 0.0

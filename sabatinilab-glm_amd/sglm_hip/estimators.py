@@ -70,8 +70,9 @@ def _as2d(X):
 
 
 # Outside fit_set, the designs packed for the last DESIGN_CACHE_ENTRIES numpy arrays (any
-# estimator) are kept and reused when a call passes an array with the same shape, dtype and
-# bytes -- an xxh3 digest of the whole buffer, so an array modified in place is packed again,
+# estimator; DESIGN_CACHE_MAX_BYTES of device memory in total) are kept and reused when a call
+# on the same device passes an array with the same shape, dtype and bytes -- an xxh3-128
+# digest of the whole buffer, so an array modified in place is packed again,
 # as sklearn would read it again.  The digest runs at host memory speed; the pack it saves is a
 # PCIe upload plus the device pack and bit-plane passes.  Designs above DESIGN_CACHE_MAX_BYTES
 # of device memory are not kept (the reference keeps every fold's model alive).
@@ -82,6 +83,7 @@ _DESIGN_CACHE_LOCK = __import__("threading").Lock()
 
 
 def _cached_design(Xa):
+    E.require_gpu()
     key = _digest(Xa)
     if key is not None:
         with _DESIGN_CACHE_LOCK:
@@ -90,14 +92,21 @@ def _cached_design(Xa):
                 _DESIGN_CACHE.move_to_end(key)
                 return d
     d = E.Design.from_host(Xa)
-    nbytes = sum(t.numel() * t.element_size() for t in (d.xb, d.xf, d.xbits, d.rbits)
-                 if t is not None)
+    nbytes = _design_bytes(d)
     if key is not None and nbytes <= DESIGN_CACHE_MAX_BYTES:
         with _DESIGN_CACHE_LOCK:
             _DESIGN_CACHE[key] = d
-            while len(_DESIGN_CACHE) > DESIGN_CACHE_ENTRIES:
+            # bounded by entry count AND by the device bytes the kept designs hold
+            while len(_DESIGN_CACHE) > DESIGN_CACHE_ENTRIES or (
+                    len(_DESIGN_CACHE) > 1 and
+                    sum(_design_bytes(v) for v in _DESIGN_CACHE.values()) > DESIGN_CACHE_MAX_BYTES):
                 _DESIGN_CACHE.popitem(last=False)
     return d
+
+
+def _design_bytes(d) -> int:
+    return sum(t.numel() * t.element_size() for t in (d.xb, d.xf, d.xbits, d.rbits, d._cbits)
+               if t is not None)
 
 
 def clear_design_cache():
@@ -107,14 +116,17 @@ def clear_design_cache():
 
 
 def _digest(X):
-    """(shape, dtype, xxh3-64 of the bytes) of a C-contiguous numpy array, else None."""
+    """(device, shape, dtype, xxh3-128 of the bytes) of a C-contiguous numpy array, else
+    None: a design packed on another device, or an array whose bytes differ, never matches."""
     if not isinstance(X, np.ndarray) or not X.flags.c_contiguous or X.dtype == object:
         return None
     try:
+        import torch
         import xxhash
     except ImportError:                       # pragma: no cover - part of the image
         return None
-    return (X.shape, X.dtype.str, xxhash.xxh3_64_intdigest(memoryview(X).cast("B")))
+    return (torch.cuda.current_device(), X.shape, X.dtype.str,
+            xxhash.xxh3_128_intdigest(memoryview(X).cast("B")))
 
 
 class _EngineRegressor:

@@ -49,7 +49,16 @@ def group_shuffle_split(groups, n_splits, test_size, random_state=None):
     else:
         rng = np.random.RandomState(random_state)
     groups = np.asarray(groups)
-    classes, gidx = np.unique(groups, return_inverse=True)
+    lo = int(groups.min()) if groups.size and groups.dtype.kind in "iu" else 0
+    if groups.size and groups.dtype.kind in "iu" and int(groups.max()) - lo < 4 * groups.size:
+        # small-range integer ids (categorical codes): the same classes / inverse by counting
+        g0 = groups.astype(np.int64) - lo
+        present = np.bincount(g0) > 0
+        classes = np.flatnonzero(present) + lo
+        lookup = np.cumsum(present) - 1
+        gidx = lookup[g0]
+    else:
+        classes, gidx = np.unique(groups, return_inverse=True)
     n_train, n_test = _validate(len(classes), test_size)
     out = []
     for _ in range(int(n_splits)):
@@ -79,8 +88,58 @@ def cv_idx_from_bucket_ids(bucket_ids, X=None, y=None, num_folds=None, test_size
 
 def trial_keys_codes(df, id_cols, package_style=False):
     """Categorical codes of the trial keys (backend/sglm_ez.py:334-340; package
-    sglm/sglm/models/split_data.py:146-152 when ``package_style``)."""
+    sglm/sglm/models/split_data.py:146-152 when ``package_style``).
+
+    The keys are built as the reference builds them -- per id column the string of the value
+    (``astype(str)`` / ``apply(str)``), prefixed with its length, joined with ``'_'`` (backend)
+    or ``'__'`` (package) -- but only for the distinct id tuples: the codes are the ranks of
+    those keys in lexicographic order (pandas' category order) taken back to the rows.  Numeric
+    id columns only; anything else takes the row-wise string path."""
     import pandas as pd
+    cols = [df[c] for c in id_cols]
+    if cols and all(isinstance(c.dtype, np.dtype) and c.dtype.kind in "biuf" for c in cols):
+        invs, strs = [], []
+        for c in cols:
+            v = c.to_numpy()
+            if v.size > 1 and bool(np.all(v[1:] >= v[:-1])):
+                # non-decreasing ids (trial counters): distinct values at the change points
+                chg = np.empty(v.size, dtype=bool)
+                chg[0] = True
+                np.not_equal(v[1:], v[:-1], out=chg[1:])
+                inv = np.cumsum(chg) - 1
+                u = v[chg]
+            else:
+                inv, u = pd.factorize(v, use_na_sentinel=False)          # hash, O(n)
+            su = pd.Series(u, dtype=c.dtype)
+            strs.append(np.asarray((su.apply(str) if package_style else su.astype(str)),
+                                   dtype=object))
+            invs.append(inv.astype(np.int64))
+        if len(invs) == 1:
+            tup, row_of = np.arange(strs[0].size)[:, None], invs[0]
+        else:
+            comb = invs[0]
+            for inv, st in zip(invs[1:], strs[1:]):
+                comb = comb * st.size + inv
+            row_of, cu = pd.factorize(comb)
+            tup = np.empty((cu.size, len(invs)), dtype=np.int64)
+            rem = cu.astype(np.int64)
+            for i in range(len(invs) - 1, -1, -1):
+                tup[:, i] = rem % strs[i].size
+                rem //= strs[i].size
+        first = strs[0][tup[:, 0]]
+        keys = [f"{len(sv)}:{sv}" for sv in first]
+        for i in range(1, len(strs)):
+            nxt = strs[i][tup[:, i]]
+            keys = ([f"{k}__{len(sv)}:{sv}" for k, sv in zip(keys, nxt)] if package_style
+                    else [f"{k}_{sv}" for k, sv in zip(keys, nxt)])
+        keys = np.asarray(keys, dtype=object)
+        order = np.argsort(keys, kind="stable")          # Python string order, as pandas
+        rank = np.empty(keys.size, dtype=np.int64)
+        rank[order] = np.arange(keys.size)
+        # distinct tuples can share a key only if two values print alike: keep pandas' codes
+        if len(set(keys.tolist())) == keys.size:
+            dt = np.int8 if keys.size < 128 else (np.int16 if keys.size < 32768 else np.int32)
+            return pd.Series(rank[row_of].astype(dt), index=df.index)
     bucket = None
     for i, idc in enumerate(id_cols):
         s = df[idc].astype(str) if not package_style else df[idc].apply(str)

@@ -46,6 +46,7 @@ class LagSource:
         self._E = None
         self._hasnan = {}        # column name -> holds a NaN cell
         self.cast = {}           # base column name -> dtype of its shift-0 copy in the frame
+        self.all_rows = None     # arange(N), built once
 
     def device(self, names):
         """Device float64 [rows][N] holding the named base columns (uploaded once, NaN kept),
@@ -58,24 +59,45 @@ class LagSource:
         if need:
             N, m = self.N, len(need)
             new = torch.empty((m, N), dtype=torch.float64, device="cuda")
+            arrs = [self._f64(c) for c in need]
+            # 0/1 columns cross PCIe as bit-planes (sglm_host_pack_bits_cols), the rest as
+            # float64 through the pinned stages below
+            nw = (N + 31) // 32
+            bits = _pinned("lagbits", max(1, m * nw), torch.int32)
+            binary = np.zeros(m, dtype=np.uint8)
+            ptrs = (ctypes.c_void_p * m)(*[a.ctypes.data for a in arrs])
+            strides = np.array([a.strides[0] // 8 for a in arrs], dtype=np.int64)
+            _lib.call("sglm_host_pack_bits_cols", ctypes.cast(ptrs, ctypes.c_void_p),
+                      strides.ctypes.data, m, N, bits.data_ptr(), binary.ctypes.data,
+                      HOST_THREADS)
+            bsel = np.flatnonzero(binary)
+            if bsel.size:
+                bd = bits[: m * nw].view(m, nw)[torch.from_numpy(bsel)].to("cuda",
+                                                                              non_blocking=True)
+                sh = torch.arange(32, dtype=torch.int32, device="cuda")
+                unp = ((bd.unsqueeze(-1) >> sh) & 1).reshape(bsel.size, nw * 32)[:, :N]
+                new[torch.from_numpy(bsel).to("cuda")] = unp.to(torch.float64)
+            raw = np.flatnonzero(binary == 0)
+            need_raw = [need[i] for i in raw]
+            arr_raw = [arrs[i] for i in raw]
             # column groups of <= 64 MB through two pinned stages: the threaded host gather of
             # group g + 1 overlaps the DMA of group g
             per = max(1, (64 << 20) // max(1, 8 * N))
             stages = [_pinned(f"lagsrc{i}", max(1, per * N), torch.float64) for i in range(2)]
             evs = [None, None]
-            for g, c0 in enumerate(range(0, m, per)):
-                grp = need[c0:c0 + per]
+            dst_rows = torch.from_numpy(raw).to("cuda") if raw.size else None
+            for g, c0 in enumerate(range(0, len(need_raw), per)):
+                grp = arr_raw[c0:c0 + per]
                 b = g % 2
                 if evs[b] is not None:
                     evs[b].synchronize()
-                arrs = [np.ascontiguousarray(self.base[c].to_numpy(dtype=np.float64,
-                                                                   na_value=NAN))
-                        for c in grp]
-                ptrs = (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+                ptrs = (ctypes.c_void_p * len(grp))(*[a.ctypes.data for a in grp])
+                strides = np.array([a.strides[0] // 8 for a in grp], dtype=np.int64)
                 _lib.call("sglm_host_gather_cols", ctypes.cast(ptrs, ctypes.c_void_p),
-                          len(arrs), N, 8, stages[b].data_ptr(), HOST_THREADS)
-                new[c0:c0 + len(grp)].view(-1).copy_(stages[b][: len(grp) * N],
-                                                     non_blocking=True)
+                          strides.ctypes.data, len(grp), N, 8, stages[b].data_ptr(),
+                          HOST_THREADS)
+                tmp = stages[b][: len(grp) * N].view(len(grp), N).to("cuda", non_blocking=True)
+                new[dst_rows[c0:c0 + len(grp)]] = tmp
                 ev = torch.cuda.Event()
                 ev.record()
                 evs[b] = ev
@@ -90,6 +112,23 @@ class LagSource:
                 self._hasnan[c] = bool(has[i])
         idx = torch.tensor([self._dev[c] for c in names], dtype=torch.int64, device="cuda")
         return self._E, idx
+
+    def _f64(self, name) -> np.ndarray:
+        """Host float64 values of a base column: a (possibly strided) view when it already is
+        float64 -- the columns of a row-major block are gathered by sglm_host_gather_cols."""
+        col = self.base[name]
+        if isinstance(col.dtype, np.dtype):
+            v = col.to_numpy()
+            if v.dtype == np.float64 and v.ndim == 1 and v.strides[0] % 8 == 0 \
+                    and v.strides[0] > 0:
+                return v
+            return np.ascontiguousarray(v.astype(np.float64))
+        return np.ascontiguousarray(col.to_numpy(dtype=np.float64, na_value=NAN))
+
+    def numeric(self, name) -> bool:
+        dt = self.base[name].dtype
+        return (isinstance(dt, np.dtype) and dt.kind in "biuf") or \
+            pd.api.types.is_numeric_dtype(dt)
 
     def has_nan(self, name) -> bool:
         """Whether an uploaded column holds a NaN cell."""
@@ -198,7 +237,11 @@ class LagFrame:
 
     def positions(self):
         """Row positions into the base frame (int64)."""
-        return np.arange(self._src.N, dtype=np.int64) if self._rows is None else self._rows
+        if self._rows is not None:
+            return self._rows
+        if self._src.all_rows is None:
+            self._src.all_rows = np.arange(self._src.N, dtype=np.int64)
+        return self._src.all_rows
 
     # ------------------------------------------------------------------ derived frames
     def _derive(self, cols=None, rows=None, index=None, keep_rows=True):
@@ -323,7 +366,8 @@ class LagFrame:
         for c in cols:
             if c in self._overlay:
                 cnt += pd.isna(self._overlay[c]).astype(np.int64)
-            elif self._spec[c][2]:
+            elif self._spec[c][2] or self._src.numeric(self._spec[c][0]):
+                # lag columns, and numeric base columns as lag 0 (device NaN flags)
                 nm, s, _ = self._spec[c]
                 lag.setdefault(s, []).append(nm)
             else:

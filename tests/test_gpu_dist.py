@@ -9,7 +9,8 @@ merge_results all-gathers the per-fit results and assembles the reference's per-
 dicts (backend/sglm_cv.py:188-200).  Rank 0's assembled grid must equal the unsharded grid
 solved in this process to 1e-5 relative, with every fit solved on exactly one rank.
 
-Row-sharded mode (the N-GPU default, sglm_hip/comm.py): each rank expands only its slab of
+Row-sharded mode (opt-in, SGLM_SHARD=rows; the default shards by fits, sglm_hip/grid.py
+SHARD_MODE, and sglm_hip/comm.py): each rank expands only its slab of
 the rows and runs every fit on it; Grams, gradients, trial losses, scores and mask statistics
 are all-reduced and the new factorisations dealt over the ranks.  Same bar against the
 unsharded grid."""

@@ -91,3 +91,22 @@ def test_row_slab_replay_follows_the_recorded_trajectory(engine, world, rank):
     assert sorted(a) == sorted(b) == list(range(len(objs) * 6))
     for i in a:
         assert np.array_equal(a[i][0], b[i][0]) and a[i][1] == b[i][1] and a[i][2] == b[i][2]
+
+
+def test_slab_multiplicity_sums_stay_local(engine):
+    """A resampled fold list (rows with multiplicity 2, others missing) whose GLOBAL count
+    equals the row count and whose slab rows are all present: the slab's own multiplicity sum
+    differs from its row count, so the constant-weight (all-rows) first Gram is not taken on
+    that slab (engine.irls ``mall``; min-reduced over the ranks in a row-sharded solve)."""
+    from sglm_hip import engine as E, synth
+    from sglm_hip.comm import row_slab
+    s = synth.make(N=20_000, m=5, L=4, family="poisson", rho=0.05, seed=2)
+    world, rank = 4, 1
+    slab = row_slab(s.N, rank, world)
+    nxt = row_slab(s.N, rank + 1, world)
+    d = E.Design.from_events(s.E, s.shifts, s.L - 1, s.N, slab=slab)
+    idx = np.sort(np.r_[np.setdiff1d(np.arange(s.N), [nxt[0]]), slab[0]])   # one dup, one gap
+    prob = E.Problem.from_index_lists(d, s.y, [0], [(idx, True), (None, False)])
+    assert prob.mask_count(0) == float(s.N) and prob.mask_nnz(0) == d.n
+    assert prob.mask_local_count(0) == float(d.n + 1)
+    assert prob.mask_local_count(1) == float(d.n)
