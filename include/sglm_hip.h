@@ -210,6 +210,20 @@ int sglm_xtr_bits_packed(const uint32_t* cbits, int64_t ld, int32_t P, int64_t n
                          const void* Rp, int32_t B, const int32_t* slots, double* G,
                          void* work, sglm_stream_t stream);
 
+/* G[q] = X^T D_q (float64) for integer-valued columns, |D| <= 256 (the base-256 digit planes
+ * of an exact X^T y): D as bf16 [Bp][ld] (Bp = ceil(B/32)*32 rows allocated), one bf16 piece,
+ * row slabs of <= 65,536 rows -- the sums are exact.  P % 512 == 0, ld < 2^26.
+ * work: sglm_xtr_bits_int_work_bytes(P, B, ld). */
+/* The operand of sglm_xtr_bits_int for an exact X^T (m y): pair i = (response pr[i] of Y
+ * [R][ldy] float64, mask pm[i] of M [F][ldm] uint8); v = rint(m y scale[i]) split into nd
+ * balanced base-256 digits, digit q of pair i -> D[q c + i][row] (bf16), rows < n only. */
+int sglm_digit_planes(const uint8_t* M, int64_t ldm, const double* Y, int64_t ldy, int64_t n,
+                      const int32_t* pr, const int32_t* pm, const double* scale, int32_t c,
+                      int32_t nd, void* D, int64_t ld, sglm_stream_t stream);
+size_t sglm_xtr_bits_int_work_bytes(int32_t P, int32_t B, int64_t ld);
+int sglm_xtr_bits_int(const uint32_t* cbits, int64_t ld, int32_t P, int64_t n, const void* D,
+                      int32_t B, double* G, void* work, sglm_stream_t stream);
+
 /* Shared-Gram elastic net for many fits per mask (multi-response lambda paths):
  * sglm_center_gram: Q[m] (float64 p x p) = G_xx - g g^T / n (center) or G_xx from the
  *   augmented Gram H[gram_of[m]] (ones column at index p, as sglm_syrk forms it with W = mask);

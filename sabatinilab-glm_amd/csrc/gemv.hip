@@ -615,6 +615,198 @@ xtr_bits4_kernel(const u32x2* __restrict__ cbits, int64_t ld, int32_t P, int64_t
     }
 }
 
+// ---- software-pipelined four-panel gradient (xtr_bits5_kernel) ----------------------------
+// The same workgroup tiling, LDS staging and MFMA sequence as xtr_bits4_kernel (so the same
+// partial sums bit for bit), scheduled the way the Gram mainloop is (syrk.hip half6): the
+// fragments of sub-step ks + 1 -- the bit expansions (32 VALU) and the R reads from LDS
+// (3 NGW ds_read_b128) -- are built while the MFMAs of sub-step ks run, one or two per MFMA gap,
+// instead of in a block between MFMA groups that a one-wave-per-SIMD kernel cannot hide.  The
+// step's single barrier sits between sub-steps 2 and 3, after the staging write of the next
+// step; the loads of step s + 2 are issued right after it (into the A registers step s no
+// longer needs), so a load has four sub-steps (~3,000 cycles at NGW = 2) to land.  R is loaded
+// in inline asm from a scalar base and one per-lane 32-bit offset (a plain load may be sunk to
+// its use by the compiler, which would expose its whole latency at the staging write).
+template <int NGW, int NPC>
+struct XFrag {
+    bf16x8 a[kXT];          // expanded bit fragments of the wave's tiles
+    bf16x8 b[NPC][NGW];     // R piece x fit group, from LDS
+};
+
+template <int NGW, int NPC>
+__device__ __forceinline__ void xfrags(const u32x2 (&ac)[kXT], const char* lb, int ks, int h,
+                                       XFrag<NGW, NPC>& f) {
+    constexpr int kF = NGW * 32;
+#pragma unroll
+    for (int m = 0; m < kXT; ++m) f.a[m] = frag_two(ac[m], ks, h);
+#pragma unroll
+    for (int pc = 0; pc < NPC; ++pc)
+#pragma unroll
+        for (int gi = 0; gi < NGW; ++gi)
+            f.b[pc][gi] = __builtin_bit_cast(
+                bf16x8, *reinterpret_cast<const u32x4*>(lb + (pc * kF + gi * 32) * kRS + 32 * ks));
+}
+
+// one sub-step's MFMAs in xtr_bits4_kernel's order (piece, group, tile)
+template <int NGW, int NPC>
+__device__ __forceinline__ void xmfma(const XFrag<NGW, NPC>& f, f32x16 (&ah)[NGW][kXT],
+                                      f32x16 (&al)[NGW][kXT]) {
+#pragma unroll
+    for (int pc = 0; pc < NPC; ++pc)
+#pragma unroll
+        for (int gi = 0; gi < NGW; ++gi)
+#pragma unroll
+            for (int m = 0; m < kXT; ++m) {
+                if (pc == 0)
+                    ah[gi][m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[m], f.b[pc][gi],
+                                                                        ah[gi][m], 0, 0, 0);
+                else
+                    al[gi][m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[m], f.b[pc][gi],
+                                                                        al[gi][m], 0, 0, 0);
+            }
+}
+
+// the sub-step's MFMAs, each followed by its share of the next fragments' LDS reads and VALU
+template <int NGW, int NPC>
+__device__ __forceinline__ void xinterleave() {
+#ifdef XTR_NO_INTERLEAVE
+    return;
+#endif
+    constexpr int NM = NPC * NGW * kXT;           // MFMAs
+    constexpr int ND = NPC * NGW;                 // ds_read_b128
+    constexpr int NV = (8 * kXT + NM - 1) / NM;   // VALU per gap (32 expansion VALU in all)
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);          // MFMA
+        if (i < ND) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+        __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);         // VALU
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int NGW, int WPE = 1, int NPC = 3>
+__global__ void __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
+xtr_bits5_kernel(const u32x2* __restrict__ cbits, int64_t ld, int32_t P, int64_t nblk,
+                 const __bf16* __restrict__ Rp, int32_t Bp, int32_t B, int32_t splits,
+                 float* __restrict__ part) {
+    constexpr int kF = NGW * 32;                 // fits per workgroup
+    constexpr int kJ = NPC * NGW;                // staging chunks per thread
+    __shared__ __attribute__((aligned(16))) char lds[2][NPC * kF * kRS];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int npan4 = P / (32 * kXT * kXW), ngrp = Bp / 32, ngrp2 = (ngrp + NGW - 1) / NGW;
+    const int L = xcd_logical(blockIdx.x, npan4 * ngrp2 * splits);
+    const int pq = L % npan4, g2 = (L / npan4) % ngrp2, z = L / (npan4 * ngrp2);
+    const int g0 = g2 * NGW, ngv = min(NGW, ngrp - g0);       // groups present (uniform)
+    const int pn = pq * kXW + wave;
+    const int64_t sps = (nblk + splits - 1) / splits;
+    const int64_t blk0 = (int64_t)z * sps;
+    const int64_t blk1 = min(blk0 + sps, nblk);
+    const int nsteps = blk1 > blk0 ? (int)(blk1 - blk0) : 0;
+    const uint64_t abase = (uint64_t)(cbits + blk0 * P);
+    const uint32_t avo = (uint32_t)((pn * (32 * kXT) + r) * 8);
+    // staging chunk j (16 B): piece j / NGW, fit (tid >> 3) + 32 (j % NGW), byte 16 (tid & 7)
+    // of the fit's 128-B row segment; an absent group (ngv < NGW) re-reads group 0 (never used)
+    const uint64_t rbase = (uint64_t)(reinterpret_cast<const char*>(Rp) + blk0 * 128 +
+                                      (int64_t)g0 * 32 * ld * 2);
+    const uint32_t rvo = (uint32_t)((tid >> 3) * ld * 2 + (tid & 7) * 16);
+    const uint64_t plane = (uint64_t)Bp * ld * 2;
+    const uint64_t gstep = (uint64_t)32 * ld * 2;
+    auto joff = [&](int j) {
+        const int gi = j % NGW;
+        return (uint64_t)(j / NGW) * plane + (gi < ngv ? (uint64_t)gi * gstep : 0);
+    };
+    const int lbase = (tid >> 3) * kRS + (tid & 7) * 16;
+    auto loff = [&](int j) { return lbase + ((j / NGW) * kF + 32 * (j % NGW)) * kRS; };
+    if (nsteps <= 0) {                          // an empty slab: zero partials, no loop
+#pragma unroll
+        for (int gi = 0; gi < NGW; ++gi) {
+            const int f = (g0 + gi) * 32 + r;
+            if (gi < ngv && f < B) {
+                float* out = part + ((int64_t)z * B + f) * P + pn * (32 * kXT);
+                for (int m = 0; m < kXT; ++m)
+                    for (int j = 0; j < 16; ++j) out[m * 32 + (j & 3) + 8 * (j >> 2) + 4 * h] = 0.0f;
+            }
+        }
+        return;
+    }
+    f32x16 ah[NGW][kXT], al[NGW][kXT];
+#pragma unroll
+    for (int gi = 0; gi < NGW; ++gi)
+#pragma unroll
+        for (int m = 0; m < kXT; ++m) {
+            ah[gi][m] = (f32x16){};
+            al[gi][m] = (f32x16){};
+        }
+    {
+        u32x2 a0[kXT] = {}, a1[kXT] = {};
+        u32x4 rv[kJ];
+        auto issue = [&](u32x2 (&an)[kXT], int s) {
+            loadA<0>(an, abase + (uint64_t)s * P * 8, avo);
+#pragma unroll
+            for (int j = 0; j < kJ; ++j) rv[j] = gld4s<0>(rbase + (uint64_t)s * 128 + joff(j), rvo);
+        };
+        auto land = [&](u32x2 (&an)[kXT], int buf) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int m = 0; m < kXT; ++m) asm volatile("" : "+v"(an[m]));
+#pragma unroll
+            for (int j = 0; j < kJ; ++j) asm volatile("" : "+v"(rv[j]));
+#pragma unroll
+            for (int j = 0; j < kJ; ++j) *reinterpret_cast<u32x4*>(&lds[buf][loff(j)]) = rv[j];
+        };
+        const int lofs = r * kRS + h * 16;
+        XFrag<NGW, NPC> F, G;
+        issue(a0, 0);
+        land(a0, 0);
+        __syncthreads();
+        if (nsteps > 1) issue(a1, 1);
+        xfrags<NGW, NPC>(a0, &lds[0][lofs], 0, h, F);
+        // step s from A registers ac and LDS buffer c (F = its sub-step 0 fragments; the loads
+        // of step s + 1 in flight into an and rv); leaves F = sub-step 0 of step s + 1
+        auto step = [&](u32x2 (&ac)[kXT], u32x2 (&an)[kXT], int s, int c) {
+            const char* lb = &lds[c][lofs];
+            __builtin_amdgcn_sched_barrier(0);
+            xfrags<NGW, NPC>(ac, lb, 1, h, G);
+            xmfma<NGW, NPC>(F, ah, al);
+            xinterleave<NGW, NPC>();
+            xfrags<NGW, NPC>(ac, lb, 2, h, F);
+            xmfma<NGW, NPC>(G, ah, al);
+            xinterleave<NGW, NPC>();
+            xfrags<NGW, NPC>(ac, lb, 3, h, G);
+            xmfma<NGW, NPC>(F, ah, al);
+            xinterleave<NGW, NPC>();
+            const bool more = s + 1 < nsteps;
+            if (more) land(an, c ^ 1);
+            __syncthreads();
+            if (s + 2 < nsteps) issue(ac, s + 2);
+            __builtin_amdgcn_sched_barrier(0);
+            // unconditional (one scheduling region with the MFMAs): past the last step it
+            // expands stale registers and LDS that nothing uses
+            xfrags<NGW, NPC>(an, &lds[c ^ 1][lofs], 0, h, F);
+            xmfma<NGW, NPC>(G, ah, al);
+            xinterleave<NGW, NPC>();
+        };
+        int s = 0;
+        for (; s + 1 < nsteps; s += 2) {
+            step(a0, a1, s, 0);
+            step(a1, a0, s + 1, 1);
+        }
+        if (s < nsteps) step(a0, a1, s, 0);
+    }
+#pragma unroll
+    for (int gi = 0; gi < NGW; ++gi) {
+        const int f = (g0 + gi) * 32 + r;
+        if (gi < ngv && f < B) {
+            float* out = part + ((int64_t)z * B + f) * P + pn * (32 * kXT);
+#pragma unroll
+            for (int m = 0; m < kXT; ++m)
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    out[m * 32 + (j & 3) + 8 * (j >> 2) + 4 * h] =
+                        NPC == 1 ? 0.5f * ah[gi][m][j] : 0.5f * (ah[gi][m][j] + al[gi][m][j]);
+        }
+    }
+}
+
 // Gradient kernel per call (read per launch: tests switch it inside one process):
 //   2 = four-panel, two fit groups per workgroup -- an even group count (P % 512 == 0);
 //   0 = one-panel -- otherwise (an odd count leaves half-empty two-group workgroups, and the
@@ -651,6 +843,21 @@ static void launch_xtr_bits(const u32x2* cbits, int64_t ld, int32_t P, int64_t n
     const int ngw = v == 2 ? 2 : 1;
     const unsigned wgs4 = (unsigned)((P / (32 * kXT * kXW)) * ((Bp / 32 + ngw - 1) / ngw) *
                                      splits);
+    // the pipelined kernel (SGLM_XTR_PIPE, read per launch) takes R's per-lane offsets in 32 bits
+    const char* ep = getenv("SGLM_XTR_PIPE");
+    const bool pipe = v != 0 && ep && ep[0] == '1' && (int64_t)32 * ld * 2 < ((int64_t)1 << 32);
+    if (pipe) {
+        if (v == 3)
+            xtr_bits5_kernel<1, 2><<<wgs4, 64 * kXW, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, B,
+                                                             splits, part);
+        else if (v == 2)
+            xtr_bits5_kernel<2><<<wgs4, 64 * kXW, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, B, splits,
+                                                          part);
+        else
+            xtr_bits5_kernel<1><<<wgs4, 64 * kXW, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, B, splits,
+                                                          part);
+        return;
+    }
     if (v == 3)
         xtr_bits4_kernel<1, 2><<<wgs4, 64 * kXW, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, B, splits,
                                                          part);
@@ -718,6 +925,31 @@ static size_t xtr_part_bytes(int32_t P, int32_t B, int64_t nblk) {
     const int s = std::max(std::max(xtr_splits_for(P, B, nblk, 0), xtr_splits_for(P, B, nblk, 3)),
                            std::max(xtr_splits_for(P, B, nblk, 1), xtr_splits_for(P, B, nblk, 2)));
     return (size_t)s * B * P * sizeof(float);
+}
+
+// Balanced base-256 digit planes of fixed-point m*y (the exact X^T(m y) of 0/1 designs):
+// pair i = (response pr[i], mask pm[i]); v = rint(m[row] * y[row] * scale[i]) (|v| < 2^38 by the
+// caller's scale), digit q = ((v + 128) mod 256) - 128, v <- (v - digit) / 256, written as bf16
+// (exact) to D[q * c + i][row].  Rows >= n are not written (the caller keeps them zero).
+__global__ void __launch_bounds__(256) digit_planes_kernel(
+    const uint8_t* __restrict__ M, int64_t ldm, const double* __restrict__ Y, int64_t ldy,
+    int64_t n, const int32_t* __restrict__ pr, const int32_t* __restrict__ pm,
+    const double* __restrict__ scale, int32_t c, int32_t nd, __bf16* __restrict__ D,
+    int64_t ld) {
+    const int i = blockIdx.y;
+    const uint8_t* m = M + (int64_t)pm[i] * ldm;
+    const double* y = Y + (int64_t)pr[i] * ldy;
+    const double sc = scale[i];
+    for (int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x; row < n;
+         row += (int64_t)gridDim.x * 256) {
+        const double mv = (double)m[row];
+        int64_t v = mv == 0.0 ? 0 : (int64_t)rint(mv * y[row] * sc);
+        for (int q = 0; q < nd; ++q) {
+            const int64_t dq = ((v + 128) & 255) - 128;       // floor mod for two's complement
+            D[((int64_t)q * c + i) * ld + row] = (__bf16)(float)dq;
+            v = (v - dq) >> 8;                                // exact: v - dq is a multiple of 256
+        }
+    }
 }
 
 }  // namespace sglm
@@ -836,6 +1068,83 @@ size_t sglm_xtr_bits_packed_work_bytes(int32_t P, int32_t B, int64_t ld) {
         mx = w > mx ? w : mx;
     }
     return mx;
+}
+
+int sglm_digit_planes(const uint8_t* M, int64_t ldm, const double* Y, int64_t ldy, int64_t n,
+                      const int32_t* pr, const int32_t* pm, const double* scale, int32_t c,
+                      int32_t nd, void* D, int64_t ld, sglm_stream_t stream) {
+    if (c <= 0 || n <= 0) return SGLM_OK;
+    if (!M || !Y || !pr || !pm || !scale || !D || nd < 1 || nd > 8 || n > ld || n > ldm ||
+        n > ldy || c > 65535) {
+        set_error("sglm_digit_planes: bad args");
+        return SGLM_EINVAL;
+    }
+    const int64_t gx = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
+    digit_planes_kernel<<<dim3((unsigned)gx, (unsigned)c), 256, 0, as_stream(stream)>>>(
+        M, ldm, Y, ldy, n, pr, pm, scale, c, nd, reinterpret_cast<__bf16*>(D), ld);
+    return check_launch("digit_planes_kernel");
+}
+
+// X^T D for integer-valued columns D (|d| <= 256, exact in bf16: one piece instead of three),
+// D given as bf16 [Bp][ld] (rows B..Bp-1 readable, their results unused).  The pipelined
+// kernel with one piece: four 32-column groups per workgroup (the accumulators the two low
+// pieces used), row slabs of <= 1024 K-steps so the f32 sums of integers stay exact (|2 d| x
+// 65,536 <= 2^25: the operand 2.0 doubles the products; sums up to 2^24 x 2 are exact in f32
+// for even integers).  P % 512 == 0.
+static int xtr_int_ngw(int32_t B) {
+    const int ngrp = (B + 31) / 32;
+    return ngrp >= 4 ? 4 : ngrp >= 2 ? 2 : 1;
+}
+static int xtr_int_splits(int32_t P, int32_t B, int64_t nblk) {
+    const int64_t ngw = xtr_int_ngw(B), ngrp = (B + 31) / 32;
+    const int64_t wps = (P / (32 * kXT * kXW)) * ((ngrp + ngw - 1) / ngw);
+    const int64_t cap = nblk / 32 > 1 ? nblk / 32 : 1;
+    int best = 1;
+    double bestc = 1e300;
+    for (int64_t s = 1; s <= cap && s <= 4096; ++s) {
+        const double c = (double)((wps * s + 255) / 256) * ((double)((nblk + s - 1) / s) + 8.0);
+        if (c < bestc) {
+            bestc = c;
+            best = (int)s;
+        }
+    }
+    const int64_t lo = (nblk + kExactSlabSteps - 1) / kExactSlabSteps;
+    return (int64_t)best < lo ? (int)lo : best;
+}
+
+size_t sglm_xtr_bits_int_work_bytes(int32_t P, int32_t B, int64_t ld) {
+    return (size_t)xtr_int_splits(P, B, ld / 64) * B * P * sizeof(float);
+}
+
+int sglm_xtr_bits_int(const uint32_t* cbits, int64_t ld, int32_t P, int64_t n, const void* D,
+                      int32_t B, double* G, void* work, sglm_stream_t stream) {
+    if (B <= 0) return SGLM_OK;
+    if (!cbits || !D || !G || !work || ld % 256 || P % 512 || n > ld ||
+        (int64_t)32 * ld * 2 >= ((int64_t)1 << 32)) {
+        set_error("sglm_xtr_bits_int: bad args (P %% 512, ld < 2^26)");
+        return SGLM_EINVAL;
+    }
+    const int32_t Bp = (B + 31) / 32 * 32;
+    const int64_t nblk = (n + 63) / 64;
+    const int splits = xtr_int_splits(P, B, ld / 64);
+    const int ngw = xtr_int_ngw(B);
+    const unsigned wgs = (unsigned)((P / (32 * kXT * kXW)) * ((Bp / 32 + ngw - 1) / ngw) * splits);
+    hipStream_t s = as_stream(stream);
+    float* part = reinterpret_cast<float*>(work);
+    const u32x2* cb = reinterpret_cast<const u32x2*>(cbits);
+    const __bf16* Db = reinterpret_cast<const __bf16*>(D);
+    if (ngw == 4)
+        xtr_bits5_kernel<4, 1, 1><<<wgs, 64 * kXW, 0, s>>>(cb, ld, P, nblk, Db, Bp, B, splits, part);
+    else if (ngw == 2)
+        xtr_bits5_kernel<2, 1, 1><<<wgs, 64 * kXW, 0, s>>>(cb, ld, P, nblk, Db, Bp, B, splits, part);
+    else
+        xtr_bits5_kernel<1, 1, 1><<<wgs, 64 * kXW, 0, s>>>(cb, ld, P, nblk, Db, Bp, B, splits, part);
+    int st = check_launch("xtr_bits5_kernel<1 piece>");
+    if (st) return st;
+    const int64_t len = (int64_t)B * P;
+    reduce_slabs_f64<<<(unsigned)((len + 255) / 256 < 4096 ? (len + 255) / 256 : 4096), 256, 0,
+                       s>>>(part, len, splits, P, nullptr, G);
+    return check_launch("reduce_slabs_f64");
 }
 
 int sglm_xtr_bits_packed(const uint32_t* cbits, int64_t ld, int32_t P, int64_t n,

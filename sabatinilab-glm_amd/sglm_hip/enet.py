@@ -65,6 +65,24 @@ class SharedGrams:
             self.slot[m] = base + i
         self.H = H
 
+    def complement(self, parts: dict):
+        """Grams of masks that are the difference of two formed ones: parts[m] = (a, b) with
+        mask m = mask a - mask b row by row, G_m = G_a - G_b -- exact (integer counts below
+        2^24 in f32) when the design is 0/1."""
+        need = [m for m in parts if m not in self.slot]
+        if not need:
+            return
+        self.ensure([v for m in need for v in parts[m]])
+        base = self.H.shape[0]
+        H = torch.empty((base + len(need), self.d.P, self.d.P), dtype=torch.float32,
+                        device=self.d.device)
+        H[:base].copy_(self.H)
+        for i, m in enumerate(need):
+            a, b = parts[m]
+            torch.sub(H[self.slot[a]], H[self.slot[b]], out=H[base + i])
+            self.slot[m] = base + i
+        self.H = H
+
     def centred(self, masks: Sequence[int], center: bool):
         """float64 Q (p x p) per (mask, center); returns the index of each requested mask."""
         self.ensure(masks)
@@ -130,6 +148,8 @@ def _xty_digits(prob: E.Problem, pairs: Sequence[tuple], out: torch.Tensor) -> t
     Y64 = prob.y64_rows()                                       # [R][n] float64
     nd = XTY_DIGITS
     top = 8 * nd - 2                                            # |m y| 2^sh < 2^top
+    if d.xtr_int_ok():
+        return _xty_digits_int(prob, pairs, out, Y64, nd, top)
     chunk = max(1, 240 // nd)
     D = torch.zeros((chunk * nd, ld), dtype=torch.float32, device=dev)
     g = torch.empty((chunk * nd, d.P), dtype=torch.float64, device=dev)
@@ -150,6 +170,40 @@ def _xty_digits(prob: E.Problem, pairs: Sequence[tuple], out: torch.Tensor) -> t
             D[q * c:(q + 1) * c, :n] = dq.to(torch.float32)
             Ri = torch.div(Ri - dq, 256, rounding_mode="floor")
         d.xtr(D[: nd * c], nd * c, g[: nd * c])
+        gq = g[: nd * c].view(nd, c, d.P)
+        out[s:s + c] = (gq * w8[:, None, None]).sum(0) * torch.exp2(-sh)[:, None]
+    return out
+
+
+def _xty_digits_int(prob: E.Problem, pairs: Sequence[tuple], out: torch.Tensor, Y64, nd: int,
+                    top: int) -> torch.Tensor:
+    """The digit planes built by one HIP pass (sglm_digit_planes) and summed by the one-piece
+    integer gradient kernel (sglm_xtr_bits_int).  The scale of a pair comes from the bound
+    max(m) max|y| of its mask and response (|m y| < 2^e)."""
+    d = prob.design
+    n, ld, dev = d.n, d.ld, d.device
+    M = prob.M
+    mmax = M[:, :n].amax(1).to(torch.float64)                   # [F]
+    ymax = Y64.abs().amax(1)                                    # [R]
+    chunk = max(1, 384 // nd)                                   # <= 384 digit columns a call
+    ncol = (min(chunk, len(pairs)) * nd + 31) // 32 * 32
+    D = torch.zeros((ncol, ld), dtype=torch.bfloat16, device=dev)   # rows >= n stay zero
+    g = torch.empty((ncol, d.P), dtype=torch.float64, device=dev)
+    w8 = torch.tensor([256.0 ** q for q in range(nd)], dtype=torch.float64, device=dev)
+    for s in range(0, len(pairs), chunk):
+        pr = pairs[s:s + chunk]
+        c = len(pr)
+        rm = torch.tensor([[r for r, _ in pr], [m for _, m in pr]], dtype=torch.int32,
+                          device=dev)
+        ri, mi = rm[0].long(), rm[1].long()
+        bnd = mmax[mi] * ymax[ri]
+        e = torch.where(bnd > 0, torch.floor(torch.log2(bnd.clamp_min(1e-300))) + 1,
+                        torch.zeros_like(bnd))
+        sh = top - e
+        scale = torch.exp2(sh)
+        _lib.call("sglm_digit_planes", E._p(M), M.stride(0), E._p(Y64), Y64.stride(0), n,
+                  E._p(rm[0]), E._p(rm[1]), E._p(scale), c, nd, E._p(D), ld, E._stream())
+        d.xtr_int(D, nd * c, g)
         gq = g[: nd * c].view(nd, c, d.P)
         out[s:s + c] = (gq * w8[:, None, None]).sum(0) * torch.exp2(-sh)[:, None]
     return out
@@ -247,6 +301,20 @@ def _mask_sum_y2(prob: E.Problem) -> np.ndarray:
     return out[:, :, 2].t().cpu().numpy()
 
 
+def _test_is_complement(prob: E.Problem, K: int, full: int) -> bool:
+    """Every test mask 2k+1 equals the full mask minus train mask 2k (0/1 designs only, Gram
+    counts within f32's exact integers)."""
+    d = prob.design
+    if d.xbits is None or not E.XTR_BITS:
+        return False
+    M = prob.M[:, :d.n]
+    if int(M[full].max()) * d.n >= (1 << 24):
+        return False
+    tr = M[0:2 * K:2].to(torch.int16)
+    te = M[1:2 * K:2].to(torch.int16)
+    return bool(((tr + te) == M[full].to(torch.int16)[None, :]).all())
+
+
 def cv_enet_path(X, Y, cv_idx, alphas: Sequence[float], l1_ratio: float = 0.5,
                  fit_intercept: bool = True, max_iter: int = 1000, score_method: str = "mse",
                  stats: Optional[dict] = None, shard: bool = True):
@@ -292,9 +360,29 @@ def cv_enet_path(X, Y, cv_idx, alphas: Sequence[float], l1_ratio: float = 0.5,
     masks.append(np.ones(n, np.uint8))
     prob = E.Problem(design, Y, masks)
     grams = SharedGrams(prob)
-    grams.ensure(range(len(masks)))
     pairs = [(r, m) for r in range(R) for m in range(len(masks))]
-    c = xty(prob, pairs)
+    if K and _test_is_complement(prob, K, FULL):
+        # test mask = all rows - train mask (GroupShuffleSplit partitions the groups): the test
+        # Grams and X^T(m y) are differences of the train and full ones, exact for 0/1 designs
+        # (integer Gram counts; X^T(m y) float64-accurate), so only K + 1 masks are formed
+        formed = [2 * k for k in range(K)] + [FULL]
+        n_formed = len(formed)
+        grams.ensure(formed)
+        grams.complement({2 * k + 1: (FULL, 2 * k) for k in range(K)})
+        bpairs = [(r, m) for r in range(R) for m in formed]
+        cb = xty(prob, bpairs)
+        bi = {pm: i for i, pm in enumerate(bpairs)}
+        test = [i for i, (r, m) in enumerate(pairs) if m < FULL and m % 2]
+        src = [bi[(r, FULL if (m < FULL and m % 2) else m)] for r, m in pairs]
+        c = cb[torch.tensor(src, dtype=torch.int64, device=dev)]
+        if test:
+            c[torch.tensor(test, dtype=torch.int64, device=dev)] -= cb[torch.tensor(
+                [bi[(pairs[i][0], pairs[i][1] - 1)] for i in test], dtype=torch.int64,
+                device=dev)]
+    else:
+        n_formed = len(masks)
+        grams.ensure(range(len(masks)))
+        c = xty(prob, pairs)
     ci = {pm: i for i, pm in enumerate(pairs)}
     fits, keys = [], []
     for r in range(R):
@@ -388,6 +476,7 @@ def cv_enet_path(X, Y, cv_idx, alphas: Sequence[float], l1_ratio: float = 0.5,
             })
         out.append(per)
     if stats is not None:
-        stats.update({"fits": len(fits), "grams": len(masks), "xty_columns": len(pairs),
+        stats.update({"fits": len(fits), "grams": len(masks), "grams_formed": n_formed,
+                      "xty_columns": len(pairs),
                       "cd_sweeps_total": int(np.sum(sw)), "cd_sweeps_max": int(np.max(sw))})
     return out

@@ -444,6 +444,23 @@ class Design:
             _lib.call("sglm_xtr", _p(self.xg), self.xtype, self.ld, self.P, self.n, _p(R), B,
                       _p(g_out), _p(w), st)
 
+    def xtr_int_ok(self) -> bool:
+        """sglm_xtr_bits_int applies: a 0/1 design with P % 512 == 0 and ld < 2^26."""
+        return (self.xbits is not None and XTR_BITS and self.P % 512 == 0
+                and 64 * self.ld < (1 << 32))
+
+    def xtr_int(self, D, B, g_out):
+        """g_out[k] (float64) = X^T D[k] for k < B, D: bf16 [ceil(B/32)*32][ld] device tensor of
+        integers |d| <= 256 (exact: one bf16 piece, f32 sums of integers within 2^24)."""
+        if not self.xtr_int_ok():
+            raise RuntimeError("xtr_int needs a 0/1 design with P % 512 == 0")
+        if D.dtype != torch.bfloat16 or D.shape[0] < (B + 31) // 32 * 32 or D.shape[1] != self.ld:
+            raise ValueError("xtr_int: D must be bf16 [ceil(B/32)*32][ld]")
+        w = _work(_lib.query("sglm_xtr_bits_int_work_bytes", self.P, B, self.ld), self.device,
+                  "xtr")
+        _lib.call("sglm_xtr_bits_int", _p(self.cbits_full()), self.ld, self.P, self.n, _p(D), B,
+                  _p(g_out), _p(w), _stream())
+
     def eta(self, beta_dev, out=None, slots=None, direction=False):
         """eta[k] = X beta[k] for a (B, P) f32 device tensor; with ``slots`` (int32 device
         tensor) only those rows k (the rest of ``out`` is left as is).  ``direction``: beta

@@ -878,6 +878,19 @@ def test_xtr_bits_four_panel_kernel_vs_float64(engine, torch_mod, B, ngw, monkey
     ref = (Rd.double() @ X.t()).cpu().numpy()
     scale = (Rd.double().abs() @ X.abs().t()).cpu().numpy()
     assert np.max(np.abs(G.cpu().numpy() - ref) / np.maximum(scale, 1e-30)) < 2e-6
+    # the software-pipelined kernel (xtr_bits5_kernel): the same MFMA sequence per wave, so
+    # the same partial sums bit for bit; also on the two-wave one-group variant
+    for pipe_env in ({"SGLM_XTR_PIPE": "1"}, {"SGLM_XTR_PIPE": "1", "SGLM_XTR_NGW": "3"}):
+        for k, v in pipe_env.items():
+            monkeypatch.setenv(k, v)
+        G2 = torch.zeros_like(G)
+        _lib.call("sglm_xtr_bits", d.cbits_full().data_ptr(), d.ld, d.P, d.n, Rd.data_ptr(), B,
+                  G2.data_ptr(), w.data_ptr(), 0)
+        if pipe_env.get("SGLM_XTR_NGW") == "3":
+            assert np.max(np.abs(G2.cpu().numpy() - ref) / np.maximum(scale, 1e-30)) < 2e-6
+        else:
+            assert torch.equal(G2, G), pipe_env
+    monkeypatch.delenv("SGLM_XTR_PIPE")
 
 
 @pytest.mark.parametrize("shifts,event_major,row0,slab", [
@@ -995,3 +1008,48 @@ def test_grid_bad_fold_index_raises_index_error(engine):
     objs = [Objective("irls", E_.FAM_TWEEDIE_LOG, 1.0, 1e-2, "n", True, 100)]
     with pytest.raises(IndexError):
         grid.run(d, s.y, [(tr, te)], objs, [0])
+
+
+@pytest.mark.parametrize("B,lim", [(45, 128), (130, 256), (7, 128)])
+def test_xtr_bits_int_exact(engine, torch_mod, B, lim):
+    """sglm_xtr_bits_int (one bf16 piece, the digit planes of an exact X^T y) equals the float64
+    X^T D exactly for integer columns |d| <= lim (one, two and four 32-column groups per
+    workgroup), and sglm_digit_planes writes the balanced base-256 digits of rint(m y s)."""
+    torch = torch_mod
+    from sglm_hip import _lib, synth
+    s = synth.make(N=70_000, m=50, L=10, rho=0.05, seed=B)
+    d = engine.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
+    assert d.P % 512 == 0 and d.xtr_int_ok()
+    rng = np.random.default_rng(B)
+    Bp = (B + 31) // 32 * 32
+    D = np.zeros((Bp, d.ld), np.float32)
+    D[:B, : s.N] = rng.integers(-lim, lim + 1, (B, s.N))
+    Dd = torch.from_numpy(D).cuda().to(torch.bfloat16)
+    G = torch.zeros((B, d.P), dtype=torch.float64, device="cuda")
+    d.xtr_int(Dd, B, G)
+    X = d.xb.double()
+    ref = (torch.from_numpy(D[:B]).cuda().double() @ X.t()).cpu().numpy()
+    assert np.array_equal(G.cpu().numpy(), ref)
+    # digit planes: 3 pairs (response, mask) with a multiplicity mask
+    R, F = 2, 2
+    Y = rng.normal(size=(R, s.N)) * np.array([[1.0], [1e3]])
+    M = np.zeros((F, d.ld), np.uint8)
+    M[0, : s.N] = rng.integers(0, 2, s.N)
+    M[1, : s.N] = rng.integers(0, 3, s.N)
+    Yd, Md = torch.from_numpy(Y).cuda(), torch.from_numpy(M).cuda()
+    pr = torch.tensor([0, 1, 1], dtype=torch.int32, device="cuda")
+    pm = torch.tensor([1, 0, 1], dtype=torch.int32, device="cuda")
+    sc = torch.tensor([2.0 ** 30, 2.0 ** 20, 2.0 ** 21], dtype=torch.float64, device="cuda")
+    nd = 5
+    Dp = torch.zeros((32, d.ld), dtype=torch.bfloat16, device="cuda")
+    _lib.call("sglm_digit_planes", Md.data_ptr(), d.ld, Yd.data_ptr(), s.N, s.N, pr.data_ptr(),
+              pm.data_ptr(), sc.data_ptr(), 3, nd, Dp.data_ptr(), d.ld, 0)
+    got = Dp.float().cpu().numpy()
+    for i, (r, m) in enumerate(((0, 1), (1, 0), (1, 1))):
+        v = np.rint(M[m, : s.N].astype(np.float64) * Y[r] * float(sc[i])).astype(np.int64)
+        for q in range(nd):
+            dq = np.mod(v + 128, 256) - 128
+            assert np.array_equal(got[q * 3 + i, : s.N], dq.astype(np.float32)), (i, q)
+            v = (v - dq) // 256
+        assert np.all(v == 0)
+        assert np.all(got[:, s.N:] == 0)

@@ -18,9 +18,12 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "sabatinilab-glm_amd")]
 VARIANTS = {
     "eta": [("dir", {"SGLM_ETA_DIR": "1"}), ("group", {"SGLM_ETA_DIR": "0"})],
     "eta3": [("staged", {"SGLM_ETA_EXACT_STAGED": "1"}), ("group", {"SGLM_ETA_EXACT_STAGED": "0"})],
-    "xtr": [("ngw2", {"SGLM_XTR4": "1", "SGLM_XTR_NGW": "2"}),
-            ("ngw1", {"SGLM_XTR4": "1", "SGLM_XTR_NGW": "1"}),
-            ("panel1", {"SGLM_XTR4": "0", "SGLM_XTR_NGW": "1"})],
+    "xtr": [("ngw2", {"SGLM_XTR4": "1", "SGLM_XTR_NGW": "2", "SGLM_XTR_PIPE": "0"}),
+            ("pipe2", {"SGLM_XTR4": "1", "SGLM_XTR_NGW": "2", "SGLM_XTR_PIPE": "1"}),
+            ("ngw1", {"SGLM_XTR4": "1", "SGLM_XTR_NGW": "1", "SGLM_XTR_PIPE": "0"}),
+            ("pipe1", {"SGLM_XTR4": "1", "SGLM_XTR_NGW": "1", "SGLM_XTR_PIPE": "1"}),
+            ("wpe2", {"SGLM_XTR4": "1", "SGLM_XTR_NGW": "3", "SGLM_XTR_PIPE": "0"}),
+            ("pipe_wpe2", {"SGLM_XTR4": "1", "SGLM_XTR_NGW": "3", "SGLM_XTR_PIPE": "1"})],
 }
 
 
