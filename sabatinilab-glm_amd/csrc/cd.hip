@@ -371,6 +371,161 @@ __global__ void __launch_bounds__(kCDT) enet_cd_reg_kernel(
     }
 }
 
+// Lane-parallel decisions (enet_cd_lane_kernel): thread t owns coordinates k = t + NT r
+// (r < RR) and holds their running gradients hv for all FPW fits of the workgroup; the FPW
+// decisions of coordinate j run on FPW lanes of the owner's wave at once (lane i = fit i,
+// the owner's hv[i] brought over by v_readlane) instead of one after another on the owner
+// thread, the divisions overlapping.  The coefficients w live in dynamic LDS ([FPW][p], only
+// the deciding lane touches them), Q rows are prefetched D coordinates ahead in a register
+// ring, and consecutive workgroups (fits of one Q and one alpha: equal sweep counts, equal
+// pace) are placed on one XCD, so a Q row fetched for one of them is an L2 hit for the others.
+// Per coordinate the arithmetic and the fold order are enet_cd_reg_kernel's: the coefficients
+// are the same bit for bit.
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), l);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+template <int FPW, int NT, int RR, int D>
+__global__ void __launch_bounds__(NT) enet_cd_lane_kernel(
+    const double* __restrict__ Qall, int32_t p, const int32_t* __restrict__ wg_fits,
+    const int32_t* __restrict__ wg_q, const double* __restrict__ qv,
+    const double* __restrict__ l1v, const double* __restrict__ l2v, int32_t max_sweeps,
+    double tol, double* __restrict__ wout, int32_t* __restrict__ sweeps_out, int32_t nwg) {
+    static_assert(NT % D == 0 && FPW <= 64, "ring tiles the owner loop; one wave of deciders");
+    extern __shared__ double s_w[];                   // [FPW][p] coefficients
+    __shared__ double s_d[2][FPW];
+    __shared__ double s_red[2][FPW][NT / 64];
+    __shared__ int s_act[FPW];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int L = xcd_logical(blockIdx.x, nwg);
+    const double* Q = Qall + (int64_t)wg_q[L] * p * p;
+    const int* fits = wg_fits + (int64_t)L * FPW;
+    // decision lane constants (lane i < FPW of every wave decides fit i)
+    const bool dl = lane < FPW;
+    const int fl = fits[dl ? lane : 0];
+    const double l1 = (dl && fl >= 0) ? l1v[fl] : 0.0;
+    const double l2 = (dl && fl >= 0) ? l2v[fl] : 0.0;
+    bool act = dl && fl >= 0;
+    int sw_done = max_sweeps;
+    double hv[FPW][RR], qdg[RR], qb[D][RR];
+#pragma unroll
+    for (int r = 0; r < RR; ++r) {
+        const int k = tid + r * NT;
+        const bool ok = k < p;
+        qdg[r] = ok ? Q[(int64_t)k * p + k] : 0.0;
+#pragma unroll
+        for (int i = 0; i < FPW; ++i) {
+            const int f = fits[i];
+            hv[i][r] = (ok && f >= 0) ? -qv[(int64_t)f * p + k] : 0.0;
+            if (ok) s_w[i * p + k] = 0.0;
+        }
+    }
+    __syncthreads();
+    for (int sweep = 0; sweep < max_sweeps; ++sweep) {
+        if (!__syncthreads_or(act ? 1 : 0)) break;
+        double mdw = 0.0, mw = 0.0;
+#pragma unroll
+        for (int u = 0; u < D; ++u)                           // rows 0 .. D-1
+#pragma unroll
+            for (int r = 0; r < RR; ++r) {
+                const int k = tid + r * NT;
+                qb[u][r] = (u < p && k < p) ? Q[(int64_t)u * p + k] : 0.0;
+            }
+#pragma unroll
+        for (int rr = 0; rr < RR; ++rr) {                     // owner register of coordinate j
+            if (rr * NT >= p) break;                          // uniform
+            for (int t0 = 0; t0 < NT; t0 += D) {
+                if (t0 + rr * NT >= p) break;                 // uniform
+#pragma unroll
+                for (int u = 0; u < D; ++u) {
+                    const int t = t0 + u;
+                    const int j = t + rr * NT;
+                    if (j >= p) break;                        // uniform
+                    double qc[RR];
+#pragma unroll
+                    for (int r = 0; r < RR; ++r) qc[r] = qb[u][r];
+                    if (j + D < p) {                          // row j + D into the freed slot
+                        const double* Qn = Q + (int64_t)(j + D) * p;
+#pragma unroll
+                        for (int r = 0; r < RR; ++r) {
+                            const int k = tid + r * NT;
+                            if (k < p) qb[u][r] = Qn[k];
+                        }
+                    }
+                    if (wave == (t >> 6)) {                   // the owner's wave decides
+                        const int ol = t & 63;
+                        double h = 0.0;
+#pragma unroll
+                        for (int i = 0; i < FPW; ++i) {
+                            const double x = readlane_d(hv[i][rr], ol);
+                            h = lane == i ? x : h;
+                        }
+                        const double qjj = readlane_d(qdg[rr], ol);
+                        if (dl) {
+                            double d = 0.0;
+                            if (act && qjj > 0.0) {
+                                const double wj = s_w[lane * p + j];
+                                const double rho = -(h - qjj * wj);
+                                const double mag = fabs(rho) - l1;
+                                const double nw = mag > 0.0 ? copysign(mag, rho) / (qjj + l2) : 0.0;
+                                d = nw - wj;
+                                s_w[lane * p + j] = nw;
+                                mdw = fmax(mdw, fabs(d));
+                                mw = fmax(mw, fabs(nw));
+                            }
+                            s_d[j & 1][lane] = d;
+                        }
+                    }
+                    __syncthreads();
+                    double dv[FPW];
+                    bool any = false;
+#pragma unroll
+                    for (int i = 0; i < FPW; ++i) {
+                        dv[i] = s_d[j & 1][i];
+                        any |= dv[i] != 0.0;
+                    }
+                    if (any) {
+#pragma unroll
+                        for (int r = 0; r < RR; ++r)
+#pragma unroll
+                            for (int i = 0; i < FPW; ++i) hv[i][r] = fma(qc[r], dv[i], hv[i][r]);
+                    }
+                }
+            }
+        }
+        // per-fit convergence: the max over the waves' deciding lanes
+        if (dl) {
+            s_red[0][lane][wave] = mdw;
+            s_red[1][lane][wave] = mw;
+        }
+        __syncthreads();
+        if (tid < FPW) {
+            double a = 0.0, b = 0.0;
+            for (int v = 0; v < NT / 64; ++v) {
+                a = fmax(a, s_red[0][tid][v]);
+                b = fmax(b, s_red[1][tid][v]);
+            }
+            s_act[tid] = !(b == 0.0 || a <= tol * b);
+        }
+        __syncthreads();
+        if (dl) {
+            if (act && !s_act[lane]) sw_done = sweep + 1;
+            act = act && s_act[lane];
+        }
+    }
+    __syncthreads();
+    if (tid < FPW && fl >= 0) sweeps_out[fl] = sw_done;
+#pragma unroll
+    for (int i = 0; i < FPW; ++i) {
+        const int f = fits[i];
+        if (f < 0) continue;
+        for (int k = tid; k < p; k += NT) wout[(int64_t)f * p + k] = s_w[i * p + k];
+    }
+}
+
 template <int FPW>
 static int launch_cd_multi(const double* Q, int32_t p, const int32_t* wg_fits, int32_t nwg,
                            const int32_t* wg_q, const double* q, const double* l1,
@@ -392,8 +547,15 @@ static int launch_cd_multi(const double* Q, int32_t p, const int32_t* wg_fits, i
 using namespace sglm;
 
 // fits per workgroup that the LDS holds ((2 fpw + 1) x p doubles within 160 KiB; 1 if none)
+// SGLM_CD_FPW (read per call): 8 (default) = enet_cd_lane_kernel (eight fits per 512-thread
+// workgroup), 4 = enet_cd_reg_kernel (four fits, 256 threads)
+static int cd_reg_fpw() {
+    const char* e = getenv("SGLM_CD_FPW");
+    return (e && e[0] == '4') ? 4 : 8;
+}
+
 extern "C" int32_t sglm_enet_cd_fits_per_wg(int32_t p) {
-    if (p <= kCDT * kRegRows) return 4;              // register-resident form
+    if (p <= kCDT * kRegRows) return cd_reg_fpw();   // register-resident forms
     const int64_t row = (int64_t)p * sizeof(double);
     for (int f : {8, 4, 2})
         if ((2 * f + 1) * row <= 160 * 1024 - 1024) return f;
@@ -412,6 +574,18 @@ extern "C" int sglm_enet_cd_grouped(const double* Q, int32_t p, const int32_t* w
         return SGLM_EINVAL;
     }
     hipStream_t s = as_stream(stream);
+    if (p <= kCDT * kRegRows && fpw == 8) {          // register-resident, lane decisions
+        const size_t lds = (size_t)8 * p * sizeof(double);
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&enet_cd_lane_kernel<8, 512, 4, 2>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+            hipSuccess) {
+            set_error("enet_cd_lane_kernel: %zu bytes of LDS refused", lds);
+            return SGLM_EHIP;
+        }
+        enet_cd_lane_kernel<8, 512, 4, 2><<<nwg, 512, lds, s>>>(Q, p, wg_fits, wg_q, q, l1, l2,
+                                                                max_sweeps, tol, w, sweeps, nwg);
+        return check_launch("enet_cd_lane_kernel");
+    }
     if (p <= kCDT * kRegRows && fpw >= 4) {          // register-resident form
         enet_cd_reg_kernel<4><<<nwg, kCDT, 0, s>>>(Q, p, wg_fits, wg_q, q, l1, l2, max_sweeps,
                                                    tol, w, sweeps);

@@ -96,6 +96,12 @@ __device__ __forceinline__ int frag_bit_source(int t) {
     return 8 * (tt >> 2) + 2 * (tt & 3) + (t >> 4);
 }
 
+// logical block id whose consecutive values share an XCD (blocks b and b + 8 do)
+__device__ __forceinline__ int xcd_logical(int w, int nwg) {
+    const int q = nwg / 8, r = nwg % 8, x = w % 8, l = w / 8;
+    return x < r ? x * (q + 1) + l : r * (q + 1) + (x - r) * q + l;
+}
+
 // bf16 2.0/0 fragment (8 elements of chunk q = 2*ks + h) from a 64-element word pair
 __device__ __forceinline__ bf16x8 frag_two(u32x2 w, int ks, int h) {
     const uint32_t word = ks < 2 ? w.x : w.y;

@@ -411,11 +411,6 @@ __device__ __forceinline__ void mmaX(const StepX& t, int h, f32x16 (&ah)[kXT],
     }
 }
 
-// logical block id whose consecutive values share an XCD (blocks b and b + 8 do)
-__device__ __forceinline__ int xcd_logical(int w, int nwg) {
-    const int q = nwg / 8, r = nwg % 8, x = w % 8, l = w / 8;
-    return x < r ? x * (q + 1) + l : r * (q + 1) + (x - r) * q + l;
-}
 
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 xtr_bits_kernel(const u32x2* __restrict__ cbits, int64_t ld, int32_t P, int64_t nblk,

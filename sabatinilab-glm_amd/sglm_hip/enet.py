@@ -256,9 +256,14 @@ def solve(prob: E.Problem, grams: SharedGrams, fits: Sequence[dict], c: torch.Te
         ev[0].record()
     if fpw >= 2:
         # fits sharing a Q go to the same workgroups, fpw at a time (padding slots -1)
+        # within a Q, fits of equal alpha (other responses) share workgroups: a workgroup
+        # sweeps until its last fit converges, and equal penalties converge alike (the
+        # near-empty large-alpha fits take one sweep instead of riding along with dense ones)
         wg_f, wg_q = [], []
+        alph = np.array([float(f["alpha"]) for f in fits])
         for qv_ in np.unique(qidx):
             fs = np.flatnonzero(qidx == qv_)
+            fs = fs[np.lexsort((fs, alph[fs]))]
             for c0 in range(0, fs.size, fpw):
                 chunk = np.full(fpw, -1, dtype=np.int32)
                 chunk[: min(fpw, fs.size - c0)] = fs[c0:c0 + fpw]

@@ -397,3 +397,29 @@ def test_hessian_reuse_keeps_the_fixed_point(engine, monkeypatch):
     for j in (0, 12):
         c, b0 = glm_ref.fit_tweedie_newton(X, s.y, float(lams[j]), 1.0)
         assert rel(fast[j]["refit_coef"], c) < TOL_POIS
+
+
+def test_enet_cd_lane_kernel_equals_reg_kernel(engine, monkeypatch):
+    """The lane-decision CD kernel (eight fits per 512-thread workgroup, SGLM_CD_FPW=8, the
+    default) and the four-fit register kernel (SGLM_CD_FPW=4) perform the same arithmetic per
+    coordinate in the same order: the coefficients agree bit for bit (p = 500, 4 responses x 5
+    alphas x 3 splits + refit = 80 fits, a ragged last workgroup)."""
+    from sglm_hip import enet, synth
+    s = synth.make(N=20_000, m=50, L=5, family="gaussian", rho=0.05, seed=8, beta_scale=0.3)
+    X = s.dense_X()
+    rng = np.random.default_rng(9)
+    Y = np.stack([s.y + rng.normal(0, 1, s.N) for _ in range(4)], 1)
+    np.random.seed(4)
+    cv_idx = folds_ref.cv_idx_from_bucket_ids(folds_ref.trial_bucket_codes([s.trial]), num_folds=3)
+    alphas = [1e-4, 1e-3, 1e-2, 1e-1, 1.0]
+    outs = {}
+    for fpw in ("4", "8"):
+        monkeypatch.setenv("SGLM_CD_FPW", fpw)
+        st = {}
+        outs[fpw] = enet.cv_enet_path(X, Y, cv_idx, alphas, l1_ratio=0.5, stats=st)
+    for r in range(4):
+        for j in range(len(alphas)):
+            a, b = outs["4"][r][j], outs["8"][r][j]
+            assert np.array_equal(a["cv_coefs"], b["cv_coefs"]), (r, j)
+            assert np.array_equal(a["refit_coef"], b["refit_coef"]), (r, j)
+            assert a["n_iter"] == b["n_iter"] and a["converged"] and b["converged"]
