@@ -595,15 +595,53 @@ __device__ __forceinline__ void gram6_loop(f32x16 (&acc)[4][4], const Addr6& ad,
     }
 }
 
+// XCD-banded placement of the Gram's 128-blocks (SGLM_SYRK_XCD): the nb block rows are cut
+// into four bands of bs = nb / 4 and the ten band pairs (I <= J) dealt to the eight XCDs --
+// six off-diagonal pairs one each, the four diagonal pairs two by two -- so an XCD's blocks
+// read the bit-plane strips of two bands (8 of the 16 at P = 2048) instead of nearly all of
+// them, and its L2 serves each strip to every block that reads it.  Blocks are dealt
+// round-robin to the XCDs (b % 8; placement only, not correctness); block b = 8 k + x is item
+// k of XCD x's list [(slot, split) major][unit]; past the list's end it returns at once.
+__device__ __forceinline__ int xcd_band_units(int x, int bs) {
+    return x < 6 ? bs * bs : bs * (bs + 1);
+}
+__device__ __forceinline__ bool xcd_band_unit(int b, int nb, int nact, int splits, int& slot,
+                                              int& split, int& bi, int& bj) {
+    const int x = b & 7, k = b >> 3, bs = nb / 4;
+    const int u = xcd_band_units(x, bs);
+    if (k >= u * nact * splits) return false;
+    const int pair = k / u, ui = k % u;
+    slot = pair / splits;
+    split = pair % splits;
+    if (x < 6) {
+        const int I = x < 3 ? 0 : (x < 5 ? 1 : 2);
+        const int J = x < 3 ? x + 1 : (x < 5 ? x - 1 : 3);
+        bi = I * bs + ui / bs;
+        bj = J * bs + ui % bs;
+    } else {
+        const int tri = bs * (bs + 1) / 2;
+        const int D = (x - 6) * 2 + (ui >= tri ? 1 : 0);
+        int ti, tj;
+        tile_coords(ui >= tri ? ui - tri : ui, bs, ti, tj);
+        bi = D * bs + ti;
+        bj = D * bs + tj;
+    }
+    return true;
+}
+
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 syrk6_kernel(const int64_t* __restrict__ desc, int32_t P, int32_t splits,
              const int32_t* __restrict__ fits, int32_t nunits, float* __restrict__ H,
-             float* __restrict__ slab, int32_t nact) {
-    const int unit = blockIdx.x % nunits;
-    const int slot = blockIdx.x / nunits;
-    const int split = blockIdx.y;
-    int bi, bj;
-    tile_coords(unit, P / 128, bi, bj);
+             float* __restrict__ slab, int32_t nact, int32_t xmap) {
+    int slot, split, bi, bj;
+    if (xmap) {
+        if (!xcd_band_unit(blockIdx.x, P / 128, nact, splits, slot, split, bi, bj)) return;
+    } else {
+        const int unit = blockIdx.x % nunits;
+        slot = blockIdx.x / nunits;
+        split = blockIdx.y;
+        tile_coords(unit, P / 128, bi, bj);
+    }
     const int fit = fits[slot];
     const int64_t* dsc = desc + 4 * slot;
     g_uint2* bits = reinterpret_cast<g_uint2*>(dsc[0]);
@@ -854,8 +892,15 @@ extern "C" int sglm_syrk_cbits(const int64_t* desc, int32_t P, const int32_t* fi
     const int nunits = nb * (nb + 1) / 2;
     hipStream_t s = as_stream(stream);
     float* slab = splits > 1 ? (float*)work : nullptr;
-    syrk6_kernel<<<dim3((unsigned)(nunits * nact), (unsigned)splits), 64, 0, s>>>(
-        desc, P, splits, fits, nunits, H, slab, nact);
+    const char* ex = getenv("SGLM_SYRK_XCD");         // read per call (A/B in one process)
+    if (ex && ex[0] == '1' && nb % 4 == 0 && nb >= 4) {
+        const int bs = nb / 4;
+        const unsigned grid = 8u * (unsigned)(bs * (bs + 1) * nact * splits);
+        syrk6_kernel<<<grid, 64, 0, s>>>(desc, P, splits, fits, nunits, H, slab, nact, 1);
+    } else {
+        syrk6_kernel<<<dim3((unsigned)(nunits * nact), (unsigned)splits), 64, 0, s>>>(
+            desc, P, splits, fits, nunits, H, slab, nact, 0);
+    }
     int st = check_launch("syrk6_kernel");
     if (st || splits == 1) return st;
     const int64_t PP = (int64_t)P * P;

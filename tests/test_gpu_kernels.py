@@ -538,6 +538,48 @@ def test_syrk_cbits_compacted_gram(engine, torch_mod):
             assert np.max(np.abs(got - ref[blk])) <= 2e-6 * scale, (splits, k)
 
 
+@pytest.mark.parametrize("L,splits", [(10, 1), (20, 3)])
+def test_syrk_cbits_xcd_banded_placement(engine, torch_mod, monkeypatch, L, splits):
+    """SGLM_SYRK_XCD=1 (128-blocks dealt to the XCDs by band pairs) computes every block with
+    the same K slabs as the default placement: the Grams are equal bit for bit (P = 512 and
+    1024, 1 and 3 row slabs, 3 fits)."""
+    torch = torch_mod
+    from sglm_hip import _lib, synth
+    s = synth.make(N=20000, m=50, L=L, rho=0.05, seed=L)
+    d = engine.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
+    assert (d.P // 128) % 4 == 0
+    rng = np.random.default_rng(L)
+    masks = [np.ones(s.N, np.uint8), (rng.random(s.N) < 0.5).astype(np.uint8),
+             np.repeat(rng.random(200) >= 0.3, 100).astype(np.uint8)]
+    prob = engine.Problem(d, [s.y], masks)
+    B = len(masks)
+    W = torch.zeros((B, d.ld), dtype=torch.float32, device="cuda")
+    for k in range(B):
+        W[k, : s.N] = torch.from_numpy(masks[k] * (0.1 + rng.random(s.N)).astype(np.float32))
+    fits = torch.arange(B, dtype=torch.int32, device="cuda")
+    cbs = [prob.compact(k) for k in range(B)]
+    nr_max = max(c[1] for c in cbs)
+    stride = max(64, (nr_max + 63) // 64 * 64)
+    wc = torch.zeros(B * stride, dtype=torch.bfloat16, device="cuda")
+    desc = torch.tensor([[c[0].data_ptr(), c[1], wc.data_ptr() + 2 * k * stride,
+                          0 if c[2] is None else c[2].data_ptr()] for k, c in enumerate(cbs)],
+                        dtype=torch.int64).cuda()
+    _lib.call("sglm_gather_w", W.data_ptr(), d.ld, fits.data_ptr(), B, desc.data_ptr(), nr_max, 0)
+    wk = torch.empty(max(_lib.query("sglm_syrk_work_bytes", d.P, B, splits), 16),
+                     dtype=torch.uint8, device="cuda")
+    blk = np.triu(np.ones((d.P, d.P), dtype=bool))
+    out = {}
+    for xm in ("0", "1"):
+        monkeypatch.setenv("SGLM_SYRK_XCD", xm)
+        H = torch.full((B, d.P, d.P), float("nan"), dtype=torch.float32, device="cuda")
+        _lib.call("sglm_syrk_cbits", desc.data_ptr(), d.P, fits.data_ptr(), B, splits,
+                  H.data_ptr(), wk.data_ptr(), 0)
+        out[xm] = H.cpu().numpy()
+    for k in range(B):
+        assert np.all(np.isfinite(out["1"][k][blk])), k
+        assert np.array_equal(out["0"][k][blk], out["1"][k][blk]), k
+
+
 def test_eta_bits_matches_float64(engine, torch_mod):
     """MFMA eta over row-major bit-planes (beta split in 3 bf16 pieces) == X @ beta to f32
     accuracy, for every row incl. padding (0), with a ragged fit count (B = 37)."""
