@@ -205,8 +205,11 @@ def bench_c5(a):
     import torch.distributed as dist
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
+    # the responses resident in HBM before the timed region, like the design (the host copy
+    # stays for the CPU baseline)
+    Yd = torch.from_numpy(Y).cuda()
     for _ in range(a.warmup):
-        enet.cv_enet_path(design, Y, cv_idx, alphas, l1_ratio=0.5)
+        enet.cv_enet_path(design, Yd, cv_idx, alphas, l1_ratio=0.5)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -214,7 +217,7 @@ def bench_c5(a):
     cd_ms = cd_flop = 0.0
     for _ in range(a.steps):
         st = {"record": True}
-        out = enet.cv_enet_path(design, Y, cv_idx, alphas, l1_ratio=0.5, stats=st)
+        out = enet.cv_enet_path(design, Yd, cv_idx, alphas, l1_ratio=0.5, stats=st)
         cd_ms += st.pop("cd_ms")
         cd_flop += st.pop("cd_flop")
         st.pop("record")

@@ -320,6 +320,60 @@ def _test_is_complement(prob: E.Problem, K: int, full: int) -> bool:
     return bool(((tr + te) == M[full].to(torch.int16)[None, :]).all())
 
 
+def _assemble(w, b, sw, conv, ss, yyh, cnt, c_pm, R: int, A: int, K: int,
+              score_method: str):
+    """Per (response, alpha) result dicts from the flat fit arrays, fits ordered (r, j, k) with
+    k = 0..K-1 the splits and k = K the refit (cv_enet_path's order); vectorised over all
+    (r, j, k).  ss[f] = [train, test] residual sums of squares of split fit f, yyh[m, r] =
+    sum over mask m of y_r^2, cnt[m] = rows of mask m (train 2k, test 2k+1), c_pm[r, m] =
+    sum over mask m of y_r.  Scores as backend/sglm_cv.py:133-170: r2 = 1 - SS_res / SS_tot
+    per split, mse = -SS_res / n; the pooled cv_R2 / cv_mse over the test rows of all splits."""
+    p = w.shape[1]
+    W5 = w.reshape(R, A, K + 1, p)
+    B3 = b.reshape(R, A, K + 1)
+    SW = np.asarray(sw).reshape(R, A, K + 1)
+    CV = np.asarray(conv).reshape(R, A, K + 1)
+    SS = np.asarray(ss).reshape(R, A, K + 1, 2)[:, :, :K, :]
+    scores, sst_side, nm_side = [], [], []
+    for side in (0, 1):
+        mt = 2 * np.arange(K) + side
+        nm = cnt[mt]                                               # [K]
+        with np.errstate(divide="ignore", invalid="ignore"):
+            ym = np.where(nm > 0, c_pm[:, mt] / np.where(nm > 0, nm, 1.0), 0.0)   # [R, K]
+            sst = np.maximum(yyh[mt, :].T - nm * ym * ym, 0.0)     # [R, K]
+            sres = SS[..., side]                                   # [R, A, K]
+            if score_method == "r2":
+                sc = np.where(sst[:, None, :] == 0, np.where(sres == 0, 1.0, 0.0),
+                              1.0 - sres / sst[:, None, :])
+            else:
+                sc = -sres / nm
+            sc = np.where(nm > 0, sc, np.nan)
+        scores.append(sc)
+        sst_side.append(sst)
+        nm_side.append(nm)
+    ss_res = SS[..., 1].sum(2)                                     # [R, A]
+    ss_tot = sst_side[1].sum(1)                                    # [R]
+    n_te = float(nm_side[1].sum())
+    out = []
+    for r in range(R):
+        per = []
+        for j in range(A):
+            s_tr, s_te = scores[0][r, j], scores[1][r, j]
+            sr, st = float(ss_res[r, j]), float(ss_tot[r])
+            per.append({
+                "cv_coefs": W5[r, j, :K].T.copy(), "cv_intercepts": B3[r, j, :K].copy(),
+                "cv_scores_train": s_tr, "cv_scores_test": s_te,
+                "cv_mean_score_train": np.mean(s_tr), "cv_mean_score": np.mean(s_te),
+                "cv_std_score": np.std(s_te),
+                "cv_R2_score": 0 if st == 0 else 1 - sr / st,
+                "cv_mse_score": sr / n_te if n_te else np.nan,
+                "refit_coef": W5[r, j, K].copy(), "refit_intercept": float(B3[r, j, K]),
+                "n_iter": [int(v) for v in SW[r, j]], "converged": bool(CV[r, j].all()),
+            })
+        out.append(per)
+    return out
+
+
 def cv_enet_path(X, Y, cv_idx, alphas: Sequence[float], l1_ratio: float = 0.5,
                  fit_intercept: bool = True, max_iter: int = 1000, score_method: str = "mse",
                  stats: Optional[dict] = None, shard: bool = True):
@@ -331,7 +385,8 @@ def cv_enet_path(X, Y, cv_idx, alphas: Sequence[float], l1_ratio: float = 0.5,
     With torch.distributed initialised the responses are dealt round-robin over the ranks
     (each rank forms the shared Grams of the masks itself) and the per-response results are
     all-gathered once (no data-path collective)."""
-    Y = np.asarray(Y, dtype=np.float64)
+    # Y: host (n x R) float64, or a device tensor (kept resident: no upload per call)
+    Y = Y.to(torch.float64) if torch.is_tensor(Y) else np.asarray(Y, dtype=np.float64)
     if Y.ndim == 1:
         Y = Y[:, None]
     from .grid import _dist
@@ -436,50 +491,8 @@ def cv_enet_path(X, Y, cv_idx, alphas: Sequence[float], l1_ratio: float = 0.5,
                   E._p(betad), E._p(c), E._p(ints[nq:]), E._p(yyd), E._p(ssd), E._p(work),
                   E._stream())
         ss[qf, np.concatenate(q_side)] = ssd.cpu().numpy()
-    kpos = {key: i for i, key in enumerate(keys)}
-    out = []
-    for r in range(R):
-        per = []
-        for j in range(A):
-            cv_coefs = np.zeros((p, K))
-            cv_b = np.zeros(K)
-            s_tr, s_te = np.zeros(K), np.zeros(K)
-            ss_res = ss_tot = n_te = 0.0
-            n_iter, conv_all, refit = [], True, None
-            for k in list(range(K)) + [-1]:
-                i = kpos[(r, j, k)]
-                n_iter.append(int(sw[i]))
-                conv_all &= bool(conv[i])
-                if k < 0:
-                    refit = (w[i].copy(), float(b[i]))
-                    continue
-                cv_coefs[:, k], cv_b[k] = w[i], b[i]
-                for side, mt, dst in ((0, 2 * k, s_tr), (1, 2 * k + 1, s_te)):
-                    sres = float(ss[i, side])
-                    nm = cnt[mt]
-                    ym = float(c_p[ci[(r, mt)]]) / nm if nm else 0.0
-                    sst = max(yyh[mt, r] - nm * ym * ym, 0.0)
-                    if nm == 0:
-                        dst[k] = np.nan
-                    elif score_method == "r2":
-                        dst[k] = (1.0 if sres == 0 else 0.0) if sst == 0 else 1.0 - sres / sst
-                    else:
-                        dst[k] = -sres / nm
-                    if mt == 2 * k + 1:
-                        ss_res += sres
-                        ss_tot += sst
-                        n_te += nm
-            per.append({
-                "cv_coefs": cv_coefs, "cv_intercepts": cv_b,
-                "cv_scores_train": s_tr, "cv_scores_test": s_te,
-                "cv_mean_score_train": np.mean(s_tr), "cv_mean_score": np.mean(s_te),
-                "cv_std_score": np.std(s_te),
-                "cv_R2_score": 0 if ss_tot == 0 else 1 - ss_res / ss_tot,
-                "cv_mse_score": ss_res / n_te if n_te else np.nan,
-                "refit_coef": refit[0], "refit_intercept": refit[1],
-                "n_iter": n_iter, "converged": conv_all,
-            })
-        out.append(per)
+    c_pm = np.array([[float(c_p[ci[(r, m)]]) for m in range(len(masks))] for r in range(R)])
+    out = _assemble(w, b, sw, conv, ss, yyh, cnt, c_pm, R, A, K, score_method)
     if stats is not None:
         stats.update({"fits": len(fits), "grams": len(masks), "grams_formed": n_formed,
                       "xty_columns": len(pairs),

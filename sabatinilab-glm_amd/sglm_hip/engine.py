@@ -598,6 +598,20 @@ def host_masks(specs, n: int, ld: int, out: Optional[np.ndarray] = None):
     return (nnz, sums, out[: nm * ld].reshape(nm, ld)) if ret else (nnz, sums)
 
 
+class _LazyHost:
+    """Host (numpy) view of a device array, copied on first access."""
+
+    def __init__(self, t):
+        self.t = t
+        self._a = None
+        self.shape = tuple(t.shape)
+
+    def __getitem__(self, idx):
+        if self._a is None:
+            self._a = self.t.cpu().numpy()
+        return self._a[idx]
+
+
 class _Columns:
     """Read-only list view of the columns of an (n x R) array (host copies on access)."""
 
@@ -631,7 +645,17 @@ class Problem:
         self._y64r = None
         self._rolled = None
         self.Yd64 = None
-        if isinstance(ys, np.ndarray) and ys.ndim == 2:
+        if isinstance(ys, torch.Tensor) and ys.ndim == 2:
+            # device-resident responses (n x R float64 on the design's device): no upload
+            if ys.shape[0] != n:
+                raise ValueError(f"response length {ys.shape[0]} != n_samples {n}")
+            if ys.device != torch.device(dev) and str(ys.device) != str(dev):
+                ys = ys.to(dev)
+            self.Yd64 = ys.to(torch.float64).contiguous()
+            self.ys = _Columns(_LazyHost(self.Yd64))
+            self.Y = torch.zeros((ys.shape[1], ld), dtype=torch.float32, device=dev)
+            self.Y[:, :n] = self.Yd64.t().float()
+        elif isinstance(ys, np.ndarray) and ys.ndim == 2:
             if ys.shape[0] != n:
                 raise ValueError(f"response length {ys.shape[0]} != n_samples {n}")
             self.ys = _Columns(ys)
