@@ -760,6 +760,7 @@ def main():
     ktime = sum(e0.elapsed_time(e1) for e0, e1, _, _ in stats.syrk_events) / 1e3
     kflop = sum(nact_flop for _, _, _, nact_flop in stats.syrk_events)
     nlaunch = len(stats.syrk_events)
+    alg_bytes = float(np.mean(stats.syrk_bytes)) if stats.syrk_bytes else None
     t = torch.tensor([elapsed, float(stats.fit_iters), ktime, kflop, float(nlaunch),
                       float(stats.gram_fits), stats.alg_flop, float(stats.reused),
                       float(stats.gram_fit_iters), float(stats.stops["stagnation"]),
@@ -879,6 +880,11 @@ def main():
                 "frac": achieved / PEAK_BF16_TFLOPS,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
+                # PMC bytes over the launch's algorithmic bytes (each compacted design once,
+                # the bf16 weights, the upper-triangle f32 output): > 1 = re-read / slab bytes
+                "algorithmic_bytes_per_launch": alg_bytes,
+                "traffic_over_algorithmic": (traffic / alg_bytes) if (traffic and alg_bytes)
+                                            else None,
                 "launches": nlaunch,
                 "avg_launch_ms": ktime / max(nlaunch, 1) * 1e3,
             },

@@ -904,6 +904,7 @@ class IrlsStats:
     """Optional instrumentation: per-launch events of the Gram kernel (bench.py)."""
     record: bool = False
     syrk_events: list = field(default_factory=list)    # (start, end, algorithmic flop)
+    syrk_bytes: list = field(default_factory=list)     # algorithmic HBM bytes per Gram launch
     fit_iters: int = 0
     newton_iters: int = 0
     gram_fits: int = 0                                  # distinct Hessians formed
@@ -2155,6 +2156,7 @@ def irls_scored(prob: Problem, reqs: List[FitReq], sets: np.ndarray,
             sums[i] = sg_sums[q]
         if stats is not None and sg is not None:
             stats.syrk_events += sg.syrk_events
+            stats.syrk_bytes += sg.syrk_bytes
             stats.fit_iters += sg.fit_iters
             stats.gram_fits += sg.gram_fits
             stats.gram_fit_iters += sg.gram_fit_iters
@@ -2300,7 +2302,9 @@ def _syrk(d: Design, bf, fits: np.ndarray, nsteps: int, ntile1: int, stats, st, 
     if stats is not None and stats.record:
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     if use_cb:
-        _syrk_cbits(d, bf, prob, fits, st, ev)
+        ab = _syrk_cbits(d, bf, prob, fits, st, ev)
+        if ev is not None:
+            stats.syrk_bytes.append(ab)
     else:
         if ev is not None:
             ev[0].record()
@@ -2369,6 +2373,11 @@ def _syrk_cbits(d: Design, bf, prob: Problem, fits: np.ndarray, st, ev=None):
             ev[1].record()
         _gram_done()
     bf.keep = (desc_d, fits_d)          # alive until the next launch is enqueued
+    # algorithmic bytes of the launch: each distinct compacted design once (rows/64 K-steps x P
+    # predictors x 8 B), each slot's bf16 weights, each slot's upper 128-block triangle (f32)
+    planes = {int(c[0].data_ptr()): int(c[1]) for c in cbs}
+    return (sum((r + 63) // 64 * d.P * 8 for r in planes.values())
+            + sum(2 * int(c[1]) for c in cbs) + nact * nb * (nb + 1) // 2 * 128 * 128 * 4)
 
 
 def score_sums(prob: Problem, family: int, power: float, eta, fit_resp: Sequence[int],
