@@ -214,64 +214,82 @@ def solve(prob: E.Problem, grams: SharedGrams, fits: Sequence[dict], c: torch.Te
     """ElasticNet per fit dict {mask, alpha, l1_ratio, fit_intercept, max_iter} with
     c[cidx[f]] = X^T(m y) of its (response, mask).  Returns (w [B][p] f64, b [B] f64,
     sweeps [B] int, converged [B] bool) as host arrays."""
+    p = prob.design.p
+    if len(fits) == 0:
+        return np.zeros((0, p)), np.zeros(0), np.zeros(0, int), np.zeros(0, bool)
+    w, b, sw, conv = solve_arrays(
+        prob, grams, np.array([int(f["mask"]) for f in fits]),
+        np.array([float(f["alpha"]) for f in fits]), np.array([float(f["l1_ratio"]) for f in fits]),
+        np.array([bool(f["fit_intercept"]) for f in fits]),
+        max(int(f["max_iter"]) for f in fits), c, np.asarray(cidx), stats)
+    return w.cpu().numpy(), b.cpu().numpy(), sw, conv
+
+
+def solve_arrays(prob: E.Problem, grams: SharedGrams, masks: np.ndarray, alpha: np.ndarray,
+                 l1_ratio: np.ndarray, fit_intercept: np.ndarray, max_iter: int,
+                 c: torch.Tensor, cidx: np.ndarray, stats: Optional[dict] = None):
+    """solve() on per-fit arrays; returns (w [B][p], b [B]) as float64 DEVICE tensors and
+    (sweeps, converged) as host arrays."""
     d = prob.design
     p, dev = d.p, d.device
-    B = len(fits)
-    if B == 0:
-        return np.zeros((0, p)), np.zeros(0), np.zeros(0, int), np.zeros(0, bool)
-    masks = [int(f["mask"]) for f in fits]
-    grams.ensure(masks)
-    cnt = np.array([float(prob.mask_count(m)) for m in masks])
+    B = int(masks.size)
+    masks = masks.astype(np.int64)
+    grams.ensure(np.unique(masks).tolist())
+    cnt_m = np.array([float(prob.mask_count(m)) for m in range(int(masks.max()) + 1)])
+    cnt = cnt_m[masks]
     q = torch.empty((B, p), dtype=torch.float64, device=dev)
     qidx = np.zeros(B, dtype=np.int32)
     cpv = torch.empty(B, dtype=torch.float64, device=dev)
     gv = torch.zeros((B, p), dtype=torch.float64, device=dev)
     for center in (True, False):
-        sel = [i for i, f in enumerate(fits) if bool(f["fit_intercept"]) == center]
-        if not sel:
+        sel = np.flatnonzero(fit_intercept == center)
+        if not sel.size:
             continue
-        qi = grams.centred([masks[i] for i in sel], center)
-        qidx[sel] = qi
-        sel_t = torch.from_numpy(np.asarray(sel, dtype=np.int64)).to(dev)
-        cc = c[torch.from_numpy(np.asarray(cidx, dtype=np.int64)[sel]).to(dev)]
+        um, inv = np.unique(masks[sel], return_inverse=True)
+        qidx[sel] = np.asarray(grams.centred(um.tolist(), center), dtype=np.int32)[inv]
+        sel_t = torch.from_numpy(sel.astype(np.int64)).to(dev)
+        cc = c[torch.from_numpy(cidx[sel].astype(np.int64)).to(dev)]
         cpv[sel_t] = cc[:, p]
         if center:
-            gslot = torch.from_numpy(np.array([grams.slot[masks[i]] for i in sel],
-                                              dtype=np.int64)).to(dev)
+            gslot = torch.from_numpy(np.array([grams.slot[int(m)] for m in um],
+                                              dtype=np.int64)[inv]).to(dev)
             g = grams.H[:, :p, p][gslot].to(torch.float64)      # X^T m (upper: rows < p)
             n = torch.from_numpy(cnt[sel]).to(dev)
             gv[sel_t] = g
             q[sel_t] = cc[:, :p] - g * (cc[:, p] / n.clamp_min(1))[:, None]
         else:
             q[sel_t] = cc[:, :p]
-    l1 = torch.from_numpy(np.array([f["alpha"] * f["l1_ratio"] for f in fits]) * cnt).to(dev)
-    l2 = torch.from_numpy(np.array([f["alpha"] * (1 - f["l1_ratio"]) for f in fits]) * cnt).to(dev)
+    l1 = torch.from_numpy(alpha * l1_ratio * cnt).to(dev)
+    l2 = torch.from_numpy(alpha * (1 - l1_ratio) * cnt).to(dev)
     w = torch.empty((B, p), dtype=torch.float64, device=dev)
     sw = torch.empty(B, dtype=torch.int32, device=dev)
-    max_sweeps = int(max(max(int(f["max_iter"]) for f in fits), 10000))
+    max_sweeps = int(max(int(max_iter), 10000))
     fpw = int(_lib.query("sglm_enet_cd_fits_per_wg", p))
     rec = stats is not None and stats.get("record")
     if rec:                          # the roofline times the CD kernel alone (bench.py)
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev[0].record()
     if fpw >= 2:
-        # fits sharing a Q go to the same workgroups, fpw at a time (padding slots -1)
+        # fits sharing a Q go to the same workgroups, fpw at a time (padding slots -1);
         # within a Q, fits of equal alpha (other responses) share workgroups: a workgroup
         # sweeps until its last fit converges, and equal penalties converge alike (the
         # near-empty large-alpha fits take one sweep instead of riding along with dense ones)
-        wg_f, wg_q = [], []
-        alph = np.array([float(f["alpha"]) for f in fits])
-        for qv_ in np.unique(qidx):
-            fs = np.flatnonzero(qidx == qv_)
-            fs = fs[np.lexsort((fs, alph[fs]))]
-            for c0 in range(0, fs.size, fpw):
-                chunk = np.full(fpw, -1, dtype=np.int32)
-                chunk[: min(fpw, fs.size - c0)] = fs[c0:c0 + fpw]
-                wg_f.append(chunk)
-                wg_q.append(int(qv_))
-        wgf_d = torch.from_numpy(np.concatenate(wg_f)).to(dev)
-        wgq_d = torch.from_numpy(np.array(wg_q, dtype=np.int32)).to(dev)
-        _lib.call("sglm_enet_cd_grouped", E._p(grams.Qt), p, E._p(wgf_d), len(wg_q), fpw,
+        order = np.lexsort((np.arange(B), alpha, qidx))           # by Q, then alpha, then index
+        qs = qidx[order]
+        starts = np.flatnonzero(np.r_[True, qs[1:] != qs[:-1]])
+        ends = np.r_[starts[1:], B]
+        nwg_q = (ends - starts + fpw - 1) // fpw
+        wgf = np.full((int(nwg_q.sum()), fpw), -1, dtype=np.int32)
+        wgq = np.repeat(qs[starts], nwg_q).astype(np.int32)
+        row = 0
+        for s0, e0, nw in zip(starts, ends, nwg_q):
+            blk = np.full(nw * fpw, -1, dtype=np.int32)
+            blk[: e0 - s0] = order[s0:e0]
+            wgf[row:row + nw] = blk.reshape(nw, fpw)
+            row += nw
+        wgf_d = torch.from_numpy(wgf.reshape(-1)).to(dev)
+        wgq_d = torch.from_numpy(wgq).to(dev)
+        _lib.call("sglm_enet_cd_grouped", E._p(grams.Qt), p, E._p(wgf_d), int(wgq.size), fpw,
                   E._p(wgq_d), E._p(q), E._p(l1), E._p(l2), max_sweeps, CD_TOL, E._p(w),
                   E._p(sw), E._stream())
     else:
@@ -280,7 +298,7 @@ def solve(prob: E.Problem, grams: SharedGrams, fits: Sequence[dict], c: torch.Te
                   E._p(l1), E._p(l2), max_sweeps, CD_TOL, E._p(w), E._p(sw), E._stream())
     if rec:
         ev[1].record()
-    fi = torch.from_numpy(np.array([bool(f["fit_intercept"]) for f in fits])).to(dev)
+    fi = torch.from_numpy(np.asarray(fit_intercept, dtype=bool)).to(dev)
     n = torch.from_numpy(cnt).to(dev)
     b = torch.where(fi & (n > 0), (cpv - (gv * w).sum(1)) / n.clamp_min(1), 0.0)
     swh = sw.cpu().numpy()
@@ -289,11 +307,16 @@ def solve(prob: E.Problem, grams: SharedGrams, fits: Sequence[dict], c: torch.Te
         # Q and updates the running gradient, 2p flop, so 2p^2 per sweep per fit (float64)
         stats["cd_ms"] = stats.get("cd_ms", 0.0) + ev[0].elapsed_time(ev[1])
         stats["cd_flop"] = stats.get("cd_flop", 0.0) + 2.0 * p * p * float(np.sum(swh))
-    return w.cpu().numpy(), b.cpu().numpy(), swh, swh < max_sweeps
+    return w, b, swh, swh < max_sweeps
 
 
 def _mask_sum_y2(prob: E.Problem) -> np.ndarray:
     """[F][R] float64 sum over each mask of m y^2 (sglm_mask_stats with a zero shift)."""
+    return _mask_sum_y2_dev(prob).cpu().numpy()
+
+
+def _mask_sum_y2_dev(prob: E.Problem) -> torch.Tensor:
+    """_mask_sum_y2 as a device tensor."""
     Y = prob.y64_rows()
     F_, R = prob.M.shape[0], Y.shape[0]
     n = prob.design.n
@@ -303,7 +326,7 @@ def _mask_sum_y2(prob: E.Problem) -> np.ndarray:
                        device=Y.device)
     _lib.call("sglm_mask_stats", E._p(prob.M), prob.M.shape[1], F_, E._p(Y), R, n, E._p(K0),
               -1.0, E._p(out), E._p(work), E._stream())
-    return out[:, :, 2].t().cpu().numpy()
+    return out[:, :, 2].t()
 
 
 def _test_is_complement(prob: E.Problem, K: int, full: int) -> bool:
@@ -443,58 +466,50 @@ def cv_enet_path(X, Y, cv_idx, alphas: Sequence[float], l1_ratio: float = 0.5,
         n_formed = len(masks)
         grams.ensure(range(len(masks)))
         c = xty(prob, pairs)
-    ci = {pm: i for i, pm in enumerate(pairs)}
-    fits, keys = [], []
-    for r in range(R):
-        for j, al in enumerate(alphas):
-            for k in list(range(K)) + [-1]:
-                m = FULL if k < 0 else 2 * k
-                fits.append({"mask": m, "alpha": float(al), "l1_ratio": float(l1_ratio),
-                             "fit_intercept": fit_intercept, "max_iter": max_iter})
-                keys.append((r, j, k))
-    w, b, sw, conv = solve(prob, grams, fits, c,
-                           [ci[(r, f["mask"])] for (r, _, _), f in zip(keys, fits)], stats)
+    F_ = len(masks)
+    # fits in (response, alpha, split) order, k = K the refit on the full mask; pairs are
+    # (response, mask) in r-major order, so pair (r, m) sits at r * F_ + m
+    nfit = R * A * (K + 1)
+    rr = np.repeat(np.arange(R), A * (K + 1))
+    jj = np.tile(np.repeat(np.arange(A), K + 1), R)
+    kk = np.tile(np.arange(K + 1), R * A)
+    fmask = np.where(kk == K, FULL, 2 * kk)
+    al = np.asarray(alphas, dtype=np.float64)[jj]
+    w_d, b_d, sw, conv = solve_arrays(prob, grams, fmask, al, np.full(nfit, float(l1_ratio)),
+                                      np.full(nfit, bool(fit_intercept)), int(max_iter), c,
+                                      rr * F_ + fmask, stats)
+    pa = p + 1
+    betad = torch.empty((nfit, pa), dtype=torch.float64, device=dev)
+    betad[:, :p] = w_d
+    betad[:, p] = b_d
+    # the coefficients to the host while the scores run (one pinned staging copy)
+    wb_h = E._pinned("enet_wb", nfit * pa, torch.float64)[: nfit * pa].view(nfit, pa)
+    wb_h.copy_(betad, non_blocking=True)
     # ---- scores from Gram algebra: SS(mask) = y'My - 2 beta'c + beta' G beta (augmented),
-    # sum m y^2 per (mask, response) from the mask-statistics kernel, the rest from
-    # sglm_gram_ss over every (split fit, train / test mask) pair, grouped by mask
-    yyh = _mask_sum_y2(prob)                                     # F x R
-    cnt = np.array([float(prob.mask_count(m)) for m in range(len(masks))])
-    c_p = c[:, p].cpu().numpy()                                  # sum m y per (r, m) pair
-    beta = np.zeros((len(fits), design.P))
-    beta[:, :p] = w
-    beta[:, p] = b
-    betad = torch.from_numpy(beta).to(dev)
-    kk = np.array([k for (_, _, k) in keys])
-    rr = np.array([r for (r, _, _) in keys])
-    q_fit, q_cidx, q_yy, q_side, grp_off, grp_slot = [], [], [], [], [0], []
+    # sum m y^2 per (mask, response) from the mask-statistics kernel, the quadratic forms of
+    # the split fits of one mask as one float64 GEMM against that mask's symmetric Gram
+    yyd = _mask_sum_y2_dev(prob)                                 # F x R (device)
+    cnt = np.array([float(prob.mask_count(m)) for m in range(F_)])
+    ssd = torch.zeros((nfit, 2), dtype=torch.float64, device=dev)
     for k in range(K):
         rows = np.flatnonzero(kk == k)
+        rows_d = torch.from_numpy(rows).to(dev)
+        rr_d = torch.from_numpy(rr[rows]).to(dev)
+        Bk = betad[rows_d]                                       # [nf, pa]
         for side, mt in ((0, 2 * k), (1, 2 * k + 1)):
-            q_fit.append(rows)
-            q_cidx.append(np.array([ci[(r, mt)] for r in rr[rows]]))
-            q_yy.append(yyh[mt, rr[rows]])
-            q_side.append(np.full(rows.size, side))
-            grp_off.append(grp_off[-1] + rows.size)
-            grp_slot.append(grams.slot[mt])
-    ss = np.zeros((len(fits), 2))                                # [train, test] per split fit
-    if grp_slot:
-        qf = np.concatenate(q_fit)
-        ssd = torch.empty(qf.size, dtype=torch.float64, device=dev)
-        work = torch.empty(_lib.query("sglm_gram_ss_work_bytes", p + 1, int(qf.size)),
-                           dtype=torch.uint8, device=dev)
-        ints = torch.from_numpy(np.concatenate([qf, np.concatenate(q_cidx), grp_off, grp_slot])
-                                .astype(np.int32)).to(dev)
-        nq, ng = int(qf.size), len(grp_slot)
-        yyd = torch.from_numpy(np.concatenate(q_yy)).to(dev)
-        _lib.call("sglm_gram_ss", E._p(grams.H), design.P, p + 1, E._p(ints[2 * nq + ng + 1:]),
-                  E._p(ints[2 * nq:]), ng, int(np.max(np.diff(grp_off))), E._p(ints), nq,
-                  E._p(betad), E._p(c), E._p(ints[nq:]), E._p(yyd), E._p(ssd), E._p(work),
-                  E._stream())
-        ss[qf, np.concatenate(q_side)] = ssd.cpu().numpy()
-    c_pm = np.array([[float(c_p[ci[(r, m)]]) for m in range(len(masks))] for r in range(R)])
+            G = grams.sym(mt)[:pa, :pa]
+            quad = ((Bk @ G) * Bk).sum(1)
+            lin = (Bk * c[rr_d * F_ + mt, :pa]).sum(1)
+            ssd[rows_d, side] = (yyd[mt, rr_d] - 2.0 * lin + quad).clamp_min(0.0)
+    yyh = yyd.cpu().numpy()
+    c_pm = c[:, p].cpu().numpy().reshape(R, F_)                  # sum m y per (r, m) pair
+    ss = ssd.cpu().numpy()
+    torch.cuda.current_stream().synchronize()                   # the pinned coefficients
+    wb = wb_h.numpy()
+    w, b = wb[:, :p], wb[:, p]
     out = _assemble(w, b, sw, conv, ss, yyh, cnt, c_pm, R, A, K, score_method)
     if stats is not None:
-        stats.update({"fits": len(fits), "grams": len(masks), "grams_formed": n_formed,
+        stats.update({"fits": nfit, "grams": len(masks), "grams_formed": n_formed,
                       "xty_columns": len(pairs),
                       "cd_sweeps_total": int(np.sum(sw)), "cd_sweeps_max": int(np.max(sw))})
     return out
