@@ -814,6 +814,14 @@ xtr_bits5_kernel(const u32x2* __restrict__ cbits, int64_t ld, int32_t P, int64_t
 // per lane leave room on every SIMD for the factorisation chain's waves (the two-group kernel
 // holds all 512), so a chain running beside the gradient progresses instead of waiting for it.
 static thread_local int t_xtr_prefer = -1;
+// SGLM_XTR_PIPE (read per launch; default 1): the software-pipelined kernel (xtr_bits5_kernel)
+// for the four-panel variants.  Measured on the C4 design, 120 / 70 fits: 1.30 / 1.19 ms
+// (two groups) -> 1.03 / 0.95 pipelined; the two-wave one-group form pipelined 0.99 / 0.72,
+// the fastest of all -- the pipelined default.
+static bool xtr_pipe() {
+    const char* ep = getenv("SGLM_XTR_PIPE");
+    return !(ep && ep[0] == '0');
+}
 static int xtr_variant(int32_t P, int32_t B) {
     const int ngrp = (B + 31) / 32;
     if (P % (32 * kXT * kXW) != 0) return 0;
@@ -826,6 +834,7 @@ static int xtr_variant(int32_t P, int32_t B) {
     if (e && e[0] == '1') return 1;
     if (e && e[0] == '2') return ngrp >= 2 ? 2 : 1;
     if (e && e[0] == '3') return 3;
+    if (xtr_pipe()) return wpe2 ? 3 : 1;
     if (ngrp >= 2 && ngrp % 2 == 0) return 2;
     return wpe2 ? 3 : 0;
 }
@@ -839,8 +848,7 @@ static void launch_xtr_bits(const u32x2* cbits, int64_t ld, int32_t P, int64_t n
     const unsigned wgs4 = (unsigned)((P / (32 * kXT * kXW)) * ((Bp / 32 + ngw - 1) / ngw) *
                                      splits);
     // the pipelined kernel (SGLM_XTR_PIPE, read per launch) takes R's per-lane offsets in 32 bits
-    const char* ep = getenv("SGLM_XTR_PIPE");
-    const bool pipe = v != 0 && ep && ep[0] == '1' && (int64_t)32 * ld * 2 < ((int64_t)1 << 32);
+    const bool pipe = v != 0 && xtr_pipe() && (int64_t)32 * ld * 2 < ((int64_t)1 << 32);
     if (pipe) {
         if (v == 3)
             xtr_bits5_kernel<1, 2><<<wgs4, 64 * kXW, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, B,

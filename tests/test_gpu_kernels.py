@@ -903,6 +903,7 @@ def test_xtr_bits_four_panel_kernel_vs_float64(engine, torch_mod, B, ngw, monkey
     float64 X^T R, ragged fit counts and a half-empty last workgroup (70 fits, two groups)."""
     torch = torch_mod
     monkeypatch.setenv("SGLM_XTR_NGW", ngw)
+    monkeypatch.setenv("SGLM_XTR_PIPE", "0")        # xtr_bits4_kernel first (the reference)
     from sglm_hip import _lib, synth
     s = synth.make(N=40_000, m=50, L=5, rho=0.05, seed=B)
     d = engine.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
@@ -922,17 +923,17 @@ def test_xtr_bits_four_panel_kernel_vs_float64(engine, torch_mod, B, ngw, monkey
     assert np.max(np.abs(G.cpu().numpy() - ref) / np.maximum(scale, 1e-30)) < 2e-6
     # the software-pipelined kernel (xtr_bits5_kernel): the same MFMA sequence per wave, so
     # the same partial sums bit for bit; also on the two-wave one-group variant
-    for pipe_env in ({"SGLM_XTR_PIPE": "1"}, {"SGLM_XTR_PIPE": "1", "SGLM_XTR_NGW": "3"}):
+    for pipe_env in ({"SGLM_XTR_PIPE": "1"}, {"SGLM_XTR_PIPE": "1", "SGLM_XTR_NGW": "3"},
+                     {"SGLM_XTR_PIPE": "1", "SGLM_XTR_NGW": "1"}):
         for k, v in pipe_env.items():
             monkeypatch.setenv(k, v)
         G2 = torch.zeros_like(G)
         _lib.call("sglm_xtr_bits", d.cbits_full().data_ptr(), d.ld, d.P, d.n, Rd.data_ptr(), B,
                   G2.data_ptr(), w.data_ptr(), 0)
-        if pipe_env.get("SGLM_XTR_NGW") == "3":
+        if pipe_env.get("SGLM_XTR_NGW", ngw) != ngw:
             assert np.max(np.abs(G2.cpu().numpy() - ref) / np.maximum(scale, 1e-30)) < 2e-6
         else:
             assert torch.equal(G2, G), pipe_env
-    monkeypatch.delenv("SGLM_XTR_PIPE")
 
 
 @pytest.mark.parametrize("shifts,event_major,row0,slab", [

@@ -24,6 +24,7 @@ VARIANTS = {
             ("pipe1", {"SGLM_XTR4": "1", "SGLM_XTR_NGW": "1", "SGLM_XTR_PIPE": "1"}),
             ("wpe2", {"SGLM_XTR4": "1", "SGLM_XTR_NGW": "3", "SGLM_XTR_PIPE": "0"}),
             ("pipe_wpe2", {"SGLM_XTR4": "1", "SGLM_XTR_NGW": "3", "SGLM_XTR_PIPE": "1"})],
+    "xtrd": [("default", {}), ("pipe0", {"SGLM_XTR_PIPE": "0"})],
 }
 
 
@@ -48,7 +49,7 @@ def main():
                 _lib.call("sglm_gemv_eta_bits", d.rbits.data_ptr(), d.ld, d.P, beta.data_ptr(),
                           B, slots.data_ptr(), int(what == "eta3"), out.data_ptr(),
                           work.data_ptr(), st)
-        else:
+        else:                                   # xtr, xtrd
             Bp = (B + 31) // 32 * 32
             rp = torch.zeros((3, Bp, d.ld), dtype=torch.bfloat16, device="cuda")
             rp[:, :B, :d.n] = torch.from_numpy(
@@ -63,6 +64,8 @@ def main():
         times = {name: [] for name, _ in VARIANTS[what]}
         for rnd in range(6):
             for name, env in VARIANTS[what]:
+                for k in ("SGLM_XTR4", "SGLM_XTR_NGW", "SGLM_XTR_PIPE"):
+                    os.environ.pop(k, None)
                 os.environ.update(env)
                 fn()
                 torch.cuda.synchronize()
