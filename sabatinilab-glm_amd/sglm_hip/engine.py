@@ -114,8 +114,6 @@ CHOL_SPLIT_MIN = int(__import__("os").environ.get("SGLM_CHOL_SPLIT_MIN", "6"))
 # 62.3 / 63.1 / 62.3 ms against 59.7 / 60.2 / 59.3 ms unpipelined, alternating on one box).
 # Default 0.
 GRAM_PIPE = int(__import__("os").environ.get("SGLM_GRAM_PIPE", "0") or 0)
-# first Grams of split fits from the complement (test) mask's counts (see _comp_gram)
-COMP_GRAM = __import__("os").environ.get("SGLM_COMP_GRAM", "1") == "1"
 # Rank decisions of unpenalised fits (float64 factor of the exact mask Gram, sglm_chol64_factor):
 # a pivot whose Schur complement is <= tol * its diagonal is a dependent column.  The Gram of a
 # 0/1 design is exact (integer counts in f32), so tol only has to clear float64 elimination
@@ -915,7 +913,6 @@ class IrlsStats:
     aliased: int = 0            # fit-iterations solved on a family representative's factor
     shared: int = 0             # fit-iterations on a lambda neighbour's Gram (own factor)
     lag_grams: int = 0          # Grams from the event cross-correlations (sglm_lag_gram)
-    comp_grams: int = 0         # first Grams from the complement mask's counts (_comp_gram)
     rank_grams: int = 0         # exact mask Grams for the rank decisions of unpenalised fits
     chain_host_s: float = 0.0   # host time spent enqueueing the factorisation chains
     aa_fit_iters: int = 0       # fit-iterations whose direction took the secant correction
@@ -1306,14 +1303,6 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
     use_lag_gram = (LAG_GRAM and fam == FAM_TWEEDIE_LOG and power == 1.0 and d.lag is not None
                     and getattr(d.lag, "ebits", None) is not None
                     and d.lag.smax - d.lag.smin <= 2048)
-    # first Grams of split fits on a 0/1 mask whose complement is another mask of the problem
-    # (GroupShuffleSplit train / test): at the intercept-only start the weight is one constant
-    # w on the mask, so H = bf16(w) (C_all - C_test) with C_all the unit-weight counts of every
-    # row (event cross-correlations) and C_test the test mask's exact count Gram -- the MFMA runs
-    # over the test rows (~1/K of them) instead of the train rows
-    comp_of = ({} if not (use_lag_gram and COMP_GRAM and comm is None and d.slab is None
-                          and not const_hess and not warm)
-               else _complement_masks(prob, [m for m in umask if not mall[m]], d.n))
     fowner = np.zeros(B0, dtype=np.int64)
     rot = 0
     # secant (Anderson-1) correction of the directions of fits that step on the same stale
@@ -1610,16 +1599,8 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
                     _lag_gram(d, bf, lagg, st)
                     if stats is not None:
                         stats.lag_grams += int(lagg.size)
-                compk = np.array([k for k in uniq if fresh_start[k] and not all_rows[k]
-                                  and int(reqs[k].mask) in comp_of], dtype=np.int32)
-                if compk.size:
-                    _comp_gram(d, bf, prob, compk,
-                               [comp_of[int(reqs[k].mask)] for k in compk], nsteps, ntile1,
-                               stats, st)
-                    if stats is not None:
-                        stats.comp_grams += int(compk.size)
-                _syrk(d, bf, np.sort(np.setdiff1d(np.setdiff1d(uniq, lagg), compk)).astype(
-                    np.int32), nsteps, ntile1, stats, st, rows=gram_rows)
+                _syrk(d, bf, np.sort(np.setdiff1d(uniq, lagg)).astype(np.int32), nsteps,
+                      ntile1, stats, st, rows=gram_rows)
                 sum_hess(uniq)
                 for k, rk in dup:
                     bf.H[k].copy_(bf.H[rk])
@@ -2267,52 +2248,6 @@ def _lag_gram(d: Design, bf, fits: np.ndarray, st):
     _lib.call("sglm_lag_gram", _p(lg.occ), _p(lg.ev_off), _p(lg.ebits), lg.nwords,
               _p(lg.shifts), lg.m, lg.K, lg.layout, lg.smin, lg.smax, lg.row0, lg.n, lg.n_raw,
               d.P, _p(bf.W), d.ld, _p(fits_d), int(fits.size), _p(bf.H), _p(work), st)
-
-
-def _complement_masks(prob: Problem, masks, n: int) -> dict:
-    """mask -> another mask of the problem with m + c = 1 on every row (both 0/1): the test
-    mask of a train mask when the split partitions the rows.  Counts pre-select the pairs, one
-    device comparison (one sync) confirms them."""
-    F_ = int(prob.M.shape[0])
-    ok01 = {f: prob.mask_nnz(f) == prob.mask_count(f) for f in range(F_)}
-    pairs = [(m, c) for m in masks if ok01.get(m) for c in range(F_)
-             if c != m and ok01[c] and prob.mask_count(m) + prob.mask_count(c) == n
-             and prob.mask_count(c) < prob.mask_count(m)]
-    if not pairs:
-        return {}
-    pm = torch.tensor([m for m, _ in pairs], dtype=torch.int64, device=prob.M.device)
-    pc = torch.tensor([c for _, c in pairs], dtype=torch.int64, device=prob.M.device)
-    good = ((prob.M[pm, :n].to(torch.int16) + prob.M[pc, :n].to(torch.int16)) == 1).all(1)
-    out = {}
-    for (m, c), g in zip(pairs, good.cpu().tolist()):
-        if g and m not in out:
-            out[m] = c
-    return out
-
-
-def _comp_gram(d: Design, bf, prob: Problem, fits: np.ndarray, comps, nsteps, ntile1, stats,
-               st):
-    """H[k] = bf16(w_k) (C_all - C_c) for fits at a constant weight w_k on a 0/1 mask whose
-    complement is mask c: C_all = X^T X (unit weights, event cross-correlations, exact counts),
-    C_c = X^T diag(m_c) X (exact count Gram over the complement's rows).  Counts are integers
-    below 2^24, exact in f32; the products with bf16(w) round once (the MFMA Gram with bf16(w)
-    on every row rounds its running sums instead).  Upper 128-blocks only, as sglm_syrk."""
-    from types import SimpleNamespace
-    P, dev = d.P, d.device
-    cm = sorted(set(int(c) for c in comps))
-    buf = _work((len(cm) + 1) * P * P * 4, dev, "compgram")
-    Hc = buf[: (len(cm) + 1) * P * P * 4].view(torch.float32).view(len(cm) + 1, P, P)
-    ones = torch.ones((1, d.ld), dtype=torch.float32, device=dev)
-    _lag_gram(d, SimpleNamespace(W=ones, H=Hc[0:1], up=None), np.zeros(1, np.int32), st)
-    ns = SimpleNamespace(W=prob.M[cm].to(torch.float32), H=Hc[1:], prob=prob,
-                         fit_mask=np.array(cm), wc=None, keep=None)
-    _syrk(d, ns, np.arange(len(cm), dtype=np.int32), nsteps, ntile1, stats, st, exact=True)
-    fits_d = torch.from_numpy(np.asarray(fits, dtype=np.int64)).to(dev)
-    # the weight is one constant on the mask and zero elsewhere: its maximum over the rows
-    wb = bf.W[fits_d].amax(1).to(torch.bfloat16).to(torch.float32)
-    for q, (k, c) in enumerate(zip(fits, comps)):
-        torch.sub(Hc[0], Hc[1 + cm.index(int(c))], out=bf.H[int(k)])
-        bf.H[int(k)].mul_(wb[q])
 
 
 class _Factor64:

@@ -1016,75 +1016,6 @@ def test_grid_first_gram_from_event_correlations(engine):
         assert rel(x["refit_coef"], y["refit_coef"]) < 1e-5
 
 
-def test_complement_gram_equals_mfma_gram(engine):
-    """_comp_gram (H = bf16(w) (C_all - C_test): event cross-correlation counts minus the test
-    mask's exact count Gram) equals the MFMA Gram of the train mask at the constant weight w to
-    f32 rounding on the upper 128-blocks, and the complement pairs are found on the device."""
-    import types
-    import torch
-    from sglm_hip import folds, synth
-    E_ = engine
-    s = synth.make(N=60_000, m=13, L=6, family="poisson", rho=0.05, seed=5)
-    d = E_.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
-    n = d.n
-    np.random.seed(2)
-    tr, te = folds.cv_idx_from_bucket_ids(np.asarray(s.trial), num_folds=4)[0]
-    masks = [folds.mask_from_idx(tr, n), folds.mask_from_idx(te, n), np.ones(n, np.uint8)]
-    prob = E_.Problem(d, [s.y], masks)
-    assert E_._complement_masks(prob, [0], n) == {0: 1}
-    assert E_._complement_masks(prob, [1], n) == {}          # the larger side is never used
-    W = torch.zeros((1, d.ld), dtype=torch.float32, device="cuda")
-    W[0, :n] = 0.3711 * torch.from_numpy(masks[0].astype(np.float32)).cuda()
-    nsteps, nt = (n + 31) // 32, (d.P // 256) * (d.P // 256 + 1) // 2
-    st = E_._stream()
-    Hs = []
-    for comp in (False, True):
-        H = torch.full((1, d.P, d.P), float("nan"), dtype=torch.float32, device="cuda")
-        ns = types.SimpleNamespace(W=W, H=H, prob=prob, fit_mask=np.array([0]), wc=None,
-                                   keep=None)
-        if comp:
-            E_._comp_gram(d, ns, prob, np.array([0], np.int32), [1], nsteps, nt, None, st)
-        else:
-            E_._syrk(d, ns, np.array([0], np.int32), nsteps, nt, None, st)
-        Hs.append(H[0].cpu().numpy())
-    blk = np.kron(np.triu(np.ones((d.P // 128, d.P // 128), bool)), np.ones((128, 128), bool))
-    a, b = Hs[0][blk], Hs[1][blk]
-    assert np.all(np.isfinite(a)) and np.all(np.isfinite(b))
-    assert np.max(np.abs(a - b)) <= 2e-6 * np.max(np.abs(a))
-
-
-def test_grid_complement_first_grams(engine):
-    """The C3-shape grid with the split fits' first Grams from the complement counts reaches the
-    same fits as with their MFMA Grams (SGLM_COMP_GRAM off)."""
-    import pandas as pd
-    from sglm_hip import folds, grid, synth
-    from sglm_hip.estimators import Objective
-    E_ = engine
-    s = synth.make(N=100_000, m=25, L=10, family="poisson", rho=0.02, seed=0)
-    d = E_.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
-    codes = folds.trial_keys_codes(pd.DataFrame({"nTrial": s.trial}), ["nTrial"]).values
-    np.random.seed(3)
-    cv_idx = folds.cv_idx_from_bucket_ids(codes, num_folds=5)
-    objs = [Objective("irls", E_.FAM_TWEEDIE_LOG, 1.0, float(a), "n", True, 100)
-            for a in np.logspace(-4, 1, 6)]
-    st = E_.IrlsStats()
-    a = grid.run(d, s.y, cv_idx, objs, [0] * 6, stats=st)
-    assert st.comp_grams >= 5
-    old = E_.COMP_GRAM
-    try:
-        E_.COMP_GRAM = False
-        st2 = E_.IrlsStats()
-        b = grid.run(d, s.y, cv_idx, objs, [0] * 6, stats=st2)
-        assert st2.comp_grams == 0
-    finally:
-        E_.COMP_GRAM = old
-    for x, y in zip(a, b):
-        assert x["converged"] and y["converged"]
-        assert rel(x["cv_coefs"], y["cv_coefs"]) < 1e-5
-        assert rel(x["refit_coef"], y["refit_coef"]) < 1e-5
-        assert np.max(np.abs(np.asarray(x["cv_scores_test"]) - y["cv_scores_test"])) < 1e-6
-
-
 def test_lag_gram_only_for_constant_weights(engine):
     """Gamma / Tweedie weights carry y on every row (h = y e^-eta for power 2) even at a
     constant eta: their first Gram must stay the MFMA Gram over the rows."""
