@@ -31,7 +31,10 @@ sys.path.insert(0, ROOT)
 
 PEAK_BF16_TFLOPS = 2500.0          # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
-PEAK_F64_TFLOPS = 78.6             # MI355X FP64 vector (AMD spec)
+# MI355X f64 vector FMA rate MEASURED on the box (tools/probe/f64_fma.hip: every CU full of
+# independent v_fma_f64 chains, 61.3 TFLOP/s): MI355X_MICROARCH.md gives the f32 peaks only;
+# AMD's spec sheet says 78.6 at the nominal clock
+PEAK_F64_TFLOPS = 61.3
 
 CONFIGS = {
     # name: (N rows, events m, L -> lags -L..L-1, n_splits, lambdas)
@@ -250,13 +253,18 @@ def bench_c5(a):
                    "parallelism": f"responses round-robin over {world} rank(s)",
                    "refit_nonzeros_r0": [int(np.sum(np.abs(out[0][j]["refit_coef"]) > 0))
                                          for j in range(nlam)]},
-        "roofline": {"bound": "valu-f64", "kernel": "enet_cd_reg_kernel (cyclic coordinate "
+        "roofline": {"bound": "valu-f64", "kernel": "enet_cd_lane_kernel (cyclic coordinate "
                                                    "descent on the shared float64 Gram)",
                      "achieved": achieved, "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / PEAK_F64_TFLOPS, "traffic": None,
                      "algorithmic_flop_per_sweep_per_fit": 2 * s.p * s.p,
                      "avg_launch_ms": cd_ms / a.steps,
-                     "peak_source": "AMD MI355X spec FP64 vector (not in MI355X_MICROARCH.md)"},
+                     "peak_source": "measured f64 FMA rate (tools/probe/f64_fma.hip, "
+                                    "profiles/r04_f64_probe.json); MI355X_MICROARCH.md "
+                                    "lists no f64 peak (AMD spec 78.6 at 2.4 GHz)",
+                     "bound_note": "the coordinate steps are sequential (one barrier per "
+                                   "coordinate): latency-bound; the Q row stream is an L2 hit "
+                                   "for the workgroups of one (Q, alpha) on an XCD"},
         "cpu_baseline": cpu}))
 
 
