@@ -224,6 +224,20 @@ size_t sglm_xtr_bits_int_work_bytes(int32_t P, int32_t B, int64_t ld);
 int sglm_xtr_bits_int(const uint32_t* cbits, int64_t ld, int32_t P, int64_t n, const void* D,
                       int32_t B, double* G, void* work, sglm_stream_t stream);
 
+/* Bit-planes of a time-shifted 0/1 event design straight from its events (no dense bf16 design):
+ * sglm_event_bits: ebits[a][w] bit i = (E[32 w + i][a] != 0), E as bf16 [m][lde] event-major,
+ * nwords = ceil(n_raw / 32).  sglm_lag_bits: the design's column planes xbits [P][ld/32]
+ * (column j < p = event cols[j] shifted by shifts[j]: X[t, j] = E[t + row0 - shifts[j]][cols[j]],
+ * zero outside the raw rows; column p = ones on rows < n; padding zero) and the row-major MFMA
+ * planes rbits [P/64][ld] x uint2 -- what sglm_pack_bits / sglm_pack_bits_t produce from the dense
+ * design.  Replaces the expansion + packing of sglm_ez.timeshift_cols' design
+ * (backend/sglm_ez.py:102-123) for 0/1 events. */
+int sglm_event_bits(const uint16_t* Eb, int64_t lde, int32_t m, int64_t n_raw, uint32_t* ebits,
+                    int64_t nwords, sglm_stream_t stream);
+int sglm_lag_bits(const uint32_t* ebits, int64_t nwords, const int32_t* cols, const int32_t* shifts,
+                  int32_t p, int64_t row0, int64_t n, int64_t ld, int32_t P, uint32_t* xbits,
+                  void* rbits, sglm_stream_t stream);
+
 /* Shared-Gram elastic net for many fits per mask (multi-response lambda paths):
  * sglm_center_gram: Q[m] (float64 p x p) = G_xx - g g^T / n (center) or G_xx from the
  *   augmented Gram H[gram_of[m]] (ones column at index p, as sglm_syrk forms it with W = mask);

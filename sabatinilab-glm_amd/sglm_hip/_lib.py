@@ -50,6 +50,8 @@ SIGNATURES = {
     "sglm_xtr_bits_packed": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _i32, _vp, _vp, _vp, _vp]),
     "sglm_xtr_bits_int_work_bytes": (_sz, [_i32, _i32, _i64]),
     "sglm_xtr_bits_int": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _i32, _vp, _vp, _vp]),
+    "sglm_event_bits": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _i64, _vp]),
+    "sglm_lag_bits": (C.c_int, [_vp, _i64, _vp, _vp, _i32, _i64, _i64, _i64, _i32, _vp, _vp, _vp]),
     "sglm_digit_planes": (C.c_int, [_vp, _i64, _vp, _i64, _i64, _vp, _vp, _vp, _i32, _i32, _vp, _i64, _vp]),
     "sglm_center_gram": (C.c_int, [_vp, _i32, _i32, _vp, _i32, _i32, _vp, _vp]),
     "sglm_enet_cd_shared": (C.c_int, [_vp, _i32, _vp, _i32, _vp, _vp, _vp, _i32, C.c_double,

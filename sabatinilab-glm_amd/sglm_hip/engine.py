@@ -114,6 +114,9 @@ CHOL_SPLIT_MIN = int(__import__("os").environ.get("SGLM_CHOL_SPLIT_MIN", "6"))
 # 62.3 / 63.1 / 62.3 ms against 59.7 / 60.2 / 59.3 ms unpipelined, alternating on one box).
 # Default 0.
 GRAM_PIPE = int(__import__("os").environ.get("SGLM_GRAM_PIPE", "0") or 0)
+# bit-planes of 0/1 event designs straight from the events (sglm_lag_bits; the dense bf16
+# design only on first use)
+LAG_BITS = __import__("os").environ.get("SGLM_LAG_BITS", "1") == "1"
 # Rank decisions of unpenalised fits (float64 factor of the exact mask Gram, sglm_chol64_factor):
 # a pivot whose Schur complement is <= tol * its diagonal is a dependent column.  The Gram of a
 # 0/1 design is exact (integer counts in f32), so tol only has to clear float64 elimination
@@ -182,13 +185,18 @@ class Design:
     xf: f32  [P, ld]  or None (only when X is not bf16-exact; used for eta and X^T r)
     """
 
-    def __init__(self, n: int, p: int, device="cuda", zero=True):
+    def __init__(self, n: int, p: int, device="cuda", zero=True, lazy_xb=None):
         require_gpu()
         self.n, self.p = int(n), int(p)
         self.P = pad_to(self.p + 1, COL_PAD)
         self.ld = pad_to(self.n + 1, ROW_PAD)     # >= 1 zero padding row (w = 0 there)
-        alloc = torch.zeros if zero else torch.empty
-        self.xb = alloc((self.P, self.ld), dtype=torch.bfloat16, device=device)
+        # lazy_xb: a callable that fills a zeroed bf16 design when xb is first read (designs
+        # whose bit-planes come straight from events never need the dense copy on the hot path)
+        self._xb_fill = lazy_xb
+        self._xb = None
+        if lazy_xb is None:
+            alloc = torch.zeros if zero else torch.empty
+            self._xb = alloc((self.P, self.ld), dtype=torch.bfloat16, device=device)
         self.xf = None
         self.xbits = None      # uint32 bit-planes [P, ld/32] when the design is 0/1
         self.rbits = None      # row-major bit-planes [P/64][ld] x uint2 (MFMA eta) when 0/1
@@ -197,6 +205,18 @@ class Design:
         self.slab = None       # (start, stop, n_total): rows [start, stop) of an n_total-row
         #                        design (one rank's share of a row-sharded solve, comm.py)
         self.device = device
+
+    @property
+    def xb(self):
+        """bf16 [P, ld] dense design (built on first use when the bit-planes came first)."""
+        if self._xb is None:
+            self._xb = torch.zeros((self.P, self.ld), dtype=torch.bfloat16, device=self.device)
+            self._xb_fill(self._xb)
+        return self._xb
+
+    @xb.setter
+    def xb(self, v):
+        self._xb = v
 
     @property
     def xtype(self):
@@ -390,9 +410,7 @@ class Design:
         N_raw, m = E.shape
         K = len(shifts)
         p = K * m
-        d = cls(n, p, device, zero=True)
         Eb = E.t().contiguous().to(torch.bfloat16)          # feature-major bf16 (m, N_raw)
-        exact = bool(torch.equal(Eb.float(), E.t()))
         if event_major:
             cols = np.repeat(np.arange(m), K)
             sh = np.tile(np.asarray(shifts), m)
@@ -401,9 +419,29 @@ class Design:
             sh = np.repeat(np.asarray(shifts), m)
         cols_d = torch.tensor(cols, dtype=torch.int32, device=device)
         sh_d = torch.tensor(sh, dtype=torch.int32, device=device)
-        _lib.call("sglm_timeshift_expand", _p(Eb), N_raw, 1, N_raw, _p(cols_d), _p(sh_d), p,
-                  _p(d.xb), n, 1, d.ld, row0, 2, 0, _stream())
-        d.xb[p, :n] = 1.0
+
+        def fill(xb):
+            _lib.call("sglm_timeshift_expand", _p(Eb), N_raw, 1, N_raw, _p(cols_d), _p(sh_d), p,
+                      _p(xb), n, 1, xb.shape[1], row0, 2, 0, _stream())
+            xb[p, :n] = 1.0
+
+        if LAG_BITS and bool(((E == 0) | (E == 1)).all()):
+            # 0/1 events: the bit-planes straight from the events' occurrence bitmaps (no dense
+            # 4-GB-at-C4 design to write and pack twice); the dense copy is built on first use
+            d = cls(n, p, device, lazy_xb=fill)
+            nwords = (N_raw + 31) // 32
+            ebits = torch.empty((m, nwords), dtype=torch.int32, device=device)
+            _lib.call("sglm_event_bits", _p(Eb), N_raw, m, N_raw, _p(ebits), nwords, _stream())
+            d.xbits = torch.empty((d.P, d.ld // 32), dtype=torch.int32, device=device)
+            d.rbits = torch.empty((d.P // 64) * d.ld * 2, dtype=torch.int32, device=device)
+            _lib.call("sglm_lag_bits", _p(ebits), nwords, _p(cols_d), _p(sh_d), p, row0, n,
+                      d.ld, d.P, _p(d.xbits), _p(d.rbits), _stream())
+            d.lag = LagStructure.build(E, shifts, row0, n, event_major, ebits=ebits)
+            d.slab = info
+            return d
+        d = cls(n, p, device, zero=True)
+        fill(d.xb)
+        exact = bool(torch.equal(Eb.float(), E.t()))
         if exact:
             d._pack_bits()
             if d.xbits is not None and bool(((E == 0) | (E == 1)).all()):
@@ -513,7 +551,7 @@ class LagStructure:
     design."""
 
     @classmethod
-    def build(cls, E, shifts, row0, n, event_major):
+    def build(cls, E, shifts, row0, n, event_major, ebits=None):
         self = cls()
         dev = E.device
         N_raw, m = E.shape
@@ -546,12 +584,12 @@ class LagStructure:
         self.ev_off = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev),
                                  torch.cumsum(cnt, 0)]).to(torch.int32).contiguous()
         self.nwords = (int(N_raw) + 31) // 32
-        nzb = torch.nn.functional.pad((E.t() != 0).to(torch.int32),
-                                      (0, self.nwords * 32 - int(N_raw))).view(m, self.nwords, 32)
-        bits = torch.zeros((m, self.nwords), dtype=torch.int32, device=dev)
-        for b in range(32):
-            bits |= nzb[:, :, b] << b
-        self.ebits = bits.contiguous()
+        if ebits is None:
+            Eb = E.t().contiguous().to(torch.bfloat16)
+            ebits = torch.empty((m, self.nwords), dtype=torch.int32, device=dev)
+            _lib.call("sglm_event_bits", _p(Eb), int(N_raw), int(m), int(N_raw), _p(ebits),
+                      self.nwords, _stream())
+        self.ebits = ebits
         return self
 
 

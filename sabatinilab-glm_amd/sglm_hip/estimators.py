@@ -105,7 +105,8 @@ def _cached_design(Xa):
 
 
 def _design_bytes(d) -> int:
-    return sum(t.numel() * t.element_size() for t in (d.xb, d.xf, d.xbits, d.rbits, d._cbits)
+    # d._xb: the dense copy only if it was built (reading d.xb would build it)
+    return sum(t.numel() * t.element_size() for t in (d._xb, d.xf, d.xbits, d.rbits, d._cbits)
                if t is not None)
 
 

@@ -1096,3 +1096,40 @@ def test_xtr_bits_int_exact(engine, torch_mod, B, lim):
             v = (v - dq) // 256
         assert np.all(v == 0)
         assert np.all(got[:, s.N:] == 0)
+
+
+@pytest.mark.parametrize("m,L,event_major,N,row0_off", [(50, 20, False, 200_003, 0),
+                                                       (7, 3, True, 13_000, 2),
+                                                       (70, 4, False, 9_000, 0)])
+def test_lag_bits_equal_packed_dense_design(engine, monkeypatch, m, L, event_major, N, row0_off):
+    """The bit-planes built straight from the events (sglm_event_bits + sglm_lag_bits) equal the
+    ones packed from the dense bf16 design (sglm_pack_bits / _pack_bits_t), the occurrence
+    bitmaps equal LagStructure's, and the lazily built dense design equals the eager one; also
+    a design whose row window reaches past the events' first rows (zero fill) and m > 64 (no
+    LagStructure)."""
+    import torch
+    from sglm_hip import synth
+    E_ = engine
+    s = synth.make(N=N, m=m, L=L, family="poisson", rho=0.05, seed=m + N)
+    row0 = s.L - 1 - row0_off
+    n = s.N - 1
+    designs = {}
+    for lb in (False, True):
+        monkeypatch.setattr(E_, "LAG_BITS", lb)
+        designs[lb] = E_.Design.from_events(s.E, s.shifts, row0, n, event_major=event_major)
+    a, b = designs[False], designs[True]
+    assert b._xb is None                               # no dense copy built yet
+    assert torch.equal(a.xbits, b.xbits)
+    assert torch.equal(a.rbits, b.rbits)
+    if a.lag is not None:
+        assert b.lag is not None and torch.equal(a.lag.ebits, b.lag.ebits)
+        # the occurrence bitmaps against numpy: bit u & 31 of word u >> 5 = (E[u, a] != 0)
+        nw = a.lag.nwords
+        nz = np.zeros((m, nw * 32), dtype=np.uint8)
+        nz[:, : s.E.shape[0]] = (np.asarray(s.E) != 0).T
+        ref = np.packbits(nz, axis=1, bitorder="little").view("<u4").view(np.int32)
+        assert np.array_equal(b.lag.ebits.cpu().numpy(), ref)
+    else:
+        assert b.lag is None
+    assert torch.equal(a.xb, b.xb)                     # built on first use
+    assert torch.equal(a.cbits_full(), b.cbits_full())
