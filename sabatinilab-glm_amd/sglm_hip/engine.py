@@ -595,7 +595,9 @@ class LagStructure:
 
 # ------------------------------------------------------------------------------ problem
 # threads of the native host-side setup helpers (sglm_host_masks, sglm_host_copy)
-HOST_THREADS = int(os.environ.get("SGLM_HOST_THREADS", "8"))
+# (SGLM_HOST_THREADS, else the process's OpenMP share -- 16 on a one-GPU box -- else 8)
+HOST_THREADS = max(1, min(int(os.environ.get("SGLM_HOST_THREADS")
+                              or os.environ.get("OMP_NUM_THREADS") or 8), os.cpu_count() or 8))
 # row-chunk size of the pinned host->device design upload (Design.from_host)
 UPLOAD_CHUNK_BYTES = int(os.environ.get("SGLM_UPLOAD_CHUNK_BYTES", str(256 << 20)))
 
