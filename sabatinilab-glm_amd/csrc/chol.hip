@@ -1027,33 +1027,6 @@ static bool upd_lds() {
     return v;
 }
 
-// The trailing update of a look-ahead group split in two (SGLM_CHOL_FORK, read per chain
-// build): the next group's band on the chain's stream, the far rows on a second stream, where
-// they overlap the next group's diagonal and panel steps.  Each tile still gets the same one
-// kernel pass (same K rows, same order), so the factor is bitwise unchanged.
-static bool chol_fork() {
-    const char* e = getenv("SGLM_CHOL_FORK");
-    return !(e && e[0] == '0');
-}
-static hipStream_t fork_stream() {
-    static thread_local hipStream_t s2 = [] {
-        hipStream_t x = nullptr;
-        if (hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) x = nullptr;
-        return x;
-    }();
-    return s2;
-}
-// fork / join events, reused chain after chain (a wait binds to the record before it)
-static hipEvent_t fork_event(int i) {
-    static thread_local std::vector<hipEvent_t> ev;
-    while ((int)ev.size() <= i) {
-        hipEvent_t e = nullptr;
-        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
-        ev.push_back(e);
-    }
-    return ev[i];
-}
-
 static void launch_update(dim3 grid, hipStream_t s, float* H, int32_t P, int32_t k0, int32_t kc,
                           int32_t s0, const int32_t* fits) {
     if (upd_lds())
@@ -1114,9 +1087,6 @@ static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t na
                                                                     nrefac);
     };
     const int la = chol_lookahead();
-    hipStream_t s2 = (Mall && nrefac > 0 && chol_fork()) ? fork_stream() : nullptr;
-    hipEvent_t far_prev = nullptr;              // the previous group's far update (second stream)
-    int nev = 0;
     for (int kb = 0; kb < nb; kb += la) {
         const int ke = kb + la < nb ? kb + la : nb;            // group [kb, ke)
         for (int b = kb; b < ke; ++b) {
@@ -1128,41 +1098,9 @@ static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t na
                               b + 1, fits);
         }
         const int T = nb - ke;
-        if (nrefac > 0 && T > 0 && !s2) {
+        if (nrefac > 0 && T > 0)
             launch_update(dim3(T * (T + 1) / 2, nrefac), s, H, P, kb * kNB, (ke - kb) * kNB, ke,
                           fits);
-        } else if (nrefac > 0 && T > 0) {
-            const int nr = T < la ? T : la;                    // the next group's band rows
-            const int s0f = ke + nr, Tf = nb - s0f;
-            hipEvent_t far = nullptr;
-            if (Tf > 0) {                                      // far rows: second stream
-                hipEvent_t ep = fork_event(nev++);
-                far = fork_event(nev++);
-                if (!ep || !far || hipEventRecord(ep, s) != hipSuccess ||
-                    hipStreamWaitEvent(s2, ep, 0) != hipSuccess) {
-                    set_error("chol fork: event record / wait failed");
-                    return SGLM_EHIP;
-                }
-                launch_update(dim3(Tf * (Tf + 1) / 2, nrefac), s2, H, P, kb * kNB,
-                              (ke - kb) * kNB, s0f, fits);
-                if (hipEventRecord(far, s2) != hipSuccess) {
-                    set_error("chol fork: event record failed");
-                    return SGLM_EHIP;
-                }
-            }
-            // the band rows were also the previous group's far rows: after that update
-            if (far_prev && hipStreamWaitEvent(s, far_prev, 0) != hipSuccess) {
-                set_error("chol fork: stream wait failed");
-                return SGLM_EHIP;
-            }
-            launch_update(dim3(nr * T - nr * (nr - 1) / 2, nrefac), s, H, P, kb * kNB,
-                          (ke - kb) * kNB, ke, fits);
-            far_prev = far;
-        }
-    }
-    if (far_prev && hipStreamWaitEvent(s, far_prev, 0) != hipSuccess) {   // join
-        set_error("chol fork: join failed");
-        return SGLM_EHIP;
     }
     st = check_launch("chol block kernels");
     if (st) return st;
@@ -1373,7 +1311,7 @@ static int factor_inv_cached(float* H, float* Minv, int32_t P, const int32_t* fi
     std::memset(&key, 0, sizeof(key));
     key.H = H; key.Minv = Minv; key.fits = fits; key.dshift = dshift; key.delta = delta;
     key.info = info; key.frozen = frozen; key.work = work;
-    key.P = P; key.n = n; key.B = B; key.la = chol_lookahead() * (chol_fork() ? -1 : 1);
+    key.P = P; key.n = n; key.B = B; key.la = chol_lookahead();
     // the lock is held across capture and launch: a concurrent eviction must not destroy the
     // entry between lookup and launch (captures are thread-local, so nothing else is stalled
     // but other chains' host enqueue, which is short next to the chain itself)

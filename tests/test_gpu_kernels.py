@@ -286,55 +286,6 @@ def test_chol_inv_many_fits_vs_float64(engine, torch_mod, P, p, B, monkeypatch):
         assert np.all(x[q, p + 1:] == 0)
 
 
-@pytest.mark.parametrize("P,p,B", [(2048, 1990, 5), (1280, 1200, 2), (448, 400, 3)])
-def test_chol_fork_chain_bitwise(engine, torch_mod, P, p, B, monkeypatch):
-    """The factor + inverse chain with each look-ahead group's far trailing update on a second
-    stream (SGLM_CHOL_FORK=1) gives the same factor, inverse and solves bit for bit as the
-    single-stream chain (=0): every tile gets the same kernel pass; graph-captured and direct
-    launches alike."""
-    torch = torch_mod
-    from sglm_hip import _lib
-    rng = np.random.default_rng(P + B)
-    H = np.zeros((B, P, P), np.float32)
-    for k in range(B):
-        A = rng.normal(size=(p + 300, p + 1))
-        H[k, : p + 1, : p + 1] = A.T @ A / 100.0
-    dsh = np.full((B, P), -1.0, np.float32)
-    dsh[:, :p] = rng.uniform(0.2, 1.0, size=(B, 1))
-    dsh[:, p] = 0.0
-    g = rng.normal(size=(B, P))
-    res = {}
-    for fork in ("0", "1"):
-        for graph in ("1", "0"):
-            monkeypatch.setenv("SGLM_CHOL_FORK", fork)
-            Hd = torch.from_numpy(H).cuda()
-            Md = torch.empty_like(Hd)
-            gd = torch.from_numpy(g).cuda()
-            out = torch.full((B, P), np.nan, dtype=torch.float32, device="cuda")
-            info = torch.zeros(B, dtype=torch.int32, device="cuda")
-            frozen = torch.zeros((B, P), dtype=torch.uint8, device="cuda")
-            dshd = torch.from_numpy(dsh).cuda()
-            cw = torch.empty(_lib.query("sglm_chol_work_bytes", P, B), dtype=torch.uint8,
-                             device="cuda")
-            lst = list(range(B))
-            tiles = [(q, 1) for q in range(B)]
-            ints = torch.tensor(np.r_[lst, lst, np.asarray(tiles).reshape(-1)].astype(np.int32),
-                                device="cuda")
-            rs = torch.ones(B, dtype=torch.float32, device="cuda")
-            if graph == "0":
-                _lib.call("sglm_chol_graph_cache_clear")
-            _lib.call("sglm_chol_solve_inv", Hd.data_ptr(), Md.data_ptr(), P, ints.data_ptr(),
-                      ints[B:].data_ptr(), rs.data_ptr(), B, B, ints[2 * B:].data_ptr(), B,
-                      gd.data_ptr(), dshd.data_ptr(), out.data_ptr(), info.data_ptr(),
-                      frozen.data_ptr(), B, cw.data_ptr(), 0)
-            torch.cuda.synchronize()
-            res[(fork, graph)] = (torch.triu(Hd).cpu(), torch.triu(Md).cpu(), out.cpu())
-    base = res[("0", "1")]
-    for key, val in res.items():
-        for a, b in zip(base, val):
-            assert torch.equal(a, b), key
-
-
 @pytest.mark.parametrize("P", [128, 2048])
 def test_chol_inv_dropped_pivots(engine, torch_mod, P):
     """Factor + inverse chain (four-wave diagonal step) on a Gram with exactly duplicated and
