@@ -610,18 +610,9 @@ __device__ __forceinline__ void wait6_12(Step6& t) {
 
 // step in `cur` (its sub-step 0 fragments in F), `nxt` = the next step (in flight), loads step
 // `snn` into `nn`; leaves F = sub-step 0 fragments of `nxt`
-// the next step's weights ANDed with vm_next once they have landed: all ones, or zero for a
-// padding step past the end, whose B fragments are then zero and whose MFMAs add nothing -- a
-// loop without a tail, so nothing copies registers of loads still in flight at a loop exit
-__device__ __forceinline__ void mask_w(Step6& t, uint32_t vm) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) t.w[k] &= (u32x4){vm, vm, vm, vm};
-}
-
 template <bool DIAG>
 __device__ __forceinline__ void step6_d2(const Step6& cur, Step6& nxt, Step6& nn, Frag6& F, int h,
-                                         f32x16 (&acc)[4][4], const Addr6& ad, int64_t snn,
-                                         uint32_t vm_next) {
+                                         f32x16 (&acc)[4][4], const Addr6& ad, int64_t snn) {
     load6(nn, ad, snn);
     __builtin_amdgcn_sched_barrier(0);
     Frag6 G;
@@ -635,7 +626,6 @@ __device__ __forceinline__ void step6_d2(const Step6& cur, Step6& nxt, Step6& nn
     mfma16<DIAG>(F, acc);
     interleave16<DIAG>();
     wait6_12(nxt);
-    mask_w(nxt, vm_next);
     frags6(nxt, 0, h, F);
     mfma16<DIAG>(G, acc);
     interleave16<DIAG>();
@@ -652,12 +642,15 @@ __device__ __forceinline__ void gram6_loop2(f32x16 (&acc)[4][4], const Addr6& ad
     load6(B, ad, cl(1));
     wait6_12(A);
     frags6(A, 0, h, F);
-    // steps in threes; the last triple's steps past the end run with zero weights
-    auto vm = [&](int t) { return t < nsteps ? 0xFFFFFFFFu : 0u; };
-    for (int s = 0; s < nsteps; s += 3) {
-        step6_d2<DIAG>(A, B, C, F, h, acc, ad, cl(s + 2), vm(s + 1));
-        step6_d2<DIAG>(B, C, A, F, h, acc, ad, cl(s + 3), vm(s + 2));
-        step6_d2<DIAG>(C, A, B, F, h, acc, ad, cl(s + 4), vm(s + 3));
+    int s = 0;
+    for (; s + 3 <= nsteps; s += 3) {
+        step6_d2<DIAG>(A, B, C, F, h, acc, ad, cl(s + 2));
+        step6_d2<DIAG>(B, C, A, F, h, acc, ad, cl(s + 3));
+        step6_d2<DIAG>(C, A, B, F, h, acc, ad, cl(s + 4));
+    }
+    if (s < nsteps) {
+        step6_d2<DIAG>(A, B, C, F, h, acc, ad, cl(s + 2));
+        if (s + 1 < nsteps) step6_d2<DIAG>(B, C, A, F, h, acc, ad, cl(s + 3));
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped reloads still in flight
 }
