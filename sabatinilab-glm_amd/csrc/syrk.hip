@@ -595,66 +595,6 @@ __device__ __forceinline__ void gram6_loop(f32x16 (&acc)[4][4], const Addr6& ad,
     }
 }
 
-// Two K-steps in flight (SGLM_SYRK_D2, default on): three register sets in rotation, the loads
-// of step s + 2 issued as step s starts and waited for (vmcnt(12): all but the 12 youngest
-// loads) only before the last sub-step of step s + 1 -- seven sub-steps (~3,500 cycles) to
-// land instead of three.  The same MFMAs in the same order: the Grams are bitwise equal.
-__device__ __forceinline__ void wait6_12(Step6& t) {
-    asm volatile("s_waitcnt vmcnt(12)"
-                 : "+v"(t.a[0]), "+v"(t.a[1]), "+v"(t.a[2]), "+v"(t.a[3]), "+v"(t.b[0]),
-                   "+v"(t.b[1]), "+v"(t.b[2]), "+v"(t.b[3]), "+v"(t.w[0]), "+v"(t.w[1]),
-                   "+v"(t.w[2]), "+v"(t.w[3])
-                 :
-                 : "memory");
-}
-
-// step in `cur` (its sub-step 0 fragments in F), `nxt` = the next step (in flight), loads step
-// `snn` into `nn`; leaves F = sub-step 0 fragments of `nxt`
-template <bool DIAG>
-__device__ __forceinline__ void step6_d2(const Step6& cur, Step6& nxt, Step6& nn, Frag6& F, int h,
-                                         f32x16 (&acc)[4][4], const Addr6& ad, int64_t snn) {
-    load6(nn, ad, snn);
-    __builtin_amdgcn_sched_barrier(0);
-    Frag6 G;
-    frags6(cur, 1, h, G);
-    mfma16<DIAG>(F, acc);
-    interleave16<DIAG>();
-    frags6(cur, 2, h, F);
-    mfma16<DIAG>(G, acc);
-    interleave16<DIAG>();
-    frags6(cur, 3, h, G);
-    mfma16<DIAG>(F, acc);
-    interleave16<DIAG>();
-    wait6_12(nxt);
-    frags6(nxt, 0, h, F);
-    mfma16<DIAG>(G, acc);
-    interleave16<DIAG>();
-}
-
-template <bool DIAG>
-__device__ __forceinline__ void gram6_loop2(f32x16 (&acc)[4][4], const Addr6& ad, int nsteps,
-                                            int h) {
-    Step6 A, B, C;                                   // three register sets, two steps in flight
-    Frag6 F;
-    const int64_t last = nsteps - 1;
-    auto cl = [&](int64_t t) { return t < nsteps ? t : last; };   // clamped: redundant reloads
-    load6(A, ad, 0);
-    load6(B, ad, cl(1));
-    wait6_12(A);
-    frags6(A, 0, h, F);
-    int s = 0;
-    for (; s + 3 <= nsteps; s += 3) {
-        step6_d2<DIAG>(A, B, C, F, h, acc, ad, cl(s + 2));
-        step6_d2<DIAG>(B, C, A, F, h, acc, ad, cl(s + 3));
-        step6_d2<DIAG>(C, A, B, F, h, acc, ad, cl(s + 4));
-    }
-    if (s < nsteps) {
-        step6_d2<DIAG>(A, B, C, F, h, acc, ad, cl(s + 2));
-        if (s + 1 < nsteps) step6_d2<DIAG>(B, C, A, F, h, acc, ad, cl(s + 3));
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped reloads still in flight
-}
-
 // XCD-banded placement of the Gram's 128-blocks (SGLM_SYRK_XCD): the nb block rows are cut
 // into four bands of bs = nb / 4 and the ten band pairs (I <= J) dealt to the eight XCDs --
 // six off-diagonal pairs one each, the four diagonal pairs two by two -- so an XCD's blocks
@@ -692,7 +632,7 @@ __device__ __forceinline__ bool xcd_band_unit(int b, int nb, int nact, int split
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 syrk6_kernel(const int64_t* __restrict__ desc, int32_t P, int32_t splits,
              const int32_t* __restrict__ fits, int32_t nunits, float* __restrict__ H,
-             float* __restrict__ slab, int32_t nact, int32_t xmap, int32_t d2) {
+             float* __restrict__ slab, int32_t nact, int32_t xmap) {
     int slot, split, bi, bj;
     if (xmap) {
         if (!xcd_band_unit(blockIdx.x, P / 128, nact, splits, slot, split, bi, bj)) return;
@@ -728,17 +668,10 @@ syrk6_kernel(const int64_t* __restrict__ desc, int32_t P, int32_t splits,
         for (int n = 0; n < 4; ++n) acc[m][n] = (f32x16){};
 
     if (nsteps > 0) {
-        if (d2) {
-            if (bi == bj)
-                gram6_loop2<true>(acc, ad, nsteps, h);
-            else
-                gram6_loop2<false>(acc, ad, nsteps, h);
-        } else {
-            if (bi == bj)
-                gram6_loop<true>(acc, ad, nsteps, h);
-            else
-                gram6_loop<false>(acc, ad, nsteps, h);
-        }
+        if (bi == bj)
+            gram6_loop<true>(acc, ad, nsteps, h);
+        else
+            gram6_loop<false>(acc, ad, nsteps, h);
     }
     float* out = slab ? slab + ((int64_t)split * nact + slot) * (int64_t)P * P
                       : H + (int64_t)fit * P * P;
@@ -960,15 +893,13 @@ extern "C" int sglm_syrk_cbits(const int64_t* desc, int32_t P, const int32_t* fi
     hipStream_t s = as_stream(stream);
     float* slab = splits > 1 ? (float*)work : nullptr;
     const char* ex = getenv("SGLM_SYRK_XCD");         // read per call (A/B in one process)
-    const char* e2 = getenv("SGLM_SYRK_D2");
-    const int d2 = (e2 && e2[0] == '0') ? 0 : 1;
     if (ex && ex[0] == '1' && nb % 4 == 0 && nb >= 4) {
         const int bs = nb / 4;
         const unsigned grid = 8u * (unsigned)(bs * (bs + 1) * nact * splits);
-        syrk6_kernel<<<grid, 64, 0, s>>>(desc, P, splits, fits, nunits, H, slab, nact, 1, d2);
+        syrk6_kernel<<<grid, 64, 0, s>>>(desc, P, splits, fits, nunits, H, slab, nact, 1);
     } else {
         syrk6_kernel<<<dim3((unsigned)(nunits * nact), (unsigned)splits), 64, 0, s>>>(
-            desc, P, splits, fits, nunits, H, slab, nact, 0, d2);
+            desc, P, splits, fits, nunits, H, slab, nact, 0);
     }
     int st = check_launch("syrk6_kernel");
     if (st || splits == 1) return st;
