@@ -625,6 +625,13 @@ int sglm_host_gather_cols(const void* const* src, const int64_t* stride, int32_t
  * value is 0.0 or 1.0.  The 0/1 event columns of a lagged frame cross PCIe as bits. */
 int sglm_host_pack_bits_cols(const void* const* src, const int64_t* stride, int32_t ncols,
                              int64_t nrows, uint32_t* bits, uint8_t* binary, int32_t nthreads);
+/* sglm_host_group_rows: the row lists of GroupShuffleSplit folds from per-group sides --
+ * out[j] (caller-allocated, len[j] entries) = the ascending rows i < n with
+ * side[(j / 2) * G + gidx[i]] == 1 + (j % 2) (1 train, 2 test), j < 2 * nsplits:
+ * np.flatnonzero(is_train[gidx]) / (is_test[gidx]) per split (sklearn _split.py:2181-2187,
+ * as backend/sglm_pp.py:236-264 draws them).  len[j] must equal the row count it selects. */
+int sglm_host_group_rows(const int64_t* gidx, int64_t n, const uint8_t* side, int32_t nsplits,
+                         int64_t G, int64_t* const* out, const int64_t* len, int32_t nthreads);
 
 #ifdef __cplusplus
 }

@@ -212,6 +212,47 @@ extern "C" int sglm_host_pack_bits_cols(const void* const* src, const int64_t* s
     const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(nthreads, nchunks));
     std::vector<std::vector<uint8_t>> bad(nt, std::vector<uint8_t>(ncols, 0));
     std::vector<std::thread> th;
+    // the columns of ONE row-major block (a DataFrame built from a C-order array: column c at
+    // base + c, row stride S >= ncols) are read row by row, each row's run of ncols values
+    // once and in address order, instead of one strided pass per column
+    const int64_t S = stride ? stride[0] : 1;
+    bool block = ncols > 1 && S >= ncols;
+    for (int c = 1; block && c < ncols; ++c)
+        block = stride[c] == S && (const double*)src[c] == (const double*)src[0] + c;
+    if (block) {
+        const double* base = (const double*)src[0];
+        for (int t = 0; t < nt; ++t)
+            th.emplace_back([=, &bad] {
+                std::vector<uint32_t> word(ncols);
+                std::vector<uint8_t> b(ncols, 0);
+                uint8_t* bl = b.data();
+                uint32_t* wd = word.data();
+                for (int64_t q = t; q < nchunks; q += nt) {
+                    const int64_t r0 = q * chunk, r1 = std::min(nrows, r0 + chunk);
+                    for (int64_t w0 = r0; w0 < r1; w0 += 32) {
+                        std::fill(word.begin(), word.end(), 0u);
+                        const int64_t e = std::min<int64_t>(32, r1 - w0);
+                        for (int64_t k = 0; k < e; ++k) {
+                            const double* row = base + (w0 + k) * S;
+                            for (int c = 0; c < ncols; ++c) {
+                                const double v = row[c];
+                                wd[c] |= (uint32_t)(v == 1.0) << k;
+                                bl[c] |= (uint8_t)!(v == 0.0 || v == 1.0);
+                            }
+                        }
+                        for (int c = 0; c < ncols; ++c) bits[(size_t)c * nwords + w0 / 32] = wd[c];
+                    }
+                }
+                for (int c = 0; c < ncols; ++c) bad[t][c] = bl[c];
+            });
+        for (auto& x : th) x.join();
+        for (int c = 0; c < ncols; ++c) {
+            uint8_t x = 0;
+            for (int t = 0; t < nt; ++t) x |= bad[t][c];
+            binary[c] = !x;
+        }
+        return SGLM_OK;
+    }
     for (int t = 0; t < nt; ++t)
         th.emplace_back([=, &bad] {
             for (int64_t q = t; q < nchunks; q += nt) {
@@ -241,5 +282,84 @@ extern "C" int sglm_host_pack_bits_cols(const void* const* src, const int64_t* s
         for (int t = 0; t < nt; ++t) b |= bad[t][c];
         binary[c] = !b;
     }
+    return SGLM_OK;
+}
+
+extern "C" int sglm_host_group_rows(const int64_t* gidx, int64_t n, const uint8_t* side,
+                                    int32_t nsplits, int64_t G, int64_t* const* out,
+                                    const int64_t* len, int32_t nthreads) {
+    if (nsplits <= 0 || n <= 0) return SGLM_OK;
+    if (!gidx || !side || !out || !len || G <= 0) {
+        sglm::set_error("sglm_host_group_rows: bad args");
+        return SGLM_EINVAL;
+    }
+    // threads own row ranges: pass 1 counts each range's rows per list (and checks the group
+    // index), the offsets are a prefix over the ranges, pass 2 writes every list's rows of the
+    // range in ascending order
+    const int nj = 2 * nsplits;
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(nthreads, (n + 65535) / 65536));
+    std::vector<int64_t> cnt((size_t)nt * nj, 0);
+    std::vector<int> bad(nt, 0);
+    auto range = [n, nt](int t, int64_t& a, int64_t& b) {
+        a = n * t / nt;
+        b = n * (t + 1) / nt;
+    };
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([=, &cnt, &bad] {
+            int64_t a, b;
+            range(t, a, b);
+            int64_t* c = cnt.data() + (size_t)t * nj;
+            for (int64_t i = a; i < b; ++i)
+                if ((uint64_t)gidx[i] >= (uint64_t)G) { bad[t] = 1; return; }
+            for (int k = 0; k < nsplits; ++k) {
+                const uint8_t* sd = side + (int64_t)k * G;
+                int64_t c1 = 0, c2 = 0;
+                for (int64_t i = a; i < b; ++i) {
+                    const uint8_t v = sd[gidx[i]];
+                    c1 += v == 1;
+                    c2 += v == 2;
+                }
+                c[2 * k] = c1;
+                c[2 * k + 1] = c2;
+            }
+        });
+    for (auto& x : th) x.join();
+    th.clear();
+    for (int t = 0; t < nt; ++t)
+        if (bad[t]) {
+            sglm::set_error("sglm_host_group_rows: group index outside [0, %lld)", (long long)G);
+            return SGLM_EINVAL;
+        }
+    std::vector<int64_t> off((size_t)nt * nj);
+    for (int j = 0; j < nj; ++j) {
+        int64_t o = 0;
+        for (int t = 0; t < nt; ++t) {
+            off[(size_t)t * nj + j] = o;
+            o += cnt[(size_t)t * nj + j];
+        }
+        if (o != len[j]) {
+            sglm::set_error("sglm_host_group_rows: list %d has %lld rows, len %lld", j,
+                            (long long)o, (long long)len[j]);
+            return SGLM_EINVAL;
+        }
+        if (o && !out[j]) { sglm::set_error("sglm_host_group_rows: null list %d", j); return SGLM_EINVAL; }
+    }
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([=, &off] {
+            int64_t a, b;
+            range(t, a, b);
+            for (int k = 0; k < nsplits; ++k) {
+                const uint8_t* sd = side + (int64_t)k * G;
+                int64_t* o1 = out[2 * k] + off[(size_t)t * nj + 2 * k];
+                int64_t* o2 = out[2 * k + 1] + off[(size_t)t * nj + 2 * k + 1];
+                for (int64_t i = a; i < b; ++i) {
+                    const uint8_t v = sd[gidx[i]];
+                    if (v == 1) *o1++ = i;
+                    else if (v == 2) *o2++ = i;
+                }
+            }
+        });
+    for (auto& x : th) x.join();
     return SGLM_OK;
 }

@@ -62,15 +62,33 @@ def group_shuffle_split(groups, n_splits, test_size, random_state=None):
     n_train, n_test = _validate(len(classes), test_size)
     G = len(classes)
     # the permutations in order (the RNG stream), then the row lists
-    sides = []
-    for _ in range(int(n_splits)):
+    S = int(n_splits)
+    side = np.zeros((max(S, 1), G), dtype=np.uint8)
+    for k in range(S):
         perm = rng.permutation(G)
-        is_tr = np.zeros(G, bool)
-        is_tr[perm[n_test:n_test + n_train]] = True
-        is_te = np.zeros(G, bool)
-        is_te[perm[:n_test]] = True
-        sides.append((is_tr, is_te))
-    return [(np.flatnonzero(tr[gidx]), np.flatnonzero(te[gidx])) for tr, te in sides]
+        side[k, perm[n_test:n_test + n_train]] = 1
+        side[k, perm[:n_test]] = 2
+    return _group_rows(np.ascontiguousarray(gidx, dtype=np.int64), side[:S], G)
+
+
+def _group_rows(gidx, side, G):
+    """Per split, (flatnonzero(side[gidx] == 1), flatnonzero(side[gidx] == 2)): the train / test
+    row lists, built by the library's host code (sglm_host_group_rows, one thread per list)."""
+    import ctypes
+    from . import _lib
+    from .engine import HOST_THREADS
+    S, n = side.shape[0], gidx.size
+    if S == 0:
+        return []
+    cnt = np.bincount(gidx, minlength=G)[:G]
+    lens = np.array([int(cnt[side[k] == v].sum()) for k in range(S) for v in (1, 2)],
+                    dtype=np.int64)
+    outs = [np.empty(int(L), dtype=np.int64) for L in lens]
+    ptrs = (ctypes.c_void_p * len(outs))(*[o.ctypes.data for o in outs])
+    side = np.ascontiguousarray(side)
+    _lib.call("sglm_host_group_rows", gidx.ctypes.data, n, side.ctypes.data, S, G,
+              ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data, HOST_THREADS)
+    return [(outs[2 * k], outs[2 * k + 1]) for k in range(S)]
 
 
 def cv_idx_from_bucket_ids(bucket_ids, X=None, y=None, num_folds=None, test_size=None):
@@ -99,16 +117,21 @@ def trial_keys_codes(df, id_cols, package_style=False):
     cols = [df[c] for c in id_cols]
     if cols and all(isinstance(c.dtype, np.dtype) and c.dtype.kind in "biuf" for c in cols):
         invs, strs = [], []
+        runs = None
         for c in cols:
             v = c.to_numpy()
             if v.size > 1 and bool(np.all(v[1:] >= v[:-1])):
-                # non-decreasing ids (trial counters): distinct values at the change points
+                # non-decreasing ids (trial counters): distinct values at the change points,
+                # the inverse as run lengths (expanded only for a multi-column key)
                 chg = np.empty(v.size, dtype=bool)
                 chg[0] = True
                 np.not_equal(v[1:], v[:-1], out=chg[1:])
-                inv = np.cumsum(chg) - 1
-                u = v[chg]
+                at = np.flatnonzero(chg)
+                u = v[at]
+                runs = np.diff(at, append=v.size)
+                inv = runs if len(cols) == 1 else np.repeat(np.arange(at.size), runs)
             else:
+                runs = None
                 inv, u = pd.factorize(v, use_na_sentinel=False)          # hash, O(n)
             if c.dtype in (np.float64, np.int64):
                 # Python's str of the float64 / int64 values: what Series.astype(str) and
@@ -118,7 +141,7 @@ def trial_keys_codes(df, id_cols, package_style=False):
                 su = pd.Series(u, dtype=c.dtype)
                 strs.append(np.asarray((su.apply(str) if package_style else su.astype(str)),
                                        dtype=object))
-            invs.append(inv.astype(np.int64))
+            invs.append(inv if runs is not None else inv.astype(np.int64))
         if len(invs) == 1:
             tup, row_of = np.arange(strs[0].size)[:, None], invs[0]
         else:
@@ -144,6 +167,8 @@ def trial_keys_codes(df, id_cols, package_style=False):
         # distinct tuples can share a key only if two values print alike: keep pandas' codes
         if len(set(keys.tolist())) == keys.size:
             dt = np.int8 if keys.size < 128 else (np.int16 if keys.size < 32768 else np.int32)
+            if len(invs) == 1 and runs is not None:
+                return pd.Series(np.repeat(rank.astype(dt), runs), index=df.index)
             return pd.Series(rank[row_of].astype(dt), index=df.index)
     bucket = None
     for i, idc in enumerate(id_cols):

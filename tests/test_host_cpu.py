@@ -141,6 +141,43 @@ def test_native_host_masks_vs_python():
         E.host_masks([(np.array([-n - 1, 3]), False)], n, ld)
 
 
+@pytest.mark.parametrize("layout", ["block", "columns", "block_subset"])
+def test_host_pack_bits_cols(layout):
+    """sglm_host_pack_bits_cols (host code, no GPU; the 0/1 event columns of a lagged frame
+    cross PCIe as bit-planes): the row-major block path (a DataFrame of a C-order array) and the
+    per-column path give np.packbits of (v == 1.0), and the 0/1 flag is cleared by NaN, 0.5
+    and 2.0 but not by -0.0; row counts not a multiple of 32 or of the 2048-row chunks."""
+    import pandas as pd
+    from sglm_hip import _lib
+    rng = np.random.default_rng(5)
+    N, m = 70_001, 11
+    E = (rng.random((N, m)) < 0.3).astype(np.float64)
+    E[17, 2] = np.nan
+    E[N - 1, 4] = 0.5
+    E[4099, 6] = 2.0
+    E[123, 8] = -0.0
+    if layout == "columns":
+        df = pd.DataFrame({f"e{a}": E[:, a].copy() for a in range(m)})
+    else:
+        df = pd.DataFrame(E, columns=[f"e{a}" for a in range(m)])
+    cols = list(df.columns) if layout != "block_subset" else ["e3", "e5", "e4"]
+    arrs = [df[c].to_numpy() for c in cols]
+    k = len(arrs)
+    nw = (N + 31) // 32
+    bits = np.zeros(k * nw, np.uint32)
+    binary = np.zeros(k, np.uint8)
+    ptrs = (ctypes.c_void_p * k)(*[a.ctypes.data for a in arrs])
+    strides = np.array([a.strides[0] // 8 for a in arrs], dtype=np.int64)
+    _lib.call("sglm_host_pack_bits_cols", ctypes.cast(ptrs, ctypes.c_void_p),
+              strides.ctypes.data, k, N, bits.ctypes.data, binary.ctypes.data, 4)
+    V = np.stack(arrs)
+    ref = np.packbits(V == 1.0, axis=1, bitorder="little")
+    ref = np.ascontiguousarray(np.pad(ref, ((0, 0), (0, 4 * nw - ref.shape[1])))).view(np.uint32)
+    np.testing.assert_array_equal(bits.reshape(k, nw), ref)
+    want = [bool(np.all((v == 0.0) | (v == 1.0))) for v in V]
+    np.testing.assert_array_equal(binary.astype(bool), want)
+
+
 def test_negative_fold_indices_wrap_like_numpy():
     """X[idx_train] (backend/sglm_cv.py:107-110) wraps indices in [-n, 0); the native mask
     builder, the Python mask builders and the row counts do the same."""
@@ -208,3 +245,28 @@ def test_row_slabs_cover_the_rows(n, world):
         assert all(b[0] % 64 == 0 for b in sl[1:])
     if n >= 64 * world:
         assert all(abs((e - s) - n / world) <= 64 for s, e in sl)
+
+
+def test_group_rows_native_vs_numpy():
+    """folds._group_rows (sglm_host_group_rows, host code) = flatnonzero(side[gidx] == 1 / 2)
+    per split, for unsorted group indices and groups on neither side; a bad group index and a
+    wrong list length are errors."""
+    from sglm_hip import _lib, folds
+    rng = np.random.default_rng(2)
+    G, n = 997, 200_003
+    gidx = rng.integers(0, G, n).astype(np.int64)
+    side = rng.integers(0, 3, (4, G)).astype(np.uint8)
+    got = folds._group_rows(gidx, side, G)
+    for k, (tr, te) in enumerate(got):
+        np.testing.assert_array_equal(tr, np.flatnonzero(side[k][gidx] == 1))
+        np.testing.assert_array_equal(te, np.flatnonzero(side[k][gidx] == 2))
+    bad = gidx.copy()
+    bad[n // 2] = G
+    with pytest.raises(Exception, match="outside"):
+        folds._group_rows(bad, side, G)
+    out = np.empty(3, dtype=np.int64)
+    ptrs = (ctypes.c_void_p * 2)(out.ctypes.data, out.ctypes.data)
+    lens = np.array([3, 3], dtype=np.int64)
+    with pytest.raises(Exception, match="len"):
+        _lib.call("sglm_host_group_rows", gidx.ctypes.data, n, side.ctypes.data, 1, G,
+                  ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data, 4)
