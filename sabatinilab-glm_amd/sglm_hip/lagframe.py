@@ -142,11 +142,13 @@ class LagFrame:
     assigned to this frame (``overlay``); rows = positions into the base (None = all)."""
 
     def __init__(self, src: LagSource, cols, spec, rows: Optional[np.ndarray] = None,
-                 index: Optional[pd.Index] = None, overlay: Optional[dict] = None):
+                 index: Optional[pd.Index] = None, overlay: Optional[dict] = None,
+                 inc: bool = False):
         self._src = src
         self._cols = list(cols)
         self._spec = spec
         self._rows = rows
+        self._inc = rows is None or inc     # rows known to be strictly increasing
         self._index = index
         self._overlay = overlay if overlay is not None else {}
         self._design = None
@@ -193,7 +195,8 @@ class LagFrame:
     def index(self):
         if self._index is None:
             b = self._src.base.index
-            self._index = b if self._rows is None else b[self._rows]
+            sp = self._span()
+            self._index = b if self._rows is None else (b[sp[0]:sp[1]] if sp else b[self._rows])
         return self._index
 
     @property
@@ -235,6 +238,18 @@ class LagFrame:
     def __contains__(self, c):
         return c in self._spec or c in self._overlay
 
+    def _span(self):
+        """(a, b) when this frame's rows are the base rows a .. b - 1 in order, else None --
+        O(1): the rows of boolean-mask / dropna selections are known to be increasing, and an
+        increasing list spanning b - a rows is the range (the NaN-row filter's result)."""
+        if self._rows is None:
+            return (0, self._src.N)
+        r = self._rows
+        if not self._inc or r.size == 0:
+            return None
+        a, b = int(r[0]), int(r[-1]) + 1
+        return (a, b) if b - a == r.size else None
+
     def positions(self):
         """Row positions into the base frame (int64)."""
         if self._rows is not None:
@@ -244,21 +259,23 @@ class LagFrame:
         return self._src.all_rows
 
     # ------------------------------------------------------------------ derived frames
-    def _derive(self, cols=None, rows=None, index=None, keep_rows=True):
+    def _derive(self, cols=None, rows=None, index=None, keep_rows=True, inc=False):
         ov = self._overlay
         if rows is not None:
             ov = {k: v[rows] for k, v in ov.items()}
             base_rows = self.positions()[rows]
+            inc = inc and self._inc
         else:
             base_rows = self._rows
+            inc = self._inc
         cols = self._cols if cols is None else list(cols)
         ov = {k: v for k, v in ov.items() if k in cols}
         return LagFrame(self._src, cols, self._spec, base_rows,
                         index if index is not None else (self._index if rows is None else None),
-                        dict(ov))
+                        dict(ov), inc=inc)
 
-    def _take(self, pos):
-        return self._derive(rows=np.asarray(pos, dtype=np.int64))
+    def _take(self, pos, inc=False):
+        return self._derive(rows=np.asarray(pos, dtype=np.int64), inc=inc)
 
     def _bool_rows(self, mask):
         if isinstance(mask, pd.Series):
@@ -268,7 +285,7 @@ class LagFrame:
         mask = np.asarray(mask, dtype=bool).reshape(-1)
         if mask.size != self._nrows():
             raise ValueError(f"Item wrong length {mask.size} instead of {self._nrows()}.")
-        return self._take(np.flatnonzero(mask))
+        return self._take(np.flatnonzero(mask), inc=True)
 
     def _check_cols(self, cols):
         missing = [c for c in cols if c not in self._spec and c not in self._overlay]
@@ -316,12 +333,12 @@ class LagFrame:
 
     def copy(self, deep=True):
         return LagFrame(self._src, self._cols, self._spec, self._rows, self._index,
-                        {k: v.copy() for k, v in self._overlay.items()})
+                        {k: v.copy() for k, v in self._overlay.items()}, inc=self._inc)
 
     def reset_index(self, drop=False, **kw):
         if drop and not kw:
             return LagFrame(self._src, self._cols, self._spec, self._rows,
-                            pd.RangeIndex(self._nrows()), dict(self._overlay))
+                            pd.RangeIndex(self._nrows()), dict(self._overlay), inc=self._inc)
         return getattr(self.to_pandas(), "reset_index")(drop=drop, **kw)
 
     def drop(self, labels=None, axis=0, columns=None, **kw):
@@ -351,7 +368,7 @@ class LagFrame:
         cols = self._cols if subset is None else list(subset)
         cnt = self.nan_counts(cols)
         keep = cnt == 0 if how == "any" else cnt < len(cols)
-        return self._take(np.flatnonzero(keep))
+        return self._take(np.flatnonzero(keep), inc=True)
 
     def nan_counts(self, cols=None) -> np.ndarray:
         """Per row of this frame, the number of NaN cells among ``cols`` (default: all): lag
@@ -389,7 +406,14 @@ class LagFrame:
         sh = np.array(sorted(lag), dtype=np.int64)
         w = np.array([len(lag[s]) for s in sh], dtype=np.int64)
         smin, smax = int(sh[0]), int(sh[-1])
-        edge = np.flatnonzero((pos < max(smax, 0)) | (pos >= N + min(smin, 0)))
+        sp = self._span()
+        lo, hi = max(smax, 0), N + min(smin, 0)
+        if sp is not None and lo <= hi:
+            # rows a .. b - 1: the edge rows are the two ends of the range
+            a, b = sp
+            edge = np.r_[np.arange(a, min(b, lo)), np.arange(max(a, hi), b)] - a
+        else:
+            edge = np.flatnonzero((pos < lo) | (pos >= hi))
         if edge.size:
             u = pos[edge]
             cw = np.r_[0, np.cumsum(w)]
@@ -429,7 +453,10 @@ class LagFrame:
 
     def _base_values(self, name) -> np.ndarray:
         v = self._src.base[name].to_numpy()
-        if self._rows is not None:
+        sp = self._span()
+        if self._rows is not None and sp is not None:
+            v = v[sp[0]:sp[1]].copy()
+        elif self._rows is not None:
             v = v[self._rows]
         elif v.base is not None or not v.flags.owndata:
             v = v.copy()
@@ -535,7 +562,8 @@ class LagFrame:
         shifts = np.array([self._spec[c][1] for c in self._cols], dtype=np.int64)
         pos = self.positions()
         n = int(pos.size)
-        if n and pos[-1] - pos[0] == n - 1 and np.all(np.diff(pos) == 1):
+        sp = self._span()
+        if n and (sp is not None or (pos[-1] - pos[0] == n - 1 and np.all(np.diff(pos) == 1))):
             d = Design.from_lagged(Esub, cols, shifts, int(pos[0]), n)
         else:
             import torch

@@ -93,6 +93,19 @@ def test_lagframe_design_equals_host_design(engine):
     lf = sglm_ez.timeshift_cols(df, cols, neg_order=-4, pos_order=3)
     xcols = sglm_ez.add_timeshifts_to_col_list(cols, cols, neg_order=-4, pos_order=3)
     f1 = lf[lf[xcols].isna().sum(axis=1) == 0]
+    assert f1._span() is not None                     # the filter leaves one row range
+    import sglm_pp
+    sglm_pp.LAGFRAME = False
+    try:
+        ref = sglm_ez.timeshift_cols(df, cols, neg_order=-4, pos_order=3)
+    finally:
+        sglm_pp.LAGFRAME = True
+    r1 = ref[ref[xcols].isna().sum(axis=1) == 0]
+    assert f1.index.equals(r1.index)
+    pd.testing.assert_series_equal(f1["nTrial"], r1["nTrial"])
+    pd.testing.assert_series_equal(f1[xcols].isna().sum(axis=1),
+                                   r1[xcols].isna().sum(axis=1), check_dtype=False)
+    pd.testing.assert_frame_equal(f1.to_pandas(), r1)
     X1 = f1[xcols]
     d1 = X1.design()
     assert d1.lag is not None                         # event-correlation Gram / gradient path
