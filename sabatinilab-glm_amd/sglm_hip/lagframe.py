@@ -45,6 +45,7 @@ class LagSource:
         self._dev = {}           # column name -> row of self._E
         self._E = None
         self._hasnan = {}        # column name -> holds a NaN cell
+        self._numeric = {}       # column name -> numeric dtype
         self.cast = {}           # base column name -> dtype of its shift-0 copy in the frame
         self.all_rows = None     # arange(N), built once
 
@@ -126,9 +127,11 @@ class LagSource:
         return np.ascontiguousarray(col.to_numpy(dtype=np.float64, na_value=NAN))
 
     def numeric(self, name) -> bool:
-        dt = self.base[name].dtype
-        return (isinstance(dt, np.dtype) and dt.kind in "biuf") or \
-            pd.api.types.is_numeric_dtype(dt)
+        if name not in self._numeric:
+            dt = self.base[name].dtype
+            self._numeric[name] = (isinstance(dt, np.dtype) and dt.kind in "biuf") or \
+                pd.api.types.is_numeric_dtype(dt)
+        return self._numeric[name]
 
     def has_nan(self, name) -> bool:
         """Whether an uploaded column holds a NaN cell."""
@@ -263,7 +266,7 @@ class LagFrame:
         ov = self._overlay
         if rows is not None:
             ov = {k: v[rows] for k, v in ov.items()}
-            base_rows = self.positions()[rows]
+            base_rows = rows if self._rows is None else self._rows[rows]
             inc = inc and self._inc
         else:
             base_rows = self._rows
@@ -427,7 +430,8 @@ class LagFrame:
             return out
         E, idx = self._src.device(names)
         row_of = {nm: int(r) for nm, r in zip(names, idx.tolist())}
-        pos_d = torch.from_numpy(pos).to("cuda")
+        pos_d = torch.arange(sp[0], sp[1], dtype=torch.int64, device="cuda") if sp is not None \
+            else torch.from_numpy(pos).to("cuda")
         acc = torch.zeros(n, dtype=torch.int64, device="cuda")
         for s, nms in lag.items():
             nn = [x for x in nms if self._src.has_nan(x)]

@@ -33,6 +33,10 @@ def main():
     pr.disable()
     pstats.Stats(pr).sort_stats("tottime").print_stats(25)
     pstats.Stats(pr).sort_stats("cumtime").print_stats(45)
+    st = pstats.Stats(pr).sort_stats("cumtime")
+    for fn in ("nan_counts", "_lag_nan_counts", "device", "design", "from_events",
+               "trial_keys_codes", "group_shuffle_split", "_run", "run_multi"):
+        st.print_callees(fn)
 
 
 if __name__ == "__main__":

@@ -18,9 +18,11 @@ def main():
     s = synth.make(N=rows, m=50, L=20, family="poisson", rho=0.02, seed=0)
     d = E.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
     rng = np.random.default_rng(1)
-    m = (rng.random(d.n) < keep).astype(np.uint8)
-    prob = E.Problem(d, [np.zeros(d.n)], [m])
-    cb = prob.compact(0)
+    nm = int(os.environ.get("SWEEP_MASKS", 1))       # distinct row masks, dealt to slots k % nm
+    ms = [(rng.random(d.n) < keep).astype(np.uint8) for _ in range(nm)]
+    prob = E.Problem(d, [np.zeros(d.n)], ms)
+    cbs = [prob.compact(i) for i in range(nm)]
+    cb = max(cbs, key=lambda c: c[1])
     Bmax = 30
     stride = max(64, (cb[1] + 63) // 64 * 64)
     g = torch.Generator(device="cuda").manual_seed(0)
@@ -28,20 +30,22 @@ def main():
     W[:, : d.n] = 0.2 + torch.rand((Bmax, d.n), generator=g, device="cuda")
     wc = torch.zeros(Bmax * stride, dtype=torch.bfloat16, device="cuda")
     fits = torch.arange(Bmax, dtype=torch.int32, device="cuda")
-    desc = torch.tensor([[cb[0].data_ptr(), cb[1], wc.data_ptr() + 2 * k * stride,
-                          0 if cb[2] is None else cb[2].data_ptr()] for k in range(Bmax)],
-                        dtype=torch.int64).cuda()
+    order = sorted(range(Bmax), key=lambda k: k % nm) if os.environ.get("SWEEP_SORT", "1") == "1" \
+        else list(range(Bmax))
+    desc = torch.tensor([[cbs[k % nm][0].data_ptr(), cbs[k % nm][1], wc.data_ptr() + 2 * k * stride,
+                          0 if cbs[k % nm][2] is None else cbs[k % nm][2].data_ptr()]
+                         for k in order], dtype=torch.int64).cuda()
     st = torch.cuda.current_stream().cuda_stream
     _lib.call("sglm_gather_w", W.data_ptr(), d.ld, fits.data_ptr(), Bmax, desc.data_ptr(), cb[1], st)
     H = torch.zeros((Bmax, d.P, d.P), dtype=torch.float32, device="cuda")
     pa = d.p + 1
     nb = d.P // 128
     nsteps = (cb[1] + 63) // 64
-    out = {"rows": int(cb[1]), "P": d.P, "p": d.p, "nsteps": nsteps, "res": []}
+    out = {"rows": int(cb[1]), "P": d.P, "p": d.p, "nsteps": nsteps, "masks": nm, "res": []}
     for B in [int(x) for x in os.environ.get("SWEEP_FITS", "1,2,3,4,6,8,12,16,30").split(",")]:
         pick = E.syrk6_splits(nb * (nb + 1) // 2 * B, nsteps, B, d.P)
         row = {"fits": B, "pick": pick, "tf": {}}
-        for sp in (1, 2, 3, 4, 6, 8, 12, 16, 24, 32):
+        for sp in [int(x) for x in os.environ.get("SWEEP_SPLITS", "1,2,3,4,6,8,12,16,24,32").split(",")]:
             if sp > max(1, nsteps // 8):
                 break
             wb = _lib.query("sglm_syrk_work_bytes", d.P, B, sp)
