@@ -10,7 +10,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsglm_hip.so")
+# SGLM_LIB: another build of the same library (kernel-variant A/B runs)
+LIB_PATH = os.environ.get("SGLM_LIB") or os.path.join(_HERE, "libsglm_hip.so")
 
 _i32, _i64, _u64, _f32, _vp, _sz = C.c_int32, C.c_int64, C.c_uint64, C.c_float, C.c_void_p, C.c_size_t
 

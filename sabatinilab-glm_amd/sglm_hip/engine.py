@@ -1182,6 +1182,7 @@ def syrk_splits(n_tiles_total: int, nsteps: int, cus: int = 256) -> int:
 # lower bound on the Gram v6 split-K factor (shorter-lived workgroups let the other IRLS
 # group's small kernels interleave with a Gram; experiment knob)
 SYRK6_MIN_SPLIT = int(__import__("os").environ.get("SGLM_SYRK6_MIN_SPLIT", "1"))
+GRAM_LOG = None                 # a list: each Gram launch appends (nact, distinct masks, splits, rows)
 
 
 def syrk6_splits(wgs1: int, nsteps: int, nact: int, P: int, slots: int = 1024) -> int:
@@ -2400,6 +2401,8 @@ def _syrk_cbits(d: Design, bf, prob: Problem, fits: np.ndarray, st, ev=None):
         fits_d = torch.from_numpy(fits.astype(np.int32)).to(d.device)
     nb = d.P // 128
     splits = syrk6_splits(nb * (nb + 1) // 2 * nact, max(1, (maxrows + 63) // 64), nact, d.P)
+    if GRAM_LOG is not None:
+        GRAM_LOG.append((nact, len(set(masks.tolist())), splits, maxrows))
     wb = _lib.query("sglm_syrk_work_bytes", d.P, nact, splits)
     work = _work(wb, d.device) if wb else None
     _lib.call("sglm_gather_w", _p(bf.W), d.ld, _p(fits_d), nact, _p(desc_d), maxrows, st)

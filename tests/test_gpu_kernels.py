@@ -632,11 +632,12 @@ def test_eta_bits_matches_float64(engine, torch_mod):
     assert torch.equal(bd2[1], bd[1]) and torch.isnan(out_r[1]).all()
 
 
-@pytest.mark.parametrize("B", [100, 33, 7])
+@pytest.mark.parametrize("B", [100, 70, 33, 7])
 def test_eta_dir_kernel_equals_per_group_kernel(engine, torch_mod, B, monkeypatch):
-    """Direction products through the LDS-staged kernel (eta_dir_kernel: 128 fits x 256 rows
-    per workgroup, ragged fit groups) equal the per-group kernel bit for bit and X d in
-    float64 to f32 accuracy, through a slot list."""
+    """Direction products through the pipelined kernel (eta_pipe_kernel<4, 4> / <2, 8> /
+    <1, 8>: 512 / 1024 rows per workgroup, waves past the last row, ragged fit groups), the
+    LDS-staged kernel (eta_dir_kernel: 128 fits x 256 rows per workgroup) and the per-group
+    kernel agree bit for bit, and X d in float64 to f32 accuracy, through a slot list."""
     torch = torch_mod
     from sglm_hip import _lib, synth
     s = synth.make(N=20000, m=30, L=6, rho=0.05, seed=B)
@@ -650,15 +651,18 @@ def test_eta_dir_kernel_equals_per_group_kernel(engine, torch_mod, B, monkeypatc
     work = torch.empty(_lib.query("sglm_eta_bits_work_bytes", d.P, B), dtype=torch.uint8,
                        device="cuda")
     outs = {}
-    for v in ("1", "0"):
-        monkeypatch.setenv("SGLM_ETA_DIR", v)
+    assert d.ld % 512 == 256                          # dead waves in the last workgroup
+    for v, (pipe, dr) in {"pipe": ("1", "0"), "dir": ("0", "1"), "group": ("0", "0")}.items():
+        monkeypatch.setenv("SGLM_ETA_PIPE", pipe)
+        monkeypatch.setenv("SGLM_ETA_DIR", dr)
         bd = torch.from_numpy(beta).cuda()
         out = torch.full((nb, d.ld), float("nan"), dtype=torch.float32, device="cuda")
         _lib.call("sglm_gemv_eta_bits", d.rbits.data_ptr(), d.ld, d.P, bd.data_ptr(), B,
                   sl.data_ptr(), 0, out.data_ptr(), work.data_ptr(), 0)
         outs[v] = (out.cpu().numpy(), bd.cpu().numpy())
-    got, br = outs["1"]
-    assert np.array_equal(got, outs["0"][0], equal_nan=True)
+    got, br = outs["pipe"]
+    assert np.array_equal(got, outs["group"][0], equal_nan=True)
+    assert np.array_equal(outs["dir"][0], outs["group"][0], equal_nan=True)
     X = d.xb.double().cpu().numpy()
     for k in slots[:12]:
         ref = br[k].astype(np.float64) @ X

@@ -17,6 +17,8 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "sabatinilab-glm_amd")]
 
 VARIANTS = {
     "eta": [("dir", {"SGLM_ETA_DIR": "1"}), ("group", {"SGLM_ETA_DIR": "0"})],
+    "etap": [("pipe", {"SGLM_ETA_PIPE": "1"}), ("dir", {"SGLM_ETA_PIPE": "0", "SGLM_ETA_DIR": "1"}),
+             ("group", {"SGLM_ETA_PIPE": "0", "SGLM_ETA_DIR": "0"})],
     "eta3": [("staged", {"SGLM_ETA_EXACT_STAGED": "1"}), ("group", {"SGLM_ETA_EXACT_STAGED": "0"})],
     "xtr": [("ngw2", {"SGLM_XTR4": "1", "SGLM_XTR_NGW": "2", "SGLM_XTR_PIPE": "0"}),
             ("pipe2", {"SGLM_XTR4": "1", "SGLM_XTR_NGW": "2", "SGLM_XTR_PIPE": "1"}),
@@ -39,7 +41,7 @@ def main():
     for B in sizes:
         rng = np.random.default_rng(B)
         slots = torch.arange(B, dtype=torch.int32, device="cuda")
-        if what in ("eta", "eta3"):
+        if what in ("eta", "etap", "eta3"):
             beta = torch.from_numpy(rng.normal(size=(B, d.P)).astype(np.float32)).cuda()
             out = torch.zeros((B, d.ld), dtype=torch.float32, device="cuda")
             work = torch.empty(_lib.query("sglm_eta_bits_work_bytes", d.P, B),
