@@ -397,6 +397,27 @@ class LagFrame:
             cnt += self._lag_nan_counts(lag)
         return cnt
 
+    def _any_nan(self) -> bool:
+        """Whether any cell of this frame is NaN.  A row range whose lag columns read only
+        base rows inside the base, from numeric sources without NaN, has none (O(1) after the
+        upload); anything else counts per row."""
+        sp = self._span()
+        specs = [self._spec.get(c) for c in self._cols]
+        if sp is None or self._overlay or any(sc is None or not self._src.numeric(sc[0])
+                                              for sc in specs):
+            return bool(self.nan_counts().any())
+        if not specs:
+            return False
+        sh = [sc[1] for sc in specs]
+        a, b = sp
+        if a - max(max(sh), 0) < 0 or b - 1 - min(min(sh), 0) > self._src.N - 1:
+            return bool(self.nan_counts().any())
+        names = sorted({sc[0] for sc in specs}, key=str)
+        self._src.device(names)
+        if any(self._src.has_nan(nm) for nm in names):
+            return bool(self.nan_counts().any())
+        return False
+
     def _lag_nan_counts(self, lag) -> np.ndarray:
         """NaN lag cells per row; ``lag``: shift -> source names (one per lag column).  A
         cell is NaN when its source row u - s is outside the base (counted on the host from
@@ -552,8 +573,7 @@ class LagFrame:
         if self._overlay:
             self._design = Design.from_host(self.to_numpy(dtype=np.float64))
             return self._design
-        bad = self.nan_counts()
-        if bad.any():
+        if self._any_nan():
             raise ValueError("Input X contains NaN.")
         srcs = [self._spec[c][0] for c in self._cols]
         names = sorted(set(srcs), key=str)
