@@ -50,13 +50,20 @@ def group_shuffle_split(groups, n_splits, test_size, random_state=None):
         rng = np.random.RandomState(random_state)
     groups = np.asarray(groups)
     lo = int(groups.min()) if groups.size and groups.dtype.kind in "iu" else 0
+    cnt = None
     if groups.size and groups.dtype.kind in "iu" and int(groups.max()) - lo < 4 * groups.size:
         # small-range integer ids (categorical codes): the same classes / inverse by counting
-        g0 = groups.astype(np.int64) - lo
-        present = np.bincount(g0) > 0
-        classes = np.flatnonzero(present) + lo
-        lookup = np.cumsum(present) - 1
-        gidx = lookup[g0]
+        g0 = groups.astype(np.int64)
+        if lo:
+            g0 -= lo
+        cnt = np.bincount(g0)
+        present = cnt > 0
+        if present.all():                     # dense codes 0 .. G-1: the inverse is the code
+            classes, gidx = np.arange(cnt.size) + lo, g0
+        else:
+            classes = np.flatnonzero(present) + lo
+            gidx = (np.cumsum(present) - 1)[g0]
+            cnt = cnt[present]
     else:
         classes, gidx = np.unique(groups, return_inverse=True)
     n_train, n_test = _validate(len(classes), test_size)
@@ -68,10 +75,10 @@ def group_shuffle_split(groups, n_splits, test_size, random_state=None):
         perm = rng.permutation(G)
         side[k, perm[n_test:n_test + n_train]] = 1
         side[k, perm[:n_test]] = 2
-    return _group_rows(np.ascontiguousarray(gidx, dtype=np.int64), side[:S], G)
+    return _group_rows(np.ascontiguousarray(gidx, dtype=np.int64), side[:S], G, cnt)
 
 
-def _group_rows(gidx, side, G):
+def _group_rows(gidx, side, G, cnt=None):
     """Per split, (flatnonzero(side[gidx] == 1), flatnonzero(side[gidx] == 2)): the train / test
     row lists, built by the library's host code (sglm_host_group_rows, one thread per list)."""
     import ctypes
@@ -80,7 +87,8 @@ def _group_rows(gidx, side, G):
     S, n = side.shape[0], gidx.size
     if S == 0:
         return []
-    cnt = np.bincount(gidx, minlength=G)[:G]
+    if cnt is None:
+        cnt = np.bincount(gidx, minlength=G)[:G]
     lens = np.array([int(cnt[side[k] == v].sum()) for k in range(S) for v in (1, 2)],
                     dtype=np.int64)
     outs = [np.empty(int(L), dtype=np.int64) for L in lens]

@@ -270,3 +270,21 @@ def test_group_rows_native_vs_numpy():
     with pytest.raises(Exception, match="len"):
         _lib.call("sglm_host_group_rows", gidx.ctypes.data, n, side.ctypes.data, 1, G,
                   ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data, 4)
+
+
+@pytest.mark.parametrize("kind", ["dense", "gaps", "offset", "float"])
+def test_group_shuffle_split_id_kinds_vs_sklearn(kind):
+    """folds.group_shuffle_split on dense codes, integer ids with gaps, ids not starting at 0
+    and float ids == sklearn GroupShuffleSplit on the same global RNG state."""
+    from sklearn.model_selection import GroupShuffleSplit
+    from sglm_hip import folds
+    rng = np.random.default_rng(4)
+    g = np.sort(rng.integers(0, 60, 5000))
+    g = {"dense": np.unique(g, return_inverse=True)[1].astype(np.int16), "gaps": g * 3,
+         "offset": g + 1000, "float": g.astype(np.float64) / 7}[kind]
+    np.random.seed(9)
+    got = folds.group_shuffle_split(g, 4, 0.25)
+    np.random.seed(9)
+    ref = list(GroupShuffleSplit(n_splits=4, test_size=0.25).split(g, None, g))
+    for (a, b), (c, d) in zip(got, ref):
+        assert np.array_equal(a, c) and np.array_equal(b, d)
