@@ -322,38 +322,42 @@ eta_dir_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
     }
 }
 
-// eta_dir_kernel<1, NG> deepened (eta_pipe_kernel): each wave covers NT 32-row tiles, so a
-// staged direction fragment feeds NT MFMAs (eta_dir_kernel: 2) and a workgroup's direction
-// tile crosses L2 once per 4 x NT x 32 rows; one wave per SIMD (the NG x NT accumulator tiles
-// fill the AGPRs), its latency covered by the loads instead of a second wave: the bit words are
-// loaded two K-steps ahead through a three-set register ring and the next step's direction
-// tile one step ahead (all loads in asm with static vmcnt counts -- loads for absent fit
-// groups and past the last step re-read valid addresses), one barrier per K-step.  Same
-// products and f32 accumulation order per (fit, row) as eta_bits_kernel<1, .>: bitwise equal.
-template <int NG, int NT>
+// eta_dir_kernel deepened (eta_pipe_kernel<NP, NG, NT>): each wave covers NT 32-row tiles, so
+// a staged coefficient fragment feeds NT MFMAs (eta_dir_kernel: 2) and a workgroup's
+// coefficient tile crosses L2 once per 4 x NT x 32 rows; one wave per SIMD (the accumulator
+// tiles fill the AGPRs), its latency covered by the loads instead of a second wave: the bit
+// words are loaded two K-steps ahead through a three-set register ring and the next step's
+// coefficient tile one step ahead (all loads in asm with static vmcnt counts -- loads for
+// absent fit groups and past the last step re-read valid addresses), one barrier per K-step.
+// NP = 1 (rounded directions): the products and f32 accumulation order per (fit, row) of
+// eta_bits_kernel<1, .> -- bitwise equal; NP = 3 (exact coefficients): those of
+// eta_dir_kernel<3, .>, a hi accumulator and a mid + lo one -- bitwise equal to it.
+template <int NT>
 struct EtaRing {
     u32x2 b[NT];
 };
 
-template <int NG, int NT>
-__device__ __forceinline__ void eta_ring_load(EtaRing<NG, NT>& t, g_uint2* pb, int64_t ld, int s) {
+template <int NT>
+__device__ __forceinline__ void eta_ring_load(EtaRing<NT>& t, g_uint2* pb, int64_t ld, int s) {
 #pragma unroll
     for (int n = 0; n < NT; ++n) t.b[n] = gld2(pb + (int64_t)s * ld + 32 * n);
 }
 
-template <int NG, int NT>
-__device__ __forceinline__ void eta_ring_tie(EtaRing<NG, NT>& t) {
+template <int NT>
+__device__ __forceinline__ void eta_ring_tie(EtaRing<NT>& t) {
 #pragma unroll
     for (int n = 0; n < NT; ++n) asm volatile("" : "+v"(t.b[n]));
 }
 
-template <int NG, int NT>
+template <int NP, int NG, int NT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 eta_pipe_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
                 const __bf16* __restrict__ Dp, int32_t Bp, int32_t B,
                 const int32_t* __restrict__ slots, float* __restrict__ eta) {
     constexpr int kF = NG * 32;
-    __shared__ __attribute__((aligned(16))) char lds[2][kF * kEDS];
+    constexpr int kJ = NP * NG;                  // staging chunks per thread
+    constexpr int kA = NP == 1 ? 1 : 2;          // accumulator sets
+    __shared__ __attribute__((aligned(16))) char lds[2][NP * kF * kEDS];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
     const int64_t row0 = (int64_t)blockIdx.x * (4 * NT * 32) + wave * (NT * 32);
     const bool live = row0 < ld;                        // wave-uniform (ld % 128 == 0)
@@ -361,34 +365,41 @@ eta_pipe_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
     const int ng = min(NG, Bp / 32 - gb);
     const int nsteps = P / 64, last = nsteps - 1;
     g_uint2* pb = as_global<g_uint2>(rbits + (live ? row0 : 0) + r);
-    // staging chunk gi of this thread: fit (tid >> 3) + 32 gi (group 0's row for an absent
-    // group), 16-B piece tid & 7 of the fit's 64-k segment of the step
+    // staging chunk j of this thread: piece j / NG, fit (tid >> 3) + 32 (j % NG) (group 0's
+    // row for an absent group), 16-B part tid & 7 of the fit's 64-k segment of the step
     const char* dbase = reinterpret_cast<const char*>(Dp) + (tid & 7) * 16;
-    int64_t doff[NG];
+    const int64_t pstride = (int64_t)Bp * P * 2;
+    int64_t doff[kJ];
 #pragma unroll
-    for (int gi = 0; gi < NG; ++gi)
-        doff[gi] = (int64_t)((gb + (gi < ng ? gi : 0)) * 32 + (tid >> 3)) * P * 2;
+    for (int j = 0; j < kJ; ++j) {
+        const int gi = j % NG;
+        doff[j] = (j / NG) * pstride +
+                  (int64_t)((gb + (gi < ng ? gi : 0)) * 32 + (tid >> 3)) * P * 2;
+    }
     const int lbase = (tid >> 3) * kEDS + (tid & 7) * 16;
-    u32x4 dv[NG];
+    u32x4 dv[kJ];
     auto dload = [&](int st) {
 #pragma unroll
-        for (int gi = 0; gi < NG; ++gi)
-            dv[gi] = gld4(as_global<g_uint4>(dbase + doff[gi] + (int64_t)st * 128));
+        for (int j = 0; j < kJ; ++j)
+            dv[j] = gld4(as_global<g_uint4>(dbase + doff[j] + (int64_t)st * 128));
     };
     auto dstore = [&](int buf) {
 #pragma unroll
-        for (int gi = 0; gi < NG; ++gi) {
-            asm volatile("" : "+v"(dv[gi]));
-            *reinterpret_cast<u32x4*>(&lds[buf][lbase + 32 * gi * kEDS]) = dv[gi];
+        for (int j = 0; j < kJ; ++j) {
+            asm volatile("" : "+v"(dv[j]));
+            *reinterpret_cast<u32x4*>(
+                &lds[buf][lbase + ((j / NG) * kF + 32 * (j % NG)) * kEDS]) = dv[j];
         }
     };
-    f32x16 acc[NG][NT];
+    f32x16 acc[kA][NG][NT];
 #pragma unroll
-    for (int gi = 0; gi < NG; ++gi)
+    for (int a = 0; a < kA; ++a)
 #pragma unroll
-        for (int n = 0; n < NT; ++n) acc[gi][n] = (f32x16){};
+        for (int gi = 0; gi < NG; ++gi)
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[a][gi][n] = (f32x16){};
 
-    auto compute = [&](const EtaRing<NG, NT>& t, int buf) {
+    auto compute = [&](const EtaRing<NT>& t, int buf) {
         const char* lb = &lds[buf][r * kEDS + h * 16];
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
@@ -396,22 +407,30 @@ eta_pipe_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
 #pragma unroll
             for (int n = 0; n < NT; ++n) bx[n] = frag_two(t.b[n], ks, h);
 #pragma unroll
-            for (int gi = 0; gi < NG; ++gi) {
-                if (gi < ng) {
-                    const bf16x8 a = __builtin_bit_cast(
-                        bf16x8, *reinterpret_cast<const u32x4*>(lb + gi * 32 * kEDS + 32 * ks));
+            for (int pc = 0; pc < NP; ++pc)
 #pragma unroll
-                    for (int n = 0; n < NT; ++n)
-                        acc[gi][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bx[n], acc[gi][n],
-                                                                            0, 0, 0);
+                for (int gi = 0; gi < NG; ++gi) {
+                    if (gi < ng) {
+                        const bf16x8 a = __builtin_bit_cast(
+                            bf16x8, *reinterpret_cast<const u32x4*>(
+                                        lb + (pc * kF + gi * 32) * kEDS + 32 * ks));
+                #pragma unroll
+                        for (int n = 0; n < NT; ++n) {
+                            if (pc == 0)
+                                acc[0][gi][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                                    a, bx[n], acc[0][gi][n], 0, 0, 0);
+                            else
+                                acc[kA - 1][gi][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                                    a, bx[n], acc[kA - 1][gi][n], 0, 0, 0);
+                        }
+                    }
                 }
-            }
         }
     };
-    // step st on ring set `cur` (its bits landed) and LDS buffer st & 1: issue the direction
+    // step st on ring set `cur` (its bits landed) and LDS buffer st & 1: issue the coefficient
     // tile of st + 1 and the bits of st + 2 into `nn`, compute, then wait for everything but
     // the NT bit loads just issued, stage the tile, barrier
-    auto step = [&](EtaRing<NG, NT>& cur, EtaRing<NG, NT>& nxt, EtaRing<NG, NT>& nn, int st) {
+    auto step = [&](EtaRing<NT>& cur, EtaRing<NT>& nxt, EtaRing<NT>& nn, int st) {
         dload(st + 1 < last ? st + 1 : last);
         eta_ring_load(nn, pb, ld, st + 2 < last ? st + 2 : last);
         __builtin_amdgcn_sched_barrier(0);
@@ -428,7 +447,7 @@ eta_pipe_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
         __syncthreads();
     };
 
-    EtaRing<NG, NT> R0, R1, R2;
+    EtaRing<NT> R0, R1, R2;
     dload(0);
     eta_ring_load(R0, pb, ld, 0);
     eta_ring_load(R1, pb, ld, 1 < last ? 1 : last);
@@ -454,15 +473,17 @@ eta_pipe_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 const int f = (gb + gi) * 32 + (j & 3) + 8 * (j >> 2) + 4 * h;
-                if (f < B)
-                    eta[(int64_t)(slots ? slots[f] : f) * ld + row0 + n * 32 + r] =
-                        0.5f * acc[gi][n][j];
+                if (f < B) {
+                    const float v = NP == 1 ? acc[0][gi][n][j]
+                                            : acc[0][gi][n][j] + acc[kA - 1][gi][n][j];
+                    eta[(int64_t)(slots ? slots[f] : f) * ld + row0 + n * 32 + r] = 0.5f * v;
+                }
             }
     }
 }
 
-// eta_pipe_kernel for rounded directions (default; SGLM_ETA_PIPE=0 for the two-wave
-// eta_dir_kernel / one-wave eta_bits_kernel choice below; read per launch)
+// eta_pipe_kernel (default, both kinds; SGLM_ETA_PIPE=0 for the two-wave eta_dir_kernel /
+// one-wave eta_bits_kernel choices below; read per launch)
 static bool eta_pipe_on() {
     const char* e = getenv("SGLM_ETA_PIPE");
     return !(e && e[0] == '0');
@@ -1147,7 +1168,11 @@ int sglm_gemv_eta_bits(const uint32_t* rbits, int64_t ld, int32_t P, float* beta
         split3_kernel<<<gs, 256, 0, s>>>(beta, P, B, Bp, slots, Dp);
         st = check_launch("split3_kernel");
         if (st) return st;
-        if (eta_exact_staged(Bp))
+        if (eta_pipe_on())
+            eta_pipe_kernel<3, 2, 4><<<dim3((unsigned)((ld + 511) / 512), (unsigned)((Bp / 32 + 1) / 2)),
+                                       256, 0, s>>>(reinterpret_cast<const u32x2*>(rbits), ld, P,
+                                                    Dp, Bp, B, slots, eta);
+        else if (eta_exact_staged(Bp))
             eta_dir_kernel<3, 2><<<dim3((unsigned)(ld / 256), (unsigned)((Bp / 32 + 1) / 2)),
                                    256, 0, s>>>(reinterpret_cast<const u32x2*>(rbits), ld, P,
                                                 Dp, Bp, B, slots, eta);
@@ -1161,13 +1186,13 @@ int sglm_gemv_eta_bits(const uint32_t* rbits, int64_t ld, int32_t P, float* beta
         const int ngr = Bp / 32;
         const u32x2* rb = reinterpret_cast<const u32x2*>(rbits);
         if (eta_pipe_on() && ngr >= 3)
-            eta_pipe_kernel<4, 4><<<dim3((unsigned)((ld + 511) / 512), (unsigned)((ngr + 3) / 4)),
+            eta_pipe_kernel<1, 4, 4><<<dim3((unsigned)((ld + 511) / 512), (unsigned)((ngr + 3) / 4)),
                                     256, 0, s>>>(rb, ld, P, Dp, Bp, B, slots, eta);
         else if (eta_pipe_on() && ngr == 2)
-            eta_pipe_kernel<2, 8><<<dim3((unsigned)((ld + 1023) / 1024), 1u), 256, 0, s>>>(
+            eta_pipe_kernel<1, 2, 8><<<dim3((unsigned)((ld + 1023) / 1024), 1u), 256, 0, s>>>(
                 rb, ld, P, Dp, Bp, B, slots, eta);
         else if (eta_pipe_on())
-            eta_pipe_kernel<1, 8><<<dim3((unsigned)((ld + 1023) / 1024), 1u), 256, 0, s>>>(
+            eta_pipe_kernel<1, 1, 8><<<dim3((unsigned)((ld + 1023) / 1024), 1u), 256, 0, s>>>(
                 rb, ld, P, Dp, Bp, B, slots, eta);
         else if (eta_dir_on(Bp))
             eta_dir_kernel<1, 4><<<dim3((unsigned)(ld / 256), (unsigned)((Bp / 32 + 3) / 4)),

@@ -663,6 +663,22 @@ def test_eta_dir_kernel_equals_per_group_kernel(engine, torch_mod, B, monkeypatc
     got, br = outs["pipe"]
     assert np.array_equal(got, outs["group"][0], equal_nan=True)
     assert np.array_equal(outs["dir"][0], outs["group"][0], equal_nan=True)
+    # exact coefficients (three pieces): the pipelined kernel == the staged one, bit for bit
+    ex = {}
+    for v, pipe in {"pipe": "1", "staged": "0"}.items():
+        monkeypatch.setenv("SGLM_ETA_PIPE", pipe)
+        monkeypatch.setenv("SGLM_ETA_EXACT_STAGED", "1")
+        bd = torch.from_numpy(beta).cuda()
+        out = torch.full((nb, d.ld), float("nan"), dtype=torch.float32, device="cuda")
+        _lib.call("sglm_gemv_eta_bits", d.rbits.data_ptr(), d.ld, d.P, bd.data_ptr(), B,
+                  sl.data_ptr(), 1, out.data_ptr(), work.data_ptr(), 0)
+        ex[v] = out.cpu().numpy()
+    assert np.array_equal(ex["pipe"], ex["staged"], equal_nan=True)
+    X64 = d.xb.double().cpu().numpy()
+    for k in slots[:6]:
+        ref = beta[k].astype(np.float64) @ X64
+        sc = np.abs(beta[k].astype(np.float64)) @ np.abs(X64)
+        assert np.max(np.abs(ex["pipe"][k] - ref) / np.maximum(sc, 1e-30)) < 1e-6, k
     X = d.xb.double().cpu().numpy()
     for k in slots[:12]:
         ref = br[k].astype(np.float64) @ X

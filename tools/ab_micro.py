@@ -20,6 +20,8 @@ VARIANTS = {
     "etap": [("pipe", {"SGLM_ETA_PIPE": "1"}), ("dir", {"SGLM_ETA_PIPE": "0", "SGLM_ETA_DIR": "1"}),
              ("group", {"SGLM_ETA_PIPE": "0", "SGLM_ETA_DIR": "0"})],
     "eta3": [("staged", {"SGLM_ETA_EXACT_STAGED": "1"}), ("group", {"SGLM_ETA_EXACT_STAGED": "0"})],
+    "eta3p": [("pipe", {"SGLM_ETA_PIPE": "1"}), ("staged", {"SGLM_ETA_PIPE": "0",
+                                                            "SGLM_ETA_EXACT_STAGED": "1"})],
     "xtr": [("ngw2", {"SGLM_XTR4": "1", "SGLM_XTR_NGW": "2", "SGLM_XTR_PIPE": "0"}),
             ("pipe2", {"SGLM_XTR4": "1", "SGLM_XTR_NGW": "2", "SGLM_XTR_PIPE": "1"}),
             ("ngw1", {"SGLM_XTR4": "1", "SGLM_XTR_NGW": "1", "SGLM_XTR_PIPE": "0"}),
@@ -41,7 +43,7 @@ def main():
     for B in sizes:
         rng = np.random.default_rng(B)
         slots = torch.arange(B, dtype=torch.int32, device="cuda")
-        if what in ("eta", "etap", "eta3"):
+        if what in ("eta", "etap", "eta3", "eta3p"):
             beta = torch.from_numpy(rng.normal(size=(B, d.P)).astype(np.float32)).cuda()
             out = torch.zeros((B, d.ld), dtype=torch.float32, device="cuda")
             work = torch.empty(_lib.query("sglm_eta_bits_work_bytes", d.P, B),
@@ -49,7 +51,7 @@ def main():
 
             def fn():
                 _lib.call("sglm_gemv_eta_bits", d.rbits.data_ptr(), d.ld, d.P, beta.data_ptr(),
-                          B, slots.data_ptr(), int(what == "eta3"), out.data_ptr(),
+                          B, slots.data_ptr(), int(what in ("eta3", "eta3p")), out.data_ptr(),
                           work.data_ptr(), st)
         else:                                   # xtr, xtrd
             Bp = (B + 31) // 32 * 32
