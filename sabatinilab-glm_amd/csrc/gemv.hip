@@ -349,8 +349,8 @@ __device__ __forceinline__ void eta_ring_tie(EtaRing<NT>& t) {
     for (int n = 0; n < NT; ++n) asm volatile("" : "+v"(t.b[n]));
 }
 
-template <int NP, int NG, int NT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+template <int NP, int NG, int NT, int WPE = 1>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 eta_pipe_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
                 const __bf16* __restrict__ Dp, int32_t Bp, int32_t B,
                 const int32_t* __restrict__ slots, float* __restrict__ eta) {
@@ -436,7 +436,9 @@ eta_pipe_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
         __builtin_amdgcn_sched_barrier(0);
         compute(cur, st & 1);
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (NT == 4)
+        if constexpr (NT == 2)
+            asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else if constexpr (NT == 4)
             asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         else if constexpr (NT == 8)
             asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -484,6 +486,13 @@ eta_pipe_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
 
 // eta_pipe_kernel (default, both kinds; SGLM_ETA_PIPE=0 for the two-wave eta_dir_kernel /
 // one-wave eta_bits_kernel choices below; read per launch)
+// experiment knob: SGLM_ETA_PIPE_CFG=1 -> <1, 2, 8> at every fit count, 2 -> <1, 4, 2> at two
+// waves per SIMD (read per launch)
+static int eta_pipe_cfg() {
+    const char* e = getenv("SGLM_ETA_PIPE_CFG");
+    return e ? atoi(e) : 0;
+}
+
 static bool eta_pipe_on() {
     const char* e = getenv("SGLM_ETA_PIPE");
     return !(e && e[0] == '0');
@@ -1185,7 +1194,14 @@ int sglm_gemv_eta_bits(const uint32_t* rbits, int64_t ld, int32_t P, float* beta
         if (st) return st;
         const int ngr = Bp / 32;
         const u32x2* rb = reinterpret_cast<const u32x2*>(rbits);
-        if (eta_pipe_on() && ngr >= 3)
+        const int cfg = eta_pipe_cfg();
+        if (eta_pipe_on() && cfg == 1)
+            eta_pipe_kernel<1, 2, 8><<<dim3((unsigned)((ld + 1023) / 1024), (unsigned)((ngr + 1) / 2)),
+                                       256, 0, s>>>(rb, ld, P, Dp, Bp, B, slots, eta);
+        else if (eta_pipe_on() && cfg == 2)
+            eta_pipe_kernel<1, 4, 2, 2><<<dim3((unsigned)((ld + 255) / 256), (unsigned)((ngr + 3) / 4)),
+                                          256, 0, s>>>(rb, ld, P, Dp, Bp, B, slots, eta);
+        else if (eta_pipe_on() && ngr >= 3)
             eta_pipe_kernel<1, 4, 4><<<dim3((unsigned)((ld + 511) / 512), (unsigned)((ngr + 3) / 4)),
                                     256, 0, s>>>(rb, ld, P, Dp, Bp, B, slots, eta);
         else if (eta_pipe_on() && ngr == 2)
