@@ -486,8 +486,12 @@ eta_pipe_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
 
 // eta_pipe_kernel (default, both kinds; SGLM_ETA_PIPE=0 for the two-wave eta_dir_kernel /
 // one-wave eta_bits_kernel choices below; read per launch)
-// experiment knob: SGLM_ETA_PIPE_CFG=1 -> <1, 2, 8> at every fit count, 2 -> <1, 4, 2> at two
-// waves per SIMD (read per launch)
+// Direction products (one piece) by fit-group count, measured in-process (tools/ab_micro.py
+// etap, C4 design): two groups take eta_pipe_kernel<1, 2, 8> (64 fits 0.40 vs 0.44-0.46 ms);
+// three or four groups stay on the two-wave eta_dir_kernel (120 fits 0.665 ms vs 0.77 for the
+// one-wave <1, 4, 4>), one group on eta_bits_kernel<1, 8>.  SGLM_ETA_PIPE_CFG forces a variant
+// for comparisons: 1 <1, 2, 8>, 2 <1, 4, 2> at two waves per SIMD, 3 <1, 4, 4>, 4 <1, 1, 8>
+// (read per launch).
 static int eta_pipe_cfg() {
     const char* e = getenv("SGLM_ETA_PIPE_CFG");
     return e ? atoi(e) : 0;
@@ -1194,22 +1198,19 @@ int sglm_gemv_eta_bits(const uint32_t* rbits, int64_t ld, int32_t P, float* beta
         if (st) return st;
         const int ngr = Bp / 32;
         const u32x2* rb = reinterpret_cast<const u32x2*>(rbits);
-        const int cfg = eta_pipe_cfg();
-        if (eta_pipe_on() && cfg == 1)
+        const int cfg = eta_pipe_on() ? eta_pipe_cfg() : -1;
+        if (cfg == 1 || (cfg == 0 && ngr == 2))
             eta_pipe_kernel<1, 2, 8><<<dim3((unsigned)((ld + 1023) / 1024), (unsigned)((ngr + 1) / 2)),
                                        256, 0, s>>>(rb, ld, P, Dp, Bp, B, slots, eta);
-        else if (eta_pipe_on() && cfg == 2)
+        else if (cfg == 2)
             eta_pipe_kernel<1, 4, 2, 2><<<dim3((unsigned)((ld + 255) / 256), (unsigned)((ngr + 3) / 4)),
                                           256, 0, s>>>(rb, ld, P, Dp, Bp, B, slots, eta);
-        else if (eta_pipe_on() && ngr >= 3)
+        else if (cfg == 3)
             eta_pipe_kernel<1, 4, 4><<<dim3((unsigned)((ld + 511) / 512), (unsigned)((ngr + 3) / 4)),
                                     256, 0, s>>>(rb, ld, P, Dp, Bp, B, slots, eta);
-        else if (eta_pipe_on() && ngr == 2)
-            eta_pipe_kernel<1, 2, 8><<<dim3((unsigned)((ld + 1023) / 1024), 1u), 256, 0, s>>>(
-                rb, ld, P, Dp, Bp, B, slots, eta);
-        else if (eta_pipe_on())
-            eta_pipe_kernel<1, 1, 8><<<dim3((unsigned)((ld + 1023) / 1024), 1u), 256, 0, s>>>(
-                rb, ld, P, Dp, Bp, B, slots, eta);
+        else if (cfg == 4)
+            eta_pipe_kernel<1, 1, 8><<<dim3((unsigned)((ld + 1023) / 1024), (unsigned)ngr), 256, 0,
+                                       s>>>(rb, ld, P, Dp, Bp, B, slots, eta);
         else if (eta_dir_on(Bp))
             eta_dir_kernel<1, 4><<<dim3((unsigned)(ld / 256), (unsigned)((Bp / 32 + 3) / 4)),
                                    256, 0, s>>>(reinterpret_cast<const u32x2*>(rbits), ld, P,

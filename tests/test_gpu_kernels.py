@@ -652,17 +652,22 @@ def test_eta_dir_kernel_equals_per_group_kernel(engine, torch_mod, B, monkeypatc
                        device="cuda")
     outs = {}
     assert d.ld % 512 == 256                          # dead waves in the last workgroup
-    for v, (pipe, dr) in {"pipe": ("1", "0"), "dir": ("0", "1"), "group": ("0", "0")}.items():
+    variants = {"pipe": ("1", "0", "0"), "dir": ("0", "1", "0"), "group": ("0", "0", "0")}
+    for c in "1234":
+        variants["cfg" + c] = ("1", "0", c)
+    for v, (pipe, dr, cfg) in variants.items():
         monkeypatch.setenv("SGLM_ETA_PIPE", pipe)
         monkeypatch.setenv("SGLM_ETA_DIR", dr)
+        monkeypatch.setenv("SGLM_ETA_PIPE_CFG", cfg)
         bd = torch.from_numpy(beta).cuda()
         out = torch.full((nb, d.ld), float("nan"), dtype=torch.float32, device="cuda")
         _lib.call("sglm_gemv_eta_bits", d.rbits.data_ptr(), d.ld, d.P, bd.data_ptr(), B,
                   sl.data_ptr(), 0, out.data_ptr(), work.data_ptr(), 0)
         outs[v] = (out.cpu().numpy(), bd.cpu().numpy())
     got, br = outs["pipe"]
-    assert np.array_equal(got, outs["group"][0], equal_nan=True)
-    assert np.array_equal(outs["dir"][0], outs["group"][0], equal_nan=True)
+    for v in variants:
+        assert np.array_equal(outs[v][0], outs["group"][0], equal_nan=True), v
+    monkeypatch.setenv("SGLM_ETA_PIPE_CFG", "0")
     # exact coefficients (three pieces): the pipelined kernel == the staged one, bit for bit
     ex = {}
     for v, pipe in {"pipe": "1", "staged": "0"}.items():
