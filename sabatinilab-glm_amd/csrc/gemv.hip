@@ -487,10 +487,11 @@ eta_pipe_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
 // eta_pipe_kernel (default, both kinds; SGLM_ETA_PIPE=0 for the two-wave eta_dir_kernel /
 // one-wave eta_bits_kernel choices below; read per launch)
 // Direction products (one piece) by fit-group count, measured in-process (tools/ab_micro.py
-// etap, C4 design): two groups take eta_pipe_kernel<1, 2, 8> (64 fits 0.40 vs 0.44-0.46 ms);
-// three or four groups stay on the two-wave eta_dir_kernel (120 fits 0.665 ms vs 0.77 for the
-// one-wave <1, 4, 4>), one group on eta_bits_kernel<1, 8>.  SGLM_ETA_PIPE_CFG forces a variant
-// for comparisons: 1 <1, 2, 8>, 2 <1, 4, 2> at two waves per SIMD, 3 <1, 4, 4>, 4 <1, 1, 8>
+// etap, C4 design): two or more groups take eta_pipe_kernel<1, 4, 2> at two waves per SIMD
+// (120 fits 0.58 ms against 0.66 for eta_dir_kernel and 0.77 for the one-wave <1, 4, 4>; 96
+// fits 0.50 vs 0.57; 64 fits 0.40 vs 0.46), one group eta_bits_kernel<1, 8>.
+// SGLM_ETA_PIPE_CFG forces a variant for comparisons: 1 <1, 2, 8>, 2 <1, 4, 2> at two waves per
+// SIMD, 3 <1, 4, 4>, 4 <1, 1, 8>; SGLM_ETA3_CFG=1 the exact <3, 2, 2> at two waves per SIMD
 // (read per launch).
 static int eta_pipe_cfg() {
     const char* e = getenv("SGLM_ETA_PIPE_CFG");
@@ -1181,7 +1182,12 @@ int sglm_gemv_eta_bits(const uint32_t* rbits, int64_t ld, int32_t P, float* beta
         split3_kernel<<<gs, 256, 0, s>>>(beta, P, B, Bp, slots, Dp);
         st = check_launch("split3_kernel");
         if (st) return st;
-        if (eta_pipe_on())
+        const char* e3 = getenv("SGLM_ETA3_CFG");
+        if (eta_pipe_on() && e3 && e3[0] == '1')
+            eta_pipe_kernel<3, 2, 2, 2><<<dim3((unsigned)(ld / 256), (unsigned)((Bp / 32 + 1) / 2)),
+                                          256, 0, s>>>(reinterpret_cast<const u32x2*>(rbits), ld,
+                                                       P, Dp, Bp, B, slots, eta);
+        else if (eta_pipe_on())
             eta_pipe_kernel<3, 2, 4><<<dim3((unsigned)((ld + 511) / 512), (unsigned)((Bp / 32 + 1) / 2)),
                                        256, 0, s>>>(reinterpret_cast<const u32x2*>(rbits), ld, P,
                                                     Dp, Bp, B, slots, eta);
@@ -1199,12 +1205,12 @@ int sglm_gemv_eta_bits(const uint32_t* rbits, int64_t ld, int32_t P, float* beta
         const int ngr = Bp / 32;
         const u32x2* rb = reinterpret_cast<const u32x2*>(rbits);
         const int cfg = eta_pipe_on() ? eta_pipe_cfg() : -1;
-        if (cfg == 1 || (cfg == 0 && ngr == 2))
-            eta_pipe_kernel<1, 2, 8><<<dim3((unsigned)((ld + 1023) / 1024), (unsigned)((ngr + 1) / 2)),
-                                       256, 0, s>>>(rb, ld, P, Dp, Bp, B, slots, eta);
-        else if (cfg == 2)
+        if (cfg == 2 || (cfg == 0 && ngr >= 2))
             eta_pipe_kernel<1, 4, 2, 2><<<dim3((unsigned)((ld + 255) / 256), (unsigned)((ngr + 3) / 4)),
                                           256, 0, s>>>(rb, ld, P, Dp, Bp, B, slots, eta);
+        else if (cfg == 1)
+            eta_pipe_kernel<1, 2, 8><<<dim3((unsigned)((ld + 1023) / 1024), (unsigned)((ngr + 1) / 2)),
+                                       256, 0, s>>>(rb, ld, P, Dp, Bp, B, slots, eta);
         else if (cfg == 3)
             eta_pipe_kernel<1, 4, 4><<<dim3((unsigned)((ld + 511) / 512), (unsigned)((ngr + 3) / 4)),
                                     256, 0, s>>>(rb, ld, P, Dp, Bp, B, slots, eta);

@@ -670,8 +670,9 @@ def test_eta_dir_kernel_equals_per_group_kernel(engine, torch_mod, B, monkeypatc
     monkeypatch.setenv("SGLM_ETA_PIPE_CFG", "0")
     # exact coefficients (three pieces): the pipelined kernel == the staged one, bit for bit
     ex = {}
-    for v, pipe in {"pipe": "1", "staged": "0"}.items():
+    for v, (pipe, c3) in {"pipe": ("1", "0"), "pipe_w2": ("1", "1"), "staged": ("0", "0")}.items():
         monkeypatch.setenv("SGLM_ETA_PIPE", pipe)
+        monkeypatch.setenv("SGLM_ETA3_CFG", c3)
         monkeypatch.setenv("SGLM_ETA_EXACT_STAGED", "1")
         bd = torch.from_numpy(beta).cuda()
         out = torch.full((nb, d.ld), float("nan"), dtype=torch.float32, device="cuda")
@@ -679,6 +680,8 @@ def test_eta_dir_kernel_equals_per_group_kernel(engine, torch_mod, B, monkeypatc
                   sl.data_ptr(), 1, out.data_ptr(), work.data_ptr(), 0)
         ex[v] = out.cpu().numpy()
     assert np.array_equal(ex["pipe"], ex["staged"], equal_nan=True)
+    assert np.array_equal(ex["pipe_w2"], ex["staged"], equal_nan=True)
+    monkeypatch.setenv("SGLM_ETA3_CFG", "0")
     X64 = d.xb.double().cpu().numpy()
     for k in slots[:6]:
         ref = beta[k].astype(np.float64) @ X64

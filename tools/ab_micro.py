@@ -17,15 +17,16 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "sabatinilab-glm_amd")]
 
 VARIANTS = {
     "eta": [("dir", {"SGLM_ETA_DIR": "1"}), ("group", {"SGLM_ETA_DIR": "0"})],
-    "etap": [("default", {"SGLM_ETA_PIPE": "1", "SGLM_ETA_PIPE_CFG": "0"}),
+    "etap": [("default", {"SGLM_ETA_PIPE": "1", "SGLM_ETA_PIPE_CFG": "0", "SGLM_ETA_DIR": "1"}),
              ("pipe28", {"SGLM_ETA_PIPE": "1", "SGLM_ETA_PIPE_CFG": "1"}),
              ("pipe42w2", {"SGLM_ETA_PIPE": "1", "SGLM_ETA_PIPE_CFG": "2"}),
              ("pipe44", {"SGLM_ETA_PIPE": "1", "SGLM_ETA_PIPE_CFG": "3"}),
              ("dir", {"SGLM_ETA_PIPE": "0", "SGLM_ETA_DIR": "1"}),
              ("group", {"SGLM_ETA_PIPE": "0", "SGLM_ETA_DIR": "0"})],
     "eta3": [("staged", {"SGLM_ETA_EXACT_STAGED": "1"}), ("group", {"SGLM_ETA_EXACT_STAGED": "0"})],
-    "eta3p": [("pipe", {"SGLM_ETA_PIPE": "1"}), ("staged", {"SGLM_ETA_PIPE": "0",
-                                                            "SGLM_ETA_EXACT_STAGED": "1"})],
+    "eta3p": [("pipe", {"SGLM_ETA_PIPE": "1", "SGLM_ETA3_CFG": "0"}),
+              ("pipe_w2", {"SGLM_ETA_PIPE": "1", "SGLM_ETA3_CFG": "1"}),
+              ("staged", {"SGLM_ETA_PIPE": "0", "SGLM_ETA_EXACT_STAGED": "1"})],
     "xtr": [("ngw2", {"SGLM_XTR4": "1", "SGLM_XTR_NGW": "2", "SGLM_XTR_PIPE": "0"}),
             ("pipe2", {"SGLM_XTR4": "1", "SGLM_XTR_NGW": "2", "SGLM_XTR_PIPE": "1"}),
             ("ngw1", {"SGLM_XTR4": "1", "SGLM_XTR_NGW": "1", "SGLM_XTR_PIPE": "0"}),
