@@ -491,8 +491,9 @@ eta_pipe_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
 // (120 fits 0.58 ms against 0.66 for eta_dir_kernel and 0.77 for the one-wave <1, 4, 4>; 96
 // fits 0.50 vs 0.57; 64 fits 0.40 vs 0.46), one group eta_bits_kernel<1, 8>.
 // SGLM_ETA_PIPE_CFG forces a variant for comparisons: 1 <1, 2, 8>, 2 <1, 4, 2> at two waves per
-// SIMD, 3 <1, 4, 4>, 4 <1, 1, 8>; SGLM_ETA3_CFG=1 the exact <3, 2, 2> at two waves per SIMD
-// (read per launch).
+// SIMD, 3 <1, 4, 4>, 4 <1, 1, 8>.  Exact coefficients take <3, 2, 2> at two waves per SIMD
+// (120 fits 1.23 ms against 1.57 for the one-wave <3, 2, 4> and 1.77 for eta_dir_kernel<3, 2>;
+// SGLM_ETA3_CFG=0 forces <3, 2, 4>) (read per launch).
 static int eta_pipe_cfg() {
     const char* e = getenv("SGLM_ETA_PIPE_CFG");
     return e ? atoi(e) : 0;
@@ -1183,7 +1184,7 @@ int sglm_gemv_eta_bits(const uint32_t* rbits, int64_t ld, int32_t P, float* beta
         st = check_launch("split3_kernel");
         if (st) return st;
         const char* e3 = getenv("SGLM_ETA3_CFG");
-        if (eta_pipe_on() && e3 && e3[0] == '1')
+        if (eta_pipe_on() && !(e3 && e3[0] == '0'))
             eta_pipe_kernel<3, 2, 2, 2><<<dim3((unsigned)(ld / 256), (unsigned)((Bp / 32 + 1) / 2)),
                                           256, 0, s>>>(reinterpret_cast<const u32x2*>(rbits), ld,
                                                        P, Dp, Bp, B, slots, eta);
