@@ -376,23 +376,30 @@ class LagFrame:
     def nan_counts(self, cols=None) -> np.ndarray:
         """Per row of this frame, the number of NaN cells among ``cols`` (default: all): lag
         columns from the device (a lag cell is NaN when its source row is outside the base or
-        the source cell is NaN), base and assigned columns on the host."""
-        import torch
+        the source cell is NaN) together with the unshifted copies of their sources; every
+        other base column (ids, responses) and assigned columns on the host, without an
+        upload."""
         cols = self._cols if cols is None else list(cols)
         self._check_cols(cols)
         n = self._nrows()
         cnt = np.zeros(n, dtype=np.int64)
         lag = {}
+        srcs = {self._spec[c][0] for c in cols if c not in self._overlay and self._spec[c][2]}
+        sp = self._span()
         for c in cols:
             if c in self._overlay:
                 cnt += pd.isna(self._overlay[c]).astype(np.int64)
-            elif self._spec[c][2] or self._src.numeric(self._spec[c][0]):
-                # lag columns, and numeric base columns as lag 0 (device NaN flags)
-                nm, s, _ = self._spec[c]
+                continue
+            nm, s, is_lag = self._spec[c]
+            if is_lag or (nm in srcs and self._src.numeric(nm)):
                 lag.setdefault(s, []).append(nm)
-            else:
-                cnt += self._src.base[self._spec[c][0]].isna().to_numpy()[self.positions()] \
-                    .astype(np.int64)
+                continue
+            v = self._src.base[nm]
+            if isinstance(v.dtype, np.dtype) and v.dtype.kind in "iub":
+                continue                                    # integer / bool: no NaN
+            na = np.isnan(v.to_numpy()) if (isinstance(v.dtype, np.dtype) and
+                                            v.dtype.kind == "f") else v.isna().to_numpy()
+            cnt += na[sp[0]:sp[1]] if sp is not None else na[self.positions()]
         if lag:
             cnt += self._lag_nan_counts(lag)
         return cnt
