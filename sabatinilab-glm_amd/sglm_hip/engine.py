@@ -759,7 +759,7 @@ class Problem:
         if ev is None:
             ev = torch.cuda.Event()
             _scratch().pinned[("problem_masks_ev", None)] = ev
-        yb[:ntot].copy_(torch.from_numpy(y))
+        _lib.call("sglm_host_copy", yb.data_ptr(), y.ctypes.data, 8 * ntot, HOST_THREADS)
         yd = torch.empty(ntot, dtype=torch.float64, device=dev)
         yd.copy_(yb[:ntot], non_blocking=True)
         ev.record()
