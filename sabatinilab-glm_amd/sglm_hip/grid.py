@@ -123,7 +123,7 @@ def _dist():
     return None
 
 
-SHARD_PLAN = "mask_major"                    # or "family_lpt", "round_robin" (comparison runs)
+SHARD_PLAN = "mask_major"                    # or "round_robin" (comparison runs)
 # "fits" (default): whole fits (cross-mask families) per rank with one all-gather of the
 # results; "rows": a process group splits the rows of the grid (every rank runs every fit on
 # its slab, sums all-reduced; comm.py).  Simulated C4 shares at 2 / 4 / 8 ranks are equal within
@@ -252,27 +252,10 @@ def rank_share(plan, groups: Sequence[dict], rank: int, world: int):
     units = {}
     for i, t in enumerate(table):
         units.setdefault((t[0], t[1]), []).append(i)
-    fam = (world > 1 and SHARD_PLAN in ("mask_major", "family_lpt") and E.HESS_XMASK_TOL > 0
+    fam = (world > 1 and SHARD_PLAN == "mask_major" and E.HESS_XMASK_TOL > 0
            and len(units) >= world
            and all(o.kind == "irls" and o.family == E.FAM_TWEEDIE_LOG
                    for g in groups for o in g["objectives"]))
-    if fam and SHARD_PLAN == "family_lpt":
-        # whole families, dealt largest-first to the least-loaded rank; a family's estimated
-        # cost grows as its penalty falls (weakly penalised fits take more Newton iterations):
-        # 1 (strongest) .. 2 (weakest) within its group
-        cost = {}
-        for u in units:
-            objs = groups[u[0]]["objectives"]
-            lam = [float(getattr(o, "alpha", 0.0)) for o in objs]
-            rank_desc = sorted(range(len(lam)), key=lambda j: (-lam[j], j)).index(u[1])
-            cost[u] = len(units[u]) * (1.0 + rank_desc / max(1, len(lam) - 1))
-        load = [0.0] * world
-        owner = {}
-        for u in sorted(units, key=lambda u: (-cost[u], u)):
-            r = min(range(world), key=lambda q: (load[q], q))
-            owner[u] = r
-            load[r] += cost[u]
-        return sorted(i for u in units if owner[u] == rank for i in units[u])
     if fam:
         # whole parameters (a penalty's split fits + refit: one cross-mask family, solved on
         # the refit's factor) per rank, in snake order of the penalty list, cut into

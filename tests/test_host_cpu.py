@@ -288,31 +288,3 @@ def test_group_shuffle_split_id_kinds_vs_sklearn(kind):
     ref = list(GroupShuffleSplit(n_splits=4, test_size=0.25).split(g, None, g))
     for (a, b), (c, d) in zip(got, ref):
         assert np.array_equal(a, c) and np.array_equal(b, d)
-
-
-@pytest.mark.parametrize("world", [2, 3, 8])
-def test_family_lpt_plan_partitions_whole_families(world, monkeypatch):
-    """grid.rank_share with SHARD_PLAN = 'family_lpt': every fit on exactly one rank, each
-    penalty's split fits + refit (one cross-mask family) on one rank, estimated loads within
-    one family of each other, the same answer on every rank."""
-    from sglm_hip import engine as E, grid
-    from sglm_hip.estimators import Objective
-    monkeypatch.setattr(grid, "SHARD_PLAN", "family_lpt")
-    n = 500
-    rng = np.random.default_rng(1)
-    cv = [(np.sort(rng.choice(n, 400, replace=False)), np.arange(3)) for _ in range(5)]
-    objs = [Objective("irls", E.FAM_TWEEDIE_LOG, 1.0, float(a), "n", True, 100)
-            for a in np.logspace(-4, 1, 20)]
-    groups = [{"cv_idx": cv, "objectives": objs, "rolls": [0] * 20}]
-    plan = grid.plan_fits(groups, n, check=False)
-    table = plan[3]
-    shares = [grid.rank_share(plan, groups, r, world) for r in range(world)]
-    flat = sorted(i for s in shares for i in s)
-    assert flat == list(range(len(table)))
-    fam_rank = {}
-    for r, s in enumerate(shares):
-        for i in s:
-            assert fam_rank.setdefault(table[i][1], r) == r
-    cost = lambda j: 6 * (1.0 + j / 19.0)             # alpha ascending: j = 0 weakest -> 2
-    loads = [sum(cost(19 - j) for j in set(table[i][1] for i in s)) for s in shares]
-    assert max(loads) - min(loads) <= 12.0 + 1e-9
