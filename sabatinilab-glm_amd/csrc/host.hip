@@ -107,84 +107,13 @@ extern "C" int sglm_host_masks(int32_t nm, const int64_t* const* idx, const int6
         j.n = n;
         j.ld = ld;
     }
-    const int nt = nthreads > 0 ? nthreads : 1;
-    // A strictly increasing in-range fold list (GroupShuffleSplit folds, the common case) is a
-    // 0/1 mask: its zero fill and its scatter are split over all threads by row / index chunks
-    // (one thread per mask left most of the box idle at 6 masks).  Every other list -- out of
-    // range, repeats (multiplicities), row lists -- takes build_mask on one thread.
-    const int64_t kChunk = 1 << 16;
-    std::vector<uint8_t> fast((size_t)nm, 0);
-    {
-        // pass 1: per (mask, index chunk) range and order checks
-        struct Piece { int f; int64_t a, b; };
-        std::vector<Piece> pieces;
-        for (int f = 0; f < nm; ++f)
-            if (jobs[f].kind == SGLM_MASK_FOLD)
-                for (int64_t a = 0; a < jobs[f].len; a += kChunk)
-                    pieces.push_back({f, a, std::min(jobs[f].len, a + kChunk)});
-        std::vector<uint8_t> ok(pieces.size(), 0);
-        std::vector<std::thread> th;
-        const int npt = (int)std::min<size_t>((size_t)nt, std::max<size_t>(pieces.size(), 1));
-        for (int t = 0; t < npt; ++t)
-            th.emplace_back([&, t] {
-                for (size_t q = (size_t)t; q < pieces.size(); q += (size_t)npt) {
-                    const Piece& pc = pieces[q];
-                    const int64_t* x = jobs[pc.f].idx;
-                    // in range, no negative index, strictly increasing inside the piece and
-                    // across its left boundary
-                    bool good = x[pc.a] >= 0 && x[pc.a] < n &&
-                                (pc.a == 0 || x[pc.a - 1] < x[pc.a]);
-                    for (int64_t k = pc.a + 1; k < pc.b; ++k)
-                        good &= x[k] > x[k - 1] && x[k] < n;
-                    ok[q] = good;
-                }
-            });
-        for (auto& x : th) x.join();
-        for (int f = 0; f < nm; ++f) fast[f] = jobs[f].kind == SGLM_MASK_FOLD;
-        for (size_t q = 0; q < pieces.size(); ++q) fast[pieces[q].f] &= ok[q];
-        // pass 2: zero fill of the fast masks by row chunks, then their scatter by index chunks
-        struct Span { int f; int64_t a, b; };
-        std::vector<Span> zero, scat;
-        for (int f = 0; f < nm; ++f) {
-            if (!fast[f]) continue;
-            for (int64_t a = 0; a < ld; a += 4 * kChunk) zero.push_back({f, a, std::min(ld, a + 4 * kChunk)});
-            for (int64_t a = 0; a < jobs[f].len; a += kChunk)
-                scat.push_back({f, a, std::min(jobs[f].len, a + kChunk)});
-        }
-        auto run = [&](const std::vector<Span>& v, bool fill) {
-            std::vector<std::thread> tt;
-            const int k = (int)std::min<size_t>((size_t)nt, std::max<size_t>(v.size(), 1));
-            for (int t = 0; t < k; ++t)
-                tt.emplace_back([&, t] {
-                    for (size_t q = (size_t)t; q < v.size(); q += (size_t)k) {
-                        const Span& sp = v[q];
-                        uint8_t* m = jobs[sp.f].out;
-                        if (fill) {
-                            std::memset(m + sp.a, 0, (size_t)(sp.b - sp.a));
-                        } else {
-                            const int64_t* x = jobs[sp.f].idx;
-                            for (int64_t e = sp.a; e < sp.b; ++e) m[x[e]] = 1;
-                        }
-                    }
-                });
-            for (auto& x : tt) x.join();
-        };
-        run(zero, true);
-        run(scat, false);
-        for (int f = 0; f < nm; ++f)
-            if (fast[f]) {
-                jobs[f].nnz = jobs[f].len;
-                jobs[f].sum = (double)jobs[f].len;
-            }
-    }
-    std::vector<int> rest;
-    for (int f = 0; f < nm; ++f)
-        if (!fast[f]) rest.push_back(f);
-    const int nr = std::min<int>(nt, (int)rest.size());
+    int nt = nthreads > 0 ? nthreads : 1;
+    if (nt > nm) nt = nm;
     std::vector<std::thread> pool;
-    for (int w = 0; w < nr; ++w)
-        pool.emplace_back([&jobs, &rest, w, nr] {
-            for (size_t q = (size_t)w; q < rest.size(); q += (size_t)nr) build_mask(jobs[rest[q]]);
+    pool.reserve((size_t)nt);
+    for (int w = 0; w < nt; ++w)
+        pool.emplace_back([&jobs, w, nt] {
+            for (size_t f = (size_t)w; f < jobs.size(); f += (size_t)nt) build_mask(jobs[f]);
         });
     for (auto& t : pool) t.join();
     for (int32_t f = 0; f < nm; ++f) {
