@@ -40,6 +40,17 @@ void launch_chol_diag4(int nact, hipStream_t s, float* Hall, int32_t P, int32_t 
                        const int32_t* fits, uint8_t* frozen_all, const float* diag_all,
                        int32_t* info, float* minv_all, float* Mall);
 
+void launch_chol_diag4q(int nact, hipStream_t s, float* Hall, int32_t P, int32_t k0,
+                        const int32_t* fits, uint8_t* frozen_all, const float* diag_all,
+                        int32_t* info, float* minv_all, float* Mall);
+
+// Four pivots per barrier in the four-wave diagonal step (chol_diag4q_kernel, bitwise the same
+// factor); SGLM_DIAG4Q=0 for two (read per chain capture; part of the chain-graph key).
+static bool diag4q() {
+    const char* e = getenv("SGLM_DIAG4Q");
+    return !(e && e[0] == '0');
+}
+
 // Four-wave diagonal step (chol_diag4.hip) in the factor + inverse chain; SGLM_DIAG4=0 keeps
 // the single-wave kernel (comparison runs).
 static bool diag4() {
@@ -1077,7 +1088,9 @@ static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t na
     // read-modify-write that bounds the chain at large batches) is swept P/(kLA*64) times
     auto factor_step = [&](int kb) {
         const int k0 = kb * kNB;
-        if (Mall && nrefac == nact && diag4())
+        if (Mall && nrefac == nact && diag4() && diag4q())
+            launch_chol_diag4q(nact, s, H, P, k0, fits, frozen, dg, info, minv, Mall);
+        else if (Mall && nrefac == nact && diag4())
             launch_chol_diag4(nact, s, H, P, k0, fits, frozen, dg, info, minv, Mall);
         else
             launch_chol_diag(nact, s, H, P, k0, fits, frozen, rhs, dg, info, nrefac, minv, Mall);
@@ -1193,7 +1206,7 @@ static int factor_inv_launch(float* H, float* Minv, int32_t P, const int32_t* fi
 // keeps `fits` in a stable buffer.  SGLM_CHOL_GRAPH=0 launches the chain directly.
 struct ChainKey {
     const void *H, *Minv, *fits, *dshift, *delta, *info, *frozen, *work;
-    int32_t P, n, B, la;
+    int32_t P, n, B, la, q;
     bool operator<(const ChainKey& o) const {
         return std::memcmp(this, &o, sizeof(ChainKey)) < 0;
     }
@@ -1311,7 +1324,7 @@ static int factor_inv_cached(float* H, float* Minv, int32_t P, const int32_t* fi
     std::memset(&key, 0, sizeof(key));
     key.H = H; key.Minv = Minv; key.fits = fits; key.dshift = dshift; key.delta = delta;
     key.info = info; key.frozen = frozen; key.work = work;
-    key.P = P; key.n = n; key.B = B; key.la = chol_lookahead();
+    key.P = P; key.n = n; key.B = B; key.la = chol_lookahead(); key.q = diag4q() ? 1 : 0;
     // the lock is held across capture and launch: a concurrent eviction must not destroy the
     // entry between lookup and launch (captures are thread-local, so nothing else is stalled
     // but other chains' host enqueue, which is short next to the chain itself)

@@ -241,6 +241,49 @@ def test_chol_solve_inv_vs_float64(engine, torch_mod, P, p, B):
         assert rel(x[q], want(src, q, sc)) < 1e-3, q
 
 
+@pytest.mark.parametrize("P,p", [(256, 200), (2048, 1990)])
+def test_chol_diag_four_pivots_equals_two(engine, torch_mod, P, p, monkeypatch):
+    """The factor + inverse chain with four pivots per barrier in the diagonal step
+    (chol_diag4q_kernel) leaves the same factor, inverse, frozen set and drop count as two
+    pivots per barrier (chol_diag4_kernel), bit for bit: a duplicated column (a dropped pivot),
+    a frozen coordinate, three fits."""
+    torch = torch_mod
+    from sglm_hip import _lib
+    rng = np.random.default_rng(P)
+    B = 3
+    H = np.zeros((B, P, P), np.float32)
+    for k in range(B):
+        A = rng.normal(size=(p + 300, p + 1))
+        A[:, 5] = A[:, 9]                                # dependent column
+        H[k, : p + 1, : p + 1] = A.T @ A / 100.0
+    dsh = np.full((B, P), -1.0, np.float32)
+    dsh[:, :p] = rng.uniform(0.0, 0.5, size=(B, 1))
+    dsh[:, p] = 0.0
+    dsh[:, 5] = 0.0                                      # unpenalised: the pivot drops
+    dsh[:, 17] = -1.0                                    # frozen
+    outs = {}
+    for q in ("1", "0"):
+        monkeypatch.setenv("SGLM_DIAG4Q", q)
+        Hd = torch.from_numpy(H).cuda()
+        Md = torch.zeros_like(Hd)
+        out = torch.zeros((B, P), dtype=torch.float32, device="cuda")
+        info = torch.zeros(B, dtype=torch.int32, device="cuda")
+        frozen = torch.zeros((B, P), dtype=torch.uint8, device="cuda")
+        dshd = torch.from_numpy(dsh).cuda()
+        cw = torch.empty(_lib.query("sglm_chol_work_bytes", P, B), dtype=torch.uint8,
+                         device="cuda")
+        lst = torch.arange(B, dtype=torch.int32, device="cuda")
+        rs = torch.ones(B, dtype=torch.float32, device="cuda")
+        _lib.call("sglm_chol_solve_inv", Hd.data_ptr(), Md.data_ptr(), P, lst.data_ptr(),
+                  lst.data_ptr(), rs.data_ptr(), B, B, None, 0, None, dshd.data_ptr(),
+                  out.data_ptr(), info.data_ptr(), frozen.data_ptr(), B, cw.data_ptr(), 0)
+        torch.cuda.synchronize()
+        outs[q] = [t.cpu().numpy() for t in (Hd, Md, info, frozen)]
+    assert (outs["1"][2] >= 1).all()                     # the dependent column dropped
+    for a, b in zip(outs["1"], outs["0"]):
+        assert np.array_equal(a, b, equal_nan=True)
+
+
 @pytest.mark.parametrize("P,p,B", [(768, 700, 6), (2048, 1990, 5)])
 def test_chol_inv_many_fits_vs_float64(engine, torch_mod, P, p, B, monkeypatch):
     """Factor + inverse chain on several fits of their own with the 128 x 128 inversion tiles
