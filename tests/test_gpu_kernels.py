@@ -259,7 +259,7 @@ def test_chol_diag_four_pivots_equals_two(engine, torch_mod, P, p, monkeypatch):
     dsh = np.full((B, P), -1.0, np.float32)
     dsh[:, :p] = rng.uniform(0.0, 0.5, size=(B, 1))
     dsh[:, p] = 0.0
-    dsh[:, 5] = 0.0                                      # unpenalised: the pivot drops
+    dsh[:, [5, 9]] = 0.0                                 # unpenalised: pivot 9 drops
     dsh[:, 17] = -1.0                                    # frozen
     outs = {}
     for q in ("1", "0"):
