@@ -45,10 +45,12 @@ void launch_chol_diag4q(int nact, hipStream_t s, float* Hall, int32_t P, int32_t
                         int32_t* info, float* minv_all, float* Mall);
 
 // Four pivots per barrier in the four-wave diagonal step (chol_diag4q_kernel, bitwise the same
-// factor); SGLM_DIAG4Q=1 selects it (read per chain capture; part of the chain-graph key).
+// factor; the default: chain of 1 / 20 representatives 1.10 -> 1.07 / 2.53 -> 2.50 ms, C4 grid
+// 47.95 -> 47.67 ms in an A/B on one box); SGLM_DIAG4Q=0 for two (read per chain capture; part
+// of the chain-graph key).
 static bool diag4q() {
     const char* e = getenv("SGLM_DIAG4Q");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
 }
 
 // Four-wave diagonal step (chol_diag4.hip) in the factor + inverse chain; SGLM_DIAG4=0 keeps
