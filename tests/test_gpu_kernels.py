@@ -675,7 +675,7 @@ def test_eta_bits_matches_float64(engine, torch_mod):
     assert torch.equal(bd2[1], bd[1]) and torch.isnan(out_r[1]).all()
 
 
-@pytest.mark.parametrize("B", [100, 70, 33, 7])
+@pytest.mark.parametrize("B", [200, 100, 70, 33, 7])
 def test_eta_dir_kernel_equals_per_group_kernel(engine, torch_mod, B, monkeypatch):
     """Direction products through the pipelined kernel (eta_pipe_kernel<4, 4> / <2, 8> /
     <1, 8>: 512 / 1024 rows per workgroup, waves past the last row, ragged fit groups), the
