@@ -970,12 +970,9 @@ extern "C" size_t sglm_chol_work_bytes(int32_t P, int32_t B) {
 // Look-ahead depth of the blocked factorisation (block steps per trailing sweep); the
 // SGLM_CHOL_LOOKAHEAD environment variable (1..8) overrides the default 4 for experiments.
 static int chol_lookahead() {
-    static const int la = [] {
-        const char* e = getenv("SGLM_CHOL_LOOKAHEAD");
-        const int v = e ? atoi(e) : 4;
-        return v >= 1 && v <= 8 ? v : 4;
-    }();
-    return la;
+    const char* e = getenv("SGLM_CHOL_LOOKAHEAD");           // read per chain (graph key)
+    const int v = e ? atoi(e) : 4;
+    return v >= 1 && v <= 8 ? v : 4;
 }
 
 // Inversion levels with the two-stage register pipeline (default; 1.52 -> 1.42 ms per 1-fit
