@@ -687,201 +687,6 @@ syrk6_kernel(const int64_t* __restrict__ desc, int32_t P, int32_t splits,
                     0.5f * acc[m][n][j];
 }
 
-// v7: the same Gram at TWO waves per SIMD -- each wave a 128 x 64 block (4 x 2 tiles, 128
-// AGPRs) instead of 128 x 128, so a second wave's MFMAs run while one wave expands bits (the
-// one-wave kernel leaves the MFMA pipe idle while its own ~80 VALU issue).  A block's A strip
-// is the same 128 columns, its B strip half as wide; per output element the same MFMA
-// sequence over the same K order as v6 (bitwise equal), diagonal 128-blocks as two halves
-// that skip the same strictly-lower 32 x 32 tiles.  The nb (nb + 1) half-blocks of the upper
-// triangle are numbered row by row: block row bi holds the halves j = 2 bi .. 2 nb - 1.
-struct Step7 {
-    u32x2 a[4], b[2];
-    u32x4 w[4];
-};
-
-__device__ __forceinline__ void load7(Step7& t, const Addr6& ad, int64_t s) {
-    const uint64_t sa = ad.a + (uint64_t)s * ad.stride_ab;
-    const uint64_t sb = ad.b + (uint64_t)s * ad.stride_ab;
-    const uint64_t sw = ad.w + (uint64_t)s * 128;
-    t.a[0] = gld2s<0>(sa, ad.voff_ab);
-    t.a[1] = gld2s<256>(sa, ad.voff_ab);
-    t.a[2] = gld2s<512>(sa, ad.voff_ab);
-    t.a[3] = gld2s<768>(sa, ad.voff_ab);
-    t.b[0] = gld2s<0>(sb, ad.voff_ab);
-    t.b[1] = gld2s<256>(sb, ad.voff_ab);
-    t.w[0] = gld4s<0>(sw, ad.voff_w);
-    t.w[1] = gld4s<32>(sw, ad.voff_w);
-    t.w[2] = gld4s<64>(sw, ad.voff_w);
-    t.w[3] = gld4s<96>(sw, ad.voff_w);
-}
-
-__device__ __forceinline__ void wait7(Step7& t) {
-    asm volatile("s_waitcnt vmcnt(0)"
-                 : "+v"(t.a[0]), "+v"(t.a[1]), "+v"(t.a[2]), "+v"(t.a[3]), "+v"(t.b[0]),
-                   "+v"(t.b[1]), "+v"(t.w[0]), "+v"(t.w[1]), "+v"(t.w[2]), "+v"(t.w[3])
-                 :
-                 : "memory");
-}
-
-struct Frag7 {
-    bf16x8 a[4], b[2];
-};
-
-__device__ __forceinline__ void frags7(const Step7& t, int ks, int h, Frag7& f) {
-    const uint32_t p0 = 8 * (ks & 1) + 4 * h;
-    const uint32_t wp[4] = {t.w[ks].x, t.w[ks].y, t.w[ks].z, t.w[ks].w};
-#pragma unroll
-    for (int m = 0; m < 4; ++m) f.a[m] = frag_two(t.a[m], ks, h);
-#pragma unroll
-    for (int n = 0; n < 2; ++n) {
-        const uint32_t word = ks < 2 ? t.b[n].x : t.b[n].y;
-        uint32_t d[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const s16x2 v = __builtin_bit_cast(s16x2, rotr32(word, (p0 + j + 17) & 31));
-            d[j] = __builtin_bit_cast(uint32_t, (s16x2)(v >> (s16x2){15, 15})) & wp[j];
-        }
-        f.b[n] = __builtin_bit_cast(bf16x8, make_uint4(d[0], d[1], d[2], d[3]));
-    }
-}
-
-// HALF = -1: an off-diagonal half-block (all 8 tiles); 0 / 1: the left / right half of a
-// diagonal 128-block (tile (m, n) is column tile 2 HALF + n of the block: skipped when below)
-template <int HALF>
-__device__ __forceinline__ constexpr bool tile7_on(int m, int n) {
-    return HALF < 0 || m <= 2 * HALF + n;
-}
-
-template <int HALF>
-__device__ __forceinline__ void mfma8(const Frag7& f, f32x16 (&acc)[4][2]) {
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < 2; ++n)
-            if (tile7_on<HALF>(m, n))
-                acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[m], f.b[n], acc[m][n],
-                                                                    0, 0, 0);
-}
-
-template <int HALF>
-__device__ __forceinline__ void interleave8() {
-    constexpr int nm = HALF < 0 ? 8 : (HALF == 0 ? 3 : 7);
-    constexpr int nv = (56 + nm - 1) / nm;
-#pragma unroll
-    for (int i = 0; i < nm; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);     // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, nv, 0);    // VALU
-    }
-    __builtin_amdgcn_sched_barrier(0);
-}
-
-template <int HALF>
-__device__ __forceinline__ void half7(const Step7& cur, Step7& nxt, Frag7& F, int h,
-                                      f32x16 (&acc)[4][2], const Addr6& ad, int64_t snext) {
-    load7(nxt, ad, snext);
-    __builtin_amdgcn_sched_barrier(0);
-    Frag7 G;
-    frags7(cur, 1, h, G);
-    mfma8<HALF>(F, acc);
-    interleave8<HALF>();
-    frags7(cur, 2, h, F);
-    mfma8<HALF>(G, acc);
-    interleave8<HALF>();
-    frags7(cur, 3, h, G);
-    mfma8<HALF>(F, acc);
-    interleave8<HALF>();
-    wait7(nxt);
-    frags7(nxt, 0, h, F);
-    mfma8<HALF>(G, acc);
-    interleave8<HALF>();
-}
-
-template <int HALF>
-__device__ __forceinline__ void gram7_loop(f32x16 (&acc)[4][2], const Addr6& ad, int nsteps,
-                                           int h) {
-    Step7 A, B;
-    Frag7 F;
-    load7(A, ad, 0);
-    wait7(A);
-    frags7(A, 0, h, F);
-    int s = 0;
-    for (; s + 1 < nsteps; s += 2) {
-        half7<HALF>(A, B, F, h, acc, ad, s + 1);
-        half7<HALF>(B, A, F, h, acc, ad, s + 2 < nsteps ? s + 2 : nsteps - 1);
-    }
-    if (s < nsteps) {
-        Frag7 G;
-        frags7(A, 1, h, G);
-        mfma8<HALF>(F, acc);
-        frags7(A, 2, h, F);
-        mfma8<HALF>(G, acc);
-        frags7(A, 3, h, G);
-        mfma8<HALF>(F, acc);
-        mfma8<HALF>(G, acc);
-    }
-}
-
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
-syrk7_kernel(const int64_t* __restrict__ desc, int32_t P, int32_t splits,
-             const int32_t* __restrict__ fits, int32_t nunits, float* __restrict__ H,
-             float* __restrict__ slab, int32_t nact) {
-    const int unit = blockIdx.x % nunits;
-    const int slot = blockIdx.x / nunits;
-    const int split = blockIdx.y;
-    const int nb = P / 128;
-    int bi = 0, start = 0;
-    while (bi + 1 < nb && start + 2 * (nb - bi) <= unit) {
-        start += 2 * (nb - bi);
-        ++bi;
-    }
-    const int j = 2 * bi + (unit - start);                      // 64-column half index
-    const int fit = fits[slot];
-    const int64_t* dsc = desc + 4 * slot;
-    g_uint2* bits = reinterpret_cast<g_uint2*>(dsc[0]);
-    const int64_t nrows = dsc[1];
-    const int64_t wbf = dsc[2];
-    const int64_t nblk = (nrows + 63) / 64;
-    const int64_t sps = (nblk + splits - 1) / splits;
-    const int64_t blk0 = (int64_t)split * sps;
-    const int64_t blk1 = min(blk0 + sps, nblk);
-    const int nsteps = blk1 > blk0 ? (int)(blk1 - blk0) : 0;
-    const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
-    Addr6 ad;
-    ad.a = reinterpret_cast<uint64_t>(bits + blk0 * P + bi * 128);
-    ad.b = reinterpret_cast<uint64_t>(bits + blk0 * P + j * 64);
-    ad.w = (uint64_t)(wbf + 2 * blk0 * 64);
-    ad.stride_ab = (uint64_t)P * 8;
-    ad.voff_ab = 8u * r;
-    ad.voff_w = 16u * h;
-
-    f32x16 acc[4][2];
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < 2; ++n) acc[m][n] = (f32x16){};
-
-    if (nsteps > 0) {
-        if (j == 2 * bi)
-            gram7_loop<0>(acc, ad, nsteps, h);
-        else if (j == 2 * bi + 1)
-            gram7_loop<1>(acc, ad, nsteps, h);
-        else
-            gram7_loop<-1>(acc, ad, nsteps, h);
-    }
-    float* out = slab ? slab + ((int64_t)split * nact + slot) * (int64_t)P * P
-                      : H + (int64_t)fit * P * P;
-    const int64_t rbase = (int64_t)bi * 128;
-    const int64_t cbase = (int64_t)j * 64;
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < 2; ++n)
-#pragma unroll
-            for (int q = 0; q < 16; ++q)
-                out[(rbase + m * 32 + (q & 3) + 8 * (q >> 2) + 4 * h) * P + cbase + n * 32 + r] =
-                    0.5f * acc[m][n][q];
-}
-
 // split-K reduction over the 128-blocks v6 writes (block row <= block col)
 __global__ void __launch_bounds__(256) syrk6_reduce(const float* __restrict__ slab, int32_t P,
                                                     int32_t nact, int32_t splits,
@@ -1088,12 +893,7 @@ extern "C" int sglm_syrk_cbits(const int64_t* desc, int32_t P, const int32_t* fi
     hipStream_t s = as_stream(stream);
     float* slab = splits > 1 ? (float*)work : nullptr;
     const char* ex = getenv("SGLM_SYRK_XCD");         // read per call (A/B in one process)
-    const char* e7 = getenv("SGLM_SYRK7");            // two-wave half-block kernel (A/B)
-    if (e7 && e7[0] == '1') {
-        const int nh = nb * (nb + 1);                   // 128 x 64 halves of the triangle
-        syrk7_kernel<<<dim3((unsigned)(nh * nact), (unsigned)splits), 64, 0, s>>>(
-            desc, P, splits, fits, nh, H, slab, nact);
-    } else if (ex && ex[0] == '1' && nb % 4 == 0 && nb >= 4) {
+    if (ex && ex[0] == '1' && nb % 4 == 0 && nb >= 4) {
         const int bs = nb / 4;
         const unsigned grid = 8u * (unsigned)(bs * (bs + 1) * nact * splits);
         syrk6_kernel<<<grid, 64, 0, s>>>(desc, P, splits, fits, nunits, H, slab, nact, 1);
@@ -1101,7 +901,7 @@ extern "C" int sglm_syrk_cbits(const int64_t* desc, int32_t P, const int32_t* fi
         syrk6_kernel<<<dim3((unsigned)(nunits * nact), (unsigned)splits), 64, 0, s>>>(
             desc, P, splits, fits, nunits, H, slab, nact, 0);
     }
-    int st = check_launch("syrk6_kernel / syrk7_kernel");
+    int st = check_launch("syrk6_kernel");
     if (st || splits == 1) return st;
     const int64_t PP = (int64_t)P * P;
     unsigned gx = (unsigned)((PP + 255) / 256 < 4096 ? (PP + 255) / 256 : 4096);

@@ -583,9 +583,9 @@ def test_syrk_cbits_compacted_gram(engine, torch_mod):
 
 @pytest.mark.parametrize("L,splits", [(10, 1), (20, 3)])
 def test_syrk_cbits_xcd_banded_placement(engine, torch_mod, monkeypatch, L, splits):
-    """SGLM_SYRK_XCD=1 (128-blocks dealt to the XCDs by band pairs) and SGLM_SYRK7=1 (two waves
-    per SIMD, 128 x 64 half-blocks) compute every block with the same K slabs as the default
-    kernel: the Grams are equal bit for bit (P = 512 and 1024, 1 and 3 row slabs, 3 fits)."""
+    """SGLM_SYRK_XCD=1 (128-blocks dealt to the XCDs by band pairs) computes every block with
+    the same K slabs as the default placement: the Grams are equal bit for bit (P = 512 and
+    1024, 1 and 3 row slabs, 3 fits)."""
     torch = torch_mod
     from sglm_hip import _lib, synth
     s = synth.make(N=20000, m=50, L=L, rho=0.05, seed=L)
@@ -611,22 +611,16 @@ def test_syrk_cbits_xcd_banded_placement(engine, torch_mod, monkeypatch, L, spli
     wk = torch.empty(max(_lib.query("sglm_syrk_work_bytes", d.P, B, splits), 16),
                      dtype=torch.uint8, device="cuda")
     blk = np.triu(np.ones((d.P, d.P), dtype=bool))
-    ib = np.arange(d.P) // 128
-    bup = ib[:, None] <= ib[None, :]                    # every 128-block a kernel writes
     out = {}
-    for xm, s7 in (("0", "0"), ("1", "0"), ("s7", "1")):
-        monkeypatch.setenv("SGLM_SYRK_XCD", "1" if xm == "1" else "0")
-        monkeypatch.setenv("SGLM_SYRK7", s7)
+    for xm in ("0", "1"):
+        monkeypatch.setenv("SGLM_SYRK_XCD", xm)
         H = torch.full((B, d.P, d.P), float("nan"), dtype=torch.float32, device="cuda")
         _lib.call("sglm_syrk_cbits", desc.data_ptr(), d.P, fits.data_ptr(), B, splits,
                   H.data_ptr(), wk.data_ptr(), 0)
         out[xm] = H.cpu().numpy()
-    monkeypatch.setenv("SGLM_SYRK7", "0")
     for k in range(B):
         assert np.all(np.isfinite(out["1"][k][blk])), k
         assert np.array_equal(out["0"][k][blk], out["1"][k][blk]), k
-        # the two-wave half-block kernel (syrk7_kernel): every written block bit for bit
-        assert np.array_equal(out["0"][k][bup], out["s7"][k][bup]), k
 
 
 def test_eta_bits_matches_float64(engine, torch_mod):
