@@ -423,6 +423,9 @@ def assemble(groups: Sequence[dict], plan, results: dict, p: int):
     """Per-param result dicts (reference key order, backend/sglm_cv.py:188-200) of every group
     from the merged per-fit results {table index: (coef, intercept, n_iter, converged, scores)}."""
     specs, gm, counts, table, roll_list = plan
+    rows = {}                                   # (group, param) -> [(table index, split)]
+    for i, t in enumerate(table):
+        rows.setdefault((t[0], t[1]), []).append((i, t[2]))
     out_all = []
     for gi, g in enumerate(groups):
         K = len(gm[gi][0])
@@ -437,9 +440,7 @@ def assemble(groups: Sequence[dict], plan, results: dict, p: int):
             conv = True
             refit = None
             hold_scores = None
-            for i, (gg, jj, k, m, r, mt) in enumerate(table):
-                if gg != gi or jj != j:
-                    continue
+            for i, k in rows.get((gi, j), ()):
                 coef, b, it, cv_ok, sc = results[i]
                 n_iter.append(it)
                 conv &= cv_ok
