@@ -622,9 +622,11 @@ int sglm_host_gather_cols(const void* const* src, const int64_t* stride, int32_t
                           int64_t nrows, int32_t elem, void* dst, int32_t nthreads);
 /* sglm_host_pack_bits_cols: float64 columns (src[c], element stride stride[c]) as bit-planes,
  * bit r of bits[c * ceil(nrows / 32) + r / 32] = (value == 1.0); binary[c] = 1 when every
- * value is 0.0 or 1.0.  The 0/1 event columns of a lagged frame cross PCIe as bits. */
+ * value is 0.0 or 1.0; ones[c] (may be NULL) = the count of 1.0 values.  The 0/1 event
+ * columns of a lagged frame cross PCIe as bits. */
 int sglm_host_pack_bits_cols(const void* const* src, const int64_t* stride, int32_t ncols,
-                             int64_t nrows, uint32_t* bits, uint8_t* binary, int32_t nthreads);
+                             int64_t nrows, uint32_t* bits, uint8_t* binary, int64_t* ones,
+                             int32_t nthreads);
 /* sglm_host_group_rows: the row lists of GroupShuffleSplit folds from per-group sides --
  * out[j] (caller-allocated, len[j] entries) = the ascending rows i < n with
  * side[(j / 2) * G + gidx[i]] == 1 + (j % 2) (1 train, 2 test), j < 2 * nsplits:

@@ -199,11 +199,12 @@ extern "C" int sglm_host_gather_cols(const void* const* src, const int64_t* stri
 // sglm_host_pack_bits_cols: for each column (float64, src[c] with element stride stride[c]),
 // bit r of bits[c * nwords + r / 32] = (value == 1.0), and binary[c] = 1 when every value is
 // 0.0 or 1.0 (a NaN, -0.0 is 0.0, or any other value clears it) -- a 0/1 event column crosses
-// PCIe as 1 bit per row instead of 8 bytes.  Threads own 2048-row ranges; nwords = ceil(nrows
+// PCIe as 1 bit per row instead of 8 bytes; ones[c] (when not NULL) = the column's count of
+// 1.0 cells.  Threads own 2048-row ranges; nwords = ceil(nrows
 // / 32).
 extern "C" int sglm_host_pack_bits_cols(const void* const* src, const int64_t* stride,
                                         int32_t ncols, int64_t nrows, uint32_t* bits,
-                                        uint8_t* binary, int32_t nthreads) {
+                                        uint8_t* binary, int64_t* ones, int32_t nthreads) {
     if (ncols <= 0 || nrows <= 0) return SGLM_OK;
     if (!src || !bits || !binary) { sglm::set_error("sglm_host_pack_bits_cols: bad args"); return SGLM_EINVAL; }
     const int64_t nwords = (nrows + 31) / 32;
@@ -211,6 +212,7 @@ extern "C" int sglm_host_pack_bits_cols(const void* const* src, const int64_t* s
     const int64_t nchunks = (nrows + chunk - 1) / chunk;
     const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(nthreads, nchunks));
     std::vector<std::vector<uint8_t>> bad(nt, std::vector<uint8_t>(ncols, 0));
+    std::vector<std::vector<int64_t>> cnt(nt, std::vector<int64_t>(ncols, 0));
     std::vector<std::thread> th;
     // the columns of ONE row-major block (a DataFrame built from a C-order array: column c at
     // base + c, row stride S >= ncols) are read row by row, each row's run of ncols values
@@ -222,7 +224,7 @@ extern "C" int sglm_host_pack_bits_cols(const void* const* src, const int64_t* s
     if (block) {
         const double* base = (const double*)src[0];
         for (int t = 0; t < nt; ++t)
-            th.emplace_back([=, &bad] {
+            th.emplace_back([=, &bad, &cnt] {
                 std::vector<uint32_t> word(ncols);
                 std::vector<uint8_t> b(ncols, 0);
                 uint8_t* bl = b.data();
@@ -240,7 +242,10 @@ extern "C" int sglm_host_pack_bits_cols(const void* const* src, const int64_t* s
                                 bl[c] |= (uint8_t)!(v == 0.0 || v == 1.0);
                             }
                         }
-                        for (int c = 0; c < ncols; ++c) bits[(size_t)c * nwords + w0 / 32] = wd[c];
+                        for (int c = 0; c < ncols; ++c) {
+                            bits[(size_t)c * nwords + w0 / 32] = wd[c];
+                            cnt[t][c] += __builtin_popcount(wd[c]);
+                        }
                     }
                 }
                 for (int c = 0; c < ncols; ++c) bad[t][c] = bl[c];
@@ -248,13 +253,18 @@ extern "C" int sglm_host_pack_bits_cols(const void* const* src, const int64_t* s
         for (auto& x : th) x.join();
         for (int c = 0; c < ncols; ++c) {
             uint8_t x = 0;
-            for (int t = 0; t < nt; ++t) x |= bad[t][c];
+            int64_t o = 0;
+            for (int t = 0; t < nt; ++t) {
+                x |= bad[t][c];
+                o += cnt[t][c];
+            }
             binary[c] = !x;
+            if (ones) ones[c] = o;
         }
         return SGLM_OK;
     }
     for (int t = 0; t < nt; ++t)
-        th.emplace_back([=, &bad] {
+        th.emplace_back([=, &bad, &cnt] {
             for (int64_t q = t; q < nchunks; q += nt) {
                 const int64_t r0 = q * chunk, r1 = std::min(nrows, r0 + chunk);
                 for (int c = 0; c < ncols; ++c) {
@@ -271,6 +281,7 @@ extern "C" int sglm_host_pack_bits_cols(const void* const* src, const int64_t* s
                             b |= (uint8_t)!(v == 0.0 || v == 1.0);
                         }
                         out[w0 / 32] = word;
+                        cnt[t][c] += __builtin_popcount(word);
                     }
                     bad[t][c] |= b;
                 }
@@ -279,8 +290,13 @@ extern "C" int sglm_host_pack_bits_cols(const void* const* src, const int64_t* s
     for (auto& x : th) x.join();
     for (int c = 0; c < ncols; ++c) {
         uint8_t b = 0;
-        for (int t = 0; t < nt; ++t) b |= bad[t][c];
+        int64_t o = 0;
+        for (int t = 0; t < nt; ++t) {
+            b |= bad[t][c];
+            o += cnt[t][c];
+        }
         binary[c] = !b;
+        if (ones) ones[c] = o;
     }
     return SGLM_OK;
 }

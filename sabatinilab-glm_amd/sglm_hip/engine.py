@@ -305,7 +305,8 @@ class Design:
                 ev.synchronize()                      # the staging buffers are reusable
 
     @classmethod
-    def from_lagged(cls, Ecm, cols, shifts, r0: int, n: int, rows=None, device="cuda"):
+    def from_lagged(cls, Ecm, cols, shifts, r0: int, n: int, rows=None, device="cuda",
+                    ones=None):
         """A design whose column j is source column cols[j] lagged by shifts[j]:
         X[t, j] = Ecm[cols[j], row(t) - shifts[j]] with row(t) = r0 + t (rows None) or rows[t]
         (a device int64 row list).  Ecm: device float64 [m][N] source columns (NaN-free on
@@ -322,7 +323,11 @@ class Design:
                 if lay is not None:
                     ev, sl = lay
                     E = Ecm[torch.from_numpy(ev).to(Ecm.device)].t()
-                    return cls.from_events(E, sl, r0, n, device=device, event_major=major)
+                    # ones: per source row of Ecm its count of 1 cells when every source is
+                    # known 0/1 (the host pack's flags): no device checks or counts to wait on
+                    hint = None if ones is None else int(np.asarray(ones, np.int64)[ev].sum())
+                    return cls.from_events(E, sl, r0, n, device=device, event_major=major,
+                                           nnz=hint)
         p = int(cols.size)
         d = cls(n, p, device, zero=True)
         c_d = torch.from_numpy(cols.astype(np.int32)).to(device)
@@ -388,7 +393,7 @@ class Design:
 
     @classmethod
     def from_events(cls, E, shifts: Sequence[int], row0: int, n: int, device="cuda",
-                    event_major=False, slab=None):
+                    event_major=False, slab=None, nnz=None):
         """Expand base events E (N_raw x m) into lag columns directly on the device.
 
         Output column (shift block b, event a) = E[t + row0 - shifts[b], a] for rows
@@ -425,7 +430,8 @@ class Design:
                       _p(xb), n, 1, xb.shape[1], row0, 2, 0, _stream())
             xb[p, :n] = 1.0
 
-        if LAG_BITS and bool(((E == 0) | (E == 1)).all()):
+        # nnz (the events' count of 1 cells) is given only for events known to be 0/1
+        if LAG_BITS and (nnz is not None or bool(((E == 0) | (E == 1)).all())):
             # 0/1 events: the bit-planes straight from the events' occurrence bitmaps (no dense
             # 4-GB-at-C4 design to write and pack twice); the dense copy is built on first use
             d = cls(n, p, device, lazy_xb=fill)
@@ -436,7 +442,7 @@ class Design:
             d.rbits = torch.empty((d.P // 64) * d.ld * 2, dtype=torch.int32, device=device)
             _lib.call("sglm_lag_bits", _p(ebits), nwords, _p(cols_d), _p(sh_d), p, row0, n,
                       d.ld, d.P, _p(d.xbits), _p(d.rbits), _stream())
-            d.lag = LagStructure.build(E, shifts, row0, n, event_major, ebits=ebits)
+            d.lag = LagStructure.build(E, shifts, row0, n, event_major, ebits=ebits, nnz=nnz)
             d.slab = info
             return d
         d = cls(n, p, device, zero=True)
@@ -551,7 +557,7 @@ class LagStructure:
     design."""
 
     @classmethod
-    def build(cls, E, shifts, row0, n, event_major, ebits=None):
+    def build(cls, E, shifts, row0, n, event_major, ebits=None, nnz=None):
         self = cls()
         dev = E.device
         N_raw, m = E.shape
@@ -560,7 +566,10 @@ class LagStructure:
         self.layout = 1 if event_major else 0
         self.row0 = int(row0)
         self.shifts = torch.from_numpy(sh.astype(np.int32)).to(dev)
-        nz = torch.nonzero(E.t() != 0)                       # (event, row), event-major order
+        # (event, row) of every occurrence, event-major; a known count sizes it without
+        # waiting for the device
+        nz = (torch.nonzero(E.t() != 0) if nnz is None
+              else torch.nonzero_static(E.t() != 0, size=int(nnz)))
         ev, rows = nz[:, 0], nz[:, 1]
         self.occ = rows.to(torch.int32).contiguous()
         U = _lib.query("sglm_lag_tile_rows")

@@ -45,6 +45,7 @@ class LagSource:
         self._dev = {}           # column name -> row of self._E
         self._E = None
         self._hasnan = {}        # column name -> holds a NaN cell
+        self._ones = {}          # 0/1 column name -> its count of 1 cells (host pack)
         self._numeric = {}       # column name -> numeric dtype
         self.cast = {}           # base column name -> dtype of its shift-0 copy in the frame
         self.all_rows = None     # arange(N), built once
@@ -66,12 +67,15 @@ class LagSource:
             nw = (N + 31) // 32
             bits = _pinned("lagbits", max(1, m * nw), torch.int32)
             binary = np.zeros(m, dtype=np.uint8)
+            ones = np.zeros(m, dtype=np.int64)
             ptrs = (ctypes.c_void_p * m)(*[a.ctypes.data for a in arrs])
             strides = np.array([a.strides[0] // 8 for a in arrs], dtype=np.int64)
             _lib.call("sglm_host_pack_bits_cols", ctypes.cast(ptrs, ctypes.c_void_p),
                       strides.ctypes.data, m, N, bits.data_ptr(), binary.ctypes.data,
-                      HOST_THREADS)
+                      ones.ctypes.data, HOST_THREADS)
             bsel = np.flatnonzero(binary)
+            for i in bsel:
+                self._ones[need[i]] = int(ones[i])
             if bsel.size:
                 bd = bits[: m * nw].view(m, nw)[torch.from_numpy(bsel)].to("cuda",
                                                                               non_blocking=True)
@@ -132,6 +136,10 @@ class LagSource:
             self._numeric[name] = (isinstance(dt, np.dtype) and dt.kind in "biuf") or \
                 pd.api.types.is_numeric_dtype(dt)
         return self._numeric[name]
+
+    def ones(self, name):
+        """Count of 1 cells of an uploaded 0/1 column (None for any other column)."""
+        return self._ones.get(name)
 
     def has_nan(self, name) -> bool:
         """Whether an uploaded column holds a NaN cell."""
@@ -594,8 +602,10 @@ class LagFrame:
         pos = self.positions()
         n = int(pos.size)
         sp = self._span()
+        ones = [self._src.ones(nm) for nm in names]
+        ones = None if any(o is None for o in ones) else ones
         if n and (sp is not None or (pos[-1] - pos[0] == n - 1 and np.all(np.diff(pos) == 1))):
-            d = Design.from_lagged(Esub, cols, shifts, int(pos[0]), n)
+            d = Design.from_lagged(Esub, cols, shifts, int(pos[0]), n, ones=ones)
         else:
             import torch
             rows_d = torch.from_numpy(np.ascontiguousarray(pos, dtype=np.int64)).to("cuda")

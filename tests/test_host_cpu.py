@@ -166,16 +166,19 @@ def test_host_pack_bits_cols(layout):
     nw = (N + 31) // 32
     bits = np.zeros(k * nw, np.uint32)
     binary = np.zeros(k, np.uint8)
+    ones = np.zeros(k, np.int64)
     ptrs = (ctypes.c_void_p * k)(*[a.ctypes.data for a in arrs])
     strides = np.array([a.strides[0] // 8 for a in arrs], dtype=np.int64)
     _lib.call("sglm_host_pack_bits_cols", ctypes.cast(ptrs, ctypes.c_void_p),
-              strides.ctypes.data, k, N, bits.ctypes.data, binary.ctypes.data, 4)
+              strides.ctypes.data, k, N, bits.ctypes.data, binary.ctypes.data,
+              ones.ctypes.data, 4)
     V = np.stack(arrs)
     ref = np.packbits(V == 1.0, axis=1, bitorder="little")
     ref = np.ascontiguousarray(np.pad(ref, ((0, 0), (0, 4 * nw - ref.shape[1])))).view(np.uint32)
     np.testing.assert_array_equal(bits.reshape(k, nw), ref)
     want = [bool(np.all((v == 0.0) | (v == 1.0))) for v in V]
     np.testing.assert_array_equal(binary.astype(bool), want)
+    np.testing.assert_array_equal(ones, (V == 1.0).sum(axis=1))
 
 
 def test_negative_fold_indices_wrap_like_numpy():
