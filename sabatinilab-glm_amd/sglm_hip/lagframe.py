@@ -55,7 +55,7 @@ class LagSource:
         and the device int64 row index of each name."""
         import ctypes
         import torch
-        from .engine import HOST_THREADS, _pinned, require_gpu
+        from .engine import HOST_THREADS, _pinned, _scratch, require_gpu
         require_gpu()
         need = [c for c in dict.fromkeys(names) if c not in self._dev]
         if need:
@@ -66,6 +66,9 @@ class LagSource:
             # float64 through the pinned stages below
             nw = (N + 31) // 32
             bits = _pinned("lagbits", max(1, m * nw), torch.int32)
+            evk = ("lagbits_ev", None)
+            if _scratch().pinned.get(evk) is not None:
+                _scratch().pinned[evk].synchronize()      # the last upload has read the stage
             binary = np.zeros(m, dtype=np.uint8)
             ones = np.zeros(m, dtype=np.int64)
             ptrs = (ctypes.c_void_p * m)(*[a.ctypes.data for a in arrs])
@@ -77,11 +80,19 @@ class LagSource:
             for i in bsel:
                 self._ones[need[i]] = int(ones[i])
             if bsel.size:
-                bd = bits[: m * nw].view(m, nw)[torch.from_numpy(bsel)].to("cuda",
-                                                                              non_blocking=True)
+                # all 0/1 (an event frame): the pinned stage goes up as it is, asynchronously
+                every = bsel.size == m
+                bd = bits[: m * nw].view(m, nw)
+                bd = (bd if every else bd[torch.from_numpy(bsel)]).to("cuda", non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+                _scratch().pinned[evk] = ev
                 sh = torch.arange(32, dtype=torch.int32, device="cuda")
                 unp = ((bd.unsqueeze(-1) >> sh) & 1).reshape(bsel.size, nw * 32)[:, :N]
-                new[torch.from_numpy(bsel).to("cuda")] = unp.to(torch.float64)
+                if every:
+                    new = unp.to(torch.float64)
+                else:
+                    new[torch.from_numpy(bsel).to("cuda")] = unp.to(torch.float64)
             raw = np.flatnonzero(binary == 0)
             need_raw = [need[i] for i in raw]
             arr_raw = [arrs[i] for i in raw]
@@ -111,11 +122,18 @@ class LagSource:
                     ev.synchronize()
             base = 0 if self._E is None else self._E.shape[0]
             self._E = new if self._E is None else torch.cat([self._E, new])
-            has = torch.isnan(new).any(1).cpu().numpy()
+            # 0/1 columns hold no NaN: only raw columns are checked on the device
+            has = (torch.isnan(new).any(1).cpu().numpy() if raw.size
+                   else np.zeros(m, dtype=bool))
             for i, c in enumerate(need):
                 self._dev[c] = base + i
                 self._hasnan[c] = bool(has[i])
-        idx = torch.tensor([self._dev[c] for c in names], dtype=torch.int64, device="cuda")
+        rows = [self._dev[c] for c in names]
+        if rows and rows == list(range(rows[0], rows[0] + len(rows))):
+            # consecutive rows (names in upload order): no host->device copy to wait on
+            idx = torch.arange(rows[0], rows[0] + len(rows), dtype=torch.int64, device="cuda")
+        else:
+            idx = torch.tensor(rows, dtype=torch.int64, device="cuda")
         return self._E, idx
 
     def _f64(self, name) -> np.ndarray:
