@@ -322,13 +322,13 @@ eta_dir_kernel(const u32x2* __restrict__ rbits, int64_t ld, int32_t P,
     }
 }
 
-// eta_dir_kernel deepened (eta_pipe_kernel<NP, NG, NT>): each wave covers NT 32-row tiles, so
-// a staged coefficient fragment feeds NT MFMAs (eta_dir_kernel: 2) and a workgroup's
-// coefficient tile crosses L2 once per 4 x NT x 32 rows; one wave per SIMD (the accumulator
-// tiles fill the AGPRs), its latency covered by the loads instead of a second wave: the bit
-// words are loaded two K-steps ahead through a three-set register ring and the next step's
-// coefficient tile one step ahead (all loads in asm with static vmcnt counts -- loads for
-// absent fit groups and past the last step re-read valid addresses), one barrier per K-step.
+// eta_dir_kernel deepened (eta_pipe_kernel<NP, NG, NT, WPE>): each wave covers NT 32-row tiles
+// (a staged coefficient fragment feeds NT MFMAs; the coefficient tile crosses L2 once per
+// 4 x NT x 32 rows) at WPE waves per SIMD; the bit words are loaded two K-steps ahead through a
+// three-set register ring and the next step's coefficient tile one step ahead (all loads in asm
+// with static vmcnt counts -- loads for absent fit groups and past the last step re-read valid
+// addresses), one barrier per K-step.  The defaults (NT = 2, two waves per SIMD) measured
+// fastest: with NT = 4 at one wave per SIMD the per-step barrier bubble is left uncovered.
 // NP = 1 (rounded directions): the products and f32 accumulation order per (fit, row) of
 // eta_bits_kernel<1, .> -- bitwise equal; NP = 3 (exact coefficients): those of
 // eta_dir_kernel<3, .>, a hi accumulator and a mid + lo one -- bitwise equal to it.
