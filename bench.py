@@ -39,6 +39,9 @@ PEAK_F64_TFLOPS = 61.3
 CONFIGS = {
     # name: (N rows, events m, L -> lags -L..L-1, n_splits, lambdas)
     "c4": (1_000_000, 50, 20, 5, 20),
+    # C4 plus the production design's two unshifted continuous counters (cumcount^2 / 5000,
+    # pp_design_mat.py:167-172): a mixed 0/1 + float64 design (csrc/mixed.hip)
+    "c4mixed": (1_000_000, 50, 20, 5, 20),
     "c3": (100_000, 25, 10, 5, 20),
     "small": (50_000, 10, 5, 5, 4),
     # C5: 64 responses x C4 design, Gaussian elastic-net lambda path (l1_ratio 0.5, 20 alphas)
@@ -657,18 +660,22 @@ def dropin_grid(df, ev, L, K, lams):
     return out[4], ph
 
 
-def newton_distance(s, design, cv_idx, res, lams, checks):
+def newton_distance(s, design, cv_idx, res, lams, checks, extra=None):
     """float64 Newton distance of a few fits of the last grid to the exact minimiser,
     max_j<p |(H^-1 g)_j| / max_j<p |beta_j| (the coefficients), from the exact design on the
     device (torch float64; outside the timed region)."""
     import torch
     m = s.E.shape[1]
     Ed = torch.from_numpy(s.E).cuda().to(torch.float64)
-    Xd = torch.empty((s.N, s.p + 1), dtype=torch.float64, device="cuda")
+    kx = 0 if extra is None else extra.shape[0]
+    p = s.p + kx
+    Xd = torch.empty((s.N, p + 1), dtype=torch.float64, device="cuda")
     r0 = s.L - 1
     for bi, sh in enumerate(s.shifts):
         Xd[:, bi * m:(bi + 1) * m] = Ed[r0 - sh:r0 - sh + s.N]
-    Xd[:, s.p] = 1.0
+    if kx:
+        Xd[:, s.p:p] = torch.from_numpy(extra.T).cuda()
+    Xd[:, p] = 1.0
     yd = torch.from_numpy(s.y).cuda()
     worst = 0.0
     for j, k in checks:
@@ -683,7 +690,7 @@ def newton_distance(s, design, cv_idx, res, lams, checks):
             w[torch.from_numpy(np.asarray(msk)).cuda()] = 1.0
         beta = torch.from_numpy(np.r_[coef, b]).cuda()
         mu = torch.exp(Xd @ beta)
-        pen = torch.full((s.p + 1,), float(lams[j]) * float(w.sum()), dtype=torch.float64,
+        pen = torch.full((p + 1,), float(lams[j]) * float(w.sum()), dtype=torch.float64,
                          device="cuda")
         pen[-1] = 0.0
         g = Xd.t() @ (w * (mu - yd)) + pen * beta
@@ -732,7 +739,8 @@ def main():
         grid.SHARD_MODE = a.shard
     rows_mode = world > 1 and grid.SHARD_MODE == "rows"
     slab = grid.rank_slab(s.N, rank, world) if rows_mode else None
-    design = E.Design.from_events(s.E, s.shifts, s.L - 1, s.N, slab=slab)
+    extra = synth.prod_counters(s.trial, seed=1) if a.config == "c4mixed" else None
+    design = E.Design.from_events(s.E, s.shifts, s.L - 1, s.N, slab=slab, extra=extra)
     codes = folds.trial_keys_codes(__import__("pandas").DataFrame({"nTrial": s.trial}), ["nTrial"]).values
     np.random.seed(3)
     cv_idx = folds.cv_idx_from_bucket_ids(codes, num_folds=K)
@@ -800,10 +808,10 @@ def main():
         traffic, traffic_src = pmc_traffic()
         conv = all(r["converged"] for r in res)
         ndist = None
-        if world == 1 and a.config == "c4":
+        if world == 1 and a.config in ("c4", "c4mixed"):
             # float64 Newton distance of the lambda = 1e-4 split-0 fit and refit (parity spot
             # check of the timed grid's output; tests/test_gpu_fullsize.py checks every fit)
-            ndist = newton_distance(s, design, cv_idx, res, lams, [(0, 0), (0, -1)])
+            ndist = newton_distance(s, design, cv_idx, res, lams, [(0, 0), (0, -1)], extra)
         dropin = None
         if world == 1 and a.config in ("c3", "c4") and not a.no_dropin:
             # the production flow through the drop-in API from a host event DataFrame (the
@@ -829,7 +837,7 @@ def main():
                                      "sglm_ez.timeshift_cols -> isna().sum(axis=1) == 0 row "
                                      "filter -> cv_idx_by_trial_id -> simple_cv_fit"}
         cpu = None
-        if not a.no_cpu and world == 1:
+        if not a.no_cpu and world == 1 and extra is None:
             cpu = cpu_reference_grid(s, cv_idx, lams, a.sklearn_rows)
             cpu["port_oracle_newton"] = cpu_port_iter(s, s.N, a.cpu_rows)
         out = {
@@ -847,8 +855,9 @@ def main():
                      "(3 bf16 pieces, f64 slab sums) / f64 coefficients and line search",
             "data": "synthetic",
             "config": {
-                "workload": f"Poisson CV grid {s.N}x{s.p} ({m} events x {len(s.shifts)} lags), "
-                            f"{K} splits x {nlam} lambdas + refits",
+                "workload": f"Poisson CV grid {s.N}x{design.p} ({m} events x {len(s.shifts)} lags"
+                            + (f" + {design.k} continuous counters" if design.k else "")
+                            + f"), {K} splits x {nlam} lambdas + refits",
                 "config_name": a.config,
                 "irls_fit_iters_per_s": fit_iters / elapsed,
                 "irls_fit_iters_counted": "fit-iterations incl. aliased / kept-factor ones "

@@ -98,6 +98,14 @@ int sglm_pack_design_rows(const void* src, int32_t src_is_f64, int64_t n, int32_
  * LinearRegression lstsq (_base.py:701). */
 
 /* eta[k][i] = sum_a X[a][i] * beta[k][a]  for k < B, i < n (f32; also used for d_eta). */
+/* sglm_pack_design_rows that also sets colflag[a] = 1 (device int32 [p], accumulated over
+ * calls) for every source column a holding a value other than 0 or 1 (NaN included), judged on
+ * the source values before rounding: the split of a mixed 0/1 + continuous design. */
+int sglm_pack_design_rows_cf(const void* src, int32_t src_is_f64, int64_t n, int32_t p,
+                             int64_t rs, int64_t cs, int32_t add_ones, uint16_t* Xb, float* Xf,
+                             int64_t ld, int32_t P, int64_t dst0, int32_t* inexact,
+                             int32_t* colflag, sglm_stream_t stream);
+
 int sglm_gemv_eta(const void* X, int32_t xtype, int64_t ld, int32_t P, int64_t n,
                   const float* beta, int32_t B, float* eta, sglm_stream_t stream);
 
@@ -359,9 +367,35 @@ int sglm_chol64_factor(const float* H, int32_t P, const int32_t* hsrc, const flo
                        const double* lamp, const int32_t* dsrc, int32_t nf, double tol,
                        double* U, uint8_t* state, int32_t* nulls, int32_t* counts, void* work,
                        sglm_stream_t stream);
+/* sglm_chol64_factor_mixed: sglm_chol64_factor for a mixed 0/1 + continuous design: the rows
+ *   and columns of the continuous coordinates j (cmap[j] = c >= 0, cmap[j] = -1 elsewhere) are
+ *   read from the float64 Gram block S[f][c][0 .. P) (sglm_mixed_gram, exact to rounding)
+ *   instead of the f32 H, so that the rank decision of a continuous column is taken on its
+ *   float64 Gram row (lstsq's float64 X, sklearn _base.py:701). */
+int sglm_chol64_factor_mixed(const float* H, int32_t P, const int32_t* hsrc, const float* dshift,
+                             const double* lamp, const int32_t* dsrc, int32_t nf, double tol,
+                             const double* S, int32_t k, const int32_t* cmap, double* U,
+                             uint8_t* state, int32_t* nulls, int32_t* counts, void* work,
+                             sglm_stream_t stream);
 int sglm_chol64_solve(const double* U, int32_t P, const uint8_t* state, const int32_t* fits,
                       const int32_t* fsrc, int32_t nq, const double* g, float* delta,
                       sglm_stream_t stream);
+/* sglm_chol64_solve_add: x[fits[q]] += U_f^-1 U_f^-T g[gsrc[q]] (float64 out; gsrc NULL: the
+ *   fit's own row) on the kept coordinates of f = fsrc[q].
+ * sglm_chol64_resid: r[fits[q]] = c[csrc[q]] - (G_f + diag(lamp[fits[q]])) x[fits[q]] (float64)
+ *   with G_f the symmetric Gram of factor f = fsrc[q] read from the f32 upper triangle
+ *   H[hsrc[f]] (exact 0/1 mask counts) and, for a mixed design, the float64 rows S[f][c] of its
+ *   continuous coordinates (cmap[j] = c >= 0); 0 on excluded coordinates (dshift < 0).
+ *   Together: the squared-loss fit in Gram space, x = (G + lam I')^-1 X^T (m y) with one float64
+ *   refinement -- the normal equations of sklearn Ridge(solver='cholesky') (_ridge.py:201-213)
+ *   and the lstsq answer of LinearRegression (_base.py:701) to float64 rounding. */
+int sglm_chol64_solve_add(const double* U, int32_t P, const uint8_t* state, const int32_t* fits,
+                          const int32_t* fsrc, const int32_t* gsrc, int32_t nq, const double* g,
+                          double* x, sglm_stream_t stream);
+int sglm_chol64_resid(const float* H, int32_t P, const int32_t* hsrc, const double* S, int32_t k,
+                      const int32_t* cmap, const int32_t* fits, const int32_t* fsrc,
+                      const int32_t* csrc, int32_t nq, const double* c, const double* lamp,
+                      const float* dshift, const double* x, double* r, sglm_stream_t stream);
 size_t sglm_chol64_minnorm_work_bytes(int32_t P, int32_t nf);
 int sglm_chol64_minnorm(const double* U, int32_t P, int32_t pw, const uint8_t* state,
                         const int32_t* nulls, const int32_t* counts, int32_t nf,
@@ -538,6 +572,51 @@ int sglm_lag_gram(const int32_t* occ, const int32_t* ev_off, const uint32_t* ebi
                   int32_t smin, int32_t smax, int64_t row0, int64_t n, int64_t n_raw, int32_t P,
                   const float* W, int64_t ldw, const int32_t* fits, int32_t nfits, float* H,
                   void* work, sglm_stream_t stream);
+
+/* sglm_lag_gram with the intercept column at pc >= m*K: columns m*K .. pc-1 (a mixed
+ * design's continuous columns, completed by sglm_mixed_gram / sglm_mixed_to_h) are written 0. */
+int sglm_lag_gram_pc(const int32_t* occ, const int32_t* ev_off, const uint32_t* ebits,
+                     int64_t nwords, const int32_t* shifts, int32_t m, int32_t K, int32_t layout,
+                     int32_t smin, int32_t smax, int64_t row0, int64_t n, int64_t n_raw, int32_t P,
+                     int32_t pc, const float* W, int64_t ldw, const int32_t* fits, int32_t nfits,
+                     float* H, void* work, sglm_stream_t stream);
+
+/* --- mixed 0/1 + continuous designs ------------------------------------------------------
+ * The production design of the reference (sglm_cb_concat_make_design_mat.py:224-244, 310) puts
+ * continuous counters (cumcount^2 / 5000, pp_design_mat.py:167-172) beside 0/1 event lags and
+ * fits it in float64 through simple_cv_fit (:356-363 -> backend/sglm_cv.py:106-131 -> sklearn).
+ * Here the k continuous columns are a float64 block C [k][ldc] at design positions cpos[c]
+ * (their bit-plane columns are zero); these calls complete the bit-plane kernels' products.
+ * Row sums are chunked and summed in a fixed order (deterministic).
+ * sglm_mixed_wc: R[q][r] = W[slots[q / k]][r] * f32(C[q % k][r]) (r < n; 0 up to ld), the f32
+ *   operand of sglm_xtr_bits for the Gram rows X^T W C of an IRLS Hessian.
+ * sglm_mixed_gram: S[s][c][cpos[c']] = S[s][c'][cpos[c]] = sum_r wt_s(r) C[c][r] C[c'][r]
+ *   (float64) for c <= c' (pairs: device int32 [2][k(k+1)/2], the (c, c') lists); wt_s =
+ *   f32 W[wsel[s]] (wmode 0) or uint8 mask M[wsel[s]] (wmode 1), rows of ldw elements.
+ * sglm_mixed_xtr: g[gslots[q]][cpos[c]] = sum_r C[c][r] R_q(r) (float64) for q < nq, R_q = row
+ *   rsel[q] (q when NULL) of: f32 [*][ldr] (rmode 0); the packed three-piece bf16 buffer of
+ *   sglm_link_update, [3][Bp][ldr] (rmode 2); one bf16 plane [*][ldr] (rmode 3).  pairs: device
+ *   int32 [2][k] = {0 .. k-1, k .. k}.  Replaces the continuous coordinates of X^T (mu - y).
+ * sglm_mixed_eta: eta[slot][r] += sum_c C[c][r] beta[slot][cpos[c]] (float64 sum, r < n) for
+ *   slot = slots[q] (q when NULL), q < nb; k <= 1024.
+ * sglm_mixed_to_h: H[slot][i][cpos[c]] = H[slot][cpos[c]][i] = f32(S[s][c][i]) for i < P,
+ *   slot = slots[s] (s when NULL).
+ * work (gram, xtr): sglm_mixed_work_bytes(ns or nq, k, n). */
+size_t sglm_mixed_work_bytes(int32_t ns, int32_t k, int64_t n);
+int sglm_mixed_wc(const float* W, int64_t ldw, const int32_t* slots, int32_t ns, const double* C,
+                  int64_t ldc, int32_t k, int64_t n, int64_t ld, float* R, sglm_stream_t stream);
+int sglm_mixed_gram(int32_t wmode, const void* wsrc, int64_t ldw, const int32_t* wsel, int32_t ns,
+                    const double* C, int64_t ldc, int32_t k, int64_t n, const int32_t* cpos,
+                    int32_t P, const int32_t* pairs, double* S, void* work, sglm_stream_t stream);
+int sglm_mixed_xtr(int32_t rmode, const void* R, int64_t ldr, int64_t Bp, const int32_t* rsel,
+                   const int32_t* gslots, int32_t nq, const double* C, int64_t ldc, int32_t k,
+                   int64_t n, const int32_t* cpos, int32_t P, const int32_t* pairs, double* g,
+                   void* work, sglm_stream_t stream);
+int sglm_mixed_eta(const double* C, int64_t ldc, int32_t k, int64_t n, const int32_t* cpos,
+                   const float* beta, int32_t P, const int32_t* slots, int32_t nb, float* eta,
+                   int64_t ld, sglm_stream_t stream);
+int sglm_mixed_to_h(const double* S, int32_t ns, int32_t k, int32_t P, const int32_t* cpos,
+                    const int32_t* slots, float* H, sglm_stream_t stream);
 
 /* --- event design matrix (pp_design_mat.make_design_mat, pp_design_mat.py:6-205) --------
  * Float64 session columns (a pandas float block) on the device.  A pandas groupby over a float

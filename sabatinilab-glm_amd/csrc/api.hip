@@ -57,12 +57,14 @@ template <typename TS>
 __global__ void __launch_bounds__(256) pack_kernel(
     const TS* __restrict__ src, int64_t n, int32_t p, int64_t rs, int64_t cs, int32_t add_ones,
     uint16_t* __restrict__ Xb, float* __restrict__ Xf, int64_t ld, int32_t* inexact,
-    int64_t dst0 = 0) {
+    int64_t dst0 = 0, int32_t* __restrict__ colflag = nullptr) {
     __shared__ float tile[64][65];
+    __shared__ int nonbin[64];
     const int64_t i0 = (int64_t)blockIdx.x * 64;
     const int32_t a0 = blockIdx.y * 64;
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;   // 64 x 4
-    int bad = 0;
+    int bad = 0, nb = 0;
+    if (threadIdx.x < 64) nonbin[threadIdx.x] = 0;
     for (int r = ty; r < 64; r += 4) {           // r: row i offset, tx: column a offset
         const int64_t i = i0 + r;
         const int32_t a = a0 + tx;
@@ -71,6 +73,7 @@ __global__ void __launch_bounds__(256) pack_kernel(
             if (a < p) {
                 const TS sv = src[i * rs + (int64_t)a * cs];
                 v = (float)sv;
+                nb |= !(sv == (TS)0 || sv == (TS)1);    // NaN included
             } else if (a == p && add_ones) {
                 v = 1.0f;
             }
@@ -78,6 +81,13 @@ __global__ void __launch_bounds__(256) pack_kernel(
         tile[r][tx] = v;
     }
     __syncthreads();
+    // per-column "holds a value other than 0 / 1" flags (mixed designs), judged on the source
+    // values before any rounding
+    if (colflag && nb) atomicOr(&nonbin[tx], 1);
+    __syncthreads();
+    if (colflag && threadIdx.x < 64 && nonbin[threadIdx.x] && a0 + (int)threadIdx.x < p &&
+        !colflag[a0 + threadIdx.x])
+        atomicOr(&colflag[a0 + threadIdx.x], 1);
     for (int c = ty; c < 64; c += 4) {           // c: column a offset, tx: row i offset
         const float v = tile[tx][c];
         const __bf16 hb = (__bf16)v;
@@ -686,6 +696,14 @@ static int timeshift_launch(const void* src, int64_t n_src, int64_t rs_src, int6
 int sglm_pack_design_rows(const void* src, int32_t src_is_f64, int64_t n, int32_t p, int64_t rs,
                           int64_t cs, int32_t add_ones, uint16_t* Xb, float* Xf, int64_t ld,
                           int32_t P, int64_t dst0, int32_t* inexact, sglm_stream_t stream) {
+    return sglm_pack_design_rows_cf(src, src_is_f64, n, p, rs, cs, add_ones, Xb, Xf, ld, P, dst0,
+                                    inexact, nullptr, stream);
+}
+
+int sglm_pack_design_rows_cf(const void* src, int32_t src_is_f64, int64_t n, int32_t p,
+                             int64_t rs, int64_t cs, int32_t add_ones, uint16_t* Xb, float* Xf,
+                             int64_t ld, int32_t P, int64_t dst0, int32_t* inexact,
+                             int32_t* colflag, sglm_stream_t stream) {
     if (n <= 0) return SGLM_OK;
     if (!Xb || !inexact || (p > 0 && !src)) { set_error("sglm_pack_design_rows: null pointer"); return SGLM_EINVAL; }
     if (ld % 64 || P % 64 || dst0 % 64 || dst0 < 0 || dst0 + n > ld || P < p + (add_ones ? 1 : 0)) {
@@ -696,9 +714,9 @@ int sglm_pack_design_rows(const void* src, int32_t src_is_f64, int64_t n, int32_
     dim3 grid((unsigned)((n + 63) / 64), (unsigned)(P / 64));
     hipStream_t s = as_stream(stream);
     if (src_is_f64)
-        pack_kernel<double><<<grid, 256, 0, s>>>((const double*)src, n, p, rs, cs, add_ones, Xb, Xf, ld, inexact, dst0);
+        pack_kernel<double><<<grid, 256, 0, s>>>((const double*)src, n, p, rs, cs, add_ones, Xb, Xf, ld, inexact, dst0, colflag);
     else
-        pack_kernel<float><<<grid, 256, 0, s>>>((const float*)src, n, p, rs, cs, add_ones, Xb, Xf, ld, inexact, dst0);
+        pack_kernel<float><<<grid, 256, 0, s>>>((const float*)src, n, p, rs, cs, add_ones, Xb, Xf, ld, inexact, dst0, colflag);
     return check_launch("pack_kernel");
 }
 

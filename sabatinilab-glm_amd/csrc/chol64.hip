@@ -39,12 +39,15 @@ enum : uint8_t { ST_KEPT = 0, ST_DEP = 1, ST_EXCL = 2, ST_ZERO = 3 };
 
 // U[f] (upper triangle, rows i <= j; the strict lower part of diagonal tiles zeroed) from the f32
 // Gram H[hsrc[f]] (i <= j read) plus the penalty row lamp[dsrc[f]] (float64) on the diagonal;
+// a mixed design's continuous coordinates (cmap[j] = c >= 0) read their rows and columns from the
+// float64 block S[f][c][0 .. P) instead (sglm_mixed_gram, exact to float64 rounding);
 // excluded (dshift < 0) and zero-diagonal coordinates become identity rows / columns.  One
 // 64 x 64 tile of the upper triangle per workgroup; diagonal tiles also write state and d0.
 __global__ void __launch_bounds__(256) c64_init_kernel(
     const float* __restrict__ H, int32_t P, const int32_t* __restrict__ hsrc,
     const float* __restrict__ dshift, const double* __restrict__ lamp,
-    const int32_t* __restrict__ dsrc, double* __restrict__ U, uint8_t* __restrict__ state,
+    const int32_t* __restrict__ dsrc, const double* __restrict__ S, int32_t k,
+    const int32_t* __restrict__ cmap, double* __restrict__ U, uint8_t* __restrict__ state,
     double* __restrict__ d0) {
     const int f = blockIdx.y;
     int t = blockIdx.x, bi = 0;
@@ -57,6 +60,16 @@ __global__ void __launch_bounds__(256) c64_init_kernel(
     const float* dsh = dshift + (int64_t)dsrc[f] * P;
     const double* lp = lamp ? lamp + (int64_t)dsrc[f] * P : nullptr;
     double* Uf = U + (int64_t)f * P * P;
+    const double* Sf = S ? S + (int64_t)f * k * P : nullptr;
+    auto gram = [&](int i, int j) -> double {
+        if (Sf) {
+            const int ci = cmap[i];
+            if (ci >= 0) return Sf[(int64_t)ci * P + j];
+            const int cj = cmap[j];
+            if (cj >= 0) return Sf[(int64_t)cj * P + i];
+        }
+        return (double)Hs[(int64_t)i * P + j];
+    };
     __shared__ uint8_t sr[kB], sc[kB];
     const int tid = threadIdx.x;
     if (tid < 2 * kB) {
@@ -65,7 +78,7 @@ __global__ void __launch_bounds__(256) c64_init_kernel(
         uint8_t s = ST_EXCL;
         double d = 0.0;
         if (!(dsh[j] < 0.0f)) {
-            d = (double)Hs[(int64_t)j * P + j] + (lp ? lp[j] : (double)dsh[j]);
+            d = gram(j, j) + (lp ? lp[j] : (double)dsh[j]);
             s = d > 0.0 ? ST_KEPT : ST_ZERO;
         }
         if (row) sr[tid] = s; else sc[tid - kB] = s;
@@ -82,7 +95,7 @@ __global__ void __launch_bounds__(256) c64_init_kernel(
         if (i > j) v = 0.0;
         else if (sr[r] != ST_KEPT || sc[c] != ST_KEPT) v = i == j ? 1.0 : 0.0;
         else {
-            v = (double)Hs[(int64_t)i * P + j];
+            v = gram(i, j);
             if (i == j) v += lp ? lp[j] : (double)dsh[j];
         }
         Uf[(int64_t)i * P + j] = v;
@@ -234,12 +247,13 @@ __global__ void __launch_bounds__(64) c64_list_kernel(const uint8_t* __restrict_
 // solution vector in LDS.  NULLV = false: delta[fits[q]] = -U^-1 U^-T g[fits[q]] on the kept
 // coordinates of factor fsrc[q] (float32 out, 0 elsewhere).  NULLV = true: right-hand side q of
 // factor blockIdx.y is dependent pivot d = nulls[f][q]; N[f][q] = e_d - U_KK^-1 U[K][d].
-template <bool NULLV>
+template <bool NULLV, bool OUT64 = false>
 __global__ void __launch_bounds__(256) c64_solve_kernel(
     const double* __restrict__ U, int32_t P, const uint8_t* __restrict__ state,
     const int32_t* __restrict__ fits, const int32_t* __restrict__ fsrc,
     const double* __restrict__ g, float* __restrict__ delta, const int32_t* __restrict__ nulls,
-    const int32_t* __restrict__ counts, double* __restrict__ N) {
+    const int32_t* __restrict__ counts, double* __restrict__ N, double* __restrict__ x64 = nullptr,
+    const int32_t* __restrict__ gsrc = nullptr) {
     extern __shared__ double z[];
     __shared__ double part[4][kB];
     __shared__ double tail[kB];
@@ -264,7 +278,7 @@ __global__ void __launch_bounds__(256) c64_solve_kernel(
         cend = (bhi + 1) * kB;
         __syncthreads();
     } else {
-        const double* gf = g + (int64_t)fit * P;
+        const double* gf = g + (int64_t)(gsrc ? gsrc[blockIdx.x] : fit) * P;
         // forward: U^T z = g, block by block
         for (int b = 0; b < nb; ++b) {
             const int c = b * kB + l;
@@ -314,9 +328,68 @@ __global__ void __launch_bounds__(256) c64_solve_kernel(
     if (NULLV) {
         double* Nq = N + ((int64_t)f * P + blockIdx.x) * P;
         for (int i = tid; i < P; i += 256) Nq[i] = i == d ? 1.0 : (i < d ? -z[i] : 0.0);
+    } else if (OUT64) {
+        double* xf = x64 + (int64_t)fit * P;
+        for (int i = tid; i < P; i += 256) xf[i] += z[i];
     } else {
         float* df = delta + (int64_t)fit * P;
         for (int i = tid; i < P; i += 256) df[i] = (float)(-z[i]);
+    }
+}
+
+// r[fit] = c[csrc[q]] - (G[f] + diag(lamp[fit])) x[fit] for fit = fits[q], f = fsrc[q]: the
+// float64 Gram-space residual of a squared-loss fit.  G[f] is read from the f32 upper triangle
+// H[hsrc[f]] (exact integer counts of a 0/1 mask Gram), a mixed design's continuous rows and
+// columns (cmap[j] = c >= 0) from the float64 rows S[f][c][0 .. P).  Coordinates excluded
+// (dshift < 0) contribute nothing.  One workgroup per fit: pass A, a wave per row j, the
+// upper part sum_{i >= j} G[j][i] x[i] (coalesced row reads, wave reduction); pass B, a lane per
+// column i, the lower part sum_{j < i} G[j][i] x[j] (coalesced per j).  Deterministic.
+__device__ __forceinline__ double g_upper(const float* __restrict__ Hs, const double* __restrict__ Sf,
+                                          const int32_t* __restrict__ cm, int32_t P, int j, int i) {
+    if (Sf) {
+        const int cj = cm[j];
+        if (cj >= 0) return Sf[(int64_t)cj * P + i];
+        const int ci = cm[i];
+        if (ci >= 0) return Sf[(int64_t)ci * P + j];
+    }
+    return (double)Hs[(int64_t)j * P + i];
+}
+
+__global__ void __launch_bounds__(256) c64_resid_kernel(
+    const float* __restrict__ H, int32_t P, const int32_t* __restrict__ hsrc,
+    const double* __restrict__ S, int32_t k, const int32_t* __restrict__ cmap,
+    const int32_t* __restrict__ fits, const int32_t* __restrict__ fsrc,
+    const int32_t* __restrict__ csrc, const double* __restrict__ c,
+    const double* __restrict__ lamp, const float* __restrict__ dshift,
+    const double* __restrict__ x, double* __restrict__ r) {
+    extern __shared__ double sh[];
+    double* xs = sh;                 // [P] x with excluded coordinates zeroed
+    double* up = sh + P;             // [P] pass-A sums
+    int32_t* cm = reinterpret_cast<int32_t*>(sh + 2 * P);
+    const int q = blockIdx.x, fit = fits[q], f = fsrc[q];
+    const float* Hs = H + (int64_t)hsrc[f] * P * P;
+    const double* Sf = S ? S + (int64_t)f * k * P : nullptr;
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+    const float* dsh = dshift + (int64_t)fit * P;
+    for (int i = tid; i < P; i += 256) {
+        xs[i] = dsh[i] < 0.0f ? 0.0 : x[(int64_t)fit * P + i];
+        cm[i] = S ? cmap[i] : -1;
+    }
+    __syncthreads();
+    for (int j = w; j < P; j += 4) {
+        double acc = 0.0;
+        for (int i = j + l; i < P; i += 64) acc = fma(g_upper(Hs, Sf, cm, P, j, i), xs[i], acc);
+        acc = wave_sum_d(acc);
+        if (l == 0) up[j] = acc;
+    }
+    __syncthreads();
+    const double* lp = lamp + (int64_t)fit * P;
+    const double* cf = c + (int64_t)csrc[q] * P;
+    for (int i = tid; i < P; i += 256) {
+        double acc = up[i];
+        for (int j = 0; j < i; ++j) acc = fma(g_upper(Hs, Sf, cm, P, j, i), xs[j], acc);
+        acc = fma(lp[i], xs[i], acc);
+        r[(int64_t)fit * P + i] = dsh[i] < 0.0f ? 0.0 : cf[i] - acc;
     }
 }
 
@@ -421,9 +494,19 @@ extern "C" int sglm_chol64_factor(const float* H, int32_t P, const int32_t* hsrc
                                   int32_t nf, double tol, double* U, uint8_t* state,
                                   int32_t* nulls, int32_t* counts, void* work,
                                   sglm_stream_t stream) {
+    return sglm_chol64_factor_mixed(H, P, hsrc, dshift, lamp, dsrc, nf, tol, nullptr, 0, nullptr,
+                                    U, state, nulls, counts, work, stream);
+}
+
+extern "C" int sglm_chol64_factor_mixed(const float* H, int32_t P, const int32_t* hsrc,
+                                        const float* dshift, const double* lamp,
+                                        const int32_t* dsrc, int32_t nf, double tol,
+                                        const double* S, int32_t k, const int32_t* cmap,
+                                        double* U, uint8_t* state, int32_t* nulls,
+                                        int32_t* counts, void* work, sglm_stream_t stream) {
     if (nf <= 0) return SGLM_OK;
     if (!H || !hsrc || !dshift || !dsrc || !U || !state || !nulls || !counts || !work ||
-        P <= 0 || P % kB || P > kMaxP64 || !(tol >= 0.0)) {
+        P <= 0 || P % kB || P > kMaxP64 || !(tol >= 0.0) || (S && (k <= 0 || !cmap))) {
         set_error("sglm_chol64_factor: bad args (P=%d must be a multiple of %d, <= %d)", P, kB,
                   kMaxP64);
         return SGLM_EINVAL;
@@ -432,7 +515,7 @@ extern "C" int sglm_chol64_factor(const float* H, int32_t P, const int32_t* hsrc
     const int nb = P / kB;
     double* d0 = (double*)work;
     c64_init_kernel<<<dim3((unsigned)(nb * (nb + 1) / 2), (unsigned)nf), 256, 0, s>>>(
-        H, P, hsrc, dshift, lamp, dsrc, U, state, d0);
+        H, P, hsrc, dshift, lamp, dsrc, S, k, cmap, U, state, d0);
     for (int kb = 0; kb < nb; ++kb) {
         c64_diag_kernel<<<nf, kB, 0, s>>>(U, P, kb, state, d0, tol);
         const int m = nb - kb - 1;
@@ -458,6 +541,40 @@ extern "C" int sglm_chol64_solve(const double* U, int32_t P, const uint8_t* stat
     c64_solve_kernel<false><<<nq, 256, lds, as_stream(stream)>>>(
         U, P, state, fits, fsrc, g, delta, nullptr, nullptr, nullptr);
     return check_launch("sglm_chol64_solve");
+}
+
+extern "C" int sglm_chol64_solve_add(const double* U, int32_t P, const uint8_t* state,
+                                     const int32_t* fits, const int32_t* fsrc,
+                                     const int32_t* gsrc, int32_t nq, const double* g,
+                                     double* x, sglm_stream_t stream) {
+    if (nq <= 0) return SGLM_OK;
+    if (!U || !state || !fits || !fsrc || !g || !x || P <= 0 || P % kB || P > kMaxP64) {
+        set_error("sglm_chol64_solve_add: bad args (P=%d)", P);
+        return SGLM_EINVAL;
+    }
+    const size_t lds = (size_t)P * sizeof(double);
+    if (int st = allow_lds(c64_solve_kernel<false, true>, lds)) return st;
+    c64_solve_kernel<false, true><<<nq, 256, lds, as_stream(stream)>>>(
+        U, P, state, fits, fsrc, g, nullptr, nullptr, nullptr, nullptr, x, gsrc);
+    return check_launch("sglm_chol64_solve_add");
+}
+
+extern "C" int sglm_chol64_resid(const float* H, int32_t P, const int32_t* hsrc, const double* S,
+                                 int32_t k, const int32_t* cmap, const int32_t* fits,
+                                 const int32_t* fsrc, const int32_t* csrc, int32_t nq,
+                                 const double* c, const double* lamp, const float* dshift,
+                                 const double* x, double* r, sglm_stream_t stream) {
+    if (nq <= 0) return SGLM_OK;
+    if (!H || !hsrc || !fits || !fsrc || !csrc || !c || !lamp || !dshift || !x || !r ||
+        P <= 0 || P % kB || P > kMaxP64 || (S && (k <= 0 || !cmap))) {
+        set_error("sglm_chol64_resid: bad args (P=%d)", P);
+        return SGLM_EINVAL;
+    }
+    const size_t lds = (size_t)P * (2 * sizeof(double) + sizeof(int32_t));
+    if (int st = allow_lds(c64_resid_kernel, lds)) return st;
+    c64_resid_kernel<<<nq, 256, lds, as_stream(stream)>>>(H, P, hsrc, S, k, cmap, fits, fsrc, csrc,
+                                                         c, lamp, dshift, x, r);
+    return check_launch("sglm_chol64_resid");
 }
 
 extern "C" size_t sglm_chol64_minnorm_work_bytes(int32_t P, int32_t nf) {

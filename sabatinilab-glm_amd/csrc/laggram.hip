@@ -29,6 +29,8 @@ struct LagGramArgs {
     const int32_t* shifts;     // [K]
     int64_t nwords, row0, n, n_raw;
     int32_t m, K, layout, P, smin, smax;
+    int32_t pc;                // intercept column (m * K, or later when continuous columns
+                               // sit between the lag columns and it: they are written as 0)
 };
 
 __device__ __forceinline__ int lower_bound_i32(const int32_t* a, int lo, int hi, int64_t x) {
@@ -130,16 +132,16 @@ __global__ void __launch_bounds__(kLgT) lag_gram_fill_kernel(LagGramArgs A,
         while (t >= rowlen) { t -= rowlen; ++I; --rowlen; }
     }
     const int J = I + t;
-    const int p = A.m * A.K;
+    const int p = A.pc, pl = A.m * A.K;     // intercept column; lag columns 0 .. pl
     const int tid = threadIdx.x;
     const int jc = J * 128 + (tid & 127);
     int bj = 0, aj = 0;
-    if (jc < p) col_of(A, jc, bj, aj);
+    if (jc < pl) col_of(A, jc, bj, aj);
     // the intercept column's count for row ic: occurrences of ic's event in its window
     for (int r = 8 * blockIdx.y + (tid >> 7); r < 8 * blockIdx.y + 8; r += kLgT / 128) {
         const int ic = I * 128 + r;
         float cnt;
-        if (ic > p || jc > p) {
+        if (ic > p || jc > p || (ic >= pl && ic < p) || (jc >= pl && jc < p)) {
             cnt = 0.0f;
         } else if (ic == p && jc == p) {
             cnt = (float)A.n;
@@ -180,16 +182,26 @@ int sglm_lag_gram(const int32_t* occ, const int32_t* ev_off, const uint32_t* ebi
                   int32_t smin, int32_t smax, int64_t row0, int64_t n, int64_t n_raw, int32_t P,
                   const float* W, int64_t ldw, const int32_t* fits, int32_t nfits, float* H,
                   void* work, sglm_stream_t stream) {
+    return sglm_lag_gram_pc(occ, ev_off, ebits, nwords, shifts, m, K, layout, smin, smax, row0, n,
+                            n_raw, P, m * K, W, ldw, fits, nfits, H, work, stream);
+}
+
+int sglm_lag_gram_pc(const int32_t* occ, const int32_t* ev_off, const uint32_t* ebits,
+                     int64_t nwords, const int32_t* shifts, int32_t m, int32_t K, int32_t layout,
+                     int32_t smin, int32_t smax, int64_t row0, int64_t n, int64_t n_raw,
+                     int32_t P, int32_t pc, const float* W, int64_t ldw, const int32_t* fits,
+                     int32_t nfits, float* H, void* work, sglm_stream_t stream) {
     if (nfits <= 0) return SGLM_OK;
     const int64_t nb = 2 * ((int64_t)smax - smin) + 1;
     if (!occ || !ev_off || !ebits || !shifts || !W || !fits || !H || !work || m <= 0 || K <= 0 ||
-        smax < smin || nb > kLgMaxBins || P % 128 || (int64_t)m * K + 1 > P || n <= 0 ||
+        smax < smin || nb > kLgMaxBins || P % 128 || pc < m * K || pc + 1 > P || n <= 0 ||
         n_raw <= 0 || nwords * 32 < n_raw || (layout != 0 && layout != 1)) {
         set_error("sglm_lag_gram: bad args (m=%d K=%d P=%d span=%d)", m, K, P, smax - smin);
         return SGLM_EINVAL;
     }
     hipStream_t s = as_stream(stream);
-    LagGramArgs A{occ, ev_off, ebits, shifts, nwords, row0, n, n_raw, m, K, layout, P, smin, smax};
+    LagGramArgs A{occ, ev_off, ebits, shifts, nwords, row0, n, n_raw, m, K, layout, P, smin, smax,
+                  pc};
     int32_t* hist = reinterpret_cast<int32_t*>(work);
     int32_t* bnd = hist + (int64_t)m * m * nb;
     lag_corr_kernel<<<dim3((unsigned)m, (unsigned)m), kLgT, (size_t)nb * sizeof(int32_t), s>>>(

@@ -24,7 +24,7 @@ import scipy.stats
 
 from sglm_hip.estimators import (ElasticNet, Lasso, LinearRegression, LogisticRegression,  # noqa: F401
                                  NotYetImplementedError, PoissonRegressor, Ridge,
-                                 TweedieRegressor)
+                                 TweedieRegressor, host_matrix)
 
 
 class GLM():
@@ -127,8 +127,8 @@ class GLM():
             print(f'Fitting: {self.kwargs} — {id_fit}')
         # each of X / X_test is packed into HBM once for the fit, both scores and the
         # residuals (the reference re-reads them from host memory four times)
-        Xv = X.values if type(X) == pd.DataFrame else X
-        Xtv = X_test.values if type(X_test) == pd.DataFrame else X_test
+        Xv = host_matrix(X) if type(X) == pd.DataFrame else X
+        Xtv = host_matrix(X_test) if type(X_test) == pd.DataFrame else X_test
         self.model._resident = {}
         try:
             for a in (Xv, Xtv):
@@ -155,7 +155,7 @@ class GLM():
 
     def predict(self, X: Union[np.ndarray, pd.DataFrame]) -> np.ndarray:
         if type(X) == pd.DataFrame:
-            X = X.values
+            X = host_matrix(X)
         return self.model.predict(X)          # a lagged frame (sglm_hip.lagframe) stays resident
 
     def log_likelihood(self, prediction, truth) -> float:

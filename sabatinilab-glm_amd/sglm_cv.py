@@ -52,6 +52,9 @@ def _values(a):
     from sglm_hip.lagframe import LagFrame
     if isinstance(a, LagFrame):
         return a.design()                      # resident lagged frame: its device design
+    if hasattr(a, "values") and not isinstance(a, np.ndarray) and getattr(a, "ndim", 1) == 2:
+        from sglm_hip.estimators import host_matrix
+        return host_matrix(a)                  # nullable (convert_dtypes) frames per block
     return a.values if hasattr(a, "values") and not isinstance(a, np.ndarray) else a
 
 

@@ -16,6 +16,7 @@ import sglm_
 import sglm_cv
 import sglm_pp
 from sglm_hip import folds as _folds
+from sglm_hip.estimators import host_matrix as _host_matrix
 from sglm_hip.lagframe import LagFrame
 
 
@@ -71,7 +72,7 @@ def add_timeshifts_to_col_list(all_cols, shifted_cols, neg_order=0, pos_order=1)
 def fit_GLM(X, y, model_name='Gaussian', *args, **kwargs):
     """backend/sglm_ez.py:149-171."""
     glm = sglm_.GLM(model_name, *args, **kwargs)
-    glm.fit(X if isinstance(X, LagFrame) else X.values, y.values)
+    glm.fit(X if isinstance(X, LagFrame) else _host_matrix(X), y.values)
     return glm
 
 
@@ -134,9 +135,10 @@ def cv_idx_by_trial_id(X, y=None, trial_id_columns=[], num_folds=5, test_size=No
 
 def simple_cv_fit(X, y, cv_idx, glm_kwarg_lst, model_type='Normal', verbose=0, score_method='mse'):
     """backend/sglm_ez.py:347-389."""
-    Xv = X if isinstance(X, LagFrame) else (
-        X.values if hasattr(X, "values") and not isinstance(X, np.ndarray) else X)
+    Xv = X if isinstance(X, LagFrame) else _host_matrix(X)
     yv = y.values if hasattr(y, "values") and not isinstance(y, np.ndarray) else y
+    if getattr(yv, "dtype", None) is not None and not isinstance(yv.dtype, np.dtype):
+        yv = np.asarray(pd.Series(yv).to_numpy(dtype=np.float64, na_value=np.nan))
     cv_results = sglm_cv.cv_glm_mult_params(Xv, yv, cv_idx, model_type, glm_kwarg_lst,
                                             verbose=verbose, score_method=score_method)
     return (cv_results['best_score'], cv_results['best_score_std'], cv_results['best_params'],
@@ -211,8 +213,7 @@ def holdout_resplit_cv(X, y, id_df, glm_kwarg_lst, num_runs=3, id_cols=('nTrial'
     groups = [{"cv_idx": [(setup[tr], setup[te]) for tr, te in cv_idx],
                "objectives": objectives, "rolls": rolls, "refit_rows": setup,
                "holdout_rows": np.flatnonzero(hold)} for hold, setup, cv_idx in runs]
-    Xv = X.design() if isinstance(X, LagFrame) else (
-        X.values if hasattr(X, "values") and not isinstance(X, np.ndarray) else X)
+    Xv = X.design() if isinstance(X, LagFrame) else _host_matrix(X)
     yv = np.asarray(y.values if hasattr(y, "values") else y, dtype=np.float64).reshape(-1)
     res = _grid.run_multi(Xv, yv, groups, score_method=score_method)
     out = []

@@ -27,6 +27,8 @@ SIGNATURES = {
                                    _i32, _vp, _vp]),
     "sglm_pack_design_rows": (C.c_int, [_vp, _i32, _i64, _i32, _i64, _i64, _i32, _vp, _vp, _i64,
                                         _i32, _i64, _vp, _vp]),
+    "sglm_pack_design_rows_cf": (C.c_int, [_vp, _i32, _i64, _i32, _i64, _i64, _i32, _vp, _vp,
+                                           _i64, _i32, _i64, _vp, _vp, _vp]),
     "sglm_gemv_eta": (C.c_int, [_vp, _i32, _i64, _i32, _i64, _vp, _i32, _vp, _vp]),
     "sglm_link_update": (C.c_int, [_i32, _f32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
                                    _vp, _vp, _vp, _vp, _vp, _vp]),
@@ -78,7 +80,12 @@ SIGNATURES = {
     "sglm_chol64_work_bytes": (_sz, [_i32, _i32]),
     "sglm_chol64_factor": (C.c_int, [_vp, _i32, _vp, _vp, _vp, _vp, _i32, C.c_double, _vp, _vp,
                                      _vp, _vp, _vp, _vp]),
+    "sglm_chol64_factor_mixed": (C.c_int, [_vp, _i32, _vp, _vp, _vp, _vp, _i32, C.c_double, _vp,
+                                           _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "sglm_chol64_solve": (C.c_int, [_vp, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp]),
+    "sglm_chol64_solve_add": (C.c_int, [_vp, _i32, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp]),
+    "sglm_chol64_resid": (C.c_int, [_vp, _i32, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _i32, _vp,
+                                    _vp, _vp, _vp, _vp, _vp]),
     "sglm_chol64_minnorm_work_bytes": (_sz, [_i32, _i32]),
     "sglm_chol64_minnorm": (C.c_int, [_vp, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _vp,
                                       _vp, _vp]),
@@ -103,6 +110,17 @@ SIGNATURES = {
     "sglm_xtr_prefer": (C.c_int, [_i32]),
     "sglm_lag_gram": (C.c_int, [_vp, _vp, _vp, _i64, _vp, _i32, _i32, _i32, _i32, _i32, _i64,
                                 _i64, _i64, _i32, _vp, _i64, _vp, _i32, _vp, _vp, _vp]),
+    "sglm_lag_gram_pc": (C.c_int, [_vp, _vp, _vp, _i64, _vp, _i32, _i32, _i32, _i32, _i32, _i64,
+                                   _i64, _i64, _i32, _i32, _vp, _i64, _vp, _i32, _vp, _vp, _vp]),
+    "sglm_mixed_work_bytes": (_sz, [_i32, _i32, _i64]),
+    "sglm_mixed_wc": (C.c_int, [_vp, _i64, _vp, _i32, _vp, _i64, _i32, _i64, _i64, _vp, _vp]),
+    "sglm_mixed_gram": (C.c_int, [_i32, _vp, _i64, _vp, _i32, _vp, _i64, _i32, _i64, _vp, _i32,
+                                  _vp, _vp, _vp, _vp]),
+    "sglm_mixed_xtr": (C.c_int, [_i32, _vp, _i64, _i64, _vp, _vp, _i32, _vp, _i64, _i32, _i64,
+                                 _vp, _i32, _vp, _vp, _vp, _vp]),
+    "sglm_mixed_eta": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _i32, _vp, _i32, _vp, _i64,
+                                 _vp]),
+    "sglm_mixed_to_h": (C.c_int, [_vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     "sglm_lag_xtr": (C.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i64, _i64, _i32, _vp, _i64,
                                _vp, _i32, _vp, _vp, _vp]),
     "sglm_group_rows_work_bytes": (_sz, [_i64]),

@@ -110,23 +110,24 @@ class SharedGrams:
 
 # base-256 digits of the fixed-point m*y in the exact X^T(m y) of 0/1 designs (5 digits: the
 # quantisation step is 2^-38 of max|m y| per (response, mask), ~1e-13 of c)
-XTY_DIGITS = 5
+XTY_DIGITS = E.XTV_DIGITS
 
 
 def xty(prob: E.Problem, pairs: Sequence[tuple]) -> torch.Tensor:
     """c[(r, m)] = X^T (m * y_r) (float64 [len(pairs)][P]; c[p] = sum m y).
 
-    0/1 designs: m*y (float64) is put on a fixed-point grid of 2^-(38 - e) (|m y| < 2^e) and
-    split into XTY_DIGITS balanced base-256 digits; each digit plane is an integer vector with
-    |digit| <= 128, so the MFMA gradient kernel (sglm_xtr_bits, row slabs <= 65,536 rows) sums
-    it EXACTLY in f32 and float64, and c = sum_q 256^q X^T digit_q is float64-accurate -- the
-    reference's float64 ElasticNet sees X^T y to rounding (the f32-accumulated hi/lo passes
-    left ~1e-8 of |c|, which is 2e-5 of alpha rho at alpha = 1e-4, C5).  Other designs: y as
-    f32 high and low parts (two exact-product passes, f32 accumulation)."""
+    0/1 (and mixed) designs: m*y (float64) is put on a fixed-point grid of 2^-(38 - e)
+    (|m y| < 2^e) and split into XTY_DIGITS balanced base-256 digits; each digit plane is an
+    integer vector with |digit| <= 128, so the MFMA gradient kernel (sglm_xtr_bits, row slabs
+    <= 65,536 rows) sums it EXACTLY in f32 and float64, and c = sum_q 256^q X^T digit_q is
+    float64-accurate (engine.xtv_digits) -- the reference's float64 ElasticNet sees X^T y to
+    rounding (the f32-accumulated hi/lo passes left ~1e-8 of |c|, which is 2e-5 of alpha rho at
+    alpha = 1e-4, C5).  Other designs: y as f32 high and low parts (two exact-product passes,
+    f32 accumulation)."""
     d = prob.design
     out = torch.empty((len(pairs), d.P), dtype=torch.float64, device=d.device)
     if d.xbits is not None and E.XTR_BITS:
-        return _xty_digits(prob, pairs, out)
+        return E.xtv_digits(d, prob.M, prob.y64_rows(), pairs, out)
     ylo = prob.y_lo()
     tmp = None if ylo is None else torch.empty((min(256, len(pairs)), d.P), dtype=torch.float64,
                                                device=d.device)
@@ -139,73 +140,6 @@ def xty(prob: E.Problem, pairs: Sequence[tuple]) -> torch.Tensor:
             R = torch.stack([prob.M[m].to(torch.float32) * ylo[r] for r, m in pr])
             d.xtr(R, len(pr), tmp[:len(pr)])
             out[s:s + len(pr)] += tmp[:len(pr)]
-    return out
-
-
-def _xty_digits(prob: E.Problem, pairs: Sequence[tuple], out: torch.Tensor) -> torch.Tensor:
-    d = prob.design
-    n, ld, dev = d.n, d.ld, d.device
-    Y64 = prob.y64_rows()                                       # [R][n] float64
-    nd = XTY_DIGITS
-    top = 8 * nd - 2                                            # |m y| 2^sh < 2^top
-    if d.xtr_int_ok():
-        return _xty_digits_int(prob, pairs, out, Y64, nd, top)
-    chunk = max(1, 240 // nd)
-    D = torch.zeros((chunk * nd, ld), dtype=torch.float32, device=dev)
-    g = torch.empty((chunk * nd, d.P), dtype=torch.float64, device=dev)
-    w8 = torch.tensor([256.0 ** q for q in range(nd)], dtype=torch.float64, device=dev)
-    for s in range(0, len(pairs), chunk):
-        pr = pairs[s:s + chunk]
-        c = len(pr)
-        ri = torch.tensor([r for r, _ in pr], dtype=torch.int64, device=dev)
-        mi = torch.tensor([m for _, m in pr], dtype=torch.int64, device=dev)
-        Rv = prob.M[mi, :n].to(torch.float64) * Y64[ri]          # [c][n]
-        amax = Rv.abs().amax(1)
-        e = torch.where(amax > 0, torch.floor(torch.log2(amax.clamp_min(1e-300))) + 1,
-                        torch.zeros_like(amax))
-        sh = (top - e)                                          # per pair exponent
-        Ri = torch.round(Rv * torch.exp2(sh)[:, None]).to(torch.int64)
-        for q in range(nd):
-            dq = torch.remainder(Ri + 128, 256) - 128           # balanced digit in [-128, 127]
-            D[q * c:(q + 1) * c, :n] = dq.to(torch.float32)
-            Ri = torch.div(Ri - dq, 256, rounding_mode="floor")
-        d.xtr(D[: nd * c], nd * c, g[: nd * c])
-        gq = g[: nd * c].view(nd, c, d.P)
-        out[s:s + c] = (gq * w8[:, None, None]).sum(0) * torch.exp2(-sh)[:, None]
-    return out
-
-
-def _xty_digits_int(prob: E.Problem, pairs: Sequence[tuple], out: torch.Tensor, Y64, nd: int,
-                    top: int) -> torch.Tensor:
-    """The digit planes built by one HIP pass (sglm_digit_planes) and summed by the one-piece
-    integer gradient kernel (sglm_xtr_bits_int).  The scale of a pair comes from the bound
-    max(m) max|y| of its mask and response (|m y| < 2^e)."""
-    d = prob.design
-    n, ld, dev = d.n, d.ld, d.device
-    M = prob.M
-    mmax = M[:, :n].amax(1).to(torch.float64)                   # [F]
-    ymax = Y64.abs().amax(1)                                    # [R]
-    chunk = max(1, 384 // nd)                                   # <= 384 digit columns a call
-    ncol = (min(chunk, len(pairs)) * nd + 31) // 32 * 32
-    D = torch.zeros((ncol, ld), dtype=torch.bfloat16, device=dev)   # rows >= n stay zero
-    g = torch.empty((ncol, d.P), dtype=torch.float64, device=dev)
-    w8 = torch.tensor([256.0 ** q for q in range(nd)], dtype=torch.float64, device=dev)
-    for s in range(0, len(pairs), chunk):
-        pr = pairs[s:s + chunk]
-        c = len(pr)
-        rm = torch.tensor([[r for r, _ in pr], [m for _, m in pr]], dtype=torch.int32,
-                          device=dev)
-        ri, mi = rm[0].long(), rm[1].long()
-        bnd = mmax[mi] * ymax[ri]
-        e = torch.where(bnd > 0, torch.floor(torch.log2(bnd.clamp_min(1e-300))) + 1,
-                        torch.zeros_like(bnd))
-        sh = top - e
-        scale = torch.exp2(sh)
-        _lib.call("sglm_digit_planes", E._p(M), M.stride(0), E._p(Y64), Y64.stride(0), n,
-                  E._p(rm[0]), E._p(rm[1]), E._p(scale), c, nd, E._p(D), ld, E._stream())
-        d.xtr_int(D, nd * c, g)
-        gq = g[: nd * c].view(nd, c, d.P)
-        out[s:s + c] = (gq * w8[:, None, None]).sum(0) * torch.exp2(-sh)[:, None]
     return out
 
 

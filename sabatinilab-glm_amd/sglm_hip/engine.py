@@ -125,6 +125,22 @@ LAG_BITS = __import__("os").environ.get("SGLM_LAG_BITS", "1") == "1"
 # is judged at the f32 factor's former threshold.
 RANK_TOL_EXACT = float(__import__("os").environ.get("SGLM_RANK_TOL_EXACT", "1e-9"))
 RANK_TOL_F32 = float(__import__("os").environ.get("SGLM_RANK_TOL_F32", "1e-6"))
+# Mixed 0/1 + continuous designs: a design whose non-binary columns are few keeps its 0/1
+# columns as bit-planes (the bf16-MFMA Gram / gradient / predictor kernels) and holds the k
+# continuous ones as a float64 block (csrc/mixed.hip), when k <= MIXED_MAX_K and the float64
+# continuous Gram block (n * k(k+1)/2 products per Gram) stays within MIXED_BUDGET; otherwise
+# the whole design is stored f32.
+MIXED_MAX_K = int(__import__("os").environ.get("SGLM_MIXED_MAX_K", "256"))
+MIXED_BUDGET = float(__import__("os").environ.get("SGLM_MIXED_BUDGET", "1e9"))
+# R rows (fits x continuous columns) per weighted-Gram X^T (W C) launch of a mixed design
+MIXED_WC_ROWS = 256
+# base-256 digits of the fixed-point products in the exact X^T (m v) of 0/1 designs (xtv_digits)
+XTV_DIGITS = 5
+
+
+def mixed_ok(n: int, k: int) -> bool:
+    """A design with k non-binary columns of n rows is stored mixed (see MIXED_MAX_K)."""
+    return 0 < k <= MIXED_MAX_K and float(n) * k * (k + 1) / 2 <= MIXED_BUDGET
 
 
 def _gram_groups(form, uniq, dup):
@@ -202,6 +218,12 @@ class Design:
         self.rbits = None      # row-major bit-planes [P/64][ld] x uint2 (MFMA eta) when 0/1
         self._cbits = None     # identity-row compacted planes [n/64][P] x uint2 (MFMA X^T R)
         self.lag = None        # LagStructure of a time-shifted 0/1 event design (from_events)
+        # mixed designs: the k non-binary columns as float64 [k][ld] (zero rows >= n) at design
+        # positions cpos (their bit-plane columns are zero; csrc/mixed.hip completes every
+        # bit-plane product over them)
+        self.cont = None
+        self.cpos = None
+        self._mix = None
         self.slab = None       # (start, stop, n_total): rows [start, stop) of an n_total-row
         #                        design (one rank's share of a row-sharded solve, comm.py)
         self.device = device
@@ -221,6 +243,97 @@ class Design:
     @property
     def xtype(self):
         return X_F32 if self.xf is not None else X_BF16
+
+    @property
+    def k(self) -> int:
+        """Number of continuous (float64) columns of a mixed design (0 otherwise)."""
+        return 0 if self.cont is None else int(self.cont.shape[0])
+
+    def _set_cont(self, C, cpos):
+        """Make this a mixed design: C = device float64 (k, >= n) continuous columns at design
+        positions cpos (their bf16 / bit-plane columns must be zero)."""
+        cpos = np.asarray(cpos, dtype=np.int64).reshape(-1)
+        k = int(cpos.size)
+        if k == 0:
+            return
+        if C.shape[0] != k or C.shape[1] < self.n:
+            raise ValueError("continuous block shape does not match its positions")
+        if np.any(cpos < 0) or np.any(cpos >= self.p) or np.unique(cpos).size != k:
+            raise ValueError("continuous column positions out of range or repeated")
+        self.cont = torch.zeros((k, self.ld), dtype=torch.float64, device=self.device)
+        self.cont[:, :self.n] = C[:, :self.n]
+        self.cpos = cpos
+        cmap = np.full(self.P, -1, dtype=np.int32)
+        cmap[cpos] = np.arange(k, dtype=np.int32)
+        iu = np.triu_indices(k)
+        pg = np.concatenate([iu[0], iu[1]]).astype(np.int32)
+        px = np.concatenate([np.arange(k), np.full(k, k)]).astype(np.int32)
+        dev = self.device
+        self._mix = dict(cpos=torch.from_numpy(cpos.astype(np.int32)).to(dev),
+                         cmap=torch.from_numpy(cmap).to(dev),
+                         pg=torch.from_numpy(pg).to(dev), px=torch.from_numpy(px).to(dev))
+
+    def mix_eta(self, beta, out, slots=None, nb=None):
+        """out[slot] += C beta[slot][cpos] for the slots (all rows of beta when None)."""
+        if self.cont is None:
+            return
+        nb = (beta.shape[0] if slots is None else int(slots.numel())) if nb is None else nb
+        _lib.call("sglm_mixed_eta", _p(self.cont), self.ld, self.k, self.n, _p(self._mix["cpos"]),
+                  _p(beta), self.P, _p(slots), int(nb), _p(out), out.shape[1], _stream())
+
+    def mix_xtr(self, rmode, R, ldr, Bp, rsel, gslots, nq, g):
+        """g[gslot_q][cpos] = C R_q (float64): the continuous coordinates of X^T R."""
+        if self.cont is None or nq <= 0:
+            return
+        w = _work(_lib.query("sglm_mixed_work_bytes", int(nq), self.k, self.n), self.device,
+                  "mixed")
+        _lib.call("sglm_mixed_xtr", int(rmode), _p(R), int(ldr), int(Bp), _p(rsel), _p(gslots),
+                  int(nq), _p(self.cont), self.ld, self.k, self.n, _p(self._mix["cpos"]), self.P,
+                  _p(self._mix["px"]), _p(g), _p(w), _stream())
+
+    def mix_gram_rows(self, W=None, wslots=None, M=None, mrows=None, upl=None):
+        """float64 S [ns][k][P]: the Gram rows of the continuous columns, S[s][c][j] = sum_r
+        wt_s(r) C[c][r] X[r][j].  Weighted (IRLS): wt_s = W[wslots[s]] (f32), the 0/1 columns
+        from the bit-plane X^T (W C) kernel (f32-accurate products).  Exact (mask Grams): wt_s
+        = M[mrows[s]] (uint8 multiplicities), the 0/1 columns from the exact digit-plane X^T (m C)
+        (xtv_digits).  The continuous block itself in float64 (sglm_mixed_gram)."""
+        k, P, n, ld, dev = self.k, self.P, self.n, self.ld, self.device
+        exact = M is not None
+        rows = np.asarray(mrows if exact else wslots, dtype=np.int64).reshape(-1)
+        ns = int(rows.size)
+        S = torch.empty((ns, k, P), dtype=torch.float64, device=dev)
+        if ns == 0:
+            return S
+        rows_d = (upl(rows, np.int32) if upl is not None
+                  else torch.from_numpy(rows.astype(np.int32)).to(dev))
+        if exact:
+            pairs = [(c, int(m)) for m in rows for c in range(k)]
+            xtv_digits(self, M, self.cont, pairs, S.view(ns * k, P), mixed=False)
+        else:
+            per = max(1, MIXED_WC_ROWS // k)
+            for s0 in range(0, ns, per):
+                cnt = min(per, ns - s0)
+                R = _work(cnt * k * ld * 4, dev, "mixed_wc")[: cnt * k * ld * 4].view(
+                    torch.float32).view(cnt * k, ld)
+                _lib.call("sglm_mixed_wc", _p(W), W.shape[1], _p(rows_d[s0:]), cnt,
+                          _p(self.cont), ld, k, n, ld, _p(R), _stream())
+                self.xtr(R, cnt * k, S[s0:s0 + cnt].view(cnt * k, P), mixed=False)
+        w = _work(_lib.query("sglm_mixed_work_bytes", ns, k, n), dev, "mixed")
+        src = M if exact else W
+        _lib.call("sglm_mixed_gram", 1 if exact else 0, _p(src), src.shape[1], _p(rows_d), ns,
+                  _p(self.cont), ld, k, n, _p(self._mix["cpos"]), P, _p(self._mix["pg"]), _p(S),
+                  _p(w), _stream())
+        return S
+
+    def mix_to_h(self, S, slots, H, upl=None):
+        """H[slots[s]]: the continuous rows and columns (f32) from S."""
+        ns = int(S.shape[0])
+        if ns == 0:
+            return
+        sl = np.asarray(slots, dtype=np.int32).reshape(-1)
+        sl = upl(sl) if upl is not None else torch.from_numpy(sl).to(self.device)
+        _lib.call("sglm_mixed_to_h", _p(S), ns, self.k, self.P, _p(self._mix["cpos"]), _p(sl),
+                  _p(H), _stream())
 
     @property
     def xg(self):
@@ -252,10 +365,13 @@ class Design:
     def _pack_chunked(self, X: np.ndarray):
         """Upload a row-major host array in row chunks of <= UPLOAD_CHUNK_BYTES: each chunk is
         copied by HOST_THREADS threads into one of two pinned staging buffers (sglm_host_copy),
-        moved by an asynchronous copy, and packed into the design's rows (sglm_pack_design_rows)
-        -- no pageable multi-GB .to(device), and the host copy of chunk k + 1 overlaps the DMA
-        and pack of chunk k.  A design that is not bf16-exact is packed again with its f32 copy
-        (the first chunk's check catches it before the rest is uploaded once for nothing)."""
+        moved by an asynchronous copy, and packed into the design's rows (sglm_pack_design_rows_cf,
+        which also flags every column holding a value other than 0 / 1) -- no pageable multi-GB
+        .to(device), and the host copy of chunk k + 1 overlaps the DMA and pack of chunk k.
+        All-0/1: bit-planes.  A few non-binary columns (mixed_ok): those columns as a float64
+        block (gathered from the host array by native threads), the rest as bit-planes.  Else the
+        design is packed again with its f32 copy (the first chunk's flags catch a design with
+        many non-binary columns before the rest is uploaded once for nothing)."""
         n, p = X.shape
         dev, is64 = self.device, X.dtype == np.float64
         item = X.itemsize
@@ -266,13 +382,14 @@ class Design:
         dbuf = [_work(rows * p * item, dev, f"h2d{i}") for i in range(2)]
         evs = [None, None]
         flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        colflag = torch.zeros(max(p, 1), dtype=torch.int32, device=dev)
         n64 = pad_to(n, 64)
         if n64 < self.ld:
             self.xb[:, n64:].zero_()
         st = _stream()
 
-        def run(xf, first_only):
-            for k, r0 in enumerate(range(0, n, rows)):
+        def run(xf, r_from, r_to):
+            for k, r0 in enumerate(range(r_from, r_to, rows)):
                 c = min(rows, n - r0)
                 b = k % 2
                 if evs[b] is not None:
@@ -284,25 +401,58 @@ class Design:
                 ev = torch.cuda.Event()
                 ev.record()
                 evs[b] = ev
-                _lib.call("sglm_pack_design_rows", dst.data_ptr(), int(is64), c, p, p, 1, 1,
-                          _p(self.xb), _p(xf), self.ld, self.P, r0, _p(flag), st)
-                if first_only:
-                    return
+                _lib.call("sglm_pack_design_rows_cf", dst.data_ptr(), int(is64), c, p, p, 1, 1,
+                          _p(self.xb), _p(xf), self.ld, self.P, r0, _p(flag),
+                          None if xf is not None else _p(colflag), st)
         if n == 0:
             return
-        run(None, True)
-        if not int(flag.item()):
-            run(None, False)
-        if int(flag.item()):
+        first = min(rows, n)
+        run(None, 0, first)
+        k_first = int((colflag[:p] != 0).sum().item()) if p else 0
+        cont = None
+        if k_first <= MIXED_MAX_K:
+            run(None, first, n)
+            cf = colflag[:p].cpu().numpy()
+            cont = np.flatnonzero(cf)
+            if cont.size and not mixed_ok(n, int(cont.size)):
+                cont = None
+        if cont is None:
             self.xf = torch.empty((self.P, self.ld), dtype=torch.float32, device=dev)
             if n64 < self.ld:
                 self.xf[:, n64:].zero_()
-            run(self.xf, False)
+            run(self.xf, 0, n)
+            if bool(torch.isnan(self.xf).any()):
+                raise ValueError("Input X contains NaN.")       # sklearn check_array's error
         else:
+            if cont.size:
+                self._gather_cont(X, cont)
+                if bool(torch.isnan(self.cont).any()):
+                    raise ValueError("Input X contains NaN.")
+                self.xb[torch.from_numpy(cont).to(dev)] = 0        # their bit columns: zero
             self._pack_bits()
+            if self.xbits is None:
+                raise RuntimeError("mixed design: the 0/1 part did not pack as bit-planes")
         for ev in evs:
             if ev is not None:
                 ev.synchronize()                      # the staging buffers are reusable
+
+    def _gather_cont(self, X: np.ndarray, cont):
+        """The float64 block of a mixed design from a host row-major array: columns ``cont``
+        gathered by native threads into a pinned column-major stage, one asynchronous upload."""
+        n, p = X.shape
+        k = int(cont.size)
+        item = X.itemsize
+        stage = _pinned("cont", k * n, torch.float64 if item == 8 else torch.float32)
+        ptrs = (ctypes.c_void_p * k)(*[X.ctypes.data + int(c) * item for c in cont])
+        strides = np.full(k, p, dtype=np.int64)
+        _lib.call("sglm_host_gather_cols", ctypes.cast(ptrs, ctypes.c_void_p),
+                  strides.ctypes.data, k, n, item, stage.data_ptr(), HOST_THREADS)
+        C = torch.empty((k, n), dtype=stage.dtype, device=self.device)
+        C.view(-1).copy_(stage[: k * n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._set_cont(C.to(torch.float64), cont)
+        ev.synchronize()                      # the pinned stage is reused by the next design
 
     @classmethod
     def from_lagged(cls, Ecm, cols, shifts, r0: int, n: int, rows=None, device="cuda",
@@ -334,19 +484,34 @@ class Design:
         s_d = torch.from_numpy(shifts.astype(np.int32)).to(device)
         N = int(Ecm.shape[1])
         Eb = Ecm.to(torch.bfloat16).contiguous()
-        exact = bool(torch.equal(Eb.double(), Ecm))
+        binsrc = ((Ecm == 0) | (Ecm == 1)).all(dim=1).cpu().numpy()
 
-        def expand(src, out, elem):
+        def expand(src, out, elem, cd=c_d, sd=s_d, ncol=p):
             if rows is None:
-                _lib.call("sglm_timeshift_expand", _p(src), N, 1, N, _p(c_d), _p(s_d), p,
+                _lib.call("sglm_timeshift_expand", _p(src), N, 1, N, _p(cd), _p(sd), ncol,
                           _p(out), n, 1, d.ld, int(r0), elem, 0, _stream())
             else:
-                _lib.call("sglm_timeshift_gather", _p(src), N, 1, N, _p(c_d), _p(s_d), p,
+                _lib.call("sglm_timeshift_gather", _p(src), N, 1, N, _p(cd), _p(sd), ncol,
                           _p(out), n, 1, d.ld, _p(rows), elem, 0, _stream())
         expand(Eb, d.xb, 2)
         d.xb[p, :n] = 1.0
-        if exact:
+        # design columns lagged from a source with values other than 0 / 1
+        contc = np.flatnonzero(~binsrc[cols]) if p else np.zeros(0, np.int64)
+        if contc.size == 0:
             d._pack_bits()
+        elif mixed_ok(n, int(contc.size)):
+            # mixed: those columns as a float64 block lagged from the float64 sources, the rest
+            # as bit-planes
+            k = int(contc.size)
+            C = torch.zeros((k, d.ld), dtype=torch.float64, device=device)
+            cc = torch.from_numpy(cols[contc].astype(np.int32)).to(device)
+            sc = torch.from_numpy(shifts[contc].astype(np.int32)).to(device)
+            expand(Ecm.contiguous(), C, 8, cc, sc, k)
+            d.xb[torch.from_numpy(contc).to(device)] = 0
+            d._pack_bits()
+            if d.xbits is None:
+                raise RuntimeError("mixed design: the 0/1 part did not pack as bit-planes")
+            d._set_cont(C, contc)
         else:
             Ef = Ecm.to(torch.float32).contiguous()
             d.xf = torch.zeros((d.P, d.ld), dtype=torch.float32, device=device)
@@ -356,10 +521,22 @@ class Design:
 
     @classmethod
     def from_device(cls, Xt, device="cuda"):
-        """Pack a device torch tensor (n x p, f32/f64, any strides)."""
+        """Pack a device torch tensor (n x p, f32/f64, any strides); a few non-binary columns
+        make a mixed design (see MIXED_MAX_K)."""
         n, p = Xt.shape
         if Xt.dtype not in (torch.float32, torch.float64):
             Xt = Xt.to(torch.float64)
+        nonbin = np.flatnonzero((~((Xt == 0) | (Xt == 1)).all(dim=0)).cpu().numpy())
+        if nonbin.size and mixed_ok(n, int(nonbin.size)):
+            d = cls(n, p, device, zero=True)
+            Xb = Xt.clone()
+            nb_d = torch.from_numpy(nonbin).to(Xt.device)
+            Xb[:, nb_d] = 0
+            d._pack(Xb, is_f64=Xb.dtype == torch.float64, rs=Xb.stride(0), cs=Xb.stride(1))
+            if d.xbits is None:
+                raise RuntimeError("mixed design: the 0/1 part did not pack as bit-planes")
+            d._set_cont(Xt[:, nb_d].t().to(torch.float64), nonbin)
+            return d
         d = cls(n, p, device, zero=False)
         d._pack(Xt, is_f64=Xt.dtype == torch.float64, rs=Xt.stride(0), cs=Xt.stride(1))
         return d
@@ -393,7 +570,7 @@ class Design:
 
     @classmethod
     def from_events(cls, E, shifts: Sequence[int], row0: int, n: int, device="cuda",
-                    event_major=False, slab=None, nnz=None):
+                    event_major=False, slab=None, nnz=None, extra=None):
         """Expand base events E (N_raw x m) into lag columns directly on the device.
 
         Output column (shift block b, event a) = E[t + row0 - shifts[b], a] for rows
@@ -402,19 +579,29 @@ class Design:
         ``event_major`` (setup_model_fit.timeshift_vals_by_dict, lag order as given).
         Source rows outside E can only occur if row0/n exceed the valid window; they are
         filled with 0.  ``slab`` = (start, stop): only rows [start, stop) of the n-row design
-        (a rank's share of a row-sharded solve, comm.py).
+        (a rank's share of a row-sharded solve, comm.py).  ``extra``: float64 (k, n) continuous
+        columns (unshifted, one value per design row -- the production design's cumcount^2 /
+        5000 counters, pp_design_mat.py:167-172) placed after the lag columns: a mixed design.
         """
         require_gpu()
         info = None
         if slab is not None:
             info = _slab_info(slab, n)
             row0, n = row0 + info[0], info[1] - info[0]
+            if extra is not None:
+                extra = extra[:, info[0]:info[1]]
+        if extra is not None:
+            extra = torch.as_tensor(extra, dtype=torch.float64).to(device)
+            if extra.ndim != 2 or extra.shape[1] != n:
+                raise ValueError(f"extra columns must be (k, {n})")
         if isinstance(E, np.ndarray):
             E = torch.from_numpy(np.ascontiguousarray(E, dtype=np.float32))
         E = E.to(device=device, dtype=torch.float32)
         N_raw, m = E.shape
         K = len(shifts)
-        p = K * m
+        pl = K * m                                          # lag columns
+        kx = 0 if extra is None else int(extra.shape[0])
+        p = pl + kx
         Eb = E.t().contiguous().to(torch.bfloat16)          # feature-major bf16 (m, N_raw)
         if event_major:
             cols = np.repeat(np.arange(m), K)
@@ -426,7 +613,7 @@ class Design:
         sh_d = torch.tensor(sh, dtype=torch.int32, device=device)
 
         def fill(xb):
-            _lib.call("sglm_timeshift_expand", _p(Eb), N_raw, 1, N_raw, _p(cols_d), _p(sh_d), p,
+            _lib.call("sglm_timeshift_expand", _p(Eb), N_raw, 1, N_raw, _p(cols_d), _p(sh_d), pl,
                       _p(xb), n, 1, xb.shape[1], row0, 2, 0, _stream())
             xb[p, :n] = 1.0
 
@@ -440,9 +627,18 @@ class Design:
             _lib.call("sglm_event_bits", _p(Eb), N_raw, m, N_raw, _p(ebits), nwords, _stream())
             d.xbits = torch.empty((d.P, d.ld // 32), dtype=torch.int32, device=device)
             d.rbits = torch.empty((d.P // 64) * d.ld * 2, dtype=torch.int32, device=device)
-            _lib.call("sglm_lag_bits", _p(ebits), nwords, _p(cols_d), _p(sh_d), p, row0, n,
+            lb, lc, ls = ebits, cols_d, sh_d
+            if kx:
+                # the continuous columns' bit columns: zero (an all-zero event row, shift 0)
+                lb = torch.cat([ebits, torch.zeros((1, nwords), dtype=torch.int32,
+                                                   device=device)])
+                lc = torch.cat([cols_d, torch.full((kx,), m, dtype=torch.int32, device=device)])
+                ls = torch.cat([sh_d, torch.zeros(kx, dtype=torch.int32, device=device)])
+            _lib.call("sglm_lag_bits", _p(lb), nwords, _p(lc), _p(ls), p, row0, n,
                       d.ld, d.P, _p(d.xbits), _p(d.rbits), _stream())
             d.lag = LagStructure.build(E, shifts, row0, n, event_major, ebits=ebits, nnz=nnz)
+            if kx:
+                d._set_cont(extra, np.arange(pl, p))
             d.slab = info
             return d
         d = cls(n, p, device, zero=True)
@@ -453,11 +649,17 @@ class Design:
             if d.xbits is not None and bool(((E == 0) | (E == 1)).all()):
                 d.lag = LagStructure.build(E, shifts, row0, n, event_major)
         if not exact:
+            if kx:
+                raise NotImplementedError("extra continuous columns need 0/1 events")
             Ef = E.t().contiguous()
             d.xf = torch.zeros((d.P, d.ld), dtype=torch.float32, device=device)
             _lib.call("sglm_timeshift_expand", _p(Ef), N_raw, 1, N_raw, _p(cols_d), _p(sh_d),
                       p, _p(d.xf), n, 1, d.ld, row0, 4, 0, _stream())
             d.xf[p, :n] = 1.0
+        elif kx:
+            if d.xbits is None:
+                raise NotImplementedError("extra continuous columns need 0/1 events")
+            d._set_cont(extra, np.arange(pl, p))
         d.slab = info
         return d
 
@@ -475,8 +677,9 @@ class Design:
                           _p(self._cbits), _stream())
         return self._cbits
 
-    def xtr(self, R, B, g_out, work=None):
-        """g_out[k] (float64) = X^T R[k] for k < B (R: [B][ld] f32 device)."""
+    def xtr(self, R, B, g_out, work=None, mixed=True):
+        """g_out[k] (float64) = X^T R[k] for k < B (R: [B][ld] f32 device); ``mixed`` = False
+        leaves a mixed design's continuous coordinates as the bit-plane kernel wrote them (0)."""
         st = _stream()
         if self.xbits is not None and XTR_BITS:
             w = _work(_lib.query("sglm_xtr_bits_work_bytes", self.P, B, self.ld), self.device,
@@ -487,13 +690,15 @@ class Design:
             w = _work(_lib.query("sglm_xtr_work_bytes", self.P, B, self.n), self.device, "xtr")
             _lib.call("sglm_xtr", _p(self.xg), self.xtype, self.ld, self.P, self.n, _p(R), B,
                       _p(g_out), _p(w), st)
+        if mixed:
+            self.mix_xtr(0, R, R.shape[1], 0, None, None, B, g_out)
 
     def xtr_int_ok(self) -> bool:
         """sglm_xtr_bits_int applies: a 0/1 design with P % 512 == 0 and ld < 2^26."""
         return (self.xbits is not None and XTR_BITS and self.P % 512 == 0
                 and 64 * self.ld < (1 << 32))
 
-    def xtr_int(self, D, B, g_out):
+    def xtr_int(self, D, B, g_out, mixed=True):
         """g_out[k] (float64) = X^T D[k] for k < B, D: bf16 [ceil(B/32)*32][ld] device tensor of
         integers |d| <= 256 (exact: one bf16 piece, f32 sums of integers within 2^24)."""
         if not self.xtr_int_ok():
@@ -504,6 +709,8 @@ class Design:
                   "xtr")
         _lib.call("sglm_xtr_bits_int", _p(self.cbits_full()), self.ld, self.P, self.n, _p(D), B,
                   _p(g_out), _p(w), _stream())
+        if mixed:
+            self.mix_xtr(3, D, D.shape[1], 0, None, None, B, g_out)
 
     def eta(self, beta_dev, out=None, slots=None, direction=False):
         """eta[k] = X beta[k] for a (B, P) f32 device tensor; with ``slots`` (int32 device
@@ -518,10 +725,78 @@ class Design:
             work = _work(_lib.query("sglm_eta_bits_work_bytes", self.P, nb), self.device, "eta")
             _lib.call("sglm_gemv_eta_bits", _p(self.rbits), self.ld, self.P, _p(beta_dev), nb,
                       _p(slots), int(not direction), _p(out), _p(work), _stream())
+            # the continuous columns of a mixed design (after the kernel rounded a direction in
+            # place: the float64 sum uses the rounded values the step takes)
+            self.mix_eta(beta_dev, out, slots, nb)
         else:
+            if self.cont is not None:
+                raise RuntimeError("a mixed design needs the bit-plane predictor kernel")
             _lib.call("sglm_gemv_eta", _p(self.xg), self.xtype, self.ld, self.P, self.n,
                       _p(beta_dev), B, _p(out), _stream())
         return out
+
+
+def xtv_digits(d: Design, M, V64, pairs, out, mixed=True):
+    """out[q] = X^T (M[m_q] * V64[v_q]) in float64 for pairs q = (v_q, m_q) of a 0/1 (or mixed)
+    design: M = uint8 row masks [F][>= n], V64 = float64 rows [R][>= n] (device).  m*v is put on
+    a fixed-point grid of 2^-(38 - e) (|m v| < 2^e) and split into XTV_DIGITS balanced base-256
+    digits; each digit plane is an integer vector with |digit| <= 128, which the bit-plane
+    gradient kernel (row slabs <= 65,536 rows) sums EXACTLY in f32 and float64, so out is
+    float64-accurate (~1e-13 of |out|).  The X^T (m y) of the elastic-net path (enet.xty) and
+    the exact Gram rows of a mixed design's continuous columns (Design.mix_gram_rows)."""
+    n, ld, dev = d.n, d.ld, d.device
+    nd = XTV_DIGITS
+    top = 8 * nd - 2                                            # |m v| 2^sh < 2^top
+    w8 = torch.tensor([256.0 ** q for q in range(nd)], dtype=torch.float64, device=dev)
+    if d.xtr_int_ok():
+        # the digit planes built by one HIP pass (sglm_digit_planes) and summed by the one-piece
+        # integer gradient kernel (sglm_xtr_bits_int); the scale of a pair comes from the bound
+        # max(m) max|v| of its mask and vector (|m v| < 2^e)
+        mmax = M[:, :n].amax(1).to(torch.float64)               # [F]
+        vmax = V64[:, :n].abs().amax(1)                         # [R]
+        chunk = max(1, 384 // nd)                               # <= 384 digit columns a call
+        ncol = (min(chunk, len(pairs)) * nd + 31) // 32 * 32
+        D = torch.zeros((ncol, ld), dtype=torch.bfloat16, device=dev)   # rows >= n stay zero
+        g = torch.empty((ncol, d.P), dtype=torch.float64, device=dev)
+        for s in range(0, len(pairs), chunk):
+            pr = pairs[s:s + chunk]
+            c = len(pr)
+            rm = torch.tensor([[r for r, _ in pr], [m for _, m in pr]], dtype=torch.int32,
+                              device=dev)
+            ri, mi = rm[0].long(), rm[1].long()
+            bnd = mmax[mi] * vmax[ri]
+            e = torch.where(bnd > 0, torch.floor(torch.log2(bnd.clamp_min(1e-300))) + 1,
+                            torch.zeros_like(bnd))
+            sh = top - e
+            scale = torch.exp2(sh)
+            _lib.call("sglm_digit_planes", _p(M), M.stride(0), _p(V64), V64.stride(0), n,
+                      _p(rm[0]), _p(rm[1]), _p(scale), c, nd, _p(D), ld, _stream())
+            d.xtr_int(D, nd * c, g, mixed=mixed)
+            gq = g[: nd * c].view(nd, c, d.P)
+            out[s:s + c] = (gq * w8[:, None, None]).sum(0) * torch.exp2(-sh)[:, None]
+        return out
+    chunk = max(1, 240 // nd)
+    D = torch.zeros((chunk * nd, ld), dtype=torch.float32, device=dev)
+    g = torch.empty((chunk * nd, d.P), dtype=torch.float64, device=dev)
+    for s in range(0, len(pairs), chunk):
+        pr = pairs[s:s + chunk]
+        c = len(pr)
+        ri = torch.tensor([r for r, _ in pr], dtype=torch.int64, device=dev)
+        mi = torch.tensor([m for _, m in pr], dtype=torch.int64, device=dev)
+        Rv = M[mi, :n].to(torch.float64) * V64[ri, :n]         # [c][n]
+        amax = Rv.abs().amax(1)
+        e = torch.where(amax > 0, torch.floor(torch.log2(amax.clamp_min(1e-300))) + 1,
+                        torch.zeros_like(amax))
+        sh = (top - e)                                          # per pair exponent
+        Ri = torch.round(Rv * torch.exp2(sh)[:, None]).to(torch.int64)
+        for q in range(nd):
+            dq = torch.remainder(Ri + 128, 256) - 128           # balanced digit in [-128, 127]
+            D[q * c:(q + 1) * c, :n] = dq.to(torch.float32)
+            Ri = torch.div(Ri - dq, 256, rounding_mode="floor")
+        d.xtr(D[: nd * c], nd * c, g[: nd * c], mixed=mixed)
+        gq = g[: nd * c].view(nd, c, d.P)
+        out[s:s + c] = (gq * w8[:, None, None]).sum(0) * torch.exp2(-sh)[:, None]
+    return out
 
 
 def _canonical_lags(cols, shifts, m, event_major):
@@ -1227,6 +1502,9 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
     fam, power = reqs[0].family, float(reqs[0].power)
     if any(r.family != fam or float(r.power) != power for r in reqs):
         raise ValueError("irls(): one loss family per batch")
+    if (fam == FAM_SQUARED and GRAM_LS and d.xbits is not None
+            and max(prob.mask_count(int(r.mask)) for r in reqs) < 2 ** 24):
+        return _gram_ls(prob, reqs, stats, bufs, comm)
     B0, P, ld, n, p = len(reqs), d.P, d.ld, d.n, d.p
     dev = d.device
     bf = (bufs or _scratch().buf).get(B0, P, ld, dev)
@@ -1371,11 +1649,16 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
     fepoch = np.zeros(B0, dtype=np.int64)
 
     def sum_hess(idx):
-        """The slab Grams of a row-sharded solve summed over the ranks (one all-reduce each)."""
+        """The slab Grams of a row-sharded solve summed over the ranks (one all-reduce each;
+        a mixed design's float64 Gram rows of the continuous columns too)."""
         if comm is not None:
+            store = getattr(bf, "mixS", None) or {}
             for k in np.asarray(idx).reshape(-1):
                 comm.sum_(bf.H[int(k)])
+                if int(k) in store:
+                    comm.sum_(store[int(k)])
     bf.prob, bf.fit_mask, bf.fit_mask_d = prob, fmask_h, fit_mask
+    bf.mixS = {}
     # cross-mask families (slot of the representative per slot, -1: none / is one)
     xmask_tol = 0.0 if const_hess else HESS_XMASK_TOL / max(1.0, abs(2.0 - power))
     repl = np.full(B0, -1, dtype=np.int64)
@@ -1543,7 +1826,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
         return keep, newh, uniq, copies, ali, fail, exact
     # the gradient: from the event occurrences for a time-shifted event design (sglm_lag_xtr,
     # R in f32 by slot), else the bit-plane MFMA with R packed into its operand
-    use_lag = d.lag is not None and LAG_XTR
+    use_lag = d.lag is not None and LAG_XTR and d.cont is None
     use_rp = d.xbits is not None and XTR_BITS and not use_lag
     fused = use_rp or use_lag          # link fused with the previous step's predictor update
     if use_rp:
@@ -1603,6 +1886,8 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
                 finally:
                     if cochain:
                         _lib.call("sglm_xtr_prefer", -1)
+                # a mixed design's continuous coordinates, float64 from the same packed R
+                d.mix_xtr(2, rp_buf, ld, pad_to(na, 32), None, act_d, na, bf.g)
             else:
                 d.xtr(bf.R, B, bf.g)
             if comm is not None:
@@ -2068,12 +2353,133 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
         has = fkey >= 0
         out_info[has] = np.maximum(0 if const_hess else out_info[has], cnt[fkey[has]])
     bf.prob = bf.keep = bf.up = bf.fit_mask_d = None   # drop the compacted designs with the problem
+    bf.mixS = None
     res = []
     for k, r in enumerate(reqs0):
         res.append(FitResult(coef=out_beta[k, :p].copy(),
                              intercept=float(out_beta[k, p]) if r.fit_intercept else 0.0,
                              n_iter=int(out_iter[k]), converged=bool(out_conv[k]),
                              dropped=int(out_info[k])))
+    return res, bf.eta
+
+
+# squared-loss fits of a 0/1 (or mixed) design in Gram space: the exact mask Gram (integer
+# counts in f32, a mixed design's continuous rows in float64), the exact X^T (m y) (digit
+# planes), a float64 factor per (mask, penalty, intercept), the solve and GRAM_LS_REFINE float64
+# refinements -- no pass over the rows per iteration, and no f32 residual in the fixed point
+GRAM_LS = __import__("os").environ.get("SGLM_GRAM_LS", "1") == "1"
+GRAM_LS_REFINE = int(__import__("os").environ.get("SGLM_GRAM_LS_REFINE", "2"))
+
+
+def _gram_ls(prob: Problem, reqs: List[FitReq], stats: Optional[IrlsStats], bufs, comm):
+    """Squared-loss (OLS / Ridge) fits of a 0/1 or mixed design: x = (G + lam I')^-1 X^T (m y)
+    in float64 -- the normal equations sklearn's Ridge(solver='cholesky') solves
+    (_ridge.py:201-213) and, with the minimum-norm projection of unpenalised fits on their exact
+    rank decisions, lstsq's LinearRegression answer (_base.py:701; backend/sglm.py:96-105).
+    G = the mask's exact Gram (sglm_syrk_cbits at the mask multiplicities: integer counts, exact
+    in f32 below 2^24; a mixed design's continuous rows in float64), X^T (m y) exact to float64
+    rounding (xtv_digits); the solve on the float64 factor (sglm_chol64_factor_mixed) plus
+    GRAM_LS_REFINE float64 refinements r = c - (G + lam I') x (sglm_chol64_resid).  Returns
+    (results, final eta [B][ld]) like irls()."""
+    d = prob.design
+    B0, P, ld, n, p = len(reqs), d.P, d.ld, d.n, d.p
+    dev = d.device
+    bf = (bufs or _scratch().buf).get(B0, P, ld, dev)
+    st = _stream()
+    up = _Uploads(dev)
+    fmask_h = np.array([r.mask for r in reqs], dtype=np.int32)
+    lam = np.array([float(r.lam) for r in reqs])
+    fi = np.array([1.0 if r.fit_intercept else 0.0 for r in reqs])
+    bf.prob, bf.fit_mask, bf.up, bf.fit_mask_d = prob, fmask_h, up, None
+    bf.mixS = {}
+    scal = up(np.concatenate([lam, fi]), np.float64)
+    lam_d, fi_d = scal[:B0], scal[B0:]
+    # coordinate shifts: lam on the predictors, 0 on a fitted intercept, -1 excluded (an
+    # unfitted intercept, the padding)
+    bf.dshift.fill_(-1.0)
+    bf.dshift[:B0, :p] = lam_d[:, None]
+    bf.dshift[:B0, p] = fi_d - 1.0
+    lamp_d = torch.zeros((B0, P), dtype=torch.float64, device=dev)
+    lamp_d[:, :p] = lam_d[:, None]
+    # one exact Gram per distinct mask (weights = the mask's multiplicities)
+    mrep = {}
+    for k, r in enumerate(reqs):
+        mrep.setdefault(int(r.mask), k)
+    rep = np.array(sorted(mrep.values()), dtype=np.int32)
+    bf.W[up(rep, np.int64)] = prob.M[up(fmask_h[rep], np.int64)].float()
+    gram_rows = np.array([float(prob.mask_nnz(int(r.mask))) if comm is not None
+                          else prob.mask_count(int(r.mask)) for r in reqs])
+    nsteps = (n + 31) // 32
+    ntile1 = (P // 256) * (P // 256 + 1) // 2
+    _syrk(d, bf, rep, nsteps, ntile1, stats, st, exact=True, rows=gram_rows)
+    if comm is not None:
+        for k in rep:
+            comm.sum_(bf.H[int(k)])
+            if int(k) in bf.mixS:
+                comm.sum_(bf.mixS[int(k)])
+    # X^T (m y) of every distinct (response, mask), exact to float64 rounding
+    pairs = sorted(set((int(r.resp), int(r.mask)) for r in reqs))
+    pidx = {pr: i for i, pr in enumerate(pairs)}
+    c = torch.empty((len(pairs), P), dtype=torch.float64, device=dev)
+    xtv_digits(d, prob.M, prob.y64_rows(), pairs, c)
+    if comm is not None:
+        comm.sum_(c)
+    cidx = np.array([pidx[(int(r.resp), int(r.mask))] for r in reqs], dtype=np.int32)
+    # one float64 factor per (mask, penalty, intercept); the unpenalised fits' factors first
+    lam0 = lam == 0.0
+    keys, k_h, k_d = {}, [], []
+    fkey = np.full(B0, -1, dtype=np.int64)
+    for k in np.argsort(~lam0, kind="stable"):
+        r = reqs[k]
+        key = (int(r.mask), float(r.lam), bool(r.fit_intercept))
+        if key not in keys:
+            keys[key] = len(k_h)
+            k_h.append(mrep[int(r.mask)])
+            k_d.append(int(k))
+        fkey[k] = keys[key]
+    f64 = _Factor64(d, bf, np.asarray(k_h), np.asarray(k_d), lamp_d, st)
+    ints = up(np.concatenate([np.arange(B0), fkey, cidx, np.asarray(k_h)]).astype(np.int32))
+    fits_d, fsrc_d, csrc_d = ints[:B0], ints[B0:2 * B0], ints[2 * B0:3 * B0]
+    hsrc_d = ints[3 * B0:]
+    x = torch.zeros((B0, P), dtype=torch.float64, device=dev)
+    _lib.call("sglm_chol64_solve_add", _p(f64.U), P, _p(f64.state), _p(fits_d), _p(fsrc_d),
+              _p(csrc_d), B0, _p(c), _p(x), st)
+    res_d = torch.empty_like(x)
+    S, k_c, cmap = f64._S, (d.k if f64._S is not None else 0), (
+        d._mix["cmap"] if f64._S is not None else None)
+    for _ in range(GRAM_LS_REFINE):
+        _lib.call("sglm_chol64_resid", _p(bf.H), P, _p(hsrc_d), _p(S), k_c, _p(cmap),
+                  _p(fits_d), _p(fsrc_d), _p(csrc_d), B0, _p(c), _p(lamp_d), _p(bf.dshift),
+                  _p(x), _p(res_d), st)
+        _lib.call("sglm_chol64_solve_add", _p(f64.U), P, _p(f64.state), _p(fits_d),
+                  _p(fsrc_d), None, B0, _p(res_d), _p(x), st)
+    # unpenalised fits: the minimum-norm point of the solution set (lstsq)
+    pf = np.flatnonzero(lam0)
+    f64.minnorm(d, bf, pf, fkey[pf], x, st)
+    bf.beta[:B0].copy_(x)
+    d.eta(bf.beta, bf.eta)
+    outs = torch.cat([x.reshape(-1), f64.counts[:, 1].to(torch.float64)]).cpu().numpy()
+    if stats is not None:
+        stats.newton_iters += 1
+        stats.fit_iters += B0
+        stats.gram_fits += int(rep.size)
+        stats.gram_fit_iters += int(rep.size)
+        stats.rank_grams += int(rep.size)
+        stats.roundtrips += 1
+        stats.stops["tol"] += B0
+        pa = float(p + 1)
+        nr = np.array([prob.mask_count(int(reqs[k].mask)) for k in rep])
+        stats.alg_flop += float(np.sum(nr * pa * (pa + 1)) + len(k_h) * pa ** 3 / 3
+                                + B0 * (1 + GRAM_LS_REFINE) * 4 * pa * pa)
+    xb = outs[: B0 * P].reshape(B0, P)
+    cnt = outs[B0 * P:].astype(np.int64)
+    bf.prob = bf.up = bf.mixS = None
+    res = []
+    for k, r in enumerate(reqs):
+        res.append(FitResult(coef=xb[k, :p].copy(),
+                             intercept=float(xb[k, p]) if r.fit_intercept else 0.0,
+                             n_iter=1 + GRAM_LS_REFINE, converged=True,
+                             dropped=int(cnt[fkey[k]])))
     return res, bf.eta
 
 
@@ -2295,9 +2701,23 @@ def _lag_gram(d: Design, bf, fits: np.ndarray, st):
     upl = getattr(bf, "up", None)
     fits = np.ascontiguousarray(fits, dtype=np.int32)
     fits_d = upl(fits, np.int32) if upl is not None else torch.from_numpy(fits).to(d.device)
-    _lib.call("sglm_lag_gram", _p(lg.occ), _p(lg.ev_off), _p(lg.ebits), lg.nwords,
+    _lib.call("sglm_lag_gram_pc", _p(lg.occ), _p(lg.ev_off), _p(lg.ebits), lg.nwords,
               _p(lg.shifts), lg.m, lg.K, lg.layout, lg.smin, lg.smax, lg.row0, lg.n, lg.n_raw,
-              d.P, _p(bf.W), d.ld, _p(fits_d), int(fits.size), _p(bf.H), _p(work), st)
+              d.P, d.p, _p(bf.W), d.ld, _p(fits_d), int(fits.size), _p(bf.H), _p(work), st)
+    if d.cont is not None:
+        _mix_hess(d, bf, fits, False)
+
+
+def _max_gram_count(bf, slots) -> float:
+    """Largest multiplicity sum over the masks of the given slots (an upper bound on every entry
+    of their exact 0/1 mask Grams); inf when the problem is unknown."""
+    prob = getattr(bf, "prob", None)
+    fm = getattr(bf, "fit_mask", None)
+    if prob is None or fm is None:
+        return float("inf")
+    fm = np.asarray(fm)
+    return max((prob.mask_count(int(fm[int(h)])) for h in np.asarray(slots).reshape(-1)),
+               default=0.0)
 
 
 class _Factor64:
@@ -2316,10 +2736,23 @@ class _Factor64:
         idx = np.concatenate([np.asarray(hsrc), np.asarray(dsrc)]).astype(np.int32)
         idx_d = upl(idx, np.int32) if upl is not None else torch.from_numpy(idx).to(dev)
         work = _work(_lib.query("sglm_chol64_work_bytes", P, nf), dev, "chol64")
-        tol = RANK_TOL_EXACT if d.xbits is not None else RANK_TOL_F32
-        _lib.call("sglm_chol64_factor", _p(bf.H), P, _p(idx_d[:nf]), _p(bf.dshift), _p(lamp_d),
-                  _p(idx_d[nf:]), nf, tol, _p(self.U), _p(self.state), _p(self.nulls),
-                  _p(self.counts), _p(work), st)
+        # the f32 Gram of a 0/1 design holds exact integer counts while every entry (at most the
+        # mask's multiplicity sum) stays below 2^24; past that f32 rounding enters the Schur
+        # complements and the float32-level threshold applies
+        tol = RANK_TOL_EXACT if (d.xbits is not None and _max_gram_count(bf, hsrc) < 2 ** 24) \
+            else RANK_TOL_F32
+        S = None
+        if d.cont is not None:
+            store = getattr(bf, "mixS", None) or {}
+            missing = [int(h) for h in hsrc if int(h) not in store]
+            if missing:
+                raise RuntimeError(f"mixed design: no float64 Gram rows for slots {missing}")
+            S = torch.stack([store[int(h)] for h in hsrc]).contiguous()
+        _lib.call("sglm_chol64_factor_mixed", _p(bf.H), P, _p(idx_d[:nf]), _p(bf.dshift),
+                  _p(lamp_d), _p(idx_d[nf:]), nf, tol, _p(S), d.k if S is not None else 0,
+                  _p(d._mix["cmap"]) if S is not None else None, _p(self.U), _p(self.state),
+                  _p(self.nulls), _p(self.counts), _p(work), st)
+        self._S = S                     # alive until the factorisation has run
 
     def minnorm(self, d: Design, bf, fits, fsrc, beta64_d, st):
         """beta[fits[q]] <- the minimum-norm point of its solution set on factor fsrc[q] (the
@@ -2383,6 +2816,28 @@ def _syrk(d: Design, bf, fits: np.ndarray, nsteps: int, ntile1: int, stats, st, 
         pa = d.p + 1
         nrows = float(np.sum(rows[fits])) if rows is not None else float(d.n) * nact
         stats.syrk_events.append((ev[0], ev[1], nact, nrows * pa * (pa + 1)))  # algorithmic flop
+    if d.cont is not None:
+        _mix_hess(d, bf, fits, exact)
+
+
+def _mix_hess(d: Design, bf, fits, exact: bool):
+    """The continuous rows / columns of the Hessians H[fits] of a mixed design (float64 Gram
+    rows S, scattered into the f32 Hessians; S kept per slot in bf.mixS for the float64 factors
+    of the exact Grams).  exact: the fits' weights are their masks' multiplicities."""
+    fits = np.asarray(fits, dtype=np.int64).reshape(-1)
+    if fits.size == 0:
+        return
+    upl = getattr(bf, "up", None)
+    if exact and getattr(bf, "prob", None) is not None:
+        S = d.mix_gram_rows(M=bf.prob.M, mrows=np.asarray(bf.fit_mask)[fits], upl=upl)
+    else:
+        S = d.mix_gram_rows(W=bf.W, wslots=fits, upl=upl)
+    d.mix_to_h(S, fits, bf.H, upl=upl)
+    store = getattr(bf, "mixS", None)
+    if store is None:
+        store = bf.mixS = {}
+    for q, k in enumerate(fits):
+        store[int(k)] = S[q]
 
 
 def _syrk_cbits(d: Design, bf, prob: Problem, fits: np.ndarray, st, ev=None):

@@ -55,15 +55,33 @@ def _check_y_range(power: float, y: np.ndarray):
         raise ValueError(f"Some value(s) of y are out of the valid range of the loss {name!r}.")
 
 
+def host_matrix(X):
+    """Host numeric values of a design given as a DataFrame / array-like.  A frame of numpy
+    numeric columns converts as ``.values`` does; a frame with pandas nullable columns (what
+    ``df.convert_dtypes()`` makes: Int64 / Float64 / boolean -- the production driver converts its
+    frame before fitting, sglm_cb_concat_make_design_mat.py:244) converts per column block to
+    float64 with pd.NA as NaN, where ``.values`` would build an object array that sklearn
+    converts element by element; an object array converts to float64."""
+    import pandas as pd
+    if isinstance(X, pd.DataFrame):
+        if all(isinstance(dt, np.dtype) and dt.kind in "fiub" for dt in X.dtypes):
+            return X.values
+        return X.to_numpy(dtype=np.float64, na_value=np.nan)
+    if hasattr(X, "values") and not isinstance(X, np.ndarray):
+        X = X.values
+    X = np.asarray(X)
+    if X.dtype == object:
+        X = np.where(pd.isna(X), np.nan, X).astype(np.float64)
+    return X
+
+
 def _as2d(X):
     from .lagframe import LagFrame
     if isinstance(X, LagFrame):             # device-resident lagged frame: no host values
         if len(X.shape) != 2:
             raise ValueError("Expected 2D array")
         return X
-    if hasattr(X, "values") and not isinstance(X, np.ndarray):
-        X = X.values
-    X = np.asarray(X)
+    X = host_matrix(X)
     if X.ndim == 1:
         raise ValueError("Expected 2D array, got 1D array instead")
     return X

@@ -35,12 +35,33 @@ from . import _lib
 NAN = float("nan")
 
 
+class _Snapshot:
+    """The columns, index and row count of a DataFrame as they were when a lagged frame was
+    made from it (the reference's timeshift_multiple returns a copy, sglm_pp.py:436-486).  Each
+    column's Series is taken at construction -- a view, no copy -- so a later column assignment
+    (``X['A'] = ...``), column insertion / deletion or row-dropping change of the caller's frame
+    (``X.dropna(inplace=True)``) leaves these arrays, and their length, as they were; only
+    element writes into the same array (``X.loc[r, 'A'] = v``) would show through."""
+
+    def __init__(self, X: pd.DataFrame):
+        self.index = X.index
+        self.columns = X.columns
+        self._cols = {c: X[c] for c in X.columns}
+        self._n = len(X)
+
+    def __getitem__(self, name):
+        return self._cols[name]
+
+    def __len__(self):
+        return self._n
+
+
 class LagSource:
-    """The frame a lagged frame was made from (host, never modified) and the device float64
-    copies of the columns the lag columns read (uploaded once, on first use)."""
+    """The frame a lagged frame was made from (a _Snapshot of its columns) and the device
+    float64 copies of the columns the lag columns read (uploaded once, on first use)."""
 
     def __init__(self, base: pd.DataFrame):
-        self.base = base
+        self.base = _Snapshot(base)
         self.N = len(base)
         self._dev = {}           # column name -> row of self._E
         self._E = None
@@ -142,11 +163,16 @@ class LagSource:
         col = self.base[name]
         if isinstance(col.dtype, np.dtype):
             v = col.to_numpy()
-            if v.dtype == np.float64 and v.ndim == 1 and v.strides[0] % 8 == 0 \
-                    and v.strides[0] > 0:
-                return v
-            return np.ascontiguousarray(v.astype(np.float64))
-        return np.ascontiguousarray(col.to_numpy(dtype=np.float64, na_value=NAN))
+            if not (v.dtype == np.float64 and v.ndim == 1 and v.strides[0] % 8 == 0
+                    and v.strides[0] > 0):
+                v = np.ascontiguousarray(v.astype(np.float64))
+        else:
+            v = np.ascontiguousarray(col.to_numpy(dtype=np.float64, na_value=NAN))
+        # the native packers read N elements from this pointer
+        if v.ndim != 1 or v.shape[0] != self.N:
+            raise ValueError(f"lagged frame source column {name!r} has {v.shape} values, "
+                             f"expected {self.N}")
+        return v
 
     def numeric(self, name) -> bool:
         if name not in self._numeric:

@@ -238,3 +238,28 @@ def designmat_session(n_trials: int, seed: int, *, lead=7, no_cue=0.03, timeout=
     trials = pd.DataFrame({"nTrial": np.arange(1, T + 1)[:keep], "tSelection": tsel[:keep],
                            "Reward": reward[:keep], "h2": h2[:keep]})
     return timeseries, trials
+
+
+def prod_counters(trial: np.ndarray, seed: int = 0) -> np.ndarray:
+    """The two unshifted continuous counters of the production design (pp_design_mat.py:167-172,
+    sglm_cb_concat_make_design_mat.py:224, 310) over design rows with trial ids ``trial`` (rows of
+    a trial contiguous): per trial a cue row and an ENL run (20-60 rows) from the trial's second
+    row -- time_from_enl_onset = cumcount over the cue + ENL rows, squared / (50*100) -- and with
+    probability 0.4 an ENLP run (8-20 rows) right after it -- time_from_enlp_onset likewise;
+    0 elsewhere.  Returns float64 (2, N)."""
+    rng = np.random.default_rng(seed)
+    trial = np.asarray(trial)
+    N = trial.size
+    start = np.r_[0, np.flatnonzero(np.diff(trial) != 0) + 1]
+    lens = np.diff(np.r_[start, N])
+    T = start.size
+    le = rng.integers(20, 61, T)
+    lp = np.where(rng.random(T) < 0.4, rng.integers(8, 21, T), 0)
+    pos = np.arange(N) - np.repeat(start, lens)                  # row within its trial
+    ti = np.repeat(np.arange(T), lens)
+    enl = pos <= le[ti]                                          # cue row 0 + ENL rows 1..le
+    enlp = (pos > le[ti]) & (pos <= le[ti] + lp[ti])
+    out = np.zeros((2, N))
+    out[0] = np.where(enl, pos.astype(np.float64) ** 2 / 5000.0, 0.0)
+    out[1] = np.where(enlp, (pos - le[ti] - 1).astype(np.float64) ** 2 / 5000.0, 0.0)
+    return out

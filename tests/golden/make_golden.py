@@ -12,6 +12,7 @@ Sources — never the reference code itself (its import/execution was denied, SU
 Usage: ``python tests/golden/make_golden.py`` -> tests/golden/*.npz / *.json
        ``python tests/golden/make_golden.py api`` -> tests/golden/api.npz only
        ``python tests/golden/make_golden.py rank`` -> tests/golden/rank.npz only
+       ``python tests/golden/make_golden.py mixed`` -> tests/golden/mixed.npz only
 """
 from __future__ import annotations
 
@@ -174,6 +175,94 @@ def rank_cases():
     return out
 
 
+def _prod_columns(N, seed):
+    """A production-like design in the layout of sglm_cb_concat_make_design_mat.py (:224-244,
+    :266, :310): 0/1 event lags (8 events x shifts 0, -5..-1, 1..4, shift-major), the two
+    unshifted counters of pp_design_mat.py:167-172 -- (ENL | Cue) rows' cumcount within the
+    trial, squared / (50*100), and the state_ENLP rows' cumcount within (trial, nENL), squared /
+    (50*100), 0 elsewhere -- and one 0/1 dummy per session (pd.get_dummies(session)).  Returns
+    (X, continuous column positions, trial ids)."""
+    rng = np.random.default_rng(seed)
+    lens = []
+    while sum(lens) < N:
+        lens.append(int(rng.integers(80, 160)))
+    nTrial = np.repeat(np.arange(1, len(lens) + 1), lens)[:N]
+    Cue, ENL, ENLP, nENL = (np.zeros(N) for _ in range(4))
+    t0 = 0
+    for ln in lens:
+        if t0 >= N:
+            break
+        Cue[t0] = 1
+        le = int(rng.integers(20, 60))
+        ENL[t0 + 1:min(N, t0 + 1 + le)] = 1
+        s0 = t0 + 1 + le
+        for q in range(int(rng.integers(0, 3))):       # 0-2 penalty periods (nENL = 1, 2)
+            lp = int(rng.integers(8, 20))
+            ENLP[s0:min(N, s0 + lp, t0 + ln)] = 1
+            nENL[s0:min(N, s0 + lp, t0 + ln)] = q + 1
+            s0 += lp + int(rng.integers(2, 6))
+        t0 += ln
+    df = pd.DataFrame({"nTrial": nTrial, "Cue": Cue, "ENL": ENL, "ENLP": ENLP, "nENL": nENL})
+    sel = (df.ENL == 1) | (df.Cue == 1)
+    t_enl = np.zeros(N)
+    t_enl[sel.values] = df.loc[sel].groupby("nTrial").cumcount().values ** 2 / (50 * 100)
+    selp = df.ENLP == 1
+    t_enlp = np.zeros(N)
+    t_enlp[selp.values] = (df.loc[selp].groupby(["nTrial", "nENL"]).cumcount().values ** 2
+                           / (50 * 100))
+    L = 5
+    E = (rng.random((N + 2 * L, 8)) < 0.04).astype(np.float32)
+    Xl = _lag_X(E, L, N)
+    ntr = int(nTrial.max())
+    session = np.minimum((nTrial - 1) * 3 // ntr, 2)
+    S = np.stack([(session == j).astype(float) for j in range(3)], 1)
+    X = np.hstack([Xl, t_enl[:, None], t_enlp[:, None], S])
+    cpos = np.array([Xl.shape[1], Xl.shape[1] + 1])
+    return X, cpos, nTrial
+
+
+def mixed_cases():
+    """Round-5 pins of the production design (mixed 0/1 + continuous, fit_intercept=False,
+    alpha = 0; sglm_cb_concat_make_design_mat.py:211-216, 356-363 -> LinearRegression, lstsq in
+    float64, sklearn _base.py:701):
+    * mx: LinearRegression(fit_intercept=False) on the design of _prod_columns (12,000 x 85);
+    * mxfi: LinearRegression() (intercept) on it minus the last session dummy;
+    * mxill: the second counter replaced by the first times (1 + 1e-4 w), w = +-1 per row (a
+      near-collinear pair: cond(X^T X) ~ 1e10, beyond any float32 Gram);
+    * mxpois: TweedieRegressor(power=1, alpha=1e-4, fit_intercept=False), newton-cholesky at tol
+      1e-12, on Poisson counts from the same design.
+    0/1 columns are stored bit-packed, the continuous ones as float64."""
+    X, cpos, trial = _prod_columns(12000, 51)
+    N, p = X.shape
+    rng = np.random.default_rng(52)
+    binc = np.setdiff1d(np.arange(p), cpos)
+    beta = rng.normal(0, 0.4, p)
+    beta[cpos] = [0.8, -0.6]
+    y = X @ beta + rng.normal(0, 1.0, N)
+    out = dict(mx_bits=np.packbits(X[:, binc].astype(np.uint8), axis=0), mx_binc=binc,
+               mx_cpos=cpos, mx_cont=X[:, cpos].copy(), mx_shape=np.array(X.shape),
+               mx_trial=trial, mx_y=y)
+    out["mx_coef"] = LinearRegression(fit_intercept=False).fit(X, y).coef_
+    fi = LinearRegression().fit(X[:, :-1], y)
+    out.update(mxfi_coef=fi.coef_, mxfi_b=np.array(fi.intercept_))
+    w = np.where(rng.random(N) < 0.5, -1.0, 1.0)
+    Xi = X.copy()
+    Xi[:, cpos[1]] = X[:, cpos[0]] * (1 + 1e-4 * w)
+    yi = Xi @ beta + rng.normal(0, 1.0, N)
+    ev = np.linalg.eigvalsh(Xi.T @ Xi)
+    out.update(mxill_cont=Xi[:, cpos].copy(), mxill_y=yi,
+               mxill_coef=LinearRegression(fit_intercept=False).fit(Xi, yi).coef_,
+               mxill_cond=np.array(ev[-1] / ev[0]))
+    bp = rng.normal(0, 0.15, p)
+    bp[-3:] = [0.5, 0.7, 0.3]
+    bp[cpos] = [0.05, -0.08]
+    yp = rng.poisson(np.exp(X @ bp)).astype(float)
+    tp = TweedieRegressor(power=1, alpha=1e-4, fit_intercept=False, solver="newton-cholesky",
+                          tol=1e-12, max_iter=1000).fit(X, yp)
+    out.update(mxpois_y=yp, mxpois_coef=tp.coef_)
+    return out
+
+
 def folds():
     out = {}
     trial = np.arange(5000) // 100
@@ -291,12 +380,17 @@ def main():
         np.savez_compressed(os.path.join(HERE, "api.npz"), **api_extras())
         print("api fixture written")
         return
+    if sys.argv[1:] == ["mixed"]:          # round-5 fixture only (others unchanged)
+        np.savez_compressed(os.path.join(HERE, "mixed.npz"), **mixed_cases())
+        print("mixed fixture written")
+        return
     if sys.argv[1:] == ["rank"]:           # round-4 fixture only (others unchanged)
         np.savez_compressed(os.path.join(HERE, "rank.npz"), **rank_cases())
         print("rank fixture written")
         return
     np.savez_compressed(os.path.join(HERE, "api.npz"), **api_extras())
     np.savez_compressed(os.path.join(HERE, "rank.npz"), **rank_cases())
+    np.savez_compressed(os.path.join(HERE, "mixed.npz"), **mixed_cases())
     np.savez_compressed(os.path.join(HERE, "timeshift_known.npz"), **timeshift_known_answers())
     f, meta = fits()
     np.savez_compressed(os.path.join(HERE, "fits.npz"), **f)

@@ -72,8 +72,9 @@ def test_design_from_events_matches_dense(engine, torch_mod):
     assert np.all(d.xb[:, s.N:].float().cpu().numpy() == 0.0)
 
 
-def test_pack_and_gemv(engine, torch_mod):
+def test_pack_and_gemv(engine, torch_mod, monkeypatch):
     torch = torch_mod
+    monkeypatch.setattr(engine, "MIXED_MAX_K", 0)      # the all-f32 design path
     rng = np.random.default_rng(2)
     X = rng.normal(size=(3000, 77))
     d = engine.Design.from_host(X)
@@ -436,9 +437,10 @@ def test_engine_batched_masks_match_oracle(engine):
         assert rel(r.coef, c) < 1e-4
 
 
-def test_syrk_f32_exact_gram(engine, torch_mod):
+def test_syrk_f32_exact_gram(engine, torch_mod, monkeypatch):
     """Real-valued (not bf16-exact) design: the f32-MFMA Gram matches float64 to ~1e-6."""
     torch = torch_mod
+    monkeypatch.setattr(engine, "MIXED_MAX_K", 0)      # the all-f32 design path
     from sglm_hip import _lib
     rng = np.random.default_rng(8)
     X = rng.normal(size=(5000, 140))

@@ -240,3 +240,38 @@ def test_rank_fixtures_pin_the_oracle(golden):
     X = rank_design(g, "pdup")
     c, b = glm_ref.fit_tweedie_newton(X, g["pdup_y"], 0.0, 1.0)
     assert rel(c, g["pdup_coef"]) < 1e-6 and abs(c[5] - c[-1]) < 1e-12
+
+
+# ------------------------------------------------------------------ mixed designs (round 5)
+def mixed_design(g, key="mx"):
+    """X of a mixed.npz case: the bit-packed 0/1 columns and the float64 continuous columns
+    (``key`` 'mxill' takes the near-collinear counter pair) at their positions."""
+    N, p = (int(v) for v in g["mx_shape"])
+    X = np.zeros((N, p))
+    X[:, g["mx_binc"]] = np.unpackbits(g["mx_bits"], axis=0)[:N].astype(np.float64)
+    X[:, g["mx_cpos"]] = g["mxill_cont"] if key == "mxill" else g["mx_cont"]
+    return X
+
+
+def test_mixed_fixtures_pin_the_oracle(golden):
+    """The production layout (0/1 lags + two cumcount^2/5000 counters + session dummies,
+    fit_intercept=False; sglm_cb_concat_make_design_mat.py:211-216, 224-244, 266): the oracle's
+    float64 lstsq / damped Newton reproduce sklearn's LinearRegression and TweedieRegressor
+    answers, including the near-collinear counter pair (cond ~7e9)."""
+    g = golden("mixed.npz")
+    X = mixed_design(g)
+    c, b = glm_ref.fit_ols(X, g["mx_y"], fit_intercept=False)
+    assert rel(c, g["mx_coef"]) < 1e-10 and b == 0.0
+    c, b = glm_ref.fit_ols(X[:, :-1], g["mx_y"])
+    assert rel(c, g["mxfi_coef"]) < 1e-10 and abs(b - float(g["mxfi_b"])) < 1e-10
+    Xi = mixed_design(g, "mxill")
+    assert 1e9 < float(g["mxill_cond"]) < 1e11
+    c, _ = glm_ref.fit_ols(Xi, g["mxill_y"], fit_intercept=False)
+    assert rel(c, g["mxill_coef"]) < 1e-7
+    c, _ = glm_ref.fit_tweedie_newton(X, g["mxpois_y"], 1e-4, 1.0, fit_intercept=False)
+    assert rel(c, g["mxpois_coef"]) < 1e-7
+    # the counters: cumcount^2 / 5000 over runs of consecutive integers
+    cont = g["mx_cont"]
+    for j in range(2):
+        v = np.round(np.sqrt(cont[:, j] * 5000)).astype(np.int64)
+        assert np.allclose(v.astype(float) ** 2 / 5000, cont[:, j], rtol=0, atol=1e-15)
