@@ -116,6 +116,167 @@ __global__ void __launch_bounds__(kMxT) mixed_finish_kernel(
     }
 }
 
+// Gradient rows: part[((q * nchunk) + chunk) * k + c] = sum over the chunk's rows of
+// C[c][r] R_q(r) for the fits q of one group of kMxG (blockIdx.y) and the columns c of one tile
+// of kMxKT (blockIdx.z).  Each lane takes 4 consecutive rows per step (one 32-B load of C per
+// column, one 8-B load of each R piece per fit): C is read once per group of fits, not once per
+// fit, and the fits' R pieces once per column tile.
+constexpr int kMxG = 8;             // fits per workgroup (gradient / predictor kernels)
+constexpr int kMxKT = 4;            // continuous columns per workgroup
+constexpr int kMxGRows = 32768;     // rows of one gradient chunk (32 steps of 4 rows per lane)
+
+template <int MODE>
+__device__ __forceinline__ void r4_at(const void* __restrict__ src, int64_t ld, int64_t row,
+                                      int64_t Bp, int64_t r, double out[4]) {
+    if (MODE == WT_F32) {
+        const float4 v = *reinterpret_cast<const float4*>(
+            reinterpret_cast<const float*>(src) + row * ld + r);
+        out[0] = v.x; out[1] = v.y; out[2] = v.z; out[3] = v.w;
+        return;
+    }
+    const uint16_t* b = reinterpret_cast<const uint16_t*>(src);
+    const int64_t o = row * ld + r;
+    const uint2 h = *reinterpret_cast<const uint2*>(b + o);
+    double t[4] = {(double)__uint_as_float(h.x << 16), (double)__uint_as_float(h.x & 0xffff0000u),
+                   (double)__uint_as_float(h.y << 16), (double)__uint_as_float(h.y & 0xffff0000u)};
+    if (MODE == R_PIECES) {
+        const int64_t ps = Bp * ld;
+        const uint2 m = *reinterpret_cast<const uint2*>(b + o + ps);
+        const uint2 l = *reinterpret_cast<const uint2*>(b + o + 2 * ps);
+        t[0] = (t[0] + (double)__uint_as_float(m.x << 16)) + (double)__uint_as_float(l.x << 16);
+        t[1] = (t[1] + (double)__uint_as_float(m.x & 0xffff0000u)) +
+               (double)__uint_as_float(l.x & 0xffff0000u);
+        t[2] = (t[2] + (double)__uint_as_float(m.y << 16)) + (double)__uint_as_float(l.y << 16);
+        t[3] = (t[3] + (double)__uint_as_float(m.y & 0xffff0000u)) +
+               (double)__uint_as_float(l.y & 0xffff0000u);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) out[j] = t[j];
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(kMxT) mixed_grad_kernel(
+    const void* __restrict__ R, int64_t ldr, int64_t Bp, const int32_t* __restrict__ rsel,
+    int32_t nq, const double* __restrict__ C, int64_t ldc, int32_t k, int64_t n,
+    int32_t nchunk, double* __restrict__ part) {
+    const int chunk = blockIdx.x, q0 = blockIdx.y * kMxG, c0 = blockIdx.z * kMxKT;
+    const int nf = min(kMxG, nq - q0), nc = min(kMxKT, k - c0);
+    int64_t row[kMxG];
+#pragma unroll
+    for (int f = 0; f < kMxG; ++f) row[f] = f < nf ? (rsel ? rsel[q0 + f] : q0 + f) : 0;
+    double acc[kMxG][kMxKT];
+#pragma unroll
+    for (int f = 0; f < kMxG; ++f)
+#pragma unroll
+        for (int c = 0; c < kMxKT; ++c) acc[f][c] = 0.0;
+    const int64_t r0 = (int64_t)chunk * kMxGRows;
+    const int64_t r1 = min<int64_t>(r0 + kMxGRows, n);
+    for (int64_t r = r0 + 4 * (int64_t)threadIdx.x; r < r1; r += 4 * kMxT) {
+        double cv[kMxKT][4];
+#pragma unroll
+        for (int c = 0; c < kMxKT; ++c) {
+            if (c < nc && r + 3 < r1) {
+                const double4 v = *reinterpret_cast<const double4*>(C + (int64_t)(c0 + c) * ldc + r);
+                cv[c][0] = v.x; cv[c][1] = v.y; cv[c][2] = v.z; cv[c][3] = v.w;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    cv[c][j] = (c < nc && r + j < r1) ? C[(int64_t)(c0 + c) * ldc + r + j] : 0.0;
+            }
+        }
+#pragma unroll
+        for (int f = 0; f < kMxG; ++f) {
+            if (f < nf) {
+                double rv[4];
+                r4_at<MODE>(R, ldr, row[f], Bp, r, rv);     // rows < ld: in bounds (ld % 4 == 0)
+#pragma unroll
+                for (int c = 0; c < kMxKT; ++c)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[f][c] = fma(cv[c][j], rv[j], acc[f][c]);
+            }
+        }
+    }
+    __shared__ double red[kMxT / kWave][kMxG * kMxKT];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int f = 0; f < kMxG; ++f)
+#pragma unroll
+        for (int c = 0; c < kMxKT; ++c) {
+            const double v = wave_sum_d(acc[f][c]);
+            if (lane == 0) red[wv][f * kMxKT + c] = v;
+        }
+    __syncthreads();
+    if (threadIdx.x < kMxG * kMxKT) {
+        const int f = threadIdx.x / kMxKT, c = threadIdx.x % kMxKT;
+        if (f < nf && c < nc) {
+            double v = red[0][threadIdx.x];
+            for (int w = 1; w < kMxT / kWave; ++w) v += red[w][threadIdx.x];
+            part[((int64_t)(q0 + f) * nchunk + chunk) * k + c0 + c] = v;
+        }
+    }
+}
+
+// eta[slot][r] += sum_c C[c][r] * beta[slot][cpos[c]] for r < n (float64 sum, one rounding) for
+// the fits of one group of kMxG (blockIdx.y): lanes take 4 consecutive rows, C read once per
+// group (columns in tiles of kMxKT)
+constexpr int kMxEtaK = 64;         // continuous columns of the grouped predictor kernel
+
+__global__ void __launch_bounds__(kMxT) mixed_eta4_kernel(
+    const double* __restrict__ C, int64_t ldc, int32_t k, int64_t n,
+    const int32_t* __restrict__ cpos, const float* __restrict__ beta, int32_t P,
+    const int32_t* __restrict__ slots, int32_t nb, float* __restrict__ eta, int64_t ld) {
+    __shared__ double b[kMxG][kMxEtaK];
+    const int q0 = blockIdx.y * kMxG;
+    const int nf = min(kMxG, nb - q0);
+    int64_t slot[kMxG];
+#pragma unroll
+    for (int f = 0; f < kMxG; ++f) slot[f] = f < nf ? (slots ? slots[q0 + f] : q0 + f) : 0;
+    for (int t = threadIdx.x; t < kMxG * k; t += kMxT) {
+        const int f = t / k, c = t % k;
+        b[f][c] = f < nf ? (double)beta[slot[f] * P + cpos[c]] : 0.0;
+    }
+    __syncthreads();
+    for (int64_t r = 4 * ((int64_t)blockIdx.x * kMxT + threadIdx.x); r < n;
+         r += 4 * (int64_t)gridDim.x * kMxT) {
+        double acc[kMxG][4];
+#pragma unroll
+        for (int f = 0; f < kMxG; ++f)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[f][j] = 0.0;
+        for (int c = 0; c < k; ++c) {
+            double cv[4];
+            if (r + 3 < n) {
+                const double4 v = *reinterpret_cast<const double4*>(C + (int64_t)c * ldc + r);
+                cv[0] = v.x; cv[1] = v.y; cv[2] = v.z; cv[3] = v.w;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) cv[j] = r + j < n ? C[(int64_t)c * ldc + r + j] : 0.0;
+            }
+#pragma unroll
+            for (int f = 0; f < kMxG; ++f)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[f][j] = fma(cv[j], b[f][c], acc[f][j]);
+        }
+#pragma unroll
+        for (int f = 0; f < kMxG; ++f) {
+            if (f < nf) {
+                float* e = eta + slot[f] * ld + r;
+                if (r + 3 < n) {
+                    float4 v = *reinterpret_cast<float4*>(e);
+                    v.x = (float)((double)v.x + acc[f][0]);
+                    v.y = (float)((double)v.y + acc[f][1]);
+                    v.z = (float)((double)v.z + acc[f][2]);
+                    v.w = (float)((double)v.w + acc[f][3]);
+                    *reinterpret_cast<float4*>(e) = v;
+                } else {
+                    for (int j = 0; j < 4 && r + j < n; ++j)
+                        e[j] = (float)((double)e[j] + acc[f][j]);
+                }
+            }
+        }
+    }
+}
+
 // eta[slot][r] += sum_c C[c][r] * beta[slot][cpos[c]] for r < n (float64 sum, one rounding)
 __global__ void __launch_bounds__(kMxT) mixed_eta_kernel(
     const double* __restrict__ C, int64_t ldc, int32_t k, int64_t n,
@@ -186,7 +347,7 @@ extern "C" {
 size_t sglm_mixed_work_bytes(int32_t ns, int32_t k, int64_t n) {
     if (ns <= 0 || k <= 0 || n <= 0) return 16;
     const int64_t npairs = (int64_t)k * (k + 1) / 2 > k ? (int64_t)k * (k + 1) / 2 : k;
-    return (size_t)((int64_t)ns * nchunks(n) * npairs * sizeof(double));
+    return (size_t)((int64_t)ns * nchunks(n) * npairs * sizeof(double));   // >= the gradient's
 }
 
 int sglm_mixed_wc(const float* W, int64_t ldw, const int32_t* slots, int32_t ns,
@@ -240,21 +401,28 @@ int sglm_mixed_xtr(int32_t rmode, const void* R, int64_t ldr, int64_t Bp, const 
         set_error("sglm_mixed_xtr: bad args (mode=%d nq=%d k=%d)", rmode, nq, k);
         return SGLM_EINVAL;
     }
+    if (ldr % 4 || ldc % 4) {
+        set_error("sglm_mixed_xtr: row strides must be multiples of 4 (ldr=%lld ldc=%lld)",
+                  (long long)ldr, (long long)ldc);
+        return SGLM_EINVAL;
+    }
     hipStream_t s = as_stream(stream);
     double* part = (double*)work;
     const int32_t* pa = pairs;        // 0 .. k-1
     const int32_t* pb = pairs + k;    // k (the ones factor)
+    const int nc = (int)((n + kMxGRows - 1) / kMxGRows);
+    dim3 grid((unsigned)nc, (unsigned)((nq + kMxG - 1) / kMxG), (unsigned)((k + kMxKT - 1) / kMxKT));
     if (rmode == WT_F32)
-        launch_dot<WT_F32>(R, ldr, 0, rsel, nq, C, ldc, k, pa, pb, k, n, part, s);
+        mixed_grad_kernel<WT_F32><<<grid, kMxT, 0, s>>>(R, ldr, Bp, rsel, nq, C, ldc, k, n, nc, part);
     else if (rmode == R_PIECES)
-        launch_dot<R_PIECES>(R, ldr, Bp, rsel, nq, C, ldc, k, pa, pb, k, n, part, s);
+        mixed_grad_kernel<R_PIECES><<<grid, kMxT, 0, s>>>(R, ldr, Bp, rsel, nq, C, ldc, k, n, nc, part);
     else
-        launch_dot<R_BF16>(R, ldr, 0, rsel, nq, C, ldc, k, pa, pb, k, n, part, s);
-    int st = check_launch("mixed_dot_kernel");
+        mixed_grad_kernel<R_BF16><<<grid, kMxT, 0, s>>>(R, ldr, Bp, rsel, nq, C, ldc, k, n, nc, part);
+    int st = check_launch("mixed_grad_kernel");
     if (st) return st;
     const int64_t tot = (int64_t)nq * k;
     mixed_finish_kernel<1><<<(unsigned)((tot + kMxT - 1) / kMxT), kMxT, 0, s>>>(
-        part, nq, nchunks(n), k, pa, pb, k, cpos, P, gslots, g);
+        part, nq, nc, k, pa, pb, k, cpos, P, gslots, g);
     return check_launch("sglm_mixed_xtr");
 }
 
@@ -265,6 +433,16 @@ int sglm_mixed_eta(const double* C, int64_t ldc, int32_t k, int64_t n, const int
     if (!C || !cpos || !beta || !eta || k > kMxMaxK || ldc < n || ld < n || nb > 65535) {
         set_error("sglm_mixed_eta: bad args (k=%d nb=%d)", k, nb);
         return SGLM_EINVAL;
+    }
+    if (ld % 4 == 0 && ldc % 4 == 0 && k <= kMxEtaK) {
+        // rows in steps of 4 per lane, fits in groups of kMxG; ~2 K workgroups in total
+        const int ng = (nb + kMxG - 1) / kMxG;
+        int64_t blocks = (n + 4 * kMxT - 1) / (4 * kMxT);
+        const int64_t want = (2048 + ng - 1) / ng;
+        if (blocks > want) blocks = want;
+        mixed_eta4_kernel<<<dim3((unsigned)blocks, (unsigned)ng), kMxT, 0, as_stream(stream)>>>(
+            C, ldc, k, n, cpos, beta, P, slots, nb, eta, ld);
+        return check_launch("sglm_mixed_eta");
     }
     int64_t blocks = (n + kMxT * 8 - 1) / (kMxT * 8);
     if (blocks > 4096) blocks = 4096;

@@ -2369,6 +2369,8 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
 # refinements -- no pass over the rows per iteration, and no f32 residual in the fixed point
 GRAM_LS = __import__("os").environ.get("SGLM_GRAM_LS", "1") == "1"
 GRAM_LS_REFINE = int(__import__("os").environ.get("SGLM_GRAM_LS_REFINE", "2"))
+# device bytes the float64 factors of one _gram_ls chunk may take
+GRAM_LS_FACTOR_BYTES = float(__import__("os").environ.get("SGLM_GRAM_LS_FACTOR_BYTES", "16e9"))
 
 
 def _gram_ls(prob: Problem, reqs: List[FitReq], stats: Optional[IrlsStats], bufs, comm):
@@ -2437,28 +2439,39 @@ def _gram_ls(prob: Problem, reqs: List[FitReq], stats: Optional[IrlsStats], bufs
             k_h.append(mrep[int(r.mask)])
             k_d.append(int(k))
         fkey[k] = keys[key]
-    f64 = _Factor64(d, bf, np.asarray(k_h), np.asarray(k_d), lamp_d, st)
-    ints = up(np.concatenate([np.arange(B0), fkey, cidx, np.asarray(k_h)]).astype(np.int32))
-    fits_d, fsrc_d, csrc_d = ints[:B0], ints[B0:2 * B0], ints[2 * B0:3 * B0]
-    hsrc_d = ints[3 * B0:]
     x = torch.zeros((B0, P), dtype=torch.float64, device=dev)
-    _lib.call("sglm_chol64_solve_add", _p(f64.U), P, _p(f64.state), _p(fits_d), _p(fsrc_d),
-              _p(csrc_d), B0, _p(c), _p(x), st)
     res_d = torch.empty_like(x)
-    S, k_c, cmap = f64._S, (d.k if f64._S is not None else 0), (
-        d._mix["cmap"] if f64._S is not None else None)
-    for _ in range(GRAM_LS_REFINE):
-        _lib.call("sglm_chol64_resid", _p(bf.H), P, _p(hsrc_d), _p(S), k_c, _p(cmap),
-                  _p(fits_d), _p(fsrc_d), _p(csrc_d), B0, _p(c), _p(lamp_d), _p(bf.dshift),
-                  _p(x), _p(res_d), st)
+    dropped = torch.zeros(len(k_h), dtype=torch.float64, device=dev)
+    # the factors in chunks of keys within GRAM_LS_FACTOR_BYTES (a factor and, for the
+    # unpenalised keys, the minimum-norm work: 16 B per P^2 entry each)
+    per = max(1, int(GRAM_LS_FACTOR_BYTES // (16 * P * P)))
+    k_h, k_d = np.asarray(k_h), np.asarray(k_d)
+    for a in range(0, len(k_h), per):
+        b = min(len(k_h), a + per)
+        sel = np.flatnonzero((fkey >= a) & (fkey < b))
+        nq = int(sel.size)
+        f64 = _Factor64(d, bf, k_h[a:b], k_d[a:b], lamp_d, st)
+        ints = up(np.concatenate([sel, fkey[sel] - a, cidx[sel], k_h[a:b]]).astype(np.int32))
+        fits_d, fsrc_d, csrc_d = ints[:nq], ints[nq:2 * nq], ints[2 * nq:3 * nq]
+        hsrc_d = ints[3 * nq:]
         _lib.call("sglm_chol64_solve_add", _p(f64.U), P, _p(f64.state), _p(fits_d),
-                  _p(fsrc_d), None, B0, _p(res_d), _p(x), st)
-    # unpenalised fits: the minimum-norm point of the solution set (lstsq)
-    pf = np.flatnonzero(lam0)
-    f64.minnorm(d, bf, pf, fkey[pf], x, st)
+                  _p(fsrc_d), _p(csrc_d), nq, _p(c), _p(x), st)
+        S, k_c, cmap = f64._S, (d.k if f64._S is not None else 0), (
+            d._mix["cmap"] if f64._S is not None else None)
+        for _ in range(GRAM_LS_REFINE):
+            _lib.call("sglm_chol64_resid", _p(bf.H), P, _p(hsrc_d), _p(S), k_c, _p(cmap),
+                      _p(fits_d), _p(fsrc_d), _p(csrc_d), nq, _p(c), _p(lamp_d),
+                      _p(bf.dshift), _p(x), _p(res_d), st)
+            _lib.call("sglm_chol64_solve_add", _p(f64.U), P, _p(f64.state), _p(fits_d),
+                      _p(fsrc_d), None, nq, _p(res_d), _p(x), st)
+        # unpenalised fits: the minimum-norm point of the solution set (lstsq)
+        pf = sel[lam0[sel]]
+        f64.minnorm(d, bf, pf, fkey[pf] - a, x, st)
+        dropped[a:b] = f64.counts[:, 1].to(torch.float64)
+        del f64
     bf.beta[:B0].copy_(x)
     d.eta(bf.beta, bf.eta)
-    outs = torch.cat([x.reshape(-1), f64.counts[:, 1].to(torch.float64)]).cpu().numpy()
+    outs = torch.cat([x.reshape(-1), dropped]).cpu().numpy()
     if stats is not None:
         stats.newton_iters += 1
         stats.fit_iters += B0
