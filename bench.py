@@ -52,6 +52,13 @@ CONFIGS = {
     "signal": (0, 0, 0, 0, 0),
     # pp_design_mat.make_design_mat: trials per session
     "designmat": (0, 0, 0, 0, 0),
+    # the reference's own logged OLS workload (02-create_features-lynne.ipynb cell 3, 483 s):
+    # ~1.58M rows, 7 events x 41 lags = 287 predictors, 10 GroupShuffleSplit splits + refit +
+    # holdout score, through the drop-in flow from a host frame
+    "olsref": (1_581_817, 7, 20, 10, 1),
+    # the production 50-split grid (er_refactored_from_scratch_cleanup.py:230-246, 421-452) at
+    # the logged 1,900,992-row frame (02-create_features-lynne-f5.ipynb): 18 events x 41 lags
+    "prod50": (1_900_992, 18, 20, 50, 1),
 }
 DM_TRIALS = 100_000                 # ~9.8M rows at 50 Hz (a ~54 h session, or a day's sessions)
 DM_CPU_TRIALS = 20_000              # the pandas sample (~2M rows, ~6 s)
@@ -597,6 +604,126 @@ def bench_designmat(a):
         "cpu_baseline": cpu}))
 
 
+def ols_flow(df, ev, L, K, timings=None):
+    """The reference's OLS production flow through the drop-in API
+    (er_refactored_from_scratch_cleanup.py:421-452): sglm_ez.timeshift_cols (shifts 0,
+    -L..-1, 1..L) -> the NaN-row filter -> holdout_split_by_trial_id (20 %) -> cv_idx_by_trial_id
+    (K splits, test 20 %) -> simple_cv_fit (OLS, fit_intercept) -> training_fit_holdout_score.
+    Returns (simple_cv_fit results, holdout R^2, setup frame)."""
+    import contextlib
+    import io
+    import torch
+    import sglm_ez
+    ph = {} if timings is None else timings
+
+    def mark(name, t):
+        torch.cuda.synchronize()
+        now = time.perf_counter()
+        ph[name] = ph.get(name, 0.0) + now - t
+        return now
+    t = time.perf_counter()
+    with contextlib.redirect_stdout(io.StringIO()):            # the reference prints as it goes
+        dfrel = sglm_ez.timeshift_cols(df, ev, neg_order=-L, pos_order=L)
+        xcols = sglm_ez.add_timeshifts_to_col_list(ev, ev, neg_order=-L, pos_order=L)
+        t = mark("timeshift_cols", t)
+        dfrel = dfrel[dfrel[["nTrial"] + xcols + ["y"]].isna().sum(axis=1) == 0]
+        t = mark("nan_filter", t)
+        np.random.seed(30186)
+        hold = sglm_ez.holdout_split_by_trial_id(dfrel, id_cols=["nTrial"], perc_holdout=0.2)
+        setup, holdout = dfrel.loc[~hold], dfrel.loc[hold]
+        cv_idx = sglm_ez.cv_idx_by_trial_id(setup, trial_id_columns=["nTrial"], num_folds=K,
+                                            test_size=0.2)
+        t = mark("holdout_and_folds", t)
+        kws = [{"alpha": 0.0, "l1_ratio": 0.0, "max_iter": 1000, "fit_intercept": True}]
+        out = sglm_ez.simple_cv_fit(setup[xcols], setup["y"], cv_idx, kws, model_type="Normal",
+                                    score_method="r2")
+        t = mark("simple_cv_fit", t)
+        _, hs, _ = sglm_ez.training_fit_holdout_score(setup[xcols], setup["y"], holdout[xcols],
+                                                      holdout["y"], out[2])
+        mark("training_fit_holdout_score", t)
+    return out, hs, setup, xcols, cv_idx
+
+
+def cpu_reference_ols(df, ev, L, setup, cv_idx, K):
+    """The reference's CPU path sampled the BASELINE.md §2 way: sklearn LinearRegression (what
+    GLM('Normal', alpha=0) selects, backend/sglm.py:96-101) on ONE full-size fold (its train rows
+    of the dense float64 lag design) and on the full setup rows (the refit), called directly
+    (the reference's import is denied); the workload = K fold fits + the refit
+    + training_fit_holdout_score's second full fit, extrapolated from the two timings."""
+    from sklearn.linear_model import LinearRegression
+    E = df[ev].to_numpy(dtype=np.float64)
+    y = df["y"].to_numpy()
+    pos = setup.positions()
+    shifts = [0] + list(range(-L, 0)) + list(range(1, L + 1))
+
+    def dense(rows):
+        X = np.empty((rows.size, len(shifts) * len(ev)))
+        for bi, sh in enumerate(shifts):
+            X[:, bi * len(ev):(bi + 1) * len(ev)] = E[rows - sh]
+        return X
+    tr = pos[np.asarray(cv_idx[0][0])]
+    X = dense(tr)
+    t0 = time.perf_counter()
+    LinearRegression().fit(X, y[tr])
+    t_fold = time.perf_counter() - t0
+    del X
+    X = dense(pos)
+    t0 = time.perf_counter()
+    LinearRegression().fit(X, y[pos])
+    t_refit = time.perf_counter() - t0
+    del X
+    total = K * t_fold + 2 * t_refit
+    return {"value": total, "unit": "s per workload (extrapolated)", "cores": _blas_threads(),
+            "kind": "reference",
+            "sample": f"sklearn LinearRegression (lstsq) on fold 0's {tr.size} train rows x "
+                      f"{len(shifts) * len(ev)} ({t_fold:.1f} s) and on the {pos.size} setup "
+                      f"rows ({t_refit:.1f} s); x{K} folds + 2 full fits",
+            "cpu": _cpu_model(), "nproc": os.cpu_count()}
+
+
+def bench_ols(a):
+    """The reference's OLS workloads end to end on one GPU: the logged notebook run (config
+    olsref) and the 50-split production grid (prod50), from a host event frame through the
+    drop-in API (ols_flow).  One step = the whole flow."""
+    import torch
+    from sglm_hip import synth
+    N, m, L, K, _ = CONFIGS[a.config]
+    df, ev, beta, b0 = synth.ols_frame(N, m, -L, L, seed=11)
+    for _ in range(a.warmup):
+        ols_flow(df, ev, L, K)
+    torch.cuda.synchronize()
+    ph = {}
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        out, hs, setup, xcols, cv_idx = ols_flow(df, ev, L, K, ph)
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / a.steps
+    best = out[3]
+    coef = np.asarray(best.model.coef_)
+    # the synthetic truth is known: the refit recovers it to the noise level
+    truth_err = float(np.max(np.abs(coef - beta.reshape(-1))))
+    cpu = None if a.no_cpu else cpu_reference_ols(df, ev, L, setup, cv_idx, K)
+    p = len(xcols)
+    print(json.dumps({
+        "metric": "IRLS iters/sec on 1M\u00d72000 design mat; CV-grid wall-clock (5-fold\u00d720 \u03bb)",
+        "value": el, "unit": "s per OLS workload (host frame -> fits -> holdout score)",
+        "n_gpus": 1, "steps": a.steps, "warmup": a.warmup, "ms_per_step": el * 1e3,
+        "higher_is_better": False, "scaling": "strong", "vs_baseline": None,
+        "dtype": "f64 (exact 0/1 Gram in f32 integers, float64 factor / normal equations)",
+        "data": "synthetic",
+        "config": {"workload": f"Gaussian OLS (fit_intercept) {N} rows x {p} predictors "
+                               f"({m} events x {2 * L + 1} lags), {K} GroupShuffleSplit splits + "
+                               f"refit + holdout score, drop-in flow from a host frame",
+                   "config_name": a.config, "setup_rows": int(setup.shape[0]),
+                   "phases_ms": {k: v / a.steps * 1e3 for k, v in ph.items()},
+                   "best_cv_R2": float(out[0]), "holdout_R2": float(hs),
+                   "refit_max_abs_err_vs_truth": truth_err,
+                   "reference_logged_s": 483.2 if a.config == "olsref" else None,
+                   "parallelism": "one GPU (the flow is one design; fits batched)"},
+        "roofline": None,
+        "cpu_baseline": cpu}))
+
+
 def spawn_ranks(a):
     """``--gpus N`` without a launcher: start N rank processes (torch.distributed.run, one per
     GPU, rendezvous on 127.0.0.1) as CHILDREN before anything touches the GPU, and exit with
@@ -721,9 +848,9 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group("gloo")
-    if a.config in ("c5", "prep", "signal", "designmat"):
+    if a.config in ("c5", "prep", "signal", "designmat", "olsref", "prod50"):
         {"c5": bench_c5, "prep": bench_prep, "signal": bench_signal,
-         "designmat": bench_designmat}[a.config](a)
+         "designmat": bench_designmat, "olsref": bench_ols, "prod50": bench_ols}[a.config](a)
         if world > 1:
             dist.destroy_process_group()
         return

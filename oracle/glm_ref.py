@@ -162,6 +162,29 @@ def fit_ols(X, y, fit_intercept=True):
     return scipy.linalg.lstsq(X, y, cond=cond)[0], 0.0
 
 
+def fit_ols_chunks(chunks, fit_intercept=True):
+    """``LinearRegression.fit`` for a design too large to hold densely: float64 sums of
+    [X, 1]^T [X, 1] and [X, 1]^T y over row chunks ((X_chunk, y_chunk) pairs), then the
+    centred normal equations solved by scipy lstsq on the Gram (the same minimiser as the dense
+    lstsq of ``fit_ols`` for a full-rank design; test infrastructure for full-size grids)."""
+    G = c = None
+    n = 0.0
+    for Xc, yc in chunks:
+        Xc = np.asarray(Xc, dtype=np.float64)
+        Xa = np.hstack([Xc, np.ones((Xc.shape[0], 1))])
+        g, cc = Xa.T @ Xa, Xa.T @ np.asarray(yc, dtype=np.float64)
+        G, c = (g, cc) if G is None else (G + g, c + cc)
+        n += Xc.shape[0]
+    p = G.shape[0] - 1
+    if not fit_intercept:
+        return scipy.linalg.lstsq(G[:p, :p], c[:p])[0], 0.0
+    xm, ym = G[:p, p] / n, c[p] / n
+    Gc = G[:p, :p] - n * np.outer(xm, xm)
+    cc = c[:p] - n * xm * ym
+    coef = scipy.linalg.lstsq(Gc, cc)[0]
+    return coef, float(ym - xm @ coef)
+
+
 def fit_ridge(X, y, alpha, fit_intercept=True):
     """``Ridge`` cholesky solver on centred data (sklearn/_ridge.py:201-213)."""
     X = np.asarray(X, dtype=np.float64)

@@ -263,3 +263,39 @@ def prod_counters(trial: np.ndarray, seed: int = 0) -> np.ndarray:
     out[0] = np.where(enl, pos.astype(np.float64) ** 2 / 5000.0, 0.0)
     out[1] = np.where(enlp, (pos - le[ti] - 1).astype(np.float64) ** 2 / 5000.0, 0.0)
     return out
+
+
+def ols_frame(N: int, m: int, neg: int, pos: int, seed: int = 0, rate=(0.005, 0.03),
+              trial_len=(120, 360)):
+    """A host session frame in the layout the reference's OLS drivers start from
+    (er_refactored_from_scratch_cleanup.py:421-452; 02-create_features-lynne.ipynb): ``nTrial``
+    (trials of ``trial_len`` rows), m float64 0/1 event columns ``e0 ..`` (Bernoulli per row at
+    rates spread over ``rate``), and a Gaussian response ``y`` = the lag design (shifts 0,
+    neg..-1, 1..pos, as sglm_ez.timeshift_cols) times random coefficients + intercept + noise,
+    NaN on the first |neg| and last pos rows (where a lag leaves the recording).  Returns
+    (DataFrame, event names, coefficient table [K][m] in timeshift_cols' shift order, intercept)."""
+    import pandas as pd
+    rng = np.random.default_rng(seed)
+    rates = np.linspace(rate[0], rate[1], m)
+    E = (rng.random((N, m)) < rates[None, :]).astype(np.float64)
+    lens = rng.integers(trial_len[0], trial_len[1] + 1, N // trial_len[0] + 2)
+    trial = np.repeat(np.arange(1, lens.size + 1), lens)[:N].astype(np.float64)
+    shifts = [0] + list(range(neg, 0)) + list(range(1, pos + 1))
+    beta = rng.normal(0, 0.3, (len(shifts), m))
+    b0 = 0.7
+    y = np.full(N, b0)
+    for bi, s in enumerate(shifts):
+        contrib = E @ beta[bi]
+        if s >= 0:
+            y[s:] += contrib[:N - s]
+        else:
+            y[:N + s] += contrib[-s:]
+    y += rng.normal(0, 1.0, N)
+    y[:max(0, pos)] = np.nan
+    if neg < 0:
+        y[N + neg:] = np.nan
+    ev = [f"e{a}" for a in range(m)]
+    df = pd.DataFrame(E, columns=ev)
+    df.insert(0, "nTrial", trial)
+    df["y"] = y
+    return df, ev, beta, b0

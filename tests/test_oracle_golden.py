@@ -275,3 +275,17 @@ def test_mixed_fixtures_pin_the_oracle(golden):
     for j in range(2):
         v = np.round(np.sqrt(cont[:, j] * 5000)).astype(np.int64)
         assert np.allclose(v.astype(float) ** 2 / 5000, cont[:, j], rtol=0, atol=1e-15)
+
+
+def test_ols_chunks_matches_dense_lstsq(golden):
+    """The chunked normal-equations OLS oracle (full-size grids) equals the dense lstsq oracle
+    and sklearn's LinearRegression golden."""
+    g = golden("fits.npz")
+    X, y = g["gau_X"], g["gau_y"]
+    ch = [(X[a:a + 700], y[a:a + 700]) for a in range(0, X.shape[0], 700)]
+    c, b = glm_ref.fit_ols_chunks(ch)
+    assert rel(c, g["ols_coef"]) < 1e-9 and abs(b - float(g["ols_b"])) < 1e-9
+    gm = golden("mixed.npz")
+    Xm = mixed_design(gm)
+    c, b = glm_ref.fit_ols_chunks([(Xm, gm["mx_y"])], fit_intercept=False)
+    assert rel(c, gm["mx_coef"]) < 1e-9 and b == 0.0
