@@ -76,6 +76,12 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-check", action="store_true",
+                    help="skip the float64 Newton-distance spot check after the timed region "
+                         "(its rocBLAS kernels stay out of a kernel-trace profile)")
+    ap.add_argument("--cpu-full-fold", type=int, default=1,
+                    help="1: the CPU baseline times one full-size split fit + refit (BASELINE.md "
+                         "§2); 0: only the row sample")
     ap.add_argument("--no-dropin", action="store_true",
                     help="skip the drop-in production-flow leg (dropin_grid_s)")
     ap.add_argument("--cpu-rows", type=int, default=100_000,
@@ -166,6 +172,32 @@ def cpu_reference_grid(s, cv_idx, lams, rows, lam_sample=(0, 10, 19), fold_threa
                       f"{sample_s:.1f} s (lbfgs iters {min(iters)}-{max(iters)}); "
                       f"x{len(lams) / len(lam_sample):.2f} lambdas x{s.N / rows:.0f} rows",
             "cpu": _cpu_model(), "nproc": os.cpu_count()}
+
+
+def cpu_reference_full(s, cv_idx, lams, j=10):
+    """The BASELINE.md §2 CPU measurement: ONE full-size split fit (split 0's train rows) and the
+    full refit at lambda index j, sklearn TweedieRegressor(power=1, alpha) with its default
+    lbfgs (backend/sglm.py:112-115) on dense float64 copies (X[idx_train] as the reference's
+    fold loop makes them, backend/sglm_cv.py:107-110); the grid = the mean of the two fit times
+    x 120 fits, labelled extrapolated.  Returns (seconds per grid, detail dict)."""
+    from sklearn.linear_model import TweedieRegressor
+    alpha = float(lams[j])
+    tr = np.asarray(cv_idx[0][0])
+    X = dense_slice(s, s.N)
+    t0 = time.perf_counter()
+    Xtr = X[tr]
+    m1 = TweedieRegressor(power=1, alpha=alpha).fit(Xtr, s.y[tr])
+    t_split = time.perf_counter() - t0
+    del Xtr
+    t0 = time.perf_counter()
+    m2 = TweedieRegressor(power=1, alpha=alpha).fit(X, s.y)
+    t_refit = time.perf_counter() - t0
+    del X
+    nfits = len(lams) * (len(cv_idx) + 1)
+    grid_s = 0.5 * (t_split + t_refit) * nfits
+    return grid_s, {"split_fit_s": round(t_split, 2), "refit_s": round(t_refit, 2),
+                    "lbfgs_iters": [int(m1.n_iter_), int(m2.n_iter_)], "lambda": alpha,
+                    "rows": [int(tr.size), int(s.N)]}
 
 
 def cpu_port_iter(s, n_rows_unit, rows):
@@ -935,7 +967,7 @@ def main():
         traffic, traffic_src = pmc_traffic()
         conv = all(r["converged"] for r in res)
         ndist = None
-        if world == 1 and a.config in ("c4", "c4mixed"):
+        if world == 1 and a.config in ("c4", "c4mixed") and not a.no_check:
             # float64 Newton distance of the lambda = 1e-4 split-0 fit and refit (parity spot
             # check of the timed grid's output; tests/test_gpu_fullsize.py checks every fit)
             ndist = newton_distance(s, design, cv_idx, res, lams, [(0, 0), (0, -1)], extra)
@@ -966,6 +998,19 @@ def main():
         cpu = None
         if not a.no_cpu and world == 1 and extra is None:
             cpu = cpu_reference_grid(s, cv_idx, lams, a.sklearn_rows)
+            if a.cpu_full_fold:
+                # the planned measurement: one full-size split fit + refit,
+                # x 120 fits; the row-sample extrapolation rides along
+                full_s, det = cpu_reference_full(s, cv_idx, lams)
+                cpu["row_sample_extrapolation_s"] = cpu["value"]
+                cpu["row_sample"] = cpu["sample"]
+                cpu["value"] = full_s
+                cpu["sample"] = (f"sklearn TweedieRegressor(power=1, alpha={det['lambda']:.3g}) "
+                                 f"lbfgs on the full-size split-0 train rows ({det['rows'][0]} x "
+                                 f"{s.p}, {det['split_fit_s']} s, {det['lbfgs_iters'][0]} iters) "
+                                 f"and the full refit ({det['rows'][1]} rows, {det['refit_s']} s, "
+                                 f"{det['lbfgs_iters'][1]} iters); mean x 120 fits")
+                cpu["full_fold"] = det
             cpu["port_oracle_newton"] = cpu_port_iter(s, s.N, a.cpu_rows)
         out = {
             "metric": "IRLS iters/sec on 1M×2000 design mat; CV-grid wall-clock (5-fold×20 λ)",
@@ -1024,6 +1069,9 @@ def main():
                 "frac": achieved / PEAK_BF16_TFLOPS,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
+                "traffic_kind": "stored PMC (the committed rocprofv3 --pmc summary named in "
+                                "traffic_source, per Gram launch of this grid; PMC counters "
+                                "cannot be read inside this process)",
                 # PMC bytes over the launch's algorithmic bytes (each compacted design once,
                 # the bf16 weights, the upper-triangle f32 output): > 1 = re-read / slab bytes
                 "algorithmic_bytes_per_launch": alg_bytes,

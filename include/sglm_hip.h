@@ -713,6 +713,13 @@ int sglm_host_pack_bits_cols(const void* const* src, const int64_t* stride, int3
  * as backend/sglm_pp.py:236-264 draws them).  len[j] must equal the row count it selects. */
 int sglm_host_group_rows(const int64_t* gidx, int64_t n, const uint8_t* side, int32_t nsplits,
                          int64_t G, int64_t* const* out, const int64_t* len, int32_t nthreads);
+/* sglm_host_group_runs: the same lists for groups laid out as runs of consecutive rows (a
+ * non-decreasing trial id column): run r = rows start[r] .. start[r] + rlen[r] - 1 of group
+ * grp[r] (runs ascending, disjoint); list 2k / 2k + 1 = the rows of the runs whose group has
+ * side[k][g] == 1 / 2.  No per-row group index (cv_idx_by_trial_id on a sorted trial column). */
+int sglm_host_group_runs(const int64_t* start, const int64_t* rlen, const int64_t* grp,
+                         int64_t nruns, const uint8_t* side, int32_t nsplits, int64_t G,
+                         int64_t* const* out, const int64_t* len, int32_t nthreads);
 
 #ifdef __cplusplus
 }

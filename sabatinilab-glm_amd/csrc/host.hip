@@ -13,6 +13,11 @@
 
 #include "common.h"
 
+extern "C" int sglm_host_simd_level(void);                      // host_simd.cpp
+extern "C" void sglm_host_pack_block_avx512(const double* base, int64_t S, int32_t ncols,
+                                            int64_t r0, int64_t r1, int64_t nwords,
+                                            uint32_t* bits, uint8_t* bad, int64_t* cnt);
+
 namespace {
 
 struct MaskJob {
@@ -221,6 +226,30 @@ extern "C" int sglm_host_pack_bits_cols(const void* const* src, const int64_t* s
     bool block = ncols > 1 && S >= ncols;
     for (int c = 1; block && c < ncols; ++c)
         block = stride[c] == S && (const double*)src[c] == (const double*)src[0] + c;
+    if (block && ncols <= 256 && sglm_host_simd_level() > 0) {
+        // AVX-512: 16 columns per vector op (host_simd.cpp)
+        const double* base = (const double*)src[0];
+        for (int t = 0; t < nt; ++t)
+            th.emplace_back([=, &bad, &cnt] {
+                for (int64_t q = t; q < nchunks; q += nt) {
+                    const int64_t r0 = q * chunk, r1 = std::min(nrows, r0 + chunk);
+                    sglm_host_pack_block_avx512(base, S, ncols, r0, r1, nwords, bits,
+                                                bad[t].data(), cnt[t].data());
+                }
+            });
+        for (auto& x : th) x.join();
+        for (int c = 0; c < ncols; ++c) {
+            uint8_t x = 0;
+            int64_t o = 0;
+            for (int t = 0; t < nt; ++t) {
+                x |= bad[t][c];
+                o += cnt[t][c];
+            }
+            binary[c] = !x;
+            if (ones) ones[c] = o;
+        }
+        return SGLM_OK;
+    }
     if (block) {
         const double* base = (const double*)src[0];
         for (int t = 0; t < nt; ++t)
@@ -377,5 +406,54 @@ extern "C" int sglm_host_group_rows(const int64_t* gidx, int64_t n, const uint8_
             }
         });
     for (auto& x : th) x.join();
+    return SGLM_OK;
+}
+
+// sglm_host_group_runs: sglm_host_group_rows for groups laid out as runs of consecutive rows
+// (a non-decreasing trial id): run r covers rows start[r] .. start[r] + rlen[r] - 1 and belongs to
+// group grp[r]; list 2k (2k + 1) = the rows of the runs whose group has side[k][g] == 1 (2), in
+// ascending order.  One thread per list; no per-row group index is read or built.
+extern "C" int sglm_host_group_runs(const int64_t* start, const int64_t* rlen, const int64_t* grp,
+                                    int64_t nruns, const uint8_t* side, int32_t nsplits,
+                                    int64_t G, int64_t* const* out, const int64_t* len,
+                                    int32_t nthreads) {
+    if (nsplits <= 0 || nruns <= 0) return SGLM_OK;
+    if (!start || !rlen || !grp || !side || !out || !len || G <= 0) {
+        sglm::set_error("sglm_host_group_runs: bad args");
+        return SGLM_EINVAL;
+    }
+    for (int64_t r = 0; r < nruns; ++r)
+        if ((uint64_t)grp[r] >= (uint64_t)G || rlen[r] < 0 ||
+            (r > 0 && start[r] < start[r - 1] + rlen[r - 1])) {
+            sglm::set_error("sglm_host_group_runs: run %lld invalid (group %lld of %lld)",
+                            (long long)r, (long long)grp[r], (long long)G);
+            return SGLM_EINVAL;
+        }
+    const int nj = 2 * nsplits;
+    std::vector<int> bad(nj, 0);
+    std::vector<std::thread> th;
+    const int nt = std::max(1, std::min<int>(nthreads, nj));
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([=, &bad] {
+            for (int j = t; j < nj; j += nt) {
+                const uint8_t* sd = side + (int64_t)(j / 2) * G;
+                const uint8_t want = (uint8_t)(1 + (j & 1));
+                int64_t* o = out[j];
+                int64_t w = 0;
+                for (int64_t r = 0; r < nruns; ++r) {
+                    if (sd[grp[r]] != want) continue;
+                    if (w + rlen[r] > len[j]) { bad[j] = 1; break; }
+                    for (int64_t i = 0; i < rlen[r]; ++i) o[w + i] = start[r] + i;
+                    w += rlen[r];
+                }
+                if (w != len[j]) bad[j] = 1;
+            }
+        });
+    for (auto& x : th) x.join();
+    for (int j = 0; j < nj; ++j)
+        if (bad[j]) {
+            sglm::set_error("sglm_host_group_runs: list %d length mismatch", j);
+            return SGLM_EINVAL;
+        }
     return SGLM_OK;
 }

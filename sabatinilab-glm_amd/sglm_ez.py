@@ -128,6 +128,12 @@ def cv_idx_by_trial_id(X, y=None, trial_id_columns=[], num_folds=5, test_size=No
     """backend/sglm_ez.py:311-343 — bit-exact with the reference's GroupShuffleSplit."""
     if not isinstance(X, LagFrame):
         X = pd.DataFrame(X)
+    runs = _folds.trial_key_runs(X, trial_id_columns)
+    if runs is not None and (y is None or len(y) == len(X)):
+        # a sorted trial column: the same codes per run, the row lists written run by run
+        if num_folds is None:
+            num_folds = int(runs[0].max()) + 1
+        return _folds.cv_idx_from_runs(*runs, num_folds, test_size)
     bucket_ids = _folds.trial_keys_codes(X, trial_id_columns)
     return sglm_pp.cv_idx_from_bucket_ids(bucket_ids, X, y=y, num_folds=num_folds,
                                           test_size=test_size)

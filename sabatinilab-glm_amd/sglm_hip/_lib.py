@@ -141,6 +141,7 @@ SIGNATURES = {
     "sglm_host_gather_cols": (C.c_int, [_vp, _vp, _i32, _i64, _i32, _vp, _i32]),
     "sglm_host_pack_bits_cols": (C.c_int, [_vp, _vp, _i32, _i64, _vp, _vp, _vp, _i32]),
     "sglm_host_group_rows": (C.c_int, [_vp, _i64, _vp, _i32, _i64, _vp, _vp, _i32]),
+    "sglm_host_group_runs": (C.c_int, [_vp, _vp, _vp, _i64, _vp, _i32, _i64, _vp, _vp, _i32]),
     "sglm_scatter_rows": (C.c_int, [_i64, _vp, _i64, _vp, _i32, _vp, _i64, _vp]),
     "sglm_signal_trials_work_bytes": (_sz, [_i64]),
     "sglm_signal_trials": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp,

@@ -520,6 +520,60 @@ class Design:
         return d
 
     @classmethod
+    def from_lagged_bits(cls, B, N_raw: int, cols, shifts, r0: int, n: int, ones):
+        """from_lagged for 0/1 sources given as device bit rows B (int32 [m][ceil(N_raw/32)],
+        bit r & 31 of word r >> 5 = source row r; lagframe.LagSource.bits) with their counts of 1
+        cells: the canonical shift-major / event-major layout of contiguous rows goes straight to
+        the bit-plane design (from_event_bits); None for any other layout."""
+        require_gpu()
+        cols = np.asarray(cols, dtype=np.int64)
+        shifts = np.asarray(shifts, dtype=np.int64)
+        for major in (False, True):
+            lay = _canonical_lags(cols, shifts, int(B.shape[0]), major)
+            if lay is not None:
+                ev, sl = lay
+                eb = B[torch.from_numpy(ev).to(B.device)].contiguous()
+                hint = int(np.asarray(ones, np.int64)[ev].sum())
+                return cls.from_event_bits(eb, int(N_raw), sl, int(r0), int(n),
+                                           device="cuda", event_major=major, nnz=hint)
+        return None
+
+    @classmethod
+    def from_event_bits(cls, ebits, N_raw: int, shifts: Sequence[int], row0: int, n: int,
+                        device="cuda", event_major=False, nnz=None):
+        """from_events for 0/1 events given as device bit rows ebits (int32 [m][nwords], bit
+        v & 31 of word v >> 5 = event row v): the lag bit-planes (sglm_lag_bits), the
+        LagStructure (occurrences unpacked from the bits) and a dense bf16 copy only on first
+        use."""
+        require_gpu()
+        m = int(ebits.shape[0])
+        nwords = int(ebits.shape[1])
+        K = len(shifts)
+        p = K * m
+        if event_major:
+            cols = np.repeat(np.arange(m), K)
+            sh = np.tile(np.asarray(shifts), m)
+        else:
+            cols = np.tile(np.arange(m), K)
+            sh = np.repeat(np.asarray(shifts), m)
+        cols_d = torch.tensor(cols, dtype=torch.int32, device=device)
+        sh_d = torch.tensor(sh, dtype=torch.int32, device=device)
+
+        def fill(xb):
+            Eb = _unpack_bits(ebits, N_raw).to(torch.bfloat16).contiguous()   # (m, N_raw)
+            _lib.call("sglm_timeshift_expand", _p(Eb), N_raw, 1, N_raw, _p(cols_d), _p(sh_d), p,
+                      _p(xb), n, 1, xb.shape[1], row0, 2, 0, _stream())
+            xb[p, :n] = 1.0
+        d = cls(n, p, device, lazy_xb=fill)
+        d.xbits = torch.empty((d.P, d.ld // 32), dtype=torch.int32, device=device)
+        d.rbits = torch.empty((d.P // 64) * d.ld * 2, dtype=torch.int32, device=device)
+        _lib.call("sglm_lag_bits", _p(ebits), nwords, _p(cols_d), _p(sh_d), p, row0, n,
+                  d.ld, d.P, _p(d.xbits), _p(d.rbits), _stream())
+        d.lag = LagStructure.build(None, shifts, row0, n, event_major, ebits=ebits, nnz=nnz,
+                                   n_raw=N_raw)
+        return d
+
+    @classmethod
     def from_device(cls, Xt, device="cuda"):
         """Pack a device torch tensor (n x p, f32/f64, any strides); a few non-binary columns
         make a mixed design (see MIXED_MAX_K)."""
@@ -799,6 +853,12 @@ def xtv_digits(d: Design, M, V64, pairs, out, mixed=True):
     return out
 
 
+def _unpack_bits(bits, n: int):
+    """uint8 [rows][n] of device bit rows (int32 [rows][nwords], bit r & 31 of word r >> 5)."""
+    sh = torch.arange(32, dtype=torch.int32, device=bits.device)
+    return ((bits.unsqueeze(-1) >> sh) & 1).to(torch.uint8).reshape(bits.shape[0], -1)[:, :n]
+
+
 def _canonical_lags(cols, shifts, m, event_major):
     """(events, shift list) when the (column, shift) pairs are every event x every shift in
     the shift-major (col = b * m' + a) or event-major (col = a * K + b) order, else None."""
@@ -832,10 +892,17 @@ class LagStructure:
     design."""
 
     @classmethod
-    def build(cls, E, shifts, row0, n, event_major, ebits=None, nnz=None):
+    def build(cls, E, shifts, row0, n, event_major, ebits=None, nnz=None, n_raw=None):
+        """E: the events (N_raw x m, device), or None with ``ebits`` (bit rows) and ``n_raw``."""
         self = cls()
-        dev = E.device
-        N_raw, m = E.shape
+        if E is None:
+            dev = ebits.device
+            N_raw, m = int(n_raw), int(ebits.shape[0])
+            occ_src = _unpack_bits(ebits, N_raw)                       # (m, N_raw) uint8
+        else:
+            dev = E.device
+            N_raw, m = E.shape
+            occ_src = E.t()
         sh = np.asarray(shifts, dtype=np.int64)
         self.m, self.K = int(m), int(sh.size)
         self.layout = 1 if event_major else 0
@@ -843,8 +910,8 @@ class LagStructure:
         self.shifts = torch.from_numpy(sh.astype(np.int32)).to(dev)
         # (event, row) of every occurrence, event-major; a known count sizes it without
         # waiting for the device
-        nz = (torch.nonzero(E.t() != 0) if nnz is None
-              else torch.nonzero_static(E.t() != 0, size=int(nnz)))
+        nz = (torch.nonzero(occ_src != 0) if nnz is None
+              else torch.nonzero_static(occ_src != 0, size=int(nnz)))
         ev, rows = nz[:, 0], nz[:, 1]
         self.occ = rows.to(torch.int32).contiguous()
         U = _lib.query("sglm_lag_tile_rows")
@@ -869,7 +936,7 @@ class LagStructure:
                                  torch.cumsum(cnt, 0)]).to(torch.int32).contiguous()
         self.nwords = (int(N_raw) + 31) // 32
         if ebits is None:
-            Eb = E.t().contiguous().to(torch.bfloat16)
+            Eb = occ_src.contiguous().to(torch.bfloat16)
             ebits = torch.empty((m, self.nwords), dtype=torch.int32, device=dev)
             _lib.call("sglm_event_bits", _p(Eb), int(N_raw), int(m), int(N_raw), _p(ebits),
                       self.nwords, _stream())

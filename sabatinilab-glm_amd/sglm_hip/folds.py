@@ -112,6 +112,83 @@ def cv_idx_from_bucket_ids(bucket_ids, X=None, y=None, num_folds=None, test_size
     return group_shuffle_split(bucket_ids, num_folds, test_size)
 
 
+def trial_key_runs(df, id_cols, package_style=False):
+    """(code per run, run starts, run lengths) of the trial-key codes of ``trial_keys_codes``
+    when the key is ONE numeric id column whose values never decrease (trial counters: each
+    distinct value is one run of rows), else None.  The codes are the same ranks of the same
+    key strings, kept per run instead of expanded per row."""
+    if len(id_cols) != 1:
+        return None
+    c = df[id_cols[0]]
+    if not (isinstance(c.dtype, np.dtype) and c.dtype.kind in "biuf"):
+        return None
+    v = c.to_numpy()
+    if v.size < 2 or not bool(np.all(v[1:] >= v[:-1])):
+        return None
+    chg = np.empty(v.size, dtype=bool)
+    chg[0] = True
+    np.not_equal(v[1:], v[:-1], out=chg[1:])
+    at = np.flatnonzero(chg)
+    u = v[at]
+    if c.dtype in (np.float64, np.int64):
+        strs = [str(x) for x in u.tolist()]
+    else:
+        su = pd_series(u, c.dtype)
+        strs = list(su.apply(str) if package_style else su.astype(str))
+    keys = [f"{len(sv)}:{sv}" for sv in strs]
+    if len(set(keys)) != len(keys):
+        return None
+    order = np.argsort(np.asarray(keys, dtype=object), kind="stable")
+    rank = np.empty(len(keys), dtype=np.int64)
+    rank[order] = np.arange(len(keys))
+    return rank, at.astype(np.int64), np.diff(at, append=v.size).astype(np.int64)
+
+
+def pd_series(values, dtype):
+    import pandas as pd
+    return pd.Series(values, dtype=dtype)
+
+
+def cv_idx_from_runs(rank, starts, lens, num_folds, test_size=None, random_state=None):
+    """cv_idx_from_bucket_ids for groups given as runs (trial_key_runs): the same
+    GroupShuffleSplit permutations of the dense codes 0 .. G-1 (every run is its own group), the
+    row lists written run by run by native threads (sglm_host_group_runs)."""
+    import ctypes
+    from . import _lib
+    from .engine import HOST_THREADS
+    if random_state is None:
+        rng = np.random.mtrand._rand
+    elif isinstance(random_state, np.random.RandomState):
+        rng = random_state
+    else:
+        rng = np.random.RandomState(random_state)
+    G = int(rank.size)
+    if test_size is None:
+        test_size = 1 / num_folds
+    n_train, n_test = _validate(G, test_size)
+    S = int(num_folds)
+    side = np.zeros((max(S, 1), G), dtype=np.uint8)
+    for k in range(S):
+        perm = rng.permutation(G)
+        side[k, perm[n_test:n_test + n_train]] = 1
+        side[k, perm[:n_test]] = 2
+    side = np.ascontiguousarray(side[:S])
+    if S == 0:
+        return []
+    sr = side[:, rank]                                   # [S][runs]: the side of each run
+    lens_l = np.stack([(lens[None, :] * (sr == 1)).sum(1), (lens[None, :] * (sr == 2)).sum(1)],
+                      1).reshape(-1).astype(np.int64)
+    outs = [np.empty(int(L), dtype=np.int64) for L in lens_l]
+    ptrs = (ctypes.c_void_p * len(outs))(*[o.ctypes.data for o in outs])
+    rank = np.ascontiguousarray(rank, dtype=np.int64)
+    starts = np.ascontiguousarray(starts, dtype=np.int64)
+    lens = np.ascontiguousarray(lens, dtype=np.int64)
+    _lib.call("sglm_host_group_runs", starts.ctypes.data, lens.ctypes.data, rank.ctypes.data,
+              int(rank.size), side.ctypes.data, S, G, ctypes.cast(ptrs, ctypes.c_void_p),
+              lens_l.ctypes.data, HOST_THREADS)
+    return [(outs[2 * k], outs[2 * k + 1]) for k in range(S)]
+
+
 def trial_keys_codes(df, id_cols, package_style=False):
     """Categorical codes of the trial keys (backend/sglm_ez.py:334-340; package
     sglm/sglm/models/split_data.py:146-152 when ``package_style``).

@@ -65,90 +65,113 @@ class LagSource:
         self.N = len(base)
         self._dev = {}           # column name -> row of self._E
         self._E = None
+        self._bits = {}          # 0/1 column name -> its device bit row (int32 [ceil(N / 32)])
         self._hasnan = {}        # column name -> holds a NaN cell
         self._ones = {}          # 0/1 column name -> its count of 1 cells (host pack)
         self._numeric = {}       # column name -> numeric dtype
         self.cast = {}           # base column name -> dtype of its shift-0 copy in the frame
         self.all_rows = None     # arange(N), built once
 
-    def device(self, names):
-        """Device float64 [rows][N] holding the named base columns (uploaded once, NaN kept),
-        and the device int64 row index of each name."""
+    def upload(self, names):
+        """Upload the named base columns once: a 0/1 column as its device bit row (crossing
+        PCIe as 1 bit per row, sglm_host_pack_bits_cols; kept packed -- the lag design's bit
+        planes and event occurrences are built from it), any other column as a float64 row of
+        the device source block (NaN kept)."""
         import ctypes
         import torch
         from .engine import HOST_THREADS, _pinned, _scratch, require_gpu
         require_gpu()
-        need = [c for c in dict.fromkeys(names) if c not in self._dev]
-        if need:
-            N, m = self.N, len(need)
-            new = torch.empty((m, N), dtype=torch.float64, device="cuda")
-            arrs = [self._f64(c) for c in need]
-            # 0/1 columns cross PCIe as bit-planes (sglm_host_pack_bits_cols), the rest as
-            # float64 through the pinned stages below
-            nw = (N + 31) // 32
-            bits = _pinned("lagbits", max(1, m * nw), torch.int32)
-            evk = ("lagbits_ev", None)
-            if _scratch().pinned.get(evk) is not None:
-                _scratch().pinned[evk].synchronize()      # the last upload has read the stage
-            binary = np.zeros(m, dtype=np.uint8)
-            ones = np.zeros(m, dtype=np.int64)
-            ptrs = (ctypes.c_void_p * m)(*[a.ctypes.data for a in arrs])
-            strides = np.array([a.strides[0] // 8 for a in arrs], dtype=np.int64)
-            _lib.call("sglm_host_pack_bits_cols", ctypes.cast(ptrs, ctypes.c_void_p),
-                      strides.ctypes.data, m, N, bits.data_ptr(), binary.ctypes.data,
-                      ones.ctypes.data, HOST_THREADS)
-            bsel = np.flatnonzero(binary)
-            for i in bsel:
+        need = [c for c in dict.fromkeys(names) if c not in self._dev and c not in self._bits]
+        if not need:
+            return
+        N, m = self.N, len(need)
+        arrs = [self._f64(c) for c in need]
+        nw = (N + 31) // 32
+        bits = _pinned("lagbits", max(1, m * nw), torch.int32)
+        evk = ("lagbits_ev", None)
+        if _scratch().pinned.get(evk) is not None:
+            _scratch().pinned[evk].synchronize()      # the last upload has read the stage
+        binary = np.zeros(m, dtype=np.uint8)
+        ones = np.zeros(m, dtype=np.int64)
+        ptrs = (ctypes.c_void_p * m)(*[a.ctypes.data for a in arrs])
+        strides = np.array([a.strides[0] // 8 for a in arrs], dtype=np.int64)
+        _lib.call("sglm_host_pack_bits_cols", ctypes.cast(ptrs, ctypes.c_void_p),
+                  strides.ctypes.data, m, N, bits.data_ptr(), binary.ctypes.data,
+                  ones.ctypes.data, HOST_THREADS)
+        bsel = np.flatnonzero(binary)
+        if bsel.size:
+            # the 0/1 columns' bit rows, one asynchronous copy out of the pinned stage
+            bd = bits[: m * nw].view(m, nw)
+            bd = (bd if bsel.size == m else bd[torch.from_numpy(bsel)]).to("cuda",
+                                                                           non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            _scratch().pinned[evk] = ev
+            for q, i in enumerate(bsel):
+                self._bits[need[i]] = bd[q]
                 self._ones[need[i]] = int(ones[i])
-            if bsel.size:
-                # all 0/1 (an event frame): the pinned stage goes up as it is, asynchronously
-                every = bsel.size == m
-                bd = bits[: m * nw].view(m, nw)
-                bd = (bd if every else bd[torch.from_numpy(bsel)]).to("cuda", non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record()
-                _scratch().pinned[evk] = ev
-                sh = torch.arange(32, dtype=torch.int32, device="cuda")
-                unp = ((bd.unsqueeze(-1) >> sh) & 1).reshape(bsel.size, nw * 32)[:, :N]
-                if every:
-                    new = unp.to(torch.float64)
-                else:
-                    new[torch.from_numpy(bsel).to("cuda")] = unp.to(torch.float64)
-            raw = np.flatnonzero(binary == 0)
-            need_raw = [need[i] for i in raw]
-            arr_raw = [arrs[i] for i in raw]
-            # column groups of <= 64 MB through two pinned stages: the threaded host gather of
-            # group g + 1 overlaps the DMA of group g
-            per = max(1, (64 << 20) // max(1, 8 * N))
-            stages = [_pinned(f"lagsrc{i}", max(1, per * N), torch.float64) for i in range(2)]
-            evs = [None, None]
-            dst_rows = torch.from_numpy(raw).to("cuda") if raw.size else None
-            for g, c0 in enumerate(range(0, len(need_raw), per)):
-                grp = arr_raw[c0:c0 + per]
-                b = g % 2
-                if evs[b] is not None:
-                    evs[b].synchronize()
-                ptrs = (ctypes.c_void_p * len(grp))(*[a.ctypes.data for a in grp])
-                strides = np.array([a.strides[0] // 8 for a in grp], dtype=np.int64)
-                _lib.call("sglm_host_gather_cols", ctypes.cast(ptrs, ctypes.c_void_p),
-                          strides.ctypes.data, len(grp), N, 8, stages[b].data_ptr(),
-                          HOST_THREADS)
-                tmp = stages[b][: len(grp) * N].view(len(grp), N).to("cuda", non_blocking=True)
-                new[dst_rows[c0:c0 + len(grp)]] = tmp
-                ev = torch.cuda.Event()
-                ev.record()
-                evs[b] = ev
-            for ev in evs:
-                if ev is not None:
-                    ev.synchronize()
-            base = 0 if self._E is None else self._E.shape[0]
-            self._E = new if self._E is None else torch.cat([self._E, new])
-            # 0/1 columns hold no NaN: only raw columns are checked on the device
-            has = (torch.isnan(new).any(1).cpu().numpy() if raw.size
-                   else np.zeros(m, dtype=bool))
-            for i, c in enumerate(need):
-                self._dev[c] = base + i
-                self._hasnan[c] = bool(has[i])
+                self._hasnan[need[i]] = False
+        raw = np.flatnonzero(binary == 0)
+        if not raw.size:
+            return
+        need_raw = [need[i] for i in raw]
+        arr_raw = [arrs[i] for i in raw]
+        new = torch.empty((len(need_raw), N), dtype=torch.float64, device="cuda")
+        # column groups of <= 64 MB through two pinned stages: the threaded host gather of
+        # group g + 1 overlaps the DMA of group g
+        per = max(1, (64 << 20) // max(1, 8 * N))
+        stages = [_pinned(f"lagsrc{i}", max(1, per * N), torch.float64) for i in range(2)]
+        evs = [None, None]
+        for g, c0 in enumerate(range(0, len(need_raw), per)):
+            grp = arr_raw[c0:c0 + per]
+            b = g % 2
+            if evs[b] is not None:
+                evs[b].synchronize()
+            ptrs = (ctypes.c_void_p * len(grp))(*[a.ctypes.data for a in grp])
+            strides = np.array([a.strides[0] // 8 for a in grp], dtype=np.int64)
+            _lib.call("sglm_host_gather_cols", ctypes.cast(ptrs, ctypes.c_void_p),
+                      strides.ctypes.data, len(grp), N, 8, stages[b].data_ptr(), HOST_THREADS)
+            new[c0:c0 + len(grp)] = stages[b][: len(grp) * N].view(len(grp), N).to(
+                "cuda", non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            evs[b] = ev
+        for ev in evs:
+            if ev is not None:
+                ev.synchronize()
+        self._append_rows(need_raw, new)
+        has = torch.isnan(new).any(1).cpu().numpy()
+        for i, c in enumerate(need_raw):
+            self._hasnan[c] = bool(has[i])
+
+    def _append_rows(self, names, new):
+        import torch
+        base = 0 if self._E is None else self._E.shape[0]
+        self._E = new if self._E is None else torch.cat([self._E, new])
+        for i, c in enumerate(names):
+            self._dev[c] = base + i
+
+    def bits(self, names):
+        """Device int32 [len(names)][ceil(N / 32)] bit rows of the named columns when every one
+        of them is 0/1 (bit r & 31 of word r >> 5 = row r), else None."""
+        import torch
+        self.upload(names)
+        if not all(c in self._bits for c in names):
+            return None
+        return torch.stack([self._bits[c] for c in names])
+
+    def device(self, names):
+        """Device float64 [rows][N] holding the named base columns (uploaded once, NaN kept;
+        0/1 columns unpacked from their bit rows on first use here), and the device int64 row
+        index of each name."""
+        import torch
+        self.upload(names)
+        lazy = [c for c in dict.fromkeys(names) if c not in self._dev]
+        if lazy:
+            B = torch.stack([self._bits[c] for c in lazy])
+            sh = torch.arange(32, dtype=torch.int32, device="cuda")
+            unp = ((B.unsqueeze(-1) >> sh) & 1).reshape(len(lazy), -1)[:, :self.N]
+            self._append_rows(lazy, unp.to(torch.float64))
         rows = [self._dev[c] for c in names]
         if rows and rows == list(range(rows[0], rows[0] + len(rows))):
             # consecutive rows (names in upload order): no host->device copy to wait on
@@ -472,7 +495,7 @@ class LagFrame:
         if a - max(max(sh), 0) < 0 or b - 1 - min(min(sh), 0) > self._src.N - 1:
             return bool(self.nan_counts().any())
         names = sorted({sc[0] for sc in specs}, key=str)
-        self._src.device(names)
+        self._src.upload(names)
         if any(self._src.has_nan(nm) for nm in names):
             return bool(self.nan_counts().any())
         return False
@@ -505,7 +528,7 @@ class LagFrame:
             le = cw[np.searchsorted(sh, u - N, side="right")]
             out[edge] = gt + le
         names = sorted({nm for v in lag.values() for nm in v}, key=str)
-        self._src.device(names)
+        self._src.upload(names)
         if not any(self._src.has_nan(nm) for nm in names):
             return out
         E, idx = self._src.device(names)
@@ -636,19 +659,31 @@ class LagFrame:
             raise ValueError("Input X contains NaN.")
         srcs = [self._spec[c][0] for c in self._cols]
         names = sorted(set(srcs), key=str)
-        E, idx = self._src.device(names)
-        Esub = E[idx]
-        if any(self._src.has_nan(nm) for nm in names):
-            Esub = Esub.nan_to_num(0.0)        # NaN source cells are never read (checked above)
         at = {nm: i for i, nm in enumerate(names)}
         cols = np.array([at[x] for x in srcs], dtype=np.int64)
         shifts = np.array([self._spec[c][1] for c in self._cols], dtype=np.int64)
         pos = self.positions()
         n = int(pos.size)
         sp = self._span()
+        contiguous = n and (sp is not None or (pos[-1] - pos[0] == n - 1
+                                               and np.all(np.diff(pos) == 1)))
+        if contiguous:
+            # every source 0/1 and the canonical lag layout: the design straight from the
+            # uploaded bit rows (no float64 copy of the sources)
+            B = self._src.bits(names)
+            if B is not None:
+                ones = np.array([self._src.ones(nm) for nm in names], dtype=np.int64)
+                d = Design.from_lagged_bits(B, self._src.N, cols, shifts, int(pos[0]), n, ones)
+                if d is not None:
+                    self._design = d
+                    return d
+        E, idx = self._src.device(names)
+        Esub = E[idx]
+        if any(self._src.has_nan(nm) for nm in names):
+            Esub = Esub.nan_to_num(0.0)        # NaN source cells are never read (checked above)
         ones = [self._src.ones(nm) for nm in names]
         ones = None if any(o is None for o in ones) else ones
-        if n and (sp is not None or (pos[-1] - pos[0] == n - 1 and np.all(np.diff(pos) == 1))):
+        if contiguous:
             d = Design.from_lagged(Esub, cols, shifts, int(pos[0]), n, ones=ones)
         else:
             import torch

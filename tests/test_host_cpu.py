@@ -52,6 +52,16 @@ def test_product_folds_bit_exact_vs_sklearn(golden):
                           g["codes_two_backend"])
     assert np.array_equal(folds.trial_keys_codes(df, ["nTrial", "iBlock"], package_style=True).values,
                           g["codes_two_package"])
+    # the drop-in entry on a sorted trial column takes the run-based path (trial_key_runs ->
+    # cv_idx_from_runs, native sglm_host_group_runs): the same sklearn folds
+    import sglm_ez
+    assert folds.trial_key_runs(df, ["nTrial"]) is not None
+    for seed in (0, 3, 17):
+        np.random.seed(seed)
+        for k, (tr, te) in enumerate(sglm_ez.cv_idx_by_trial_id(df, trial_id_columns=["nTrial"],
+                                                                 num_folds=5)):
+            assert np.array_equal(tr, g[f"f{seed}_k{k}_train"])
+            assert np.array_equal(te, g[f"f{seed}_k{k}_test"])
     np.random.seed(5)
     sp = folds.cv_idx_from_bucket_ids(folds.bucket_ids_by_timeframe(437, 20))
     assert len(sp) == int(g["tf_nsplits"])
