@@ -58,6 +58,8 @@ XTR_BITS = True                # X^T R on the MFMA from compacted bit-planes for
 # X^T R of a time-shifted 0/1 event design (Design.from_events) from the event occurrences
 LAG_XTR = __import__("os").environ.get("SGLM_LAG_XTR", "0") == "1"
 ETA_BITS = True                # eta on the MFMA from row-major bit-planes for 0/1 designs
+ETA_FINAL_ALL = False          # recompute every fit's final eta (else only ETA_FINAL_ITERS+)
+ETA_FINAL_ITERS = 8
 SYRK_CBITS = True              # ... and its row-compacted register-only form (v6) when fits
                                # carry masks (the default path for event designs)
 # Hessian reuse (log-link families): a fit keeps its last Hessian factor while the drift of
@@ -2215,6 +2217,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
         sc_h.copy_(sc, non_blocking=True)
         if use_aa:
             aa_rm_h.copy_(aa_rm.view(-1), non_blocking=True)
+            aa_used[aa_idx] = bf.delta[aa_idx]       # the rounded directions the step uses
         t_sync = time.perf_counter()
         torch.cuda.current_stream().synchronize()              # the iteration's round trip
         if stats is not None:
@@ -2232,8 +2235,6 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
         def objectives(Lm, tv):
             return Lm + 0.5 * (A_[:, None] + 2 * tv[None, :] * B_[:, None]
                                + tv[None, :] ** 2 * C_[:, None])
-        if use_aa:
-            aa_used[aa_idx] = bf.delta[aa_idx]       # the rounded directions the step uses
         step_a = np.zeros(na)
         tix = np.zeros(na, dtype=np.int64)      # index of the chosen step in TS_ALL
         obj = objectives(L, ts)
@@ -2266,26 +2267,9 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
             step_a[more[h2]] = ts2[f2[h2]]
             tix[more[h2]] = 5 + f2[h2]
         t0 = tick("it_linesearch", t0)
-        # ---- update (coefficients on the device: w += t d), launched below with the
-        # predictor update once the stopping decisions are made (one upload for all of them)
-        if not const_hess:
-            drift[act] += step_a * dmaxeta            # max_i |t d_eta_i| over the fit's rows
-        fresh_start[act[step_a != 0.0]] = False
-        aa_t[act] = step_a
-        n_iter[act] += 1
-        if stats is not None:
-            stats.newton_iters += 1
-            stats.fit_iters += na
-            # SURVEY.md §8(d) F per fit-iteration, charged for work actually done: the Gram
-            # term only where a Gram was computed (not for a Hessian shared from another fit),
-            # the factorisation where a new factor was formed (a kept or aliased factor costs
-            # the two triangular solves only)
-            pa = float(p + 1)
-            nr = rows[act]
-            stats.alg_flop += float(np.sum(np.where(gram_comp[act], nr * pa * (pa + 1), 0.0)
-                                           + np.where(gram_now[act], pa ** 3 / 3, 0.0)
-                                           + 4.0 * nr * pa + 2 * pa * pa))
-            stats.gram_fit_iters += int(np.sum(gram_comp[act]))
+        # ---- stopping decisions first (they need only this iteration's readback), so the
+        # coefficient / predictor update and the next link go to the GPU before the host's
+        # remaining bookkeeping (drift, sharing / aliasing flags, statistics, the next plan)
         # the step is measured against the coefficients' own scale (max|w_j| over j < p after
         # the step, the intercept excluded), floored at STOP_SCALE_FLOOR: the parity tests
         # measure errors relative to max|coef|, so a fit with small coefficients (strong
@@ -2308,20 +2292,6 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
         stepa = step_a
         fresh = (gram_now[act] & exact_h[act]) | const_hess
         ls_fail = stepa == 0.0
-        # a failed line search on a kept (stale) factor, or on a Hessian shared from a lambda
-        # neighbour, is not a verdict: the next iteration forms a fresh Hessian of the fit's
-        # own instead of stopping it
-        if not const_hess:
-            drift[act[ls_fail & ~fresh]] = np.inf
-            no_share[act[ls_fail & gram_now[act] & ~exact_h[act]]] = True
-            # a fit whose step on the representative's factor failed, or contracted slowly,
-            # forms its own Hessians from here on
-            was_alias = alias[act] >= 0
-            slow = was_alias & (relv > XMASK_SLOW * prev_rel[act]) & (relv > tol)
-            drop = was_alias & (ls_fail | slow)
-            no_alias[act[drop]] = True
-            if stats is not None:
-                stats.stops["alias_dropped"] += int(np.sum(drop))
         stop_tol = ~ls_fail & (relv <= tol)
         # stagnation (the f32 noise floor): a step no better than half the previous one, judged
         # only on steps taken with a fresh Hessian -- a kept factor contracts by up to
@@ -2334,35 +2304,16 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
         stop_fail = ls_fail & fresh
         stop = stop_tol | stop_stag | stop_fail
         conv_now = stop_tol | (stop_fail & (prop <= tol))
-        active[act[stop]] = False
-        converged[act[stop]] = conv_now[stop]
+        n_iter[act] += 1
         out_of_iters = ~stop & (n_iter[act] >= max_iter[act])
-        active[act[out_of_iters]] = False
-        if stats is not None and stats.iter_log is not None:
-            stats.iter_log.append(dict(
-                it=it, active=int(na), keep=int(0 if const_hess else keep.size),
-                alias=int(0 if const_hess else ali.size), form=int(nref if not dist_f else -1),
-                grams=int(gram_comp.sum()), stop_tol=int(stop_tol.sum()),
-                ls_fail=int(ls_fail.sum()), step1=int(np.sum(step_a == 1.0)),
-                rel_max=float(relv.max()), rel_med=float(np.median(relv)),
-                lam_active=[float(lam[k]) for k in act[~stop]][:40],
-                rate=[float(x) for x in (relv / np.maximum(prev_rel[act], 1e-300))[~stop]][:40]))
-        prev_rel[act] = relv
-        if stats is not None:
-            stats.stops["tol"] += int(np.sum(stop_tol))
-            stats.stops["stagnation"] += int(np.sum(stop_stag))
-            stats.stops["line_search_converged"] += int(np.sum(stop_fail & (prop <= tol)))
-            stats.stops["line_search_failed"] += int(np.sum(stop_fail & (prop > tol)))
-            stats.stops["max_iter"] += int(np.sum(out_of_iters))
-            stats.stops["stale_factor_retry"] += int(np.sum(ls_fail & ~fresh))
+        cont = ~stop & ~out_of_iters
+        nxt = act[cont]
         # predictor update eta += t d_eta: fused into the next iteration's link for the fits
         # that continue (0/1 designs), a plain axpy for the others
         linked = None
-        nxt = np.flatnonzero(active)
         up.batch()
         step_d = up(step_a, np.float64)
         if fused and nxt.size:
-            cont = active[act]
             done = np.flatnonzero(~cont & (step_a != 0.0))
             if done.size:
                 done_d, tdone_d = up(act[done], np.int32), up(step_a[done], np.float32)
@@ -2384,6 +2335,58 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
                       _p(beta64_d), st)
             _lib.call("sglm_eta_axpy", n, ld, na, _p(act_d), _p(t32_d), _p(bf.deta),
                       _p(bf.eta), st)
+        # ---- bookkeeping of this iteration (overlaps the update on the GPU)
+        if not const_hess:
+            drift[act] += step_a * dmaxeta            # max_i |t d_eta_i| over the fit's rows
+        fresh_start[act[step_a != 0.0]] = False
+        aa_t[act] = step_a
+        if stats is not None:
+            stats.newton_iters += 1
+            stats.fit_iters += na
+            # SURVEY.md §8(d) F per fit-iteration, charged for work actually done: the Gram
+            # term only where a Gram was computed (not for a Hessian shared from another fit),
+            # the factorisation where a new factor was formed (a kept or aliased factor costs
+            # the two triangular solves only)
+            pa = float(p + 1)
+            nr = rows[act]
+            stats.alg_flop += float(np.sum(np.where(gram_comp[act], nr * pa * (pa + 1), 0.0)
+                                           + np.where(gram_now[act], pa ** 3 / 3, 0.0)
+                                           + 4.0 * nr * pa + 2 * pa * pa))
+            stats.gram_fit_iters += int(np.sum(gram_comp[act]))
+        # a failed line search on a kept (stale) factor, or on a Hessian shared from a lambda
+        # neighbour, is not a verdict: the next iteration forms a fresh Hessian of the fit's
+        # own instead of stopping it
+        if not const_hess:
+            drift[act[ls_fail & ~fresh]] = np.inf
+            no_share[act[ls_fail & gram_now[act] & ~exact_h[act]]] = True
+            # a fit whose step on the representative's factor failed, or contracted slowly,
+            # forms its own Hessians from here on
+            was_alias = alias[act] >= 0
+            slow = was_alias & (relv > XMASK_SLOW * prev_rel[act]) & (relv > tol)
+            drop = was_alias & (ls_fail | slow)
+            no_alias[act[drop]] = True
+            if stats is not None:
+                stats.stops["alias_dropped"] += int(np.sum(drop))
+        active[act[stop]] = False
+        converged[act[stop]] = conv_now[stop]
+        active[act[out_of_iters]] = False
+        if stats is not None and stats.iter_log is not None:
+            stats.iter_log.append(dict(
+                it=it, active=int(na), keep=int(0 if const_hess else keep.size),
+                alias=int(0 if const_hess else ali.size), form=int(nref if not dist_f else -1),
+                grams=int(gram_comp.sum()), stop_tol=int(stop_tol.sum()),
+                ls_fail=int(ls_fail.sum()), step1=int(np.sum(step_a == 1.0)),
+                rel_max=float(relv.max()), rel_med=float(np.median(relv)),
+                lam_active=[float(lam[k]) for k in act[~stop]][:40],
+                rate=[float(x) for x in (relv / np.maximum(prev_rel[act], 1e-300))[~stop]][:40]))
+        prev_rel[act] = relv
+        if stats is not None:
+            stats.stops["tol"] += int(np.sum(stop_tol))
+            stats.stops["stagnation"] += int(np.sum(stop_stag))
+            stats.stops["line_search_converged"] += int(np.sum(stop_fail & (prop <= tol)))
+            stats.stops["line_search_failed"] += int(np.sum(stop_fail & (prop > tol)))
+            stats.stops["max_iter"] += int(np.sum(out_of_iters))
+            stats.stops["stale_factor_retry"] += int(np.sum(ls_fail & ~fresh))
         if not const_hess and nxt.size:
             # the next iteration's Hessian decisions and their distances, enqueued behind
             # this iteration's predictor update (read back without a stall next iteration)
@@ -2392,13 +2395,21 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
 
     # unpenalised fits: the minimum-norm point of the solution set (lstsq's answer on a
     # rank-deficient design; the fitted values on the fit's rows are unchanged)
+    pf = np.zeros(0, dtype=np.int64)
     if f64 is not None:
         pf = np.flatnonzero(lam0 & (fkey >= 0))
         f64.minnorm(d, bf, pf, fkey[pf], beta64_d, st)
-    # final linear predictor from the final coefficients, in request order (no accumulated
-    # drift), enqueued before the readbacks so the host's one wait covers it
+    # final linear predictor from the final coefficients, enqueued before the readbacks so
+    # the host's one wait covers it.  The loop keeps eta = X beta up to one f32 rounding per
+    # step, so only fits whose beta moved without eta (the minimum-norm projection) or that
+    # took many steps are recomputed (the full pass costs ~1.2 ms on a 120-fit grid)
     bf.beta[:B0].copy_(beta64_d)
-    d.eta(bf.beta, bf.eta)
+    if ETA_FINAL_ALL or d.rbits is None or not ETA_BITS:
+        d.eta(bf.beta, bf.eta)
+    else:
+        ref = np.union1d(pf, np.flatnonzero(n_iter > ETA_FINAL_ITERS))
+        if ref.size:
+            d.eta(bf.beta, bf.eta, slots=torch.from_numpy(ref.astype(np.int32)).to(dev))
     out_iter[:] = n_iter
     out_conv[:] = converged
     if dist_f:

@@ -177,3 +177,43 @@ def test_production_flow_resident_equals_host_path_c3(engine):
     assert rel(glm_a.coef_, glm_b.coef_) < 1e-5
     assert abs(hs_a - hs_b) < 1e-6 and abs(hm_a - hm_b) < 1e-6 * max(1.0, abs(hm_b))
     assert rel(pred_a, pred_b) < 1e-5
+
+
+def test_lagframe_snapshot_and_uploads(engine):
+    """The lagged frame takes the caller's columns when it is made: a column assignment, a
+    column drop and an in-place row drop of the caller's frame afterwards change nothing (the
+    reference's timeshift_multiple returns a copy); source columns uploaded by separate calls
+    (0/1 ones as bit rows, a real one as float64, one of them a second time) give the host
+    values; the occurrence list sized by the host counts equals the one sized on the device."""
+    import torch
+    import sglm_ez
+    import sglm_pp
+    from sglm_hip import engine as E
+    df = _frame(N=2500, seed=5, nan_rows=())
+    cols = ["ev0", "ev1", "ev2", "sig"]
+    sglm_pp.LAGFRAME = False
+    try:
+        ref = sglm_ez.timeshift_cols(df.copy(), cols, neg_order=-2, pos_order=2)
+    finally:
+        sglm_pp.LAGFRAME = True
+    lf = sglm_ez.timeshift_cols(df, cols, neg_order=-2, pos_order=2)
+    df["ev0"] = 7.0                              # assignment replaces the caller's column
+    df.drop(columns=["sig"], inplace=True)
+    df.drop(index=df.index[:300], inplace=True)  # shorter than the frame's row count
+    pd.testing.assert_frame_equal(lf.to_pandas(), ref)
+    src = lf._src
+    # uploads in two calls: 0/1 columns first, then a real column with one repeated name
+    src.upload(["ev2", "ev0"])
+    src.upload(["sig", "ev2"])
+    assert src.bits(["ev0", "ev2"]) is not None and src.bits(["sig"]) is None
+    Ed, idx = src.device(["ev0", "sig", "ev2"])
+    got = Ed[idx].cpu().numpy()
+    exp = np.stack([ref["ev0"].to_numpy(), ref["sig"].to_numpy(), ref["ev2"].to_numpy()])
+    assert np.array_equal(got, exp, equal_nan=True)
+    # the occurrence list: sized from the host pack's counts == sized on the device
+    B = src.bits(["ev0", "ev1", "ev2"])
+    ones = sum(src.ones(c) for c in ("ev0", "ev1", "ev2"))
+    a = E.LagStructure.build(None, [0, 1, -1], 1, 2400, False, ebits=B, nnz=ones, n_raw=2500)
+    b = E.LagStructure.build(None, [0, 1, -1], 1, 2400, False, ebits=B, nnz=None, n_raw=2500)
+    assert torch.equal(a.occ, b.occ) and torch.equal(a.tbeg, b.tbeg)
+    assert torch.equal(a.tend, b.tend)
