@@ -624,9 +624,11 @@ int sglm_mixed_to_h(const double* S, int32_t ns, int32_t k, int32_t P, const int
  * sglm_group_rows: perm[0 .. m) = the rows whose key (and key2, when not NULL) is not NaN,
  *   grouped by key value (lexicographic (key, key2)), row order kept within a group (pandas'
  *   group and within-group order; NaN-key rows are dropped as groupby drops them);
- *   seg[0 .. nseg] = group starts in perm plus m; counts = {m, nseg} (device int64).  The
- *   ordering check synchronises the stream once; *sorted_out (host, may be NULL) reports
- *   whether the keys were already ordered (stable partition) or were radix-sorted.  n < 2^31.
+ *   seg[0 .. nseg] = group starts in perm plus m; counts = {m, nseg, ordered} (device int64,
+ *   3 entries).  Ordered keys (non-decreasing over the valid rows) take a stable compaction,
+ *   others a stable LSD radix sort; both paths are enqueued and the device picks one, so the
+ *   call never waits on the host -- unless sorted_out (host, may be NULL) asks for the verdict,
+ *   which costs one stream synchronisation.  work: sglm_group_rows_work_bytes(n).  n < 2^31.
  *   Replaces groupby('nTrial') / groupby(['nTrial', 'nENL']) (:52, 114-120, 171-175, 200).
  * sglm_trial_lookup: tidx[i] = position of key[i] in the ascending, unique trial ids tkeys,
  *   -1 when NaN or absent -- Series.map(trials[...]) (:93, 112, 123, 192).
@@ -645,9 +647,14 @@ int sglm_mixed_to_h(const double* S, int32_t ns, int32_t k, int32_t P, const int
  * sglm_dm_pull: pull_lick_from_bout (:26-58) for positions nth[0 .. npull) in processing order:
  *   cols[j] = 1 on the (nth - 1)-th (negative: from the end) bout == 1 row of each group, that
  *   bout row set to 0.  npull <= 16; nth and cols are host arrays.
+ * sglm_dm_heatmap_k / sglm_dm_counters_k / sglm_dm_pull_k: the same with the grouping keys
+ *   (key = nTrial, key2 = nENL of the second grouping): the per-row default pass then writes only
+ *   the rows outside the groups (the group walks write every row of a group), a second write
+ *   of the whole column saved.  NULL keys: the entries above.
  * sglm_trial_map: dst[dst_cols[c]][i] = (src_cols[c] < 0 ? 1 : src[src_cols[c]][i]) *
  *   vals[val_cols[c]][tidx[i]] (NaN when tidx[i] < 0): event_interactions_dummies (:87-99)
- *   and the flag's mapped isna (:192).  Index arrays on the device.
+ *   and the flag's mapped isna (:192).  Index arrays on the device.  sglm_trial_map_u8: the same
+ *   with a uint8 value table (0/1 dummy products and isna flags: exact, 1/8 of the upload).
  * sglm_zero_groups_flag: flag = 1 on every row of the groups whose listed columns sum to 0
  *   (skipna) -- the trials without a cue dummy (:198-203); group_zero (may be NULL, >= nseg
  *   bytes) gets 1 for those groups (the printed trials_without_dummies, :201-202). */
@@ -671,10 +678,26 @@ int sglm_dm_counters(const double* enl, const double* cue, const double* senlp, 
 int sglm_dm_pull(double* bout, int64_t n, const int64_t* perm, const int64_t* seg,
                  const int64_t* counts, const int32_t* nth, int32_t npull, double* const* cols,
                  sglm_stream_t stream);
+int sglm_dm_heatmap_k(const double* clock, const double* cue, const double* cons,
+                      const double* scons, const double* key, int64_t n, const int64_t* perm,
+                      const int64_t* seg, const int64_t* counts, const int32_t* tidx,
+                      const double* tsel, double* out, int64_t ld_out, sglm_stream_t stream);
+int sglm_dm_counters_k(const double* enl, const double* cue, const double* senlp,
+                       const double* key, const double* key2, int64_t n, const int64_t* perm,
+                       const int64_t* seg, const int64_t* counts, const int64_t* perm2,
+                       const int64_t* seg2, const int64_t* counts2, double* tenl, double* tenlp,
+                       double* cue_on, sglm_stream_t stream);
+int sglm_dm_pull_k(double* bout, const double* key, int64_t n, const int64_t* perm,
+                   const int64_t* seg, const int64_t* counts, const int32_t* nth, int32_t npull,
+                   double* const* cols, sglm_stream_t stream);
 int sglm_trial_map(int64_t n, const int32_t* tidx, const double* src, int64_t ld_src,
                    const int32_t* src_cols, const double* vals, int64_t nt,
                    const int32_t* val_cols, int32_t ncols, double* dst, int64_t ld_dst,
                    const int32_t* dst_cols, sglm_stream_t stream);
+int sglm_trial_map_u8(int64_t n, const int32_t* tidx, const double* src, int64_t ld_src,
+                      const int32_t* src_cols, const uint8_t* vals, int64_t nt,
+                      const int32_t* val_cols, int32_t ncols, double* dst, int64_t ld_dst,
+                      const int32_t* dst_cols, sglm_stream_t stream);
 int sglm_zero_groups_flag(int64_t n, const int64_t* perm, const int64_t* seg,
                           const int64_t* counts, const double* src, int64_t ld,
                           const int32_t* cols, int32_t ncols, double* flag,

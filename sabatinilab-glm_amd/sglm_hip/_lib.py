@@ -132,8 +132,15 @@ SIGNATURES = {
     "sglm_dm_counters": (C.c_int, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                    _vp, _vp]),
     "sglm_dm_pull": (C.c_int, [_vp, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
+    "sglm_dm_heatmap_k": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp,
+                                    _i64, _vp]),
+    "sglm_dm_counters_k": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp,
+                                     _vp, _vp, _vp, _vp]),
+    "sglm_dm_pull_k": (C.c_int, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
     "sglm_trial_map": (C.c_int, [_i64, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _i32, _vp, _i64, _vp,
                                  _vp]),
+    "sglm_trial_map_u8": (C.c_int, [_i64, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _i32, _vp, _i64,
+                                    _vp, _vp]),
     "sglm_zero_groups_flag": (C.c_int, [_i64, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp,
                                         _vp]),
     "sglm_host_masks": (C.c_int, [_i32, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _i32]),

@@ -55,15 +55,65 @@ def _ptrs(tensors):
     return ctypes.cast(arr, ctypes.c_void_p), arr
 
 
+class _Stage:
+    """The small host inputs of one design matrix (trial ids, mapped per-trial values, index
+    lists) in ONE asynchronous copy from pinned memory: a pageable ``.to('cuda')`` waits for
+    every kernel queued before it, a host round trip per upload.  A ring of pinned buffers;
+    a buffer is rewritten only after the copy out of it (event) has run."""
+
+    SLOTS = 4
+
+    def __init__(self):
+        self.h = [None] * self.SLOTS
+        self.d = [None] * self.SLOTS
+        self.ev = [None] * self.SLOTS
+        self.i = 0
+
+    def upload(self, arrays, dev):
+        arrs = [np.ascontiguousarray(a) for a in arrays]
+        offs, o = [], 0
+        for a in arrs:
+            offs.append(o)
+            o += (a.nbytes + 255) // 256 * 256
+        k = self.i
+        self.i = (k + 1) % self.SLOTS
+        if self.ev[k] is not None:
+            self.ev[k].synchronize()
+        if self.h[k] is None or self.h[k].numel() < o:
+            self.h[k] = torch.empty(max(o, 256) * 2, dtype=torch.uint8).pin_memory()
+            self.d[k] = torch.empty(self.h[k].numel(), dtype=torch.uint8, device=dev)
+        hb = self.h[k].numpy()
+        for a, off in zip(arrs, offs):
+            hb[off:off + a.nbytes] = a.reshape(-1).view(np.uint8)
+        self.d[k][:o].copy_(self.h[k][:o], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+        self.ev[k] = ev
+        out = []
+        for a, off in zip(arrs, offs):
+            t = self.d[k][off:off + a.nbytes].view(_TORCH_DT[a.dtype])
+            out.append(t.view(a.shape))
+        return out
+
+
+_TORCH_DT = {np.dtype(np.float64): torch.float64, np.dtype(np.int32): torch.int32,
+             np.dtype(np.uint8): torch.uint8}
+_STAGE = _Stage()
+
+
 @dataclass
 class Grouping:
     """A pandas groupby over float keys on the device: perm[:m] = the rows with non-NaN keys,
-    grouped by key (row order within a group), seg = group starts (+ m), counts = {m, nseg}
-    (device), sorted = the keys were already ordered (no sort was needed)."""
+    grouped by key (row order within a group), seg = group starts (+ m), counts = {m, nseg,
+    ordered} (device).  ``sorted``: the keys were already ordered (no sort was needed) -- a
+    readback, so only asked for by tests."""
     perm: "torch.Tensor"
     seg: "torch.Tensor"
     counts: "torch.Tensor"
-    sorted: bool
+
+    @property
+    def sorted(self) -> bool:
+        return bool(self.counts[2].item())
 
 
 class Workspace:
@@ -87,11 +137,10 @@ def group_rows(key, key2=None, ws: Optional[Workspace] = None) -> Grouping:
     dev = key.device
     perm = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
     seg = torch.empty(n + 1, dtype=torch.int64, device=dev)
-    counts = torch.zeros(2, dtype=torch.int64, device=dev)
-    srt = ctypes.c_int32(0)
-    _lib.call("sglm_group_rows", _p(key), _p(key2), n, _p(perm), _p(seg), _p(counts),
-              ctypes.addressof(srt), _p((ws or _WS).get(n, dev)), _stream())
-    return Grouping(perm, seg, counts, bool(srt.value))
+    counts = torch.empty(3, dtype=torch.int64, device=dev)
+    _lib.call("sglm_group_rows", _p(key), _p(key2), n, _p(perm), _p(seg), _p(counts), None,
+              _p((ws or _WS).get(n, dev)), _stream())
+    return Grouping(perm, seg, counts)
 
 
 class TrialTable:
@@ -160,17 +209,17 @@ def counters(cols, g: Grouping, g2: Grouping):
     return tenl, tenlp, cue
 
 
-def pull(bout, g: Grouping, nth_order: List[int], cols: List["torch.Tensor"]):
+def pull(bout, g: Grouping, nth_order: List[int], cols: List["torch.Tensor"], key=None):
     """pull_lick_from_bout (:44-53) over positions in processing order (bout updated in
-    place)."""
+    place).  ``key``: the grouping's key (the zero pass then skips the group rows)."""
     if len(nth_order) > MAX_PULL:
         raise ValueError(f"at most {MAX_PULL} lick positions")
     if not nth_order:
         return
     nth = (ctypes.c_int32 * len(nth_order))(*[int(v) for v in nth_order])
     cp, keep = _ptrs(cols)
-    _lib.call("sglm_dm_pull", _p(bout), int(bout.numel()), _p(g.perm), _p(g.seg), _p(g.counts),
-              ctypes.cast(nth, ctypes.c_void_p), len(nth_order), cp, _stream())
+    _lib.call("sglm_dm_pull_k", _p(bout), _p(key), int(bout.numel()), _p(g.perm), _p(g.seg),
+              _p(g.counts), ctypes.cast(nth, ctypes.c_void_p), len(nth_order), cp, _stream())
 
 
 def trial_map(tidx, block, src_cols, vals, val_cols, out_block, dst_cols):
@@ -199,22 +248,102 @@ DEVICE_INPUTS = ["nTrial", "nENL", "iSpout", "Cue", "ENL", "state_ENLP", "Consum
                  "stateConsumption", "trial_clock"]
 
 
-def _dummy_labels(series, trial_type):
+def _masked(series):
+    """(values, NA mask) of a numeric numpy or nullable (masked) trial-table column, else
+    None: the plain arrays, without pandas' per-call conversions."""
+    arr = series.array
+    data, mask = getattr(arr, "_data", None), getattr(arr, "_mask", None)
+    if isinstance(data, np.ndarray) and isinstance(mask, np.ndarray) and data.dtype.kind in "iufb":
+        return data, mask
+    v = series.to_numpy()
+    if isinstance(v, np.ndarray) and v.dtype.kind in "iub":
+        return v, np.zeros(v.shape, dtype=bool)
+    if isinstance(v, np.ndarray) and v.dtype.kind == "f":
+        return v, np.isnan(v)
+    return None
+
+
+def _f64(series):
+    """series.to_numpy(float64, na_value=nan)."""
+    dm = _masked(series)
+    if dm is None:
+        return series.to_numpy(dtype=np.float64, na_value=np.nan)
+    data, mask = dm
+    out = data.astype(np.float64)
+    out[mask] = np.nan
+    return out
+
+
+def _na_mask(series):
+    """series.isna() as a bool array."""
+    dm = _masked(series)
+    return series.isna().to_numpy(dtype=bool) if dm is None else dm[1]
+
+
+def _isna(series):
+    """series.isna() as float64 0/1."""
+    return _na_mask(series).astype(np.float64)
+
+
+def _dummy_rows(series, trial_type):
     """pd.get_dummies(trials[trial_type], prefix=trial_type) (:88) on the host (a trial-table
     column): the labels the reference puts in the new names (dummy_col.split('_')[-1], :96)
-    and the per-trial 0/1 values."""
+    and the 0/1 indicator of each level as uint8 rows [level][trial].  Numeric / nullable
+    numeric columns: the sorted distinct non-NA values (get_dummies' categories:
+    factorize(sort=True)), formatted as pandas formats the column names; other dtypes
+    through pandas."""
+    dm = _masked(series)
+    if dm is not None:
+        data, mask = dm
+        anyna = bool(mask.any())
+        v = data[~mask] if anyna else data
+        levels = None
+        if v.dtype.kind in "iu" and v.size:
+            lo, hi = int(v.min()), int(v.max())
+            if hi - lo < 65536:                      # small integer codes: a count, no sort
+                cnt = np.bincount(v if lo == 0 else v - lo, minlength=hi - lo + 1)
+                levels = (np.flatnonzero(cnt) + lo).astype(v.dtype)
+        if levels is None:
+            levels = np.unique(v)
+        if not (levels.dtype.kind == "f" and np.isnan(levels).any()):
+            rows = np.empty((levels.size, data.size), dtype=np.uint8)
+            for d, lv in enumerate(levels):
+                eq = data == lv
+                if anyna:
+                    eq &= ~mask
+                rows[d] = eq
+            return [str(f"{trial_type}_{x}").split("_")[-1] for x in levels.tolist()], rows
     import pandas as pd
     d = pd.get_dummies(series, prefix=trial_type)
-    return [str(c).split("_")[-1] for c in d.columns], d.to_numpy(dtype=np.float64)
+    return ([str(c).split("_")[-1] for c in d.columns],
+            np.ascontiguousarray(d.to_numpy(dtype=np.uint8).T))
+
+
+def _dummy_labels(series, trial_type):
+    """_dummy_rows with float64 values [trial][level] (get_dummies' frame layout)."""
+    labels, rows = _dummy_rows(series, trial_type)
+    return labels, rows.T.astype(np.float64)
 
 
 @dataclass
 class DesignResult:
     names: List[str]
     block: "torch.Tensor"          # [len(names)][n] float64 device, in `names` order
-    dtypes: List[object]
+    base_dtypes: List[object]      # per column, before the mapped-NaN rule below
+    factored: List[bool]           # the column is a product with mapped trial dummies
+    mapped_nan: object = False     # device bool: some row maps to no trial (dummies -> NaN)
     lick: Optional["torch.Tensor"] = None          # the Lick column (:160)
     without: Optional[np.ndarray] = None           # trials_without_dummies (:201)
+
+    @property
+    def dtypes(self) -> List[object]:
+        """pandas' dtypes: a dummy product is float64 (object in pandas) when some row's trial
+        is unmapped.  Resolving it reads one flag back (after the block's download in
+        to_frame, so it costs nothing there)."""
+        if not isinstance(self.mapped_nan, bool):
+            self.mapped_nan = bool(self.mapped_nan.item())
+        return [np.dtype(np.float64) if (self.mapped_nan and f) else dt
+                for dt, f in zip(self.base_dtypes, self.factored)]
 
 
 @dataclass
@@ -304,8 +433,8 @@ def _plan(orig, src_dtypes, states, nth_licks, interactions, trials_idx):
                     f"interaction pattern {pat!r} picks the 'flag' / 'nTrial' column, which the "
                     "reference then fails to update (KeyError at pp_design_mat.py:192)")
             later = [c for c in names if c not in picked]
-            labels, dvals = _dummy_labels(trials_idx[trial_type], trial_type)
-            dummies[trial_type] = dvals
+            labels, drows = _dummy_rows(trials_idx[trial_type], trial_type)
+            dummies[trial_type] = drows
             new = []
             for d, lab in enumerate(labels):
                 for c in picked:
@@ -361,15 +490,46 @@ def design_matrix_device(cols, src_dtypes, n, trials_idx, states, nth_licks, int
         slot[b] = K + scratch.index(b)
     blk = torch.empty((K + len(scratch), max(n, 1)), dtype=torch.float64, device=dev)
     row = lambda b: blk[slot[b]]                  # noqa: E731
+    # every host input of the kernels below (the trial table's ids in ascending order and its
+    # mapped rows, the trial-map index lists, the cue-like columns) in ONE staged copy,
+    # enqueued before the first kernel: no host round trip in the whole matrix
+    ids = trials_idx.index.to_numpy(dtype=np.float64, na_value=np.nan)
+    nt = int(ids.size)
+    # the trial table in ascending id order (usually it already is: no gather then)
+    if nt < 2 or bool(np.all(ids[1:] > ids[:-1])):
+        asc = lambda a: a                                           # noqa: E731
+    else:
+        torder = np.argsort(ids, kind="stable")
+        asc = lambda a: np.ascontiguousarray(a[..., torder])        # noqa: E731
+    inter = [c for c in names if rec[c].factors]
+    fq = names.index("flag")
+    cue_like = [names.index(c) for c in names if str(c).endswith("cue")]
+    # per interaction column its per-trial factor, the product of its 0/1 dummies (uint8:
+    # exact, an eighth of the float64 upload)
+    fv = np.ones((len(inter), nt), dtype=np.uint8)
+    for j, c in enumerate(inter):
+        for tt_name, d in rec[c].factors:
+            fv[j] &= dummies[tt_name][d]
+    isna = np.zeros(nt, dtype=bool)
+    for trial_type in (interactions or {}):
+        isna |= _na_mask(trials_idx[trial_type])
+    i32 = lambda v: np.asarray(v, dtype=np.int32)          # noqa: E731
+    (tkeys, tsel, fvd, isnad, isrc, ival, idst, fsrc, fval, fdst, cd) = _STAGE.upload([
+        asc(ids), asc(_f64(trials_idx["tSelection"])), asc(fv),
+        asc(isna.view(np.uint8))[None, :],
+        i32([slot[rec[c].base] for c in inter]), i32(range(len(inter))),
+        i32([names.index(c) for c in inter]), i32([-1]), i32([0]), i32([fq]),
+        i32(cue_like if cue_like else [0])], dev)
     g = group_rows(cols["nTrial"])
     g2 = group_rows(cols["nTrial"], cols["nENL"])
-    tt = TrialTable(trials_idx.index.to_numpy(dtype=np.float64, na_value=np.nan), dev)
-    tidx = tt.lookup(cols["nTrial"])
-    tsel = tt.values(trials_idx["tSelection"].to_numpy(dtype=np.float64, na_value=np.nan))
+    tidx = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    _lib.call("sglm_trial_lookup", _p(cols["nTrial"]), n, _p(tkeys), nt, _p(tidx), _stream())
     # add_heatmap_columns: the five hm rows are consecutive at the end of the block
-    _lib.call("sglm_dm_heatmap", _p(cols["trial_clock"]), _p(cols["Cue"]),
-              _p(cols["Consumption"]), _p(cols["stateConsumption"]), n, _p(g.perm), _p(g.seg),
-              _p(g.counts), _p(tidx), _p(tsel[0]), _p(row("hm:0")), blk.shape[1], _stream())
+    # (the _k entries: the per-row default passes write only the rows outside every group)
+    _lib.call("sglm_dm_heatmap_k", _p(cols["trial_clock"]), _p(cols["Cue"]),
+              _p(cols["Consumption"]), _p(cols["stateConsumption"]), _p(cols["nTrial"]), n,
+              _p(g.perm), _p(g.seg), _p(g.counts), _p(tidx), _p(tsel), _p(row("hm:0")),
+              blk.shape[1], _stream())
     lick_col = torch.empty(max(n, 1), dtype=torch.float64, device=dev)
     st_src = [cols[st] for st in states]
     st_dst = [row("lick:" + f"{st[:3].lower()}_lick") for st in states]
@@ -377,44 +537,34 @@ def design_matrix_device(cols, src_dtypes, n, trials_idx, states, nth_licks, int
     dp, k2 = _ptrs(st_dst)
     _lib.call("sglm_dm_licks", _p(cols["iSpout"]), 1, sp, len(states), n, dp, _p(lick_col),
               _stream())
-    _lib.call("sglm_dm_counters", _p(cols["ENL"]), _p(cols["Cue"]), _p(cols["state_ENLP"]), n,
-              _p(g.perm), _p(g.seg), _p(g.counts), _p(g2.perm), _p(g2.seg), _p(g2.counts),
-              _p(row("tenl")), _p(row("tenlp")), _p(row("cue")), _stream())
+    _lib.call("sglm_dm_counters_k", _p(cols["ENL"]), _p(cols["Cue"]), _p(cols["state_ENLP"]),
+              _p(cols["nTrial"]), _p(cols["nENL"]), n, _p(g.perm), _p(g.seg), _p(g.counts),
+              _p(g2.perm), _p(g2.seg), _p(g2.counts), _p(row("tenl")), _p(row("tenlp")),
+              _p(row("cue")), _stream())
     # inputs that are columns of the matrix (or sources of interactions) are copied in
     for b, q in slot.items():
         if b.startswith("in:"):
             blk[q, :n].copy_(cols[b[3:]][:n])
-    pull(row(bout_base), g, order, [row("pull:" + f"con_lick_{nth}") for nth in order])
+    pull(row(bout_base), g, order, [row("pull:" + f"con_lick_{nth}") for nth in order],
+         key=cols["nTrial"])
     # interactions: every column with factors in one trial-map launch, the per-trial factor
     # the product of its dummies (0/1 exact, in any order)
-    inter = [c for c in names if rec[c].factors]
-    mapped_nan = bool(interactions) and bool((tidx < 0).any().item())
+    ld = blk.shape[1]
     if inter:
-        fv = np.ones((len(inter), tt.n))
-        for j, c in enumerate(inter):
-            for tt_name, d in rec[c].factors:
-                fv[j] *= dummies[tt_name][:, d]
-        trial_map(tidx, blk, [slot[rec[c].base] for c in inter], tt.values(fv),
-                  list(range(len(inter))), blk, [names.index(c) for c in inter])
+        _lib.call("sglm_trial_map_u8", n, _p(tidx), _p(blk), ld, _p(isrc), _p(fvd), nt,
+                  _p(ival), len(inter), _p(blk), ld, _p(idst), _stream())
     # flag (:189-203): the mapped isna sums, clipped
-    fq = names.index("flag")
     if interactions:
-        isna = np.zeros(tt.n)
-        for trial_type in interactions:
-            isna = isna + trials_idx[trial_type].isna().to_numpy(dtype=np.float64)
-        trial_map(tidx, None, [-1], tt.values(np.minimum(isna, 1.0)), [0], blk, [fq])
+        _lib.call("sglm_trial_map_u8", n, _p(tidx), None, 0, _p(fsrc), _p(isnad), nt, _p(fval),
+                  1, _p(blk), ld, _p(fdst), _stream())
     else:
         blk[fq].zero_()
-    cue_like = [names.index(c) for c in names if str(c).endswith("cue")]
     gz = torch.zeros(max(n, 1), dtype=torch.uint8, device=dev) if verbose else None
-    cd = torch.tensor(cue_like if cue_like else [0], dtype=torch.int32, device=dev)
-    _lib.call("sglm_zero_groups_flag", n, _p(g.perm), _p(g.seg), _p(g.counts), _p(blk),
-              blk.shape[1], _p(cd), len(cue_like), _p(blk[fq]), _p(gz), _stream())
-    dtypes = []
-    for c in names:
-        dt = rec[c].dtype
-        dtypes.append(np.dtype(np.float64) if (mapped_nan and rec[c].factors) else dt)
-    res = DesignResult(names, blk[:K, :n], dtypes, lick_col[:n])
+    _lib.call("sglm_zero_groups_flag", n, _p(g.perm), _p(g.seg), _p(g.counts), _p(blk), ld,
+              _p(cd), len(cue_like), _p(blk[fq]), _p(gz), _stream())
+    mapped_nan = (tidx[:n] < 0).any() if (interactions and n) else False
+    res = DesignResult(names, blk[:K, :n], [rec[c].dtype for c in names],
+                       [bool(rec[c].factors) for c in names], mapped_nan, lick_col[:n])
     if verbose:
         res.without = _without(g, gz, cols["nTrial"])
         print(f"trials_without_dummies = {res.without!r}")
@@ -423,7 +573,7 @@ def design_matrix_device(cols, src_dtypes, n, trials_idx, states, nth_licks, int
 
 def _without(g: Grouping, gz, key):
     """The keys of the groups flagged for having no cue dummy (one small readback)."""
-    m, ns = (int(v) for v in g.counts.cpu().tolist())
+    m, ns = (int(v) for v in g.counts[:2].cpu().tolist())
     if ns == 0:
         return np.array([], dtype=np.float64)
     z = gz[:ns].cpu().numpy().astype(bool)

@@ -96,9 +96,14 @@ def test_group_rows_vs_numpy(engine):
     import torch
     from sglm_hip import designmat
     rng = np.random.default_rng(1)
-    for n, ordered in ((1, True), (5000, True), (70001, False), (300_000, False)):
-        k = np.sort(rng.integers(-5, 40, n).astype(np.float64)) if ordered else \
-            rng.integers(-5, 40, n).astype(np.float64)
+    for n, ordered in ((1, True), (5000, True), (7, False), (70001, False), (300_000, False),
+                       (40_000, "wide")):
+        if ordered == "wide":                       # every digit pass of the radix path
+            k = rng.standard_normal(n) * 10.0 ** rng.integers(-300, 300, n)
+            k[::7] = k[3]                           # repeated keys (groups of many rows)
+        else:
+            k = np.sort(rng.integers(-5, 40, n).astype(np.float64)) if ordered is True else \
+                rng.integers(-5, 40, n).astype(np.float64)
         k[rng.random(n) < 0.05] = np.nan
         k[k == 0] = -0.0
         k2 = rng.integers(0, 3, n).astype(np.float64)
@@ -106,7 +111,9 @@ def test_group_rows_vs_numpy(engine):
         for two in (False, True):
             kk = torch.from_numpy(k).cuda()
             g = designmat.group_rows(kk, torch.from_numpy(k2).cuda() if two else None)
-            m, ns = g.counts.cpu().tolist()
+            m, ns, srt = g.counts.cpu().tolist()
+            if ordered is not True:
+                assert srt == 0
             valid = ~np.isnan(k) & (~np.isnan(k2) if two else True)
             rows = np.flatnonzero(valid)
             kz = np.where(k == 0, 0.0, k)
