@@ -130,6 +130,13 @@ def trial_key_runs(df, id_cols, package_style=False):
     np.not_equal(v[1:], v[:-1], out=chg[1:])
     at = np.flatnonzero(chg)
     u = v[at]
+    lens = np.diff(at, append=v.size).astype(np.int64)
+    if c.dtype in (np.float64, np.int64) and u.size and u[0] >= 0 and \
+            u[-1] < (1e7 if c.dtype == np.float64 else 1e9) and bool(np.all(u == np.floor(u))):
+        # non-negative integral ids whose strings ("12" / "12.0") have at most 9 characters:
+        # the key "<len>:<str>" orders by length (one digit), then lexicographically, i.e.
+        # numerically -- the runs (increasing) are already in key order
+        return np.arange(u.size, dtype=np.int64), at.astype(np.int64), lens
     if c.dtype in (np.float64, np.int64):
         strs = [str(x) for x in u.tolist()]
     else:
@@ -141,7 +148,7 @@ def trial_key_runs(df, id_cols, package_style=False):
     order = np.argsort(np.asarray(keys, dtype=object), kind="stable")
     rank = np.empty(len(keys), dtype=np.int64)
     rank[order] = np.arange(len(keys))
-    return rank, at.astype(np.int64), np.diff(at, append=v.size).astype(np.int64)
+    return rank, at.astype(np.int64), lens
 
 
 def pd_series(values, dtype):

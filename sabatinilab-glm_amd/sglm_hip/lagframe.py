@@ -86,6 +86,11 @@ class LagSource:
             return
         N, m = self.N, len(need)
         arrs = [self._f64(c) for c in need]
+        # address order: the columns of one row-major block then arrive as the packer's block
+        # (each row's run of values read once) whatever order the names came in
+        order = sorted(range(m), key=lambda i: (arrs[i].strides[0], arrs[i].ctypes.data))
+        need = [need[i] for i in order]
+        arrs = [arrs[i] for i in order]
         nw = (N + 31) // 32
         bits = _pinned("lagbits", max(1, m * nw), torch.int32)
         evk = ("lagbits_ev", None)

@@ -19,6 +19,20 @@ def timed_device(self, names):
     torch.cuda.synchronize(); T["device"] = T.get("device", 0) + time.perf_counter() - t
     return r
 lagframe.LagSource.device = timed_device
+orig_up = lagframe.LagSource.upload
+def timed_upload(self, names):
+    t = time.perf_counter()
+    r = orig_up(self, names)
+    T["upload"] = T.get("upload", 0) + time.perf_counter() - t
+    return r
+lagframe.LagSource.upload = timed_upload
+orig_lnc = lagframe.LagFrame._lag_nan_counts
+def timed_lnc(self, lag):
+    t = time.perf_counter()
+    r = orig_lnc(self, lag)
+    T["lag_nan_counts"] = T.get("lag_nan_counts", 0) + time.perf_counter() - t
+    return r
+lagframe.LagFrame._lag_nan_counts = timed_lnc
 for rep in range(4):
     T.clear()
     torch.cuda.synchronize(); t0 = time.perf_counter()
@@ -36,4 +50,5 @@ for rep in range(4):
     torch.cuda.synchronize(); t6 = time.perf_counter()
     print({"timeshift": round(1e3*(t1-t0),2), "select": round(1e3*(t2-t1),2), "isna": round(1e3*(t3-t2),2),
            "sum": round(1e3*(t4-t3),2), "cmp": round(1e3*(t5-t4),2), "bool_rows": round(1e3*(t6-t5),2),
-           "device_in_sum": round(1e3*T.get("device",0),2)})
+           "device_in_sum": round(1e3*T.get("device",0),2), "upload": round(1e3*T.get("upload",0),2),
+           "lag_nan_counts": round(1e3*T.get("lag_nan_counts",0),2)})
