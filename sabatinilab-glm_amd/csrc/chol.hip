@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "common.h"
+#include "chol_tile.h"
 
 namespace sglm {
 
@@ -43,6 +44,13 @@ void launch_chol_diag4(int nact, hipStream_t s, float* Hall, int32_t P, int32_t 
 void launch_chol_diag4q(int nact, hipStream_t s, float* Hall, int32_t P, int32_t k0,
                         const int32_t* fits, uint8_t* frozen_all, const float* diag_all,
                         int32_t* info, float* minv_all, float* Mall);
+void launch_chol_diag4l(int nact, hipStream_t s, float* Hall, int32_t P, int32_t k0,
+                        const int32_t* fits, uint8_t* frozen_all, const float* diag_all,
+                        int32_t* info, float* minv_all, float* Mall);
+void launch_chol_update_diag4l(dim3 grid, hipStream_t s, float* Hall, int32_t P, int32_t k0,
+                               int32_t kc, int32_t s0, const int32_t* fits, uint8_t* frozen_all,
+                               const float* diag_all, int32_t* info, float* minv_all,
+                               float* Mall);
 
 // Four pivots per barrier in the four-wave diagonal step (chol_diag4q_kernel, bitwise the same
 // factor; the default: chain of 1 / 20 representatives 1.10 -> 1.07 / 2.53 -> 2.50 ms, C4 grid
@@ -50,6 +58,21 @@ void launch_chol_diag4q(int nact, hipStream_t s, float* Hall, int32_t P, int32_t
 // of the chain-graph key).
 static bool diag4q() {
     const char* e = getenv("SGLM_DIAG4Q");
+    return !(e && e[0] == '0');
+}
+
+// The four-pivot step with look-ahead and packed FMAs (chol_diag4l_kernel, bitwise the same
+// factor); SGLM_DIAG4L=0 for chol_diag4q_kernel (read per chain capture; part of the key).
+static bool diag4l() {
+    const char* e = getenv("SGLM_DIAG4L");
+    return !(e && e[0] == '0');
+}
+
+// The trailing update fused with the next diagonal step (chol_update_diag4l_kernel; with
+// chol_diag4l_kernel, bitwise the same factor); SGLM_UPD_DIAG=0 launches them separately
+// (read per chain capture; part of the key).
+static bool upd_diag() {
+    const char* e = getenv("SGLM_UPD_DIAG");
     return !(e && e[0] == '0');
 }
 
@@ -286,67 +309,14 @@ __global__ void __launch_bounds__(kCT) chol_update_kernel(float* __restrict__ Ha
 // (the default): K in blocks of 32 rows, each strip loaded once per workgroup with float4
 // row loads (the register variant has every wave fetch its own 32 columns of both strips, so
 // each crosses L2 twice, as scalar loads), two LDS buffers with the next block's loads in
-// registers during this block's 16 MFMAs per wave, one barrier per block.
-constexpr int kLU = 68;             // strip row stride (floats)
+// registers during this block's 16 MFMAs per wave, one barrier per block (chol_tile.h).
 __global__ void __launch_bounds__(kCT) chol_update_lds_kernel(float* __restrict__ Hall,
                                                               int32_t P, int32_t k0, int32_t kc,
                                                               int32_t s0,
                                                               const int32_t* __restrict__ fits) {
-    __shared__ __attribute__((aligned(16))) float sa[2][32 * kLU];
-    __shared__ __attribute__((aligned(16))) float sb[2][32 * kLU];
+    __shared__ __attribute__((aligned(16))) float lds[kLUFloats];
     const int fit = fits[blockIdx.y];
-    float* H = Hall + (int64_t)fit * P * P;
-    const int T = P / kNB - s0;
-    int t = blockIdx.x, bi = 0, bj;
-    {
-        int rowlen = T;
-        while (t >= rowlen) { t -= rowlen; ++bi; --rowlen; }
-        bj = bi + t;
-    }
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int r32 = lane & 31, kh = lane >> 5;
-    const int wr = wave >> 1, wc = wave & 1;
-    const int ca = (s0 + bi) * kNB, cb = (s0 + bj) * kNB;     // strip columns
-    const int lr = tid >> 3, lcol = 8 * (tid & 7);             // this thread's block share
-    const float* ga = H + (int64_t)(k0 + lr) * P + ca + lcol;
-    const float* gb = H + (int64_t)(k0 + lr) * P + cb + lcol;
-    f32x4 ra0, ra1, rb0, rb1;
-    auto gload = [&](int r) {
-        ra0 = *reinterpret_cast<const f32x4*>(ga + (int64_t)r * P);
-        ra1 = *reinterpret_cast<const f32x4*>(ga + (int64_t)r * P + 4);
-        rb0 = *reinterpret_cast<const f32x4*>(gb + (int64_t)r * P);
-        rb1 = *reinterpret_cast<const f32x4*>(gb + (int64_t)r * P + 4);
-    };
-    auto sstore = [&](int buf) {
-        *reinterpret_cast<f32x4*>(&sa[buf][lr * kLU + lcol]) = ra0;
-        *reinterpret_cast<f32x4*>(&sa[buf][lr * kLU + lcol + 4]) = ra1;
-        *reinterpret_cast<f32x4*>(&sb[buf][lr * kLU + lcol]) = rb0;
-        *reinterpret_cast<f32x4*>(&sb[buf][lr * kLU + lcol + 4]) = rb1;
-    };
-    f32x16 acc = {};
-    gload(0);
-    sstore(0);
-    __syncthreads();
-    int cur = 0;
-    for (int r = 0; r < kc; r += 32) {
-        const bool more = r + 32 < kc;
-        if (more) gload(r + 32);
-        const float* A = &sa[cur][kh * kLU + wr * 32 + r32];
-        const float* Bq = &sb[cur][kh * kLU + wc * 32 + r32];
-#pragma unroll
-        for (int u = 0; u < 16; ++u)
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(A[2 * u * kLU], Bq[2 * u * kLU], acc, 0, 0,
-                                                       0);
-        if (more) sstore(cur ^ 1);
-        __syncthreads();
-        cur ^= 1;
-    }
-    const int ci = ca + wr * 32, cj = cb + wc * 32;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        float* h = &H[(int64_t)(ci + (q & 3) + 8 * (q >> 2) + 4 * kh) * P + cj + r32];
-        *h -= acc[q];
-    }
+    update_lds_tile(Hall + (int64_t)fit * P * P, P, k0, kc, s0, blockIdx.x, lds);
 }
 
 // Triangular solves on a stored factor, right-looking, one 1024-thread workgroup per fit: per
@@ -1085,9 +1055,16 @@ static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t na
     // rows b+1 .. (end of the group) is updated with panel b (K = 64), and once per group ONE
     // rank-(kLA*64) update of the rest of the trailing matrix -- the trailing matrix (the HBM
     // read-modify-write that bounds the chain at large batches) is swept P/(kLA*64) times
+    const bool fuse = Mall && nrefac == nact && diag4() && diag4q() && diag4l() && upd_lds() &&
+                      upd_diag();
+    bool have_diag = false;                  // the next diagonal step ran inside an update
     auto factor_step = [&](int kb) {
         const int k0 = kb * kNB;
-        if (Mall && nrefac == nact && diag4() && diag4q())
+        if (have_diag)
+            ;
+        else if (Mall && nrefac == nact && diag4() && diag4q() && diag4l())
+            launch_chol_diag4l(nact, s, H, P, k0, fits, frozen, dg, info, minv, Mall);
+        else if (Mall && nrefac == nact && diag4() && diag4q())
             launch_chol_diag4q(nact, s, H, P, k0, fits, frozen, dg, info, minv, Mall);
         else if (Mall && nrefac == nact && diag4())
             launch_chol_diag4(nact, s, H, P, k0, fits, frozen, dg, info, minv, Mall);
@@ -1103,16 +1080,32 @@ static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t na
         const int ke = kb + la < nb ? kb + la : nb;            // group [kb, ke)
         for (int b = kb; b < ke; ++b) {
             factor_step(b);
+            have_diag = false;
             const int nr = ke - 1 - b;                         // band rows b+1 .. ke-1
             const int T = nb - b - 1;
-            if (nrefac > 0 && nr > 0)
-                launch_update(dim3(nr * T - nr * (nr - 1) / 2, nrefac), s, H, P, b * kNB, kNB,
-                              b + 1, fits);
+            if (nrefac > 0 && nr > 0) {
+                const dim3 g(nr * T - nr * (nr - 1) / 2, nrefac);
+                if (fuse) {
+                    // tile (b+1, b+1) is complete after this band update: factor it there
+                    launch_chol_update_diag4l(g, s, H, P, b * kNB, kNB, b + 1, fits, frozen, dg,
+                                              info, minv, Mall);
+                    have_diag = true;
+                } else {
+                    launch_update(g, s, H, P, b * kNB, kNB, b + 1, fits);
+                }
+            }
         }
         const int T = nb - ke;
-        if (nrefac > 0 && T > 0)
-            launch_update(dim3(T * (T + 1) / 2, nrefac), s, H, P, kb * kNB, (ke - kb) * kNB, ke,
-                          fits);
+        if (nrefac > 0 && T > 0) {
+            const dim3 g(T * (T + 1) / 2, nrefac);
+            if (fuse) {
+                launch_chol_update_diag4l(g, s, H, P, kb * kNB, (ke - kb) * kNB, ke, fits, frozen,
+                                          dg, info, minv, Mall);
+                have_diag = true;
+            } else {
+                launch_update(g, s, H, P, kb * kNB, (ke - kb) * kNB, ke, fits);
+            }
+        }
     }
     st = check_launch("chol block kernels");
     if (st) return st;
@@ -1323,7 +1316,7 @@ static int factor_inv_cached(float* H, float* Minv, int32_t P, const int32_t* fi
     std::memset(&key, 0, sizeof(key));
     key.H = H; key.Minv = Minv; key.fits = fits; key.dshift = dshift; key.delta = delta;
     key.info = info; key.frozen = frozen; key.work = work;
-    key.P = P; key.n = n; key.B = B; key.la = chol_lookahead(); key.q = diag4q() ? 1 : 0;
+    key.P = P; key.n = n; key.B = B; key.la = chol_lookahead(); key.q = diag4q() ? (diag4l() ? (upd_diag() ? 3 : 2) : 1) : 0;
     // the lock is held across capture and launch: a concurrent eviction must not destroy the
     // entry between lookup and launch (captures are thread-local, so nothing else is stalled
     // but other chains' host enqueue, which is short next to the chain itself)

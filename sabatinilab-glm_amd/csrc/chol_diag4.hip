@@ -14,6 +14,7 @@
 // diagonal 1, V row zero -- and counted in info.  The rhs forward solve of chol_diag_kernel is
 // not done: the inverse chain solves on the explicit inverse later.
 #include "common.h"
+#include "chol_tile.h"
 
 namespace sglm {
 
@@ -252,6 +253,205 @@ static __global__ void __launch_bounds__(256) chol_diag4q_kernel(
     for (int e = 0; e < 16; e += 4)
         *reinterpret_cast<f32x4*>(mr + e) = f32x4{sv[cc][part + e], sv[cc][part + e + 1],
                                                   sv[cc][part + e + 2], sv[cc][part + e + 3]};
+}
+
+// Four pivots per barrier with look-ahead and packed FMAs (chol_diag4l_kernel, bitwise the
+// same factor and inverse as chol_diag4q_kernel).  In diag4q the quad's owner forms its four
+// pivots while the other three waves wait at the barrier, and then every wave applies the
+// quad's terms: per quad the serial pivot chain and the 128-FMA update run one after the
+// other.  Here the owner of the NEXT quad first applies quad Q's terms to its four rows of
+// quad Q + 4, forms quad Q + 4's pivots and publishes them (the other buffer), and only then
+// applies quad Q's terms to its other rows -- while the other waves apply theirs: the pivot
+// chain overlaps the update.  Rows of A and of V are held as pairs (a, v) so that both
+// rank-1 terms of an element are one v_pk_fma_f32.  Per element the same FMAs in the same
+// order as before.
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+
+// the owner's four pivots of quad Q (rows Q + h in registers 4 (Q >> 4) + h), published into
+// one buffer: row multipliers by row position, U and V multipliers by column
+__device__ __forceinline__ void diag4l_quad(const int Q, f32x2v (&av)[16], const int c,
+                                            const float thr, int& myfrz, int& dropped,
+                                            const int rpos, float* srow_b, float* scol_b,
+                                            float* sx_b) {
+    const int k = 4 * (Q >> 4);
+    float u[4], x[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        const int q = Q + h;
+        const int verdict = (myfrz ? 2 : 0) | (av[k + h].x > thr ? 0 : 1);
+        const int vq = __builtin_amdgcn_readlane(verdict, q);
+        const bool drop = vq != 0;
+        const bool newly = drop && (vq & 2) == 0 && c == q;
+        const float piv = lane4f(av[k + h].x, q);
+        const float rr = drop ? 0.0f : __builtin_amdgcn_rsqf(piv);
+        const float d = drop ? 1.0f : piv * rr;
+        u[h] = c > q ? av[k + h].x * rr : 0.0f;                       // U[q][c]
+        av[k + h].x = c == q ? d : (c > q ? u[h] : av[k + h].x);
+        x[h] = av[k + h].y * rr;                                      // V[q][c]
+        av[k + h].y = x[h];
+        myfrz = newly ? 1 : myfrz;
+        dropped = newly ? 1 : dropped;
+#pragma unroll
+        for (int g = h + 1; g < 4; ++g) {
+            const float t = lane4f(u[h], Q + g);                      // U[q][Q+g]
+            av[k + g].x = fmaf(-t, u[h], av[k + g].x);
+            av[k + g].y = fmaf(-t, x[h], av[k + g].y);
+        }
+    }
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        const bool own_later = c > Q + h && c <= Q + 3;   // already applied by the owner
+        srow_b[h * 64 + rpos] = own_later ? 0.0f : u[h];
+        scol_b[h * 64 + c] = u[h];
+        sx_b[h * 64 + c] = x[h];
+    }
+}
+
+// quad Q's four terms (buffer b) on register group g (rows of av[4g .. 4g+3])
+__device__ __forceinline__ void diag4l_apply(f32x2v (&av)[16], const int g, const float* srow_b,
+                                             const float* scol_b, const float* sx_b,
+                                             const int w, const int c) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        const f32x2v m = {scol_b[h * 64 + c], sx_b[h * 64 + c]};
+        const f32x4 ui = reinterpret_cast<const f32x4*>(&srow_b[h * 64 + w * 16])[g];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const f32x2v nu = {-ui[e], -ui[e]};
+            av[4 * g + e] = __builtin_elementwise_fma(nu, m, av[4 * g + e]);
+        }
+    }
+}
+
+struct Diag4lSmem {
+    __attribute__((aligned(16))) float srow[2][4][64];
+    float scol[2][4][64];
+    float sx[2][4][64];
+    float sv[64][65];
+};
+
+// the diagonal step of block k0 for fit `fit` (launch slot `slot`: its block inverse goes to
+// minv_all + slot * 64 * 64) by one 256-thread workgroup
+__device__ __forceinline__ void diag4l_block(float* __restrict__ Hall, int32_t P, int32_t k0,
+                                             int fit, int slot, uint8_t* __restrict__ frozen_all,
+                                             const float* __restrict__ diag_all,
+                                             int32_t* __restrict__ info,
+                                             float* __restrict__ minv_all,
+                                             float* __restrict__ Mall, Diag4lSmem& sm) {
+    float* H = Hall + (int64_t)fit * P * P;
+    uint8_t* frz = frozen_all + (int64_t)fit * P + k0;
+    const int c = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // register k of wave w holds row 16 (k >> 2) + 4 w + (k & 3)
+    f32x2v av[16];
+    {
+        int cl = c;
+        asm volatile("" : "+v"(cl));
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int r = 16 * (k >> 2) + 4 * w + (k & 3);
+            const float x = H[(int64_t)(k0 + r) * P + k0 + c];
+            av[k].x = r <= cl ? x : 0.0f;
+            av[k].y = r == cl ? 1.0f : 0.0f;
+        }
+    }
+    int myfrz = frz[c];
+    const float thr = 1e-6f * diag_all[(int64_t)fit * P + k0 + c];
+    int dropped = 0;
+    const int rpos = ((c >> 2) & 3) * 16 + 4 * (c >> 4) + (c & 3);
+    if (w == 0)
+        diag4l_quad(0, av, c, thr, myfrz, dropped, rpos, &sm.srow[0][0][0], &sm.scol[0][0][0],
+                    &sm.sx[0][0][0]);
+    __syncthreads();
+#pragma unroll
+    for (int Q = 0; Q < 64; Q += 4) {
+        const int buf = (Q >> 2) & 1;
+        const float* rb = &sm.srow[buf][0][0];
+        const float* cb = &sm.scol[buf][0][0];
+        const float* xb = &sm.sx[buf][0][0];
+        const int Qn = Q + 4;
+        if (Qn < 64 && w == ((Qn >> 2) & 3)) {       // wave-uniform: the next quad's owner
+            const int gn = Qn >> 4;
+            diag4l_apply(av, gn, rb, cb, xb, w, c);
+            diag4l_quad(Qn, av, c, thr, myfrz, dropped, rpos, &sm.srow[buf ^ 1][0][0],
+                        &sm.scol[buf ^ 1][0][0], &sm.sx[buf ^ 1][0][0]);
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                if (g != gn) diag4l_apply(av, g, rb, cb, xb, w, c);
+        } else {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) diag4l_apply(av, g, rb, cb, xb, w, c);
+        }
+        __syncthreads();
+    }
+    float* mo = minv_all + (int64_t)slot * 64 * 64 + c;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int r = 16 * (k >> 2) + 4 * w + (k & 3);
+        H[(int64_t)(k0 + r) * P + k0 + c] = av[k].x;
+        mo[r * 64] = av[k].y;
+        sm.sv[c][r] = av[k].y;
+    }
+    if (((c >> 2) & 3) == w) {                       // the owner of step c
+        frz[c] = (uint8_t)myfrz;
+        if (dropped) atomicAdd(&info[fit], 1);
+    }
+    if (!Mall) return;
+    __syncthreads();
+    const int cc = threadIdx.x >> 2, part = (threadIdx.x & 3) * 16;
+    float* mr = Mall + (int64_t)fit * P * P + (int64_t)(k0 + cc) * P + k0 + part;
+#pragma unroll
+    for (int e = 0; e < 16; e += 4)
+        *reinterpret_cast<f32x4*>(mr + e) = f32x4{sm.sv[cc][part + e], sm.sv[cc][part + e + 1],
+                                                  sm.sv[cc][part + e + 2],
+                                                  sm.sv[cc][part + e + 3]};
+}
+
+static __global__ void __launch_bounds__(256) chol_diag4l_kernel(
+    float* __restrict__ Hall, int32_t P, int32_t k0, const int32_t* __restrict__ fits,
+    uint8_t* __restrict__ frozen_all, const float* __restrict__ diag_all,
+    int32_t* __restrict__ info, float* __restrict__ minv_all, float* __restrict__ Mall) {
+    __shared__ Diag4lSmem sm;
+    diag4l_block(Hall, P, k0, fits[blockIdx.x], blockIdx.x, frozen_all, diag_all, info, minv_all,
+                 Mall, sm);
+}
+
+// The trailing update (chol_tile.h) fused with the NEXT diagonal step: the workgroup of tile
+// (s0, s0) -- the first tile of the launch, and the last piece of the next diagonal block --
+// factors that block right after updating it, while the other tiles' workgroups run on: one
+// launch (and one dependency) fewer per block step, the diagonal step's latency overlapped
+// with the rest of the update.  The panel step of block s0 follows the launch.
+union UpdDiagSmem {
+    float upd[kLUFloats];
+    Diag4lSmem diag;
+};
+
+static __global__ void __launch_bounds__(256) chol_update_diag4l_kernel(
+    float* __restrict__ Hall, int32_t P, int32_t k0, int32_t kc, int32_t s0,
+    const int32_t* __restrict__ fits, uint8_t* __restrict__ frozen_all,
+    const float* __restrict__ diag_all, int32_t* __restrict__ info, float* __restrict__ minv_all,
+    float* __restrict__ Mall) {
+    __shared__ UpdDiagSmem sm;
+    const int fit = fits[blockIdx.y];
+    update_lds_tile(Hall + (int64_t)fit * P * P, P, k0, kc, s0, blockIdx.x, sm.upd);
+    if (blockIdx.x != 0) return;
+    __syncthreads();                    // the tile's update is visible to the whole workgroup
+    diag4l_block(Hall, P, s0 * 64, fit, blockIdx.y, frozen_all, diag_all, info, minv_all, Mall,
+                 sm.diag);
+}
+
+void launch_chol_update_diag4l(dim3 grid, hipStream_t s, float* Hall, int32_t P, int32_t k0,
+                               int32_t kc, int32_t s0, const int32_t* fits, uint8_t* frozen_all,
+                               const float* diag_all, int32_t* info, float* minv_all,
+                               float* Mall) {
+    chol_update_diag4l_kernel<<<grid, 256, 0, s>>>(Hall, P, k0, kc, s0, fits, frozen_all,
+                                                   diag_all, info, minv_all, Mall);
+}
+
+void launch_chol_diag4l(int nact, hipStream_t s, float* Hall, int32_t P, int32_t k0,
+                        const int32_t* fits, uint8_t* frozen_all, const float* diag_all,
+                        int32_t* info, float* minv_all, float* Mall) {
+    chol_diag4l_kernel<<<nact, 256, 0, s>>>(Hall, P, k0, fits, frozen_all, diag_all, info,
+                                            minv_all, Mall);
 }
 
 void launch_chol_diag4q(int nact, hipStream_t s, float* Hall, int32_t P, int32_t k0,

@@ -245,9 +245,10 @@ def test_chol_solve_inv_vs_float64(engine, torch_mod, P, p, B):
 @pytest.mark.parametrize("P,p", [(256, 200), (2048, 1990)])
 def test_chol_diag_four_pivots_equals_two(engine, torch_mod, P, p, monkeypatch):
     """The factor + inverse chain with four pivots per barrier in the diagonal step
-    (chol_diag4q_kernel) leaves the same factor, inverse, frozen set and drop count as two
-    pivots per barrier (chol_diag4_kernel), bit for bit: a duplicated column (a dropped pivot),
-    a frozen coordinate, three fits."""
+    (chol_diag4q_kernel), and with look-ahead and packed FMAs (chol_diag4l_kernel), leaves the
+    same factor, inverse, frozen set and drop count as two pivots per barrier
+    (chol_diag4_kernel), bit for bit: a duplicated column (a dropped pivot), a frozen
+    coordinate, three fits."""
     torch = torch_mod
     from sglm_hip import _lib
     rng = np.random.default_rng(P)
@@ -263,8 +264,9 @@ def test_chol_diag_four_pivots_equals_two(engine, torch_mod, P, p, monkeypatch):
     dsh[:, [5, 9]] = 0.0                                 # unpenalised: pivot 9 drops
     dsh[:, 17] = -1.0                                    # frozen
     outs = {}
-    for q in ("1", "0"):
-        monkeypatch.setenv("SGLM_DIAG4Q", q)
+    for q in ("l", "1", "0"):
+        monkeypatch.setenv("SGLM_DIAG4Q", "0" if q == "0" else "1")
+        monkeypatch.setenv("SGLM_DIAG4L", "1" if q == "l" else "0")
         Hd = torch.from_numpy(H).cuda()
         Md = torch.zeros_like(Hd)
         out = torch.zeros((B, P), dtype=torch.float32, device="cuda")
@@ -281,8 +283,9 @@ def test_chol_diag_four_pivots_equals_two(engine, torch_mod, P, p, monkeypatch):
         torch.cuda.synchronize()
         outs[q] = [t.cpu().numpy() for t in (Hd, Md, info, frozen)]
     assert (outs["1"][2] >= 1).all()                     # the dependent column dropped
-    for a, b in zip(outs["1"], outs["0"]):
-        assert np.array_equal(a, b, equal_nan=True)
+    for v in ("1", "l"):
+        for a, b in zip(outs[v], outs["0"]):
+            assert np.array_equal(a, b, equal_nan=True), v
 
 
 @pytest.mark.parametrize("P,p,B", [(768, 700, 6), (2048, 1990, 5)])

@@ -23,7 +23,23 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--P", type=int, default=2048)
     ap.add_argument("--p", type=int, default=2000)
+    ap.add_argument("--env", default=None,
+                    help="NAME=v1,v2: time each value of an environment switch (alternating)")
     a = ap.parse_args()
+    if a.env:
+        name, vals = a.env.split("=")
+        res = {}
+        for r in range(3):
+            for v in vals.split(","):
+                os.environ[name] = v
+                res.setdefault(v, []).append(run(a))
+        print(json.dumps({v: {n: float(np.median([x[n]["ms_median"] for x in rs]))
+                              for n in a.n} for v, rs in res.items()}))
+        return
+    print(json.dumps(run(a)))
+
+
+def run(a):
     import torch
     from sglm_hip import _lib
     P, p = a.P, a.p
@@ -71,7 +87,7 @@ def main():
         out[n] = {"ms_median": float(np.median(times)), "ms_min": float(np.min(times)),
                   "host_ms_median": float(np.median(host)),
                   "inv_err": err, "dropped": int(info.sum().item())}
-    print(json.dumps(out))
+    return out
 
 
 if __name__ == "__main__":
