@@ -121,6 +121,14 @@ int sglm_link_update(int32_t family, float power, int64_t n, int64_t ld, int32_t
                      const int32_t* slots, float* eta, const float* Y, const uint8_t* M,
                      const int32_t* fit_resp, const int32_t* fit_mask, float* W, float* R,
                      void* Rp, const float* step, const float* deta, sglm_stream_t stream);
+/* sglm_link_update_rp: sglm_link_update (slots required) writing launch row y's packed R into
+ * row rpos[y] of planes of Bp rows (rpos[y] < 0: no packed row; W, R and the fused predictor
+ * update as usual) -- the rows of the fits that continue, compacted by sglm_step_decide. */
+int sglm_link_update_rp(int32_t family, float power, int64_t n, int64_t ld, int32_t B,
+                        const int32_t* slots, float* eta, const float* Y, const uint8_t* M,
+                        const int32_t* fit_resp, const int32_t* fit_mask, float* W, float* R,
+                        void* Rp, int32_t Bp, const int32_t* rpos, const float* step,
+                        const float* deta, sglm_stream_t stream);
 
 /* G[k][a] = sum_i X[a][i] * R[k][i] (float64 out; f32 MFMA partial sums, fixed-order
  * float64 reduction over row chunks).  `work`: sglm_xtr_work_bytes(P, B, n). */
@@ -217,6 +225,11 @@ size_t sglm_xtr_bits_packed_work_bytes(int32_t P, int32_t B, int64_t ld);
 int sglm_xtr_bits_packed(const uint32_t* cbits, int64_t ld, int32_t P, int64_t n,
                          const void* Rp, int32_t B, const int32_t* slots, double* G,
                          void* work, sglm_stream_t stream);
+/* sglm_xtr_bits_packed_bp: the same with the packed planes' row stride Bp given (>= the padded
+ * fit count): the R rows sglm_link_update_rp wrote at compacted positions of a longer launch. */
+int sglm_xtr_bits_packed_bp(const uint32_t* cbits, int64_t ld, int32_t P, int64_t n,
+                            const void* Rp, int32_t B, int32_t Bp, const int32_t* slots,
+                            double* G, void* work, sglm_stream_t stream);
 
 /* G[q] = X^T D_q (float64) for integer-valued columns, |D| <= 256 (the base-256 digit planes
  * of an exact X^T y): D as bf16 [Bp][ld] (Bp = ceil(B/32)*32 rows allocated), one bf16 piece,
@@ -413,6 +426,23 @@ int sglm_step_scalars(int32_t P, int32_t ncoef, int32_t B, const int32_t* slots,
                       const double* beta, const float* delta, const double* lamp,
                       const double* t, int32_t T, double* out, sglm_stream_t stream);
 /* beta[k] += step[q] * delta[k] for k = slots[q], q < B (float64 coefficients). */
+/* sglm_step_decide: the Newton iteration's decisions for na active fits (slots act) on the
+ * device -- engine.irls' stage-1 Armijo search over ts[1..4] from the trial losses L [na][5]
+ * and the step scalars sc [na][6 + nts] (sglm_loss_trials_max / sglm_step_scalars), the stopping
+ * rule (tol, stagnation on a fresh Hessian, failed search, iteration cap; sfloor / legacy as
+ * STOP_SCALE_FLOOR / STOP_LEGACY; aa_rm [slot][2] the secant's raw steps or NULL) with the
+ * per-fit prev_rel, fresh, n_iter, max_iter.  Out per fit: step64 / step32 (0 when stage 1
+ * fails: flag 256, the host's stage 2 decides), relv, prop, flags (1 hit, 2 stop, 4 converged,
+ * 8 out of iterations, 16 stop_tol, 32 stagnation, 64 failed, 256 stage 2, 512 a packed-R row),
+ * tix (index into ts); rpos[q] = the fit's row among those that continue or await stage 2
+ * (act order, -1 none), nxt[0 .. *cnt) their slots.  One workgroup. */
+int sglm_step_decide(int32_t na, const int32_t* act, const double* L, const double* sc,
+                     int32_t nts, const double* ts, double sigma, double tol, double sfloor,
+                     int32_t legacy, const float* aa_rm, const double* prev_rel,
+                     const uint8_t* fresh, const int32_t* n_iter, const int32_t* max_iter,
+                     double* step64, float* step32, double* relv, double* prop, int32_t* flags,
+                     int32_t* tix, int32_t* rpos, int32_t* nxt, int32_t* cnt,
+                     sglm_stream_t stream);
 int sglm_step_update(int32_t P, int32_t B, const int32_t* slots, const double* step,
                      const float* delta, double* beta, sglm_stream_t stream);
 

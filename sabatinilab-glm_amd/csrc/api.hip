@@ -157,9 +157,11 @@ __global__ void __launch_bounds__(256) link_kernel(int32_t family, float power, 
                                                    float* __restrict__ W, float* __restrict__ R,
                                                    __bf16* __restrict__ Rp, int32_t Bp,
                                                    const float* __restrict__ step,
-                                                   const float* __restrict__ deta) {
+                                                   const float* __restrict__ deta,
+                                                   const int32_t* __restrict__ rpos) {
     const int y = blockIdx.y;
     const int k = slots ? slots[y] : y;
+    const int ry = rpos ? rpos[y] : y;          // packed-R row of this fit (< 0: none)
     float* e = eta + (int64_t)k * ld;
     // fused predictor update of the previous Newton step: eta += step[y] * deta (then the link)
     const float t = deta ? step[y] : 0.0f;
@@ -169,7 +171,7 @@ __global__ void __launch_bounds__(256) link_kernel(int32_t family, float power, 
     float* w = W + (int64_t)k * ld;
     float* r = R ? R + (int64_t)k * ld : nullptr;
     const int64_t plane = (int64_t)Bp * ld;
-    __bf16* rp = Rp ? Rp + (int64_t)y * ld : nullptr;
+    __bf16* rp = (Rp && ry >= 0) ? Rp + (int64_t)ry * ld : nullptr;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < ld;
          i += (int64_t)gridDim.x * 256) {
         float wi = 0.0f, ri = 0.0f;
@@ -627,6 +629,125 @@ __global__ void __launch_bounds__(256) step_update_kernel(int32_t P,
         beta[(int64_t)k * P + a] += t * (double)delta[(int64_t)k * P + a];
 }
 
+// The Newton iteration's decisions on the device (engine.irls restated; the host reads the
+// verdicts back with the trial losses instead of recomputing them, so the step and the next
+// link are enqueued before the host has seen anything): per active fit q (slot act[q]),
+//   stage-1 Armijo over t in ts[1..4] of obj(t) = L(t) + (A + 2 t B + t^2 C) / 2: the first t
+//   with obj(t) - obj(0) <= sigma t g.d, or |obj(t) - obj(0)| <= 1e-13 |obj(0)|;
+//   scale = max(max|w + t d|, floor) (legacy: 1 + max|w + t d|), prop = max(max|d| / scale,
+//   |d_intercept|) (legacy: max|d| / scale), relv = t prop (with the secant's raw-step floor);
+//   stop on tol, stagnation (fresh Hessian, relv < 1e-4, no better than half the previous) or a
+//   failed search on a fresh Hessian; out of iterations; continue otherwise.
+// A fit whose stage-1 search fails goes to the host's stage 2: it keeps t = 0 here and a packed
+// R row (rpos) reserved.  Fits that continue (or await stage 2) get consecutive rows in act
+// order: rpos[q] (-1: none), nxt[0 .. *cnt) their slots.  f64 operations are written out
+// (_rn intrinsics, no contraction) in the order of the host's numpy expressions.
+enum DecideFlags {
+    kDecHit = 1, kDecStop = 2, kDecConv = 4, kDecOoi = 8, kDecTol = 16, kDecStag = 32,
+    kDecFail = 64, kDecLsFail = 128, kDecMore = 256, kDecRow = 512
+};
+constexpr int kDecT = 1024;
+__global__ void __launch_bounds__(kDecT) step_decide_kernel(
+    int32_t na, const int32_t* __restrict__ act, const double* __restrict__ L,
+    const double* __restrict__ sc, int32_t nts, const double* __restrict__ ts, double sigma,
+    double tol, double sfloor, int32_t legacy, const float* __restrict__ aa_rm,
+    const double* __restrict__ prev_rel, const uint8_t* __restrict__ fresh,
+    const int32_t* __restrict__ n_iter, const int32_t* __restrict__ max_iter,
+    double* __restrict__ step64, float* __restrict__ step32, double* __restrict__ relv_o,
+    double* __restrict__ prop_o, int32_t* __restrict__ flags, int32_t* __restrict__ tix_o,
+    int32_t* __restrict__ rpos, int32_t* __restrict__ nxt, int32_t* __restrict__ cnt) {
+    __shared__ int32_t sh[kDecT];
+    __shared__ int32_t base;
+    if (threadIdx.x == 0) base = 0;
+    __syncthreads();
+    const int W = 6 + nts;
+    for (int q0 = 0; q0 < na; q0 += kDecT) {
+        const int q = q0 + threadIdx.x;
+        int row = 0;
+        if (q < na) {
+            const double* Lq = L + (int64_t)q * 5;
+            const double* s = sc + (int64_t)q * W;
+            const double gdir = s[0], A = s[1], B = s[2], C = s[3], maxd = s[4];
+            const double maxdi = s[5 + nts];
+            double obj[5];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                const double t = ts[j];
+                const double lin = __dadd_rn(A, __dmul_rn(__dmul_rn(2.0, t), B));
+                const double quad = __dadd_rn(lin, __dmul_rn(__dmul_rn(t, t), C));
+                obj[j] = __dadd_rn(Lq[j], __dmul_rn(0.5, quad));
+            }
+            int tix = 0;
+            for (int j = 1; j < 5; ++j) {
+                const double dlt = __dsub_rn(obj[j], obj[0]);
+                const bool ok = dlt <= __dmul_rn(__dmul_rn(sigma, ts[j]), gdir) ||
+                                fabs(dlt) <= __dmul_rn(1e-13, fabs(obj[0]));
+                if (ok) { tix = j; break; }
+            }
+            const bool hit = tix > 0;
+            const double step = hit ? ts[tix] : 0.0;
+            int f = hit ? kDecHit : kDecMore;
+            double relv = 0.0, prop = 0.0;
+            if (hit) {
+                const double mb = s[5 + tix];
+                double scale, pr;
+                if (legacy) {
+                    scale = __dadd_rn(1.0, mb);
+                    pr = __ddiv_rn(maxd, scale);
+                } else {
+                    scale = fmax(mb, sfloor);
+                    pr = fmax(__ddiv_rn(maxd, scale), maxdi);
+                }
+                prop = pr;
+                relv = __dmul_rn(step, pr);
+                if (aa_rm) {
+                    const int k = act[q];
+                    const double rm0 = (double)aa_rm[2 * k], rm1 = (double)aa_rm[2 * k + 1];
+                    relv = fmax(relv, fmax(__ddiv_rn(rm0, scale), rm1));
+                }
+                const bool fr = fresh[q] != 0;
+                const bool stop_tol = relv <= tol;
+                const bool stop_stag = !stop_tol && fr && relv < 1e-4 &&
+                                       relv >= __dmul_rn(0.5, prev_rel[q]);
+                const bool stop = stop_tol || stop_stag;
+                const bool ooi = !stop && (n_iter[q] + 1 >= max_iter[q]);
+                if (stop_tol) f |= kDecTol | kDecConv;
+                if (stop_stag) f |= kDecStag;
+                if (stop) f |= kDecStop;
+                if (ooi) f |= kDecOoi;
+                row = !stop && !ooi;
+            } else {
+                row = 1;                                   // stage 2 decides; a row reserved
+            }
+            if (row) f |= kDecRow;
+            step64[q] = step;
+            step32[q] = (float)step;
+            relv_o[q] = relv;
+            prop_o[q] = prop;
+            flags[q] = f;
+            tix_o[q] = tix;
+        }
+        // rows in act order: inclusive scan of the row flags of this chunk
+        sh[threadIdx.x] = row;
+        __syncthreads();
+        for (int o = 1; o < kDecT; o <<= 1) {
+            const int v = threadIdx.x >= o ? sh[threadIdx.x - o] : 0;
+            __syncthreads();
+            sh[threadIdx.x] += v;
+            __syncthreads();
+        }
+        if (q < na) {
+            const int pos = base + sh[threadIdx.x] - row;
+            rpos[q] = row ? pos : -1;
+            if (row) nxt[pos] = act[q];
+        }
+        __syncthreads();
+        if (threadIdx.x == kDecT - 1) base += sh[kDecT - 1];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *cnt = base;
+}
+
 static unsigned grid1(int64_t work, int64_t per_block, unsigned cap = 8192) {
     int64_t g = (work + per_block - 1) / per_block;
     if (g < 1) g = 1;
@@ -760,7 +881,25 @@ int sglm_link_update(int32_t family, float power, int64_t n, int64_t ld, int32_t
     dim3 grid(grid1(ld, 256, 1024), (unsigned)B);
     link_kernel<<<grid, 256, 0, as_stream(stream)>>>(family, power, n, ld, slots, eta, Y, M,
                                                      fit_resp, fit_mask, W, R, (__bf16*)Rp,
-                                                     (B + 31) / 32 * 32, step, deta);
+                                                     (B + 31) / 32 * 32, step, deta, nullptr);
+    return check_launch("link_kernel");
+}
+
+int sglm_link_update_rp(int32_t family, float power, int64_t n, int64_t ld, int32_t B,
+                        const int32_t* slots, float* eta, const float* Y, const uint8_t* M,
+                        const int32_t* fit_resp, const int32_t* fit_mask, float* W, float* R,
+                        void* Rp, int32_t Bp, const int32_t* rpos, const float* step,
+                        const float* deta, sglm_stream_t stream) {
+    if (B <= 0) return SGLM_OK;
+    if (!eta || !Y || !M || !fit_resp || !fit_mask || !W || (!R && !Rp) || !slots ||
+        (Rp && (!rpos || Bp < B || Bp % 32)) || (deta && !step)) {
+        set_error("sglm_link_update_rp: bad args");
+        return SGLM_EINVAL;
+    }
+    dim3 grid(grid1(ld, 256, 1024), (unsigned)B);
+    link_kernel<<<grid, 256, 0, as_stream(stream)>>>(family, power, n, ld, slots, eta, Y, M,
+                                                     fit_resp, fit_mask, W, R, (__bf16*)Rp, Bp,
+                                                     step, deta, rpos);
     return check_launch("link_kernel");
 }
 
@@ -891,6 +1030,26 @@ int sglm_step_scalars(int32_t P, int32_t ncoef, int32_t B, const int32_t* slots,
     step_scalars_kernel<<<(unsigned)B, 256, 0, as_stream(stream)>>>(P, ncoef, slots, g, beta,
                                                                     delta, lamp, t, T, out);
     return check_launch("step_scalars_kernel");
+}
+
+int sglm_step_decide(int32_t na, const int32_t* act, const double* L, const double* sc,
+                     int32_t nts, const double* ts, double sigma, double tol, double sfloor,
+                     int32_t legacy, const float* aa_rm, const double* prev_rel,
+                     const uint8_t* fresh, const int32_t* n_iter, const int32_t* max_iter,
+                     double* step64, float* step32, double* relv, double* prop, int32_t* flags,
+                     int32_t* tix, int32_t* rpos, int32_t* nxt, int32_t* cnt,
+                     sglm_stream_t stream) {
+    if (na <= 0) return SGLM_OK;
+    if (!act || !L || !sc || !ts || nts < 5 || nts > kMaxStepT || !prev_rel || !fresh ||
+        !n_iter || !max_iter || !step64 || !step32 || !relv || !prop || !flags || !tix ||
+        !rpos || !nxt || !cnt) {
+        set_error("sglm_step_decide: bad args");
+        return SGLM_EINVAL;
+    }
+    step_decide_kernel<<<1, kDecT, 0, as_stream(stream)>>>(
+        na, act, L, sc, nts, ts, sigma, tol, sfloor, legacy, aa_rm, prev_rel, fresh, n_iter,
+        max_iter, step64, step32, relv, prop, flags, tix, rpos, nxt, cnt);
+    return check_launch("step_decide_kernel");
 }
 
 int sglm_step_update(int32_t P, int32_t B, const int32_t* slots, const double* step,

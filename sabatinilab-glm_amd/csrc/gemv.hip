@@ -596,8 +596,8 @@ __device__ __forceinline__ void mmaX(const StepX& t, int h, f32x16 (&ah)[kXT],
 
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 xtr_bits_kernel(const u32x2* __restrict__ cbits, int64_t ld, int32_t P, int64_t nblk,
-                const __bf16* __restrict__ Rp, int32_t Bp, int32_t B, int32_t splits,
-                float* __restrict__ part) {
+                const __bf16* __restrict__ Rp, int32_t Bp, int32_t Bps, int32_t B,
+                int32_t splits, float* __restrict__ part) {
     const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
     const int npan = P / (32 * kXT), ngrp = Bp / 32;
     const int L = xcd_logical(blockIdx.x, npan * ngrp * splits);
@@ -610,7 +610,7 @@ xtr_bits_kernel(const u32x2* __restrict__ cbits, int64_t ld, int32_t P, int64_t 
     const uint32_t avo = (uint32_t)((pn * (32 * kXT) + r) * 8);
     const uint64_t bbase = (uint64_t)(Rp + blk0 * 64);
     const uint32_t bvo = (uint32_t)(((int64_t)(g * 32 + r) * ld + 8 * h) * 2);
-    const uint64_t plane = (uint64_t)Bp * ld * 2;
+    const uint64_t plane = (uint64_t)Bps * ld * 2;     // rows per R piece plane
 
     f32x16 ah[kXT], al[kXT];
 #pragma unroll
@@ -667,8 +667,8 @@ constexpr int kRS = 144;            // LDS bytes per fit segment (128 + pad)
 template <int NGW, int WPE = 1>
 __global__ void __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 xtr_bits4_kernel(const u32x2* __restrict__ cbits, int64_t ld, int32_t P, int64_t nblk,
-                 const __bf16* __restrict__ Rp, int32_t Bp, int32_t B, int32_t splits,
-                 float* __restrict__ part) {
+                 const __bf16* __restrict__ Rp, int32_t Bp, int32_t Bps, int32_t B,
+                 int32_t splits, float* __restrict__ part) {
     constexpr int kF = NGW * 32;                 // fits per workgroup
     constexpr int kJ = 3 * NGW;                  // staging chunks per thread
     __shared__ __attribute__((aligned(16))) char lds[2][3 * kF * kRS];
@@ -687,7 +687,7 @@ xtr_bits4_kernel(const u32x2* __restrict__ cbits, int64_t ld, int32_t P, int64_t
     // R staging: thread tid moves 16-B chunks c = tid + 256 j of the step's tile: piece
     // c / (256 NGW), fit (c >> 3) % kF, chunk c & 7 of that fit's 128-B row segment
     const char* rb = reinterpret_cast<const char*>(Rp) + blk0 * 128;
-    const int64_t plane = (int64_t)Bp * ld * 2;
+    const int64_t plane = (int64_t)Bps * ld * 2;       // rows per R piece plane
     // chunk j: piece j / NGW, fit (tid >> 3) + 32 (j % NGW) -- a per-thread base plus
     // wave-uniform strides (kept in scalar registers)
     const int64_t gbase = (int64_t)(g0 * 32 + (tid >> 3)) * ld * 2 + (tid & 7) * 16;
@@ -863,8 +863,8 @@ __device__ __forceinline__ void xinterleave() {
 template <int NGW, int WPE = 1, int NPC = 3>
 __global__ void __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 xtr_bits5_kernel(const u32x2* __restrict__ cbits, int64_t ld, int32_t P, int64_t nblk,
-                 const __bf16* __restrict__ Rp, int32_t Bp, int32_t B, int32_t splits,
-                 float* __restrict__ part) {
+                 const __bf16* __restrict__ Rp, int32_t Bp, int32_t Bps, int32_t B,
+                 int32_t splits, float* __restrict__ part) {
     constexpr int kF = NGW * 32;                 // fits per workgroup
     constexpr int kJ = NPC * NGW;                // staging chunks per thread
     __shared__ __attribute__((aligned(16))) char lds[2][NPC * kF * kRS];
@@ -885,7 +885,7 @@ xtr_bits5_kernel(const u32x2* __restrict__ cbits, int64_t ld, int32_t P, int64_t
     const uint64_t rbase = (uint64_t)(reinterpret_cast<const char*>(Rp) + blk0 * 128 +
                                       (int64_t)g0 * 32 * ld * 2);
     const uint32_t rvo = (uint32_t)((tid >> 3) * ld * 2 + (tid & 7) * 16);
-    const uint64_t plane = (uint64_t)Bp * ld * 2;
+    const uint64_t plane = (uint64_t)Bps * ld * 2;     // rows per R piece plane
     const uint64_t gstep = (uint64_t)32 * ld * 2;
     auto joff = [&](int j) {
         const int gi = j % NGW;
@@ -1022,8 +1022,8 @@ static int xtr_variant(int32_t P, int32_t B) {
 }
 
 static void launch_xtr_bits(const u32x2* cbits, int64_t ld, int32_t P, int64_t nblk,
-                            const __bf16* Rp, int32_t Bp, int32_t B, int32_t splits, float* part,
-                            hipStream_t s) {
+                            const __bf16* Rp, int32_t Bp, int32_t Bps, int32_t B, int32_t splits,
+                            float* part, hipStream_t s) {
     const int v = xtr_variant(P, B);
     const unsigned tiles = (unsigned)((P / (32 * kXT)) * (Bp / 32) * splits);
     const int ngw = v == 2 ? 2 : 1;
@@ -1033,25 +1033,25 @@ static void launch_xtr_bits(const u32x2* cbits, int64_t ld, int32_t P, int64_t n
     const bool pipe = v != 0 && xtr_pipe() && (int64_t)32 * ld * 2 < ((int64_t)1 << 32);
     if (pipe) {
         if (v == 3)
-            xtr_bits5_kernel<1, 2><<<wgs4, 64 * kXW, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, B,
+            xtr_bits5_kernel<1, 2><<<wgs4, 64 * kXW, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, Bps, B,
                                                              splits, part);
         else if (v == 2)
-            xtr_bits5_kernel<2><<<wgs4, 64 * kXW, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, B, splits,
+            xtr_bits5_kernel<2><<<wgs4, 64 * kXW, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, Bps, B, splits,
                                                           part);
         else
-            xtr_bits5_kernel<1><<<wgs4, 64 * kXW, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, B, splits,
+            xtr_bits5_kernel<1><<<wgs4, 64 * kXW, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, Bps, B, splits,
                                                           part);
         return;
     }
     if (v == 3)
-        xtr_bits4_kernel<1, 2><<<wgs4, 64 * kXW, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, B, splits,
+        xtr_bits4_kernel<1, 2><<<wgs4, 64 * kXW, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, Bps, B, splits,
                                                          part);
     else if (v == 2)
-        xtr_bits4_kernel<2><<<wgs4, 64 * kXW, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, B, splits, part);
+        xtr_bits4_kernel<2><<<wgs4, 64 * kXW, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, Bps, B, splits, part);
     else if (v == 1)
-        xtr_bits4_kernel<1><<<wgs4, 64 * kXW, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, B, splits, part);
+        xtr_bits4_kernel<1><<<wgs4, 64 * kXW, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, Bps, B, splits, part);
     else
-        xtr_bits_kernel<<<tiles, 64, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, B, splits, part);
+        xtr_bits_kernel<<<tiles, 64, 0, s>>>(cbits, ld, P, nblk, Rp, Bp, Bps, B, splits, part);
 }
 
 // out[slots[f]][a] = sum over slabs z of part[z][f][a] (f = e / P), fixed order
@@ -1256,7 +1256,7 @@ int sglm_xtr_bits(const uint32_t* cbits, int64_t ld, int32_t P, int64_t n, const
                     s>>>(R, ld, B, Bp, nullptr, Rp);
     int st = check_launch("split3_kernel");
     if (st) return st;
-    launch_xtr_bits(reinterpret_cast<const u32x2*>(cbits), ld, P, nblk, Rp, Bp, B, splits,
+    launch_xtr_bits(reinterpret_cast<const u32x2*>(cbits), ld, P, nblk, Rp, Bp, Bp, B, splits,
                     part, s);
     st = check_launch("xtr_bits_kernel");
     if (st) return st;
@@ -1343,11 +1343,11 @@ int sglm_xtr_bits_int(const uint32_t* cbits, int64_t ld, int32_t P, int64_t n, c
     const u32x2* cb = reinterpret_cast<const u32x2*>(cbits);
     const __bf16* Db = reinterpret_cast<const __bf16*>(D);
     if (ngw == 4)
-        xtr_bits5_kernel<4, 1, 1><<<wgs, 64 * kXW, 0, s>>>(cb, ld, P, nblk, Db, Bp, B, splits, part);
+        xtr_bits5_kernel<4, 1, 1><<<wgs, 64 * kXW, 0, s>>>(cb, ld, P, nblk, Db, Bp, Bp, B, splits, part);
     else if (ngw == 2)
-        xtr_bits5_kernel<2, 1, 1><<<wgs, 64 * kXW, 0, s>>>(cb, ld, P, nblk, Db, Bp, B, splits, part);
+        xtr_bits5_kernel<2, 1, 1><<<wgs, 64 * kXW, 0, s>>>(cb, ld, P, nblk, Db, Bp, Bp, B, splits, part);
     else
-        xtr_bits5_kernel<1, 1, 1><<<wgs, 64 * kXW, 0, s>>>(cb, ld, P, nblk, Db, Bp, B, splits, part);
+        xtr_bits5_kernel<1, 1, 1><<<wgs, 64 * kXW, 0, s>>>(cb, ld, P, nblk, Db, Bp, Bp, B, splits, part);
     int st = check_launch("xtr_bits5_kernel<1 piece>");
     if (st) return st;
     const int64_t len = (int64_t)B * P;
@@ -1359,18 +1359,27 @@ int sglm_xtr_bits_int(const uint32_t* cbits, int64_t ld, int32_t P, int64_t n, c
 int sglm_xtr_bits_packed(const uint32_t* cbits, int64_t ld, int32_t P, int64_t n,
                          const void* Rp, int32_t B, const int32_t* slots, double* G, void* work,
                          sglm_stream_t stream) {
+    return sglm_xtr_bits_packed_bp(cbits, ld, P, n, Rp, B, (B + 31) / 32 * 32, slots, G, work,
+                                   stream);
+}
+
+int sglm_xtr_bits_packed_bp(const uint32_t* cbits, int64_t ld, int32_t P, int64_t n,
+                            const void* Rp, int32_t B, int32_t Bp, const int32_t* slots,
+                            double* G, void* work, sglm_stream_t stream) {
     if (B <= 0) return SGLM_OK;
-    if (!cbits || !Rp || !G || !work || ld % 256 || P % 256 || n > ld) {
+    if (!cbits || !Rp || !G || !work || ld % 256 || P % 256 || n > ld || Bp % 32 ||
+        Bp < (B + 31) / 32 * 32) {
         set_error("sglm_xtr_bits_packed: bad args");
         return SGLM_EINVAL;
     }
-    const int32_t Bp = (B + 31) / 32 * 32;
     const int64_t nblk = (n + 63) / 64;
     const int splits = xtr_bits_splits(P, B, ld / 64);
     hipStream_t s = as_stream(stream);
     float* part = reinterpret_cast<float*>(work);
+    // Bp: the planes' row stride (>= the fit groups' padded count, which the kernels use)
     launch_xtr_bits(reinterpret_cast<const u32x2*>(cbits), ld, P, nblk,
-                    reinterpret_cast<const __bf16*>(Rp), Bp, B, splits, part, s);
+                    reinterpret_cast<const __bf16*>(Rp), (B + 31) / 32 * 32, Bp, B, splits, part,
+                    s);
     int st = check_launch("xtr_bits_kernel");
     if (st) return st;
     const int64_t len = (int64_t)B * P;

@@ -32,6 +32,8 @@ SIGNATURES = {
     "sglm_gemv_eta": (C.c_int, [_vp, _i32, _i64, _i32, _i64, _vp, _i32, _vp, _vp]),
     "sglm_link_update": (C.c_int, [_i32, _f32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
                                    _vp, _vp, _vp, _vp, _vp, _vp]),
+    "sglm_link_update_rp": (C.c_int, [_i32, _f32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
+                                      _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp]),
     "sglm_xtr_work_bytes": (_sz, [_i32, _i32, _i64]),
     "sglm_xtr": (C.c_int, [_vp, _i32, _i64, _i32, _i64, _vp, _i32, _vp, _vp, _vp]),
     "sglm_syrk_work_bytes": (_sz, [_i32, _i32, _i32]),
@@ -51,6 +53,8 @@ SIGNATURES = {
     "sglm_xtr_bits": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _i32, _vp, _vp, _vp]),
     "sglm_xtr_bits_packed_work_bytes": (_sz, [_i32, _i32, _i64]),
     "sglm_xtr_bits_packed": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _i32, _vp, _vp, _vp, _vp]),
+    "sglm_xtr_bits_packed_bp": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _i32, _i32, _vp, _vp, _vp,
+                                          _vp]),
     "sglm_xtr_bits_int_work_bytes": (_sz, [_i32, _i32, _i64]),
     "sglm_xtr_bits_int": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _i32, _vp, _vp, _vp]),
     "sglm_event_bits": (C.c_int, [_vp, _i64, _i32, _i64, _vp, _i64, _vp]),
@@ -91,6 +95,9 @@ SIGNATURES = {
                                       _vp, _vp]),
     "sglm_step_scalars": (C.c_int, [_i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
     "sglm_step_update": (C.c_int, [_i32, _i32, _vp, _vp, _vp, _vp, _vp]),
+    "sglm_step_decide": (C.c_int, [_i32, _vp, _vp, _vp, _i32, _vp, C.c_double, C.c_double,
+                                   C.c_double, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                   _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "sglm_mask_stats_work_bytes": (_sz, [_i32, _i32, _i64]),
     "sglm_mask_stats": (C.c_int, [_vp, _i64, _i32, _vp, _i32, _i64, _vp, C.c_double, _vp, _vp,
                                   _vp]),

@@ -60,6 +60,12 @@ LAG_XTR = __import__("os").environ.get("SGLM_LAG_XTR", "0") == "1"
 ETA_BITS = True                # eta on the MFMA from row-major bit-planes for 0/1 designs
 ETA_FINAL_ALL = False          # recompute every fit's final eta (else only ETA_FINAL_ITERS+)
 ETA_FINAL_ITERS = 8
+# the Newton decisions (stage-1 Armijo, stopping rule) on the device (sglm_step_decide), the
+# step and the next link enqueued before the host reads the iteration back.  Off by default:
+# measured slower on the C4 grid (47.9 vs 46.8 ms, interleaved A/B on one box) -- the link then
+# runs over every active fit, stopped ones included, and the host still waits for the next
+# Hessian plan's readback behind it, so little host time leaves the critical path
+DEV_DECIDE = __import__("os").environ.get("SGLM_DEV_DECIDE", "0") == "1"
 SYRK_CBITS = True              # ... and its row-compacted register-only form (v6) when fits
                                # carry masks (the default path for event designs)
 # Hessian reuse (log-link families): a fit keeps its last Hessian factor while the drift of
@@ -1904,6 +1910,19 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
     if use_lag:
         lag_work = _work(_lib.query("sglm_lag_xtr_work_bytes", P, d.lag.K, B0, n), dev, "xtr")
     R_out, Rp_out = (_p(bf.R), None) if use_lag else (None, _p(rp_buf) if use_rp else None)
+    # device-side decisions (packed-R designs, one process): the iteration's verdicts come back
+    # with its losses while the step and the next link already run; the next gradient reads the
+    # packed R rows of the fits that continue at the positions the device gave them
+    dev_dec = DEV_DECIDE and use_rp and comm is None
+    if dev_dec:
+        dec64 = torch.empty((3, B0), dtype=torch.float64, device=dev)     # step, relv, prop
+        dec32 = torch.empty(B0, dtype=torch.float32, device=dev)          # step (f32)
+        deci = torch.empty(4 * B0 + 1, dtype=torch.int32, device=dev)     # flags tix rpos nxt cnt
+        dec64_h = _pinned("dec64", 3 * B0, torch.float64)
+        deci_h = _pinned("deci", 4 * B0 + 1, torch.int32)
+        ev_dec = torch.cuda.Event()
+    grad_d, grad_n, grad_bp = None, 0, 0     # the gradient's slots, count and R plane stride
+    dev_linked = False                       # this iteration's link ran at the previous one's end
 
     import time
     tick = stats.mark if (stats is not None and (stats.trace_phases or stats.host_phases)) \
@@ -1918,8 +1937,12 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
         na = int(act.size)
         if na == 0:
             break
-        act_d = linked if linked is not None else up(act, np.int32)
-        if fused:
+        if dev_linked:
+            act_d = up(act, np.int32)        # the gradient keeps the device's list (grad_d)
+        else:
+            act_d = linked if linked is not None else up(act, np.int32)
+            grad_d, grad_n, grad_bp = act_d, na, pad_to(na, 32)
+        if fused and not dev_linked:
             if linked is None:
                 _lib.call("sglm_link_update", fam, power, n, ld, na, _p(act_d), _p(bf.eta),
                           _p(prob.Y), _p(prob.M), _p(fit_resp), _p(fit_mask), _p(bf.W), R_out,
@@ -1950,13 +1973,13 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
                 if cochain:
                     _lib.call("sglm_xtr_prefer", 1)
                 try:
-                    _lib.call("sglm_xtr_bits_packed", _p(d.cbits_full()), ld, P, n, _p(rp_buf),
-                              na, _p(act_d), _p(bf.g), _p(gx_work), st)
+                    _lib.call("sglm_xtr_bits_packed_bp", _p(d.cbits_full()), ld, P, n,
+                              _p(rp_buf), grad_n, grad_bp, _p(grad_d), _p(bf.g), _p(gx_work), st)
                 finally:
                     if cochain:
                         _lib.call("sglm_xtr_prefer", -1)
                 # a mixed design's continuous coordinates, float64 from the same packed R
-                d.mix_xtr(2, rp_buf, ld, pad_to(na, 32), None, act_d, na, bf.g)
+                d.mix_xtr(2, rp_buf, ld, grad_bp, None, grad_d, grad_n, bf.g)
             else:
                 d.xtr(bf.R, B, bf.g)
             if comm is not None:
@@ -2218,8 +2241,34 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
         if use_aa:
             aa_rm_h.copy_(aa_rm.view(-1), non_blocking=True)
             aa_used[aa_idx] = bf.delta[aa_idx]       # the rounded directions the step uses
+        if dev_dec:
+            up.batch()
+            prev_d = up(prev_rel[act], np.float64)
+            fresh_d = up(((gram_now[act] & exact_h[act]) | const_hess).astype(np.uint8))
+            nit_d = up(n_iter[act], np.int32)
+            mit_d = up(max_iter[act], np.int32)
+            up.flush()
+            _lib.call("sglm_step_decide", na, _p(act_d), _p(Ltr), _p(sc), nts, _p(ts_all),
+                      ARMIJO_SIGMA, float(tol), STOP_SCALE_FLOOR, int(STOP_LEGACY),
+                      _p(aa_rm) if use_aa else None, _p(prev_d), _p(fresh_d), _p(nit_d),
+                      _p(mit_d), _p(dec64[0]), _p(dec32), _p(dec64[1]), _p(dec64[2]), _p(deci),
+                      _p(deci[B0:]), _p(deci[2 * B0:]), _p(deci[3 * B0:]), _p(deci[4 * B0:]), st)
+            dec64_h.copy_(dec64.view(-1), non_blocking=True)
+            deci_h.copy_(deci, non_blocking=True)
+            ev_dec.record()
+            # the step (coefficients) and the next link with the fused predictor update, for
+            # every active fit (t = 0 where stage 2 decides): the GPU runs them while the host
+            # reads the verdicts and plans the next iteration
+            _lib.call("sglm_step_update", P, na, _p(act_d), _p(dec64[0]), _p(bf.delta),
+                      _p(beta64_d), st)
+            _lib.call("sglm_link_update_rp", fam, power, n, ld, na, _p(act_d), _p(bf.eta),
+                      _p(prob.Y), _p(prob.M), _p(fit_resp), _p(fit_mask), _p(bf.W), None,
+                      _p(rp_buf), pad_to(na, 32), _p(deci[2 * B0:]), _p(dec32), _p(bf.deta), st)
         t_sync = time.perf_counter()
-        torch.cuda.current_stream().synchronize()              # the iteration's round trip
+        if dev_dec:
+            ev_dec.synchronize()                 # the iteration's round trip (not the link)
+        else:
+            torch.cuda.current_stream().synchronize()          # the iteration's round trip
         if stats is not None:
             stats.sync_wait_s += time.perf_counter() - t_sync
             stats.roundtrips += 1
@@ -2235,15 +2284,24 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
         def objectives(Lm, tv):
             return Lm + 0.5 * (A_[:, None] + 2 * tv[None, :] * B_[:, None]
                                + tv[None, :] ** 2 * C_[:, None])
-        step_a = np.zeros(na)
-        tix = np.zeros(na, dtype=np.int64)      # index of the chosen step in TS_ALL
-        obj = objectives(L, ts)
-        ok = ((obj[:, 1:] - obj[:, :1] <= ARMIJO_SIGMA * ts[None, 1:] * gdir[:, None]) |
-              (np.abs(obj[:, 1:] - obj[:, :1]) <= 1e-13 * np.abs(obj[:, :1])))
-        first = np.argmax(ok, axis=1)
-        hit = ok[np.arange(na), first]
-        step_a[hit] = ts[1:][first[hit]]
-        tix[hit] = 1 + first[hit]
+        if dev_dec:
+            # the device's stage-1 verdicts (sglm_step_decide)
+            dh = dec64_h.numpy().reshape(3, B0)
+            di = deci_h.numpy()
+            step_a = dh[0, :na].copy()
+            tix = di[B0:B0 + na].astype(np.int64)
+            dflags = di[:na].copy()
+            hit = (dflags & 1) != 0
+        else:
+            step_a = np.zeros(na)
+            tix = np.zeros(na, dtype=np.int64)  # index of the chosen step in TS_ALL
+            obj = objectives(L, ts)
+            ok = ((obj[:, 1:] - obj[:, :1] <= ARMIJO_SIGMA * ts[None, 1:] * gdir[:, None]) |
+                  (np.abs(obj[:, 1:] - obj[:, :1]) <= 1e-13 * np.abs(obj[:, :1])))
+            first = np.argmax(ok, axis=1)
+            hit = ok[np.arange(na), first]
+            step_a[hit] = ts[1:][first[hit]]
+            tix[hit] = 1 + first[hit]
         more = np.flatnonzero(~hit)                         # positions in act
         if more.size:
             sub_d = up(act[more], np.int32)
@@ -2302,18 +2360,53 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
         # a failed search on a fresh Hessian: converged only if the proposed step itself is
         # within tol (the iterate already sits at the minimiser up to rounding)
         stop_fail = ls_fail & fresh
+        if dev_dec and hit.any():
+            # the device's verdicts for the fits its stage 1 decided (the packed R rows of the
+            # next gradient follow them); the host's own formulas only for the stage-2 fits
+            relv[hit] = dh[1, :na][hit]
+            prop[hit] = dh[2, :na][hit]
+            stop_tol[hit] = (dflags[hit] & 16) != 0
+            stop_stag[hit] = (dflags[hit] & 32) != 0
         stop = stop_tol | stop_stag | stop_fail
         conv_now = stop_tol | (stop_fail & (prop <= tol))
         n_iter[act] += 1
         out_of_iters = ~stop & (n_iter[act] >= max_iter[act])
         cont = ~stop & ~out_of_iters
         nxt = act[cont]
+        if dev_dec and not np.array_equal(cont[hit], (dflags[hit] & 512) != 0):
+            raise RuntimeError("sglm_step_decide disagrees with the host's stopping rule")
         # predictor update eta += t d_eta: fused into the next iteration's link for the fits
         # that continue (0/1 designs), a plain axpy for the others
         linked = None
         up.batch()
         step_d = up(step_a, np.float64)
-        if fused and nxt.size:
+        if dev_dec:
+            # the device enqueued the step and the link; the stage-2 fits (t = 0 there) take
+            # their step now, and those that continue refresh their link at the same rows
+            if more.size:
+                mv = more[step_a[more] != 0.0]
+                if mv.size:
+                    mv_d = up(act[mv], np.int32)
+                    ms_d = up(step_a[mv], np.float64)
+                    mt_d = up(step_a[mv], np.float32)
+                    mc = mv[cont[mv]]
+                    if mc.size:
+                        mc_d = up(act[mc], np.int32)
+                        mr_d = up(di[2 * B0:2 * B0 + na][mc], np.int32)
+                    up.flush()
+                    _lib.call("sglm_step_update", P, int(mv.size), _p(mv_d), _p(ms_d),
+                              _p(bf.delta), _p(beta64_d), st)
+                    _lib.call("sglm_eta_axpy", n, ld, int(mv.size), _p(mv_d), _p(mt_d),
+                              _p(bf.deta), _p(bf.eta), st)
+                    if mc.size:
+                        _lib.call("sglm_link_update_rp", fam, power, n, ld, int(mc.size),
+                                  _p(mc_d), _p(bf.eta), _p(prob.Y), _p(prob.M), _p(fit_resp),
+                                  _p(fit_mask), _p(bf.W), None, _p(rp_buf), pad_to(na, 32),
+                                  _p(mr_d), None, None, st)
+            up.flush()
+            grad_d, grad_n, grad_bp = deci[3 * B0:], int(di[4 * B0]), pad_to(na, 32)
+            dev_linked = True
+        elif fused and nxt.size:
             done = np.flatnonzero(~cont & (step_a != 0.0))
             if done.size:
                 done_d, tdone_d = up(act[done], np.int32), up(step_a[done], np.float32)
