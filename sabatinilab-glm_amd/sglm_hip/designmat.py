@@ -80,8 +80,13 @@ class _Stage:
         if self.ev[k] is not None:
             self.ev[k].synchronize()
         if self.h[k] is None or self.h[k].numel() < o:
-            self.h[k] = torch.empty(max(o, 256) * 2, dtype=torch.uint8).pin_memory()
-            self.d[k] = torch.empty(self.h[k].numel(), dtype=torch.uint8, device=dev)
+            # every slot at once (page-locking is slow: not once per call of the first few)
+            size = max(o, 256) * 2
+            for j in range(self.SLOTS):
+                if self.ev[j] is not None:
+                    self.ev[j].synchronize()
+                self.h[j] = torch.empty(size, dtype=torch.uint8).pin_memory()
+                self.d[j] = torch.empty(size, dtype=torch.uint8, device=dev)
         hb = self.h[k].numpy()
         for a, off in zip(arrs, offs):
             hb[off:off + a.nbytes] = a.reshape(-1).view(np.uint8)
