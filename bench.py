@@ -72,8 +72,10 @@ INIT_PASSES = 2
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default 2; 20 for the millisecond-scale designmat step)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 1; 3 for "
+                    "designmat)")
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-check", action="store_true",
@@ -93,7 +95,13 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI) for real runs; gloo to rehearse several ranks "
                          "on fewer GPUs")
-    return ap.parse_args()
+    a = ap.parse_args()
+    short = a.config == "designmat"
+    if a.steps is None:
+        a.steps = 20 if short else 2
+    if a.warmup is None:
+        a.warmup = 3 if short else 1
+    return a
 
 
 def dense_slice(s, rows):
