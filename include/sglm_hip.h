@@ -443,6 +443,14 @@ int sglm_step_decide(int32_t na, const int32_t* act, const double* L, const doub
                      double* step64, float* step32, double* relv, double* prop, int32_t* flags,
                      int32_t* tix, int32_t* rpos, int32_t* nxt, int32_t* cnt,
                      sglm_stream_t stream);
+/* sglm_aa_step: the Anderson (secant) correction of the Newton directions of the na active
+ * fits (slots; engine.irls ANDERSON) in one launch: where sel[q], delta[k] becomes f - gamma (db
+ * + df) (f = delta[k], df = f - raw_prev[k], db = used_prev[k] * tprev[q], gamma = df.f / df.df)
+ * when that is a descent direction with gamma in [-2, 0.5]; rm[k] = (max_{j<p} |f_j|, |f_p|)
+ * there, (0, 0) elsewhere; raw_prev[k] = f for every fit.  float32, fixed-order sums. */
+int sglm_aa_step(int32_t P, int32_t p, int32_t na, const int32_t* slots, const uint8_t* sel,
+                 const float* tprev, float* delta, float* raw_prev, const float* used_prev,
+                 const double* gtot, float* rm, sglm_stream_t stream);
 int sglm_step_update(int32_t P, int32_t B, const int32_t* slots, const double* step,
                      const float* delta, double* beta, sglm_stream_t stream);
 

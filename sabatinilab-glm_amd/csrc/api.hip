@@ -616,6 +616,86 @@ __global__ void __launch_bounds__(256) step_scalars_kernel(
     }
 }
 
+// The Anderson (secant) correction of the Newton directions (engine.irls, ANDERSON), one
+// workgroup per active fit k = slots[q]: f = delta[k] (this iteration's raw direction); where
+// sel[q] (the same factor as the previous step, which was taken with t = tprev[q]):
+//   df = f - raw_prev, db = used_prev * t, gamma = df.f / max(df.df, 1e-30),
+//   d = f - gamma (db + df), kept when df.df > 1e-12 f.f, gamma in [-2, 0.5] and g.d < 0;
+// rm[k] = (max_{j < p} |f_j|, |f_p|) for those (0 elsewhere), raw_prev[k] = f for every fit.
+// float32 as the torch expressions it replaces; sums in a fixed order.
+__global__ void __launch_bounds__(256) aa_step_kernel(int32_t P, int32_t p,
+                                                      const int32_t* __restrict__ slots,
+                                                      const uint8_t* __restrict__ sel,
+                                                      const float* __restrict__ tprev,
+                                                      float* __restrict__ delta,
+                                                      float* __restrict__ raw_prev,
+                                                      const float* __restrict__ used_prev,
+                                                      const double* __restrict__ gtot,
+                                                      float* __restrict__ rm) {
+    __shared__ float sh[4][8];
+    const int q = blockIdx.x, k = slots[q];
+    float* d = delta + (int64_t)k * P;
+    float* rp = raw_prev + (int64_t)k * P;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (!sel[q]) {
+        for (int a = tid; a < P; a += 256) rp[a] = d[a];
+        if (tid == 0) { rm[2 * k] = 0.0f; rm[2 * k + 1] = 0.0f; }
+        return;
+    }
+    const float t = tprev[q];
+    const float* up_ = used_prev + (int64_t)k * P;
+    const double* g = gtot + (int64_t)k * P;
+    float den = 0.0f, num = 0.0f, ff = 0.0f, mx = 0.0f, fp = 0.0f;
+    for (int a = tid; a < P; a += 256) {
+        const float f = d[a];
+        const float df = f - rp[a];
+        den = fmaf(df, df, den);
+        num = fmaf(df, f, num);
+        ff = fmaf(f, f, ff);
+        if (a < p) mx = fmaxf(mx, fabsf(f));
+        if (a == p) fp = fabsf(f);
+    }
+    auto wsum = [&](float v) { for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64); return v; };
+    den = wsum(den); num = wsum(num); ff = wsum(ff);
+    for (int o = 32; o > 0; o >>= 1) {
+        mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+        fp = fmaxf(fp, __shfl_xor(fp, o, 64));
+    }
+    if (lane == 0) {
+        sh[w][0] = den; sh[w][1] = num; sh[w][2] = ff; sh[w][3] = mx; sh[w][5] = fp;
+    }
+    __syncthreads();
+    den = sh[0][0] + sh[1][0] + sh[2][0] + sh[3][0];
+    num = sh[0][1] + sh[1][1] + sh[2][1] + sh[3][1];
+    ff = sh[0][2] + sh[1][2] + sh[2][2] + sh[3][2];
+    mx = fmaxf(fmaxf(sh[0][3], sh[1][3]), fmaxf(sh[2][3], sh[3][3]));
+    fp = fmaxf(fmaxf(sh[0][5], sh[1][5]), fmaxf(sh[2][5], sh[3][5]));
+    const float gam = num / fmaxf(den, 1e-30f);
+    // g.d of the corrected direction
+    float gdn = 0.0f;
+    for (int a = tid; a < P; a += 256) {
+        const float f = d[a];
+        const float df = f - rp[a];
+        const float db = up_[a] * t;
+        const float dn = f - gam * (db + df);
+        gdn = fmaf((float)g[a], dn, gdn);
+    }
+    gdn = wsum(gdn);
+    __syncthreads();
+    if (lane == 0) sh[w][4] = gdn;
+    __syncthreads();
+    gdn = sh[0][4] + sh[1][4] + sh[2][4] + sh[3][4];
+    const bool good = den > 1e-12f * ff && gam >= -2.0f && gam <= 0.5f && gdn < 0.0f;
+    for (int a = tid; a < P; a += 256) {
+        const float f = d[a];
+        const float df = f - rp[a];
+        const float db = up_[a] * t;
+        if (good) d[a] = f - gam * (db + df);
+        rp[a] = f;
+    }
+    if (tid == 0) { rm[2 * k] = mx; rm[2 * k + 1] = fp; }
+}
+
 // beta[k] += step[q] * delta[k] for k = slots[q] (float64 coefficients, f32 direction)
 __global__ void __launch_bounds__(256) step_update_kernel(int32_t P,
                                                           const int32_t* __restrict__ slots,
@@ -1050,6 +1130,20 @@ int sglm_step_decide(int32_t na, const int32_t* act, const double* L, const doub
         na, act, L, sc, nts, ts, sigma, tol, sfloor, legacy, aa_rm, prev_rel, fresh, n_iter,
         max_iter, step64, step32, relv, prop, flags, tix, rpos, nxt, cnt);
     return check_launch("step_decide_kernel");
+}
+
+int sglm_aa_step(int32_t P, int32_t p, int32_t na, const int32_t* slots, const uint8_t* sel,
+                 const float* tprev, float* delta, float* raw_prev, const float* used_prev,
+                 const double* gtot, float* rm, sglm_stream_t stream) {
+    if (na <= 0) return SGLM_OK;
+    if (!slots || !sel || !tprev || !delta || !raw_prev || !used_prev || !gtot || !rm ||
+        p < 0 || p >= P) {
+        set_error("sglm_aa_step: bad args");
+        return SGLM_EINVAL;
+    }
+    aa_step_kernel<<<(unsigned)na, 256, 0, as_stream(stream)>>>(P, p, slots, sel, tprev, delta,
+                                                                raw_prev, used_prev, gtot, rm);
+    return check_launch("aa_step_kernel");
 }
 
 int sglm_step_update(int32_t P, int32_t B, const int32_t* slots, const double* step,

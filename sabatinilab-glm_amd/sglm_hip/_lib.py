@@ -95,6 +95,7 @@ SIGNATURES = {
                                       _vp, _vp]),
     "sglm_step_scalars": (C.c_int, [_i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
     "sglm_step_update": (C.c_int, [_i32, _i32, _vp, _vp, _vp, _vp, _vp]),
+    "sglm_aa_step": (C.c_int, [_i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "sglm_step_decide": (C.c_int, [_i32, _vp, _vp, _vp, _i32, _vp, C.c_double, C.c_double,
                                    C.c_double, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                    _vp, _vp, _vp, _vp, _vp, _vp, _vp]),

@@ -66,6 +66,10 @@ ETA_FINAL_ITERS = 8
 # runs over every active fit, stopped ones included, and the host still waits for the next
 # Hessian plan's readback behind it, so little host time leaves the critical path
 DEV_DECIDE = __import__("os").environ.get("SGLM_DEV_DECIDE", "0") == "1"
+# the Anderson correction as one kernel (sglm_aa_step) instead of ~20 torch operations.
+# Parity-green but off by default: no measured gain on the C4 grid (46.0 vs 45.8 ms,
+# interleaved A/B) -- the torch ops overlap the host's own work, off the critical path
+AA_KERNEL = __import__("os").environ.get("SGLM_AA_KERNEL", "0") == "1"
 SYRK_CBITS = True              # ... and its row-compacted register-only form (v6) when fits
                                # carry masks (the default path for event designs)
 # Hessian reuse (log-link families): a fit keeps its last Hessian factor while the drift of
@@ -2193,9 +2197,19 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
             src_now = np.where(alias[act] >= 0, alias[act], act)
             key_now = src_now * 1_000_000 + fepoch[src_now]
             aa_idx = up(act, np.int64)
-            raw = bf.delta[aa_idx]                     # this iteration's raw directions
-            aa_rm.zero_()
-            sel = np.flatnonzero((aa_key[act] == key_now) & ~gram_now[act] & (aa_t[act] > 0))
+            selm = (aa_key[act] == key_now) & ~gram_now[act] & (aa_t[act] > 0)
+            sel = np.flatnonzero(selm)
+            if AA_KERNEL:
+                # one launch (sglm_aa_step): the correction, the raw directions kept, rm
+                _lib.call("sglm_aa_step", P, p, na, _p(act_d), _p(up(selm.astype(np.uint8))),
+                          _p(up(aa_t[act], np.float32)), _p(bf.delta), _p(aa_raw), _p(aa_used),
+                          _p(bf.gtot), _p(aa_rm), st)
+                if stats is not None:
+                    stats.aa_fit_iters += int(sel.size)
+                sel = sel[:0]
+            else:
+                raw = bf.delta[aa_idx]                 # this iteration's raw directions
+                aa_rm.zero_()
             if sel.size:
                 # d = f - gamma (dbeta + df), gamma = df.f / df.df (f: raw direction, df its
                 # change on the same factor, dbeta the previous step taken); kept only when
@@ -2214,7 +2228,8 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
                 aa_rm[aa_idx[sel_d], 1] = f[:, p].abs()
                 if stats is not None:
                     stats.aa_fit_iters += int(sel.size)
-            aa_raw[aa_idx] = raw
+            if not AA_KERNEL:
+                aa_raw[aa_idx] = raw
             aa_key[act] = key_now
         # the directions are rounded to bf16 in place (X d on one MFMA piece); the step below
         # uses the rounded values, so eta stays X beta and the fixed point (exact gradient) is

@@ -281,7 +281,8 @@ def run_multi(X, y, groups: Sequence[dict], score_method: str = "mse", coef0=Non
     with ``holdout_rows`` every dict also carries ``refit_holdout_r2`` (R^2 / D^2) and
     ``refit_holdout_neg_mse`` — what ``training_fit_holdout_score`` reports for that param."""
     import time
-    tick = stats.mark if (stats is not None and stats.trace_phases) else (lambda name, t: t)
+    tick = stats.mark if (stats is not None and (stats.trace_phases or stats.host_phases)) \
+        else (lambda name, t: t)
     t0 = tick("-", time.perf_counter())
     from .comm import RowComm, SimComm, row_slab
     dist = _dist() if shard and simulate is None else None
