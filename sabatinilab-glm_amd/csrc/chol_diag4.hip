@@ -264,7 +264,12 @@ static __global__ void __launch_bounds__(256) chol_diag4q_kernel(
 // applies quad Q's terms to its other rows -- while the other waves apply theirs: the pivot
 // chain overlaps the update.  Rows of A and of V are held as pairs (a, v) so that both
 // rank-1 terms of an element are one v_pk_fma_f32.  Per element the same FMAs in the same
-// order as before.
+// order as before, except that a register group whose rows all precede quad Q (16 g + 15 < Q)
+// is not sent quad Q's terms: their multipliers U[Q+h][row] are exact zeros there (a no-op up
+// to the sign of a zero).  Timestamps inside the kernel (s_memtime, one fit, a probe build):
+// per quad ~1,700 clocks, of them ~250 the owner's apply to its next rows, ~820 its four
+// pivots, the rest its other rows' applies and the barrier; skipping the dead groups took the
+// 1-fit chain 1.00 -> 0.97 ms, 20 fits 2.90 -> 2.86 ms.
 typedef float f32x2v __attribute__((ext_vector_type(2)));
 
 // the owner's four pivots of quad Q (rows Q + h in registers 4 (Q >> 4) + h), published into
@@ -376,10 +381,11 @@ __device__ __forceinline__ void diag4l_block(float* __restrict__ Hall, int32_t P
                         &sm.scol[buf ^ 1][0][0], &sm.sx[buf ^ 1][0][0]);
 #pragma unroll
             for (int g = 0; g < 4; ++g)
-                if (g != gn) diag4l_apply(av, g, rb, cb, xb, w, c);
+                if (g != gn && 16 * g + 15 >= Q) diag4l_apply(av, g, rb, cb, xb, w, c);
         } else {
 #pragma unroll
-            for (int g = 0; g < 4; ++g) diag4l_apply(av, g, rb, cb, xb, w, c);
+            for (int g = 0; g < 4; ++g)
+                if (16 * g + 15 >= Q) diag4l_apply(av, g, rb, cb, xb, w, c);
         }
         __syncthreads();
     }
