@@ -464,16 +464,24 @@ class LagFrame:
         n = self._nrows()
         cnt = np.zeros(n, dtype=np.int64)
         lag = {}
-        srcs = {self._spec[c][0] for c in cols if c not in self._overlay and self._spec[c][2]}
+        ov, spec = self._overlay, self._spec
+        # one pass over the (thousands of) column specs: lag columns grouped by shift, the
+        # unshifted copies of numeric lag sources with them, everything else on the host
+        specs = [spec[c] for c in cols if c not in ov]
+        srcs = {t[0] for t in specs if t[2]}
+        num = {nm: self._src.numeric(nm) for nm in srcs}
+        host = []
+        for t in specs:
+            if t[2] or num.get(t[0], False):
+                lag.setdefault(t[1], []).append(t[0])
+            else:
+                host.append(t[0])
+        if ov:
+            for c in cols:
+                if c in ov:
+                    cnt += pd.isna(ov[c]).astype(np.int64)
         sp = self._span()
-        for c in cols:
-            if c in self._overlay:
-                cnt += pd.isna(self._overlay[c]).astype(np.int64)
-                continue
-            nm, s, is_lag = self._spec[c]
-            if is_lag or (nm in srcs and self._src.numeric(nm)):
-                lag.setdefault(s, []).append(nm)
-                continue
+        for nm in host:
             v = self._src.base[nm]
             if isinstance(v.dtype, np.dtype) and v.dtype.kind in "iub":
                 continue                                    # integer / bool: no NaN
@@ -481,7 +489,7 @@ class LagFrame:
                                             v.dtype.kind == "f") else v.isna().to_numpy()
             cnt += na[sp[0]:sp[1]] if sp is not None else na[self.positions()]
         if lag:
-            cnt += self._lag_nan_counts(lag)
+            self._lag_nan_counts(lag, cnt)
         return cnt
 
     def _any_nan(self) -> bool:
@@ -505,15 +513,15 @@ class LagFrame:
             return bool(self.nan_counts().any())
         return False
 
-    def _lag_nan_counts(self, lag) -> np.ndarray:
-        """NaN lag cells per row; ``lag``: shift -> source names (one per lag column).  A
-        cell is NaN when its source row u - s is outside the base (counted on the host from
-        the edge rows only) or its source cell is NaN (device, for sources that hold any)."""
+    def _lag_nan_counts(self, lag, out: np.ndarray) -> None:
+        """Adds the NaN lag cells per row to ``out``; ``lag``: shift -> source names (one per
+        lag column).  A cell is NaN when its source row u - s is outside the base (counted on
+        the host from the edge rows only) or its source cell is NaN (device, for sources that
+        hold any)."""
         import torch
         N = self._src.N
         pos = self.positions()
         n = pos.size
-        out = np.zeros(n, dtype=np.int64)
         sh = np.array(sorted(lag), dtype=np.int64)
         w = np.array([len(lag[s]) for s in sh], dtype=np.int64)
         smin, smax = int(sh[0]), int(sh[-1])
@@ -531,11 +539,11 @@ class LagFrame:
             # shifts s > u (source row u - s < 0) plus shifts s <= u - N (u - s >= N)
             gt = cw[-1] - cw[np.searchsorted(sh, u, side="right")]
             le = cw[np.searchsorted(sh, u - N, side="right")]
-            out[edge] = gt + le
+            out[edge] += gt + le
         names = sorted({nm for v in lag.values() for nm in v}, key=str)
         self._src.upload(names)
         if not any(self._src.has_nan(nm) for nm in names):
-            return out
+            return
         E, idx = self._src.device(names)
         row_of = {nm: int(r) for nm, r in zip(names, idx.tolist())}
         pos_d = torch.arange(sp[0], sp[1], dtype=torch.int64, device="cuda") if sp is not None \
@@ -550,7 +558,7 @@ class LagFrame:
             u = pos_d - int(s)
             inside = (u >= 0) & (u < N)
             acc += torch.where(inside, per_row[u.clamp(0, N - 1)], torch.zeros_like(u))
-        return out + acc.cpu().numpy()
+        out += acc.cpu().numpy()
 
     # ------------------------------------------------------------------ values
     def _series(self, name) -> pd.Series:

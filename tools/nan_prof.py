@@ -27,9 +27,9 @@ def timed_upload(self, names):
     return r
 lagframe.LagSource.upload = timed_upload
 orig_lnc = lagframe.LagFrame._lag_nan_counts
-def timed_lnc(self, lag):
+def timed_lnc(self, lag, out):
     t = time.perf_counter()
-    r = orig_lnc(self, lag)
+    r = orig_lnc(self, lag, out)
     T["lag_nan_counts"] = T.get("lag_nan_counts", 0) + time.perf_counter() - t
     return r
 lagframe.LagFrame._lag_nan_counts = timed_lnc
