@@ -222,7 +222,7 @@ def cpu_port_iter(s, n_rows_unit, rows):
             "iters": int(iters), "s": round(dt, 2)}
 
 
-def pmc_traffic():
+def pmc_traffic(kernel="syrk6_kernel"):
     """HBM bytes per Gram launch from the newest committed PMC summary (profiles/*_pmc_traffic.json,
     written by tools/pmc_traffic.py from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this
     bench's grid; gfx950 corrections applied there).  PMC counters cannot be read in-process."""
@@ -233,7 +233,7 @@ def pmc_traffic():
     with open(files[-1]) as f:
         d = json.load(f)
     dom = d.get("dominant") or {}
-    if "syrk6_kernel" not in dom.get("kernel", ""):
+    if kernel not in dom.get("kernel", ""):
         return None, None
     return dom["traffic_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
 
@@ -972,7 +972,9 @@ def main():
     if rank == 0:
         grid_s = elapsed / a.steps
         achieved = kflop / ktime / 1e12 if ktime > 0 else 0.0
-        traffic, traffic_src = pmc_traffic()
+        # the Gram kernel that ran: the event-structured one when the design keeps its events
+        gram_kernel = "lag_gram_w_kernel" if E._lagw(design) is not None else "syrk6_kernel"
+        traffic, traffic_src = pmc_traffic(gram_kernel)
         conv = all(r["converged"] for r in res)
         ndist = None
         if world == 1 and a.config in ("c4", "c4mixed") and not a.no_check:
@@ -1070,7 +1072,7 @@ def main():
             },
             "roofline": {
                 "bound": "mfma",
-                "kernel": "syrk6_kernel",
+                "kernel": gram_kernel,
                 "achieved": achieved,
                 "peak": PEAK_BF16_TFLOPS,
                 "unit": "TFLOP/s",

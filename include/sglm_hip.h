@@ -191,6 +191,27 @@ int sglm_gather_w(const float* W, int64_t ld, const int32_t* fits, int32_t nact,
 int sglm_syrk_cbits(const int64_t* desc, int32_t P, const int32_t* fits, int32_t nact,
                     int32_t splits, float* H, void* work, sglm_stream_t stream);
 
+/* Weighted Gram of a time-shifted 0/1 event design from its events (lagw.hip): for each
+ * fits[f], H[fits[f]] = X^T diag(bf16(W[fits[f]])) X with X[t][col(b, a)] =
+ * e_a(t + row0 - shifts[b]) and the ones column p = K m, written on the upper triangle
+ * (row <= col; the padding columns > p zeroed).  col(b, a) = layout ? a K + b : b m + a.
+ * R: sglm_lag_rowwords of the events; occ / ev_off: every event's occurrence rows, event-major,
+ * ascending, and the event segments (m + 1); bidx[s - smin] = b of shift s (-1 if absent).
+ * Replaces the dense Gram's n p^2 products by nnz(E) m (2 (smax - smin) + 1) K per fit.
+ * The shift set must be a contiguous range (in any order). */
+int sglm_lag_gram_w(const uint64_t* R, const int32_t* occ, const int32_t* ev_off, int32_t m,
+                    int32_t nraw, const int32_t* shifts, const int32_t* bidx, int32_t K,
+                    int32_t smin, int32_t smax, int32_t layout, int32_t row0, int32_t n,
+                    const float* W, int64_t ld, const int32_t* fits, int32_t nf, float* H,
+                    int32_t P, void* work, sglm_stream_t stream);
+/* work bytes of sglm_lag_gram_w (8 shifted bf16 copies of the launch's weights) */
+size_t sglm_lag_gram_w_work_bytes(int32_t nraw, int32_t K, int32_t nf);
+
+/* Row words of m <= 63 events: R[u] bit a = e_a(u) (ebits[m][nwords], bit u & 31 of word
+ * u >> 5), bit m = 1, for u < nraw. */
+int sglm_lag_rowwords(const int32_t* ebits, int32_t m, int32_t nwords, int32_t nraw,
+                      uint64_t* R, sglm_stream_t stream);
+
 /* Row-major bit-planes of a 0/1 design for the MFMA GEMVs: out[(t * ld + i) * 2 + {0,1}] =
  * the bits of X[64t + alpha][i], alpha = 0..63, fragment order (see sglm_pack_bits_rows).
  * Size (P/64) * ld * 8 bytes.  *nonbinary as for sglm_pack_bits. */

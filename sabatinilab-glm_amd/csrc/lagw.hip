@@ -1,0 +1,395 @@
+// Weighted Gram of a time-shifted 0/1 event design from its events (sglm_lag_gram_w).
+//
+// The design's column (b, a) is event a shifted by s_b: X[t][(b, a)] = e_a(t + row0 - s_b), plus
+// the ones column p.  For one fit with row weights w (the IRLS weights, mask multiplicities
+// folded in) the Gram entry of columns (b1, a1), (b2, a2) is, with v = t + row0 - s_b1 an
+// occurrence of a1 and d = s_b1 - s_b2,
+//     H[(b1,a1)][(b2,a2)] = sum over v in occ(a1) of e_a2(v + d) * w(v - row0 + s_b1)
+// -- for each event a1 ONE matrix product over a1's occurrences (K = |occ(a1)|):
+//     G_a1[(d, a2)][(f, b1)] = sum_v A[v][(d, a2)] B[v][(f, b1)],
+//     A[v][(d, a2)] = e_a2(v + d)            (bit a2 of the row word R[v + d])
+//     B[v][(f, b1)] = bf16(w_f(v - row0 + s_b1))
+// and every G entry is one H entry (b2 = the shift s_b1 - d).  The dense Gram sums n rows of
+// p^2 products; this sums nnz(E) occurrences of m (2 L - 1) x L products per fit: 2 rho of the
+// dense work at event density rho (C4: 0.04).  The products are the dense kernel's (bf16 w times
+// exact 0/1, f32 accumulation), in another order.
+//
+// Layout: R[u] (u64 per raw row u): bit a = e_a(u), bit m = 1 (the ones column: d = 0).
+// Workgroup: 4 waves, one event a1, 4 MT tiles of 32 (d, a2) rows (a2 >= a1 only: the rest are
+// the transposes of later events' blocks) x NT tiles of 32 (f, b1) columns, over ALL of a1's
+// occurrences (no split: every H entry is written once, by one lane, no reduction).  Per stage
+// of KS occurrences the row words of the workgroup's d range and the bf16 weights are staged in
+// LDS (double buffered, the next stage's loads in flight during this stage's MFMAs); the A
+// operand is expanded from the staged words (bf16 2.0 / 0, the factor 2 removed at the store),
+// the B operand is one ds_read_b128 per N tile.
+#include "common.h"
+
+namespace sglm {
+namespace {
+
+constexpr int kKS = 64;             // occurrences per stage (4 MFMA K-steps)
+constexpr int kWS = kKS + 8;        // weight row stride (bf16): conflict-free b128 reads
+
+struct LagWArgs {
+    const uint16_t* Wt;             // 8 shifted copies of the bf16 weights by (raw row, fit)
+    int64_t wlen;                   // elements per copy (a multiple of 8)
+    const uint64_t* R;
+    const int32_t* occ;
+    const int32_t* ev_off;
+    const int32_t* shifts;          // [K]
+    const int32_t* bidx;            // [smax - smin + 1]: b of shift smin + i, -1 if absent
+    const float* W;
+    const int32_t* fits;
+    float* H;
+    int64_t ld;
+    int32_t nf, P, p, m, K, smin, smax, layout, row0, n, nraw, nh, D, Gm;
+};
+
+__device__ __forceinline__ int lag_col(const LagWArgs& a, int b, int ev) {
+    return a.layout ? ev * a.K + b : b * a.m + ev;
+}
+
+template <int MT, int NT, int WM, int WN>
+struct LagWSmem {
+    uint32_t rw[2][2][WM * MT + 1][kKS];              // [buf][lo/hi word][d row][occurrence]
+    __attribute__((aligned(16))) uint16_t ws[2][WN * NT * 32][kWS];   // [buf][(f, b1)][occ]
+    int32_t occ[3][kKS];
+};
+
+// WM x WN waves (two per SIMD): wave (wm, wn) holds MT x NT accumulator tiles (128 AGPRs), the
+// workgroup WM MT (d, a2) tiles x WN NT (f, b1) tiles.  Tiles past the event's last are computed
+// on a valid address and dropped at the store (no branch in the MFMA stream).
+template <int MT, int NT, int WM, int WN>
+__global__ void __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(2, 2)))
+lag_gram_w_kernel(LagWArgs a) {
+    constexpr int NTH = 64 * WM * WN;
+    constexpr int MB = WM * MT;                          // M tiles per workgroup
+    constexpr int ND = MB + 1;
+    constexpr int NN = WN * NT * 32;                     // columns per workgroup
+    __shared__ LagWSmem<MT, NT, WM, WN> sm;
+    const int a1 = blockIdx.x / a.Gm, g = blockIdx.x % a.Gm;
+    const int h0 = a1 >> 5;                              // a2 halves below a1 are skipped
+    const int nh1 = a.nh - h0;
+    const int Tm = a.D * nh1;
+    const int t0 = g * MB;
+    if (t0 >= Tm) return;
+    const int di0 = t0 / nh1;
+    const int di1 = min(Tm - 1, t0 + MB - 1) / nh1;
+    const int nd = di1 - di0 + 1;
+    const int dmin = a.smin - a.smax;
+    const int o_beg = a.ev_off[a1], o_end = a.ev_off[a1 + 1];
+    const int nst = (o_end - o_beg + kKS - 1) / kKS;
+    const int n0 = blockIdx.y * NN;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r = lane & 31;
+    const int wm = wave % WM, wn = wave / WM;
+
+    // weights: column n = sb nf + f (shift smin + sb, fit f) of occurrence v is Wt[v nf + n], so a
+    // stage's columns n0 .. n0 + NN of one occurrence are one contiguous run, read as 16-byte
+    // pieces from the copy whose shift makes the run 16-byte aligned.  Task of this thread:
+    // occurrence pair kp, piece e (8 columns) -> 8 column rows of the staged tile, 2 occurrences
+    constexpr int kNP = NN / 8;                          // pieces per occurrence
+    constexpr int kWTN = (kKS / 2) * kNP;                // tasks per stage
+    constexpr int kWT = (kWTN + NTH - 1) / NTH;          // tasks per thread (at most)
+    constexpr int kRE = (ND * kKS + NTH - 1) / NTH;      // row words per thread (at most)
+
+    uint64_t rreg[kRE];
+    uint4 wreg[kWT][2];
+    int32_t oreg = 0;
+
+    auto occ_load = [&](int s) {                         // occurrence rows of stage s
+        const int o = o_beg + s * kKS + tid;
+        oreg = (tid < kKS && s < nst && o < o_end) ? a.occ[o] : -1;
+    };
+    auto occ_store = [&](int s) {
+        if (tid < kKS) sm.occ[s % 3][tid] = oreg;
+    };
+    auto data_load = [&](int s) {                        // stage s's words and weights -> regs
+        const int* ov = sm.occ[s % 3];
+#pragma unroll
+        for (int i = 0; i < kRE; ++i) {
+            const int e = tid + NTH * i;
+            uint64_t x = 0;
+            if (e < nd * kKS) {
+                const int dl = e / kKS, k = e % kKS;
+                const int v = ov[k];
+                const int u = v + dmin + di0 + dl;
+                if (v >= 0 && u >= 0 && u < a.nraw) x = a.R[u];
+            }
+            rreg[i] = x;
+        }
+#pragma unroll
+        for (int i = 0; i < kWT; ++i) {
+            const int task = tid + NTH * i;
+            const int kp = (task / kNP) % (kKS / 2), e = task % kNP;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int v = ov[2 * kp + j];
+                uint4 q = make_uint4(0, 0, 0, 0);
+                if (v >= 0 && task < kWTN) {
+                    const int64_t x = (int64_t)v * a.nf + n0 + 8 * e;
+                    const int c = (int)(x & 7);
+                    q = *reinterpret_cast<const uint4*>(a.Wt + c * a.wlen + (x - c));
+                }
+                wreg[i][j] = q;
+            }
+        }
+    };
+    auto data_store = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < kRE; ++i) {
+            const int e = tid + NTH * i;
+            if (e < nd * kKS) {
+                const int dl = e / kKS, k = e % kKS;
+                sm.rw[buf][0][dl][k] = (uint32_t)rreg[i];
+                sm.rw[buf][1][dl][k] = (uint32_t)(rreg[i] >> 32);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < kWT; ++i) {
+            const int task = tid + NTH * i;
+            if (task >= kWTN) continue;
+            const int kp = task / kNP, e = task % kNP;
+            const uint32_t q0[4] = {wreg[i][0].x, wreg[i][0].y, wreg[i][0].z, wreg[i][0].w};
+            const uint32_t q1[4] = {wreg[i][1].x, wreg[i][1].y, wreg[i][1].z, wreg[i][1].w};
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const uint32_t lo = (q0[c >> 1] >> (16 * (c & 1))) & 0xffffu;
+                const uint32_t hi = (q1[c >> 1] >> (16 * (c & 1))) & 0xffffu;
+                *reinterpret_cast<uint32_t*>(&sm.ws[buf][8 * e + c][2 * kp]) = lo | (hi << 16);
+            }
+        }
+    };
+
+    f32x16 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = (f32x16){};
+
+    // this wave's tiles: tau = t0 + wm MT + i -> (d row, a2 half); LDS offsets of their words
+    int toff[MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+        const int tau = min(t0 + wm * MT + i, Tm - 1);
+        const int dl = tau / nh1 - di0, hf = h0 + tau % nh1;
+        toff[i] = (hf * ND + dl) * kKS + 8 * h;         // in words, within one buffer
+    }
+    const int boff = (wn * NT * 32 + r) * kWS + 8 * h;   // in bf16, within one buffer
+
+    if (nst > 0) {
+        occ_load(0);
+        occ_store(0);
+        occ_load(1);
+        occ_store(1);
+        __syncthreads();
+        data_load(0);
+        data_store(0);
+        occ_load(2);
+    }
+    int buf = 0;
+    for (int s = 0; s < nst; ++s) {
+        occ_store(s + 2);                                // stage s + 2's rows (or -1s)
+        __syncthreads();
+        const bool more = s + 1 < nst;
+        if (more) data_load(s + 1);
+        occ_load(s + 3);
+        const uint32_t* rwb = &sm.rw[buf][0][0][0];
+        const uint16_t* wsb = &sm.ws[buf][0][0];
+#pragma unroll 2
+        for (int ks = 0; ks < kKS / 16; ++ks) {
+            bf16x8 bq[NT];
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+                bq[j] = *reinterpret_cast<const bf16x8*>(wsb + boff + j * 32 * kWS + 16 * ks);
+#pragma unroll
+            for (int i = 0; i < MT; ++i) {
+                const uint32_t* wp = rwb + toff[i] + 16 * ks;
+                const uint4 w0 = *reinterpret_cast<const uint4*>(wp);
+                const uint4 w1 = *reinterpret_cast<const uint4*>(wp + 4);
+                const uint32_t wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+                uint32_t dq[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    dq[q] = (rotr32(wv[2 * q], (r - 14) & 31) & 0x4000u) |
+                            (rotr32(wv[2 * q + 1], (r - 30) & 31) & 0x40000000u);
+                const bf16x8 aq = __builtin_bit_cast(bf16x8, make_uint4(dq[0], dq[1], dq[2], dq[3]));
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq, bq[j], acc[i][j], 0, 0,
+                                                                        0);
+            }
+        }
+        if (more) data_store(buf ^ 1);
+        buf ^= 1;
+    }
+
+    // epilogue: G entry (d, a2) x (f, b1) -> H_f[(b1, a1)][(b2, a2)], upper triangle
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int nn = n0 + (wn * NT + j) * 32 + r;
+        const int sb = nn / a.nf, f = nn % a.nf;           // column: shift smin + sb, fit f
+        if (sb >= a.K) continue;
+        float* Hf = a.H + (int64_t)a.fits[f] * a.P * a.P;
+        const int s1 = a.smin + sb;
+        const int b1 = a.bidx[sb];
+        const int ci = lag_col(a, b1, a1);
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+            const int tau = t0 + wm * MT + i;
+            if (tau >= Tm) continue;
+            const int dd = dmin + tau / nh1;
+            const int hf = h0 + tau % nh1;
+            const int s2 = s1 - dd;
+            if (s2 < a.smin || s2 > a.smax) continue;
+            const int b2 = a.bidx[s2 - a.smin];
+            if (b2 < 0) continue;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int a2 = 32 * hf + (q & 3) + 8 * (q >> 2) + 4 * h;
+                const float val = 0.5f * acc[i][j][q];
+                if (a2 < a.m) {
+                    if (a2 < a1) continue;
+                    const int cj = lag_col(a, b2, a2);
+                    if (a2 == a1 && ci > cj) continue;
+                    const int lo = min(ci, cj), hi = max(ci, cj);
+                    Hf[(int64_t)lo * a.P + hi] = val;
+                } else if (a2 == a.m && dd == 0) {
+                    Hf[(int64_t)ci * a.P + a.p] = val;
+                }
+            }
+        }
+    }
+}
+
+// H_f[p][p] = sum_t bf16(w_f(t)) (block 0 of each fit) and the padding columns / rows of the
+// upper triangle zeroed (the dense kernel's zero bits there)
+__global__ void __launch_bounds__(256) lag_gram_w_aux(const float* __restrict__ W, int64_t ld,
+                                                      int32_t n, const int32_t* __restrict__ fits,
+                                                      float* __restrict__ H, int32_t P,
+                                                      int32_t p) {
+    float* Hf = H + (int64_t)fits[blockIdx.y] * P * P;
+    if (blockIdx.x == 0) {
+        const float* w = W + (int64_t)fits[blockIdx.y] * ld;
+        float s = 0.0f;
+        for (int t = threadIdx.x; t < n; t += 256) s += (float)(__bf16)w[t];
+        __shared__ float red[256];
+        red[threadIdx.x] = s;
+        __syncthreads();
+        for (int o = 128; o > 0; o >>= 1) {
+            if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) Hf[(int64_t)p * P + p] = red[0];
+        return;
+    }
+    const int w = P - p - 1;                             // padding columns p + 1 .. P - 1
+    const int64_t tot = (int64_t)P * w;
+    for (int64_t e = (int64_t)(blockIdx.x - 1) * 256 + threadIdx.x; e < tot;
+         e += (int64_t)(gridDim.x - 1) * 256) {
+        const int64_t i = e / w, j = p + 1 + e % w;
+        if (i <= j) Hf[i * P + j] = 0.0f;
+    }
+}
+
+// Wt copy c, element j = bf16(W[fits[f]][u - row0 + smin]) at i = j + c = u nf + f (0 off the
+// design's rows): the weights of raw rows u - smin .. in (row, fit) order, shifted by c
+__global__ void __launch_bounds__(256) lag_gram_w_prep(const float* __restrict__ W, int64_t ld,
+                                                       int32_t n, const int32_t* __restrict__ fits,
+                                                       int32_t nf, int32_t row0, int32_t smin,
+                                                       int64_t wlen, uint16_t* __restrict__ Wt) {
+    const int c = blockIdx.y;
+    for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < wlen;
+         j += (int64_t)gridDim.x * 256) {
+        const int64_t i = j + c;
+        const int64_t u = i / nf;
+        const int f = (int)(i % nf);
+        const int64_t t = u - row0 + smin;
+        const float x = (t >= 0 && t < n) ? W[(int64_t)fits[f] * ld + t] : 0.0f;
+        Wt[c * wlen + j] = __builtin_bit_cast(uint16_t, (__bf16)x);
+    }
+}
+
+template <int MT, int NT, int WM, int WN>
+int launch_lagw(const LagWArgs& a, hipStream_t s) {
+    LagWArgs b = a;
+    b.Gm = (a.D * a.nh + WM * MT - 1) / (WM * MT);
+    const int NN = WN * NT * 32;
+    const dim3 grid((unsigned)(a.m * b.Gm), (unsigned)((a.nf * a.K + NN - 1) / NN));
+    lag_gram_w_kernel<MT, NT, WM, WN><<<grid, 64 * WM * WN, 0, s>>>(b);
+    return check_launch("lag_gram_w_kernel");
+}
+
+}  // namespace
+}  // namespace sglm
+
+using namespace sglm;
+
+// elements of one weight copy (sglm_lag_gram_w's work: 8 copies of 2-byte elements)
+static int64_t lagw_wlen(int32_t nraw, int32_t K, int32_t nf) {
+    return ((int64_t)(nraw + K + 64) * nf + 256 + 7) / 8 * 8;
+}
+
+extern "C" size_t sglm_lag_gram_w_work_bytes(int32_t nraw, int32_t K, int32_t nf) {
+    return (size_t)(8 * lagw_wlen(nraw, K, nf) * 2);
+}
+
+extern "C" int sglm_lag_gram_w(const uint64_t* R, const int32_t* occ, const int32_t* ev_off,
+                               int32_t m, int32_t nraw, const int32_t* shifts,
+                               const int32_t* bidx, int32_t K, int32_t smin, int32_t smax,
+                               int32_t layout, int32_t row0, int32_t n, const float* W,
+                               int64_t ld, const int32_t* fits, int32_t nf, float* H, int32_t P,
+                               void* work, sglm_stream_t stream) {
+    if (nf <= 0) return SGLM_OK;
+    const int p = K * m;
+    if (!R || !occ || !ev_off || !shifts || !bidx || !W || !fits || !H || !work || m < 1 ||
+        m > 63 || K < 1 || smax - smin + 1 != K || p + 1 > P || n < 0 || ld < n) {
+        set_error("sglm_lag_gram_w: bad args (m=%d K=%d P=%d)", m, K, P);
+        return SGLM_EINVAL;
+    }
+    hipStream_t s = as_stream(stream);
+    LagWArgs a{};
+    a.wlen = lagw_wlen(nraw, K, nf);
+    a.Wt = (const uint16_t*)work;
+    lag_gram_w_prep<<<dim3(1024, 8), 256, 0, s>>>(W, ld, n, fits, nf, row0, smin, a.wlen,
+                                                  (uint16_t*)work);
+    {
+        const int st0 = check_launch("lag_gram_w_prep");
+        if (st0) return st0;
+    }
+    a.R = R; a.occ = occ; a.ev_off = ev_off; a.shifts = shifts; a.bidx = bidx; a.W = W;
+    a.fits = fits; a.H = H; a.ld = ld; a.nf = nf; a.P = P; a.p = p; a.m = m; a.K = K;
+    a.smin = smin; a.smax = smax; a.layout = layout; a.row0 = row0; a.n = n; a.nraw = nraw;
+    a.nh = (m + 1 + 31) / 32;
+    a.D = 2 * (smax - smin) + 1;
+    const int64_t pad = (int64_t)P * (P - p - 1);
+    const unsigned gx = 1 + (unsigned)((pad + 255) / 256 < 512 ? (pad + 255) / 256 : 512);
+    lag_gram_w_aux<<<dim3(gx, (unsigned)nf), 256, 0, s>>>(W, ld, n, fits, H, P, p);
+    int st = check_launch("lag_gram_w_aux");
+    if (st) return st;
+    if (nf * K <= 64) return launch_lagw<4, 2, 8, 1>(a, s);
+    return launch_lagw<2, 4, 8, 1>(a, s);
+}
+
+// R[u] = sum_a bit(e_a(u)) << a | 1 << m from the occurrence bitmaps ebits[m][nwords]
+__global__ void __launch_bounds__(256) lag_rowwords_kernel(const int32_t* __restrict__ ebits,
+                                                           int32_t m, int32_t nwords,
+                                                           int32_t nraw, uint64_t* __restrict__ R) {
+    const int u = blockIdx.x * 256 + threadIdx.x;
+    if (u >= nraw) return;
+    uint64_t x = (uint64_t)1 << m;
+    for (int e = 0; e < m; ++e)
+        x |= (uint64_t)(((uint32_t)ebits[(int64_t)e * nwords + (u >> 5)] >> (u & 31)) & 1u) << e;
+    R[u] = x;
+}
+
+extern "C" int sglm_lag_rowwords(const int32_t* ebits, int32_t m, int32_t nwords, int32_t nraw,
+                                 uint64_t* R, sglm_stream_t stream) {
+    if (!ebits || !R || m < 1 || m > 63 || nraw < 0 || nwords * 32 < nraw) {
+        set_error("sglm_lag_rowwords: bad args");
+        return SGLM_EINVAL;
+    }
+    if (nraw == 0) return SGLM_OK;
+    lag_rowwords_kernel<<<(nraw + 255) / 256, 256, 0, as_stream(stream)>>>(ebits, m, nwords, nraw,
+                                                                           R);
+    return check_launch("lag_rowwords_kernel");
+}

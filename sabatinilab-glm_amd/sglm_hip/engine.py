@@ -72,6 +72,11 @@ DEV_DECIDE = __import__("os").environ.get("SGLM_DEV_DECIDE", "0") == "1"
 AA_KERNEL = __import__("os").environ.get("SGLM_AA_KERNEL", "0") == "1"
 SYRK_CBITS = True              # ... and its row-compacted register-only form (v6) when fits
                                # carry masks (the default path for event designs)
+# the Gram of a time-shifted 0/1 event design from its events (sglm_lag_gram_w: one matrix
+# product per event over its occurrences, 2 rho of the dense Gram's products at event density
+# rho) when the design keeps its event structure and the events are sparse enough
+LAG_GRAM_W = __import__("os").environ.get("SGLM_LAG_GRAM_W", "1") == "1"
+LAG_GRAM_W_MAX_RHO = 0.2        # above it the dense bit-plane Gram does fewer products
 # Hessian reuse (log-link families): a fit keeps its last Hessian factor while the drift of
 # its linear predictor since that Hessian was formed, D = sum of max_i |t d_eta_i| over the
 # steps taken since, stays <= HESS_REUSE_TOL.  The IRLS weights then differ from the ones the
@@ -2983,6 +2988,15 @@ def _syrk(d: Design, bf, fits: np.ndarray, nsteps: int, ntile1: int, stats, st, 
     ev = None
     if stats is not None and stats.record:
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    lg = _lagw(d) if (use_cb or (exact and d.xf is None and d.xbits is not None)) else None
+    if lg is not None:
+        ab, flop = _lag_gram_w(d, lg, bf, fits, st, ev)
+        if ev is not None:
+            stats.syrk_bytes.append(ab)
+            stats.syrk_events.append((ev[0], ev[1], nact, flop))   # the structured products
+        if d.cont is not None:
+            _mix_hess(d, bf, fits, exact)
+        return
     if use_cb:
         ab = _syrk_cbits(d, bf, prob, fits, st, ev)
         if ev is not None:
@@ -3037,6 +3051,62 @@ def _mix_hess(d: Design, bf, fits, exact: bool):
         store = bf.mixS = {}
     for q, k in enumerate(fits):
         store[int(k)] = S[q]
+
+
+def _lagw(d: Design):
+    """The design's event structure for sglm_lag_gram_w (row words and the shift table built
+    on first use), or None: no structure, continuous columns, > 63 events, or events too
+    dense for the structured product to pay."""
+    lg = getattr(d, "lag", None)
+    if not LAG_GRAM_W or lg is None or d.cont is not None or lg.m > 63:
+        return None
+    if getattr(lg, "R", None) is None:
+        if getattr(lg, "R_off", False):
+            return None
+        cnt = np.diff(lg.ev_off.cpu().numpy().astype(np.int64))
+        rho = float(cnt.sum()) / max(1.0, float(lg.m) * float(lg.n_raw))
+        sh = lg.shifts.cpu().numpy().astype(np.int64)
+        if (rho > LAG_GRAM_W_MAX_RHO or d.p != lg.m * lg.K
+                or not np.array_equal(np.sort(sh), np.arange(lg.smin, lg.smin + sh.size))):
+            lg.R_off = True
+            return None
+        R = torch.empty(max(1, lg.n_raw), dtype=torch.int64, device=d.device)
+        _lib.call("sglm_lag_rowwords", _p(lg.ebits), lg.m, lg.nwords, lg.n_raw, _p(R),
+                  _stream())
+        bidx = np.full(lg.smax - lg.smin + 1, -1, dtype=np.int32)
+        bidx[sh - lg.smin] = np.arange(sh.size, dtype=np.int32)
+        lg.bidx = torch.from_numpy(bidx).to(d.device)
+        # algorithmic flop per fit: one product per (occurrence of a1, b1, b2, a2 >= a1) and per
+        # (occurrence, b1) for the ones column -- the H entries' own terms (the launch also forms
+        # the G entries whose shift s_b1 - d is not a column, and pads rows and columns to 32)
+        lg.flop1 = float(2.0 * sum(int(c) * ((lg.m - a) * lg.K + 1) for a, c in enumerate(cnt))
+                         * lg.K)
+        lg.R = R
+    return lg
+
+
+def _lag_gram_w(d: Design, lg, bf, fits: np.ndarray, st, ev=None):
+    """H[k] = X^T diag(bf16 W[k]) X for k in fits from the design's events (sglm_lag_gram_w);
+    returns (algorithmic bytes, structured flop) of the launch."""
+    nact = int(fits.size)
+    upl = getattr(bf, "up", None)
+    fits_d = upl(fits, np.int32) if upl is not None else \
+        torch.from_numpy(np.asarray(fits, dtype=np.int32)).to(d.device)
+    work = _work(_lib.query("sglm_lag_gram_w_work_bytes", lg.n_raw, lg.K, nact), d.device,
+                 "lagw")
+    with _GRAM_LOCK:
+        _gram_turn()
+        if ev is not None:
+            ev[0].record()
+        _lib.call("sglm_lag_gram_w", _p(lg.R), _p(lg.occ), _p(lg.ev_off), lg.m, lg.n_raw,
+                  _p(lg.shifts), _p(lg.bidx), lg.K, lg.smin, lg.smax, lg.layout, lg.row0,
+                  lg.n, _p(bf.W), d.ld, _p(fits_d), nact, _p(bf.H), d.P, _p(work), st)
+        if ev is not None:
+            ev[1].record()
+        _gram_done()
+    bf.keep = (fits_d,)
+    pa = d.p + 1
+    return (8 * lg.n_raw + nact * (4 * lg.n + 4 * pa * (pa + 1) // 2), nact * lg.flop1)
 
 
 def _syrk_cbits(d: Design, bf, prob: Problem, fits: np.ndarray, st, ev=None):
