@@ -53,7 +53,7 @@ template <int MT, int NT, int WM, int WN>
 struct LagWSmem {
     uint32_t rw[2][2][WM * MT + 1][kKS];              // [buf][lo/hi word][d row][occurrence]
     __attribute__((aligned(16))) uint16_t ws[2][WN * NT * 32][kWS];   // [buf][(f, b1)][occ]
-    int32_t occ[3][kKS];
+    int32_t occ[4][kKS];
 };
 
 // WM x WN waves (two per SIMD): wave (wm, wn) holds MT x NT accumulator tiles (128 AGPRs), the
@@ -87,13 +87,16 @@ lag_gram_w_kernel(LagWArgs a) {
     // stage's columns n0 .. n0 + NN of one occurrence are one contiguous run, read as 16-byte
     // pieces from the copy whose shift makes the run 16-byte aligned.  Task of this thread:
     // occurrence pair kp, piece e (8 columns) -> 8 column rows of the staged tile, 2 occurrences
+    // (consecutive lanes take consecutive pairs: the transposed 4-byte stores hit distinct banks)
     constexpr int kNP = NN / 8;                          // pieces per occurrence
     constexpr int kWTN = (kKS / 2) * kNP;                // tasks per stage
     constexpr int kWT = (kWTN + NTH - 1) / NTH;          // tasks per thread (at most)
     constexpr int kRE = (ND * kKS + NTH - 1) / NTH;      // row words per thread (at most)
 
-    uint64_t rreg[kRE];
-    uint4 wreg[kWT][2];
+    // two register sets: while stage s is multiplied, the loads of stage s + 2 are in flight
+    // and stage s + 1 (loaded during stage s - 1) waits in the other set for the LDS store
+    uint64_t rA[kRE], rB[kRE];
+    uint4 wA[kWT][2], wB[kWT][2];
     int32_t oreg = 0;
 
     auto occ_load = [&](int s) {                         // occurrence rows of stage s
@@ -101,10 +104,10 @@ lag_gram_w_kernel(LagWArgs a) {
         oreg = (tid < kKS && s < nst && o < o_end) ? a.occ[o] : -1;
     };
     auto occ_store = [&](int s) {
-        if (tid < kKS) sm.occ[s % 3][tid] = oreg;
+        if (tid < kKS) sm.occ[s & 3][tid] = oreg;
     };
-    auto data_load = [&](int s) {                        // stage s's words and weights -> regs
-        const int* ov = sm.occ[s % 3];
+    auto data_load = [&](int s, uint64_t (&rreg)[kRE], uint4 (&wreg)[kWT][2]) {
+        const int* ov = sm.occ[s & 3];
 #pragma unroll
         for (int i = 0; i < kRE; ++i) {
             const int e = tid + NTH * i;
@@ -120,7 +123,7 @@ lag_gram_w_kernel(LagWArgs a) {
 #pragma unroll
         for (int i = 0; i < kWT; ++i) {
             const int task = tid + NTH * i;
-            const int kp = (task / kNP) % (kKS / 2), e = task % kNP;
+            const int kp = task % (kKS / 2), e = (task / (kKS / 2)) % kNP;
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 const int v = ov[2 * kp + j];
@@ -134,7 +137,7 @@ lag_gram_w_kernel(LagWArgs a) {
             }
         }
     };
-    auto data_store = [&](int buf) {
+    auto data_store = [&](int buf, const uint64_t (&rreg)[kRE], const uint4 (&wreg)[kWT][2]) {
 #pragma unroll
         for (int i = 0; i < kRE; ++i) {
             const int e = tid + NTH * i;
@@ -148,7 +151,7 @@ lag_gram_w_kernel(LagWArgs a) {
         for (int i = 0; i < kWT; ++i) {
             const int task = tid + NTH * i;
             if (task >= kWTN) continue;
-            const int kp = task / kNP, e = task % kNP;
+            const int kp = task % (kKS / 2), e = task / (kKS / 2);
             const uint32_t q0[4] = {wreg[i][0].x, wreg[i][0].y, wreg[i][0].z, wreg[i][0].w};
             const uint32_t q1[4] = {wreg[i][1].x, wreg[i][1].y, wreg[i][1].z, wreg[i][1].w};
 #pragma unroll
@@ -176,23 +179,7 @@ lag_gram_w_kernel(LagWArgs a) {
     }
     const int boff = (wn * NT * 32 + r) * kWS + 8 * h;   // in bf16, within one buffer
 
-    if (nst > 0) {
-        occ_load(0);
-        occ_store(0);
-        occ_load(1);
-        occ_store(1);
-        __syncthreads();
-        data_load(0);
-        data_store(0);
-        occ_load(2);
-    }
-    int buf = 0;
-    for (int s = 0; s < nst; ++s) {
-        occ_store(s + 2);                                // stage s + 2's rows (or -1s)
-        __syncthreads();
-        const bool more = s + 1 < nst;
-        if (more) data_load(s + 1);
-        occ_load(s + 3);
+    auto compute = [&](int buf) {
         const uint32_t* rwb = &sm.rw[buf][0][0][0];
         const uint16_t* wsb = &sm.ws[buf][0][0];
 #pragma unroll 2
@@ -219,8 +206,33 @@ lag_gram_w_kernel(LagWArgs a) {
                                                                         0);
             }
         }
-        if (more) data_store(buf ^ 1);
-        buf ^= 1;
+    };
+    // stage s: cur holds stage s + 1 (stored to LDS at the end), nxt receives stage s + 2
+    auto step = [&](int s, uint64_t (&rc)[kRE], uint4 (&wc)[kWT][2], uint64_t (&rn)[kRE],
+                    uint4 (&wn_)[kWT][2]) {
+        occ_store(s + 3);                                // stage s + 3's rows (or -1s)
+        __syncthreads();
+        if (s + 2 < nst) data_load(s + 2, rn, wn_);
+        occ_load(s + 4);
+        compute(s & 1);
+        if (s + 1 < nst) data_store((s + 1) & 1, rc, wc);
+    };
+
+    if (nst > 0) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            occ_load(j);
+            occ_store(j);
+        }
+        __syncthreads();
+        data_load(0, rA, wA);
+        data_store(0, rA, wA);
+        if (nst > 1) data_load(1, rA, wA);
+        occ_load(3);
+    }
+    for (int s = 0; s < nst; s += 2) {
+        step(s, rA, wA, rB, wB);
+        if (s + 1 < nst) step(s + 1, rB, wB, rA, wA);
     }
 
     // epilogue: G entry (d, a2) x (f, b1) -> H_f[(b1, a1)][(b2, a2)], upper triangle
@@ -261,25 +273,40 @@ lag_gram_w_kernel(LagWArgs a) {
     }
 }
 
-// H_f[p][p] = sum_t bf16(w_f(t)) (block 0 of each fit) and the padding columns / rows of the
-// upper triangle zeroed (the dense kernel's zero bits there)
-__global__ void __launch_bounds__(256) lag_gram_w_aux(const float* __restrict__ W, int64_t ld,
-                                                      int32_t n, const int32_t* __restrict__ fits,
+// H_f[p][p] = sum_t bf16(w_f(t)): kLwRed partial sums per fit (fixed row chunks, fixed tree
+// order), then summed in order by lag_gram_w_aux; the padding columns / rows of the upper
+// triangle zeroed there (the dense kernel's zero bits)
+constexpr int kLwRed = 128;
+
+__global__ void __launch_bounds__(256) lag_gram_w_part(const float* __restrict__ W, int64_t ld,
+                                                       int32_t n, const int32_t* __restrict__ fits,
+                                                       float* __restrict__ part) {
+    const float* w = W + (int64_t)fits[blockIdx.y] * ld;
+    const int64_t chunk = ((int64_t)n + kLwRed - 1) / kLwRed;
+    const int64_t t0 = (int64_t)blockIdx.x * chunk, t1 = min((int64_t)n, t0 + chunk);
+    float s = 0.0f;
+    for (int64_t t = t0 + threadIdx.x; t < t1; t += 256) s += (float)(__bf16)w[t];
+    __shared__ float red[256];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.y * kLwRed + blockIdx.x] = red[0];
+}
+
+__global__ void __launch_bounds__(256) lag_gram_w_aux(const float* __restrict__ part,
+                                                      const int32_t* __restrict__ fits,
                                                       float* __restrict__ H, int32_t P,
                                                       int32_t p) {
     float* Hf = H + (int64_t)fits[blockIdx.y] * P * P;
     if (blockIdx.x == 0) {
-        const float* w = W + (int64_t)fits[blockIdx.y] * ld;
-        float s = 0.0f;
-        for (int t = threadIdx.x; t < n; t += 256) s += (float)(__bf16)w[t];
-        __shared__ float red[256];
-        red[threadIdx.x] = s;
-        __syncthreads();
-        for (int o = 128; o > 0; o >>= 1) {
-            if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-            __syncthreads();
+        if (threadIdx.x == 0) {
+            float t = 0.0f;
+            for (int b = 0; b < kLwRed; ++b) t += part[blockIdx.y * kLwRed + b];
+            Hf[(int64_t)p * P + p] = t;
         }
-        if (threadIdx.x == 0) Hf[(int64_t)p * P + p] = red[0];
         return;
     }
     const int w = P - p - 1;                             // padding columns p + 1 .. P - 1
@@ -330,7 +357,7 @@ static int64_t lagw_wlen(int32_t nraw, int32_t K, int32_t nf) {
 }
 
 extern "C" size_t sglm_lag_gram_w_work_bytes(int32_t nraw, int32_t K, int32_t nf) {
-    return (size_t)(8 * lagw_wlen(nraw, K, nf) * 2);
+    return (size_t)(8 * lagw_wlen(nraw, K, nf) * 2) + (size_t)nf * kLwRed * 4;
 }
 
 extern "C" int sglm_lag_gram_w(const uint64_t* R, const int32_t* occ, const int32_t* ev_off,
@@ -363,7 +390,9 @@ extern "C" int sglm_lag_gram_w(const uint64_t* R, const int32_t* occ, const int3
     a.D = 2 * (smax - smin) + 1;
     const int64_t pad = (int64_t)P * (P - p - 1);
     const unsigned gx = 1 + (unsigned)((pad + 255) / 256 < 512 ? (pad + 255) / 256 : 512);
-    lag_gram_w_aux<<<dim3(gx, (unsigned)nf), 256, 0, s>>>(W, ld, n, fits, H, P, p);
+    float* part = (float*)((uint16_t*)work + 8 * a.wlen);
+    lag_gram_w_part<<<dim3(kLwRed, (unsigned)nf), 256, 0, s>>>(W, ld, n, fits, part);
+    lag_gram_w_aux<<<dim3(gx, (unsigned)nf), 256, 0, s>>>(part, fits, H, P, p);
     int st = check_launch("lag_gram_w_aux");
     if (st) return st;
     if (nf * K <= 64) return launch_lagw<4, 2, 8, 1>(a, s);
