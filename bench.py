@@ -227,15 +227,13 @@ def pmc_traffic(kernel="syrk6_kernel"):
     written by tools/pmc_traffic.py from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this
     bench's grid; gfx950 corrections applied there).  PMC counters cannot be read in-process."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        d = json.load(f)
-    dom = d.get("dominant") or {}
-    if kernel not in dom.get("kernel", ""):
-        return None, None
-    return dom["traffic_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+    for fn in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))[::-1]:
+        with open(fn) as f:
+            d = json.load(f)
+        dom = d.get("dominant") or {}
+        if kernel in dom.get("kernel", ""):
+            return dom["traffic_bytes_per_launch"], os.path.relpath(fn, ROOT)
+    return None, None
 
 
 def bench_c5(a):
@@ -944,6 +942,7 @@ def main():
     kflop = sum(nact_flop for _, _, _, nact_flop in stats.syrk_events)
     nlaunch = len(stats.syrk_events)
     alg_bytes = float(np.mean(stats.syrk_bytes)) if stats.syrk_bytes else None
+    exec_flop = float(np.sum(stats.syrk_exec)) if stats.syrk_exec else None
     t = torch.tensor([elapsed, float(stats.fit_iters), ktime, kflop, float(nlaunch),
                       float(stats.gram_fits), stats.alg_flop, float(stats.reused),
                       float(stats.gram_fit_iters), float(stats.stops["stagnation"]),
@@ -1089,6 +1088,10 @@ def main():
                                             else None,
                 "launches": nlaunch,
                 "avg_launch_ms": ktime / max(nlaunch, 1) * 1e3,
+                # the event-structured Gram executes more MFMA work than its algorithmic
+                # products (G entries that are no H entry, 32-row / 32-column padding)
+                "executed_frac": (exec_flop / ktime / 1e12 / PEAK_BF16_TFLOPS
+                                  if (exec_flop and ktime > 0 and world == 1) else None),
             },
             "cpu_baseline": cpu,
         }

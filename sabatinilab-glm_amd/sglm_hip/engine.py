@@ -66,10 +66,9 @@ ETA_FINAL_ITERS = 8
 # runs over every active fit, stopped ones included, and the host still waits for the next
 # Hessian plan's readback behind it, so little host time leaves the critical path
 DEV_DECIDE = __import__("os").environ.get("SGLM_DEV_DECIDE", "0") == "1"
-# the Anderson correction as one kernel (sglm_aa_step) instead of ~20 torch operations.
-# Parity-green but off by default: no measured gain on the C4 grid (46.0 vs 45.8 ms,
-# interleaved A/B) -- the torch ops overlap the host's own work, off the critical path
-AA_KERNEL = __import__("os").environ.get("SGLM_AA_KERNEL", "0") == "1"
+# the Anderson correction as one kernel (sglm_aa_step) instead of ~20 torch operations
+# (C4 grid 35.26 -> 34.69 ms, interleaved A/B with the event-structured Gram)
+AA_KERNEL = __import__("os").environ.get("SGLM_AA_KERNEL", "1") == "1"
 SYRK_CBITS = True              # ... and its row-compacted register-only form (v6) when fits
                                # carry masks (the default path for event designs)
 # the Gram of a time-shifted 0/1 event design from its events (sglm_lag_gram_w: one matrix
@@ -1313,6 +1312,7 @@ class IrlsStats:
     record: bool = False
     syrk_events: list = field(default_factory=list)    # (start, end, algorithmic flop)
     syrk_bytes: list = field(default_factory=list)     # algorithmic HBM bytes per Gram launch
+    syrk_exec: list = field(default_factory=list)      # executed MFMA flop per Gram launch
     fit_iters: int = 0
     newton_iters: int = 0
     gram_fits: int = 0                                  # distinct Hessians formed
@@ -2989,10 +2989,13 @@ def _syrk(d: Design, bf, fits: np.ndarray, nsteps: int, ntile1: int, stats, st, 
     if stats is not None and stats.record:
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     lg = _lagw(d) if (use_cb or (exact and d.xf is None and d.xbits is not None)) else None
+    if lg is not None and not _lagw_pays(d, lg, nact):
+        lg = None
     if lg is not None:
-        ab, flop = _lag_gram_w(d, lg, bf, fits, st, ev)
+        ab, flop, xflop = _lag_gram_w(d, lg, bf, fits, st, ev)
         if ev is not None:
             stats.syrk_bytes.append(ab)
+            stats.syrk_exec.append(xflop)
             stats.syrk_events.append((ev[0], ev[1], nact, flop))   # the structured products
         if d.cont is not None:
             _mix_hess(d, bf, fits, exact)
@@ -3081,6 +3084,7 @@ def _lagw(d: Design):
         # the G entries whose shift s_b1 - d is not a column, and pads rows and columns to 32)
         lg.flop1 = float(2.0 * sum(int(c) * ((lg.m - a) * lg.K + 1) for a, c in enumerate(cnt))
                          * lg.K)
+        lg.cnt = cnt
         lg.R = R
     return lg
 
@@ -3106,7 +3110,37 @@ def _lag_gram_w(d: Design, lg, bf, fits: np.ndarray, st, ev=None):
         _gram_done()
     bf.keep = (fits_d,)
     pa = d.p + 1
-    return (8 * lg.n_raw + nact * (4 * lg.n + 4 * pa * (pa + 1) // 2), nact * lg.flop1)
+    return (8 * lg.n_raw + nact * (4 * lg.n + 4 * pa * (pa + 1) // 2), nact * lg.flop1,
+            _lagw_exec_flop(lg, nact))
+
+
+def _lagw_pays(d: Design, lg, nact: int) -> bool:
+    """Whether the event-structured Gram beats the dense bit-plane one for this launch: MFMA
+    work at the rates each reaches on the C4 grid (0.28 / 0.8 of the dense bf16 peak) plus the
+    structured path's weight copies (8 x 2 B per raw row per fit) and launch overheads."""
+    nb = d.P // 128
+    dense = 2.0 * d.n * (nb * (nb + 1) // 2) * 128 * 128 * nact / (0.8 * 2.5e15)
+    lag = (_lagw_exec_flop(lg, nact) / (0.28 * 2.5e15) + 16.0 * lg.n_raw * nact / 3e12
+           + 40e-6)
+    return lag < dense
+
+
+def _lagw_exec_flop(lg, nact: int) -> float:
+    """MFMA flop the sglm_lag_gram_w launch executes (csrc/lagw.hip's tiling: per event, its
+    occurrences in stages of 64, its (d, a2) tiles in workgroup blocks, the (shift, fit)
+    columns in groups): the structured products plus the G entries that are no H entry and the
+    padding."""
+    cnt = lg.cnt
+    D = 2 * (lg.smax - lg.smin) + 1
+    nh = (lg.m + 1 + 31) // 32
+    nq = nact * lg.K
+    MB, NN = (32, 64) if nq <= 64 else (16, 128)
+    cols = -(-nq // NN) * NN
+    tot = 0.0
+    for a, c in enumerate(cnt):
+        tm = D * (nh - (a >> 5))
+        tot += float(-(-int(c) // 64) * 64) * (-(-tm // MB) * MB * 32)
+    return 2.0 * tot * cols
 
 
 def _syrk_cbits(d: Design, bf, prob: Problem, fits: np.ndarray, st, ev=None):

@@ -96,6 +96,20 @@ def test_lag_gram_w_matches_dense(engine, torch_mod, m, shifts, row0, event_majo
         assert np.max(np.abs(a - b)) <= 2e-6 * max(1.0, float(np.max(np.abs(a)))), k
 
 
+def test_lag_gram_w_cost_model(engine, torch_mod):
+    """The structured Gram is chosen for the C4 shape (2000 lag columns, 2 % events) and not
+    for a small design whose dense Gram costs microseconds."""
+    from sglm_hip import synth
+    s = synth.make(N=200_000, m=50, L=40, family="poisson", rho=0.02, seed=0)
+    d = engine.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
+    lg = engine._lagw(d)
+    assert lg is not None and engine._lagw_pays(d, lg, 5)
+    s2 = synth.make(N=20_000, m=6, L=5, family="poisson", rho=0.05, seed=1)
+    d2 = engine.Design.from_events(s2.E, s2.shifts, s2.L - 1, s2.N)
+    lg2 = engine._lagw(d2)
+    assert lg2 is not None and not engine._lagw_pays(d2, lg2, 5)
+
+
 def test_lag_gram_w_irregular_shifts_fall_back(engine, torch_mod):
     rng = np.random.default_rng(3)
     E = _events(rng, 3000, 9, 0.05)
@@ -117,6 +131,7 @@ def test_lag_gram_w_in_grid_matches_dense_path(engine, torch_mod, monkeypatch):
     objs = [Objective("irls", engine.FAM_TWEEDIE_LOG, 1.0, float(al), "n", True, 100)
             for al in (1e-3, 1e-2, 1e-1)]
     out = {}
+    monkeypatch.setattr(engine, "_lagw_pays", lambda d, lg, nact: True)   # small: force it
     for flag in (True, False):
         monkeypatch.setattr(engine, "LAG_GRAM_W", flag)
         out[flag] = grid.run(d, s.y, cv, objs, [0] * len(objs))

@@ -28,6 +28,8 @@ def parse(v):
 
 
 def type_of(val):
+    if val in ("True", "False"):
+        return val == "True"
     for t in (int, float):
         try:
             return t(val)
