@@ -82,6 +82,14 @@ lag_gram_w_kernel(LagWArgs a) {
     const int n0 = blockIdx.y * NN;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r = lane & 31;
     const int wm = wave % WM, wn = wave / WM;
+    // a G entry of row d and a column of shift smin + sb is an H entry only when the second
+    // shift smin + sb - d is a column, i.e. sb in [d, d + K - 1]: a workgroup whose d rows and
+    // columns never meet has nothing to store
+    {
+        const int sb_lo = n0 / a.nf, sb_hi = min(a.K - 1, (n0 + NN - 1) / a.nf);
+        const int dd_lo = dmin + di0, dd_hi = dmin + di1;
+        if (sb_hi < dd_lo || sb_lo > dd_hi + a.K - 1) return;
+    }
 
     // weights: column n = sb nf + f (shift smin + sb, fit f) of occurrence v is Wt[v nf + n], so a
     // stage's columns n0 .. n0 + NN of one occurrence are one contiguous run, read as 16-byte
@@ -169,14 +177,25 @@ lag_gram_w_kernel(LagWArgs a) {
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = (f32x16){};
 
-    // this wave's tiles: tau = t0 + wm MT + i -> (d row, a2 half); LDS offsets of their words
+    // this wave's tiles: tau = t0 + wm MT + i -> (d row, a2 half); LDS offsets of their words;
+    // live bit (i, j): tile i's d meets a column of N tile j (else its products are no H entry)
     int toff[MT];
+    uint32_t live = 0;
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
         const int tau = min(t0 + wm * MT + i, Tm - 1);
         const int dl = tau / nh1 - di0, hf = h0 + tau % nh1;
         toff[i] = (hf * ND + dl) * kKS + 8 * h;         // in words, within one buffer
+        const int dd = dmin + di0 + dl;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const int c0 = n0 + (wn * NT + j) * 32;
+            const int sb_lo = c0 / a.nf, sb_hi = min(a.K - 1, (c0 + 31) / a.nf);
+            if (t0 + wm * MT + i < Tm && sb_hi >= dd && sb_lo <= dd + a.K - 1)
+                live |= 1u << (i * NT + j);
+        }
     }
+    live = __builtin_amdgcn_readfirstlane(live);
     const int boff = (wn * NT * 32 + r) * kWS + 8 * h;   // in bf16, within one buffer
 
     auto compute = [&](int buf) {
@@ -190,6 +209,7 @@ lag_gram_w_kernel(LagWArgs a) {
                 bq[j] = *reinterpret_cast<const bf16x8*>(wsb + boff + j * 32 * kWS + 16 * ks);
 #pragma unroll
             for (int i = 0; i < MT; ++i) {
+                if (!((live >> (i * NT)) & ((1u << NT) - 1))) continue;
                 const uint32_t* wp = rwb + toff[i] + 16 * ks;
                 const uint4 w0 = *reinterpret_cast<const uint4*>(wp);
                 const uint4 w1 = *reinterpret_cast<const uint4*>(wp + 4);
@@ -202,8 +222,9 @@ lag_gram_w_kernel(LagWArgs a) {
                 const bf16x8 aq = __builtin_bit_cast(bf16x8, make_uint4(dq[0], dq[1], dq[2], dq[3]));
 #pragma unroll
                 for (int j = 0; j < NT; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq, bq[j], acc[i][j], 0, 0,
-                                                                        0);
+                    if ((live >> (i * NT + j)) & 1u)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq, bq[j], acc[i][j],
+                                                                            0, 0, 0);
             }
         }
     };
