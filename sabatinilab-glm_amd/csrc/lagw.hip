@@ -88,7 +88,7 @@ lag_gram_w_kernel(LagWArgs a) {
     {
         const int sb_lo = n0 / a.nf, sb_hi = min(a.K - 1, (n0 + NN - 1) / a.nf);
         const int dd_lo = dmin + di0, dd_hi = dmin + di1;
-        if (sb_hi < dd_lo || sb_lo > dd_hi + a.K - 1) return;
+        if (sb_lo >= a.K || sb_hi < dd_lo || sb_lo > dd_hi + a.K - 1) return;
     }
 
     // weights: column n = sb nf + f (shift smin + sb, fit f) of occurrence v is Wt[v nf + n], so a
@@ -191,7 +191,7 @@ lag_gram_w_kernel(LagWArgs a) {
         for (int j = 0; j < NT; ++j) {
             const int c0 = n0 + (wn * NT + j) * 32;
             const int sb_lo = c0 / a.nf, sb_hi = min(a.K - 1, (c0 + 31) / a.nf);
-            if (t0 + wm * MT + i < Tm && sb_hi >= dd && sb_lo <= dd + a.K - 1)
+            if (t0 + wm * MT + i < Tm && sb_lo < a.K && sb_hi >= dd && sb_lo <= dd + a.K - 1)
                 live |= 1u << (i * NT + j);
         }
     }
