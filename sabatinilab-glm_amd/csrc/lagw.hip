@@ -27,7 +27,7 @@
 namespace sglm {
 namespace {
 
-constexpr int kKS = 64;             // occurrences per stage (4 MFMA K-steps)
+constexpr int kKS = 128;            // occurrences per stage (8 MFMA K-steps)
 constexpr int kWS = kKS + 8;        // weight row stride (bf16): conflict-free b128 reads
 
 struct LagWArgs {
@@ -51,7 +51,10 @@ __device__ __forceinline__ int lag_col(const LagWArgs& a, int b, int ev) {
 
 template <int MT, int NT, int WM, int WN>
 struct LagWSmem {
-    uint32_t rw[2][2][WM * MT + 1][kKS];              // [buf][lo/hi word][d row][occurrence]
+    // [buf][lo/hi word][d row][X/Y][occurrence pair]: X = low halves of the pair's two words
+    // (w0 & 0xffff | w1 << 16), Y = their high halves, so that lane r of an A fragment finds
+    // bit r of both words 16 apart in one word: one rotate and one mask per dword
+    uint32_t rw[2][2][WM * MT + 1][2][kKS / 2];
     __attribute__((aligned(16))) uint16_t ws[2][WN * NT * 32][kWS];   // [buf][(f, b1)][occ]
     int32_t occ[4][kKS];
 };
@@ -99,11 +102,11 @@ lag_gram_w_kernel(LagWArgs a) {
     constexpr int kNP = NN / 8;                          // pieces per occurrence
     constexpr int kWTN = (kKS / 2) * kNP;                // tasks per stage
     constexpr int kWT = (kWTN + NTH - 1) / NTH;          // tasks per thread (at most)
-    constexpr int kRE = (ND * kKS + NTH - 1) / NTH;      // row words per thread (at most)
+    constexpr int kRE = (ND * (kKS / 2) + NTH - 1) / NTH;   // word pairs per thread (at most)
 
     // two register sets: while stage s is multiplied, the loads of stage s + 2 are in flight
     // and stage s + 1 (loaded during stage s - 1) waits in the other set for the LDS store
-    uint64_t rA[kRE], rB[kRE];
+    uint64_t rA[kRE][2], rB[kRE][2];
     uint4 wA[kWT][2], wB[kWT][2];
     int32_t oreg = 0;
 
@@ -114,19 +117,22 @@ lag_gram_w_kernel(LagWArgs a) {
     auto occ_store = [&](int s) {
         if (tid < kKS) sm.occ[s & 3][tid] = oreg;
     };
-    auto data_load = [&](int s, uint64_t (&rreg)[kRE], uint4 (&wreg)[kWT][2]) {
+    auto data_load = [&](int s, uint64_t (&rreg)[kRE][2], uint4 (&wreg)[kWT][2]) {
         const int* ov = sm.occ[s & 3];
 #pragma unroll
         for (int i = 0; i < kRE; ++i) {
             const int e = tid + NTH * i;
-            uint64_t x = 0;
-            if (e < nd * kKS) {
-                const int dl = e / kKS, k = e % kKS;
-                const int v = ov[k];
-                const int u = v + dmin + di0 + dl;
-                if (v >= 0 && u >= 0 && u < a.nraw) x = a.R[u];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                uint64_t x = 0;
+                if (e < nd * (kKS / 2)) {
+                    const int dl = e / (kKS / 2), k = 2 * (e % (kKS / 2)) + j;
+                    const int v = ov[k];
+                    const int u = v + dmin + di0 + dl;
+                    if (v >= 0 && u >= 0 && u < a.nraw) x = a.R[u];
+                }
+                rreg[i][j] = x;
             }
-            rreg[i] = x;
         }
 #pragma unroll
         for (int i = 0; i < kWT; ++i) {
@@ -145,14 +151,20 @@ lag_gram_w_kernel(LagWArgs a) {
             }
         }
     };
-    auto data_store = [&](int buf, const uint64_t (&rreg)[kRE], const uint4 (&wreg)[kWT][2]) {
+    auto data_store = [&](int buf, const uint64_t (&rreg)[kRE][2],
+                          const uint4 (&wreg)[kWT][2]) {
 #pragma unroll
         for (int i = 0; i < kRE; ++i) {
             const int e = tid + NTH * i;
-            if (e < nd * kKS) {
-                const int dl = e / kKS, k = e % kKS;
-                sm.rw[buf][0][dl][k] = (uint32_t)rreg[i];
-                sm.rw[buf][1][dl][k] = (uint32_t)(rreg[i] >> 32);
+            if (e < nd * (kKS / 2)) {
+                const int dl = e / (kKS / 2), kp = e % (kKS / 2);
+#pragma unroll
+                for (int pl = 0; pl < 2; ++pl) {
+                    const uint32_t w0 = (uint32_t)(rreg[i][0] >> (32 * pl));
+                    const uint32_t w1 = (uint32_t)(rreg[i][1] >> (32 * pl));
+                    sm.rw[buf][pl][dl][0][kp] = (w0 & 0xffffu) | (w1 << 16);
+                    sm.rw[buf][pl][dl][1][kp] = (w0 >> 16) | (w1 & 0xffff0000u);
+                }
             }
         }
 #pragma unroll
@@ -185,7 +197,7 @@ lag_gram_w_kernel(LagWArgs a) {
     for (int i = 0; i < MT; ++i) {
         const int tau = min(t0 + wm * MT + i, Tm - 1);
         const int dl = tau / nh1 - di0, hf = h0 + tau % nh1;
-        toff[i] = (hf * ND + dl) * kKS + 8 * h;         // in words, within one buffer
+        toff[i] = ((hf * ND + dl) * 2 + (r >> 4)) * (kKS / 2) + 4 * h;   // words, one buffer
         const int dd = dmin + di0 + dl;
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
@@ -197,9 +209,10 @@ lag_gram_w_kernel(LagWArgs a) {
     }
     live = __builtin_amdgcn_readfirstlane(live);
     const int boff = (wn * NT * 32 + r) * kWS + 8 * h;   // in bf16, within one buffer
+    const uint32_t rsh = (uint32_t)(r - 14 - 16 * (r >> 4)) & 31u;   // bit r (mod 16) -> 14
 
     auto compute = [&](int buf) {
-        const uint32_t* rwb = &sm.rw[buf][0][0][0];
+        const uint32_t* rwb = &sm.rw[buf][0][0][0][0];
         const uint16_t* wsb = &sm.ws[buf][0][0];
 #pragma unroll 2
         for (int ks = 0; ks < kKS / 16; ++ks) {
@@ -210,15 +223,11 @@ lag_gram_w_kernel(LagWArgs a) {
 #pragma unroll
             for (int i = 0; i < MT; ++i) {
                 if (!((live >> (i * NT)) & ((1u << NT) - 1))) continue;
-                const uint32_t* wp = rwb + toff[i] + 16 * ks;
-                const uint4 w0 = *reinterpret_cast<const uint4*>(wp);
-                const uint4 w1 = *reinterpret_cast<const uint4*>(wp + 4);
-                const uint32_t wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+                const uint4 wq = *reinterpret_cast<const uint4*>(rwb + toff[i] + 8 * ks);
+                const uint32_t wv[4] = {wq.x, wq.y, wq.z, wq.w};
                 uint32_t dq[4];
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    dq[q] = (rotr32(wv[2 * q], (r - 14) & 31) & 0x4000u) |
-                            (rotr32(wv[2 * q + 1], (r - 30) & 31) & 0x40000000u);
+                for (int q = 0; q < 4; ++q) dq[q] = rotr32(wv[q], rsh) & 0x40004000u;
                 const bf16x8 aq = __builtin_bit_cast(bf16x8, make_uint4(dq[0], dq[1], dq[2], dq[3]));
 #pragma unroll
                 for (int j = 0; j < NT; ++j)
@@ -229,7 +238,7 @@ lag_gram_w_kernel(LagWArgs a) {
         }
     };
     // stage s: cur holds stage s + 1 (stored to LDS at the end), nxt receives stage s + 2
-    auto step = [&](int s, uint64_t (&rc)[kRE], uint4 (&wc)[kWT][2], uint64_t (&rn)[kRE],
+    auto step = [&](int s, uint64_t (&rc)[kRE][2], uint4 (&wc)[kWT][2], uint64_t (&rn)[kRE][2],
                     uint4 (&wn_)[kWT][2]) {
         occ_store(s + 3);                                // stage s + 3's rows (or -1s)
         __syncthreads();
