@@ -15,8 +15,11 @@
 // exact 0/1, f32 accumulation), in another order.
 //
 // Layout: R[u] (u64 per raw row u): bit a = e_a(u), bit m = 1 (the ones column: d = 0).
-// Workgroup: 4 waves, one event a1, 4 MT tiles of 32 (d, a2) rows (a2 >= a1 only: the rest are
-// the transposes of later events' blocks) x NT tiles of 32 (f, b1) columns, over ALL of a1's
+// Rows: every a2 but only d >= 0 -- the entry of d < 0 is the transpose of event a2's entry at
+// -d > 0 (and at d = 0, a2 < a1 is left to a2's launch): each H entry formed once, half the d
+// range of forming every entry from both sides.
+// Workgroup: 8 waves, one event a1, WM MT tiles of 32 (d, a2) rows x WN NT tiles of 32 (shift,
+// fit) columns, over ALL of a1's
 // occurrences (no split: every H entry is written once, by one lane, no reduction).  Per stage
 // of KS occurrences the row words of the workgroup's d range and the bf16 weights are staged in
 // LDS (double buffered, the next stage's loads in flight during this stage's MFMAs); the A
@@ -71,7 +74,7 @@ lag_gram_w_kernel(LagWArgs a) {
     constexpr int NN = WN * NT * 32;                     // columns per workgroup
     __shared__ LagWSmem<MT, NT, WM, WN> sm;
     const int a1 = blockIdx.x / a.Gm, g = blockIdx.x % a.Gm;
-    const int h0 = a1 >> 5;                              // a2 halves below a1 are skipped
+    const int h0 = 0;                                    // every a2 (both 32-event halves)
     const int nh1 = a.nh - h0;
     const int Tm = a.D * nh1;
     const int t0 = g * MB;
@@ -79,7 +82,7 @@ lag_gram_w_kernel(LagWArgs a) {
     const int di0 = t0 / nh1;
     const int di1 = min(Tm - 1, t0 + MB - 1) / nh1;
     const int nd = di1 - di0 + 1;
-    const int dmin = a.smin - a.smax;
+    const int dmin = 0;                                  // d = 0 .. K - 1 (see below)
     const int o_beg = a.ev_off[a1], o_end = a.ev_off[a1 + 1];
     const int nst = (o_end - o_beg + kKS - 1) / kKS;
     const int n0 = blockIdx.y * NN;
@@ -290,9 +293,8 @@ lag_gram_w_kernel(LagWArgs a) {
                 const int a2 = 32 * hf + (q & 3) + 8 * (q >> 2) + 4 * h;
                 const float val = 0.5f * acc[i][j][q];
                 if (a2 < a.m) {
-                    if (a2 < a1) continue;
+                    if (dd == 0 && a2 < a1) continue;        // formed by event a2's launch
                     const int cj = lag_col(a, b2, a2);
-                    if (a2 == a1 && ci > cj) continue;
                     const int lo = min(ci, cj), hi = max(ci, cj);
                     Hf[(int64_t)lo * a.P + hi] = val;
                 } else if (a2 == a.m && dd == 0) {
@@ -417,7 +419,7 @@ extern "C" int sglm_lag_gram_w(const uint64_t* R, const int32_t* occ, const int3
     a.fits = fits; a.H = H; a.ld = ld; a.nf = nf; a.P = P; a.p = p; a.m = m; a.K = K;
     a.smin = smin; a.smax = smax; a.layout = layout; a.row0 = row0; a.n = n; a.nraw = nraw;
     a.nh = (m + 1 + 31) / 32;
-    a.D = 2 * (smax - smin) + 1;
+    a.D = K;                                             // d = s_b1 - s_b2 >= 0 only
     const int64_t pad = (int64_t)P * (P - p - 1);
     const unsigned gx = 1 + (unsigned)((pad + 255) / 256 < 512 ? (pad + 255) / 256 : 512);
     float* part = (float*)((uint16_t*)work + 8 * a.wlen);

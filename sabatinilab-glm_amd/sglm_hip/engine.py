@@ -3131,14 +3131,14 @@ def _lagw_exec_flop(lg, nact: int) -> float:
     columns in groups): the structured products plus the G entries that are no H entry and the
     padding."""
     cnt = lg.cnt
-    D = 2 * (lg.smax - lg.smin) + 1
+    D = lg.K                                             # d = 0 .. K - 1, every a2
     nh = (lg.m + 1 + 31) // 32
     nq = nact * lg.K
     MB, NN = (32, 64) if nq <= 64 else (16, 128)
     cols = -(-nq // NN) * NN
     tot = 0.0
     for a, c in enumerate(cnt):
-        tm = D * (nh - (a >> 5))
+        tm = D * nh
         tot += float(-(-int(c) // 64) * 64) * (-(-tm // MB) * MB * 32)
     return 2.0 * tot * cols
 
