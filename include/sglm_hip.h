@@ -197,7 +197,8 @@ int sglm_syrk_cbits(const int64_t* desc, int32_t P, const int32_t* fits, int32_t
  * (row <= col; the padding columns > p zeroed).  col(b, a) = layout ? a K + b : b m + a.
  * R: sglm_lag_rowwords of the events; occ / ev_off: every event's occurrence rows, event-major,
  * ascending, and the event segments (m + 1); bidx[s - smin] = b of shift s (-1 if absent).
- * Replaces the dense Gram's n p^2 products by nnz(E) m (2 (smax - smin) + 1) K per fit.
+ * Replaces the dense Gram's n p^2 products by about nnz(E) (m + 1) K^2 per fit (each event's
+ * occurrences x every event at the shift differences d >= 0 x the shifts).
  * The shift set must be a contiguous range (in any order). */
 int sglm_lag_gram_w(const uint64_t* R, const int32_t* occ, const int32_t* ev_off, int32_t m,
                     int32_t nraw, const int32_t* shifts, const int32_t* bidx, int32_t K,

@@ -5,26 +5,26 @@
 // folded in) the Gram entry of columns (b1, a1), (b2, a2) is, with v = t + row0 - s_b1 an
 // occurrence of a1 and d = s_b1 - s_b2,
 //     H[(b1,a1)][(b2,a2)] = sum over v in occ(a1) of e_a2(v + d) * w(v - row0 + s_b1)
-// -- for each event a1 ONE matrix product over a1's occurrences (K = |occ(a1)|):
-//     G_a1[(d, a2)][(f, b1)] = sum_v A[v][(d, a2)] B[v][(f, b1)],
+// -- for each event a1 ONE matrix product over a1's occurrences:
+//     G_a1[(d, a2)][(s, f)] = sum_v A[v][(d, a2)] B[v][(s, f)],
 //     A[v][(d, a2)] = e_a2(v + d)            (bit a2 of the row word R[v + d])
-//     B[v][(f, b1)] = bf16(w_f(v - row0 + s_b1))
-// and every G entry is one H entry (b2 = the shift s_b1 - d).  The dense Gram sums n rows of
-// p^2 products; this sums nnz(E) occurrences of m (2 L - 1) x L products per fit: 2 rho of the
-// dense work at event density rho (C4: 0.04).  The products are the dense kernel's (bf16 w times
-// exact 0/1, f32 accumulation), in another order.
+//     B[v][(s, f)] = bf16(w_f(v - row0 + s))
+// and every G entry whose second shift s - d is a column is one H entry.  The dense Gram sums n
+// rows of p^2 products; this sums nnz(E) occurrences of about (m + 1) L^2 products per fit,
+// rho of the dense work at event density rho (C4: 0.02).  The products are the dense kernel's
+// (bf16 w times exact 0/1, f32 accumulation), in another order.
 //
 // Layout: R[u] (u64 per raw row u): bit a = e_a(u), bit m = 1 (the ones column: d = 0).
 // Rows: every a2 but only d >= 0 -- the entry of d < 0 is the transpose of event a2's entry at
 // -d > 0 (and at d = 0, a2 < a1 is left to a2's launch): each H entry formed once, half the d
 // range of forming every entry from both sides.
 // Workgroup: 8 waves, one event a1, WM MT tiles of 32 (d, a2) rows x WN NT tiles of 32 (shift,
-// fit) columns, over ALL of a1's
-// occurrences (no split: every H entry is written once, by one lane, no reduction).  Per stage
-// of KS occurrences the row words of the workgroup's d range and the bf16 weights are staged in
-// LDS (double buffered, the next stage's loads in flight during this stage's MFMAs); the A
+// fit) columns, over ALL of a1's occurrences (no split: every H entry is written once, by one
+// lane, no reduction).  Per stage of KS occurrences the row words of the workgroup's d range and
+// the bf16 weights are staged in LDS (double buffered, two stages of loads in flight); the A
 // operand is expanded from the staged words (bf16 2.0 / 0, the factor 2 removed at the store),
-// the B operand is one ds_read_b128 per N tile.
+// the B operand is one ds_read_b128 per N tile; (d, shift-tile) pairs that form no H entry are
+// skipped.
 #include "common.h"
 
 namespace sglm {
