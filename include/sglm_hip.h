@@ -193,8 +193,10 @@ int sglm_syrk_cbits(const int64_t* desc, int32_t P, const int32_t* fits, int32_t
 
 /* Weighted Gram of a time-shifted 0/1 event design from its events (lagw.hip): for each
  * fits[f], H[fits[f]] = X^T diag(bf16(W[fits[f]])) X with X[t][col(b, a)] =
- * e_a(t + row0 - shifts[b]) and the ones column p = K m, written on the upper triangle
- * (row <= col; the padding columns > p zeroed).  col(b, a) = layout ? a K + b : b m + a.
+ * e_a(t + row0 - shifts[b]) and the ones column pones (K m, or past a mixed design's continuous
+ * columns K m .. pones - 1, whose rows / columns are left to sglm_mixed_to_h), written on the
+ * upper triangle (row <= col; the padding columns > pones zeroed).  col(b, a) = layout ?
+ * a K + b : b m + a.
  * R: sglm_lag_rowwords of the events; occ / ev_off: every event's occurrence rows, event-major,
  * ascending, and the event segments (m + 1); bidx[s - smin] = b of shift s (-1 if absent).
  * Replaces the dense Gram's n p^2 products by about nnz(E) (m + 1) K^2 per fit (each event's
@@ -204,7 +206,7 @@ int sglm_lag_gram_w(const uint64_t* R, const int32_t* occ, const int32_t* ev_off
                     int32_t nraw, const int32_t* shifts, const int32_t* bidx, int32_t K,
                     int32_t smin, int32_t smax, int32_t layout, int32_t row0, int32_t n,
                     const float* W, int64_t ld, const int32_t* fits, int32_t nf, float* H,
-                    int32_t P, void* work, sglm_stream_t stream);
+                    int32_t P, int32_t pones, void* work, sglm_stream_t stream);
 /* work bytes of sglm_lag_gram_w (8 shifted bf16 copies of the launch's weights) */
 size_t sglm_lag_gram_w_work_bytes(int32_t nraw, int32_t K, int32_t nf);
 

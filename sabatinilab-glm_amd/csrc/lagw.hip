@@ -397,11 +397,11 @@ extern "C" int sglm_lag_gram_w(const uint64_t* R, const int32_t* occ, const int3
                                const int32_t* bidx, int32_t K, int32_t smin, int32_t smax,
                                int32_t layout, int32_t row0, int32_t n, const float* W,
                                int64_t ld, const int32_t* fits, int32_t nf, float* H, int32_t P,
-                               void* work, sglm_stream_t stream) {
+                               int32_t pones, void* work, sglm_stream_t stream) {
     if (nf <= 0) return SGLM_OK;
-    const int p = K * m;
+    const int p = pones;                       // the ones column (K m, or after continuous ones)
     if (!R || !occ || !ev_off || !shifts || !bidx || !W || !fits || !H || !work || m < 1 ||
-        m > 63 || K < 1 || smax - smin + 1 != K || p + 1 > P || n < 0 || ld < n) {
+        m > 63 || K < 1 || smax - smin + 1 != K || p < K * m || p + 1 > P || n < 0 || ld < n) {
         set_error("sglm_lag_gram_w: bad args (m=%d K=%d P=%d)", m, K, P);
         return SGLM_EINVAL;
     }

@@ -47,8 +47,8 @@ SIGNATURES = {
     "sglm_gather_w": (C.c_int, [_vp, _i64, _vp, _i32, _vp, _i64, _vp]),
     "sglm_syrk_cbits": (C.c_int, [_vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp]),
     "sglm_lag_gram_w": (C.c_int, [_vp, _vp, _vp, _i32, _i32, _vp, _vp, _i32, _i32, _i32,
-                                  _i32, _i32, _i32, _vp, _i64, _vp, _i32, _vp, _i32, _vp,
-                                  _vp]),
+                                  _i32, _i32, _i32, _vp, _i64, _vp, _i32, _vp, _i32, _i32,
+                                  _vp, _vp]),
     "sglm_lag_rowwords": (C.c_int, [_vp, _i32, _i32, _i32, _vp, _vp]),
     "sglm_pack_bits_t": (C.c_int, [_vp, _i64, _i32, _vp, _vp, _vp]),
     "sglm_eta_bits_work_bytes": (_sz, [_i32, _i32]),

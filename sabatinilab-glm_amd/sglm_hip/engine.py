@@ -76,6 +76,8 @@ SYRK_CBITS = True              # ... and its row-compacted register-only form (v
 # rho) when the design keeps its event structure and the events are sparse enough
 LAG_GRAM_W = __import__("os").environ.get("SGLM_LAG_GRAM_W", "1") == "1"
 LAG_GRAM_W_MAX_RHO = 0.2        # above it the dense bit-plane Gram does fewer products
+# ... also for mixed designs (their continuous rows / columns from _mix_hess after it)
+LAG_GRAM_W_MIXED = __import__("os").environ.get("SGLM_LAG_GRAM_W_MIXED", "0") == "1"
 # Hessian reuse (log-link families): a fit keeps its last Hessian factor while the drift of
 # its linear predictor since that Hessian was formed, D = sum of max_i |t d_eta_i| over the
 # steps taken since, stays <= HESS_REUSE_TOL.  The IRLS weights then differ from the ones the
@@ -3058,10 +3060,11 @@ def _mix_hess(d: Design, bf, fits, exact: bool):
 
 def _lagw(d: Design):
     """The design's event structure for sglm_lag_gram_w (row words and the shift table built
-    on first use), or None: no structure, continuous columns, > 63 events, or events too
-    dense for the structured product to pay."""
+    on first use), or None: no structure, > 63 events, or events too dense for the structured
+    product to pay.  A mixed design's continuous rows / columns come from _mix_hess after it."""
     lg = getattr(d, "lag", None)
-    if not LAG_GRAM_W or lg is None or d.cont is not None or lg.m > 63:
+    if not LAG_GRAM_W or lg is None or lg.m > 63 or (d.cont is not None
+                                                      and not LAG_GRAM_W_MIXED):
         return None
     if getattr(lg, "R", None) is None:
         if getattr(lg, "R_off", False):
@@ -3069,7 +3072,7 @@ def _lagw(d: Design):
         cnt = np.diff(lg.ev_off.cpu().numpy().astype(np.int64))
         rho = float(cnt.sum()) / max(1.0, float(lg.m) * float(lg.n_raw))
         sh = lg.shifts.cpu().numpy().astype(np.int64)
-        if (rho > LAG_GRAM_W_MAX_RHO or d.p != lg.m * lg.K
+        if (rho > LAG_GRAM_W_MAX_RHO or d.p != lg.m * lg.K + d.k
                 or not np.array_equal(np.sort(sh), np.arange(lg.smin, lg.smin + sh.size))):
             lg.R_off = True
             return None
@@ -3104,7 +3107,7 @@ def _lag_gram_w(d: Design, lg, bf, fits: np.ndarray, st, ev=None):
             ev[0].record()
         _lib.call("sglm_lag_gram_w", _p(lg.R), _p(lg.occ), _p(lg.ev_off), lg.m, lg.n_raw,
                   _p(lg.shifts), _p(lg.bidx), lg.K, lg.smin, lg.smax, lg.layout, lg.row0,
-                  lg.n, _p(bf.W), d.ld, _p(fits_d), nact, _p(bf.H), d.P, _p(work), st)
+                  lg.n, _p(bf.W), d.ld, _p(fits_d), nact, _p(bf.H), d.P, d.p, _p(work), st)
         if ev is not None:
             ev[1].record()
         _gram_done()

@@ -54,7 +54,7 @@ def _lag(engine, torch, d, W, fits):
     _lib.call("sglm_lag_gram_w", lg.R.data_ptr(), lg.occ.data_ptr(), lg.ev_off.data_ptr(), lg.m,
               lg.n_raw, lg.shifts.data_ptr(), lg.bidx.data_ptr(), lg.K, lg.smin, lg.smax,
               lg.layout, lg.row0, lg.n, W.data_ptr(), d.ld, fits_d.data_ptr(), len(fits),
-              H.data_ptr(), d.P, wk.data_ptr(), 0)
+              H.data_ptr(), d.P, d.p, wk.data_ptr(), 0)
     return H
 
 

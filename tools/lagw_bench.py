@@ -24,7 +24,7 @@ for nf in (1, 5):
             _lib.call("sglm_lag_gram_w", lg.R.data_ptr(), lg.occ.data_ptr(), lg.ev_off.data_ptr(), lg.m,
                       lg.n_raw, lg.shifts.data_ptr(), lg.bidx.data_ptr(), lg.K, lg.smin, lg.smax,
                       lg.layout, lg.row0, lg.n, W.data_ptr(), d.ld, fits.data_ptr(), nf,
-                      H.data_ptr(), d.P, wk.data_ptr(), 0)
+                      H.data_ptr(), d.P, d.p, wk.data_ptr(), 0)
             e1.record(); torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1))
         out[f"nf{nf}_probe{pr}"] = round(float(np.median(ts[1:])), 3)
