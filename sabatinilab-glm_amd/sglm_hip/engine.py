@@ -77,7 +77,8 @@ SYRK_CBITS = True              # ... and its row-compacted register-only form (v
 LAG_GRAM_W = __import__("os").environ.get("SGLM_LAG_GRAM_W", "1") == "1"
 LAG_GRAM_W_MAX_RHO = 0.2        # above it the dense bit-plane Gram does fewer products
 # ... also for mixed designs (their continuous rows / columns from _mix_hess after it)
-LAG_GRAM_W_MIXED = __import__("os").environ.get("SGLM_LAG_GRAM_W_MIXED", "0") == "1"
+# (c4mixed 49.4 -> 35.1 ms = 1.10x the C4 grid; tests/test_gpu_mixed.py green)
+LAG_GRAM_W_MIXED = __import__("os").environ.get("SGLM_LAG_GRAM_W_MIXED", "1") == "1"
 # Hessian reuse (log-link families): a fit keeps its last Hessian factor while the drift of
 # its linear predictor since that Hessian was formed, D = sum of max_i |t d_eta_i| over the
 # steps taken since, stays <= HESS_REUSE_TOL.  The IRLS weights then differ from the ones the
