@@ -3131,9 +3131,12 @@ def _lagw_pays(d: Design, lg, nact: int) -> bool:
 
 def _lagw_exec_flop(lg, nact: int) -> float:
     """MFMA flop the sglm_lag_gram_w launch executes (csrc/lagw.hip's tiling: per event, its
-    occurrences in stages of 64, its (d, a2) tiles in workgroup blocks, the (shift, fit)
+    occurrences in stages of 128, its (d, a2) tiles in workgroup blocks, the (shift, fit)
     columns in groups): the structured products plus the G entries that are no H entry and the
     padding."""
+    memo = lg.__dict__.setdefault("exec_flop", {})
+    if nact in memo:
+        return memo[nact]
     cnt = lg.cnt
     D = lg.K                                             # d = 0 .. K - 1, every a2
     nh = (lg.m + 1 + 31) // 32
@@ -3143,8 +3146,9 @@ def _lagw_exec_flop(lg, nact: int) -> float:
     tot = 0.0
     for a, c in enumerate(cnt):
         tm = D * nh
-        tot += float(-(-int(c) // 64) * 64) * (-(-tm // MB) * MB * 32)
-    return 2.0 * tot * cols
+        tot += float(-(-int(c) // 128) * 128) * (-(-tm // MB) * MB * 32)
+    memo[nact] = 2.0 * tot * cols
+    return memo[nact]
 
 
 def _syrk_cbits(d: Design, bf, prob: Problem, fits: np.ndarray, st, ev=None):
