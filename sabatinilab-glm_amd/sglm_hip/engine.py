@@ -3131,25 +3131,26 @@ def _lagw_pays(d: Design, lg, nact: int) -> bool:
 
 def _lagw_exec_flop(lg, nact: int) -> float:
     """MFMA flop the sglm_lag_gram_w launch executes (csrc/lagw.hip's tiling: per event, its
-    occurrences in stages of 128, its (d, a2) tiles in workgroup blocks, the (shift, fit)
-    columns in groups): the structured products plus the G entries that are no H entry and the
-    padding."""
+    occurrences in stages of 128; rows (d, a2) for d = 0 .. K - 1 in two 32-event halves; the
+    (shift, fit) columns in 32-column tiles, a (d, tile) pair run only when some column of the
+    tile forms an H entry at that d): the structured products plus the G entries that are no H
+    entry and the padding."""
     memo = lg.__dict__.setdefault("exec_flop", {})
     if nact in memo:
         return memo[nact]
-    cnt = lg.cnt
-    D = lg.K                                             # d = 0 .. K - 1, every a2
+    K = lg.K
     nh = (lg.m + 1 + 31) // 32
-    nq = nact * lg.K
-    MB, NN = (32, 64) if nq <= 64 else (16, 128)
-    cols = -(-nq // NN) * NN
-    tot = 0.0
-    for a, c in enumerate(cnt):
-        tm = D * nh
-        tot += float(-(-int(c) // 128) * 128) * (-(-tm // MB) * MB * 32)
-    memo[nact] = 2.0 * tot * cols
+    nq = nact * K
+    NN = 64 if nq <= 64 else 128
+    ntiles = -(-nq // NN) * NN // 32
+    pairs = 0
+    for j in range(ntiles):
+        lo, hi = (32 * j) // nact, min(K - 1, (32 * j + 31) // nact)
+        if lo < K:
+            pairs += hi + 1                      # live for d = 0 .. hi
+    occ = float(sum(-(-int(c) // 128) * 128 for c in lg.cnt))
+    memo[nact] = 2.0 * occ * nh * pairs * 32 * 32
     return memo[nact]
-
 
 def _syrk_cbits(d: Design, bf, prob: Problem, fits: np.ndarray, st, ev=None):
     """Gram v6 over per-mask compacted bit-planes.  Slots are ordered by mask so that the
