@@ -39,13 +39,10 @@ struct LagWArgs {
     const uint64_t* R;
     const int32_t* occ;
     const int32_t* ev_off;
-    const int32_t* shifts;          // [K]
     const int32_t* bidx;            // [smax - smin + 1]: b of shift smin + i, -1 if absent
-    const float* W;
     const int32_t* fits;
     float* H;
-    int64_t ld;
-    int32_t nf, P, p, m, K, smin, smax, layout, row0, n, nraw, nh, D, Gm;
+    int32_t nf, P, p, m, K, smin, smax, layout, nraw, nh, D, Gm;
 };
 
 __device__ __forceinline__ int lag_col(const LagWArgs& a, int b, int ev) {
@@ -415,9 +412,9 @@ extern "C" int sglm_lag_gram_w(const uint64_t* R, const int32_t* occ, const int3
         const int st0 = check_launch("lag_gram_w_prep");
         if (st0) return st0;
     }
-    a.R = R; a.occ = occ; a.ev_off = ev_off; a.shifts = shifts; a.bidx = bidx; a.W = W;
-    a.fits = fits; a.H = H; a.ld = ld; a.nf = nf; a.P = P; a.p = p; a.m = m; a.K = K;
-    a.smin = smin; a.smax = smax; a.layout = layout; a.row0 = row0; a.n = n; a.nraw = nraw;
+    a.R = R; a.occ = occ; a.ev_off = ev_off; a.bidx = bidx;
+    a.fits = fits; a.H = H; a.nf = nf; a.P = P; a.p = p; a.m = m; a.K = K;
+    a.smin = smin; a.smax = smax; a.layout = layout; a.nraw = nraw;
     a.nh = (m + 1 + 31) / 32;
     a.D = K;                                             // d = s_b1 - s_b2 >= 0 only
     const int64_t pad = (int64_t)P * (P - p - 1);
