@@ -59,6 +59,10 @@ CONFIGS = {
     # the production 50-split grid (er_refactored_from_scratch_cleanup.py:230-246, 421-452) at
     # the logged 1,900,992-row frame (02-create_features-lynne-f5.ipynb): 18 events x 41 lags
     "prod50": (1_900_992, 18, 20, 50, 1),
+    # the multi-session production flow of sglm_cb_concat_make_design_mat.py:244-363 at the
+    # logged frame size: 18 events x 41 lags + 2 counters + session dummies, 3 splits, OLS
+    # without intercept
+    "cbprod": (1_900_992, 18, 20, 3, 1),
 }
 DM_TRIALS = 100_000                 # ~9.8M rows at 50 Hz (a ~54 h session, or a day's sessions)
 DM_CPU_TRIALS = 20_000              # the pandas sample (~2M rows, ~6 s)
@@ -182,30 +186,35 @@ def cpu_reference_grid(s, cv_idx, lams, rows, lam_sample=(0, 10, 19), fold_threa
             "cpu": _cpu_model(), "nproc": os.cpu_count()}
 
 
-def cpu_reference_full(s, cv_idx, lams, j=10):
-    """The BASELINE.md §2 CPU measurement: ONE full-size split fit (split 0's train rows) and the
-    full refit at lambda index j, sklearn TweedieRegressor(power=1, alpha) with its default
-    lbfgs (backend/sglm.py:112-115) on dense float64 copies (X[idx_train] as the reference's
-    fold loop makes them, backend/sglm_cv.py:107-110); the grid = the mean of the two fit times
-    x 120 fits, labelled extrapolated.  Returns (seconds per grid, detail dict)."""
+def cpu_reference_full(s, cv_idx, lams, js=(0, 10, 19)):
+    """The BASELINE.md §2 CPU measurement at full size: for each sampled lambda index j, ONE
+    split fit (split 0's train rows) and the full refit, sklearn TweedieRegressor(power=1,
+    alpha) with its default lbfgs (backend/sglm.py:112-115) on dense float64 copies
+    (X[idx_train] as the reference's fold loop makes them, backend/sglm_cv.py:107-110).  The
+    strongest, middle and weakest penalties are sampled because lbfgs' iteration count moves
+    with lambda.  Grid = mean over the sampled lambdas of (n_splits x split fit + refit) x the
+    lambda count, labelled extrapolated.  Returns (seconds per grid, detail dict)."""
     from sklearn.linear_model import TweedieRegressor
-    alpha = float(lams[j])
     tr = np.asarray(cv_idx[0][0])
     X = dense_slice(s, s.N)
-    t0 = time.perf_counter()
     Xtr = X[tr]
-    m1 = TweedieRegressor(power=1, alpha=alpha).fit(Xtr, s.y[tr])
-    t_split = time.perf_counter() - t0
-    del Xtr
-    t0 = time.perf_counter()
-    m2 = TweedieRegressor(power=1, alpha=alpha).fit(X, s.y)
-    t_refit = time.perf_counter() - t0
-    del X
-    nfits = len(lams) * (len(cv_idx) + 1)
-    grid_s = 0.5 * (t_split + t_refit) * nfits
-    return grid_s, {"split_fit_s": round(t_split, 2), "refit_s": round(t_refit, 2),
-                    "lbfgs_iters": [int(m1.n_iter_), int(m2.n_iter_)], "lambda": alpha,
-                    "rows": [int(tr.size), int(s.N)]}
+    ytr = s.y[tr]
+    per = []
+    for j in js:
+        alpha = float(lams[j])
+        t0 = time.perf_counter()
+        m1 = TweedieRegressor(power=1, alpha=alpha).fit(Xtr, ytr)
+        t_split = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        m2 = TweedieRegressor(power=1, alpha=alpha).fit(X, s.y)
+        t_refit = time.perf_counter() - t0
+        per.append({"lambda_index": int(j), "lambda": alpha, "split_fit_s": round(t_split, 2),
+                    "refit_s": round(t_refit, 2),
+                    "lbfgs_iters": [int(m1.n_iter_), int(m2.n_iter_)]})
+    del X, Xtr
+    nspl = len(cv_idx)
+    grid_s = float(np.mean([nspl * q["split_fit_s"] + q["refit_s"] for q in per])) * len(lams)
+    return grid_s, {"lambdas": per, "rows": [int(tr.size), int(s.N)]}
 
 
 def cpu_port_iter(s, n_rows_unit, rows):
@@ -762,6 +771,145 @@ def bench_ols(a):
         "cpu_baseline": cpu}))
 
 
+CB_NOT_SFTD = ["time_from_enl_onset", "time_from_enlp_onset"]
+CB_TRIAL_CONSTANTS = ["iBlock", "nTrial"]
+
+
+def cb_flow(df0, X_cols, neg, pos, folds=3, timings=None, y_="grn"):
+    """sglm_cb_concat_make_design_mat.py:244-363 replayed through the drop-in API: the frame
+    convert_dtypes()'d (:244), the response's NaN rows dropped (:251), session dummies (:262),
+    the event columns shifted (sglm_ez.timeshift_cols for the driver's own pandas CB_timeshifts
+    -- the same columns and names, :50-74, 271-276; the lagged frame stays on the device), the
+    flagged trials dropped (:281-283), the trial constants assigned back (:287), dropna (:294),
+    holdout_split_by_trial_id 20 % (:305-311), cv_idx_by_trial_id (folds, test 20 %, :330-334),
+    nTrial dropped (:343-344), simple_cv_fit OLS fit_intercept=False (:346-352) and
+    training_fit_holdout_score (:357; the driver's function, :131-153).  Returns (simple_cv_fit
+    results, holdout R^2, X_setup, y_setup, cv indices, column list)."""
+    import contextlib
+    import io
+    import random
+    import pandas as pd
+    import torch
+    import sglm_ez
+    ph = {} if timings is None else timings
+
+    def mark(name, t):
+        torch.cuda.synchronize()
+        now = time.perf_counter()
+        ph[name] = ph.get(name, 0.0) + now - t
+        return now
+    t = time.perf_counter()
+    with contextlib.redirect_stdout(io.StringIO()):
+        df = df0.convert_dtypes()
+        df_y = df.dropna(subset=y_).reset_index(drop=True)
+        df_y = pd.get_dummies(df_y, columns=["session"])
+        session_constants = [c for c in df_y.columns if "session" in c]
+        t = mark("prepare", t)
+        dfrel = sglm_ez.timeshift_cols(df_y, X_cols, neg_order=neg, pos_order=pos)
+        X_cols_sftd = sglm_ez.add_timeshifts_to_col_list(X_cols, X_cols, neg_order=neg,
+                                                         pos_order=pos)
+        t = mark("timeshift_cols", t)
+        dfrel = dfrel.loc[df_y["flag"] == 0]
+        df_y = df_y.loc[df_y["flag"] == 0]
+        dfrel[CB_TRIAL_CONSTANTS] = df_y[CB_TRIAL_CONSTANTS]
+        assert np.all(dfrel.index == df_y.index)
+        dfrel = dfrel.dropna()
+        df_y = df_y.loc[df_y.index.isin(dfrel.index.values)]
+        t = mark("flag_constants_dropna", t)
+        X_cols_sftd = X_cols_sftd + ["nTrial"] + CB_NOT_SFTD + session_constants
+        np.random.seed(30186)
+        random.seed(30186)
+        holdout = sglm_ez.holdout_split_by_trial_id(dfrel, id_cols=["nTrial"], perc_holdout=0.2)
+        dfrel_holdout, dfrel_setup = dfrel.loc[holdout], dfrel.loc[~holdout]
+        X_setup, X_holdout = dfrel_setup[X_cols_sftd].copy(), dfrel_holdout[X_cols_sftd].copy()
+        y_setup, y_holdout = dfrel_setup[y_].copy(), dfrel_holdout[y_].copy()
+        cv = sglm_ez.cv_idx_by_trial_id(X_setup, y=y_setup, trial_id_columns=["nTrial"],
+                                        num_folds=folds, test_size=0.2)
+        dfrel["holdout_mask"] = holdout
+        X_setup = X_setup.drop(columns=["nTrial"])
+        X_holdout = X_holdout.drop(columns=["nTrial"])
+        t = mark("holdout_and_folds", t)
+        hp = [{"alpha": 0.0, "l1_ratio": 0.0, "max_iter": 1000, "fit_intercept": False}]
+        out = sglm_ez.simple_cv_fit(X_setup, y_setup, cv, hp, model_type="Normal", verbose=0,
+                                    score_method="r2")
+        t = mark("simple_cv_fit", t)
+        _, hs, _ = sglm_ez.training_fit_holdout_score(X_setup, y_setup, X_holdout, y_holdout,
+                                                      out[2])
+        mark("training_fit_holdout_score", t)
+    return out, hs, X_setup, y_setup, cv, [c for c in X_cols_sftd if c != "nTrial"]
+
+
+def cpu_reference_cb(X_setup, y_setup, cv, folds):
+    """The reference's CPU path for the cb flow sampled the BASELINE.md §2 way: sklearn
+    LinearRegression(fit_intercept=False) (GLM('Normal', alpha=0, fit_intercept=False),
+    backend/sglm.py:96-101) on ONE full-size fold's train rows of the materialised float64
+    design and on the full setup rows (the refit); workload = folds x fold fit + 2 full fits
+    (simple_cv_fit's refit and training_fit_holdout_score's), extrapolated."""
+    from sklearn.linear_model import LinearRegression
+    X = X_setup.to_numpy(dtype=np.float64)
+    y = np.asarray(y_setup.to_numpy(dtype=np.float64, na_value=np.nan))
+    tr = np.asarray(cv[0][0])
+    Xtr = X[tr]
+    t0 = time.perf_counter()
+    LinearRegression(fit_intercept=False).fit(Xtr, y[tr])
+    t_fold = time.perf_counter() - t0
+    del Xtr
+    t0 = time.perf_counter()
+    LinearRegression(fit_intercept=False).fit(X, y)
+    t_refit = time.perf_counter() - t0
+    total = folds * t_fold + 2 * t_refit
+    return {"value": total, "unit": "s per workload (extrapolated)", "cores": _blas_threads(),
+            "kind": "reference",
+            "sample": f"sklearn LinearRegression(fit_intercept=False) on fold 0's {tr.size} "
+                      f"train rows x {X.shape[1]} ({t_fold:.1f} s) and on the {X.shape[0]} "
+                      f"setup rows ({t_refit:.1f} s); x{folds} folds + 2 full fits",
+            "cpu": _cpu_model(), "nproc": os.cpu_count()}
+
+
+def bench_cb(a):
+    """The multi-session production flow of sglm_cb_concat_make_design_mat.py (cb_flow) on one
+    GPU at the logged production frame size: 1,900,992 rows, 18 events x 41 lags + the two
+    counters + one dummy per session (4 sessions), 3 splits.  One step = the whole flow from the
+    host frame."""
+    import torch
+    from sglm_hip import synth
+    N, m, L, K, _ = CONFIGS[a.config]
+    df, ev, beta, gamma, offs = synth.cb_frame(N, m, -L, L, sessions=4, seed=13)
+    for _ in range(a.warmup):
+        cb_flow(df, ev, -L, L, K)
+    torch.cuda.synchronize()
+    ph = {}
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        out, hs, X_setup, y_setup, cv, xcols = cb_flow(df, ev, -L, L, K, ph)
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / a.steps
+    coef = np.asarray(out[3].model.coef_)
+    nl = len(ev) * (2 * L + 1)
+    truth_err = float(np.max(np.abs(coef[:nl] - beta.reshape(-1))))
+    cpu = None if a.no_cpu else cpu_reference_cb(X_setup, y_setup, cv, K)
+    print(json.dumps({
+        "metric": "IRLS iters/sec on 1M\u00d72000 design mat; CV-grid wall-clock (5-fold\u00d720 \u03bb)",
+        "value": el, "unit": "s per production workload (host frame -> fits -> holdout score)",
+        "n_gpus": 1, "steps": a.steps, "warmup": a.warmup, "ms_per_step": el * 1e3,
+        "higher_is_better": False, "scaling": "strong", "vs_baseline": None,
+        "dtype": "f64 (exact 0/1 Gram in f32 integers + float64 continuous rows, float64 "
+                 "normal equations)",
+        "data": "synthetic",
+        "config": {"workload": f"Gaussian OLS (fit_intercept=False) {N} rows x {len(xcols)} "
+                               f"predictors ({m} events x {2 * L + 1} lags + 2 counters + "
+                               f"{len(xcols) - nl - 2} session dummies), {K} splits + refit + "
+                               f"holdout score, sglm_cb_concat_make_design_mat.py:244-363 from "
+                               f"a host frame",
+                   "config_name": a.config, "setup_rows": int(X_setup.shape[0]),
+                   "phases_ms": {k: v / a.steps * 1e3 for k, v in ph.items()},
+                   "best_cv_R2": float(out[0]), "holdout_R2": float(hs),
+                   "refit_lag_coef_max_abs_err_vs_truth": truth_err,
+                   "parallelism": "one GPU (the flow is one design; fits batched)"},
+        "roofline": None,
+        "cpu_baseline": cpu}))
+
+
 def spawn_ranks(a):
     """``--gpus N`` without a launcher: start N rank processes (torch.distributed.run, one per
     GPU, rendezvous on 127.0.0.1) as CHILDREN before anything touches the GPU, and exit with
@@ -886,9 +1034,10 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group("gloo")
-    if a.config in ("c5", "prep", "signal", "designmat", "olsref", "prod50"):
+    if a.config in ("c5", "prep", "signal", "designmat", "olsref", "prod50", "cbprod"):
         {"c5": bench_c5, "prep": bench_prep, "signal": bench_signal,
-         "designmat": bench_designmat, "olsref": bench_ols, "prod50": bench_ols}[a.config](a)
+         "designmat": bench_designmat, "olsref": bench_ols, "prod50": bench_ols,
+         "cbprod": bench_cb}[a.config](a)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -948,7 +1097,7 @@ def main():
                       float(stats.gram_fit_iters), float(stats.stops["stagnation"]),
                       float(stats.stops["line_search_failed"] + stats.stops["max_iter"]),
                       float(stats.aliased), float(stats.newton_iters), float(stats.shared),
-                  float(stats.roundtrips), stats.sync_wait_s],
+                  float(stats.roundtrips), stats.sync_wait_s, stats.alg_flop_dense],
                      dtype=torch.float64, device="cuda" if a.dist_backend == "nccl" else "cpu")
     if world > 1:
         mx = t.clone()
@@ -961,13 +1110,14 @@ def main():
             # every rank runs every fit: the fit / Newton / Gram counts and the algorithmic
             # flop are the same on all ranks (not disjoint shares); the Gram launches, their
             # time and flop and the host waits are per rank
-            for q in (1, 5, 6, 7, 8, 9, 10, 11, 12, 13):
+            for q in (1, 5, 6, 7, 8, 9, 10, 11, 12, 13, 16):
                 t[q] /= world
     fit_iters, ktime, kflop, nlaunch = float(t[1]), float(t[2]), float(t[3]), int(t[4])
     gram_fits, alg_flop, reused, gram_iters = float(t[5]), float(t[6]), float(t[7]), float(t[8])
     stag, failed = int(t[9]), int(t[10])
     aliased, newton_iters = float(t[11]), float(t[12])
     shared, roundtrips, sync_wait = float(t[13]), float(t[14]), float(t[15])
+    alg_flop_dense = float(t[16])
     if rank == 0:
         grid_s = elapsed / a.steps
         achieved = kflop / ktime / 1e12 if ktime > 0 else 0.0
@@ -1014,11 +1164,17 @@ def main():
                 cpu["row_sample_extrapolation_s"] = cpu["value"]
                 cpu["row_sample"] = cpu["sample"]
                 cpu["value"] = full_s
-                cpu["sample"] = (f"sklearn TweedieRegressor(power=1, alpha={det['lambda']:.3g}) "
-                                 f"lbfgs on the full-size split-0 train rows ({det['rows'][0]} x "
-                                 f"{s.p}, {det['split_fit_s']} s, {det['lbfgs_iters'][0]} iters) "
-                                 f"and the full refit ({det['rows'][1]} rows, {det['refit_s']} s, "
-                                 f"{det['lbfgs_iters'][1]} iters); mean x 120 fits")
+                lq = det["lambdas"]
+                cpu["sample"] = ("sklearn TweedieRegressor(power=1) lbfgs at lambda index "
+                                 + ", ".join(str(q["lambda_index"]) for q in lq)
+                                 + f": the full-size split-0 train rows ({det['rows'][0]} x "
+                                 f"{s.p}) and the full refit ({det['rows'][1]} rows); split fits "
+                                 + "/".join(str(q["split_fit_s"]) for q in lq) + " s, refits "
+                                 + "/".join(str(q["refit_s"]) for q in lq) + " s, lbfgs iters "
+                                 + "/".join(f"{q['lbfgs_iters'][0]}+{q['lbfgs_iters'][1]}"
+                                            for q in lq)
+                                 + f"; mean of ({len(cv_idx)} x split + refit) x {len(lams)} "
+                                 "lambdas")
                 cpu["full_fold"] = det
             cpu["port_oracle_newton"] = cpu_port_iter(s, s.N, a.cpu_rows)
         out = {
@@ -1058,7 +1214,15 @@ def main():
                                          / a.steps / max(world, 1) * 1e3,
                 "newton_iters_per_grid": newton_iters / a.steps,
                 "computed_grams_per_grid": gram_fits / a.steps,
+                # flop the grid's kernels executed (each Gram at the count of the kernel that
+                # formed it: event-structured Grams at their structured products, the event
+                # correlations at their histogram adds) / wall / peak
                 "grid_roofline_frac": alg_flop / elapsed / (world * PEAK_BF16_TFLOPS * 1e12),
+                "grid_roofline_frac_kind": "executed (structured Grams at their own count)",
+                # the same grid with every computed Gram charged SURVEY.md §8(d)'s dense
+                # n p'(p'+1): the work a dense Gram would have done (not executed here)
+                "grid_dense_equiv_frac": alg_flop_dense / elapsed
+                                         / (world * PEAK_BF16_TFLOPS * 1e12),
                 "all_converged": bool(conv),
                 "stagnation_or_failed_stops": stag + failed,
                 "newton_dist_f64": ndist,

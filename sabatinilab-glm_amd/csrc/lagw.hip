@@ -25,6 +25,8 @@
 // operand is expanded from the staged words (bf16 2.0 / 0, the factor 2 removed at the store),
 // the B operand is one ds_read_b128 per N tile; (d, shift-tile) pairs that form no H entry are
 // skipped.
+#include <type_traits>
+
 #include "common.h"
 
 namespace sglm {
@@ -47,6 +49,10 @@ struct LagWArgs {
 
 __device__ __forceinline__ int lag_col(const LagWArgs& a, int b, int ev) {
     return a.layout ? ev * a.K + b : b * a.m + ev;
+}
+
+__device__ __forceinline__ int lag_col2(int layout, int m, int K, int b, int ev) {
+    return layout ? ev * K + b : b * m + ev;
 }
 
 template <int MT, int NT, int WM, int WN>
@@ -129,7 +135,8 @@ lag_gram_w_kernel(LagWArgs a) {
                     const int dl = e / (kKS / 2), k = 2 * (e % (kKS / 2)) + j;
                     const int v = ov[k];
                     const int u = v + dmin + di0 + dl;
-                    if (v >= 0 && u >= 0 && u < a.nraw) x = a.R[u];
+                    if (v >= 0 && u >= 0 && u < a.nraw)
+                        x = a.R[u];
                 }
                 rreg[i][j] = x;
             }
@@ -347,12 +354,14 @@ __global__ void __launch_bounds__(256) lag_gram_w_aux(const float* __restrict__ 
     }
 }
 
-// Wt copy c, element j = bf16(W[fits[f]][u - row0 + smin]) at i = j + c = u nf + f (0 off the
-// design's rows): the weights of raw rows u - smin .. in (row, fit) order, shifted by c
+// Wt copy c, element j = bf16(W[fits[f]][u - row0 + smin]) at i = j + c = u nf + f: the weights of
+// raw rows u - smin .. in (row, fit) order, shifted by c; 0 off the
+// design's rows and for raw rows u >= zrow (the zero row a workgroup reads past its event's end)
 __global__ void __launch_bounds__(256) lag_gram_w_prep(const float* __restrict__ W, int64_t ld,
                                                        int32_t n, const int32_t* __restrict__ fits,
                                                        int32_t nf, int32_t row0, int32_t smin,
-                                                       int64_t wlen, uint16_t* __restrict__ Wt) {
+                                                       int64_t wlen, int64_t zrow,
+                                                       uint16_t* __restrict__ Wt) {
     const int c = blockIdx.y;
     for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < wlen;
          j += (int64_t)gridDim.x * 256) {
@@ -360,7 +369,7 @@ __global__ void __launch_bounds__(256) lag_gram_w_prep(const float* __restrict__
         const int64_t u = i / nf;
         const int f = (int)(i % nf);
         const int64_t t = u - row0 + smin;
-        const float x = (t >= 0 && t < n) ? W[(int64_t)fits[f] * ld + t] : 0.0f;
+        const float x = (t >= 0 && t < n && u < zrow) ? W[(int64_t)fits[f] * ld + t] : 0.0f;
         Wt[c * wlen + j] = __builtin_bit_cast(uint16_t, (__bf16)x);
     }
 }
@@ -375,14 +384,419 @@ int launch_lagw(const LagWArgs& a, hipStream_t s) {
     return check_launch("lag_gram_w_kernel");
 }
 
+
+// ---- v2 (round 6): coalesced staging, transposed-read weight image, XCD-local pieces ----------
+//
+// The same products as lag_gram_w_kernel; what changed is how the operands reach the LDS and how
+// the result leaves it:
+// * weights: 16 lanes stage one occurrence's NN columns (a contiguous run of the (row, fit)
+//   weights, one aligned copy of the 8) with 16-byte loads and ds_write_b128 into an [occurrence]
+//   [column] image whose 16-byte chunks are XOR-swizzled by row; the B operand comes back with two
+//   ds_read_b64_tr_b16 (the hardware transpose), conflict-free on that image;
+// * row words: lanes over the d rows of one occurrence pair (consecutive words: one or two lines
+//   per 8 lanes instead of one line per lane), stored pair-interleaved with a 4-dword pad per d row
+//   (conflict-free 4-byte stores);
+// * pieces: a workgroup is (event a1, d group g, column block y); XCD x (blocks b = x mod 8) takes
+//   the pieces [x Q, x Q + Q) in event-major order, so the workgroups that stream one event's
+//   occurrences share an XCD's L2 (the weights once per event, not once per d group);
+// * result: every H entry is written at the row of the column (s_b1, a1) that formed it --
+//   H[(b1, a1)][(b2, a2)], a2 contiguous in a shift-major design -- and lag_gram_w_sym then builds
+//   the upper triangle from whichever of (i, j) / (j, i) holds an entry (the old epilogue wrote
+//   every d > 0 entry down a column of the upper triangle: 4-byte scatter, 9x write amplification).
+constexpr int kKS2 = 128;                 // occurrences per stage
+constexpr int kKP2 = kKS2 / 2;            // occurrence pairs per stage
+constexpr int kRX2 = kKP2 + 4;            // dwords per (half, X / Y) row of a d row's words
+constexpr int kRS2 = 4 * kRX2 + 4;        // dwords per d row of the staged row words
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+struct LagW2Args {
+    const uint16_t* Wt;             // 8 shifted copies of the bf16 weights by (raw row, fit)
+    int64_t wlen;                   // elements per copy (a multiple of 8)
+    const uint64_t* R;
+    const int32_t* occ;
+    const int32_t* ev_off;
+    const int32_t* bidx;            // [K]: b of shift smin + i
+    const int32_t* fits;
+    float* H;
+    int32_t nf, P, p, m, K, smin, smax, layout, nraw, nh, D, Gm, Gy, Q, npieces, zrow;
+};
+
+template <int NCH>
+__device__ __forceinline__ int lagw_swz(int row) {       // chunk XOR of the weight image's row
+    return NCH == 16 ? ((row & 3) << 2) : (((row >> 1) & 1) << 2);
+}
+
+template <int MT, int NT, int WM, int WN>
+struct LagW2Smem {
+    static constexpr int MB = WM * MT, NN = WN * NT * 32;
+    uint32_t rw[2][MB * kRS2];                                  // [buf][d row][pl][xy][pair]
+    __attribute__((aligned(16))) uint16_t ws[2][kKS2 * NN];     // [buf][occurrence][column]
+    int32_t occ[4][64 * WM * WN];          // every thread stores (rows kKS2 .. : unread)
+};
+
+template <int MT, int NT, int WM, int WN>
+__global__ void __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(2, 2)))
+lag_gram_w2_kernel(LagW2Args a) {
+    using SM = LagW2Smem<MT, NT, WM, WN>;
+    constexpr int NTH = 64 * WM * WN, MB = SM::MB, NN = SM::NN, NCH = NN / 8;
+    static_assert((kKS2 * NCH) % NTH == 0, "weight tasks per thread");
+    constexpr int kWT = kKS2 * NCH / NTH;
+    constexpr int kRT = (kKP2 * MB + NTH - 1) / NTH;
+    __shared__ SM sm;
+    // piece of this workgroup: XCD x = b mod 8 takes pieces [x Q, x Q + Q), event-major, the
+    // d groups of one column block adjacent (they stream the same weights)
+    const int pc = (int)(blockIdx.x & 7) * a.Q + (int)(blockIdx.x >> 3);
+    if (pc >= a.npieces) return;
+    const int per = a.Gm * a.Gy;
+    const int a1 = pc / per, rem = pc % per;
+    const int g = rem % a.Gm, y = rem / a.Gm;
+    const int nh = a.nh, Tm = a.D * nh;
+    const int t0 = g * MB;
+    if (t0 >= Tm) return;
+    const int di0 = t0 / nh;
+    const int di1 = min(Tm - 1, t0 + MB - 1) / nh;
+    const int nd = di1 - di0 + 1;
+    const int n0 = y * NN;
+    // a G entry of row d and a column of shift smin + sb is an H entry only when sb >= d (its
+    // second shift smin + sb - d is then a column): a piece whose columns all precede its d rows
+    // has nothing to store
+    if (n0 / a.nf >= a.K || min(a.K - 1, (n0 + NN - 1) / a.nf) < di0) return;
+    const int o_beg = a.ev_off[a1], o_end = a.ev_off[a1 + 1];
+    // stages, rounded up to even (the loop body is two stages; a stage past the event's end
+    // reads the zero row and adds nothing): every load of the pipeline is unconditional, so the
+    // compiler's wait counts stay exact
+    const int nst = (o_end - o_beg + 2 * kKS2 - 1) / (2 * kKS2) * 2;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r = lane & 31;
+    const int wm = wave % WM, wn = wave / WM;
+
+    // the row-word tasks of this thread (the same every stage): pair kp, d row dl
+    const int ntr = kKP2 * nd;
+    int rkp[kRT], rdl[kRT];
+#pragma unroll
+    for (int i = 0; i < kRT; ++i) {
+        const int t = tid + NTH * i;
+        rkp[i] = t < ntr ? t / nd : -1;
+        rdl[i] = t < ntr ? t % nd : 0;
+    }
+
+    // Every load below is unconditional, from a clamped address, and what is invalid is masked
+    // when the registers are stored (a load whose result is selected against a constant makes
+    // hipcc wait for it right away, which would serialise the staging pipeline)
+    uint4 wA[kWT], wB[kWT];
+    uint64_t rA[kRT][2], rB[kRT][2];
+    uint32_t vA = 0, vB = 0;                  // validity of the row-word loads, bit 2 i + j
+    int32_t oreg = 0;
+    bool ovalid = false;
+
+    auto occ_load = [&](int s) {
+        const int o = o_beg + s * kKS2 + tid;
+        ovalid = tid < kKS2 && o < o_end;
+        oreg = a.occ[ovalid ? o : o_beg];
+    };
+    auto occ_store = [&](int s) { sm.occ[s & 3][tid] = ovalid ? oreg : -1; };
+    auto data_load = [&](int s, uint4 (&wreg)[kWT], uint64_t (&rreg)[kRT][2], uint32_t& vreg) {
+        const int* ov = sm.occ[s & 3];
+#pragma unroll
+        for (int i = 0; i < kWT; ++i) {
+            const int t = tid + NTH * i;
+            const int k = t / NCH, ch = t % NCH;
+            const int v = ov[k];
+            const int64_t u = v >= 0 ? v : a.zrow;          // past the event's end: zero weights
+            const int64_t x = u * a.nf + n0 + 8 * ch;
+            const int c = (int)(x & 7);
+            wreg[i] = *reinterpret_cast<const uint4*>(a.Wt + c * a.wlen + (x - c));
+        }
+        uint32_t vb = 0;
+#pragma unroll
+        for (int i = 0; i < kRT; ++i) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int v = ov[2 * max(rkp[i], 0) + j];
+                const int u = v + di0 + rdl[i];
+                const bool ok = rkp[i] >= 0 && v >= 0 && u < a.nraw;
+                vb |= (uint32_t)ok << (2 * i + j);
+                rreg[i][j] = a.R[ok ? u : 0];
+            }
+        }
+        vreg = vb;
+    };
+    auto data_store = [&](int buf, const uint4 (&wreg)[kWT], const uint64_t (&rreg)[kRT][2],
+                          uint32_t vreg) {
+#pragma unroll
+        for (int i = 0; i < kWT; ++i) {
+            const int t = tid + NTH * i;
+            const int k = t / NCH, ch = t % NCH;
+            *reinterpret_cast<uint4*>(&sm.ws[buf][k * NN + 8 * (ch ^ lagw_swz<NCH>(k))]) = wreg[i];
+        }
+#pragma unroll
+        for (int i = 0; i < kRT; ++i) {
+            if (rkp[i] < 0) continue;
+            uint32_t* dst = &sm.rw[buf][rdl[i] * kRS2 + rkp[i]];
+            const uint64_t r0 = ((vreg >> (2 * i)) & 1u) ? rreg[i][0] : 0ull;
+            const uint64_t r1 = ((vreg >> (2 * i + 1)) & 1u) ? rreg[i][1] : 0ull;
+#pragma unroll
+            for (int pl = 0; pl < 2; ++pl) {
+                const uint32_t w0 = (uint32_t)(r0 >> (32 * pl));
+                const uint32_t w1 = (uint32_t)(r1 >> (32 * pl));
+                dst[(2 * pl) * kRX2] = (w0 & 0xffffu) | (w1 << 16);
+                dst[(2 * pl + 1) * kRX2] = (w0 >> 16) | (w1 & 0xffff0000u);
+            }
+        }
+    };
+
+    f32x16 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = (f32x16){};
+
+    // A: tile i = (d row, event half) -> its staged words.  Live N tiles: tile j's columns meet a
+    // d of this wave's tiles with a second shift that is a column (sb_hi(j) >= d) and are not
+    // all padding (sb_lo(j) < K) -- a range [j0, j1] of the wave's tiles, wave-uniform and fixed
+    // for the whole launch: the stage loop is instantiated per range (below), so the MFMA stream
+    // has no branch and the fragment reads can be scheduled ahead of it
+    int aoff[MT];
+    int dmin_w = 1 << 30;
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+        const int tau = min(t0 + wm * MT + i, Tm - 1);
+        const int dl = tau / nh - di0, hf = tau % nh;
+        aoff[i] = dl * kRS2 + (2 * hf + (r >> 4)) * kRX2 + 4 * h;
+        if (t0 + wm * MT + i < Tm) dmin_w = min(dmin_w, di0 + dl);
+    }
+    int j0 = NT, j1 = -1;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int c0 = n0 + (wn * NT + j) * 32;
+        const int sb_lo = c0 / a.nf, sb_hi = min(a.K - 1, (c0 + 31) / a.nf);
+        if (sb_lo < a.K && sb_hi >= dmin_w) {
+            j0 = min(j0, j);
+            j1 = max(j1, j);
+        }
+    }
+    const int jcode = __builtin_amdgcn_readfirstlane(j0 > j1 ? -1 : j0 * NT + j1);
+    // B: lane 4q + pp of 16-lane group g4 supplies row 8 (g4 >> 1) + q (+ 4), columns
+    // 16 (g4 & 1) + 4 pp .. + 3 of N tile j; it receives column r of rows 8 h .. 8 h + 7
+    int boff[NT];
+    {
+        const int g4 = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+        const int row = 8 * (g4 >> 1) + q;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const int col = (wn * NT + j) * 32 + 16 * (g4 & 1) + 4 * pp;
+            boff[j] = row * NN * 2 + 16 * ((col >> 3) ^ lagw_swz<NCH>(row)) + 8 * (pp & 1);
+        }
+    }
+    const uint32_t rsh = (uint32_t)(r - 14 - 16 * (r >> 4)) & 31u;   // bit r (mod 16) -> 14
+
+    // the multiplication of one staged stage over the live N tiles J0 .. J1
+    auto compute = [&](int buf, auto J0c, auto J1c) {
+        constexpr int J0 = decltype(J0c)::value, J1 = decltype(J1c)::value;
+        const uint32_t* rwb = &sm.rw[buf][0];
+        const char* wsb = reinterpret_cast<const char*>(&sm.ws[buf][0]);
+#pragma unroll 2
+        for (int ks = 0; ks < kKS2 / 16; ++ks) {
+            bf16x8 bq[NT];
+#pragma unroll
+            for (int j = J0; j <= J1; ++j) {
+                const char* pb = wsb + boff[j] + ks * 16 * NN * 2;
+                const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (lds_s16x4*)(__attribute__((address_space(3))) char*)pb);
+                const s16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (lds_s16x4*)(__attribute__((address_space(3))) char*)(pb + 4 * NN * 2));
+                const uint2 u1 = __builtin_bit_cast(uint2, t1), u2 = __builtin_bit_cast(uint2, t2);
+                bq[j] = __builtin_bit_cast(bf16x8, make_uint4(u1.x, u1.y, u2.x, u2.y));
+            }
+            bf16x8 aq[MT];
+#pragma unroll
+            for (int i = 0; i < MT; ++i) {
+                const uint4 wq = *reinterpret_cast<const uint4*>(rwb + aoff[i] + 8 * ks);
+                const uint32_t wv[4] = {wq.x, wq.y, wq.z, wq.w};
+                uint32_t dq[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) dq[q] = rotr32(wv[q], rsh) & 0x40004000u;
+                aq[i] = __builtin_bit_cast(bf16x8, make_uint4(dq[0], dq[1], dq[2], dq[3]));
+            }
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = J0; j <= J1; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq[i], bq[j], acc[i][j],
+                                                                        0, 0, 0);
+        }
+    };
+    // stage s: the occurrence rows of stage s + 4 and the data of stage s + 2 are loaded, stage s
+    // is multiplied, and stage s + 1 (loaded during stage s - 1) is stored to the other buffer
+    auto main_loop = [&](auto J0c, auto J1c) {
+        auto step = [&](int s, uint4 (&wc)[kWT], uint64_t (&rc)[kRT][2], uint32_t& vc,
+                        uint4 (&wn_)[kWT], uint64_t (&rn)[kRT][2], uint32_t& vn) {
+            occ_store(s + 3);
+            __syncthreads();
+            occ_load(s + 4);
+            data_load(s + 2, wn_, rn, vn);       // past the end: zero rows, never stored
+            compute(s & 1, J0c, J1c);
+            if (s + 1 < nst) data_store((s + 1) & 1, wc, rc, vc);
+        };
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            occ_load(j);
+            occ_store(j);
+        }
+        __syncthreads();
+        data_load(0, wA, rA, vA);
+        data_store(0, wA, rA, vA);
+        occ_load(3);
+        data_load(1, wA, rA, vA);
+        for (int s = 0; s < nst; s += 2) {
+            step(s, wA, rA, vA, wB, rB, vB);
+            step(s + 1, wB, rB, vB, wA, rA, vA);
+        }
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    using IN = std::integral_constant<int, -1>;
+    if (nst > 0) {
+        // an event that never occurs leaves acc = 0 (its H entries are written as zeros)
+        if constexpr (NT == 4) {
+            switch (jcode) {
+                case 0: main_loop(I0{}, I0{}); break;
+                case 1: main_loop(I0{}, I1{}); break;
+                case 2: main_loop(I0{}, I2{}); break;
+                case 3: main_loop(I0{}, I3{}); break;
+                case 5: main_loop(I1{}, I1{}); break;
+                case 6: main_loop(I1{}, I2{}); break;
+                case 7: main_loop(I1{}, I3{}); break;
+                case 10: main_loop(I2{}, I2{}); break;
+                case 11: main_loop(I2{}, I3{}); break;
+                case 15: main_loop(I3{}, I3{}); break;
+                default: main_loop(I0{}, IN{}); break;      // no live tile: staging only
+            }
+        } else {
+            static_assert(NT == 2, "N tiles per wave");
+            switch (jcode) {
+                case 0: main_loop(I0{}, I0{}); break;
+                case 1: main_loop(I0{}, I1{}); break;
+                case 3: main_loop(I1{}, I1{}); break;
+                default: main_loop(I0{}, IN{}); break;
+            }
+        }
+    }
+
+    // epilogue: G entry (d, a2) x (f, b1) -> H_f[(b1, a1)][(b2, a2)] at the row of (b1, a1)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int nn = n0 + (wn * NT + j) * 32 + r;
+        const int sb = nn / a.nf, f = nn % a.nf;           // column: shift smin + sb, fit f
+        if (sb >= a.K) continue;
+        const int b1 = a.bidx[sb];
+        if (b1 < 0) continue;
+        float* Hrow = a.H + (int64_t)a.fits[f] * a.P * a.P + (int64_t)lag_col2(a.layout, a.m, a.K,
+                                                                             b1, a1) * a.P;
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+            const int tau = t0 + wm * MT + i;
+            if (tau >= Tm) continue;
+            const int dd = tau / nh;
+            const int hf = tau % nh;
+            if (sb < dd) continue;                           // second shift below smin
+            const int b2 = a.bidx[sb - dd];
+            if (b2 < 0) continue;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int a2 = 32 * hf + (q & 3) + 8 * (q >> 2) + 4 * h;
+                const float val = 0.5f * acc[i][j][q];
+                if (a2 < a.m) {
+                    if (dd == 0 && a2 < a1) continue;        // formed by event a2's piece
+                    Hrow[lag_col2(a.layout, a.m, a.K, b2, a2)] = val;
+                } else if (a2 == a.m && dd == 0) {
+                    Hrow[a.p] = val;
+                }
+            }
+        }
+    }
+}
+
+// Upper triangle of H_f from the entries lag_gram_w2_kernel wrote: entry {i, j} (i < j) sits at
+// row i when column i has the larger shift, or the same shift and the smaller event (the ones
+// column p: at row i); continuous columns of a mixed design and the padding columns are zeroed
+// (the continuous rows / columns are written after this by _mix_hess).  One 256-thread workgroup
+// per 64 x 64 upper tile (I, J) of one fit: the transposed tile (J, I) staged through LDS.
+__global__ void __launch_bounds__(256) lag_gram_w_sym(float* __restrict__ H,
+                                                      const int32_t* __restrict__ fits, int32_t P,
+                                                      int32_t p, int32_t m, int32_t K,
+                                                      int32_t layout,
+                                                      const int32_t* __restrict__ shifts) {
+    __shared__ float tl[64][65];
+    __shared__ int ks_i[64], ks_j[64];           // (shift, event) keys of the tile's columns
+    const int T = P / 64;
+    int I = 0, rem = blockIdx.x;
+    while (rem >= T - I) { rem -= T - I; ++I; }  // tile (I, J), I <= J, row-major over the upper
+    const int J = I + rem;
+    float* Hf = H + (int64_t)fits[blockIdx.y] * P * P;
+    const int tid = threadIdx.x;
+    const int plag = m * K;
+    if (tid < 128) {
+        const int c = (tid < 64 ? I : J) * 64 + (tid & 63);
+        int key = -1;                            // -1: no lag column
+        if (c < plag) {
+            const int b = layout ? c % K : c / m, e = layout ? c / K : c % m;
+            key = (shifts[b] + 65536) * 64 + (63 - e);    // larger key = the row that holds it
+        }
+        (tid < 64 ? ks_i : ks_j)[tid & 63] = key;
+    }
+    // stage H rows J*64.., columns I*64.. (the lower counterpart)
+    for (int e = tid; e < 64 * 64; e += 256) {
+        const int rr = e >> 6, cc = e & 63;
+        tl[rr][cc] = Hf[(int64_t)(J * 64 + rr) * P + I * 64 + cc];
+    }
+    __syncthreads();
+    for (int e = tid; e < 64 * 64; e += 256) {
+        const int il = e >> 6, jl = e & 63;
+        const int i = I * 64 + il, j = J * 64 + jl;
+        if (i > j) continue;
+        float* dst = Hf + (int64_t)i * P + j;
+        if (j > p) {                             // padding (and its diagonal)
+            *dst = 0.0f;
+            continue;
+        }
+        if (i == j) continue;                    // diagonal: written in place (H[p][p] by aux)
+        if (j == p) {
+            if (i >= plag) *dst = 0.0f;          // a continuous column's ones entry
+            continue;                            // a lag column's: at row i
+        }
+        const int ki = ks_i[il], kj = ks_j[jl];
+        if (ki < 0 || kj < 0) *dst = 0.0f;       // a continuous column
+        else if (kj > ki) *dst = tl[jl][il];     // held at row j
+    }
+}
+
+template <int MT, int NT, int WM, int WN>
+int launch_lagw2(const LagW2Args& a0, hipStream_t s) {
+    LagW2Args a = a0;
+    constexpr int MB = WM * MT, NN = WN * NT * 32;
+    a.Gm = (a.D * a.nh + MB - 1) / MB;
+    a.Gy = (a.nf * a.K + NN - 1) / NN;
+    a.npieces = a.m * a.Gm * a.Gy;
+    a.Q = (a.npieces + 7) / 8;
+    lag_gram_w2_kernel<MT, NT, WM, WN><<<dim3((unsigned)(8 * a.Q)), 64 * WM * WN, 0, s>>>(a);
+    return check_launch("lag_gram_w2_kernel");
+}
+
 }  // namespace
 }  // namespace sglm
 
 using namespace sglm;
 
-// elements of one weight copy (sglm_lag_gram_w's work: 8 copies of 2-byte elements)
+// the zero raw row (weights 0) and the elements of one weight copy (sglm_lag_gram_w's work: 8
+// copies of 2-byte elements): every read of a workgroup -- a valid occurrence's columns, the last
+// column block's padding columns, the zero row's -- lies below wlen
+static int64_t lagw_zrow(int32_t nraw, int32_t K) { return (int64_t)nraw + K + 8; }
 static int64_t lagw_wlen(int32_t nraw, int32_t K, int32_t nf) {
-    return ((int64_t)(nraw + K + 64) * nf + 256 + 7) / 8 * 8;
+    return ((lagw_zrow(nraw, K) + K + 8) * nf + 512 + 7) / 8 * 8;
 }
 
 extern "C" size_t sglm_lag_gram_w_work_bytes(int32_t nraw, int32_t K, int32_t nf) {
@@ -407,7 +821,7 @@ extern "C" int sglm_lag_gram_w(const uint64_t* R, const int32_t* occ, const int3
     a.wlen = lagw_wlen(nraw, K, nf);
     a.Wt = (const uint16_t*)work;
     lag_gram_w_prep<<<dim3(1024, 8), 256, 0, s>>>(W, ld, n, fits, nf, row0, smin, a.wlen,
-                                                  (uint16_t*)work);
+                                                  lagw_zrow(nraw, K), (uint16_t*)work);
     {
         const int st0 = check_launch("lag_gram_w_prep");
         if (st0) return st0;
@@ -421,11 +835,29 @@ extern "C" int sglm_lag_gram_w(const uint64_t* R, const int32_t* occ, const int3
     const unsigned gx = 1 + (unsigned)((pad + 255) / 256 < 512 ? (pad + 255) / 256 : 512);
     float* part = (float*)((uint16_t*)work + 8 * a.wlen);
     lag_gram_w_part<<<dim3(kLwRed, (unsigned)nf), 256, 0, s>>>(W, ld, n, fits, part);
-    lag_gram_w_aux<<<dim3(gx, (unsigned)nf), 256, 0, s>>>(part, fits, H, P, p);
-    int st = check_launch("lag_gram_w_aux");
+    static const int v1 = [] {
+        const char* e = getenv("SGLM_LAGW_V1");
+        return e ? atoi(e) : 0;
+    }();
+    if (v1) {
+        lag_gram_w_aux<<<dim3(gx, (unsigned)nf), 256, 0, s>>>(part, fits, H, P, p);
+        int st = check_launch("lag_gram_w_aux");
+        if (st) return st;
+        if (nf * K <= 64) return launch_lagw<4, 2, 8, 1>(a, s);
+        return launch_lagw<2, 4, 8, 1>(a, s);
+    }
+    LagW2Args b{};
+    b.Wt = a.Wt; b.wlen = a.wlen; b.R = R; b.occ = occ; b.ev_off = ev_off; b.bidx = bidx;
+    b.fits = fits; b.H = H; b.nf = nf; b.P = P; b.p = p; b.m = m; b.K = K; b.smin = smin;
+    b.smax = smax; b.layout = layout; b.nraw = nraw; b.nh = a.nh; b.D = K;
+    b.zrow = (int32_t)lagw_zrow(nraw, K);
+    const int st = (nf * K <= 64) ? launch_lagw2<2, 2, 8, 1>(b, s) : launch_lagw2<2, 4, 8, 1>(b, s);
     if (st) return st;
-    if (nf * K <= 64) return launch_lagw<4, 2, 8, 1>(a, s);
-    return launch_lagw<2, 4, 8, 1>(a, s);
+    const int T = P / 64;
+    lag_gram_w_sym<<<dim3((unsigned)(T * (T + 1) / 2), (unsigned)nf), 256, 0, s>>>(
+        H, fits, P, p, m, K, layout, shifts);
+    lag_gram_w_aux<<<dim3(1, (unsigned)nf), 256, 0, s>>>(part, fits, H, P, p);
+    return check_launch("lag_gram_w_aux");
 }
 
 // R[u] = sum_a bit(e_a(u)) << a | 1 << m from the occurrence bitmaps ebits[m][nwords]

@@ -497,6 +497,24 @@ class Design:
                     hint = None if ones is None else int(np.asarray(ones, np.int64)[ev].sum())
                     return cls.from_events(E, sl, r0, n, device=device, event_major=major,
                                            nnz=hint)
+            # a canonical lag block followed by unshifted columns -- the production design's
+            # counters and session dummies after the event lags (sglm_cb_concat_make_design_
+            # mat.py:286, 310): the lag block from its events (LagStructure: structured Gram and
+            # correlation start), the others as the float64 block of a mixed design
+            L0 = _lag_block_split(cols, shifts)
+            if L0 is not None and mixed_ok(n, int(cols.size) - L0):
+                for major in (False, True):
+                    lay = _canonical_lags(cols[:L0], shifts[:L0], m, major)
+                    if lay is None:
+                        continue
+                    ev, sl = lay
+                    E = Ecm[torch.from_numpy(ev).to(Ecm.device)]
+                    if not bool(((E == 0) | (E == 1)).all()):
+                        break
+                    extra = Ecm[torch.from_numpy(cols[L0:]).to(Ecm.device), r0:r0 + n]
+                    hint = None if ones is None else int(np.asarray(ones, np.int64)[ev].sum())
+                    return cls.from_events(E.t(), sl, r0, n, device=device, event_major=major,
+                                           nnz=hint, extra=extra)
         p = int(cols.size)
         d = cls(n, p, device, zero=True)
         c_d = torch.from_numpy(cols.astype(np.int32)).to(device)
@@ -599,6 +617,10 @@ class Design:
         n, p = Xt.shape
         if Xt.dtype not in (torch.float32, torch.float64):
             Xt = Xt.to(torch.float64)
+        # sklearn's check (as the host upload path and the lagged frame raise it): a NaN would
+        # otherwise sit in the float64 block or the f32 copy and give NaN coefficients
+        if bool(torch.isnan(Xt).any()):
+            raise ValueError("Input X contains NaN.")
         nonbin = np.flatnonzero((~((Xt == 0) | (Xt == 1)).all(dim=0)).cpu().numpy())
         if nonbin.size and mixed_ok(n, int(nonbin.size)):
             d = cls(n, p, device, zero=True)
@@ -667,6 +689,8 @@ class Design:
             extra = torch.as_tensor(extra, dtype=torch.float64).to(device)
             if extra.ndim != 2 or extra.shape[1] != n:
                 raise ValueError(f"extra columns must be (k, {n})")
+            if bool(torch.isnan(extra).any()):
+                raise ValueError("Input X contains NaN.")
         if isinstance(E, np.ndarray):
             E = torch.from_numpy(np.ascontiguousarray(E, dtype=np.float32))
         E = E.to(device=device, dtype=torch.float32)
@@ -876,6 +900,22 @@ def _unpack_bits(bits, n: int):
     """uint8 [rows][n] of device bit rows (int32 [rows][nwords], bit r & 31 of word r >> 5)."""
     sh = torch.arange(32, dtype=torch.int32, device=bits.device)
     return ((bits.unsqueeze(-1) >> sh) & 1).to(torch.uint8).reshape(bits.shape[0], -1)[:, :n]
+
+
+def _lag_block_split(cols, shifts):
+    """L0 when columns 0 .. L0 - 1 are lags of the sources that are ever shifted and every later
+    column is an unshifted column of another source (a lag block followed by extra columns);
+    None otherwise (or when there are no extra columns)."""
+    cols = np.asarray(cols)
+    shifts = np.asarray(shifts)
+    lagged = set(cols[shifts != 0].tolist())
+    if not lagged:
+        return None
+    inl = np.fromiter((c in lagged for c in cols.tolist()), dtype=bool, count=cols.size)
+    L0 = int(np.argmin(inl)) if not inl.all() else cols.size
+    if L0 == 0 or L0 == cols.size or inl[L0:].any() or np.any(shifts[L0:] != 0):
+        return None
+    return L0
 
 
 def _canonical_lags(cols, shifts, m, event_major):
@@ -1327,7 +1367,12 @@ class IrlsStats:
     rank_grams: int = 0         # exact mask Grams for the rank decisions of unpenalised fits
     chain_host_s: float = 0.0   # host time spent enqueueing the factorisation chains
     aa_fit_iters: int = 0       # fit-iterations whose direction took the secant correction
-    alg_flop: float = 0.0       # SURVEY.md §8(d) F summed over fit-iterations
+    # flop actually executed by the algorithm, summed over fit-iterations: each computed Gram at
+    # the count of the kernel that formed it (dense: n p'(p'+1); event-structured: LagStructure
+    # flop1; event correlations: their histogram adds), new factors p'^3/3, gradient / eta /
+    # solves 4 n p' + 2 p'^2
+    alg_flop: float = 0.0
+    alg_flop_dense: float = 0.0  # the same with every computed Gram at SURVEY.md §8(d)'s dense F
     sync_wait_s: float = 0.0    # host time blocked in the per-iteration stream synchronisation
     roundtrips: int = 0         # host<->device round trips (stream synchronisations) of the solve
     trace_phases: bool = False                          # sync + time grid phases (tools)
@@ -2038,6 +2083,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
                     _lag_gram(d, bf, lagg, st)
                     if stats is not None:
                         stats.lag_grams += int(lagg.size)
+                        stats.alg_flop += _lag_corr_flop(d.lag)
                 _syrk(d, bf, np.sort(np.setdiff1d(uniq, lagg)).astype(np.int32), nsteps,
                       ntile1, stats, st, rows=gram_rows)
                 sum_hess(uniq)
@@ -2465,9 +2511,11 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
             # the two triangular solves only)
             pa = float(p + 1)
             nr = rows[act]
-            stats.alg_flop += float(np.sum(np.where(gram_comp[act], nr * pa * (pa + 1), 0.0)
-                                           + np.where(gram_now[act], pa ** 3 / 3, 0.0)
-                                           + 4.0 * nr * pa + 2 * pa * pa))
+            rest = float(np.sum(np.where(gram_now[act], pa ** 3 / 3, 0.0)
+                                + 4.0 * nr * pa + 2 * pa * pa))
+            stats.alg_flop += rest              # the Grams were charged where they were formed
+            stats.alg_flop_dense += rest + float(np.sum(np.where(gram_comp[act],
+                                                                 nr * pa * (pa + 1), 0.0)))
             stats.gram_fit_iters += int(np.sum(gram_comp[act]))
         # a failed line search on a kept (stale) factor, or on a Hessian shared from a lambda
         # neighbour, is not a verdict: the next iteration forms a fresh Hessian of the fit's
@@ -2915,6 +2963,15 @@ def _lag_gram(d: Design, bf, fits: np.ndarray, st):
         _mix_hess(d, bf, fits, False)
 
 
+def _lag_corr_flop(lg) -> float:
+    """Work of one sglm_lag_gram call counted as flop: per occurrence of an event, one bitmap
+    test and histogram add per (other event, lag difference d in (-K, K)) -- 2 ops each."""
+    if lg is None:
+        return 0.0
+    nnz = float(lg.occ.numel())
+    return 2.0 * nnz * (lg.m + 1) * (2 * lg.K - 1)
+
+
 def _max_gram_count(bf, slots) -> float:
     """Largest multiplicity sum over the masks of the given slots (an upper bound on every entry
     of their exact 0/1 mask Grams); inf when the problem is unknown."""
@@ -2996,6 +3053,8 @@ def _syrk(d: Design, bf, fits: np.ndarray, nsteps: int, ntile1: int, stats, st, 
         lg = None
     if lg is not None:
         ab, flop, xflop = _lag_gram_w(d, lg, bf, fits, st, ev)
+        if stats is not None:
+            stats.alg_flop += flop
         if ev is not None:
             stats.syrk_bytes.append(ab)
             stats.syrk_exec.append(xflop)
@@ -3031,9 +3090,11 @@ def _syrk(d: Design, bf, fits: np.ndarray, nsteps: int, ntile1: int, stats, st, 
                       splits, _p(bf.H), _p(work), st)
         if ev is not None:
             ev[1].record()
-    if ev is not None:
+    if stats is not None:
         pa = d.p + 1
         nrows = float(np.sum(rows[fits])) if rows is not None else float(d.n) * nact
+        stats.alg_flop += nrows * pa * (pa + 1)
+    if ev is not None:
         stats.syrk_events.append((ev[0], ev[1], nact, nrows * pa * (pa + 1)))  # algorithmic flop
     if d.cont is not None:
         _mix_hess(d, bf, fits, exact)
@@ -3083,14 +3144,24 @@ def _lagw(d: Design):
         bidx = np.full(lg.smax - lg.smin + 1, -1, dtype=np.int32)
         bidx[sh - lg.smin] = np.arange(sh.size, dtype=np.int32)
         lg.bidx = torch.from_numpy(bidx).to(d.device)
-        # algorithmic flop per fit: one product per (occurrence of a1, b1, b2, a2 >= a1) and per
-        # (occurrence, b1) for the ones column -- the H entries' own terms (the launch also forms
-        # the G entries whose shift s_b1 - d is not a column, and pads rows and columns to 32)
-        lg.flop1 = float(2.0 * sum(int(c) * ((lg.m - a) * lg.K + 1) for a, c in enumerate(cnt))
-                         * lg.K)
+        # algorithmic flop per fit, in the kernel's own decomposition (each H entry's terms
+        # once): per occurrence of a1, the rows d = s_b1 - s_b2 >= 0 -- at d = 0 the events
+        # a2 >= a1 and the ones column, K columns each; at d > 0 every event a2 and the K - d
+        # shifts s_b1 whose s_b1 - d is a column.  The launch also forms the G entries whose
+        # second shift is no column and pads rows and columns to 32 (_lagw_exec_flop >= this)
+        lg.flop1 = _lagw_alg_flop1(lg.m, lg.K, cnt)
         lg.cnt = cnt
         lg.R = R
     return lg
+
+
+def _lagw_alg_flop1(m: int, K: int, cnt) -> float:
+    """Algorithmic flop of the event-structured Gram per fit, in the kernel's decomposition:
+    per occurrence of event a1 the H entries it forms -- at d = s_b1 - s_b2 = 0 the events
+    a2 >= a1 and the ones column over all K shifts, at d > 0 every event a2 over the K - d
+    shifts s_b1 whose s_b1 - d is a column -- one multiply-add each."""
+    return float(2.0 * sum(int(c) * (K * (m - a + 1) + m * K * (K - 1) // 2)
+                           for a, c in enumerate(cnt)))
 
 
 def _lag_gram_w(d: Design, lg, bf, fits: np.ndarray, st, ev=None):
@@ -3100,15 +3171,22 @@ def _lag_gram_w(d: Design, lg, bf, fits: np.ndarray, st, ev=None):
     upl = getattr(bf, "up", None)
     fits_d = upl(fits, np.int32) if upl is not None else \
         torch.from_numpy(np.asarray(fits, dtype=np.int32)).to(d.device)
-    work = _work(_lib.query("sglm_lag_gram_w_work_bytes", lg.n_raw, lg.K, nact), d.device,
+    # the launch's scratch (8 shifted bf16 copies of the fits' weights over every raw row,
+    # ~16 B per raw row per fit) stays within LAGW_WORK_BUDGET: fits in chunks of at most that
+    per1 = _lib.query("sglm_lag_gram_w_work_bytes", lg.n_raw, lg.K, 1)
+    chunk = max(1, min(nact, int(LAGW_WORK_BUDGET // max(1, per1))))
+    work = _work(_lib.query("sglm_lag_gram_w_work_bytes", lg.n_raw, lg.K, chunk), d.device,
                  "lagw")
     with _GRAM_LOCK:
         _gram_turn()
         if ev is not None:
             ev[0].record()
-        _lib.call("sglm_lag_gram_w", _p(lg.R), _p(lg.occ), _p(lg.ev_off), lg.m, lg.n_raw,
-                  _p(lg.shifts), _p(lg.bidx), lg.K, lg.smin, lg.smax, lg.layout, lg.row0,
-                  lg.n, _p(bf.W), d.ld, _p(fits_d), nact, _p(bf.H), d.P, d.p, _p(work), st)
+        for c0 in range(0, nact, chunk):
+            nc = min(chunk, nact - c0)
+            _lib.call("sglm_lag_gram_w", _p(lg.R), _p(lg.occ), _p(lg.ev_off), lg.m, lg.n_raw,
+                      _p(lg.shifts), _p(lg.bidx), lg.K, lg.smin, lg.smax, lg.layout, lg.row0,
+                      lg.n, _p(bf.W), d.ld, _p(fits_d[c0:c0 + nc]), nc, _p(bf.H), d.P, d.p,
+                      _p(work), st)
         if ev is not None:
             ev[1].record()
         _gram_done()
@@ -3116,6 +3194,11 @@ def _lag_gram_w(d: Design, lg, bf, fits: np.ndarray, st, ev=None):
     pa = d.p + 1
     return (8 * lg.n_raw + nact * (4 * lg.n + 4 * pa * (pa + 1) // 2), nact * lg.flop1,
             _lagw_exec_flop(lg, nact))
+
+
+# bytes of sglm_lag_gram_w scratch one launch may use (its fits are split into launches beyond
+# that; the buffer is cached per device, so this bounds what a session keeps allocated)
+LAGW_WORK_BUDGET = float(os.environ.get("SGLM_LAGW_WORK_BUDGET", str(2 << 30)))
 
 
 def _lagw_pays(d: Design, lg, nact: int) -> bool:

@@ -218,15 +218,44 @@ class LagSource:
         return self._hasnan[name]
 
 
-class LagFrame:
-    """A DataFrame-like view: columns ``cols`` (names), each either a base column of
-    ``src.base`` (``spec[c] = (name, 0, False)``), a lag column (``spec[c] = (source name,
-    shift, True)``: value at frame row r = base[name] at row r - shift, NaN outside), or a column
-    assigned to this frame (``overlay``); rows = positions into the base (None = all)."""
+def _lazy(fn):
+    """A LagFrame method answered from the specs while the frame is lazy, and by pandas'
+    DataFrame implementation once it has been materialised."""
+    name = fn.__name__
+
+    def wrap(self, *a, **k):
+        if self._mat is not None:
+            return getattr(super(LagFrame, self), name)(*a, **k)
+        return fn(self, *a, **k)
+    wrap.__name__, wrap.__doc__, wrap.__qualname__ = name, fn.__doc__, fn.__qualname__
+    return wrap
+
+
+class LagFrame(pd.DataFrame):
+    """A pandas DataFrame whose values stay on the device until something needs them:
+    columns ``cols`` (names), each either a base column of ``src.base`` (``spec[c] = (name, 0,
+    False)``), a lag column (``spec[c] = (source name, shift, True)``: value at frame row r =
+    base[name] at row r - shift, NaN outside), or a column assigned to this frame (``overlay``);
+    rows = positions into the base (None = all).
+
+    It IS a ``pd.DataFrame`` (``isinstance`` holds, as for the frame the reference's
+    timeshift_multiple returns, backend/sglm_pp.py:485): the operations of the production flows
+    (column / row selections, boolean ``.loc``, ``dropna``, ``isna().sum(axis=1)``, assignments,
+    ``drop``, ``copy``, the fits) are answered lazily from the specs; anything else -- pandas
+    methods, ``pd.concat``, ``to_parquet``, arithmetic -- reads the frame's block manager, which
+    is then built once from the materialised values (``to_pandas()``), and from there on the
+    object behaves exactly as that DataFrame (every lazy method defers to pandas)."""
 
     def __init__(self, src: LagSource, cols, spec, rows: Optional[np.ndarray] = None,
                  index: Optional[pd.Index] = None, overlay: Optional[dict] = None,
                  inc: bool = False):
+        # the attributes pandas' NDFrame.__init__ sets -- without a manager: it is built from
+        # the materialised values on first use (_mgr below)
+        object.__setattr__(self, "_is_copy", None)
+        object.__setattr__(self, "_item_cache", {})
+        object.__setattr__(self, "_attrs", {})
+        object.__setattr__(self, "_flags", pd.Flags(self, allows_duplicate_labels=True))
+        object.__setattr__(self, "_mat", None)
         self._src = src
         self._cols = list(cols)
         self._spec = spec
@@ -235,6 +264,39 @@ class LagFrame:
         self._index = index
         self._overlay = overlay if overlay is not None else {}
         self._design = None
+
+    # ------------------------------------------------------------------ pandas plumbing
+    @property
+    def _mgr(self):
+        """pandas' block manager: built from the materialised values the first time pandas
+        code touches it (the frame is a plain DataFrame from then on)."""
+        if self._mat is None:
+            object.__setattr__(self, "_mat", self.to_pandas()._mgr)
+        return self._mat
+
+    @_mgr.setter
+    def _mgr(self, value):
+        object.__setattr__(self, "_mat", value)
+
+    @property
+    def _constructor(self):
+        return pd.DataFrame
+
+    def __setattr__(self, name, value):
+        if name.startswith("_"):
+            object.__setattr__(self, name, value)
+        else:
+            self._mgr                                     # materialise, then as pandas does
+            super().__setattr__(name, value)
+
+    def __reduce__(self):
+        return (pd.DataFrame, (self.to_pandas() if self._mat is None else
+                               pd.DataFrame(self._mat),))
+
+    @property
+    def is_lazy(self) -> bool:
+        """True while the values live on the device only (no block manager built yet)."""
+        return self._mat is None
 
     # ------------------------------------------------------------------ construction
     @classmethod
@@ -272,24 +334,42 @@ class LagFrame:
     # ------------------------------------------------------------------ shape / labels
     @property
     def columns(self):
+        if self._mat is not None:
+            return pd.DataFrame.columns.__get__(self, type(self))
         return pd.Index(self._cols)
+
+    @columns.setter
+    def columns(self, value):
+        self._mgr
+        pd.DataFrame.columns.__set__(self, value)
 
     @property
     def index(self):
+        if self._mat is not None:
+            return pd.DataFrame.index.__get__(self, type(self))
         if self._index is None:
             b = self._src.base.index
             sp = self._span()
             self._index = b if self._rows is None else (b[sp[0]:sp[1]] if sp else b[self._rows])
         return self._index
 
+    @index.setter
+    def index(self, value):
+        self._mgr
+        pd.DataFrame.index.__set__(self, value)
+
     @property
     def shape(self):
+        if self._mat is not None:
+            return super().shape
         return (self._nrows(), len(self._cols))
 
     def _nrows(self):
         return self._src.N if self._rows is None else int(self._rows.size)
 
     def __len__(self):
+        if self._mat is not None:
+            return super().__len__()
         return self._nrows()
 
     @property
@@ -298,7 +378,8 @@ class LagFrame:
 
     @property
     def size(self):
-        return self._nrows() * len(self._cols)
+        k, m = self.shape
+        return k * m
 
     @property
     def empty(self):
@@ -306,18 +387,23 @@ class LagFrame:
 
     @property
     def dtypes(self):
+        if self._mat is not None:
+            return super().dtypes
         b = self._src.base
         return pd.Series([self._overlay[c].dtype if c in self._overlay else
                           (np.dtype(np.float64) if self._spec[c][2] else
                            self._src.cast.get(c, b[self._spec[c][0]].dtype))
                           for c in self._cols], index=self.columns, dtype=object)
 
+    @_lazy
     def keys(self):
         return self.columns
 
+    @_lazy
     def __iter__(self):
         return iter(self._cols)
 
+    @_lazy
     def __contains__(self, c):
         return c in self._spec or c in self._overlay
 
@@ -375,15 +461,16 @@ class LagFrame:
         if missing:
             raise KeyError(f"{missing} not in index")
 
+    @_lazy
     def __getitem__(self, key):
         if isinstance(key, str) or (np.isscalar(key) and not isinstance(key, (bool, np.bool_))):
-            return self._series(key)
+            return self._col_series(key)
         if isinstance(key, slice):
             return self._take(np.arange(self._nrows())[key])
         if isinstance(key, LagFrame):
             raise TypeError("boolean frames as keys are not supported on a lagged frame")
         arr = key if isinstance(key, (pd.Series, pd.Index, np.ndarray)) else np.asarray(key)
-        if getattr(arr, "dtype", None) is not None and arr.dtype == bool:
+        if getattr(arr, "dtype", None) is not None and pd.api.types.is_bool_dtype(arr.dtype):
             return self._bool_rows(key)
         cols = list(key)
         self._check_cols(cols)
@@ -391,7 +478,27 @@ class LagFrame:
             return self._base_frame(cols)               # id / response columns: a real frame
         return self._derive(cols=cols)
 
+    @_lazy
     def __setitem__(self, name, value):
+        if isinstance(name, (list, pd.Index, np.ndarray)):
+            # frame[[a, b]] = other[[a, b]] (sglm_cb_concat_make_design_mat.py:275): column by
+            # column, a DataFrame's columns by position, aligned on the index
+            names = list(name)
+            if isinstance(value, pd.DataFrame):
+                if value.shape[1] != len(names):
+                    raise ValueError("Columns must be same length as key")
+                for nm, c in zip(names, range(value.shape[1])):
+                    self[nm] = value.iloc[:, c]
+            elif np.ndim(value) == 2:
+                value = np.asarray(value)
+                if value.shape[1] != len(names):
+                    raise ValueError("Columns must be same length as key")
+                for j, nm in enumerate(names):
+                    self[nm] = value[:, j]
+            else:
+                for nm in names:
+                    self[nm] = value
+            return
         n = self._nrows()
         if isinstance(value, pd.Series):
             value = value.reindex(self.index).to_numpy()
@@ -408,22 +515,25 @@ class LagFrame:
 
     @property
     def loc(self):
-        return _Loc(self)
+        return super().loc if self._mat is not None else _Loc(self)
 
     @property
     def iloc(self):
-        return _ILoc(self)
+        return super().iloc if self._mat is not None else _ILoc(self)
 
+    @_lazy
     def copy(self, deep=True):
         return LagFrame(self._src, self._cols, self._spec, self._rows, self._index,
                         {k: v.copy() for k, v in self._overlay.items()}, inc=self._inc)
 
+    @_lazy
     def reset_index(self, drop=False, **kw):
         if drop and not kw:
             return LagFrame(self._src, self._cols, self._spec, self._rows,
                             pd.RangeIndex(self._nrows()), dict(self._overlay), inc=self._inc)
         return getattr(self.to_pandas(), "reset_index")(drop=drop, **kw)
 
+    @_lazy
     def drop(self, labels=None, axis=0, columns=None, **kw):
         if columns is None and axis in (1, "columns"):
             columns, labels = labels, None
@@ -434,16 +544,19 @@ class LagFrame:
         return self.to_pandas().drop(labels=labels, axis=axis, columns=columns, **kw)
 
     # ------------------------------------------------------------------ missing values
+    @_lazy
     def isna(self):
         return _LagNA(self)
 
     isnull = isna
 
+    @_lazy
     def notna(self):
         return _LagNA(self, negate=True)
 
     notnull = notna
 
+    @_lazy
     def dropna(self, axis=0, how="any", subset=None, inplace=False, **kw):
         if axis not in (0, "index") or inplace or kw:
             return self.to_pandas().dropna(axis=axis, how=how, subset=subset, inplace=inplace,
@@ -561,7 +674,7 @@ class LagFrame:
         out += acc.cpu().numpy()
 
     # ------------------------------------------------------------------ values
-    def _series(self, name) -> pd.Series:
+    def _col_series(self, name) -> pd.Series:
         if name in self._overlay:
             return pd.Series(self._overlay[name], index=self.index, name=name)
         if name not in self._spec:
@@ -622,25 +735,30 @@ class LagFrame:
                 data[c] = self._base_values(self._spec[c][0])
         return pd.DataFrame(data, index=self.index, columns=self._cols)
 
+    @_lazy
     def to_numpy(self, dtype=None, copy=False, na_value=None):
         a = self.to_pandas().to_numpy(dtype=dtype)
         return a
 
     @property
     def values(self):
-        return self.to_numpy()
+        return super().values if self._mat is not None else self.to_numpy()
 
+    @_lazy
     def __array__(self, dtype=None, copy=None):
         a = self.to_numpy()
         return a if dtype is None else a.astype(dtype)
 
+    @_lazy
     def head(self, n=5):
         return self._take(np.arange(min(n, self._nrows()))).to_pandas()
 
+    @_lazy
     def tail(self, n=5):
         k = self._nrows()
         return self._take(np.arange(max(0, k - n), k)).to_pandas()
 
+    @_lazy
     def __repr__(self):
         k, m = self.shape
         if k <= 10:
@@ -652,35 +770,51 @@ class LagFrame:
         return f"{body}\n\n[{k} rows x {m} columns]"
 
     def __getattr__(self, name):
+        # only names that normal lookup did not find (pandas' methods are class attributes):
+        # a column as an attribute, as DataFrame.__getattr__ gives it
         if name.startswith("_"):
             raise AttributeError(name)
+        if self._mat is not None:
+            return pd.DataFrame.__getattr__(self, name)
         if name in self._spec or name in self._overlay:
-            return self._series(name)
-        return getattr(self.to_pandas(), name)
+            return self._col_series(name)
+        raise AttributeError(f"'LagFrame' object has no attribute {name!r}")
 
     # ------------------------------------------------------------------ device design
     def design(self):
         """engine.Design of this frame's values (every column numeric, no NaN cell), built from
-        the device sources: lag and base columns alike are (source, shift) pairs."""
+        the device sources: lag and base columns alike are (source, shift) pairs; a column
+        assigned to this frame (an overlay, e.g. the trial constants of
+        sglm_cb_concat_make_design_mat.py:275) becomes a device source row holding its values at
+        the frame's base rows (shift 0)."""
         if self._design is not None:
             return self._design
         from .engine import Design
-        if self._overlay:
+        if self._mat is not None:
+            # materialised (pandas code may have changed the values): the values as they are
+            self._design = Design.from_host(self.to_numpy(dtype=np.float64))
+            return self._design
+        pos = self.positions()
+        n = int(pos.size)
+        ov = [c for c in self._cols if c in self._overlay]
+        if ov and not self._inc and np.unique(pos).size != n:
+            # repeated base rows: an assigned column's values have no one base row each
             self._design = Design.from_host(self.to_numpy(dtype=np.float64))
             return self._design
         if self._any_nan():
             raise ValueError("Input X contains NaN.")
-        srcs = [self._spec[c][0] for c in self._cols]
+        srcs = [self._spec[c][0] for c in self._cols if c not in self._overlay]
         names = sorted(set(srcs), key=str)
         at = {nm: i for i, nm in enumerate(names)}
-        cols = np.array([at[x] for x in srcs], dtype=np.int64)
-        shifts = np.array([self._spec[c][1] for c in self._cols], dtype=np.int64)
-        pos = self.positions()
-        n = int(pos.size)
+        at.update({("__overlay__", c): len(names) + j for j, c in enumerate(ov)})
+        cols = np.array([at[("__overlay__", c)] if c in self._overlay else at[self._spec[c][0]]
+                         for c in self._cols], dtype=np.int64)
+        shifts = np.array([0 if c in self._overlay else self._spec[c][1] for c in self._cols],
+                          dtype=np.int64)
         sp = self._span()
         contiguous = n and (sp is not None or (pos[-1] - pos[0] == n - 1
                                                and np.all(np.diff(pos) == 1)))
-        if contiguous:
+        if contiguous and not ov:
             # every source 0/1 and the canonical lag layout: the design straight from the
             # uploaded bit rows (no float64 copy of the sources)
             B = self._src.bits(names)
@@ -690,16 +824,30 @@ class LagFrame:
                 if d is not None:
                     self._design = d
                     return d
-        E, idx = self._src.device(names)
-        Esub = E[idx]
-        if any(self._src.has_nan(nm) for nm in names):
-            Esub = Esub.nan_to_num(0.0)        # NaN source cells are never read (checked above)
+        import torch
+        if names:
+            E, idx = self._src.device(names)
+            Esub = E[idx]
+            if any(self._src.has_nan(nm) for nm in names):
+                Esub = Esub.nan_to_num(0.0)    # NaN source cells are never read (checked above)
+        else:
+            Esub = torch.zeros((0, self._src.N), dtype=torch.float64, device="cuda")
         ones = [self._src.ones(nm) for nm in names]
         ones = None if any(o is None for o in ones) else ones
+        if ov:
+            # assigned columns: device rows over the base rows, their values at this frame's
+            # rows (0 elsewhere: never read, and a 0/1 column stays 0/1)
+            vals = np.stack([pd.array(self._overlay[c]).to_numpy(dtype=np.float64,
+                                                                  na_value=np.nan)
+                             for c in ov])
+            Eov = torch.zeros((len(ov), self._src.N), dtype=torch.float64, device="cuda")
+            pos_d = torch.from_numpy(np.ascontiguousarray(pos, dtype=np.int64)).to("cuda")
+            Eov[:, pos_d] = torch.from_numpy(vals).to("cuda")
+            Esub = torch.cat([Esub, Eov])
+            ones = None
         if contiguous:
             d = Design.from_lagged(Esub, cols, shifts, int(pos[0]), n, ones=ones)
         else:
-            import torch
             rows_d = torch.from_numpy(np.ascontiguousarray(pos, dtype=np.int64)).to("cuda")
             d = Design.from_lagged(Esub, cols, shifts, 0, n, rows=rows_d)
         self._design = d
@@ -759,7 +907,7 @@ class _Loc:
                 return out[ck]
             return out.loc[:, ck]
         arr = key if isinstance(key, (pd.Series, np.ndarray, pd.Index)) else None
-        if arr is not None and arr.dtype == bool:
+        if arr is not None and pd.api.types.is_bool_dtype(arr.dtype):
             return f._bool_rows(key)
         if isinstance(key, slice):
             sl = f.index.slice_indexer(key.start, key.stop, key.step)

@@ -299,3 +299,62 @@ def ols_frame(N: int, m: int, neg: int, pos: int, seed: int = 0, rate=(0.005, 0.
     df.insert(0, "nTrial", trial)
     df["y"] = y
     return df, ev, beta, b0
+
+
+def cb_frame(N: int, m: int, neg: int, pos: int, sessions: int = 4, seed: int = 0,
+             rate=(0.005, 0.03), trial_len=(120, 360), nan_frac=0.02):
+    """A concatenated multi-session host frame in the layout sglm_cb_concat_make_design_mat.py
+    starts from (:219-244: ``load_sessions.read_in_multi_sessions`` output): ``nTrial``,
+    ``iBlock`` (trial-wide constants), ``session`` (a label per session), ``flag`` (1 on every row
+    of ~10 % of the trials: timeouts, dropped after the shifts, :268), m float64 0/1 event
+    columns ``e0 ..``, the two unshifted counters ``time_from_enl_onset`` /
+    ``time_from_enlp_onset`` (prod_counters) and a photometry response ``grn`` that is NaN on
+    short runs of rows (lost signal, dropped before the shifts, :251).  Over the rows that keep
+    their signal, ``grn`` = the lag design (shifts 0, neg..-1, 1..pos of the compacted rows,
+    sglm_ez.timeshift_cols' order) x coefficients + counters x gamma + a per-session offset
+    + noise.  Returns (DataFrame, event names, coefficient table [K][m], gamma, session offsets)."""
+    import pandas as pd
+    rng = np.random.default_rng(seed)
+    rates = np.linspace(rate[0], rate[1], m)
+    E = (rng.random((N, m)) < rates[None, :]).astype(np.float64)
+    lens = rng.integers(trial_len[0], trial_len[1] + 1, N // trial_len[0] + 2)
+    trial = np.repeat(np.arange(1, lens.size + 1), lens)[:N]
+    ntr = int(trial.max())
+    block = (trial - 1) // 20
+    sess_of_trial = np.minimum((np.arange(1, ntr + 1) - 1) * sessions // ntr, sessions - 1)
+    sess = sess_of_trial[trial - 1]
+    flag_tr = (rng.random(ntr + 1) < 0.1).astype(np.int64)
+    flag = flag_tr[trial]
+    cnt = prod_counters(trial, seed=seed + 1)
+    # lost-signal runs (NaN photometry), dropped before the shifts
+    keep = np.ones(N, dtype=bool)
+    nrun = max(1, int(N * nan_frac / 50))
+    for s0 in rng.integers(0, max(1, N - 50), nrun):
+        keep[s0:s0 + rng.integers(10, 50)] = False
+    rows = np.flatnonzero(keep)
+    Ek = E[rows]
+    n = rows.size
+    shifts = [0] + list(range(neg, 0)) + list(range(1, pos + 1))
+    beta = rng.normal(0, 0.3, (len(shifts), m))
+    gamma = np.array([0.8, -0.5])
+    offs = rng.normal(0.5, 0.3, sessions)
+    y = offs[sess[rows]] + gamma @ cnt[:, rows]
+    for bi, s in enumerate(shifts):
+        contrib = Ek @ beta[bi]
+        if s >= 0:
+            y[s:] += contrib[:n - s]
+        else:
+            y[:n + s] += contrib[-s:]
+    y += rng.normal(0, 1.0, n)
+    grn = np.full(N, np.nan)
+    grn[rows] = y
+    ev = [f"e{a}" for a in range(m)]
+    df = pd.DataFrame(E, columns=ev)
+    df.insert(0, "nTrial", trial.astype(np.int64))
+    df.insert(1, "iBlock", block.astype(np.int64))
+    df.insert(2, "session", np.array([f"2024-0{1 + q}-1{q}" for q in range(sessions)])[sess])
+    df.insert(3, "flag", flag)
+    df["time_from_enl_onset"] = cnt[0]
+    df["time_from_enlp_onset"] = cnt[1]
+    df["grn"] = grn
+    return df, ev, beta, gamma, offs

@@ -217,3 +217,54 @@ def test_lagframe_snapshot_and_uploads(engine):
     b = E.LagStructure.build(None, [0, 1, -1], 1, 2400, False, ebits=B, nnz=None, n_raw=2500)
     assert torch.equal(a.occ, b.occ) and torch.equal(a.tbeg, b.tbeg)
     assert torch.equal(a.tend, b.tend)
+
+
+def test_lagframe_is_a_dataframe(engine, tmp_path):
+    """The lagged frame passes isinstance(x, pd.DataFrame) (the reference's timeshift_multiple
+    returns one, backend/sglm_pp.py:485): the flow's operations stay lazy, and any other pandas
+    use -- pd.concat, set_index, to_parquet, get_dummies, insert, pickling -- sees exactly the
+    materialised DataFrame."""
+    import pickle
+    import sglm_ez
+    import sglm_pp
+    from sglm_hip.lagframe import LagFrame
+    df = _frame(seed=3)
+    cols = ["ev0", "ev1", "sig"]
+    lf = sglm_ez.timeshift_cols(df, cols, neg_order=-2, pos_order=2)
+    sglm_pp.LAGFRAME = False
+    try:
+        ref = sglm_ez.timeshift_cols(df, cols, neg_order=-2, pos_order=2)
+    finally:
+        sglm_pp.LAGFRAME = True
+    assert isinstance(lf, LagFrame) and isinstance(lf, pd.DataFrame) and lf.is_lazy
+    r1 = ref.dropna()
+    # the flow's operations keep it lazy
+    xcols = sglm_ez.add_timeshifts_to_col_list(cols, cols, neg_order=-2, pos_order=2)
+    k = lf[lf[["nTrial"] + xcols].isna().sum(axis=1) == 0]
+    k2 = k.loc[k["nTrial"] % 3 == 0, xcols]
+    k2["extra"] = 1.0
+    assert k.is_lazy and k2.is_lazy and lf.is_lazy
+    assert isinstance(k2, pd.DataFrame)
+    # pandas uses of the frame: the materialised values
+    f1 = lf.dropna()
+    pd.testing.assert_frame_equal(pd.concat([f1, r1.iloc[:5]]), pd.concat([r1, r1.iloc[:5]]))
+    assert not f1.is_lazy
+    pd.testing.assert_frame_equal(lf.dropna().set_index("nTrial"), r1.set_index("nTrial"))
+    fn = tmp_path / "f.parquet"
+    lf.dropna().to_parquet(fn)
+    pd.testing.assert_frame_equal(pd.read_parquet(fn), r1)
+    pd.testing.assert_frame_equal(pd.get_dummies(lf.dropna(), columns=["cnt"]),
+                                  pd.get_dummies(r1, columns=["cnt"]))
+    h = lf.dropna()
+    h.insert(0, "z", 2.0)
+    r = r1.copy()
+    r.insert(0, "z", 2.0)
+    pd.testing.assert_frame_equal(h, r)
+    assert list(h.columns) == list(r.columns) and h.shape == r.shape
+    pd.testing.assert_series_equal(h["z"], r["z"])
+    q = pickle.loads(pickle.dumps(lf.dropna()))
+    assert type(q) is pd.DataFrame
+    pd.testing.assert_frame_equal(q, r1)
+    # arithmetic and reductions as pandas gives them
+    pd.testing.assert_series_equal(lf.dropna().sum(), r1.sum())
+    pd.testing.assert_frame_equal(lf.dropna() * 2, r1 * 2)

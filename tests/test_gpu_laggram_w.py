@@ -63,6 +63,8 @@ def _lag(engine, torch, d, W, fits):
     (40, list(range(0, 12)), 11, True, 2),              # two halves, event-major
     (20, list(range(3, -4, -1)), 7, False, 14),         # descending shifts, two column groups
     (50, list(range(-20, 20)), 20, False, 5),           # the C4 layout, 200 columns
+    (30, list(range(-8, 8)), 8, False, 17),             # 272 columns: three column blocks
+    (45, list(range(5, -5, -1)), 9, True, 1),           # event-major, descending, one fit
 ])
 def test_lag_gram_w_matches_dense(engine, torch_mod, m, shifts, row0, event_major, nf):
     torch = torch_mod
@@ -139,3 +141,27 @@ def test_lag_gram_w_in_grid_matches_dense_path(engine, torch_mod, monkeypatch):
         assert np.allclose(a["refit_coef"], b["refit_coef"], rtol=1e-4, atol=1e-6)
         assert np.allclose(a["cv_coefs"], b["cv_coefs"], rtol=1e-4, atol=1e-6)
         assert abs(a["cv_mean_score"] - b["cv_mean_score"]) <= 1e-6 * max(1, abs(b["cv_mean_score"]))
+
+
+def test_lag_gram_w_scratch_budget_chunks_fits(engine, torch_mod, monkeypatch):
+    """The launch's scratch (8 bf16 weight copies per fit) is bounded: with a budget of two
+    fits the seven fits run as four launches and give bitwise the same Hessians."""
+    from types import SimpleNamespace
+    torch = torch_mod
+    rng = np.random.default_rng(7)
+    E = _events(rng, 5000, 20, 0.04)
+    d = engine.Design.from_events(E, list(range(-6, 6)), 6, 4988)
+    lg = engine._lagw(d)
+    fits = np.array([0, 2, 3, 5, 6, 8, 9], dtype=np.int32)
+    W = torch.rand((10, d.ld), device="cuda")
+    out = []
+    for budget in (float(1 << 40), 2.5 * engine._lib.query("sglm_lag_gram_w_work_bytes",
+                                                             lg.n_raw, lg.K, 1)):
+        monkeypatch.setattr(engine, "LAGW_WORK_BUDGET", budget)
+        bf = SimpleNamespace(W=W, H=torch.zeros((10, d.P, d.P), device="cuda"))
+        engine._lag_gram_w(d, lg, bf, fits, 0)
+        torch.cuda.synchronize()
+        out.append(bf.H.cpu().numpy())
+    blk = np.triu(np.ones((d.P, d.P), dtype=bool))
+    for k in fits:
+        assert np.array_equal(out[0][k][blk], out[1][k][blk]), k

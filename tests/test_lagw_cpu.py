@@ -17,8 +17,13 @@ def test_exec_flop_covers_the_algorithmic_products():
         prev = 0.0
         for nact in (1, 2, 5, 14):
             ex = E._lagw_exec_flop(lg, nact)
-            alg = 2.0 * sum(int(c) * ((m - a) * K + 1) for a, c in enumerate(lg.cnt)) * K * nact
-            assert ex >= 0.5 * alg, (m, K, nact, ex, alg)     # both count each H entry once
+            alg = E._lagw_alg_flop1(m, K, lg.cnt) * nact
+            assert ex >= alg, (m, K, nact, ex, alg)   # the kernel's own decomposition, padded
+            # every H entry of the upper triangle once: (mK(mK+1)/2 + mK) entries, each summing
+            # the occurrences of one of its two events (equal counts: exactly that many terms)
+            flat = E._lagw_alg_flop1(m, K, np.full(m, 7))
+            pl = m * K
+            assert flat == 2.0 * 7 * (pl * (pl + 1) // 2 + pl)
             assert ex >= prev                                    # 32-column tiles: flat inside one
             prev = ex
         assert E._lagw_exec_flop(lg, 5) == lg.exec_flop[5]    # memoised per launch size

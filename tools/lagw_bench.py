@@ -16,9 +16,11 @@ for nf in (1, 5):
     W = torch.rand((nf, d.ld), device="cuda")
     H = torch.zeros((nf, d.P, d.P), device="cuda")
     wk = torch.empty(_lib.query("sglm_lag_gram_w_work_bytes", lg.n_raw, lg.K, nf), dtype=torch.uint8, device="cuda")
-    for pr in (0,):
+    probes = [int(x) for x in os.environ.get("LAGW_PROBES", "0").split(",")]
+    for pr in probes:
+        os.environ["SGLM_LAGW_PROBE"] = str(pr)
         ts = []
-        for rep in range(4):
+        for rep in range(int(os.environ.get('LAGW_REPS', '4'))):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             _lib.call("sglm_lag_gram_w", lg.R.data_ptr(), lg.occ.data_ptr(), lg.ev_off.data_ptr(), lg.m,
