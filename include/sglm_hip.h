@@ -194,20 +194,24 @@ int sglm_syrk_cbits(const int64_t* desc, int32_t P, const int32_t* fits, int32_t
 /* Weighted Gram of a time-shifted 0/1 event design from its events (lagw.hip): for each
  * fits[f], H[fits[f]] = X^T diag(bf16(W[fits[f]])) X with X[t][col(b, a)] =
  * e_a(t + row0 - shifts[b]) and the ones column pones (K m, or past a mixed design's continuous
- * columns K m .. pones - 1, whose rows / columns are left to sglm_mixed_to_h), written on the
- * upper triangle (row <= col; the padding columns > pones zeroed).  col(b, a) = layout ?
- * a K + b : b m + a.
+ * columns K m .. pones - 1, whose rows / columns are zeroed here and left to sglm_mixed_to_h),
+ * written on the upper triangle (row <= col; the padding columns > pones zeroed; the lower
+ * triangle is scratch: the kernel writes each entry at the row of its column with the larger
+ * shift and a symmetrize pass builds the upper triangle).  col(b, a) = layout ? a K + b : b m + a.
  * R: sglm_lag_rowwords of the events; occ / ev_off: every event's occurrence rows, event-major,
- * ascending, and the event segments (m + 1); bidx[s - smin] = b of shift s (-1 if absent).
+ * ascending, and the event segments (m + 1); shifts[b] = the shift of block b, which must be
+ * exactly the values smin .. smax (K = smax - smin + 1 distinct shifts, in any order), and
+ * bidx[s - smin] = b of shift s -- its inverse permutation (the caller builds both; an entry
+ * < 0 of bidx is skipped, never written through).
  * Replaces the dense Gram's n p^2 products by about nnz(E) (m + 1) K^2 per fit (each event's
- * occurrences x every event at the shift differences d >= 0 x the shifts).
- * The shift set must be a contiguous range (in any order). */
+ * occurrences x every event at the shift differences d >= 0 x the shifts). */
 int sglm_lag_gram_w(const uint64_t* R, const int32_t* occ, const int32_t* ev_off, int32_t m,
                     int32_t nraw, const int32_t* shifts, const int32_t* bidx, int32_t K,
                     int32_t smin, int32_t smax, int32_t layout, int32_t row0, int32_t n,
                     const float* W, int64_t ld, const int32_t* fits, int32_t nf, float* H,
                     int32_t P, int32_t pones, void* work, sglm_stream_t stream);
-/* work bytes of sglm_lag_gram_w (8 shifted bf16 copies of the launch's weights) */
+/* work bytes of sglm_lag_gram_w: 8 shifted bf16 copies of the launch's weights over every raw
+ * row (~16 B per raw row per fit -- the engine splits large launches to bound it) */
 size_t sglm_lag_gram_w_work_bytes(int32_t nraw, int32_t K, int32_t nf);
 
 /* Row words of m <= 63 events: R[u] bit a = e_a(u) (ebits[m][nwords], bit u & 31 of word

@@ -464,10 +464,9 @@ lag_gram_w2_kernel(LagW2Args a) {
     // has nothing to store
     if (n0 / a.nf >= a.K || min(a.K - 1, (n0 + NN - 1) / a.nf) < di0) return;
     const int o_beg = a.ev_off[a1], o_end = a.ev_off[a1 + 1];
-    // stages, rounded up to even (the loop body is two stages; a stage past the event's end
-    // reads the zero row and adds nothing): every load of the pipeline is unconditional, so the
-    // compiler's wait counts stay exact
-    const int nst = (o_end - o_beg + 2 * kKS2 - 1) / (2 * kKS2) * 2;
+    // every load of the pipeline is unconditional (a stage past the event's end reads the zero
+    // row), so the compiler's wait counts stay exact
+    const int nst = (o_end - o_beg + kKS2 - 1) / kKS2;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r = lane & 31;
     const int wm = wave % WM, wn = wave / WM;
 
@@ -484,19 +483,22 @@ lag_gram_w2_kernel(LagW2Args a) {
     // Every load below is unconditional, from a clamped address, and what is invalid is masked
     // when the registers are stored (a load whose result is selected against a constant makes
     // hipcc wait for it right away, which would serialise the staging pipeline)
-    uint4 wA[kWT], wB[kWT];
-    uint64_t rA[kRT][2], rB[kRT][2];
-    uint32_t vA = 0, vB = 0;                  // validity of the row-word loads, bit 2 i + j
+    // one register set: a stage is stored to LDS right after the barrier, then the registers
+    // receive the stage after next (clang vectors: arrays of HIP's uint4 struct stay allocas)
+    u32x4 wA[kWT];
+    uint64_t rA[kRT][2];
+    uint32_t vA = 0;                          // validity of the row-word loads, bit 2 i + j
     int32_t oreg = 0;
     bool ovalid = false;
 
-    auto occ_load = [&](int s) {
+    auto occ_load = [&](int s) __attribute__((always_inline)) {
         const int o = o_beg + s * kKS2 + tid;
         ovalid = tid < kKS2 && o < o_end;
         oreg = a.occ[ovalid ? o : o_beg];
     };
-    auto occ_store = [&](int s) { sm.occ[s & 3][tid] = ovalid ? oreg : -1; };
-    auto data_load = [&](int s, uint4 (&wreg)[kWT], uint64_t (&rreg)[kRT][2], uint32_t& vreg) {
+    auto occ_store = [&](int s) __attribute__((always_inline)) { sm.occ[s & 3][tid] = ovalid ? oreg : -1; };
+    auto data_load = [&](int s, u32x4 (&wreg)[kWT], uint64_t (&rreg)[kRT][2], uint32_t& vreg)
+        __attribute__((always_inline)) {
         const int* ov = sm.occ[s & 3];
 #pragma unroll
         for (int i = 0; i < kWT; ++i) {
@@ -506,7 +508,7 @@ lag_gram_w2_kernel(LagW2Args a) {
             const int64_t u = v >= 0 ? v : a.zrow;          // past the event's end: zero weights
             const int64_t x = u * a.nf + n0 + 8 * ch;
             const int c = (int)(x & 7);
-            wreg[i] = *reinterpret_cast<const uint4*>(a.Wt + c * a.wlen + (x - c));
+            wreg[i] = *reinterpret_cast<const u32x4*>(a.Wt + c * a.wlen + (x - c));
         }
         uint32_t vb = 0;
 #pragma unroll
@@ -522,13 +524,13 @@ lag_gram_w2_kernel(LagW2Args a) {
         }
         vreg = vb;
     };
-    auto data_store = [&](int buf, const uint4 (&wreg)[kWT], const uint64_t (&rreg)[kRT][2],
-                          uint32_t vreg) {
+    auto data_store = [&](int buf, const u32x4 (&wreg)[kWT], const uint64_t (&rreg)[kRT][2],
+                          uint32_t vreg) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < kWT; ++i) {
             const int t = tid + NTH * i;
             const int k = t / NCH, ch = t % NCH;
-            *reinterpret_cast<uint4*>(&sm.ws[buf][k * NN + 8 * (ch ^ lagw_swz<NCH>(k))]) = wreg[i];
+            *reinterpret_cast<u32x4*>(&sm.ws[buf][k * NN + 8 * (ch ^ lagw_swz<NCH>(k))]) = wreg[i];
         }
 #pragma unroll
         for (int i = 0; i < kRT; ++i) {
@@ -592,7 +594,7 @@ lag_gram_w2_kernel(LagW2Args a) {
     const uint32_t rsh = (uint32_t)(r - 14 - 16 * (r >> 4)) & 31u;   // bit r (mod 16) -> 14
 
     // the multiplication of one staged stage over the live N tiles J0 .. J1
-    auto compute = [&](int buf, auto J0c, auto J1c) {
+    auto compute = [&](int buf, auto J0c, auto J1c) __attribute__((always_inline)) {
         constexpr int J0 = decltype(J0c)::value, J1 = decltype(J1c)::value;
         const uint32_t* rwb = &sm.rw[buf][0];
         const char* wsb = reinterpret_cast<const char*>(&sm.ws[buf][0]);
@@ -627,18 +629,10 @@ lag_gram_w2_kernel(LagW2Args a) {
                                                                         0, 0, 0);
         }
     };
-    // stage s: the occurrence rows of stage s + 4 and the data of stage s + 2 are loaded, stage s
-    // is multiplied, and stage s + 1 (loaded during stage s - 1) is stored to the other buffer
-    auto main_loop = [&](auto J0c, auto J1c) {
-        auto step = [&](int s, uint4 (&wc)[kWT], uint64_t (&rc)[kRT][2], uint32_t& vc,
-                        uint4 (&wn_)[kWT], uint64_t (&rn)[kRT][2], uint32_t& vn) {
-            occ_store(s + 3);
-            __syncthreads();
-            occ_load(s + 4);
-            data_load(s + 2, wn_, rn, vn);       // past the end: zero rows, never stored
-            compute(s & 1, J0c, J1c);
-            if (s + 1 < nst) data_store((s + 1) & 1, wc, rc, vc);
-        };
+    // stage s: stage s + 1 (loaded during stage s - 1) is stored to the other buffer, the
+    // occurrence rows of stage s + 4 and the data of stage s + 2 are loaded, stage s is
+    // multiplied (its loads overlap it)
+    auto main_loop = [&](auto J0c, auto J1c) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
             occ_load(j);
@@ -649,9 +643,13 @@ lag_gram_w2_kernel(LagW2Args a) {
         data_store(0, wA, rA, vA);
         occ_load(3);
         data_load(1, wA, rA, vA);
-        for (int s = 0; s < nst; s += 2) {
-            step(s, wA, rA, vA, wB, rB, vB);
-            step(s + 1, wB, rB, vB, wA, rA, vA);
+        for (int s = 0; s < nst; ++s) {
+            occ_store(s + 3);
+            __syncthreads();
+            if (s + 1 < nst) data_store((s + 1) & 1, wA, rA, vA);
+            occ_load(s + 4);
+            data_load(s + 2, wA, rA, vA);    // past the end: the zero row, never stored
+            compute(s & 1, J0c, J1c);
         }
     };
     using I0 = std::integral_constant<int, 0>;
