@@ -25,6 +25,7 @@
 // operand is expanded from the staged words (bf16 2.0 / 0, the factor 2 removed at the store),
 // the B operand is one ds_read_b128 per N tile; (d, shift-tile) pairs that form no H entry are
 // skipped.
+#include <algorithm>
 #include <type_traits>
 
 #include "common.h"
@@ -421,6 +422,11 @@ struct LagW2Args {
     const int32_t* fits;
     float* H;
     int32_t nf, P, p, m, K, smin, smax, layout, nraw, nh, D, Gm, Gy, Q, npieces, zrow;
+    // piece order: ntypes > 0 -> block b runs piece type types[b / m] (types in decreasing
+    // order of work) of event b % m (longest pieces first: the last round holds the lightest);
+    // ntypes == 0 -> XCD x = b mod 8 takes the pieces [x Q, x Q + Q), event-major
+    int32_t ntypes;
+    uint8_t types[128];             // type = g + Gm y
 };
 
 template <int NCH>
@@ -436,8 +442,8 @@ struct LagW2Smem {
     int32_t occ[4][64 * WM * WN];          // every thread stores (rows kKS2 .. : unread)
 };
 
-template <int MT, int NT, int WM, int WN>
-__global__ void __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(2, 2)))
+template <int MT, int NT, int WM, int WN, int WPS>
+__global__ void __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(WPS, WPS)))
 lag_gram_w2_kernel(LagW2Args a) {
     using SM = LagW2Smem<MT, NT, WM, WN>;
     constexpr int NTH = 64 * WM * WN, MB = SM::MB, NN = SM::NN, NCH = NN / 8;
@@ -447,10 +453,19 @@ lag_gram_w2_kernel(LagW2Args a) {
     __shared__ SM sm;
     // piece of this workgroup: XCD x = b mod 8 takes pieces [x Q, x Q + Q), event-major, the
     // d groups of one column block adjacent (they stream the same weights)
-    const int pc = (int)(blockIdx.x & 7) * a.Q + (int)(blockIdx.x >> 3);
-    if (pc >= a.npieces) return;
-    const int per = a.Gm * a.Gy;
-    const int a1 = pc / per, rem = pc % per;
+    int a1, rem;
+    if (a.ntypes > 0) {
+        const int b = blockIdx.x;
+        if (b >= a.ntypes * a.m) return;
+        a1 = b % a.m;
+        rem = a.types[b / a.m];
+    } else {
+        const int pc = (int)(blockIdx.x & 7) * a.Q + (int)(blockIdx.x >> 3);
+        if (pc >= a.npieces) return;
+        const int per = a.Gm * a.Gy;
+        a1 = pc / per;
+        rem = pc % per;
+    }
     const int g = rem % a.Gm, y = rem / a.Gm;
     const int nh = a.nh, Tm = a.D * nh;
     const int t0 = g * MB;
@@ -497,19 +512,20 @@ lag_gram_w2_kernel(LagW2Args a) {
         oreg = a.occ[ovalid ? o : o_beg];
     };
     auto occ_store = [&](int s) __attribute__((always_inline)) { sm.occ[s & 3][tid] = ovalid ? oreg : -1; };
-    auto data_load = [&](int s, u32x4 (&wreg)[kWT], uint64_t (&rreg)[kRT][2], uint32_t& vreg)
-        __attribute__((always_inline)) {
+    // staging pieces: weight chunk task i, and all row-word tasks (loads of stage s into the
+    // registers; stores of the registers to buffer buf)
+    auto load_w = [&](int s, int i) __attribute__((always_inline)) {
         const int* ov = sm.occ[s & 3];
-#pragma unroll
-        for (int i = 0; i < kWT; ++i) {
-            const int t = tid + NTH * i;
-            const int k = t / NCH, ch = t % NCH;
-            const int v = ov[k];
-            const int64_t u = v >= 0 ? v : a.zrow;          // past the event's end: zero weights
-            const int64_t x = u * a.nf + n0 + 8 * ch;
-            const int c = (int)(x & 7);
-            wreg[i] = *reinterpret_cast<const u32x4*>(a.Wt + c * a.wlen + (x - c));
-        }
+        const int t = tid + NTH * i;
+        const int k = t / NCH, ch = t % NCH;
+        const int v = ov[k];
+        const int64_t u = v >= 0 ? v : a.zrow;              // past the event's end: zero weights
+        const int64_t x = u * a.nf + n0 + 8 * ch;
+        const int c = (int)(x & 7);
+        wA[i] = *reinterpret_cast<const u32x4*>(a.Wt + c * a.wlen + (x - c));
+    };
+    auto load_r = [&](int s) __attribute__((always_inline)) {
+        const int* ov = sm.occ[s & 3];
         uint32_t vb = 0;
 #pragma unroll
         for (int i = 0; i < kRT; ++i) {
@@ -519,25 +535,23 @@ lag_gram_w2_kernel(LagW2Args a) {
                 const int u = v + di0 + rdl[i];
                 const bool ok = rkp[i] >= 0 && v >= 0 && u < a.nraw;
                 vb |= (uint32_t)ok << (2 * i + j);
-                rreg[i][j] = a.R[ok ? u : 0];
+                rA[i][j] = a.R[ok ? u : 0];
             }
         }
-        vreg = vb;
+        vA = vb;
     };
-    auto data_store = [&](int buf, const u32x4 (&wreg)[kWT], const uint64_t (&rreg)[kRT][2],
-                          uint32_t vreg) __attribute__((always_inline)) {
-#pragma unroll
-        for (int i = 0; i < kWT; ++i) {
-            const int t = tid + NTH * i;
-            const int k = t / NCH, ch = t % NCH;
-            *reinterpret_cast<u32x4*>(&sm.ws[buf][k * NN + 8 * (ch ^ lagw_swz<NCH>(k))]) = wreg[i];
-        }
+    auto store_w = [&](int buf, int i) __attribute__((always_inline)) {
+        const int t = tid + NTH * i;
+        const int k = t / NCH, ch = t % NCH;
+        *reinterpret_cast<u32x4*>(&sm.ws[buf][k * NN + 8 * (ch ^ lagw_swz<NCH>(k))]) = wA[i];
+    };
+    auto store_r = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < kRT; ++i) {
-            if (rkp[i] < 0) continue;
-            uint32_t* dst = &sm.rw[buf][rdl[i] * kRS2 + rkp[i]];
-            const uint64_t r0 = ((vreg >> (2 * i)) & 1u) ? rreg[i][0] : 0ull;
-            const uint64_t r1 = ((vreg >> (2 * i + 1)) & 1u) ? rreg[i][1] : 0ull;
+            // a thread without a task writes a pad dword (kp 64 of d row 0: never read)
+            uint32_t* dst = &sm.rw[buf][rkp[i] >= 0 ? rdl[i] * kRS2 + rkp[i] : kKP2];
+            const uint64_t r0 = ((vA >> (2 * i)) & 1u) ? rA[i][0] : 0ull;
+            const uint64_t r1 = ((vA >> (2 * i + 1)) & 1u) ? rA[i][1] : 0ull;
 #pragma unroll
             for (int pl = 0; pl < 2; ++pl) {
                 const uint32_t w0 = (uint32_t)(r0 >> (32 * pl));
@@ -546,6 +560,16 @@ lag_gram_w2_kernel(LagW2Args a) {
                 dst[(2 * pl + 1) * kRX2] = (w0 >> 16) | (w1 & 0xffff0000u);
             }
         }
+    };
+    auto data_load = [&](int s) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < kWT; ++i) load_w(s, i);
+        load_r(s);
+    };
+    auto data_store = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < kWT; ++i) store_w(buf, i);
+        store_r(buf);
     };
 
     f32x16 acc[MT][NT];
@@ -593,13 +617,70 @@ lag_gram_w2_kernel(LagW2Args a) {
     }
     const uint32_t rsh = (uint32_t)(r - 14 - 16 * (r >> 4)) & 31u;   // bit r (mod 16) -> 14
 
-    // the multiplication of one staged stage over the live N tiles J0 .. J1
-    auto compute = [&](int buf, auto J0c, auto J1c) __attribute__((always_inline)) {
+    // the multiplication of stage s (buffer s & 1) over the live N tiles J0 .. J1; with two
+    // waves per SIMD the staging of the next stages rides inside its K-steps: stage s + 1 is
+    // stored to the other buffer over the first K-steps (one piece behind each K-step's
+    // MFMAs) and stage s + 2 is loaded into the freed registers over the last ones, so the
+    // LDS writes and the address work of the staging overlap the MFMAs instead of following
+    // the barrier in lockstep on both waves of a SIMD
+    auto compute = [&](int s, auto J0c, auto J1c) __attribute__((always_inline)) {
         constexpr int J0 = decltype(J0c)::value, J1 = decltype(J1c)::value;
+        const int buf = s & 1;
         const uint32_t* rwb = &sm.rw[buf][0];
         const char* wsb = reinterpret_cast<const char*>(&sm.ws[buf][0]);
-#pragma unroll 2
+        if constexpr (WPS == 1) {
+            // one wave per SIMD: nothing else hides the LDS latency, so the fragments of K-step
+            // ks + 1 are read (two register sets) while the MFMAs of ks run
+            u32x4 wq[2][MT];
+            s16x4 t1[2][NT], t2[2][NT];
+            auto fetch = [&](int ks, int st) __attribute__((always_inline)) {
+#pragma unroll
+                for (int j = J0; j <= J1; ++j) {
+                    const char* pb = wsb + boff[j] + ks * 16 * NN * 2;
+                    t1[st][j] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (lds_s16x4*)(__attribute__((address_space(3))) char*)pb);
+                    t2[st][j] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (lds_s16x4*)(__attribute__((address_space(3))) char*)(pb + 4 * NN * 2));
+                }
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+                    wq[st][i] = *reinterpret_cast<const u32x4*>(rwb + aoff[i] + 8 * ks);
+            };
+            fetch(0, 0);
+#pragma unroll
+            for (int ks = 0; ks < kKS2 / 16; ++ks) {
+                const int st = ks & 1;
+                if (ks + 1 < kKS2 / 16) fetch(ks + 1, st ^ 1);
+                bf16x8 bq[NT];
+#pragma unroll
+                for (int j = J0; j <= J1; ++j) {
+                    const uint2 u1 = __builtin_bit_cast(uint2, t1[st][j]);
+                    const uint2 u2 = __builtin_bit_cast(uint2, t2[st][j]);
+                    bq[j] = __builtin_bit_cast(bf16x8, make_uint4(u1.x, u1.y, u2.x, u2.y));
+                }
+#pragma unroll
+                for (int i = 0; i < MT; ++i) {
+                    uint32_t dq[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) dq[q] = rotr32(wq[st][i][q], rsh) & 0x40004000u;
+                    const bf16x8 aq =
+                        __builtin_bit_cast(bf16x8, make_uint4(dq[0], dq[1], dq[2], dq[3]));
+#pragma unroll
+                    for (int j = J0; j <= J1; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq, bq[j], acc[i][j],
+                                                                            0, 0, 0);
+                }
+            }
+            return;
+        }
+        static_assert(WPS == 1 || kWT <= 4, "staging pieces per K-step");
+#pragma unroll
         for (int ks = 0; ks < kKS2 / 16; ++ks) {
+            if (ks < kWT) store_w(buf ^ 1, ks);
+            if (ks == kWT) store_r(buf ^ 1);
+            if (ks == 4) occ_load(s + 4);
+            if (ks >= 4 && ks - 4 < kWT) load_w(s + 2, ks - 4);
+            if (ks == 7) load_r(s + 2);
             bf16x8 bq[NT];
 #pragma unroll
             for (int j = J0; j <= J1; ++j) {
@@ -639,17 +720,19 @@ lag_gram_w2_kernel(LagW2Args a) {
             occ_store(j);
         }
         __syncthreads();
-        data_load(0, wA, rA, vA);
-        data_store(0, wA, rA, vA);
+        data_load(0);
+        data_store(0);
         occ_load(3);
-        data_load(1, wA, rA, vA);
+        data_load(1);
         for (int s = 0; s < nst; ++s) {
             occ_store(s + 3);
             __syncthreads();
-            if (s + 1 < nst) data_store((s + 1) & 1, wA, rA, vA);
-            occ_load(s + 4);
-            data_load(s + 2, wA, rA, vA);    // past the end: the zero row, never stored
-            compute(s & 1, J0c, J1c);
+            if constexpr (WPS == 1) {
+                data_store((s + 1) & 1);     // past the end: zero rows, never read
+                occ_load(s + 4);
+                data_load(s + 2);
+            }
+            compute(s, J0c, J1c);            // WPS 2: stores s + 1, loads s + 2 inside
         }
     };
     using I0 = std::integral_constant<int, 0>;
@@ -772,7 +855,7 @@ __global__ void __launch_bounds__(256) lag_gram_w_sym(float* __restrict__ H,
     }
 }
 
-template <int MT, int NT, int WM, int WN>
+template <int MT, int NT, int WM, int WN, int WPS>
 int launch_lagw2(const LagW2Args& a0, hipStream_t s) {
     LagW2Args a = a0;
     constexpr int MB = WM * MT, NN = WN * NT * 32;
@@ -780,7 +863,48 @@ int launch_lagw2(const LagW2Args& a0, hipStream_t s) {
     a.Gy = (a.nf * a.K + NN - 1) / NN;
     a.npieces = a.m * a.Gm * a.Gy;
     a.Q = (a.npieces + 7) / 8;
-    lag_gram_w2_kernel<MT, NT, WM, WN><<<dim3((unsigned)(8 * a.Q)), 64 * WM * WN, 0, s>>>(a);
+    a.ntypes = 0;
+    // longest pieces first (default; measured 0.634 -> 0.600 ms per launch on the C4 grid
+    // against the XCD-local ranges: the last round of workgroups then holds the lightest pieces,
+    // which outweighs the L2 sharing of one event's pieces); SGLM_LAGW_ORDER=0: XCD ranges
+    static const int lpt = [] {
+        const char* e = getenv("SGLM_LAGW_ORDER");
+        return e ? atoi(e) : 1;
+    }();
+    const int per = a.Gm * a.Gy;
+    if (lpt && per <= 128) {
+        // work of a piece type: its live (M tile, N tile) MFMA pairs per K-step plus the
+        // staging every piece does (about a quarter of a full piece's MFMA time)
+        int cost[128];
+        for (int t = 0; t < per; ++t) {
+            const int g = t % a.Gm, y = t / a.Gm;
+            const int t0 = g * MB, Tm = a.D * a.nh;
+            int live = 0;
+            for (int tau = t0; tau < t0 + MB && tau < Tm; ++tau) {
+                const int d = tau / a.nh;
+                for (int j = 0; j < NN / 32; ++j) {
+                    const int c0 = y * NN + 32 * j;
+                    const int sb_lo = c0 / a.nf, sb_hi = std::min(a.K - 1, (c0 + 31) / a.nf);
+                    if (sb_lo < a.K && sb_hi >= d) ++live;
+                }
+            }
+            const int n0 = y * NN, di0 = t0 / a.nh;
+            const bool dead = t0 >= Tm || n0 / a.nf >= a.K ||
+                              std::min(a.K - 1, (n0 + NN - 1) / a.nf) < di0;
+            cost[t] = dead ? -1 : live + MB * (NN / 32) / 4;
+        }
+        int nt = 0;
+        for (int t = 0; t < per; ++t)
+            if (cost[t] >= 0) a.types[nt++] = (uint8_t)t;
+        std::stable_sort(a.types, a.types + nt,
+                         [&](uint8_t x, uint8_t y) { return cost[x] > cost[y]; });
+        a.ntypes = nt;
+        if (nt == 0) return SGLM_OK;
+        lag_gram_w2_kernel<MT, NT, WM, WN, WPS><<<dim3((unsigned)(nt * a.m)), 64 * WM * WN, 0,
+                                                  s>>>(a);
+        return check_launch("lag_gram_w2_kernel");
+    }
+    lag_gram_w2_kernel<MT, NT, WM, WN, WPS><<<dim3((unsigned)(8 * a.Q)), 64 * WM * WN, 0, s>>>(a);
     return check_launch("lag_gram_w2_kernel");
 }
 
@@ -849,7 +973,14 @@ extern "C" int sglm_lag_gram_w(const uint64_t* R, const int32_t* occ, const int3
     b.fits = fits; b.H = H; b.nf = nf; b.P = P; b.p = p; b.m = m; b.K = K; b.smin = smin;
     b.smax = smax; b.layout = layout; b.nraw = nraw; b.nh = a.nh; b.D = K;
     b.zrow = (int32_t)lagw_zrow(nraw, K);
-    const int st = (nf * K <= 64) ? launch_lagw2<2, 2, 8, 1>(b, s) : launch_lagw2<2, 4, 8, 1>(b, s);
+    static const int wps1 = [] {
+        const char* e = getenv("SGLM_LAGW_WPS1");
+        return e ? atoi(e) : 0;
+    }();
+    const int st = wps1 ? ((nf * K <= 64) ? launch_lagw2<4, 2, 4, 1, 1>(b, s)
+                                          : launch_lagw2<4, 4, 4, 1, 1>(b, s))
+                        : ((nf * K <= 64) ? launch_lagw2<2, 2, 8, 1, 2>(b, s)
+                                          : launch_lagw2<2, 4, 8, 1, 2>(b, s));
     if (st) return st;
     const int T = P / 64;
     lag_gram_w_sym<<<dim3((unsigned)(T * (T + 1) / 2), (unsigned)nf), 256, 0, s>>>(
