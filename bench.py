@@ -1122,7 +1122,7 @@ def main():
         grid_s = elapsed / a.steps
         achieved = kflop / ktime / 1e12 if ktime > 0 else 0.0
         # the Gram kernel that ran: the event-structured one when the design keeps its events
-        gram_kernel = "lag_gram_w_kernel" if E._lagw(design) is not None else "syrk6_kernel"
+        gram_kernel = "lag_gram_w2_kernel" if E._lagw(design) is not None else "syrk6_kernel"
         traffic, traffic_src = pmc_traffic(gram_kernel)
         conv = all(r["converged"] for r in res)
         ndist = None
