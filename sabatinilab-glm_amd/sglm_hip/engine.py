@@ -3149,6 +3149,22 @@ def _lagw(d: Design):
         # a2 >= a1 and the ones column, K columns each; at d > 0 every event a2 and the K - d
         # shifts s_b1 whose s_b1 - d is a column.  The launch also forms the G entries whose
         # second shift is no column and pads rows and columns to 32 (_lagw_exec_flop >= this)
+        # the occurrences the launch iterates: those whose window of design rows
+        # [v - row0 + smin, v - row0 + smax] meets [0, n) -- every occurrence for a whole design,
+        # a row slab's own share for one rank of a row-sharded solve (the others only ever meet
+        # zero weights)
+        lo, hi = lg.row0 - lg.smax, lg.row0 + lg.n - 1 - lg.smin
+        lg.w_occ, lg.w_ev_off = lg.occ, lg.ev_off
+        if lo > 0 or hi < lg.n_raw - 1:
+            keep = (lg.occ >= lo) & (lg.occ <= hi)
+            evi = torch.repeat_interleave(
+                torch.arange(lg.m, device=lg.occ.device),
+                torch.from_numpy(cnt).to(lg.occ.device))
+            lg.w_occ = lg.occ[keep].contiguous()
+            wc = torch.bincount(evi[keep], minlength=lg.m)
+            lg.w_ev_off = torch.cat([torch.zeros(1, dtype=torch.int64, device=lg.occ.device),
+                                     torch.cumsum(wc, 0)]).to(torch.int32).contiguous()
+            cnt = wc.cpu().numpy().astype(np.int64)
         lg.flop1 = _lagw_alg_flop1(lg.m, lg.K, cnt)
         lg.cnt = cnt
         lg.R = R
@@ -3183,7 +3199,7 @@ def _lag_gram_w(d: Design, lg, bf, fits: np.ndarray, st, ev=None):
             ev[0].record()
         for c0 in range(0, nact, chunk):
             nc = min(chunk, nact - c0)
-            _lib.call("sglm_lag_gram_w", _p(lg.R), _p(lg.occ), _p(lg.ev_off), lg.m, lg.n_raw,
+            _lib.call("sglm_lag_gram_w", _p(lg.R), _p(lg.w_occ), _p(lg.w_ev_off), lg.m, lg.n_raw,
                       _p(lg.shifts), _p(lg.bidx), lg.K, lg.smin, lg.smax, lg.layout, lg.row0,
                       lg.n, _p(bf.W), d.ld, _p(fits_d[c0:c0 + nc]), nc, _p(bf.H), d.P, d.p,
                       _p(work), st)

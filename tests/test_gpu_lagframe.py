@@ -268,3 +268,46 @@ def test_lagframe_is_a_dataframe(engine, tmp_path):
     # arithmetic and reductions as pandas gives them
     pd.testing.assert_series_equal(lf.dropna().sum(), r1.sum())
     pd.testing.assert_frame_equal(lf.dropna() * 2, r1 * 2)
+
+
+def test_lagframe_lag_block_with_extra_columns(engine):
+    """A contiguous lagged frame whose columns are the canonical lag block followed by unshifted
+    extra columns -- the production design's counters, an assigned (overlay) column and a 0/1
+    dummy (sglm_cb_concat_make_design_mat.py:286, 310) -- builds its design from the events
+    (LagStructure: structured Gram and correlation start) with the extras as the float64 block
+    of a mixed design, never from a host copy; its fits equal the host-packed design's."""
+    import sglm_ez
+    from sglm_hip import engine as E
+    rng = np.random.default_rng(5)
+    df = _frame(N=6000, nan_rows=())
+    df["cnt2"] = (rng.integers(0, 40, len(df)) ** 2) / 5000.0    # a continuous counter
+    df["dum"] = (np.arange(len(df)) >= 3000).astype(np.float64)   # a session dummy
+    cols = ["ev0", "ev1", "ev2", "ev3"]
+    lf = sglm_ez.timeshift_cols(df, cols, neg_order=-3, pos_order=3)
+    xcols = sglm_ez.add_timeshifts_to_col_list(cols, cols, neg_order=-3, pos_order=3)
+    f1 = lf[lf[xcols].isna().sum(axis=1) == 0]
+    f1["asg"] = np.linspace(0.0, 1.0, len(f1))                    # an assigned column
+    X = f1[xcols + ["cnt2", "dum", "asg"]]
+    host = X.to_pandas().to_numpy(dtype=np.float64)
+    calls = []
+    orig = E.Design.from_host.__func__
+
+    def spy(cls, *a, **k):
+        calls.append(1)
+        return orig(cls, *a, **k)
+    E.Design.from_host = classmethod(spy)
+    try:
+        d = X.design()
+    finally:
+        E.Design.from_host = classmethod(orig)
+    assert not calls
+    assert d.lag is not None and d.k == 3 and d.p == len(xcols) + 3
+    assert E._lagw(d) is not None
+    y = rng.poisson(np.exp(0.3 * host[:, 0] - 0.2 * host[:, -1] + 0.5)).astype(float)
+    import sglm
+    g1 = sglm.GLM("Poisson", alpha=1e-3)
+    g1.fit(X, y)
+    g2 = sglm.GLM("Poisson", alpha=1e-3)
+    g2.fit(host, y)
+    assert rel(g1.coef_, g2.coef_) < 1e-4
+    assert abs(g1.intercept_ - g2.intercept_) < 1e-4 * max(1.0, abs(g2.intercept_))

@@ -165,3 +165,30 @@ def test_lag_gram_w_scratch_budget_chunks_fits(engine, torch_mod, monkeypatch):
     blk = np.triu(np.ones((d.P, d.P), dtype=bool))
     for k in fits:
         assert np.array_equal(out[0][k][blk], out[1][k][blk]), k
+
+
+def test_lag_gram_w_row_slab(engine, torch_mod):
+    """A row slab of the design (one rank of a row-sharded solve, comm.py): the launch iterates
+    only the occurrences whose lag window meets the slab's rows, and the slab's Gram is bitwise
+    the dense bit-plane Gram of the same slab on integer weights."""
+    from types import SimpleNamespace
+    torch = torch_mod
+    rng = np.random.default_rng(11)
+    N, m, shifts, row0 = 9000, 24, list(range(-6, 6)), 6
+    E = _events(rng, N, m, 0.03)
+    n = N - row0 - 6
+    d = engine.Design.from_events(E, shifts, row0, n, slab=(2000, 5000))
+    lg = engine._lagw(d)
+    assert lg is not None and d.n == 3000
+    assert int(lg.w_occ.numel()) < int(lg.occ.numel())       # the other occurrences dropped
+    fits = np.array([0, 2], dtype=np.int32)
+    W = torch.zeros((3, d.ld), dtype=torch.float32, device="cuda")
+    for k in fits:
+        W[k, :d.n] = torch.from_numpy(rng.integers(0, 3, d.n).astype(np.float32))
+    bf = SimpleNamespace(W=W, H=torch.full((3, d.P, d.P), float("nan"), device="cuda"))
+    engine._lag_gram_w(d, lg, bf, fits, 0)
+    Hd = _dense(engine, torch, d, W, list(fits))
+    blk = np.triu(np.ones((d.P, d.P), dtype=bool))
+    for k in fits:
+        a, b = Hd[k].cpu().numpy()[blk], bf.H[k].cpu().numpy()[blk]
+        assert np.array_equal(a, b), (k, np.flatnonzero(a != b)[:5])
