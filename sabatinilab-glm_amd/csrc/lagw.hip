@@ -16,15 +16,29 @@
 //
 // Layout: R[u] (u64 per raw row u): bit a = e_a(u), bit m = 1 (the ones column: d = 0).
 // Rows: every a2 but only d >= 0 -- the entry of d < 0 is the transpose of event a2's entry at
-// -d > 0 (and at d = 0, a2 < a1 is left to a2's launch): each H entry formed once, half the d
-// range of forming every entry from both sides.
-// Workgroup: 8 waves, one event a1, WM MT tiles of 32 (d, a2) rows x WN NT tiles of 32 (shift,
-// fit) columns, over ALL of a1's occurrences (no split: every H entry is written once, by one
-// lane, no reduction).  Per stage of KS occurrences the row words of the workgroup's d range and
-// the bf16 weights are staged in LDS (double buffered, two stages of loads in flight); the A
-// operand is expanded from the staged words (bf16 2.0 / 0, the factor 2 removed at the store),
-// the B operand is one ds_read_b128 per N tile; (d, shift-tile) pairs that form no H entry are
-// skipped.
+// -d > 0 (and at d = 0, a2 < a1 is left to a2's piece): each H entry formed once.
+// Workgroup ("piece"): one event a1, a group of d rows (both 32-event halves) and a block of
+// (shift, fit) columns, over ALL of a1's occurrences (no split: every H entry is written once, by
+// one lane, no reduction).  8 waves (two per SIMD), each 2 M tiles x 4 N tiles of
+// v_mfma_f32_32x32x16_bf16.  Per stage of 128 occurrences:
+// * weights: 16 lanes stage one occurrence's columns (a contiguous run of the (row, fit) weights,
+//   one aligned copy of the 8) with 16-byte loads and ds_write_b128 into an [occurrence][column]
+//   image whose 16-byte chunks are XOR-swizzled by row; the B operand comes back with two
+//   ds_read_b64_tr_b16 (the hardware transpose), conflict-free on that image;
+// * row words: lanes over the d rows of one occurrence pair (consecutive words), stored
+//   pair-interleaved (the two words' low / high halves in one dword: the A fragment is one
+//   rotate and one mask per dword), rows padded so that stores and b128 reads are conflict-free;
+// * the staging of stage s + 1 (stores) and s + 2 (loads) rides inside the K-steps of stage s,
+//   every load unconditional (clamped addresses, validity applied at the store) so the
+//   compiler's wait counts stay exact;
+// * each wave's live N tiles (those whose columns meet one of its d rows with a second shift
+//   that is a column) are a range fixed for the launch: the stage loop is instantiated per range,
+//   so the MFMA stream has no branch;
+// * pieces run longest first (the last round of workgroups holds the lightest);
+// * result: every H entry is written at the row of the column (s_b1, a1) that formed it
+//   (H[(b1, a1)][(b2, a2)]: a2 contiguous in a shift-major design) and lag_gram_w_sym builds the
+//   upper triangle from whichever of (i, j) / (j, i) holds an entry (round 5's kernel wrote every
+//   d > 0 entry down a column of the upper triangle: 4-byte scatter, 9x write amplification).
 #include <algorithm>
 #include <type_traits>
 
@@ -33,281 +47,8 @@
 namespace sglm {
 namespace {
 
-constexpr int kKS = 128;            // occurrences per stage (8 MFMA K-steps)
-constexpr int kWS = kKS + 8;        // weight row stride (bf16): conflict-free b128 reads
-
-struct LagWArgs {
-    const uint16_t* Wt;             // 8 shifted copies of the bf16 weights by (raw row, fit)
-    int64_t wlen;                   // elements per copy (a multiple of 8)
-    const uint64_t* R;
-    const int32_t* occ;
-    const int32_t* ev_off;
-    const int32_t* bidx;            // [smax - smin + 1]: b of shift smin + i, -1 if absent
-    const int32_t* fits;
-    float* H;
-    int32_t nf, P, p, m, K, smin, smax, layout, nraw, nh, D, Gm;
-};
-
-__device__ __forceinline__ int lag_col(const LagWArgs& a, int b, int ev) {
-    return a.layout ? ev * a.K + b : b * a.m + ev;
-}
-
 __device__ __forceinline__ int lag_col2(int layout, int m, int K, int b, int ev) {
     return layout ? ev * K + b : b * m + ev;
-}
-
-template <int MT, int NT, int WM, int WN>
-struct LagWSmem {
-    // [buf][lo/hi word][d row][X/Y][occurrence pair]: X = low halves of the pair's two words
-    // (w0 & 0xffff | w1 << 16), Y = their high halves, so that lane r of an A fragment finds
-    // bit r of both words 16 apart in one word: one rotate and one mask per dword
-    uint32_t rw[2][2][WM * MT + 1][2][kKS / 2];
-    __attribute__((aligned(16))) uint16_t ws[2][WN * NT * 32][kWS];   // [buf][(f, b1)][occ]
-    int32_t occ[4][kKS];
-};
-
-// WM x WN waves (two per SIMD): wave (wm, wn) holds MT x NT accumulator tiles (128 AGPRs), the
-// workgroup WM MT (d, a2) tiles x WN NT (f, b1) tiles.  Tiles past the event's last are computed
-// on a valid address and dropped at the store (no branch in the MFMA stream).
-template <int MT, int NT, int WM, int WN>
-__global__ void __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(2, 2)))
-lag_gram_w_kernel(LagWArgs a) {
-    constexpr int NTH = 64 * WM * WN;
-    constexpr int MB = WM * MT;                          // M tiles per workgroup
-    constexpr int ND = MB + 1;
-    constexpr int NN = WN * NT * 32;                     // columns per workgroup
-    __shared__ LagWSmem<MT, NT, WM, WN> sm;
-    const int a1 = blockIdx.x / a.Gm, g = blockIdx.x % a.Gm;
-    const int h0 = 0;                                    // every a2 (both 32-event halves)
-    const int nh1 = a.nh - h0;
-    const int Tm = a.D * nh1;
-    const int t0 = g * MB;
-    if (t0 >= Tm) return;
-    const int di0 = t0 / nh1;
-    const int di1 = min(Tm - 1, t0 + MB - 1) / nh1;
-    const int nd = di1 - di0 + 1;
-    const int dmin = 0;                                  // d = 0 .. K - 1 (see below)
-    const int o_beg = a.ev_off[a1], o_end = a.ev_off[a1 + 1];
-    const int nst = (o_end - o_beg + kKS - 1) / kKS;
-    const int n0 = blockIdx.y * NN;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r = lane & 31;
-    const int wm = wave % WM, wn = wave / WM;
-    // a G entry of row d and a column of shift smin + sb is an H entry only when the second
-    // shift smin + sb - d is a column, i.e. sb in [d, d + K - 1]: a workgroup whose d rows and
-    // columns never meet has nothing to store
-    {
-        const int sb_lo = n0 / a.nf, sb_hi = min(a.K - 1, (n0 + NN - 1) / a.nf);
-        const int dd_lo = dmin + di0, dd_hi = dmin + di1;
-        if (sb_lo >= a.K || sb_hi < dd_lo || sb_lo > dd_hi + a.K - 1) return;
-    }
-
-    // weights: column n = sb nf + f (shift smin + sb, fit f) of occurrence v is Wt[v nf + n], so a
-    // stage's columns n0 .. n0 + NN of one occurrence are one contiguous run, read as 16-byte
-    // pieces from the copy whose shift makes the run 16-byte aligned.  Task of this thread:
-    // occurrence pair kp, piece e (8 columns) -> 8 column rows of the staged tile, 2 occurrences
-    // (consecutive lanes take consecutive pairs: the transposed 4-byte stores hit distinct banks)
-    constexpr int kNP = NN / 8;                          // pieces per occurrence
-    constexpr int kWTN = (kKS / 2) * kNP;                // tasks per stage
-    constexpr int kWT = (kWTN + NTH - 1) / NTH;          // tasks per thread (at most)
-    constexpr int kRE = (ND * (kKS / 2) + NTH - 1) / NTH;   // word pairs per thread (at most)
-
-    // two register sets: while stage s is multiplied, the loads of stage s + 2 are in flight
-    // and stage s + 1 (loaded during stage s - 1) waits in the other set for the LDS store
-    uint64_t rA[kRE][2], rB[kRE][2];
-    uint4 wA[kWT][2], wB[kWT][2];
-    int32_t oreg = 0;
-
-    auto occ_load = [&](int s) {                         // occurrence rows of stage s
-        const int o = o_beg + s * kKS + tid;
-        oreg = (tid < kKS && s < nst && o < o_end) ? a.occ[o] : -1;
-    };
-    auto occ_store = [&](int s) {
-        if (tid < kKS) sm.occ[s & 3][tid] = oreg;
-    };
-    auto data_load = [&](int s, uint64_t (&rreg)[kRE][2], uint4 (&wreg)[kWT][2]) {
-        const int* ov = sm.occ[s & 3];
-#pragma unroll
-        for (int i = 0; i < kRE; ++i) {
-            const int e = tid + NTH * i;
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                uint64_t x = 0;
-                if (e < nd * (kKS / 2)) {
-                    const int dl = e / (kKS / 2), k = 2 * (e % (kKS / 2)) + j;
-                    const int v = ov[k];
-                    const int u = v + dmin + di0 + dl;
-                    if (v >= 0 && u >= 0 && u < a.nraw)
-                        x = a.R[u];
-                }
-                rreg[i][j] = x;
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < kWT; ++i) {
-            const int task = tid + NTH * i;
-            const int kp = task % (kKS / 2), e = (task / (kKS / 2)) % kNP;
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int v = ov[2 * kp + j];
-                uint4 q = make_uint4(0, 0, 0, 0);
-                if (v >= 0 && task < kWTN) {
-                    const int64_t x = (int64_t)v * a.nf + n0 + 8 * e;
-                    const int c = (int)(x & 7);
-                    q = *reinterpret_cast<const uint4*>(a.Wt + c * a.wlen + (x - c));
-                }
-                wreg[i][j] = q;
-            }
-        }
-    };
-    auto data_store = [&](int buf, const uint64_t (&rreg)[kRE][2],
-                          const uint4 (&wreg)[kWT][2]) {
-#pragma unroll
-        for (int i = 0; i < kRE; ++i) {
-            const int e = tid + NTH * i;
-            if (e < nd * (kKS / 2)) {
-                const int dl = e / (kKS / 2), kp = e % (kKS / 2);
-#pragma unroll
-                for (int pl = 0; pl < 2; ++pl) {
-                    const uint32_t w0 = (uint32_t)(rreg[i][0] >> (32 * pl));
-                    const uint32_t w1 = (uint32_t)(rreg[i][1] >> (32 * pl));
-                    sm.rw[buf][pl][dl][0][kp] = (w0 & 0xffffu) | (w1 << 16);
-                    sm.rw[buf][pl][dl][1][kp] = (w0 >> 16) | (w1 & 0xffff0000u);
-                }
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < kWT; ++i) {
-            const int task = tid + NTH * i;
-            if (task >= kWTN) continue;
-            const int kp = task % (kKS / 2), e = task / (kKS / 2);
-            const uint32_t q0[4] = {wreg[i][0].x, wreg[i][0].y, wreg[i][0].z, wreg[i][0].w};
-            const uint32_t q1[4] = {wreg[i][1].x, wreg[i][1].y, wreg[i][1].z, wreg[i][1].w};
-#pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                const uint32_t lo = (q0[c >> 1] >> (16 * (c & 1))) & 0xffffu;
-                const uint32_t hi = (q1[c >> 1] >> (16 * (c & 1))) & 0xffffu;
-                *reinterpret_cast<uint32_t*>(&sm.ws[buf][8 * e + c][2 * kp]) = lo | (hi << 16);
-            }
-        }
-    };
-
-    f32x16 acc[MT][NT];
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j) acc[i][j] = (f32x16){};
-
-    // this wave's tiles: tau = t0 + wm MT + i -> (d row, a2 half); LDS offsets of their words;
-    // live bit (i, j): tile i's d meets a column of N tile j (else its products are no H entry)
-    int toff[MT];
-    uint32_t live = 0;
-#pragma unroll
-    for (int i = 0; i < MT; ++i) {
-        const int tau = min(t0 + wm * MT + i, Tm - 1);
-        const int dl = tau / nh1 - di0, hf = h0 + tau % nh1;
-        toff[i] = ((hf * ND + dl) * 2 + (r >> 4)) * (kKS / 2) + 4 * h;   // words, one buffer
-        const int dd = dmin + di0 + dl;
-#pragma unroll
-        for (int j = 0; j < NT; ++j) {
-            const int c0 = n0 + (wn * NT + j) * 32;
-            const int sb_lo = c0 / a.nf, sb_hi = min(a.K - 1, (c0 + 31) / a.nf);
-            if (t0 + wm * MT + i < Tm && sb_lo < a.K && sb_hi >= dd && sb_lo <= dd + a.K - 1)
-                live |= 1u << (i * NT + j);
-        }
-    }
-    live = __builtin_amdgcn_readfirstlane(live);
-    const int boff = (wn * NT * 32 + r) * kWS + 8 * h;   // in bf16, within one buffer
-    const uint32_t rsh = (uint32_t)(r - 14 - 16 * (r >> 4)) & 31u;   // bit r (mod 16) -> 14
-
-    auto compute = [&](int buf) {
-        const uint32_t* rwb = &sm.rw[buf][0][0][0][0];
-        const uint16_t* wsb = &sm.ws[buf][0][0];
-#pragma unroll 2
-        for (int ks = 0; ks < kKS / 16; ++ks) {
-            bf16x8 bq[NT];
-#pragma unroll
-            for (int j = 0; j < NT; ++j)
-                bq[j] = *reinterpret_cast<const bf16x8*>(wsb + boff + j * 32 * kWS + 16 * ks);
-#pragma unroll
-            for (int i = 0; i < MT; ++i) {
-                if (!((live >> (i * NT)) & ((1u << NT) - 1))) continue;
-                const uint4 wq = *reinterpret_cast<const uint4*>(rwb + toff[i] + 8 * ks);
-                const uint32_t wv[4] = {wq.x, wq.y, wq.z, wq.w};
-                uint32_t dq[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) dq[q] = rotr32(wv[q], rsh) & 0x40004000u;
-                const bf16x8 aq = __builtin_bit_cast(bf16x8, make_uint4(dq[0], dq[1], dq[2], dq[3]));
-#pragma unroll
-                for (int j = 0; j < NT; ++j)
-                    if ((live >> (i * NT + j)) & 1u)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq, bq[j], acc[i][j],
-                                                                            0, 0, 0);
-            }
-        }
-    };
-    // stage s: cur holds stage s + 1 (stored to LDS at the end), nxt receives stage s + 2
-    auto step = [&](int s, uint64_t (&rc)[kRE][2], uint4 (&wc)[kWT][2], uint64_t (&rn)[kRE][2],
-                    uint4 (&wn_)[kWT][2]) {
-        occ_store(s + 3);                                // stage s + 3's rows (or -1s)
-        __syncthreads();
-        if (s + 2 < nst) data_load(s + 2, rn, wn_);
-        occ_load(s + 4);
-        compute(s & 1);
-        if (s + 1 < nst) data_store((s + 1) & 1, rc, wc);
-    };
-
-    if (nst > 0) {
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            occ_load(j);
-            occ_store(j);
-        }
-        __syncthreads();
-        data_load(0, rA, wA);
-        data_store(0, rA, wA);
-        if (nst > 1) data_load(1, rA, wA);
-        occ_load(3);
-    }
-    for (int s = 0; s < nst; s += 2) {
-        step(s, rA, wA, rB, wB);
-        if (s + 1 < nst) step(s + 1, rB, wB, rA, wA);
-    }
-
-    // epilogue: G entry (d, a2) x (f, b1) -> H_f[(b1, a1)][(b2, a2)], upper triangle
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-        const int nn = n0 + (wn * NT + j) * 32 + r;
-        const int sb = nn / a.nf, f = nn % a.nf;           // column: shift smin + sb, fit f
-        if (sb >= a.K) continue;
-        float* Hf = a.H + (int64_t)a.fits[f] * a.P * a.P;
-        const int s1 = a.smin + sb;
-        const int b1 = a.bidx[sb];
-        const int ci = lag_col(a, b1, a1);
-#pragma unroll
-        for (int i = 0; i < MT; ++i) {
-            const int tau = t0 + wm * MT + i;
-            if (tau >= Tm) continue;
-            const int dd = dmin + tau / nh1;
-            const int hf = h0 + tau % nh1;
-            const int s2 = s1 - dd;
-            if (s2 < a.smin || s2 > a.smax) continue;
-            const int b2 = a.bidx[s2 - a.smin];
-            if (b2 < 0) continue;
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int a2 = 32 * hf + (q & 3) + 8 * (q >> 2) + 4 * h;
-                const float val = 0.5f * acc[i][j][q];
-                if (a2 < a.m) {
-                    if (dd == 0 && a2 < a1) continue;        // formed by event a2's launch
-                    const int cj = lag_col(a, b2, a2);
-                    const int lo = min(ci, cj), hi = max(ci, cj);
-                    Hf[(int64_t)lo * a.P + hi] = val;
-                } else if (a2 == a.m && dd == 0) {
-                    Hf[(int64_t)ci * a.P + a.p] = val;
-                }
-            }
-        }
-    }
 }
 
 // H_f[p][p] = sum_t bf16(w_f(t)): kLwRed partial sums per fit (fixed row chunks, fixed tree
@@ -375,35 +116,6 @@ __global__ void __launch_bounds__(256) lag_gram_w_prep(const float* __restrict__
     }
 }
 
-template <int MT, int NT, int WM, int WN>
-int launch_lagw(const LagWArgs& a, hipStream_t s) {
-    LagWArgs b = a;
-    b.Gm = (a.D * a.nh + WM * MT - 1) / (WM * MT);
-    const int NN = WN * NT * 32;
-    const dim3 grid((unsigned)(a.m * b.Gm), (unsigned)((a.nf * a.K + NN - 1) / NN));
-    lag_gram_w_kernel<MT, NT, WM, WN><<<grid, 64 * WM * WN, 0, s>>>(b);
-    return check_launch("lag_gram_w_kernel");
-}
-
-
-// ---- v2 (round 6): coalesced staging, transposed-read weight image, XCD-local pieces ----------
-//
-// The same products as lag_gram_w_kernel; what changed is how the operands reach the LDS and how
-// the result leaves it:
-// * weights: 16 lanes stage one occurrence's NN columns (a contiguous run of the (row, fit)
-//   weights, one aligned copy of the 8) with 16-byte loads and ds_write_b128 into an [occurrence]
-//   [column] image whose 16-byte chunks are XOR-swizzled by row; the B operand comes back with two
-//   ds_read_b64_tr_b16 (the hardware transpose), conflict-free on that image;
-// * row words: lanes over the d rows of one occurrence pair (consecutive words: one or two lines
-//   per 8 lanes instead of one line per lane), stored pair-interleaved with a 4-dword pad per d row
-//   (conflict-free 4-byte stores);
-// * pieces: a workgroup is (event a1, d group g, column block y); XCD x (blocks b = x mod 8) takes
-//   the pieces [x Q, x Q + Q) in event-major order, so the workgroups that stream one event's
-//   occurrences share an XCD's L2 (the weights once per event, not once per d group);
-// * result: every H entry is written at the row of the column (s_b1, a1) that formed it --
-//   H[(b1, a1)][(b2, a2)], a2 contiguous in a shift-major design -- and lag_gram_w_sym then builds
-//   the upper triangle from whichever of (i, j) / (j, i) holds an entry (the old epilogue wrote
-//   every d > 0 entry down a column of the upper triangle: 4-byte scatter, 9x write amplification).
 constexpr int kKS2 = 128;                 // occurrences per stage
 constexpr int kKP2 = kKS2 / 2;            // occurrence pairs per stage
 constexpr int kRX2 = kKP2 + 4;            // dwords per (half, X / Y) row of a d row's words
@@ -939,40 +651,23 @@ extern "C" int sglm_lag_gram_w(const uint64_t* R, const int32_t* occ, const int3
         return SGLM_EINVAL;
     }
     hipStream_t s = as_stream(stream);
-    LagWArgs a{};
-    a.wlen = lagw_wlen(nraw, K, nf);
-    a.Wt = (const uint16_t*)work;
-    lag_gram_w_prep<<<dim3(1024, 8), 256, 0, s>>>(W, ld, n, fits, nf, row0, smin, a.wlen,
-                                                  lagw_zrow(nraw, K), (uint16_t*)work);
+    LagW2Args b{};
+    b.wlen = lagw_wlen(nraw, K, nf);
+    b.Wt = (const uint16_t*)work;
+    b.zrow = (int32_t)lagw_zrow(nraw, K);
+    lag_gram_w_prep<<<dim3(1024, 8), 256, 0, s>>>(W, ld, n, fits, nf, row0, smin, b.wlen, b.zrow,
+                                                  (uint16_t*)work);
     {
         const int st0 = check_launch("lag_gram_w_prep");
         if (st0) return st0;
     }
-    a.R = R; a.occ = occ; a.ev_off = ev_off; a.bidx = bidx;
-    a.fits = fits; a.H = H; a.nf = nf; a.P = P; a.p = p; a.m = m; a.K = K;
-    a.smin = smin; a.smax = smax; a.layout = layout; a.nraw = nraw;
-    a.nh = (m + 1 + 31) / 32;
-    a.D = K;                                             // d = s_b1 - s_b2 >= 0 only
-    const int64_t pad = (int64_t)P * (P - p - 1);
-    const unsigned gx = 1 + (unsigned)((pad + 255) / 256 < 512 ? (pad + 255) / 256 : 512);
-    float* part = (float*)((uint16_t*)work + 8 * a.wlen);
+    b.R = R; b.occ = occ; b.ev_off = ev_off; b.bidx = bidx;
+    b.fits = fits; b.H = H; b.nf = nf; b.P = P; b.p = p; b.m = m; b.K = K;
+    b.smin = smin; b.smax = smax; b.layout = layout; b.nraw = nraw;
+    b.nh = (m + 1 + 31) / 32;
+    b.D = K;                                             // d = s_b1 - s_b2 >= 0 only
+    float* part = (float*)((uint16_t*)work + 8 * b.wlen);
     lag_gram_w_part<<<dim3(kLwRed, (unsigned)nf), 256, 0, s>>>(W, ld, n, fits, part);
-    static const int v1 = [] {
-        const char* e = getenv("SGLM_LAGW_V1");
-        return e ? atoi(e) : 0;
-    }();
-    if (v1) {
-        lag_gram_w_aux<<<dim3(gx, (unsigned)nf), 256, 0, s>>>(part, fits, H, P, p);
-        int st = check_launch("lag_gram_w_aux");
-        if (st) return st;
-        if (nf * K <= 64) return launch_lagw<4, 2, 8, 1>(a, s);
-        return launch_lagw<2, 4, 8, 1>(a, s);
-    }
-    LagW2Args b{};
-    b.Wt = a.Wt; b.wlen = a.wlen; b.R = R; b.occ = occ; b.ev_off = ev_off; b.bidx = bidx;
-    b.fits = fits; b.H = H; b.nf = nf; b.P = P; b.p = p; b.m = m; b.K = K; b.smin = smin;
-    b.smax = smax; b.layout = layout; b.nraw = nraw; b.nh = a.nh; b.D = K;
-    b.zrow = (int32_t)lagw_zrow(nraw, K);
     static const int wps1 = [] {
         const char* e = getenv("SGLM_LAGW_WPS1");
         return e ? atoi(e) : 0;
