@@ -211,8 +211,9 @@ int sglm_lag_gram_w(const uint64_t* R, const int32_t* occ, const int32_t* ev_off
                     const float* W, int64_t ld, const int32_t* fits, int32_t nf, float* H,
                     int32_t P, int32_t pones, void* work, sglm_stream_t stream);
 /* work bytes of sglm_lag_gram_w: 8 shifted bf16 copies of the launch's weights over every raw
- * row (~16 B per raw row per fit -- the engine splits large launches to bound it) */
-size_t sglm_lag_gram_w_work_bytes(int32_t nraw, int32_t K, int32_t nf);
+ * row (~16 B per raw row per fit -- the engine splits large launches to bound it) and a P x P
+ * f32 image per fit for the second halves of the pieces a launch splits (load balance) */
+size_t sglm_lag_gram_w_work_bytes(int32_t nraw, int32_t K, int32_t nf, int32_t P);
 
 /* Row words of m <= 63 events: R[u] bit a = e_a(u) (ebits[m][nwords], bit u & 31 of word
  * u >> 5), bit m = 1, for u < nraw. */

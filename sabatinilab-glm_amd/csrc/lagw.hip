@@ -40,7 +40,13 @@
 //   upper triangle from whichever of (i, j) / (j, i) holds an entry (round 5's kernel wrote every
 //   d > 0 entry down a column of the upper triangle: 4-byte scatter, 9x write amplification).
 #include <algorithm>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <mutex>
+#include <queue>
 #include <type_traits>
+#include <vector>
 
 #include "common.h"
 
@@ -97,8 +103,8 @@ __global__ void __launch_bounds__(256) lag_gram_w_aux(const float* __restrict__ 
 }
 
 // Wt copy c, element j = bf16(W[fits[f]][u - row0 + smin]) at i = j + c = u nf + f: the weights of
-// raw rows u - smin .. in (row, fit) order, shifted by c; 0 off the
-// design's rows and for raw rows u >= zrow (the zero row a workgroup reads past its event's end)
+// raw rows u - smin .. in (row, fit) order, shifted by c; 0 off the design's rows and for raw rows
+// u >= zrow (the padding columns of the last column block read there)
 __global__ void __launch_bounds__(256) lag_gram_w_prep(const float* __restrict__ W, int64_t ld,
                                                        int32_t n, const int32_t* __restrict__ fits,
                                                        int32_t nf, int32_t row0, int32_t smin,
@@ -120,6 +126,9 @@ constexpr int kKS2 = 128;                 // occurrences per stage
 constexpr int kKP2 = kKS2 / 2;            // occurrence pairs per stage
 constexpr int kRX2 = kKP2 + 4;            // dwords per (half, X / Y) row of a d row's words
 constexpr int kRS2 = 4 * kRX2 + 4;        // dwords per d row of the staged row words
+constexpr int kSentR = -(1 << 28);        // row index of a past-the-end occurrence: its R reads
+                                          // (x 8 bytes, unsigned) fall past the buffer -> zeros
+constexpr uint32_t kSentW = 0xfffff000u;  // weight byte offset of a past-the-end occurrence
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -133,12 +142,17 @@ struct LagW2Args {
     const int32_t* bidx;            // [K]: b of shift smin + i
     const int32_t* fits;
     float* H;
-    int32_t nf, P, p, m, K, smin, smax, layout, nraw, nh, D, Gm, Gy, Q, npieces, zrow;
-    // piece order: ntypes > 0 -> block b runs piece type types[b / m] (types in decreasing
-    // order of work) of event b % m (longest pieces first: the last round holds the lightest);
-    // ntypes == 0 -> XCD x = b mod 8 takes the pieces [x Q, x Q + Q), event-major
-    int32_t ntypes;
-    uint8_t types[128];             // type = g + Gm y
+    float* Hb;                      // [nf][P][P]: the second halves of split pieces
+    int32_t nf, P, p, m, K, smin, smax, layout, nraw, D, Gm, Gy;
+    // job list (longest first): block b runs job jobs[b / m] on event b % m.  A job is a piece
+    // type t = g + Gm y (bits 0-13) and the stages it covers (bits 14-15: 0 all, 1 the first
+    // half -> H, 2 the second half -> Hb; lag_gram_w_sym adds the two, first + second, so the
+    // result is deterministic).  njobs == 0: block b runs piece type b / m whole.
+    int32_t njobs;
+    uint16_t jobs[256];
+#ifdef SGLM_LAGW_TRACE
+    uint64_t* trace;                // probe build: per block start / end clock, hardware slot, job
+#endif
 };
 
 template <int NCH>
@@ -146,130 +160,141 @@ __device__ __forceinline__ int lagw_swz(int row) {       // chunk XOR of the wei
     return NCH == 16 ? ((row & 3) << 2) : (((row >> 1) & 1) << 2);
 }
 
-template <int MT, int NT, int WM, int WN>
+template <int MT, int NT, int WM, int WN, int NH>
 struct LagW2Smem {
-    static constexpr int MB = WM * MT, NN = WN * NT * 32;
-    uint32_t rw[2][MB * kRS2];                                  // [buf][d row][pl][xy][pair]
+    static constexpr int MB = WM * MT, NN = WN * NT * 32, ND = MB / NH;
+    uint32_t rw[2][ND * kRS2];                                  // [buf][d row][pl][xy][pair]
     __attribute__((aligned(16))) uint16_t ws[2][kKS2 * NN];     // [buf][occurrence][column]
-    int32_t occ[4][64 * WM * WN];          // every thread stores (rows kKS2 .. : unread)
+    int32_t vo[4][kKS2];            // per occurrence of a stage: its raw row (kSentR past the end)
+    uint32_t wo[4][kKS2];           // the byte offset of its weight columns (kSentW past the end)
 };
 
-template <int MT, int NT, int WM, int WN, int WPS>
-__global__ void __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(WPS, WPS)))
+// Staging of one stage (128 occurrences) per workgroup: every load is an unconditional
+// buffer load whose range check supplies the zeros (raw rows past the end, occurrences past the
+// event's end), so no address is selected and the compiler's wait counts stay exact; the
+// per-occurrence address arithmetic is done once, by the thread that loads the occurrence.
+template <int MT, int NT, int WM, int WN, int NH, bool PRIO>
+__global__ void __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(2, 2)))
 lag_gram_w2_kernel(LagW2Args a) {
-    using SM = LagW2Smem<MT, NT, WM, WN>;
-    constexpr int NTH = 64 * WM * WN, MB = SM::MB, NN = SM::NN, NCH = NN / 8;
+    using SM = LagW2Smem<MT, NT, WM, WN, NH>;
+    constexpr int NTH = 64 * WM * WN, MB = SM::MB, NN = SM::NN, ND = SM::ND, NCH = NN / 8;
+    static_assert(MB % NH == 0, "d rows per piece");
     static_assert((kKS2 * NCH) % NTH == 0, "weight tasks per thread");
     constexpr int kWT = kKS2 * NCH / NTH;
-    constexpr int kRT = (kKP2 * MB + NTH - 1) / NTH;
+    static_assert((kKP2 * ND) % NTH == 0, "row-word tasks per thread");
+    constexpr int kRT = kKP2 * ND / NTH;
+    static_assert(kWT <= 4, "staging pieces per K-step");
     __shared__ SM sm;
-    // piece of this workgroup: XCD x = b mod 8 takes pieces [x Q, x Q + Q), event-major, the
-    // d groups of one column block adjacent (they stream the same weights)
-    int a1, rem;
-    if (a.ntypes > 0) {
-        const int b = blockIdx.x;
-        if (b >= a.ntypes * a.m) return;
-        a1 = b % a.m;
-        rem = a.types[b / a.m];
+#ifdef SGLM_LAGW_TRACE
+    const uint64_t t_beg = __builtin_amdgcn_s_memrealtime();
+#endif
+    const int blk = blockIdx.x;
+    const int a1 = blk % a.m;
+    int type, half = 0;
+    if (a.njobs > 0) {
+        if (blk >= a.njobs * a.m) return;
+        const int jb = a.jobs[blk / a.m];
+        type = jb & 0x3fff;
+        half = jb >> 14;
     } else {
-        const int pc = (int)(blockIdx.x & 7) * a.Q + (int)(blockIdx.x >> 3);
-        if (pc >= a.npieces) return;
-        const int per = a.Gm * a.Gy;
-        a1 = pc / per;
-        rem = pc % per;
+        type = blk / a.m;
+        if (type >= a.Gm * a.Gy) return;
     }
-    const int g = rem % a.Gm, y = rem / a.Gm;
-    const int nh = a.nh, Tm = a.D * nh;
+    const int g = type % a.Gm, y = type / a.Gm;
+    const int Tm = a.D * NH;
     const int t0 = g * MB;
     if (t0 >= Tm) return;
-    const int di0 = t0 / nh;
-    const int di1 = min(Tm - 1, t0 + MB - 1) / nh;
-    const int nd = di1 - di0 + 1;
+    const int di0 = t0 / NH;
     const int n0 = y * NN;
     // a G entry of row d and a column of shift smin + sb is an H entry only when sb >= d (its
     // second shift smin + sb - d is then a column): a piece whose columns all precede its d rows
     // has nothing to store
     if (n0 / a.nf >= a.K || min(a.K - 1, (n0 + NN - 1) / a.nf) < di0) return;
-    const int o_beg = a.ev_off[a1], o_end = a.ev_off[a1 + 1];
-    // every load of the pipeline is unconditional (a stage past the event's end reads the zero
-    // row), so the compiler's wait counts stay exact
-    const int nst = (o_end - o_beg + kKS2 - 1) / kKS2;
+    int o_beg = a.ev_off[a1], o_end = a.ev_off[a1 + 1];
+    if (half) {
+        const int hs = ((o_end - o_beg + kKS2 - 1) / kKS2 + 1) / 2;   // stages of the first half
+        if (half == 1) o_end = min(o_end, o_beg + hs * kKS2);
+        else o_beg += hs * kKS2;
+    }
+    const int nst = max(0, (o_end - o_beg + kKS2 - 1) / kKS2);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r = lane & 31;
     const int wm = wave % WM, wn = wave / WM;
 
-    // the row-word tasks of this thread (the same every stage): pair kp, d row dl
-    const int ntr = kKP2 * nd;
+    const __amdgpu_buffer_rsrc_t rsR =
+        __builtin_amdgcn_make_buffer_rsrc((void*)a.R, 0, a.nraw * 8, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsW =
+        __builtin_amdgcn_make_buffer_rsrc((void*)a.Wt, 0, (int)(uint32_t)(a.wlen * 16), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsO =
+        __builtin_amdgcn_make_buffer_rsrc((void*)a.occ, 0, a.ev_off[a.m] * 4, 0x00020000);
+
+    // the fixed tasks of this thread: weight chunks i (occurrence k, 16-byte chunk ch: its LDS
+    // slot), row-word tasks i (pair kp, d row dl: its LDS slot and row offset)
+    int wk[kWT], wsl[kWT];
+#pragma unroll
+    for (int i = 0; i < kWT; ++i) {
+        const int t = tid + NTH * i;
+        wk[i] = t / NCH;
+        const int ch = t % NCH;
+        wsl[i] = wk[i] * NN + 8 * (ch ^ lagw_swz<NCH>(wk[i]));
+        wk[i] = wk[i] | (ch << 16);
+    }
     int rkp[kRT], rdl[kRT];
 #pragma unroll
     for (int i = 0; i < kRT; ++i) {
         const int t = tid + NTH * i;
-        rkp[i] = t < ntr ? t / nd : -1;
-        rdl[i] = t < ntr ? t % nd : 0;
+        rkp[i] = t / ND;
+        rdl[i] = t % ND;
     }
 
-    // Every load below is unconditional, from a clamped address, and what is invalid is masked
-    // when the registers are stored (a load whose result is selected against a constant makes
-    // hipcc wait for it right away, which would serialise the staging pipeline)
-    // one register set: a stage is stored to LDS right after the barrier, then the registers
-    // receive the stage after next (clang vectors: arrays of HIP's uint4 struct stay allocas)
+    // one register set: a stage is stored to LDS during the next stage's first K-steps, then
+    // the registers receive the stage after next (clang vectors: arrays of HIP's uint4 struct
+    // stay allocas)
     u32x4 wA[kWT];
-    uint64_t rA[kRT][2];
-    uint32_t vA = 0;                          // validity of the row-word loads, bit 2 i + j
+    u32x2 rA[kRT][2];
     int32_t oreg = 0;
     bool ovalid = false;
 
     auto occ_load = [&](int s) __attribute__((always_inline)) {
-        const int o = o_beg + s * kKS2 + tid;
-        ovalid = tid < kKS2 && o < o_end;
-        oreg = a.occ[ovalid ? o : o_beg];
+        const int o = o_beg + s * kKS2 + (tid & (kKS2 - 1));
+        ovalid = o < o_end;
+        oreg = __builtin_amdgcn_raw_buffer_load_b32(rsO, o * 4, 0, 0);
     };
-    auto occ_store = [&](int s) __attribute__((always_inline)) { sm.occ[s & 3][tid] = ovalid ? oreg : -1; };
-    // staging pieces: weight chunk task i, and all row-word tasks (loads of stage s into the
-    // registers; stores of the registers to buffer buf)
+    auto occ_store = [&](int s) __attribute__((always_inline)) {
+        if (tid < kKS2) {                                        // wave-uniform
+            const int v = ovalid ? oreg : kSentR;
+            const int64_t x = (int64_t)(ovalid ? oreg : 0) * a.nf + n0;
+            const int c = (int)(x & 7);
+            sm.vo[s & 3][tid] = v;
+            sm.wo[s & 3][tid] = ovalid ? (uint32_t)(2 * (c * a.wlen + x - c)) : kSentW;
+        }
+    };
     auto load_w = [&](int s, int i) __attribute__((always_inline)) {
-        const int* ov = sm.occ[s & 3];
-        const int t = tid + NTH * i;
-        const int k = t / NCH, ch = t % NCH;
-        const int v = ov[k];
-        const int64_t u = v >= 0 ? v : a.zrow;              // past the event's end: zero weights
-        const int64_t x = u * a.nf + n0 + 8 * ch;
-        const int c = (int)(x & 7);
-        wA[i] = *reinterpret_cast<const u32x4*>(a.Wt + c * a.wlen + (x - c));
+        const uint32_t off = sm.wo[s & 3][wk[i] & 0xffff];
+        wA[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              rsW, off + 16 * (wk[i] >> 16), 0, 0));
     };
     auto load_r = [&](int s) __attribute__((always_inline)) {
-        const int* ov = sm.occ[s & 3];
-        uint32_t vb = 0;
 #pragma unroll
-        for (int i = 0; i < kRT; ++i) {
+        for (int i = 0; i < kRT; ++i)
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
-                const int v = ov[2 * max(rkp[i], 0) + j];
-                const int u = v + di0 + rdl[i];
-                const bool ok = rkp[i] >= 0 && v >= 0 && u < a.nraw;
-                vb |= (uint32_t)ok << (2 * i + j);
-                rA[i][j] = a.R[ok ? u : 0];
+                const int u = sm.vo[s & 3][2 * rkp[i] + j] + di0 + rdl[i];
+                rA[i][j] = __builtin_bit_cast(
+                    u32x2, __builtin_amdgcn_raw_buffer_load_b64(rsR, (uint32_t)u << 3, 0, 0));
             }
-        }
-        vA = vb;
     };
     auto store_w = [&](int buf, int i) __attribute__((always_inline)) {
-        const int t = tid + NTH * i;
-        const int k = t / NCH, ch = t % NCH;
-        *reinterpret_cast<u32x4*>(&sm.ws[buf][k * NN + 8 * (ch ^ lagw_swz<NCH>(k))]) = wA[i];
+        *reinterpret_cast<u32x4*>(&sm.ws[buf][wsl[i]]) = wA[i];
     };
     auto store_r = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < kRT; ++i) {
-            // a thread without a task writes a pad dword (kp 64 of d row 0: never read)
-            uint32_t* dst = &sm.rw[buf][rkp[i] >= 0 ? rdl[i] * kRS2 + rkp[i] : kKP2];
-            const uint64_t r0 = ((vA >> (2 * i)) & 1u) ? rA[i][0] : 0ull;
-            const uint64_t r1 = ((vA >> (2 * i + 1)) & 1u) ? rA[i][1] : 0ull;
+            uint32_t* dst = &sm.rw[buf][rdl[i] * kRS2 + rkp[i]];
 #pragma unroll
-            for (int pl = 0; pl < 2; ++pl) {
-                const uint32_t w0 = (uint32_t)(r0 >> (32 * pl));
-                const uint32_t w1 = (uint32_t)(r1 >> (32 * pl));
-                dst[(2 * pl) * kRX2] = (w0 & 0xffffu) | (w1 << 16);
-                dst[(2 * pl + 1) * kRX2] = (w0 >> 16) | (w1 & 0xffff0000u);
+            for (int pl = 0; pl < NH; ++pl) {
+                const uint32_t w0 = rA[i][0][pl], w1 = rA[i][1][pl];
+                dst[(2 * pl) * kRX2] = __builtin_amdgcn_perm(w1, w0, 0x05040100u);
+                dst[(2 * pl + 1) * kRX2] = __builtin_amdgcn_perm(w1, w0, 0x07060302u);
             }
         }
     };
@@ -300,7 +325,7 @@ lag_gram_w2_kernel(LagW2Args a) {
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
         const int tau = min(t0 + wm * MT + i, Tm - 1);
-        const int dl = tau / nh - di0, hf = tau % nh;
+        const int dl = tau / NH - di0, hf = tau % NH;
         aoff[i] = dl * kRS2 + (2 * hf + (r >> 4)) * kRX2 + 4 * h;
         if (t0 + wm * MT + i < Tm) dmin_w = min(dmin_w, di0 + dl);
     }
@@ -329,89 +354,56 @@ lag_gram_w2_kernel(LagW2Args a) {
     }
     const uint32_t rsh = (uint32_t)(r - 14 - 16 * (r >> 4)) & 31u;   // bit r (mod 16) -> 14
 
-    // the multiplication of stage s (buffer s & 1) over the live N tiles J0 .. J1; with two
-    // waves per SIMD the staging of the next stages rides inside its K-steps: stage s + 1 is
-    // stored to the other buffer over the first K-steps (one piece behind each K-step's
-    // MFMAs) and stage s + 2 is loaded into the freed registers over the last ones, so the
-    // LDS writes and the address work of the staging overlap the MFMAs instead of following
-    // the barrier in lockstep on both waves of a SIMD
+    // the multiplication of stage s (buffer s & 1) over the live N tiles J0 .. J1, with the
+    // staging of the next stages inside its K-steps: stage s + 1 is stored to the other buffer
+    // over the first K-steps (one piece behind each K-step's MFMAs) and stage s + 2 is loaded
+    // into the freed registers over the last ones, so the LDS writes and the address work of the
+    // staging overlap the MFMAs instead of following the barrier in lockstep on both waves of a
+    // SIMD
     auto compute = [&](int s, auto J0c, auto J1c) __attribute__((always_inline)) {
         constexpr int J0 = decltype(J0c)::value, J1 = decltype(J1c)::value;
         const int buf = s & 1;
         const uint32_t* rwb = &sm.rw[buf][0];
         const char* wsb = reinterpret_cast<const char*>(&sm.ws[buf][0]);
-        if constexpr (WPS == 1) {
-            // one wave per SIMD: nothing else hides the LDS latency, so the fragments of K-step
-            // ks + 1 are read (two register sets) while the MFMAs of ks run
-            u32x4 wq[2][MT];
-            s16x4 t1[2][NT], t2[2][NT];
-            auto fetch = [&](int ks, int st) __attribute__((always_inline)) {
-#pragma unroll
-                for (int j = J0; j <= J1; ++j) {
-                    const char* pb = wsb + boff[j] + ks * 16 * NN * 2;
-                    t1[st][j] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (lds_s16x4*)(__attribute__((address_space(3))) char*)pb);
-                    t2[st][j] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (lds_s16x4*)(__attribute__((address_space(3))) char*)(pb + 4 * NN * 2));
-                }
-#pragma unroll
-                for (int i = 0; i < MT; ++i)
-                    wq[st][i] = *reinterpret_cast<const u32x4*>(rwb + aoff[i] + 8 * ks);
-            };
-            fetch(0, 0);
-#pragma unroll
-            for (int ks = 0; ks < kKS2 / 16; ++ks) {
-                const int st = ks & 1;
-                if (ks + 1 < kKS2 / 16) fetch(ks + 1, st ^ 1);
-                bf16x8 bq[NT];
-#pragma unroll
-                for (int j = J0; j <= J1; ++j) {
-                    const uint2 u1 = __builtin_bit_cast(uint2, t1[st][j]);
-                    const uint2 u2 = __builtin_bit_cast(uint2, t2[st][j]);
-                    bq[j] = __builtin_bit_cast(bf16x8, make_uint4(u1.x, u1.y, u2.x, u2.y));
-                }
-#pragma unroll
-                for (int i = 0; i < MT; ++i) {
-                    uint32_t dq[4];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) dq[q] = rotr32(wq[st][i][q], rsh) & 0x40004000u;
-                    const bf16x8 aq =
-                        __builtin_bit_cast(bf16x8, make_uint4(dq[0], dq[1], dq[2], dq[3]));
-#pragma unroll
-                    for (int j = J0; j <= J1; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq, bq[j], acc[i][j],
-                                                                            0, 0, 0);
-                }
-            }
-            return;
-        }
-        static_assert(WPS == 1 || kWT <= 4, "staging pieces per K-step");
-#pragma unroll
-        for (int ks = 0; ks < kKS2 / 16; ++ks) {
-            if (ks < kWT) store_w(buf ^ 1, ks);
-            if (ks == kWT) store_r(buf ^ 1);
-            if (ks == 4) occ_load(s + 4);
-            if (ks >= 4 && ks - 4 < kWT) load_w(s + 2, ks - 4);
-            if (ks == 7) load_r(s + 2);
-            bf16x8 bq[NT];
+        // the fragments of K-step ks: A as the staged row words (expanded below), B as read
+        auto fetch = [&](int ks, u32x4 (&wq)[MT], s16x4 (&t1)[NT], s16x4 (&t2)[NT])
+                         __attribute__((always_inline)) {
 #pragma unroll
             for (int j = J0; j <= J1; ++j) {
                 const char* pb = wsb + boff[j] + ks * 16 * NN * 2;
-                const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                t1[j] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                     (lds_s16x4*)(__attribute__((address_space(3))) char*)pb);
-                const s16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                t2[j] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                     (lds_s16x4*)(__attribute__((address_space(3))) char*)(pb + 4 * NN * 2));
-                const uint2 u1 = __builtin_bit_cast(uint2, t1), u2 = __builtin_bit_cast(uint2, t2);
+            }
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+                wq[i] = *reinterpret_cast<const u32x4*>(rwb + aoff[i] + 8 * ks);
+        };
+        auto mult = [&](const u32x4 (&wq)[MT], const s16x4 (&t1)[NT], const s16x4 (&t2)[NT])
+                        __attribute__((always_inline)) {
+#if defined(SGLM_LAGW_PROBE) && SGLM_LAGW_PROBE == 2
+            // timing probe: fragments read and consumed by one add, no expansion, no MFMA
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = J0; j <= J1; ++j)
+                    acc[i][j][0] += __builtin_bit_cast(float, wq[i][0] ^ __builtin_bit_cast(uint2, t1[j]).x ^ __builtin_bit_cast(uint2, t2[j]).y);
+            return;
+#endif
+            bf16x8 bq[NT];
+#pragma unroll
+            for (int j = J0; j <= J1; ++j) {
+                const uint2 u1 = __builtin_bit_cast(uint2, t1[j]);
+                const uint2 u2 = __builtin_bit_cast(uint2, t2[j]);
                 bq[j] = __builtin_bit_cast(bf16x8, make_uint4(u1.x, u1.y, u2.x, u2.y));
             }
             bf16x8 aq[MT];
 #pragma unroll
             for (int i = 0; i < MT; ++i) {
-                const uint4 wq = *reinterpret_cast<const uint4*>(rwb + aoff[i] + 8 * ks);
-                const uint32_t wv[4] = {wq.x, wq.y, wq.z, wq.w};
                 uint32_t dq[4];
 #pragma unroll
-                for (int q = 0; q < 4; ++q) dq[q] = rotr32(wv[q], rsh) & 0x40004000u;
+                for (int q = 0; q < 4; ++q) dq[q] = rotr32(wq[i][q], rsh) & 0x40004000u;
                 aq[i] = __builtin_bit_cast(bf16x8, make_uint4(dq[0], dq[1], dq[2], dq[3]));
             }
 #pragma unroll
@@ -420,11 +412,37 @@ lag_gram_w2_kernel(LagW2Args a) {
                 for (int j = J0; j <= J1; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq[i], bq[j], acc[i][j],
                                                                         0, 0, 0);
+        };
+        auto staging = [&](int ks) __attribute__((always_inline)) {
+#if defined(SGLM_LAGW_PROBE) && SGLM_LAGW_PROBE == 1
+            return;                                  // timing probe: no staging in the loop
+#endif
+            if (ks < kWT) store_w(buf ^ 1, ks);
+            if (ks == kWT) store_r(buf ^ 1);
+            if (ks == 4) occ_load(s + 4);
+            if (ks >= 4 && ks - 4 < kWT) load_w(s + 2, ks - 4);
+            if (ks == 7) load_r(s + 2);
+        };
+        // the fragments of K-step ks + 1 are read while the MFMAs of ks run (in-grid 0.598 ->
+        // ~0.52 ms per launch together with the staging rework; hipcc sinks the reads to their
+        // MFMAs unless the scheduling barriers hold them ahead)
+        u32x4 wq[2][MT];
+        s16x4 t1[2][NT], t2[2][NT];
+        fetch(0, wq[0], t1[0], t2[0]);
+#pragma unroll
+        for (int ks = 0; ks < kKS2 / 16; ++ks) {
+            staging(ks);
+            if (ks + 1 < kKS2 / 16)
+                fetch(ks + 1, wq[(ks + 1) & 1], t1[(ks + 1) & 1], t2[(ks + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+            mult(wq[ks & 1], t1[ks & 1], t2[ks & 1]);
+            if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
         }
     };
-    // stage s: stage s + 1 (loaded during stage s - 1) is stored to the other buffer, the
-    // occurrence rows of stage s + 4 and the data of stage s + 2 are loaded, stage s is
-    // multiplied (its loads overlap it)
+    // stage s: the occurrences of stage s + 3 are stored, stage s is multiplied (stage s + 1 is
+    // stored, the occurrences of stage s + 4 and the data of stage s + 2 are loaded inside)
     auto main_loop = [&](auto J0c, auto J1c) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
@@ -439,12 +457,7 @@ lag_gram_w2_kernel(LagW2Args a) {
         for (int s = 0; s < nst; ++s) {
             occ_store(s + 3);
             __syncthreads();
-            if constexpr (WPS == 1) {
-                data_store((s + 1) & 1);     // past the end: zero rows, never read
-                occ_load(s + 4);
-                data_load(s + 2);
-            }
-            compute(s, J0c, J1c);            // WPS 2: stores s + 1, loads s + 2 inside
+            compute(s, J0c, J1c);
         }
     };
     using I0 = std::integral_constant<int, 0>;
@@ -487,14 +500,15 @@ lag_gram_w2_kernel(LagW2Args a) {
         if (sb >= a.K) continue;
         const int b1 = a.bidx[sb];
         if (b1 < 0) continue;
-        float* Hrow = a.H + (int64_t)a.fits[f] * a.P * a.P + (int64_t)lag_col2(a.layout, a.m, a.K,
-                                                                             b1, a1) * a.P;
+        float* Hrow = (half == 2 ? a.Hb + (int64_t)f * a.P * a.P
+                                 : a.H + (int64_t)a.fits[f] * a.P * a.P) +
+                      (int64_t)lag_col2(a.layout, a.m, a.K, b1, a1) * a.P;
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
             const int tau = t0 + wm * MT + i;
             if (tau >= Tm) continue;
-            const int dd = tau / nh;
-            const int hf = tau % nh;
+            const int dd = tau / NH;
+            const int hf = tau % NH;
             if (sb < dd) continue;                           // second shift below smin
             const int b2 = a.bidx[sb - dd];
             if (b2 < 0) continue;
@@ -511,25 +525,49 @@ lag_gram_w2_kernel(LagW2Args a) {
             }
         }
     }
+#ifdef SGLM_LAGW_TRACE
+    __syncthreads();
+    if (tid == 0) {
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        const uint32_t hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW_ID
+        const uint32_t xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // XCC_ID
+        a.trace[4 * blk + 0] = t_beg;
+        a.trace[4 * blk + 1] = t_end;
+        a.trace[4 * blk + 2] = (uint64_t)hw | ((uint64_t)xcc << 32);
+        a.trace[4 * blk + 3] = (uint64_t)type | ((uint64_t)a1 << 16) | ((uint64_t)nst << 32);
+    }
+#endif
 }
+
+// The pieces a launch split in two (their second halves in Hb): the piece type of an entry is
+// found from its holder row's column (b1, a1) and its column (b2, a2) -- d = s1 - s2, the event
+// half of a2, the (shift, fit) column of (s1, f).
+struct LagwSplit {
+    const float* Hb;                // null: nothing split
+    int32_t smin, nh, MB, NN, Gm, nf;
+    uint32_t mask[8];               // bit t: piece type t split
+};
 
 // Upper triangle of H_f from the entries lag_gram_w2_kernel wrote: entry {i, j} (i < j) sits at
 // row i when column i has the larger shift, or the same shift and the smaller event (the ones
 // column p: at row i); continuous columns of a mixed design and the padding columns are zeroed
 // (the continuous rows / columns are written after this by _mix_hess).  One 256-thread workgroup
-// per 64 x 64 upper tile (I, J) of one fit: the transposed tile (J, I) staged through LDS.
+// per 64 x 64 upper tile (I, J) of one fit: the transposed tile (J, I) staged through LDS.  A
+// split piece's entries are its first half (H) + its second half (Hb), in that order.
 __global__ void __launch_bounds__(256) lag_gram_w_sym(float* __restrict__ H,
                                                       const int32_t* __restrict__ fits, int32_t P,
                                                       int32_t p, int32_t m, int32_t K,
                                                       int32_t layout,
-                                                      const int32_t* __restrict__ shifts) {
-    __shared__ float tl[64][65];
+                                                      const int32_t* __restrict__ shifts,
+                                                      LagwSplit sp) {
+    __shared__ float tl[64][65], tb[64][65];     // H and Hb rows J*64.., columns I*64..
     __shared__ int ks_i[64], ks_j[64];           // (shift, event) keys of the tile's columns
     const int T = P / 64;
     int I = 0, rem = blockIdx.x;
     while (rem >= T - I) { rem -= T - I; ++I; }  // tile (I, J), I <= J, row-major over the upper
     const int J = I + rem;
     float* Hf = H + (int64_t)fits[blockIdx.y] * P * P;
+    const float* Hbf = sp.Hb ? sp.Hb + (int64_t)blockIdx.y * P * P : nullptr;
     const int tid = threadIdx.x;
     const int plag = m * K;
     if (tid < 128) {
@@ -541,10 +579,20 @@ __global__ void __launch_bounds__(256) lag_gram_w_sym(float* __restrict__ H,
         }
         (tid < 64 ? ks_i : ks_j)[tid & 63] = key;
     }
-    // stage H rows J*64.., columns I*64.. (the lower counterpart)
+    // split piece of the entry held at row (key kr) and column (key kc; event a2 = m: ones)
+    auto split = [&](int kr, int kc, int a2) -> bool {
+        if (!Hbf) return false;
+        const int s1 = kr / 64 - 65536, s2 = kc / 64 - 65536;
+        const int tau = (s1 - s2) * sp.nh + a2 / 32;
+        const int y = ((s1 - sp.smin) * sp.nf + (int)blockIdx.y) / sp.NN;
+        const int t = tau / sp.MB + sp.Gm * y;
+        return (sp.mask[t >> 5] >> (t & 31)) & 1u;
+    };
+    // stage H rows J*64.., columns I*64.. (the lower counterpart), and Hb's when split
     for (int e = tid; e < 64 * 64; e += 256) {
         const int rr = e >> 6, cc = e & 63;
         tl[rr][cc] = Hf[(int64_t)(J * 64 + rr) * P + I * 64 + cc];
+        if (Hbf) tb[rr][cc] = Hbf[(int64_t)(J * 64 + rr) * P + I * 64 + cc];
     }
     __syncthreads();
     for (int e = tid; e < 64 * 64; e += 256) {
@@ -556,67 +604,202 @@ __global__ void __launch_bounds__(256) lag_gram_w_sym(float* __restrict__ H,
             *dst = 0.0f;
             continue;
         }
-        if (i == j) continue;                    // diagonal: written in place (H[p][p] by aux)
+        const int ki = ks_i[il], kj = ks_j[jl];
+        if (i == j) {                            // diagonal: in place (H[p][p] by aux)
+            if (ki >= 0 && split(ki, ki, 63 - ki % 64)) *dst += Hbf[(int64_t)i * P + j];
+            continue;
+        }
         if (j == p) {
             if (i >= plag) *dst = 0.0f;          // a continuous column's ones entry
-            continue;                            // a lag column's: at row i
+            else if (split(ki, ki, m)) *dst += Hbf[(int64_t)i * P + j];   // a lag column's: row i
+            continue;
         }
-        const int ki = ks_i[il], kj = ks_j[jl];
         if (ki < 0 || kj < 0) *dst = 0.0f;       // a continuous column
-        else if (kj > ki) *dst = tl[jl][il];     // held at row j
+        else if (kj > ki)                        // held at row j
+            *dst = split(kj, ki, 63 - ki % 64) ? tl[jl][il] + tb[jl][il] : tl[jl][il];
+        else if (split(ki, kj, 63 - kj % 64))    // held at row i
+            *dst += Hbf[(int64_t)i * P + j];
     }
 }
 
-template <int MT, int NT, int WM, int WN, int WPS>
-int launch_lagw2(const LagW2Args& a0, hipStream_t s) {
-    LagW2Args a = a0;
-    constexpr int MB = WM * MT, NN = WN * NT * 32;
-    a.Gm = (a.D * a.nh + MB - 1) / MB;
-    a.Gy = (a.nf * a.K + NN - 1) / NN;
-    a.npieces = a.m * a.Gm * a.Gy;
-    a.Q = (a.npieces + 7) / 8;
-    a.ntypes = 0;
-    // longest pieces first (default; measured 0.634 -> 0.600 ms per launch on the C4 grid
-    // against the XCD-local ranges: the last round of workgroups then holds the lightest pieces,
-    // which outweighs the L2 sharing of one event's pieces); SGLM_LAGW_ORDER=0: XCD ranges
-    static const int lpt = [] {
-        const char* e = getenv("SGLM_LAGW_ORDER");
-        return e ? atoi(e) : 1;
+// The launch's job list.  Piece order: longest first (measured 0.634 -> 0.600 ms per C4
+// launch against XCD-local ranges: the last round of workgroups holds the lightest pieces).  Work
+// of a piece type per stage, in units of one live MFMA per K-step: the live MFMAs of the busier
+// SIMD (waves w and w + 4 share one) + 7 for the staging every piece does (fitted to per-piece
+// timelines of the C4 launches, tools/lagw_trace.py).  With one workgroup per CU and ~2 pieces per
+// CU, LPT still left the CUs 20 % idle over a 5-fit launch (the heaviest pieces + a light one set
+// the end), so the heaviest types may run as two half-occurrence jobs: the split set is chosen
+// by simulating the greedy dispatch (each free CU takes the next job) over the CU count, a half
+// priced at half its piece + 2 % of the heaviest.  (Adding the halves into zeroed H entries with
+// float atomics cost more than the tail: 0.881 -> 1.085 ms per 5-fit call; the second halves
+// now go to a scratch image that the symmetrize pass adds.)  Cached per launch shape.
+struct LagwPlan {
+    int njobs = 0;                                     // -1: no live piece
+    bool split = false;
+    uint16_t jobs[256];
+    uint32_t mask[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+};
+
+static int lagw_cus() {
+    static const int n = [] {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            v <= 0)
+            v = 256;
+        return v;
     }();
-    const int per = a.Gm * a.Gy;
-    if (lpt && per <= 128) {
-        // work of a piece type: its live (M tile, N tile) MFMA pairs per K-step plus the
-        // staging every piece does (about a quarter of a full piece's MFMA time)
-        int cost[128];
-        for (int t = 0; t < per; ++t) {
-            const int g = t % a.Gm, y = t / a.Gm;
-            const int t0 = g * MB, Tm = a.D * a.nh;
-            int live = 0;
-            for (int tau = t0; tau < t0 + MB && tau < Tm; ++tau) {
-                const int d = tau / a.nh;
-                for (int j = 0; j < NN / 32; ++j) {
-                    const int c0 = y * NN + 32 * j;
-                    const int sb_lo = c0 / a.nf, sb_hi = std::min(a.K - 1, (c0 + 31) / a.nf);
-                    if (sb_lo < a.K && sb_hi >= d) ++live;
+    return n;
+}
+
+static LagwPlan lagw_plan(int m, int K, int nf, int NH, int MT, int NT, int WM, int Gm, int Gy,
+                          bool can_split) {
+    static std::mutex mu;
+    static std::map<std::vector<int>, LagwPlan> cache;
+    const char* e = getenv("SGLM_LAGW_SPLIT");          // read per launch (A/B, tests)
+    const bool sp_ok = can_split && !(e && e[0] == '0');
+    const std::vector<int> key{m, K, nf, NH, MT, NT, WM, Gm, Gy, sp_ok};
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    LagwPlan pl;
+    const int per = Gm * Gy, MB = WM * MT, NN = NT * 32, Tm = K * NH;
+    if (per > 128) return cache[key] = pl;              // natural order (njobs = 0)
+    std::vector<std::pair<double, int>> types;          // (cost, type), live types only
+    for (int t = 0; t < per; ++t) {
+        const int g = t % Gm, y = t / Gm;
+        const int t0 = g * MB, n0 = y * NN, di0 = t0 / NH;
+        if (t0 >= Tm || n0 / nf >= K || std::min(K - 1, (n0 + NN - 1) / nf) < di0) continue;
+        int simd[4] = {0, 0, 0, 0};
+        for (int wm = 0; wm < WM; ++wm) {
+            int dmin = 1 << 30;
+            for (int i = 0; i < MT; ++i)
+                if (t0 + wm * MT + i < Tm) dmin = std::min(dmin, (t0 + wm * MT + i) / NH);
+            int j0 = NT, j1 = -1;
+            for (int j = 0; j < NT; ++j) {
+                const int c0 = n0 + 32 * j;
+                if (c0 / nf < K && std::min(K - 1, (c0 + 31) / nf) >= dmin) {
+                    j0 = std::min(j0, j);
+                    j1 = std::max(j1, j);
                 }
             }
-            const int n0 = y * NN, di0 = t0 / a.nh;
-            const bool dead = t0 >= Tm || n0 / a.nf >= a.K ||
-                              std::min(a.K - 1, (n0 + NN - 1) / a.nf) < di0;
-            cost[t] = dead ? -1 : live + MB * (NN / 32) / 4;
+            simd[wm % 4] += j1 >= j0 ? MT * (j1 - j0 + 1) : 0;
         }
-        int nt = 0;
-        for (int t = 0; t < per; ++t)
-            if (cost[t] >= 0) a.types[nt++] = (uint8_t)t;
-        std::stable_sort(a.types, a.types + nt,
-                         [&](uint8_t x, uint8_t y) { return cost[x] > cost[y]; });
-        a.ntypes = nt;
-        if (nt == 0) return SGLM_OK;
-        lag_gram_w2_kernel<MT, NT, WM, WN, WPS><<<dim3((unsigned)(nt * a.m)), 64 * WM * WN, 0,
-                                                  s>>>(a);
-        return check_launch("lag_gram_w2_kernel");
+        const int mx = std::max(std::max(simd[0], simd[1]), std::max(simd[2], simd[3]));
+        types.push_back({mx + 7.0, t});
     }
-    lag_gram_w2_kernel<MT, NT, WM, WN, WPS><<<dim3((unsigned)(8 * a.Q)), 64 * WM * WN, 0, s>>>(a);
+    std::stable_sort(types.begin(), types.end(),
+                     [](const std::pair<double, int>& x, const std::pair<double, int>& y) {
+                         return x.first > y.first;
+                     });
+    const int nt = (int)types.size();
+    if (nt == 0) {
+        pl.njobs = -1;
+        return cache[key] = pl;
+    }
+    // split the ns heaviest types, ns = 0 .. nt: the best simulated makespan (ties: fewer)
+    const int ncu = lagw_cus();
+    const double fix = 0.02 * types[0].first;
+    int best_ns = 0;
+    double best = 0.0;
+    for (int ns = 0; ns <= (sp_ok ? nt : 0); ++ns) {
+        if (nt + ns > 256) break;
+        std::vector<double> jc;
+        for (int i = 0; i < nt; ++i) {
+            const double c = types[i].first;
+            if (i < ns) jc.insert(jc.end(), 2 * (size_t)m, 0.5 * c + fix);
+            else jc.insert(jc.end(), (size_t)m, c);
+        }
+        std::stable_sort(jc.begin(), jc.end(), std::greater<double>());
+        std::priority_queue<double, std::vector<double>, std::greater<double>> q;
+        for (int c = 0; c < ncu; ++c) q.push(0.0);
+        double mk = 0.0;
+        for (double c : jc) {
+            const double t = q.top() + c;
+            q.pop();
+            q.push(t);
+            mk = std::max(mk, t);
+        }
+        if (ns == 0 || mk < best * 0.98) {
+            best = mk;
+            best_ns = ns;
+        }
+    }
+    std::vector<std::pair<double, int>> jl;
+    for (int i = 0; i < nt; ++i) {
+        const double c = types[i].first;
+        const int t = types[i].second;
+        if (i < best_ns) {
+            jl.push_back({0.5 * c + fix, t | (1 << 14)});
+            jl.push_back({0.5 * c + fix, t | (2 << 14)});
+            pl.mask[t >> 5] |= 1u << (t & 31);
+        } else {
+            jl.push_back({c, t});
+        }
+    }
+    std::stable_sort(jl.begin(), jl.end(),
+                     [](const std::pair<double, int>& x, const std::pair<double, int>& y) {
+                         return x.first > y.first;
+                     });
+    pl.njobs = (int)jl.size();
+    pl.split = best_ns > 0;
+    for (int i = 0; i < pl.njobs; ++i) pl.jobs[i] = (uint16_t)jl[i].second;
+    return cache[key] = pl;
+}
+
+template <int MT, int NT, int WM, int WN, int NH>
+int launch_lagw2(const LagW2Args& a0, hipStream_t s, LagwSplit& sp) {
+    LagW2Args a = a0;
+    constexpr int MB = WM * MT, NN = WN * NT * 32;
+    static_assert(WN == 1, "one wave column");
+    a.Gm = (a.D * NH + MB - 1) / MB;
+    a.Gy = (a.nf * a.K + NN - 1) / NN;
+    const LagwPlan pl = lagw_plan(a.m, a.K, a.nf, NH, MT, NT, WM, a.Gm, a.Gy, a.Hb != nullptr);
+    if (pl.njobs < 0) return SGLM_OK;
+    sp.Hb = pl.split ? a.Hb : nullptr;
+    sp.smin = a.smin;
+    sp.nh = NH;
+    sp.MB = MB;
+    sp.NN = NN;
+    sp.Gm = a.Gm;
+    sp.nf = a.nf;
+    std::memcpy(sp.mask, pl.mask, sizeof(sp.mask));
+    unsigned nblk;
+    if (pl.njobs > 0) {
+        a.njobs = pl.njobs;
+        std::memcpy(a.jobs, pl.jobs, sizeof(a.jobs));
+        nblk = (unsigned)(pl.njobs * a.m);
+    } else {
+        a.njobs = 0;
+        nblk = (unsigned)(a.Gm * a.Gy * a.m);
+    }
+#ifdef SGLM_LAGW_TRACE
+    hipMalloc(&a.trace, (size_t)nblk * 32);
+    hipMemsetAsync(a.trace, 0, (size_t)nblk * 32, s);
+#endif
+    const char* e = getenv("SGLM_LAGW_PRIO");           // read per launch (A/B)
+    if (!(e && e[0] == '1'))
+        lag_gram_w2_kernel<MT, NT, WM, WN, NH, false><<<dim3(nblk), 64 * WM * WN, 0, s>>>(a);
+    else
+        lag_gram_w2_kernel<MT, NT, WM, WN, NH, true><<<dim3(nblk), 64 * WM * WN, 0, s>>>(a);
+#ifdef SGLM_LAGW_TRACE
+    {
+        static int seq = 0;
+        std::vector<uint64_t> tr((size_t)nblk * 4);
+        hipStreamSynchronize(s);
+        hipMemcpy(tr.data(), a.trace, tr.size() * 8, hipMemcpyDeviceToHost);
+        hipFree(a.trace);
+        const char* out = getenv("SGLM_LAGW_TRACE_OUT");
+        if (out) {
+            char path[512];
+            snprintf(path, sizeof(path), "%s_%d_nf%d.bin", out, seq++, a.nf);
+            if (FILE* f = fopen(path, "wb")) {
+                fwrite(tr.data(), 8, tr.size(), f);
+                fclose(f);
+            }
+        }
+    }
+#endif
     return check_launch("lag_gram_w2_kernel");
 }
 
@@ -633,8 +816,13 @@ static int64_t lagw_wlen(int32_t nraw, int32_t K, int32_t nf) {
     return ((lagw_zrow(nraw, K) + K + 8) * nf + 512 + 7) / 8 * 8;
 }
 
-extern "C" size_t sglm_lag_gram_w_work_bytes(int32_t nraw, int32_t K, int32_t nf) {
-    return (size_t)(8 * lagw_wlen(nraw, K, nf) * 2) + (size_t)nf * kLwRed * 4;
+// work: the weight copies, the ones-diagonal partial sums, the split pieces' second halves
+static size_t lagw_hb_off(int32_t nraw, int32_t K, int32_t nf) {
+    return ((size_t)(8 * lagw_wlen(nraw, K, nf) * 2) + (size_t)nf * kLwRed * 4 + 255) / 256 * 256;
+}
+
+extern "C" size_t sglm_lag_gram_w_work_bytes(int32_t nraw, int32_t K, int32_t nf, int32_t P) {
+    return lagw_hb_off(nraw, K, nf) + (size_t)nf * P * P * 4;
 }
 
 extern "C" int sglm_lag_gram_w(const uint64_t* R, const int32_t* occ, const int32_t* ev_off,
@@ -650,13 +838,19 @@ extern "C" int sglm_lag_gram_w(const uint64_t* R, const int32_t* occ, const int3
         set_error("sglm_lag_gram_w: bad args (m=%d K=%d P=%d)", m, K, P);
         return SGLM_EINVAL;
     }
+    const int64_t wlen = lagw_wlen(nraw, K, nf);
+    if (nraw >= (1 << 28) || wlen >= ((int64_t)1 << 27)) {
+        // the launch addresses R and the weight image through 32-bit buffer offsets
+        set_error("sglm_lag_gram_w: %d raw rows x %d fits exceed one launch (split the fits)",
+                  nraw, nf);
+        return SGLM_EINVAL;
+    }
     hipStream_t s = as_stream(stream);
     LagW2Args b{};
-    b.wlen = lagw_wlen(nraw, K, nf);
+    b.wlen = wlen;
     b.Wt = (const uint16_t*)work;
-    b.zrow = (int32_t)lagw_zrow(nraw, K);
-    lag_gram_w_prep<<<dim3(1024, 8), 256, 0, s>>>(W, ld, n, fits, nf, row0, smin, b.wlen, b.zrow,
-                                                  (uint16_t*)work);
+    lag_gram_w_prep<<<dim3(1024, 8), 256, 0, s>>>(W, ld, n, fits, nf, row0, smin, b.wlen,
+                                                  lagw_zrow(nraw, K), (uint16_t*)work);
     {
         const int st0 = check_launch("lag_gram_w_prep");
         if (st0) return st0;
@@ -664,22 +858,20 @@ extern "C" int sglm_lag_gram_w(const uint64_t* R, const int32_t* occ, const int3
     b.R = R; b.occ = occ; b.ev_off = ev_off; b.bidx = bidx;
     b.fits = fits; b.H = H; b.nf = nf; b.P = P; b.p = p; b.m = m; b.K = K;
     b.smin = smin; b.smax = smax; b.layout = layout; b.nraw = nraw;
-    b.nh = (m + 1 + 31) / 32;
     b.D = K;                                             // d = s_b1 - s_b2 >= 0 only
     float* part = (float*)((uint16_t*)work + 8 * b.wlen);
     lag_gram_w_part<<<dim3(kLwRed, (unsigned)nf), 256, 0, s>>>(W, ld, n, fits, part);
-    static const int wps1 = [] {
-        const char* e = getenv("SGLM_LAGW_WPS1");
-        return e ? atoi(e) : 0;
-    }();
-    const int st = wps1 ? ((nf * K <= 64) ? launch_lagw2<4, 2, 4, 1, 1>(b, s)
-                                          : launch_lagw2<4, 4, 4, 1, 1>(b, s))
-                        : ((nf * K <= 64) ? launch_lagw2<2, 2, 8, 1, 2>(b, s)
-                                          : launch_lagw2<2, 4, 8, 1, 2>(b, s));
+    b.Hb = (float*)((char*)work + lagw_hb_off(nraw, K, nf));
+    const bool two = m + 1 > 32;                         // two 32-event halves per d row
+    LagwSplit sp{};
+    const int st = (nf * K <= 64) ? (two ? launch_lagw2<2, 2, 8, 1, 2>(b, s, sp)
+                                         : launch_lagw2<2, 2, 8, 1, 1>(b, s, sp))
+                                  : (two ? launch_lagw2<2, 4, 8, 1, 2>(b, s, sp)
+                                         : launch_lagw2<2, 4, 8, 1, 1>(b, s, sp));
     if (st) return st;
     const int T = P / 64;
     lag_gram_w_sym<<<dim3((unsigned)(T * (T + 1) / 2), (unsigned)nf), 256, 0, s>>>(
-        H, fits, P, p, m, K, layout, shifts);
+        H, fits, P, p, m, K, layout, shifts, sp);
     lag_gram_w_aux<<<dim3(1, (unsigned)nf), 256, 0, s>>>(part, fits, H, P, p);
     return check_launch("lag_gram_w_aux");
 }

@@ -3188,10 +3188,11 @@ def _lag_gram_w(d: Design, lg, bf, fits: np.ndarray, st, ev=None):
     fits_d = upl(fits, np.int32) if upl is not None else \
         torch.from_numpy(np.asarray(fits, dtype=np.int32)).to(d.device)
     # the launch's scratch (8 shifted bf16 copies of the fits' weights over every raw row,
-    # ~16 B per raw row per fit) stays within LAGW_WORK_BUDGET: fits in chunks of at most that
-    per1 = _lib.query("sglm_lag_gram_w_work_bytes", lg.n_raw, lg.K, 1)
+    # ~16 B per raw row per fit, and a P x P image per fit for the split pieces' second halves)
+    # stays within LAGW_WORK_BUDGET: fits in chunks of at most that
+    per1 = _lib.query("sglm_lag_gram_w_work_bytes", lg.n_raw, lg.K, 1, d.P)
     chunk = max(1, min(nact, int(LAGW_WORK_BUDGET // max(1, per1))))
-    work = _work(_lib.query("sglm_lag_gram_w_work_bytes", lg.n_raw, lg.K, chunk), d.device,
+    work = _work(_lib.query("sglm_lag_gram_w_work_bytes", lg.n_raw, lg.K, chunk, d.P), d.device,
                  "lagw")
     with _GRAM_LOCK:
         _gram_turn()

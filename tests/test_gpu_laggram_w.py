@@ -49,7 +49,7 @@ def _lag(engine, torch, d, W, fits):
     fits_d = torch.tensor(fits, dtype=torch.int32, device="cuda")
     H = torch.full((int(max(fits)) + 1, d.P, d.P), float("nan"), dtype=torch.float32,
                    device="cuda")
-    wk = torch.empty(_lib.query("sglm_lag_gram_w_work_bytes", lg.n_raw, lg.K, len(fits)),
+    wk = torch.empty(_lib.query("sglm_lag_gram_w_work_bytes", lg.n_raw, lg.K, len(fits), d.P),
                      dtype=torch.uint8, device="cuda")
     _lib.call("sglm_lag_gram_w", lg.R.data_ptr(), lg.occ.data_ptr(), lg.ev_off.data_ptr(), lg.m,
               lg.n_raw, lg.shifts.data_ptr(), lg.bidx.data_ptr(), lg.K, lg.smin, lg.smax,
@@ -98,6 +98,37 @@ def test_lag_gram_w_matches_dense(engine, torch_mod, m, shifts, row0, event_majo
         assert np.max(np.abs(a - b)) <= 2e-6 * max(1.0, float(np.max(np.abs(a)))), k
 
 
+@pytest.mark.parametrize("split", ["0", "1"])
+def test_lag_gram_w_split_pieces(engine, torch_mod, monkeypatch, split):
+    """With and without the load-balancing split (the heaviest pieces run as two
+    half-occurrence jobs whose second halves the symmetrize pass adds): integer weights bitwise
+    the dense Gram, IRLS-like weights within f32 summation noise; the C4 layout (two event
+    halves) at 5 fits and one fit."""
+    torch = torch_mod
+    monkeypatch.setenv("SGLM_LAGW_SPLIT", split)
+    rng = np.random.default_rng(21)
+    N, m, shifts, row0 = 20000, 50, list(range(-20, 20)), 20
+    E = _events(rng, N, m, 0.02)
+    n = N - row0 - 19
+    d = engine.Design.from_events(E, shifts, row0, n)
+    blk = np.triu(np.ones((d.P, d.P), dtype=bool))
+    for nf in (5, 1):
+        fits = list(range(nf))
+        Wi = torch.zeros((nf, d.ld), dtype=torch.float32, device="cuda")
+        Wf = torch.zeros((nf, d.ld), dtype=torch.float32, device="cuda")
+        for k in fits:
+            Wi[k, :n] = torch.from_numpy(rng.integers(0, 3, n).astype(np.float32))
+            Wf[k, :n] = torch.from_numpy(np.exp(rng.normal(0, 1, n)).astype(np.float32))
+        Hd, Hl = _dense(engine, torch, d, Wi, fits), _lag(engine, torch, d, Wi, fits)
+        for k in fits:
+            a, b = Hd[k].cpu().numpy()[blk], Hl[k].cpu().numpy()[blk]
+            assert np.array_equal(a, b), (nf, k, np.flatnonzero(a != b)[:5])
+        Hd, Hl = _dense(engine, torch, d, Wf, fits), _lag(engine, torch, d, Wf, fits)
+        for k in fits:
+            a, b = Hd[k].cpu().numpy()[blk], Hl[k].cpu().numpy()[blk]
+            assert np.max(np.abs(a - b)) <= 2e-6 * float(np.max(np.abs(a))), (nf, k)
+
+
 def test_lag_gram_w_cost_model(engine, torch_mod):
     """The structured Gram is chosen for the C4 shape (2000 lag columns, 2 % events) and not
     for a small design whose dense Gram costs microseconds."""
@@ -144,8 +175,9 @@ def test_lag_gram_w_in_grid_matches_dense_path(engine, torch_mod, monkeypatch):
 
 
 def test_lag_gram_w_scratch_budget_chunks_fits(engine, torch_mod, monkeypatch):
-    """The launch's scratch (8 bf16 weight copies per fit) is bounded: with a budget of two
-    fits the seven fits run as four launches and give bitwise the same Hessians."""
+    """The launch's scratch (8 bf16 weight copies and a split-half image per fit) is bounded:
+    with a budget of two fits the seven fits run as four launches and give bitwise the same
+    Hessians (integer weights: exact sums, whichever pieces each launch shape splits)."""
     from types import SimpleNamespace
     torch = torch_mod
     rng = np.random.default_rng(7)
@@ -153,10 +185,10 @@ def test_lag_gram_w_scratch_budget_chunks_fits(engine, torch_mod, monkeypatch):
     d = engine.Design.from_events(E, list(range(-6, 6)), 6, 4988)
     lg = engine._lagw(d)
     fits = np.array([0, 2, 3, 5, 6, 8, 9], dtype=np.int32)
-    W = torch.rand((10, d.ld), device="cuda")
+    W = torch.randint(0, 4, (10, d.ld), device="cuda").float()
     out = []
     for budget in (float(1 << 40), 2.5 * engine._lib.query("sglm_lag_gram_w_work_bytes",
-                                                             lg.n_raw, lg.K, 1)):
+                                                             lg.n_raw, lg.K, 1, d.P)):
         monkeypatch.setattr(engine, "LAGW_WORK_BUDGET", budget)
         bf = SimpleNamespace(W=W, H=torch.zeros((10, d.P, d.P), device="cuda"))
         engine._lag_gram_w(d, lg, bf, fits, 0)

@@ -15,7 +15,7 @@ for nf in (1, 5):
     fits = torch.arange(nf, dtype=torch.int32, device="cuda")
     W = torch.rand((nf, d.ld), device="cuda")
     H = torch.zeros((nf, d.P, d.P), device="cuda")
-    wk = torch.empty(_lib.query("sglm_lag_gram_w_work_bytes", lg.n_raw, lg.K, nf), dtype=torch.uint8, device="cuda")
+    wk = torch.empty(_lib.query("sglm_lag_gram_w_work_bytes", lg.n_raw, lg.K, nf, d.P), dtype=torch.uint8, device="cuda")
     probes = [int(x) for x in os.environ.get("LAGW_PROBES", "0").split(",")]
     for pr in probes:
         os.environ["SGLM_LAGW_PROBE"] = str(pr)
