@@ -173,7 +173,7 @@ struct LagW2Smem {
 // buffer load whose range check supplies the zeros (raw rows past the end, occurrences past the
 // event's end), so no address is selected and the compiler's wait counts stay exact; the
 // per-occurrence address arithmetic is done once, by the thread that loads the occurrence.
-template <int MT, int NT, int WM, int WN, int NH, bool PRIO>
+template <int MT, int NT, int WM, int WN, int NH>
 __global__ void __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(2, 2)))
 lag_gram_w2_kernel(LagW2Args a) {
     using SM = LagW2Smem<MT, NT, WM, WN, NH>;
@@ -435,9 +435,7 @@ lag_gram_w2_kernel(LagW2Args a) {
             if (ks + 1 < kKS2 / 16)
                 fetch(ks + 1, wq[(ks + 1) & 1], t1[(ks + 1) & 1], t2[(ks + 1) & 1]);
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
             mult(wq[ks & 1], t1[ks & 1], t2[ks & 1]);
-            if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
             __builtin_amdgcn_sched_barrier(0);
         }
     };
@@ -777,11 +775,9 @@ int launch_lagw2(const LagW2Args& a0, hipStream_t s, LagwSplit& sp) {
     hipMalloc(&a.trace, (size_t)nblk * 32);
     hipMemsetAsync(a.trace, 0, (size_t)nblk * 32, s);
 #endif
-    const char* e = getenv("SGLM_LAGW_PRIO");           // read per launch (A/B)
-    if (!(e && e[0] == '1'))
-        lag_gram_w2_kernel<MT, NT, WM, WN, NH, false><<<dim3(nblk), 64 * WM * WN, 0, s>>>(a);
-    else
-        lag_gram_w2_kernel<MT, NT, WM, WN, NH, true><<<dim3(nblk), 64 * WM * WN, 0, s>>>(a);
+    // (MFMA bursts at raised wave priority, s_setprio 1: no gain, 0.848 / 0.890 vs 0.893 / 0.886
+    // ms per 5-fit call on one box)
+    lag_gram_w2_kernel<MT, NT, WM, WN, NH><<<dim3(nblk), 64 * WM * WN, 0, s>>>(a);
 #ifdef SGLM_LAGW_TRACE
     {
         static int seq = 0;
