@@ -149,6 +149,7 @@ struct LagW2Args {
     // half -> H, 2 the second half -> Hb; lag_gram_w_sym adds the two, first + second, so the
     // result is deterministic).  njobs == 0: block b runs piece type b / m whole.
     int32_t njobs;
+    int32_t ms;                     // blocks per job (= m)
     uint16_t jobs[256];
 #ifdef SGLM_LAGW_TRACE
     uint64_t* trace;                // probe build: per block start / end clock, hardware slot, job
@@ -189,15 +190,16 @@ lag_gram_w2_kernel(LagW2Args a) {
     const uint64_t t_beg = __builtin_amdgcn_s_memrealtime();
 #endif
     const int blk = blockIdx.x;
-    const int a1 = blk % a.m;
+    const int a1 = blk % a.ms;
+    if (a1 >= a.m) return;
     int type, half = 0;
     if (a.njobs > 0) {
-        if (blk >= a.njobs * a.m) return;
-        const int jb = a.jobs[blk / a.m];
+        if (blk >= a.njobs * a.ms) return;
+        const int jb = a.jobs[blk / a.ms];
         type = jb & 0x3fff;
         half = jb >> 14;
     } else {
-        type = blk / a.m;
+        type = blk / a.ms;
         if (type >= a.Gm * a.Gy) return;
     }
     const int g = type % a.Gm, y = type / a.Gm;
@@ -762,14 +764,20 @@ int launch_lagw2(const LagW2Args& a0, hipStream_t s, LagwSplit& sp) {
     sp.Gm = a.Gm;
     sp.nf = a.nf;
     std::memcpy(sp.mask, pl.mask, sizeof(sp.mask));
+    // (Rounding the blocks per job up to a multiple of 8, so that every piece of an event -- its
+    // d groups, column blocks and halves, which stream the same weight rows -- lands on one
+    // XCD's L2 (block b -> XCD b mod 8): HBM reads 1294 -> 1133 MB per launch, but the XCDs'
+    // fixed event sets unbalance the launch: 5-fit call 0.854 -> 0.930 ms, 1-fit 0.312 -> 0.407
+    // ms.  Dropped.)
+    a.ms = a.m;
     unsigned nblk;
     if (pl.njobs > 0) {
         a.njobs = pl.njobs;
         std::memcpy(a.jobs, pl.jobs, sizeof(a.jobs));
-        nblk = (unsigned)(pl.njobs * a.m);
+        nblk = (unsigned)(pl.njobs * a.ms);
     } else {
         a.njobs = 0;
-        nblk = (unsigned)(a.Gm * a.Gy * a.m);
+        nblk = (unsigned)(a.Gm * a.Gy * a.ms);
     }
 #ifdef SGLM_LAGW_TRACE
     hipMalloc(&a.trace, (size_t)nblk * 32);
