@@ -1053,7 +1053,8 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
-    from sglm_hip import engine as E, folds, grid, synth
+    import ctypes
+    from sglm_hip import _lib, engine as E, folds, grid, synth
     from sglm_hip.estimators import Objective
 
     N, m, L, K, nlam = CONFIGS[a.config]
@@ -1090,6 +1091,11 @@ def main():
     stats = E.IrlsStats(record=True)
     if world > 1:
         dist.barrier()
+    # the structured Gram's kernel launches bracketed by HIP events inside the library (the
+    # roofline divides by the kernel's own time, as rocprofv3 reports it)
+    ktimer = E._lagw(design) is not None
+    if ktimer:
+        _lib.call("sglm_lag_gram_w_timing", 1, None, None)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
@@ -1098,10 +1104,18 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    # roofline of the dominant kernel (Gram) from HIP events on the launch stream
+    # roofline of the dominant kernel (Gram) from HIP events on the launch stream: the whole
+    # Gram call (the engine's events) and, for the structured Gram, the kernel alone
     ktime = sum(e0.elapsed_time(e1) for e0, e1, _, _ in stats.syrk_events) / 1e3
     kflop = sum(nact_flop for _, _, _, nact_flop in stats.syrk_events)
     nlaunch = len(stats.syrk_events)
+    call_ms = ktime / max(nlaunch, 1) * 1e3
+    if ktimer:
+        kms, kn = ctypes.c_double(0.0), ctypes.c_int32(0)
+        _lib.call("sglm_lag_gram_w_timing", 2, ctypes.byref(kms), ctypes.byref(kn))
+        _lib.call("sglm_lag_gram_w_timing", 0, None, None)
+        if kn.value > 0:
+            ktime, nlaunch = kms.value / 1e3, kn.value
     alg_bytes = float(np.mean(stats.syrk_bytes)) if stats.syrk_bytes else None
     exec_flop = float(np.sum(stats.syrk_exec)) if stats.syrk_exec else None
     t = torch.tensor([elapsed, float(stats.fit_iters), ktime, kflop, float(nlaunch),
@@ -1264,6 +1278,10 @@ def main():
                                             else None,
                 "launches": nlaunch,
                 "avg_launch_ms": ktime / max(nlaunch, 1) * 1e3,
+                "timed": ("the kernel alone (HIP events around each lag_gram_w2_kernel launch "
+                          "inside the library, sglm_lag_gram_w_timing)" if ktimer else
+                          "the Gram call (HIP events on its stream)"),
+                "call_avg_ms": call_ms,
                 # the event-structured Gram executes more MFMA work than its algorithmic
                 # products (G entries that are no H entry, 32-row / 32-column padding)
                 "executed_frac": (exec_flop / ktime / 1e12 / PEAK_BF16_TFLOPS

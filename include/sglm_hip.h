@@ -214,6 +214,10 @@ int sglm_lag_gram_w(const uint64_t* R, const int32_t* occ, const int32_t* ev_off
  * row (~16 B per raw row per fit -- the engine splits large launches to bound it) and a P x P
  * f32 image per fit for the second halves of the pieces a launch splits (load balance) */
 size_t sglm_lag_gram_w_work_bytes(int32_t nraw, int32_t K, int32_t nf, int32_t P);
+/* Measurement hook (no reference counterpart): mode 1 clears and starts bracketing every
+ * structured-Gram kernel launch with HIP events on its stream, mode 2 waits for the recorded
+ * launches and returns their summed kernel time (ms) and count, then clears, mode 0 stops. */
+int sglm_lag_gram_w_timing(int32_t mode, double* ms, int32_t* n);
 
 /* Row words of m <= 63 events: R[u] bit a = e_a(u) (ebits[m][nwords], bit u & 31 of word
  * u >> 5), bit m = 1, for u < nraw. */

@@ -747,6 +747,25 @@ static LagwPlan lagw_plan(int m, int K, int nf, int NH, int MT, int NT, int WM, 
     return cache[key] = pl;
 }
 
+// Kernel-only timing (sglm_lag_gram_w_timing): while on, every lag_gram_w2_kernel launch is
+// bracketed by two HIP events on its stream -- the bench's roofline divides by exactly the
+// kernel's time, the figure rocprofv3 reports for it (the call also holds the weight copies, the
+// ones sum and the symmetrize pass).  Events come from a pool; nothing is timed while off.
+std::mutex g_tmu;
+bool g_ton = false;
+std::vector<hipEvent_t> g_tpool;
+std::vector<std::pair<hipEvent_t, hipEvent_t>> g_trec;
+
+hipEvent_t lagw_event() {
+    if (!g_tpool.empty()) {
+        hipEvent_t e = g_tpool.back();
+        g_tpool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    return hipEventCreate(&e) == hipSuccess ? e : nullptr;
+}
+
 template <int MT, int NT, int WM, int WN, int NH>
 int launch_lagw2(const LagW2Args& a0, hipStream_t s, LagwSplit& sp) {
     LagW2Args a = a0;
@@ -785,7 +804,21 @@ int launch_lagw2(const LagW2Args& a0, hipStream_t s, LagwSplit& sp) {
 #endif
     // (MFMA bursts at raised wave priority, s_setprio 1: no gain, 0.848 / 0.890 vs 0.893 / 0.886
     // ms per 5-fit call on one box)
+    hipEvent_t t0 = nullptr, t1 = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_tmu);
+        if (g_ton) {
+            t0 = lagw_event();
+            t1 = lagw_event();
+        }
+    }
+    if (t0 && t1) (void)hipEventRecord(t0, s);
     lag_gram_w2_kernel<MT, NT, WM, WN, NH><<<dim3(nblk), 64 * WM * WN, 0, s>>>(a);
+    if (t0 && t1) {
+        (void)hipEventRecord(t1, s);
+        std::lock_guard<std::mutex> lk(g_tmu);
+        g_trec.push_back({t0, t1});
+    }
 #ifdef SGLM_LAGW_TRACE
     {
         static int seq = 0;
@@ -878,6 +911,33 @@ extern "C" int sglm_lag_gram_w(const uint64_t* R, const int32_t* occ, const int3
         H, fits, P, p, m, K, layout, shifts, sp);
     lag_gram_w_aux<<<dim3(1, (unsigned)nf), 256, 0, s>>>(part, fits, H, P, p);
     return check_launch("lag_gram_w_aux");
+}
+
+extern "C" int sglm_lag_gram_w_timing(int32_t mode, double* ms, int32_t* n) {
+    std::lock_guard<std::mutex> lk(g_tmu);
+    if (mode == 0) {
+        g_ton = false;
+        return SGLM_OK;
+    }
+    double tot = 0.0;
+    int cnt = 0;
+    for (auto& pr : g_trec) {
+        if (mode == 2) {
+            float x = 0.0f;
+            if (hipEventSynchronize(pr.second) == hipSuccess &&
+                hipEventElapsedTime(&x, pr.first, pr.second) == hipSuccess) {
+                tot += x;
+                ++cnt;
+            }
+        }
+        g_tpool.push_back(pr.first);
+        g_tpool.push_back(pr.second);
+    }
+    g_trec.clear();
+    if (mode == 1) g_ton = true;
+    if (ms) *ms = tot;
+    if (n) *n = cnt;
+    return SGLM_OK;
 }
 
 // R[u] = sum_a bit(e_a(u)) << a | 1 << m from the occurrence bitmaps ebits[m][nwords]

@@ -120,6 +120,7 @@ SIGNATURES = {
     "sglm_lag_xtr_work_bytes": (_sz, [_i32, _i32, _i32, _i64]),
     "sglm_lag_gram_work_bytes": (_sz, [_i32, _i32, _i32]),
     "sglm_lag_gram_w_work_bytes": (_sz, [_i32, _i32, _i32, _i32]),
+    "sglm_lag_gram_w_timing": (C.c_int, [_i32, _vp, _vp]),
     "sglm_xtr_prefer": (C.c_int, [_i32]),
     "sglm_lag_gram": (C.c_int, [_vp, _vp, _vp, _i64, _vp, _i32, _i32, _i32, _i32, _i32, _i64,
                                 _i64, _i64, _i32, _vp, _i64, _vp, _i32, _vp, _vp, _vp]),
