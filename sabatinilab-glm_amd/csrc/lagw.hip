@@ -384,15 +384,6 @@ lag_gram_w2_kernel(LagW2Args a) {
         };
         auto mult = [&](const u32x4 (&wq)[MT], const s16x4 (&t1)[NT], const s16x4 (&t2)[NT])
                         __attribute__((always_inline)) {
-#if defined(SGLM_LAGW_PROBE) && SGLM_LAGW_PROBE == 2
-            // timing probe: fragments read and consumed by one add, no expansion, no MFMA
-#pragma unroll
-            for (int i = 0; i < MT; ++i)
-#pragma unroll
-                for (int j = J0; j <= J1; ++j)
-                    acc[i][j][0] += __builtin_bit_cast(float, wq[i][0] ^ __builtin_bit_cast(uint2, t1[j]).x ^ __builtin_bit_cast(uint2, t2[j]).y);
-            return;
-#endif
             bf16x8 bq[NT];
 #pragma unroll
             for (int j = J0; j <= J1; ++j) {
@@ -416,18 +407,16 @@ lag_gram_w2_kernel(LagW2Args a) {
                                                                         0, 0, 0);
         };
         auto staging = [&](int ks) __attribute__((always_inline)) {
-#if defined(SGLM_LAGW_PROBE) && SGLM_LAGW_PROBE == 1
-            return;                                  // timing probe: no staging in the loop
-#endif
             if (ks < kWT) store_w(buf ^ 1, ks);
             if (ks == kWT) store_r(buf ^ 1);
             if (ks == 4) occ_load(s + 4);
             if (ks >= 4 && ks - 4 < kWT) load_w(s + 2, ks - 4);
             if (ks == 7) load_r(s + 2);
         };
-        // the fragments of K-step ks + 1 are read while the MFMAs of ks run (in-grid 0.598 ->
-        // ~0.52 ms per launch together with the staging rework; hipcc sinks the reads to their
-        // MFMAs unless the scheduling barriers hold them ahead)
+        // the fragments of K-step ks + 1 are read while the MFMAs of ks run (hipcc sinks the
+        // reads to their MFMAs unless the scheduling barriers hold them ahead).  (Three buffers
+        // with the barrier after the stores and the next stage's first fragments read during
+        // K-step 7 -- no stage starting on an LDS round trip -- spilled 150+ VGPRs; not kept.)
         u32x4 wq[2][MT];
         s16x4 t1[2][NT], t2[2][NT];
         fetch(0, wq[0], t1[0], t2[0]);
