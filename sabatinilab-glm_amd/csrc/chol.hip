@@ -19,6 +19,7 @@
 // triangular solves run (chol_fwd2 / chol_back2).
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <vector>
@@ -663,6 +664,108 @@ __global__ void __launch_bounds__(kCT) chol_inv_level_lds_kernel(const float* __
     }
 }
 
+// Block column J of M = U^-1, left-looking (round 6):
+//     M[I][J] = -(sum_{k=I}^{J-1} M[I][k] U[k][J]) M[J][J]      for the row blocks I < J,
+// one 64 x 64 tile per workgroup (blockIdx.x = I), the product staged exactly as in
+// chol_inv_level_lds_kernel, then the tile times the diagonal block's inverse M[J][J] (written
+// by the diagonal step; exact zeros below its diagonal and in the columns of dropped pivots, so
+// frozen columns of M stay zero).  Everything it reads is final once block J is factored: U's
+// block rows k < J after their panel steps, M's columns < J from the launches for J' < J.  So
+// the chain launches it on a branch of its own right after the launch that factored block J,
+// beside the rest of the factorisation, and only the last column follows the chain (the
+// recursive-doubling levels all ran after it: 0.12 ms at one fit, 0.88 ms at 20).
+__global__ void __launch_bounds__(kCT) chol_inv_col_kernel(const float* __restrict__ Hall,
+                                                           float* __restrict__ Mall, int32_t P,
+                                                           int32_t J,
+                                                           const int32_t* __restrict__ fits) {
+    __shared__ __attribute__((aligned(16))) float sa[2][64 * kLA];
+    __shared__ __attribute__((aligned(16))) float sb[2][32 * kLB];
+    const int fit = fits[blockIdx.y];
+    const float* H = Hall + (int64_t)fit * P * P;
+    float* M = Mall + (int64_t)fit * P * P;
+    const int ti = blockIdx.x;
+    if (ti >= J) return;
+    const int c0 = J * kNB;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r32 = lane & 31, kh = lane >> 5;
+    const int wr = wave >> 1, wc = wave & 1;
+    // A = M[ti rows][k], B = U[k][c0 + j] (H's upper triangle), k in [64 ti, 64 J)
+    const float* ga = M + (int64_t)(ti * kNB) * P;
+    const float* gb = H + c0;
+    const int klo = ti * kNB, khi = c0;
+    const int ar = tid >> 2, ak = 8 * (tid & 3);
+    const int bk = tid >> 3, bj = 8 * (tid & 7);
+    f32x4 ra0, ra1, rb0, rb1;
+    auto gload = [&](int kb) {
+        const float* pa = ga + (int64_t)ar * P + kb + ak;
+        ra0 = *reinterpret_cast<const f32x4*>(pa);
+        ra1 = *reinterpret_cast<const f32x4*>(pa + 4);
+        const float* pb = gb + (int64_t)(kb + bk) * P + bj;
+        rb0 = *reinterpret_cast<const f32x4*>(pb);
+        rb1 = *reinterpret_cast<const f32x4*>(pb + 4);
+    };
+    auto sstore = [&](int buf) {
+        *reinterpret_cast<f32x4*>(&sa[buf][ar * kLA + ak]) = ra0;
+        *reinterpret_cast<f32x4*>(&sa[buf][ar * kLA + ak + 4]) = ra1;
+        *reinterpret_cast<f32x4*>(&sb[buf][bk * kLB + bj]) = rb0;
+        *reinterpret_cast<f32x4*>(&sb[buf][bk * kLB + bj + 4]) = rb1;
+    };
+    f32x16 acc = {};
+    gload(klo);
+    sstore(0);
+    __syncthreads();
+    int cur = 0;
+    for (int kb = klo; kb < khi; kb += 32) {
+        const bool more = kb + 32 < khi;
+        if (more) gload(kb + 32);
+        const float* A = &sa[cur][(wr * 32 + r32) * kLA + 4 * kh];
+        const float* Bq = &sb[cur][(4 * kh) * kLB + wc * 32 + r32];
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const f32x4 a = *reinterpret_cast<const f32x4*>(A + 8 * kk);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], Bq[(8 * kk + u) * kLB], acc, 0,
+                                                           0, 0);
+        }
+        if (more) sstore(cur ^ 1);
+        __syncthreads();
+        cur ^= 1;
+    }
+    // the tile Y (rows wr 32 .., columns wc 32 .. per wave) into LDS as the A operand of the
+    // second product, M[J][J] as its B operand (64 rows over the two B buffers)
+    constexpr int kLY = 68;
+    float* sy = &sa[0][0];
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+        sy[(wr * 32 + (q & 3) + 8 * (q >> 2) + 4 * kh) * kLY + wc * 32 + r32] = acc[q];
+    {
+        const int k = tid >> 2, cq = 16 * (tid & 3);
+        const float* pm = M + (int64_t)(c0 + k) * P + c0 + cq;
+        float* dst = &sb[0][0] + k * kLB + cq;
+#pragma unroll
+        for (int e = 0; e < 16; e += 4)
+            *reinterpret_cast<f32x4*>(dst + e) = *reinterpret_cast<const f32x4*>(pm + e);
+    }
+    __syncthreads();
+    f32x16 z = {};
+    const float* A = sy + (wr * 32 + r32) * kLY + 4 * kh;
+    const float* Bq = &sb[0][0] + (4 * kh) * kLB + wc * 32 + r32;
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(A + 8 * kk);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            z = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], Bq[(8 * kk + u) * kLB], z, 0, 0, 0);
+    }
+    const int i0 = ti * kNB + wr * 32, j0 = c0 + wc * 32;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int i = i0 + (q & 3) + 8 * (q >> 2) + 4 * kh;
+        M[(int64_t)i * P + j0 + r32] = -z[q];
+    }
+}
+
 // The same level on 128 x 128 output tiles (levels with s >= 128 when enough fits fill the
 // chip): four waves of 64 x 64 (2 x 2 quadrants of v_mfma_f32_32x32x2f32), K in blocks of
 // 16 staged through double-buffered LDS (37 KB: static LDS stays under 64 KB) -- half the
@@ -1023,7 +1126,8 @@ static void launch_update(dim3 grid, hipStream_t s, float* H, int32_t P, int32_t
 static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t nact,
                             int32_t nrefac, const double* g, const float* dshift, float* delta,
                             int32_t* info, uint8_t* frozen, int32_t B, void* work,
-                            hipStream_t s, float* Mall = nullptr) {
+                            hipStream_t s, float* Mall = nullptr,
+                            const std::function<void(int)>* on_diag = nullptr) {
     if (nact <= 0) return SGLM_OK;
     if (!H || !fits || (!g && !Mall) || !dshift || !delta || !info || !frozen || !work ||
         P % kNB || P > kMaxP || B < nact || nrefac < 0 || nrefac > nact) {
@@ -1070,6 +1174,7 @@ static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t na
             launch_chol_diag4(nact, s, H, P, k0, fits, frozen, dg, info, minv, Mall);
         else
             launch_chol_diag(nact, s, H, P, k0, fits, frozen, rhs, dg, info, nrefac, minv, Mall);
+        if (!have_diag && on_diag) (*on_diag)(kb);        // block kb factored by this launch
         const int rem = P - k0 - kNB;
         if (rem > 0)
             chol_panel_kernel<<<dim3(nact, rem / kNB), kCT, 0, s>>>(H, P, k0, fits, minv, rhs,
@@ -1090,6 +1195,7 @@ static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t na
                     launch_chol_update_diag4l(g, s, H, P, b * kNB, kNB, b + 1, fits, frozen, dg,
                                               info, minv, Mall);
                     have_diag = true;
+                    if (on_diag) (*on_diag)(b + 1);
                 } else {
                     launch_update(g, s, H, P, b * kNB, kNB, b + 1, fits);
                 }
@@ -1102,6 +1208,7 @@ static int chol_solve_mixed(float* H, int32_t P, const int32_t* fits, int32_t na
                 launch_chol_update_diag4l(g, s, H, P, kb * kNB, (ke - kb) * kNB, ke, fits, frozen,
                                           dg, info, minv, Mall);
                 have_diag = true;
+                if (on_diag) (*on_diag)(ke);
             } else {
                 launch_update(g, s, H, P, kb * kNB, (ke - kb) * kNB, ke, fits);
             }
@@ -1156,11 +1263,77 @@ extern "C" int sglm_chol_solve_mixed(float* H, int32_t P, const int32_t* fits, i
 }
 
 
-// The factorisation + inversion chain (~110 launches) of fits[0 .. n).
+// The inverse by left-looking block columns beside the factorisation (chol_inv_col_kernel);
+// opt-in, SGLM_INV_COL=1 (read per chain capture; part of the chain-graph key).  Measured
+// slower than the recursive-doubling levels after the chain (tools/chol_bench.py, one box,
+// profiles/r06_inv_col_ab.json): chain of 1 / 3 / 11 / 20 representatives 0.95 / 1.13 / 1.92 /
+// 2.83 -> 1.18 / 1.31 / 2.01 / 2.80 ms, C4 grid 34.2 -> 37.3 ms.  A column's longest tile runs
+// K = 64 J serially (~40 us at J = 31), longer than a block step of the chain, so the branch
+// falls behind and its last columns trail the chain by ~3 columns; at 20 fits the columns'
+// work competes with the chain's group-end updates instead of filling idle CUs.
+static bool inv_col() {
+    const char* e = getenv("SGLM_INV_COL");
+    return e && e[0] == '1';
+}
+
+// The branch the inverse columns run on: one stream and a set of events per host thread and
+// device, created before any capture begins (a chain captured on stream s forks onto it at
+// each factored block and joins back at its end, so the graph holds both branches).
+struct InvColCtx {
+    hipStream_t s2 = nullptr;
+    std::vector<hipEvent_t> ev;
+};
+
+static InvColCtx* inv_col_ctx(int nev) {
+    thread_local std::map<int, InvColCtx> ctxs;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    InvColCtx& c = ctxs[dev];
+    if (!c.s2 && hipStreamCreateWithFlags(&c.s2, hipStreamNonBlocking) != hipSuccess) {
+        c.s2 = nullptr;
+        return nullptr;
+    }
+    while ((int)c.ev.size() < nev) {
+        hipEvent_t e = nullptr;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+        c.ev.push_back(e);
+    }
+    return &c;
+}
+
+// The factorisation + inversion chain (~110 launches) of fits[0 .. n).  ctx: the inverse
+// columns' branch (inv_col), or null for the recursive-doubling levels after the chain.
 static int factor_inv_launch(float* H, float* Minv, int32_t P, const int32_t* fits, int32_t n,
                              const float* dshift, float* delta, int32_t* info, uint8_t* frozen,
-                             int32_t B, void* work, hipStream_t s) {
+                             int32_t B, void* work, hipStream_t s, InvColCtx* ctx = nullptr) {
     int st;
+    if (ctx) {
+        int nev = 0, st2 = SGLM_OK;
+        const std::function<void(int)> hook = [&](int J) {
+            if (J <= 0 || st2 != SGLM_OK) return;
+            const hipEvent_t e = ctx->ev[nev++];
+            if (hipEventRecord(e, s) != hipSuccess || hipStreamWaitEvent(ctx->s2, e, 0) != hipSuccess) {
+                set_error("chol inverse columns: fork failed");
+                st2 = SGLM_EHIP;
+                return;
+            }
+            chol_inv_col_kernel<<<dim3((unsigned)J, (unsigned)n), kCT, 0, ctx->s2>>>(H, Minv, P, J,
+                                                                                  fits);
+        };
+        st = chol_solve_mixed(H, P, fits, n, n, nullptr, dshift, delta, info, frozen, B, work, s,
+                              Minv, &hook);
+        if (nev > 0) {                       // join the branch back (also after an error)
+            const hipEvent_t e = ctx->ev[nev];
+            if ((hipEventRecord(e, ctx->s2) != hipSuccess || hipStreamWaitEvent(s, e, 0) != hipSuccess)
+                && !st && !st2) {
+                set_error("chol inverse columns: join failed");
+                st2 = SGLM_EHIP;
+            }
+        }
+        if (st) return st;
+        if (st2) return st2;
+        return check_launch("chol_inv_col_kernel");
+    }
     if ((st = chol_solve_mixed(H, P, fits, n, n, nullptr, dshift, delta, info, frozen, B, work, s,
                                Minv)))
         return st;
@@ -1297,26 +1470,30 @@ extern "C" int sglm_chol_graph_cache_clear(void) {
 
 static int factor_inv_cached(float* H, float* Minv, int32_t P, const int32_t* fits, int32_t n,
                              const float* dshift, float* delta, int32_t* info, uint8_t* frozen,
-                             int32_t B, void* work, hipStream_t s);
+                             int32_t B, void* work, hipStream_t s, InvColCtx* ctx);
 
 static int factor_inv(float* H, float* Minv, int32_t P, const int32_t* fits, int32_t n,
                       const float* dshift, float* delta, int32_t* info, uint8_t* frozen,
                       int32_t B, void* work, hipStream_t s) {
+    // (every diagonal-step variant writes its block of M, which the columns read)
+    InvColCtx* ctx = inv_col() ? inv_col_ctx(P / kNB + 1) : nullptr;
     if (!chol_graphs_enabled() || s == nullptr)      // the null stream cannot be captured
-        return factor_inv_launch(H, Minv, P, fits, n, dshift, delta, info, frozen, B, work, s);
-    const int st = factor_inv_cached(H, Minv, P, fits, n, dshift, delta, info, frozen, B, work, s);
+        return factor_inv_launch(H, Minv, P, fits, n, dshift, delta, info, frozen, B, work, s,
+                                 ctx);
+    const int st = factor_inv_cached(H, Minv, P, fits, n, dshift, delta, info, frozen, B, work, s,
+                                     ctx);
     chain_pending_reap(false);                        // evicted chains that finished, unlocked
     return st;
 }
 
 static int factor_inv_cached(float* H, float* Minv, int32_t P, const int32_t* fits, int32_t n,
                              const float* dshift, float* delta, int32_t* info, uint8_t* frozen,
-                             int32_t B, void* work, hipStream_t s) {
+                             int32_t B, void* work, hipStream_t s, InvColCtx* ctx) {
     ChainKey key;
     std::memset(&key, 0, sizeof(key));
     key.H = H; key.Minv = Minv; key.fits = fits; key.dshift = dshift; key.delta = delta;
     key.info = info; key.frozen = frozen; key.work = work;
-    key.P = P; key.n = n; key.B = B; key.la = chol_lookahead(); key.q = diag4q() ? (diag4l() ? (upd_diag() ? 3 : 2) : 1) : 0;
+    key.P = P; key.n = n; key.B = B; key.la = chol_lookahead(); key.q = (diag4q() ? (diag4l() ? (upd_diag() ? 3 : 2) : 1) : 0) | (ctx ? 4 : 0);
     // the lock is held across capture and launch: a concurrent eviction must not destroy the
     // entry between lookup and launch (captures are thread-local, so nothing else is stalled
     // but other chains' host enqueue, which is short next to the chain itself)
@@ -1329,7 +1506,7 @@ static int factor_inv_cached(float* H, float* Minv, int32_t P, const int32_t* fi
             return SGLM_EHIP;
         }
         const int st = factor_inv_launch(H, Minv, P, fits, n, dshift, delta, info, frozen, B,
-                                         work, s);
+                                         work, s, ctx);
         const hipError_t ec = hipStreamEndCapture(s, &graph);
         if (st) {
             if (graph) (void)hipGraphDestroy(graph);

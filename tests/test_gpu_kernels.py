@@ -288,6 +288,68 @@ def test_chol_diag_four_pivots_equals_two(engine, torch_mod, P, p, monkeypatch):
             assert np.array_equal(a, b, equal_nan=True), v
 
 
+@pytest.mark.parametrize("P,p,graph", [(192, 150, False), (2048, 1990, False), (2048, 1990, True)])
+def test_chol_inv_columns_equal_levels(engine, torch_mod, P, p, graph, monkeypatch):
+    """The inverse by left-looking block columns on a branch beside the factorisation
+    (chol_inv_col_kernel, SGLM_INV_COL=1, the default) leaves the factor, frozen set and drop
+    count bit for bit as the recursive-doubling levels after the chain (SGLM_INV_COL=0), and
+    the same inverse to f32 rounding (zeros in the frozen and dropped columns): a dependent
+    column, a frozen coordinate, three fits, on the null stream (direct launches) and on a
+    stream (the cached chain graph with its two branches)."""
+    torch = torch_mod
+    from sglm_hip import _lib
+    rng = np.random.default_rng(P + 11)
+    B = 3
+    H = np.zeros((B, P, P), np.float32)
+    for k in range(B):
+        A = rng.normal(size=(p + 300, p + 1))
+        A[:, 5] = A[:, 9]                                # dependent column
+        H[k, : p + 1, : p + 1] = A.T @ A / 100.0
+    dsh = np.full((B, P), -1.0, np.float32)
+    dsh[:, :p] = rng.uniform(0.0, 0.5, size=(B, 1))
+    dsh[:, p] = 0.0
+    dsh[:, [5, 9]] = 0.0                                 # unpenalised: pivot 9 drops
+    dsh[:, 17] = -1.0                                    # frozen
+    outs = {}
+    st = torch.cuda.Stream() if graph else None
+    for v in ("1", "0", "1"):
+        monkeypatch.setenv("SGLM_INV_COL", v)
+        Hd = torch.from_numpy(H).cuda()
+        Md = torch.zeros_like(Hd)
+        out = torch.zeros((B, P), dtype=torch.float32, device="cuda")
+        info = torch.zeros(B, dtype=torch.int32, device="cuda")
+        frozen = torch.zeros((B, P), dtype=torch.uint8, device="cuda")
+        dshd = torch.from_numpy(dsh).cuda()
+        cw = torch.empty(_lib.query("sglm_chol_work_bytes", P, B), dtype=torch.uint8,
+                         device="cuda")
+        lst = torch.arange(B, dtype=torch.int32, device="cuda")
+        rs = torch.ones(B, dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        _lib.call("sglm_chol_solve_inv", Hd.data_ptr(), Md.data_ptr(), P, lst.data_ptr(),
+                  lst.data_ptr(), rs.data_ptr(), B, B, None, 0, None, dshd.data_ptr(),
+                  out.data_ptr(), info.data_ptr(), frozen.data_ptr(), B, cw.data_ptr(),
+                  st.cuda_stream if graph else 0)
+        torch.cuda.synchronize()
+        res = [t.cpu().numpy() for t in (Hd, Md, info, frozen)]
+        if v in outs:                                    # a replay (graph) is deterministic
+            for a, b in zip(res, outs[v]):
+                assert np.array_equal(a, b, equal_nan=True)
+        outs[v] = res
+    (Hc, Mc, ic, fc), (Hl, Ml, il, fl) = outs["1"], outs["0"]
+    assert (ic >= 1).all() and np.array_equal(ic, il) and np.array_equal(fc, fl)
+    up = np.triu(np.ones((P, P), bool))
+    assert np.array_equal(Hc[:, up], Hl[:, up])          # the factor is untouched
+    for k in range(B):
+        Uc, Ul = np.triu(Mc[k]).astype(np.float64), np.triu(Ml[k]).astype(np.float64)
+        assert np.linalg.norm(Uc - Ul) <= 1e-5 * np.linalg.norm(Ul), k
+        dead = fc[k].astype(bool)
+        assert np.all(Mc[k][:, dead][up[:, dead]] == 0)  # frozen / dropped columns of M
+        U = np.triu(Hc[k]).astype(np.float64)
+        keep = np.flatnonzero(~dead)
+        Iu = Uc[np.ix_(keep, keep)] @ U[np.ix_(keep, keep)]
+        assert np.abs(Iu - np.eye(keep.size)).max() < 1e-3, k
+
+
 @pytest.mark.parametrize("P,p,B", [(768, 700, 6), (2048, 1990, 5)])
 def test_chol_inv_many_fits_vs_float64(engine, torch_mod, P, p, B, monkeypatch):
     """Factor + inverse chain on several fits of their own with the 128 x 128 inversion tiles
