@@ -150,6 +150,7 @@ struct LagW2Args {
     // result is deterministic).  njobs == 0: block b runs piece type b / m whole.
     int32_t njobs;
     int32_t ms;                     // blocks per job (= m)
+    int32_t wsh;                    // 1: a piece's column window starts at its first d row
     uint16_t jobs[256];
 #ifdef SGLM_LAGW_TRACE
     uint64_t* trace;                // probe build: per block start / end clock, hardware slot, job
@@ -207,7 +208,10 @@ lag_gram_w2_kernel(LagW2Args a) {
     const int t0 = g * MB;
     if (t0 >= Tm) return;
     const int di0 = t0 / NH;
-    const int n0 = y * NN;
+    // the piece's column window starts at its first d row's first live column (shift smin + di0,
+    // fit 0): the columns below hold no H entry for any of its rows (round 6: 1-fit launches
+    // issue a third fewer MFMAs, 5-fit ones 8 %)
+    const int n0 = y * NN + a.wsh * di0 * a.nf;
     // a G entry of row d and a column of shift smin + sb is an H entry only when sb >= d (its
     // second shift smin + sb - d is then a column): a piece whose columns all precede its d rows
     // has nothing to store
@@ -533,7 +537,7 @@ lag_gram_w2_kernel(LagW2Args a) {
 // half of a2, the (shift, fit) column of (s1, f).
 struct LagwSplit {
     const float* Hb;                // null: nothing split
-    int32_t smin, nh, MB, NN, Gm, nf;
+    int32_t smin, nh, MB, NN, Gm, nf, wsh;
     uint32_t mask[8];               // bit t: piece type t split
 };
 
@@ -573,8 +577,10 @@ __global__ void __launch_bounds__(256) lag_gram_w_sym(float* __restrict__ H,
         if (!Hbf) return false;
         const int s1 = kr / 64 - 65536, s2 = kc / 64 - 65536;
         const int tau = (s1 - s2) * sp.nh + a2 / 32;
-        const int y = ((s1 - sp.smin) * sp.nf + (int)blockIdx.y) / sp.NN;
-        const int t = tau / sp.MB + sp.Gm * y;
+        const int g = tau / sp.MB;                       // its piece: d group, column block
+        const int y = ((s1 - sp.smin - sp.wsh * (g * sp.MB / sp.nh)) * sp.nf + (int)blockIdx.y) /
+                      sp.NN;
+        const int t = g + sp.Gm * y;
         return (sp.mask[t >> 5] >> (t & 31)) & 1u;
     };
     // stage H rows J*64.., columns I*64.. (the lower counterpart), and Hb's when split
@@ -642,12 +648,12 @@ static int lagw_cus() {
 }
 
 static LagwPlan lagw_plan(int m, int K, int nf, int NH, int MT, int NT, int WM, int Gm, int Gy,
-                          bool can_split) {
+                          bool can_split, int wsh) {
     static std::mutex mu;
     static std::map<std::vector<int>, LagwPlan> cache;
     const char* e = getenv("SGLM_LAGW_SPLIT");          // read per launch (A/B, tests)
     const bool sp_ok = can_split && !(e && e[0] == '0');
-    const std::vector<int> key{m, K, nf, NH, MT, NT, WM, Gm, Gy, sp_ok};
+    const std::vector<int> key{m, K, nf, NH, MT, NT, WM, Gm, Gy, sp_ok, wsh};
     std::lock_guard<std::mutex> lk(mu);
     auto it = cache.find(key);
     if (it != cache.end()) return it->second;
@@ -657,7 +663,7 @@ static LagwPlan lagw_plan(int m, int K, int nf, int NH, int MT, int NT, int WM, 
     std::vector<std::pair<double, int>> types;          // (cost, type), live types only
     for (int t = 0; t < per; ++t) {
         const int g = t % Gm, y = t / Gm;
-        const int t0 = g * MB, n0 = y * NN, di0 = t0 / NH;
+        const int t0 = g * MB, di0 = t0 / NH, n0 = y * NN + wsh * di0 * nf;   // the kernel's
         if (t0 >= Tm || n0 / nf >= K || std::min(K - 1, (n0 + NN - 1) / nf) < di0) continue;
         int simd[4] = {0, 0, 0, 0};
         for (int wm = 0; wm < WM; ++wm) {
@@ -762,7 +768,12 @@ int launch_lagw2(const LagW2Args& a0, hipStream_t s, LagwSplit& sp) {
     static_assert(WN == 1, "one wave column");
     a.Gm = (a.D * NH + MB - 1) / MB;
     a.Gy = (a.nf * a.K + NN - 1) / NN;
-    const LagwPlan pl = lagw_plan(a.m, a.K, a.nf, NH, MT, NT, WM, a.Gm, a.Gy, a.Hb != nullptr);
+    // (SGLM_LAGW_WSHIFT=0: every piece's window at column 0 of its block, the round-6 v3 tiling;
+    // read per launch, A/B)
+    const char* ew = getenv("SGLM_LAGW_WSHIFT");
+    a.wsh = (ew && ew[0] == '0') ? 0 : 1;
+    const LagwPlan pl = lagw_plan(a.m, a.K, a.nf, NH, MT, NT, WM, a.Gm, a.Gy, a.Hb != nullptr,
+                                  a.wsh);
     if (pl.njobs < 0) return SGLM_OK;
     sp.Hb = pl.split ? a.Hb : nullptr;
     sp.smin = a.smin;
@@ -771,6 +782,7 @@ int launch_lagw2(const LagW2Args& a0, hipStream_t s, LagwSplit& sp) {
     sp.NN = NN;
     sp.Gm = a.Gm;
     sp.nf = a.nf;
+    sp.wsh = a.wsh;
     std::memcpy(sp.mask, pl.mask, sizeof(sp.mask));
     // (Rounding the blocks per job up to a multiple of 8, so that every piece of an event -- its
     // d groups, column blocks and halves, which stream the same weight rows -- lands on one

@@ -112,6 +112,9 @@ CHOL_STREAM = __import__("os").environ.get("SGLM_CHOL_STREAM", "side")
 # correction extrapolates along the secant (C4: 9 -> 7 Newton iterations, 636 -> 589
 # fit-iterations, 51.4 -> 50.3 ms in one process; the fixed point is the exact gradient's)
 ANDERSON = __import__("os").environ.get("SGLM_ANDERSON", "1") == "1"
+# first iteration: link + gradient once per (mask, response, intercept) start key, the other
+# fits' gradient rows copied (bitwise the same values; round 6)
+GRAD_DEDUP = __import__("os").environ.get("SGLM_GRAD_DEDUP", "1") == "1"
 # gradient enqueued before the Hessian decisions' device wait when no Hessian is planned
 GRAD_FIRST = __import__("os").environ.get("SGLM_GRAD_FIRST", "1") == "1"
 # gradient kernel that co-resides with the factorisation chain in iterations that form factors
@@ -1364,6 +1367,7 @@ class IrlsStats:
     aliased: int = 0            # fit-iterations solved on a family representative's factor
     shared: int = 0             # fit-iterations on a lambda neighbour's Gram (own factor)
     lag_grams: int = 0          # Grams from the event cross-correlations (sglm_lag_gram)
+    grad_dedup: int = 0         # fit gradients copied from an identical start (GRAD_DEDUP)
     rank_grams: int = 0         # exact mask Grams for the rank decisions of unpenalised fits
     chain_host_s: float = 0.0   # host time spent enqueueing the factorisation chains
     aa_fit_iters: int = 0       # fit-iterations whose direction took the secant correction
@@ -1999,9 +2003,32 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
         else:
             act_d = linked if linked is not None else up(act, np.int32)
             grad_d, grad_n, grad_bp = act_d, na, pad_to(na, 32)
+        g_copy = None                        # (fits, their lead fits): gradient rows copied
+        link_d, link_n = act_d, na
+        if GRAD_DEDUP and use_rp and fused and not dev_linked and linked is None:
+            # fits still at their common start with one (mask, response, intercept) key
+            # (hkey) have one predictor, hence bitwise one W, R and X^T R: the link and the
+            # gradient run once per key and the other fits' gradient rows are copies (at C4:
+            # 6 of 120 fits in the first iteration, where the factorisation chain runs beside
+            # the gradient); nothing else reads a copied fit's W or R before its next link
+            lead_of, first = {}, {}
+            for k in act:
+                if fresh_start[k]:
+                    rk = first.setdefault(hkey(k), int(k))
+                    if rk != k:
+                        lead_of[int(k)] = rk
+            if lead_of:
+                lead = np.array([k for k in act if int(k) not in lead_of], dtype=np.int32)
+                link_d, link_n = up(lead, np.int32), int(lead.size)
+                grad_d, grad_n, grad_bp = link_d, link_n, pad_to(link_n, 32)
+                cp = up(np.array([[k, r] for k, r in lead_of.items()], np.int64).T.reshape(-1),
+                        np.int64)
+                g_copy = (cp[:len(lead_of)], cp[len(lead_of):])
+                if stats is not None:
+                    stats.grad_dedup += len(lead_of)
         if fused and not dev_linked:
             if linked is None:
-                _lib.call("sglm_link_update", fam, power, n, ld, na, _p(act_d), _p(bf.eta),
+                _lib.call("sglm_link_update", fam, power, n, ld, link_n, _p(link_d), _p(bf.eta),
                           _p(prob.Y), _p(prob.M), _p(fit_resp), _p(fit_mask), _p(bf.W), R_out,
                           Rp_out, None, None, st)
         else:
@@ -2037,6 +2064,8 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
                         _lib.call("sglm_xtr_prefer", -1)
                 # a mixed design's continuous coordinates, float64 from the same packed R
                 d.mix_xtr(2, rp_buf, ld, grad_bp, None, grad_d, grad_n, bf.g)
+                if g_copy is not None:
+                    bf.g[g_copy[0]] = bf.g[g_copy[1]]
             else:
                 d.xtr(bf.R, B, bf.g)
             if comm is not None:
@@ -3231,25 +3260,38 @@ def _lagw_pays(d: Design, lg, nact: int) -> bool:
 
 def _lagw_exec_flop(lg, nact: int) -> float:
     """MFMA flop the sglm_lag_gram_w launch executes (csrc/lagw.hip's tiling: per event, its
-    occurrences in stages of 128; rows (d, a2) for d = 0 .. K - 1 in two 32-event halves; the
-    (shift, fit) columns in 32-column tiles, a (d, tile) pair run only when some column of the
-    tile forms an H entry at that d): the structured products plus the G entries that are no H
-    entry and the padding."""
+    occurrences in stages of 128; pieces of 8 waves x 2 M tiles -- the (d, 32-event half) rows
+    -- by a window of NN (shift, fit) columns starting at the piece's first d row; each wave runs
+    the contiguous range of its 32-column tiles that meet a d of its rows with a second shift
+    that is a column): the structured products plus the G entries that are no H entry and the
+    padding."""
     memo = lg.__dict__.setdefault("exec_flop", {})
     if nact in memo:
         return memo[nact]
-    K = lg.K
-    nh = (lg.m + 1 + 31) // 32
-    nq = nact * K
-    NN = 64 if nq <= 64 else 128
-    ntiles = -(-nq // NN) * NN // 32
-    pairs = 0
-    for j in range(ntiles):
-        lo, hi = (32 * j) // nact, min(K - 1, (32 * j + 31) // nact)
-        if lo < K:
-            pairs += hi + 1                      # live for d = 0 .. hi
+    K, MT, WM = lg.K, 2, 8
+    NH = 2 if lg.m + 1 > 32 else 1
+    NT = 2 if nact * K <= 64 else 4
+    NN, MB, Tm = NT * 32, WM * MT, K * NH
+    Gm, Gy = -(-Tm // MB), -(-(nact * K) // NN)
+    tiles = 0
+    for g in range(Gm):
+        t0 = g * MB
+        di0 = t0 // NH
+        for y in range(Gy):
+            n0 = y * NN + di0 * nact
+            if t0 >= Tm or n0 // nact >= K or min(K - 1, (n0 + NN - 1) // nact) < di0:
+                continue
+            for wm in range(WM):
+                rows = [t for t in range(t0 + wm * MT, t0 + wm * MT + MT) if t < Tm]
+                if not rows:
+                    continue
+                dmin = min(t // NH for t in rows)
+                live = [j for j in range(NT) if (n0 + 32 * j) // nact < K
+                        and min(K - 1, (n0 + 32 * j + 31) // nact) >= dmin]
+                if live:
+                    tiles += MT * (max(live) - min(live) + 1)
     occ = float(sum(-(-int(c) // 128) * 128 for c in lg.cnt))
-    memo[nact] = 2.0 * occ * nh * pairs * 32 * 32
+    memo[nact] = 2.0 * occ * tiles * 32 * 32
     return memo[nact]
 
 def _syrk_cbits(d: Design, bf, prob: Problem, fits: np.ndarray, st, ev=None):
