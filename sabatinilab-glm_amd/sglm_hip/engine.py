@@ -1495,13 +1495,14 @@ def _side_stream(j: int = 0):
     """This thread's j-th side stream on the current device (the factorisation chains,
     overlapped with the gradient)."""
     streams = _scratch().streams
-    key = (torch.cuda.current_device(), "chol") if j == 0 else (torch.cuda.current_device(),
-                                                                 "chol", j)
+    prio = CHOL_STREAM == "prio"
+    key = ((torch.cuda.current_device(), "chol") if j == 0 else (torch.cuda.current_device(),
+                                                                  "chol", j)) + (prio,)
     sd = streams.get(key)
     if sd is None:
         # high priority: the chain's small latency-bound launches are dispatched ahead of the
         # gradient's workgroups as slots free up, instead of queueing behind a full-chip grid
-        sd = streams[key] = torch.cuda.Stream(priority=-1 if CHOL_STREAM == "prio" else 0)
+        sd = streams[key] = torch.cuda.Stream(priority=-1 if prio else 0)
     return sd
 
 
