@@ -372,6 +372,18 @@ int sglm_chol_solve_inv(float* H, float* Minv, int32_t P, const int32_t* fits,
                         const float* dshift, float* delta, int32_t* info, uint8_t* frozen,
                         int32_t B, void* work, sglm_stream_t stream);
 
+/* The two halves of sglm_chol_solve_inv's factorisation (round 6).  sglm_chol_factor: the chain
+ * alone for fits[0 .. n) -- penalty shift, frozen set, blocked Cholesky, the diagonal blocks of
+ * M = U^-1 written to Minv -- after which sglm_chol_solve_alias solves on the factors;
+ * sglm_chol_invert: the recursive-doubling levels that complete M, on any later stream point
+ * before a sglm_chol_solve_inv solve (nrefac = 0) reads it.  Factor and inverse are bitwise those
+ * of sglm_chol_solve_inv.  work: sglm_chol_work_bytes(P, B), a buffer of its own per stream. */
+int sglm_chol_factor(float* H, float* Minv, int32_t P, const int32_t* fits, int32_t n,
+                     const float* dshift, int32_t* info, uint8_t* frozen, int32_t B, void* work,
+                     sglm_stream_t stream);
+int sglm_chol_invert(const float* H, float* Minv, int32_t P, const int32_t* fits, int32_t n,
+                     int32_t B, void* work, sglm_stream_t stream);
+
 /* The factor + inverse chain of sglm_chol_solve_inv is captured per argument set (device
  * pointers, P, n, B) into a HIP graph and replayed.  The cache is a bounded LRU
  * (SGLM_CHOL_GRAPH_CAP entries, default 32); an evicted executable is destroyed after its last

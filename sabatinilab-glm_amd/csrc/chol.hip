@@ -1303,11 +1303,15 @@ static InvColCtx* inv_col_ctx(int nev) {
 
 // The factorisation + inversion chain (~110 launches) of fits[0 .. n).  ctx: the inverse
 // columns' branch (inv_col), or null for the recursive-doubling levels after the chain.
+static int inv_levels(const float* H, float* Minv, int32_t P, const int32_t* fits, int32_t n,
+                      int32_t B, void* work, hipStream_t s);
+
 static int factor_inv_launch(float* H, float* Minv, int32_t P, const int32_t* fits, int32_t n,
                              const float* dshift, float* delta, int32_t* info, uint8_t* frozen,
-                             int32_t B, void* work, hipStream_t s, InvColCtx* ctx = nullptr) {
+                             int32_t B, void* work, hipStream_t s, InvColCtx* ctx = nullptr,
+                             bool levels = true) {
     int st;
-    if (ctx) {
+    if (ctx && levels) {
         int nev = 0, st2 = SGLM_OK;
         const std::function<void(int)> hook = [&](int J) {
             if (J <= 0 || st2 != SGLM_OK) return;
@@ -1337,6 +1341,14 @@ static int factor_inv_launch(float* H, float* Minv, int32_t P, const int32_t* fi
     if ((st = chol_solve_mixed(H, P, fits, n, n, nullptr, dshift, delta, info, frozen, B, work, s,
                                Minv)))
         return st;
+    return levels ? inv_levels(H, Minv, P, fits, n, B, work, s) : SGLM_OK;
+}
+
+// The explicit inverses M = U^-1 of fits[0 .. n) whose factors (and the diagonal blocks of M)
+// a factorisation chain left in H / Minv: recursive doubling over aligned super-blocks,
+// (U^-1)_AC = -M_A (B M_C), two launches per level, log2(P / 64) levels.
+static int inv_levels(const float* H, float* Minv, int32_t P, const int32_t* fits, int32_t n,
+                      int32_t B, void* work, hipStream_t s) {
     // work: rhs, original diagonal (B x P each), diagonal-block inverses (B x 64 x 64),
     // Y (B x P), T (B x tcap)
     float* T = (float*)work + (size_t)3 * B * P + (size_t)B * kNB * kNB;
@@ -1470,30 +1482,30 @@ extern "C" int sglm_chol_graph_cache_clear(void) {
 
 static int factor_inv_cached(float* H, float* Minv, int32_t P, const int32_t* fits, int32_t n,
                              const float* dshift, float* delta, int32_t* info, uint8_t* frozen,
-                             int32_t B, void* work, hipStream_t s, InvColCtx* ctx);
+                             int32_t B, void* work, hipStream_t s, InvColCtx* ctx, bool levels);
 
 static int factor_inv(float* H, float* Minv, int32_t P, const int32_t* fits, int32_t n,
                       const float* dshift, float* delta, int32_t* info, uint8_t* frozen,
-                      int32_t B, void* work, hipStream_t s) {
+                      int32_t B, void* work, hipStream_t s, bool levels = true) {
     // (every diagonal-step variant writes its block of M, which the columns read)
-    InvColCtx* ctx = inv_col() ? inv_col_ctx(P / kNB + 1) : nullptr;
+    InvColCtx* ctx = (levels && inv_col()) ? inv_col_ctx(P / kNB + 1) : nullptr;
     if (!chol_graphs_enabled() || s == nullptr)      // the null stream cannot be captured
         return factor_inv_launch(H, Minv, P, fits, n, dshift, delta, info, frozen, B, work, s,
-                                 ctx);
+                                 ctx, levels);
     const int st = factor_inv_cached(H, Minv, P, fits, n, dshift, delta, info, frozen, B, work, s,
-                                     ctx);
+                                     ctx, levels);
     chain_pending_reap(false);                        // evicted chains that finished, unlocked
     return st;
 }
 
 static int factor_inv_cached(float* H, float* Minv, int32_t P, const int32_t* fits, int32_t n,
                              const float* dshift, float* delta, int32_t* info, uint8_t* frozen,
-                             int32_t B, void* work, hipStream_t s, InvColCtx* ctx) {
+                             int32_t B, void* work, hipStream_t s, InvColCtx* ctx, bool levels) {
     ChainKey key;
     std::memset(&key, 0, sizeof(key));
     key.H = H; key.Minv = Minv; key.fits = fits; key.dshift = dshift; key.delta = delta;
     key.info = info; key.frozen = frozen; key.work = work;
-    key.P = P; key.n = n; key.B = B; key.la = chol_lookahead(); key.q = (diag4q() ? (diag4l() ? (upd_diag() ? 3 : 2) : 1) : 0) | (ctx ? 4 : 0);
+    key.P = P; key.n = n; key.B = B; key.la = chol_lookahead(); key.q = (diag4q() ? (diag4l() ? (upd_diag() ? 3 : 2) : 1) : 0) | (ctx ? 4 : 0) | (levels ? 0 : 8);
     // the lock is held across capture and launch: a concurrent eviction must not destroy the
     // entry between lookup and launch (captures are thread-local, so nothing else is stalled
     // but other chains' host enqueue, which is short next to the chain itself)
@@ -1506,7 +1518,7 @@ static int factor_inv_cached(float* H, float* Minv, int32_t P, const int32_t* fi
             return SGLM_EHIP;
         }
         const int st = factor_inv_launch(H, Minv, P, fits, n, dshift, delta, info, frozen, B,
-                                         work, s, ctx);
+                                         work, s, ctx, levels);
         const hipError_t ec = hipStreamEndCapture(s, &graph);
         if (st) {
             if (graph) (void)hipGraphDestroy(graph);
@@ -1578,4 +1590,33 @@ extern "C" int sglm_chol_solve_inv(float* H, float* Minv, int32_t P, const int32
     chol_inv_apply_kernel<true><<<grid, kCT, 0, s>>>(Minv, P, fits, fsrc, rscale, tiles, g,
                                                       frozen, Y, delta);
     return check_launch("chol_inv_apply_kernel");
+}
+
+// The two halves of sglm_chol_solve_inv's factorisation (round 6): sglm_chol_factor runs the
+// chain (penalty shift, frozen set, blocked Cholesky; the diagonal blocks of M written) and
+// sglm_chol_invert the inversion levels after it -- bitwise the factor and inverse of
+// sglm_chol_solve_inv.  The engine solves the iteration on the fresh factors by substitution
+// (sglm_chol_solve_alias) and leaves the inversion to run beside its next main-stream work.
+extern "C" int sglm_chol_factor(float* H, float* Minv, int32_t P, const int32_t* fits,
+                                int32_t n, const float* dshift, int32_t* info, uint8_t* frozen,
+                                int32_t B, void* work, sglm_stream_t stream) {
+    if (n <= 0) return SGLM_OK;
+    if (!H || !Minv || !fits || !dshift || !info || !frozen || !work || P % kNB || P > kMaxP ||
+        B < n) {
+        set_error("sglm_chol_factor: bad args (P=%d, max %d)", P, kMaxP);
+        return SGLM_EINVAL;
+    }
+    float* scratch = (float*)work + (size_t)2 * B * P + (size_t)B * kNB * kNB;   // unused delta
+    return factor_inv(H, Minv, P, fits, n, dshift, scratch, info, frozen, B, work,
+                      as_stream(stream), false);
+}
+
+extern "C" int sglm_chol_invert(const float* H, float* Minv, int32_t P, const int32_t* fits,
+                                int32_t n, int32_t B, void* work, sglm_stream_t stream) {
+    if (n <= 0) return SGLM_OK;
+    if (!H || !Minv || !fits || !work || P % kNB || P > kMaxP || B < n) {
+        set_error("sglm_chol_invert: bad args (P=%d, max %d)", P, kMaxP);
+        return SGLM_EINVAL;
+    }
+    return inv_levels(H, Minv, P, fits, n, B, work, as_stream(stream));
 }

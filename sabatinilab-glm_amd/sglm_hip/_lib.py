@@ -81,6 +81,8 @@ SIGNATURES = {
                                       _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
     "sglm_chol_solve_mixed": (C.c_int, [_vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32,
                                         _vp, _vp]),
+    "sglm_chol_factor": (C.c_int, [_vp, _vp, _i32, _vp, _i32, _vp, _vp, _vp, _i32, _vp, _vp]),
+    "sglm_chol_invert": (C.c_int, [_vp, _vp, _i32, _vp, _i32, _i32, _vp, _vp]),
     "sglm_chol_graph_cache_size": (_i32, []),
     "sglm_chol_graph_cache_clear": (C.c_int, []),
     "sglm_chol_solve_alias": (C.c_int, [_vp, _i32, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _i32, _vp,

@@ -115,6 +115,11 @@ ANDERSON = __import__("os").environ.get("SGLM_ANDERSON", "1") == "1"
 # first iteration: link + gradient once per (mask, response, intercept) start key, the other
 # fits' gradient rows copied (bitwise the same values; round 6)
 GRAD_DEDUP = __import__("os").environ.get("SGLM_GRAD_DEDUP", "1") == "1"
+# a batch of >= DEFER_INV_MIN new factorisations is solved on its fresh factors by substitution
+# (sglm_chol_solve_alias) and its explicit inverses (the recursive-doubling levels, ~0.9 ms for
+# 20 fits at P = 2048, until now on the critical path after the chain) are formed on the side
+# stream behind it, beside the next main-stream work; 0 turns it off (round 6)
+DEFER_INV_MIN = int(__import__("os").environ.get("SGLM_DEFER_INV_MIN", "10"))
 # gradient enqueued before the Hessian decisions' device wait when no Hessian is planned
 GRAD_FIRST = __import__("os").environ.get("SGLM_GRAD_FIRST", "1") == "1"
 # gradient kernel that co-resides with the factorisation chain in iterations that form factors
@@ -1991,6 +1996,7 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
         else (lambda name, t: t)
     t0 = tick("irls_setup", time.perf_counter())
     plan = None
+    pending_inv = None      # event after the last deferred inversion (side stream)
     linked = None           # slot list whose link (and predictor update) is already enqueued
     for it in range(int(max_iter.max()) + 1):
         # every per-fit kernel runs over the active slots only (slot lists): no compaction,
@@ -2074,6 +2080,11 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
             torch.addcmul(bf.g[:B], lamp_d, beta64_d[:B], out=bf.gtot[:B])   # + lam * w
 
         # ---- Hessian
+        if pending_inv is not None:
+            # the previous iteration's deferred inversion reads bf.H: this iteration's Grams
+            # (main stream) write it only after (it ran beside the line search and link)
+            torch.cuda.current_stream().wait_event(pending_inv)
+            pending_inv = None
         gram_comp = np.zeros(B, dtype=bool)     # fits whose Gram is computed this iteration
         pipe_groups = None
         if const_hess:
@@ -2177,6 +2188,13 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
             rsc_d = up(rsc, np.float32)
             nl = int(lst.size)
             fact_done = None
+            defer = False                  # this iteration's inverses formed after its solve
+            if pending_inv is not None:
+                # the last deferred inversion reads bf.fact_fits / writes Minv: the main stream
+                # orders after it before rewriting the list or reading those inverses (long
+                # done by now: it ran beside the previous iteration's main-stream work)
+                torch.cuda.current_stream().wait_event(pending_inv)
+                pending_inv = None
             if nref and CHOL_STREAM == "serial":
                 bf.fact_fits[:nref].copy_(ints[:nref])
                 _lib.call("sglm_chol_solve_inv", _p(bf.H), _p(bf.Minv), P, _p(bf.fact_fits), None,
@@ -2222,6 +2240,8 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
                     cuts = np.linspace(0, int(nref), nsplit + 1).round().astype(int)
                     chains += [(ready, int(cuts[j]), int(cuts[j + 1] - cuts[j]))
                                for j in range(nsplit) if cuts[j + 1] > cuts[j]]
+                    defer = (DEFER_INV_MIN > 0 and nref >= DEFER_INV_MIN and len(chains) == 1
+                             and comm is None)
                 _gradient()
                 t0 = tick("it_gradient", t0)
                 dones = []
@@ -2229,11 +2249,16 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
                     sd = side if (pipe_groups is not None or j == 0) else _side_stream(j)
                     sd.wait_event(ready)
                     t_ch = time.perf_counter()
-                    _lib.call("sglm_chol_solve_inv", _p(bf.H), _p(bf.Minv), P,
-                              _p(bf.fact_fits[off:]), None, None, ng, ng, None, 0, None,
-                              _p(bf.dshift), _p(bf.delta), _p(bf.info), _p(bf.frozen), B,
-                              _p(bf.chol_work(j if pipe_groups is None else 0)),
-                              sd.cuda_stream)
+                    if defer:
+                        _lib.call("sglm_chol_factor", _p(bf.H), _p(bf.Minv), P,
+                                  _p(bf.fact_fits[off:]), ng, _p(bf.dshift), _p(bf.info),
+                                  _p(bf.frozen), B, _p(bf.chol_work(0)), sd.cuda_stream)
+                    else:
+                        _lib.call("sglm_chol_solve_inv", _p(bf.H), _p(bf.Minv), P,
+                                  _p(bf.fact_fits[off:]), None, None, ng, ng, None, 0, None,
+                                  _p(bf.dshift), _p(bf.delta), _p(bf.info), _p(bf.frozen), B,
+                                  _p(bf.chol_work(j if pipe_groups is None else 0)),
+                                  sd.cuda_stream)
                     if stats is not None:
                         stats.chain_host_s += time.perf_counter() - t_ch
                     if sd is not side:
@@ -2244,12 +2269,44 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
                     side.wait_event(ev_)
                 fact_done = torch.cuda.Event()
                 fact_done.record(side)
+                if defer:
+                    # the inverses of these factors, behind the chain on the side stream
+                    _lib.call("sglm_chol_invert", _p(bf.H), _p(bf.Minv), P, _p(bf.fact_fits),
+                              int(nref), B, _p(bf.chol_work(0)), side.cuda_stream)
+                    pending_inv = torch.cuda.Event()
+                    pending_inv.record(side)
             if fact_done is None:
                 _gradient()
                 t0 = tick("it_gradient", t0)
             if fact_done is not None:
                 torch.cuda.current_stream().wait_event(fact_done)
-            if nl:
+            if nl and defer:
+                # fits on this iteration's factors: substitution on the factors (the same
+                # delta = -r F^-1 F^-T g as the inverse's two GEMMs, other rounding); the rest
+                # (kept factors, aliases of older representatives) on their complete inverses
+                newf = np.isin(fsrc, order[:nref])
+                if (~newf).any():
+                    lo, fo, ro = lst[~newf], fsrc[~newf], rsc[~newf]
+                    tl, q = [], 0               # runs of <= 32 fits sharing one factor
+                    while q < lo.size:
+                        e = q + 1
+                        while e < lo.size and e - q < 32 and fo[e] == fo[q]:
+                            e += 1
+                        tl.append((q, e - q))
+                        q = e
+                    io = up(np.concatenate([lo, fo, np.asarray(tl, np.int32).reshape(-1)]),
+                            np.int32)
+                    no = int(lo.size)
+                    _lib.call("sglm_chol_solve_inv", _p(bf.H), _p(bf.Minv), P, _p(io),
+                              _p(io[no:]), _p(up(ro, np.float32)), no, 0, _p(io[2 * no:]),
+                              len(tl), _p(bf.gtot), _p(bf.dshift), _p(bf.delta), _p(bf.info),
+                              _p(bf.frozen), B, _p(bf.cwork), st)
+                ln, fn, rn = lst[newf], fsrc[newf], rsc[newf]
+                idn = up(np.stack([ln, fn]), np.int32)
+                _lib.call("sglm_chol_solve_alias", _p(bf.H), P, _p(idn[0]), _p(idn[1]),
+                          int(ln.size), _p(bf.gtot), _p(up(rn, np.float32)), _p(bf.delta),
+                          _p(bf.frozen), B, _p(bf.cwork), st)
+            elif nl:
                 _lib.call("sglm_chol_solve_inv", _p(bf.H), _p(bf.Minv), P, _p(ints),
                           _p(ints[nl:]), _p(rsc_d), nl, 0, _p(ints[2 * nl:]), len(tiles),
                           _p(bf.gtot), _p(bf.dshift), _p(bf.delta), _p(bf.info), _p(bf.frozen),
@@ -2587,6 +2644,8 @@ def irls(prob: Problem, reqs: List[FitReq], tol: Optional[float] = None,
             plan = hess_plan(nxt)
         t0 = tick("it_update", t0)
 
+    if pending_inv is not None:              # a deferred inversion still reads bf.H / fact_fits
+        torch.cuda.current_stream().wait_event(pending_inv)
     # unpenalised fits: the minimum-norm point of the solution set (lstsq's answer on a
     # rank-deficient design; the fitted values on the fit's rows are unchanged)
     pf = np.zeros(0, dtype=np.int64)

@@ -350,6 +350,75 @@ def test_chol_inv_columns_equal_levels(engine, torch_mod, P, p, graph, monkeypat
         assert np.abs(Iu - np.eye(keep.size)).max() < 1e-3, k
 
 
+@pytest.mark.parametrize("P,p,graph", [(192, 150, False), (2048, 1990, True)])
+def test_chol_factor_then_invert(engine, torch_mod, P, p, graph):
+    """sglm_chol_factor + sglm_chol_invert (the engine's deferred inversion) leave the factor,
+    inverse, frozen set and drop count of sglm_chol_solve_inv bit for bit, and the substitution
+    solve on the fresh factors (sglm_chol_solve_alias: own and aliased fits) matches the float64
+    solve: a dependent column, a frozen coordinate, three fits."""
+    torch = torch_mod
+    from sglm_hip import _lib
+    rng = np.random.default_rng(P + 23)
+    B = 3
+    H = np.zeros((B, P, P), np.float32)
+    for k in range(B):
+        A = rng.normal(size=(p + 300, p + 1))
+        A[:, 5] = A[:, 9]
+        H[k, : p + 1, : p + 1] = A.T @ A / 100.0
+    dsh = np.full((B, P), -1.0, np.float32)
+    dsh[:, :p] = rng.uniform(0.1, 0.5, size=(B, 1))
+    dsh[:, p] = 0.0
+    dsh[:, [5, 9]] = 0.0                                 # unpenalised: pivot 9 drops
+    dsh[:, 17] = -1.0
+    g = rng.normal(size=(B, P))
+    st = torch.cuda.Stream() if graph else None
+    sp = st.cuda_stream if graph else 0
+    outs = []
+    for mode in ("whole", "split"):
+        Hd = torch.from_numpy(H).cuda()
+        Md = torch.zeros_like(Hd)
+        out = torch.zeros((B, P), dtype=torch.float32, device="cuda")
+        info = torch.zeros(B, dtype=torch.int32, device="cuda")
+        frozen = torch.zeros((B, P), dtype=torch.uint8, device="cuda")
+        dshd = torch.from_numpy(dsh).cuda()
+        cw = torch.empty(_lib.query("sglm_chol_work_bytes", P, B), dtype=torch.uint8,
+                         device="cuda")
+        lst = torch.arange(B, dtype=torch.int32, device="cuda")
+        rs = torch.ones(B, dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        if mode == "whole":
+            _lib.call("sglm_chol_solve_inv", Hd.data_ptr(), Md.data_ptr(), P, lst.data_ptr(),
+                      lst.data_ptr(), rs.data_ptr(), B, B, None, 0, None, dshd.data_ptr(),
+                      out.data_ptr(), info.data_ptr(), frozen.data_ptr(), B, cw.data_ptr(), sp)
+        else:
+            _lib.call("sglm_chol_factor", Hd.data_ptr(), Md.data_ptr(), P, lst.data_ptr(), B,
+                      dshd.data_ptr(), info.data_ptr(), frozen.data_ptr(), B, cw.data_ptr(), sp)
+            # substitution on the fresh factors: fits 0, 1 on their own, fit 2 aliased to 0
+            gd = torch.from_numpy(g).cuda()
+            fl = torch.tensor([0, 1, 2], dtype=torch.int32, device="cuda")
+            fs = torch.tensor([0, 1, 0], dtype=torch.int32, device="cuda")
+            rsc = torch.tensor([1.0, 1.0, 0.8], dtype=torch.float32, device="cuda")
+            cw2 = torch.empty_like(cw)
+            _lib.call("sglm_chol_solve_alias", Hd.data_ptr(), P, fl.data_ptr(), fs.data_ptr(), 3,
+                      gd.data_ptr(), rsc.data_ptr(), out.data_ptr(), frozen.data_ptr(), B,
+                      cw2.data_ptr(), sp)
+            _lib.call("sglm_chol_invert", Hd.data_ptr(), Md.data_ptr(), P, lst.data_ptr(), B, B,
+                      cw.data_ptr(), sp)
+        torch.cuda.synchronize()
+        outs.append([t.cpu().numpy() for t in (Hd, Md, info, frozen, out)])
+    (Hw, Mw, iw, fw, _), (Hs, Ms, is_, fs_, xs) = outs
+    up = np.triu(np.ones((P, P), bool))
+    assert np.array_equal(Hw[:, up], Hs[:, up]) and np.array_equal(Mw[:, up], Ms[:, up])
+    assert np.array_equal(iw, is_) and np.array_equal(fw, fs_) and (iw >= 1).all()
+    for q, src, sc in ((0, 0, 1.0), (1, 1, 1.0), (2, 0, 0.8)):
+        keep = np.flatnonzero(~fs_[src].astype(bool))
+        Mm = H[src].astype(np.float64)[np.ix_(keep, keep)] + np.diag(dsh[src, keep])
+        ref = np.zeros(P)
+        ref[keep] = -sc * np.linalg.solve(Mm, g[q, keep])
+        assert rel(xs[q], ref) < 1e-3, (q, rel(xs[q], ref))
+        assert np.all(xs[q, fs_[src].astype(bool)] == 0)
+
+
 @pytest.mark.parametrize("P,p,B", [(768, 700, 6), (2048, 1990, 5)])
 def test_chol_inv_many_fits_vs_float64(engine, torch_mod, P, p, B, monkeypatch):
     """Factor + inverse chain on several fits of their own with the 128 x 128 inversion tiles
