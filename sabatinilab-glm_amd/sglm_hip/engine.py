@@ -119,7 +119,7 @@ GRAD_DEDUP = __import__("os").environ.get("SGLM_GRAD_DEDUP", "1") == "1"
 # (sglm_chol_solve_alias) and its explicit inverses (the recursive-doubling levels, ~0.9 ms for
 # 20 fits at P = 2048, until now on the critical path after the chain) are formed on the side
 # stream behind it, beside the next main-stream work; 0 turns it off (round 6)
-DEFER_INV_MIN = int(__import__("os").environ.get("SGLM_DEFER_INV_MIN", "10"))
+DEFER_INV_MIN = int(__import__("os").environ.get("SGLM_DEFER_INV_MIN", "0"))
 # gradient enqueued before the Hessian decisions' device wait when no Hessian is planned
 GRAD_FIRST = __import__("os").environ.get("SGLM_GRAD_FIRST", "1") == "1"
 # gradient kernel that co-resides with the factorisation chain in iterations that form factors
