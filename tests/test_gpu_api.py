@@ -399,6 +399,40 @@ def test_hessian_reuse_keeps_the_fixed_point(engine, monkeypatch):
         assert rel(fast[j]["refit_coef"], c) < TOL_POIS
 
 
+def test_first_iteration_gradient_dedup(engine, monkeypatch):
+    """GRAD_DEDUP (round 6): in the first iteration the link and the gradient run once per
+    (mask, response, intercept) start key and the other fits' gradient rows are copies.  A
+    C3-shape 5-split x 20-lambda Poisson grid plus a no-intercept and a rolled-response group
+    (distinct keys of one mask) matches the same grid with every fit's own link and gradient
+    (1e-6 relative: the gradient's split-K slabs follow the batch size) and converges
+    everywhere."""
+    import pandas as pd
+    from sglm_hip import engine as E, folds, grid, synth
+    from sglm_hip.estimators import Objective
+    s = synth.make(N=100_000, m=25, L=10, family="poisson", rho=0.02, seed=2)
+    d = E.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
+    codes = folds.trial_keys_codes(pd.DataFrame({"nTrial": s.trial}), ["nTrial"]).values
+    np.random.seed(5)
+    cv_idx = folds.cv_idx_from_bucket_ids(codes, num_folds=5)
+    lams = np.logspace(-4, 1, 20)
+    objs = ([Objective("irls", E.FAM_TWEEDIE_LOG, 1.0, float(a), "n", True, 100) for a in lams]
+            + [Objective("irls", E.FAM_TWEEDIE_LOG, 1.0, float(a), "n", False, 100)
+               for a in lams[:3]])
+    rolls = [0] * len(lams) + [7] * 3
+    st = E.IrlsStats()
+    on = grid.run(d, s.y, cv_idx, objs, rolls, stats=st)
+    assert st.grad_dedup > 0
+    monkeypatch.setattr(E, "GRAD_DEDUP", False)
+    st0 = E.IrlsStats()
+    off = grid.run(d, s.y, cv_idx, objs, rolls, stats=st0)
+    assert st0.grad_dedup == 0
+    for a, b in zip(on, off):
+        assert rel(a["cv_coefs"], b["cv_coefs"]) < 1e-6
+        assert rel(a["cv_intercepts"], b["cv_intercepts"]) < 1e-6
+        assert rel(a["refit_coef"], b["refit_coef"]) < 1e-6
+        assert a["converged"] and b["converged"]
+
+
 def test_enet_cd_lane_kernel_equals_reg_kernel(engine, monkeypatch):
     """The lane-decision CD kernel (eight fits per 512-thread workgroup, SGLM_CD_FPW=8, the
     default) and the four-fit register kernel (SGLM_CD_FPW=4) perform the same arithmetic per
