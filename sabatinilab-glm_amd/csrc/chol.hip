@@ -664,6 +664,121 @@ __global__ void __launch_bounds__(kCT) chol_inv_level_lds_kernel(const float* __
     }
 }
 
+// The same level with split-precision products (round 6, the default; SGLM_INV_X3=0 for the
+// f32 kernel above): the staging
+// of chol_inv_level_lds_kernel, but each 16-deep K-step as three v_mfma_f32_32x32x16_bf16 on
+// the operands split x = hi + lo (hi = bf16(x), lo = bf16(x - hi)): hi hi + hi lo + lo hi, ~2^-17
+// relative per product (f32 accumulation) -- M is a preconditioner (delta = -M M^T g, the
+// direction rounded to bf16 before use; the fixed point is the exact gradient's), so its f32
+// rounding is not needed; 16 bf16 products per MFMA against 2 f32 ones.
+__device__ __forceinline__ void split8(const float (&x)[8], bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const __bf16 h = (__bf16)x[j];
+        hi[j] = h;
+        lo[j] = (__bf16)(x[j] - (float)h);
+    }
+}
+
+template <int STEP>
+__global__ void __launch_bounds__(kCT) chol_inv_level_x3_kernel(const float* __restrict__ Hall,
+                                                                float* __restrict__ Mall,
+                                                                float* __restrict__ Tall,
+                                                                int32_t P, int32_t s,
+                                                                const int32_t* __restrict__ fits,
+                                                                int64_t tcap) {
+    __shared__ __attribute__((aligned(16))) float sa[2][64 * kLA];
+    __shared__ __attribute__((aligned(16))) float sb[2][32 * kLB];
+    const int fit = fits[blockIdx.y];
+    const float* H = Hall + (int64_t)fit * P * P;
+    float* M = Mall + (int64_t)fit * P * P;
+    const int nsb = s / kNB;
+    int t = blockIdx.x;
+    const int pair = t / (nsb * nsb);
+    t -= pair * nsb * nsb;
+    const int ti = t / nsb, tj = t - ti * nsb;
+    const int a0 = 2 * s * pair, c0 = a0 + s;
+    const int cs = min(s, P - c0);
+    if (cs <= 0 || tj * kNB >= cs) return;
+    float* T = Tall + (int64_t)blockIdx.y * tcap + (int64_t)pair * s * s;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r32 = lane & 31, h = lane >> 5;
+    const int wr = wave >> 1, wc = wave & 1;
+    const float* ga;
+    const float* gb;
+    int64_t ldb;
+    int klo, khi;
+    if (STEP == 0) {
+        ga = H + (int64_t)(a0 + ti * kNB) * P + c0;
+        gb = M + (int64_t)c0 * P + c0 + tj * kNB;
+        ldb = P;
+        klo = 0;
+        khi = (tj + 1) * kNB;
+    } else {
+        ga = M + (int64_t)(a0 + ti * kNB) * P + a0;
+        gb = T + tj * kNB;
+        ldb = s;
+        klo = ti * kNB;
+        khi = s;
+    }
+    const int ar = tid >> 2, ak = 8 * (tid & 3);
+    const int bk = tid >> 3, bj = 8 * (tid & 7);
+    f32x4 ra0, ra1, rb0, rb1;
+    auto gload = [&](int kb) {
+        const float* pa = ga + (int64_t)ar * P + kb + ak;
+        ra0 = *reinterpret_cast<const f32x4*>(pa);
+        ra1 = *reinterpret_cast<const f32x4*>(pa + 4);
+        const float* pb = gb + (int64_t)(kb + bk) * ldb + bj;
+        rb0 = *reinterpret_cast<const f32x4*>(pb);
+        rb1 = *reinterpret_cast<const f32x4*>(pb + 4);
+    };
+    auto sstore = [&](int buf) {
+        *reinterpret_cast<f32x4*>(&sa[buf][ar * kLA + ak]) = ra0;
+        *reinterpret_cast<f32x4*>(&sa[buf][ar * kLA + ak + 4]) = ra1;
+        *reinterpret_cast<f32x4*>(&sb[buf][bk * kLB + bj]) = rb0;
+        *reinterpret_cast<f32x4*>(&sb[buf][bk * kLB + bj + 4]) = rb1;
+    };
+    f32x16 acc = {};
+    gload(klo);
+    sstore(0);
+    __syncthreads();
+    int cur = 0;
+    for (int kb = klo; kb < khi; kb += 32) {
+        const bool more = kb + 32 < khi;
+        if (more) gload(kb + 32);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            // A[row wr 32 + r32][k = 16 ks + 8 h + j], B[k = 16 ks + 8 h + j][col wc 32 + r32]
+            const float* A = &sa[cur][(wr * 32 + r32) * kLA + 16 * ks + 8 * h];
+            const float* Bq = &sb[cur][(16 * ks + 8 * h) * kLB + wc * 32 + r32];
+            const f32x4 a0v = *reinterpret_cast<const f32x4*>(A);
+            const f32x4 a1v = *reinterpret_cast<const f32x4*>(A + 4);
+            float xa[8] = {a0v[0], a0v[1], a0v[2], a0v[3], a1v[0], a1v[1], a1v[2], a1v[3]};
+            float xb[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xb[j] = Bq[j * kLB];
+            bf16x8 ah, al, bh, bl;
+            split8(xa, ah, al);
+            split8(xb, bh, bl);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+        }
+        if (more) sstore(cur ^ 1);
+        __syncthreads();
+        cur ^= 1;
+    }
+    const int i0 = ti * kNB + wr * 32, j0 = tj * kNB + wc * 32;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int i = i0 + (q & 3) + 8 * (q >> 2) + 4 * h, j = j0 + r32;
+        if (STEP == 0)
+            T[(int64_t)i * s + j] = acc[q];
+        else
+            M[(int64_t)(a0 + i) * P + c0 + j] = -acc[q];
+    }
+}
+
 // Block column J of M = U^-1, left-looking (round 6):
 //     M[I][J] = -(sum_{k=I}^{J-1} M[I][k] U[k][J]) M[J][J]      for the row blocks I < J,
 // one 64 x 64 tile per workgroup (blockIdx.x = I), the product staged exactly as in
@@ -1061,6 +1176,15 @@ static bool inv_pipe() {
 // Inversion levels through LDS (chol_inv_level_lds_kernel; default: 1-fit chain 1.22 -> 1.16 ms,
 // 3 fits 1.47 -> 1.33 ms, C4 grid 60-62 -> 58-59 ms on one box), SGLM_INV_LDS=0 for the
 // register variants.
+// Split-precision inversion levels (chol_inv_level_x3_kernel, the default: chain of 1 / 6 / 11
+// / 20 representatives 0.97 / 1.39 / 1.92 / 2.86 -> 0.95 / 1.28 / 1.74 / 2.53 ms, C4 grid
+// 28.82 -> 28.41 ms in a 10-round A/B, profiles/r06b_inv_x3_ab.json); SGLM_INV_X3=0 for the f32
+// MFMA levels (read per chain capture; part of the chain-graph key).
+static bool inv_x3() {
+    const char* e = getenv("SGLM_INV_X3");
+    return !(e && e[0] == '0');
+}
+
 static bool inv_lds() {
     static const bool v = [] {
         const char* e = getenv("SGLM_INV_LDS");
@@ -1363,6 +1487,9 @@ static int inv_levels(const float* H, float* Minv, int32_t P, const int32_t* fit
             const dim3 grid2((unsigned)(pairs * sb2 * sb2), (unsigned)n);
             chol_inv_level128_kernel<0><<<grid2, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
             chol_inv_level128_kernel<1><<<grid2, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
+        } else if (inv_x3()) {
+            chol_inv_level_x3_kernel<0><<<grid, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
+            chol_inv_level_x3_kernel<1><<<grid, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
         } else if (inv_lds()) {
             chol_inv_level_lds_kernel<0><<<grid, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
             chol_inv_level_lds_kernel<1><<<grid, kCT, 0, s>>>(H, Minv, T, P, sz, fits, tcap);
@@ -1505,7 +1632,7 @@ static int factor_inv_cached(float* H, float* Minv, int32_t P, const int32_t* fi
     std::memset(&key, 0, sizeof(key));
     key.H = H; key.Minv = Minv; key.fits = fits; key.dshift = dshift; key.delta = delta;
     key.info = info; key.frozen = frozen; key.work = work;
-    key.P = P; key.n = n; key.B = B; key.la = chol_lookahead(); key.q = (diag4q() ? (diag4l() ? (upd_diag() ? 3 : 2) : 1) : 0) | (ctx ? 4 : 0) | (levels ? 0 : 8);
+    key.P = P; key.n = n; key.B = B; key.la = chol_lookahead(); key.q = (diag4q() ? (diag4l() ? (upd_diag() ? 3 : 2) : 1) : 0) | (ctx ? 4 : 0) | (levels ? 0 : 8) | (inv_x3() ? 16 : 0);
     // the lock is held across capture and launch: a concurrent eviction must not destroy the
     // entry between lookup and launch (captures are thread-local, so nothing else is stalled
     // but other chains' host enqueue, which is short next to the chain itself)

@@ -312,6 +312,7 @@ def test_chol_inv_columns_equal_levels(engine, torch_mod, P, p, graph, monkeypat
     dsh[:, 17] = -1.0                                    # frozen
     outs = {}
     st = torch.cuda.Stream() if graph else None
+    monkeypatch.setenv("SGLM_INV_X3", "0")              # the levels in f32, as the columns
     for v in ("1", "0", "1"):
         monkeypatch.setenv("SGLM_INV_COL", v)
         Hd = torch.from_numpy(H).cuda()
@@ -417,6 +418,62 @@ def test_chol_factor_then_invert(engine, torch_mod, P, p, graph):
         ref[keep] = -sc * np.linalg.solve(Mm, g[q, keep])
         assert rel(xs[q], ref) < 1e-3, (q, rel(xs[q], ref))
         assert np.all(xs[q, fs_[src].astype(bool)] == 0)
+
+
+@pytest.mark.parametrize("P,p", [(192, 150), (2048, 1990)])
+def test_chol_inv_split_precision_levels(engine, torch_mod, P, p, monkeypatch):
+    """The inversion levels with split-precision products (SGLM_INV_X3, the default: three
+    bf16 MFMAs per product, hi hi + hi lo + lo hi) leave the factor, frozen set and drop count
+    of the f32 levels bit for bit and an inverse within 1e-4 of theirs (relative, Frobenius)
+    whose solves match float64 at the other tests' 1e-3."""
+    torch = torch_mod
+    from sglm_hip import _lib
+    rng = np.random.default_rng(P + 31)
+    B = 2
+    H = np.zeros((B, P, P), np.float32)
+    for k in range(B):
+        A = rng.normal(size=(p + 300, p + 1))
+        A[:, 5] = A[:, 9]
+        H[k, : p + 1, : p + 1] = A.T @ A / 100.0
+    dsh = np.full((B, P), -1.0, np.float32)
+    dsh[:, :p] = rng.uniform(0.05, 0.5, size=(B, 1))
+    dsh[:, p] = 0.0
+    dsh[:, [5, 9]] = 0.0
+    dsh[:, 17] = -1.0
+    g = rng.normal(size=(B, P))
+    outs = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("SGLM_INV_X3", v)
+        Hd = torch.from_numpy(H).cuda()
+        Md = torch.zeros_like(Hd)
+        gd = torch.from_numpy(g).cuda()
+        out = torch.zeros((B, P), dtype=torch.float32, device="cuda")
+        info = torch.zeros(B, dtype=torch.int32, device="cuda")
+        frozen = torch.zeros((B, P), dtype=torch.uint8, device="cuda")
+        dshd = torch.from_numpy(dsh).cuda()
+        cw = torch.empty(_lib.query("sglm_chol_work_bytes", P, B), dtype=torch.uint8,
+                         device="cuda")
+        ints = torch.tensor(np.r_[np.arange(B), np.arange(B), np.c_[np.arange(B), np.ones(B)]
+                                  .reshape(-1)].astype(np.int32), device="cuda")
+        rs = torch.ones(B, dtype=torch.float32, device="cuda")
+        _lib.call("sglm_chol_solve_inv", Hd.data_ptr(), Md.data_ptr(), P, ints.data_ptr(),
+                  ints[B:].data_ptr(), rs.data_ptr(), B, B, ints[2 * B:].data_ptr(), B,
+                  gd.data_ptr(), dshd.data_ptr(), out.data_ptr(), info.data_ptr(),
+                  frozen.data_ptr(), B, cw.data_ptr(), 0)
+        torch.cuda.synchronize()
+        outs[v] = [t.cpu().numpy() for t in (Hd, Md, info, frozen, out)]
+    (Hx, Mx, ix, fx, xx), (Hf, Mf, if_, ff, _) = outs["1"], outs["0"]
+    up = np.triu(np.ones((P, P), bool))
+    assert np.array_equal(Hx[:, up], Hf[:, up]) and np.array_equal(ix, if_)
+    assert np.array_equal(fx, ff) and (ix >= 1).all()
+    for k in range(B):
+        Ux, Uf = np.triu(Mx[k]).astype(np.float64), np.triu(Mf[k]).astype(np.float64)
+        assert np.linalg.norm(Ux - Uf) <= 1e-4 * np.linalg.norm(Uf), k
+        keep = np.flatnonzero(~fx[k].astype(bool))
+        Mm = H[k].astype(np.float64)[np.ix_(keep, keep)] + np.diag(dsh[k, keep])
+        ref = np.zeros(P)
+        ref[keep] = -np.linalg.solve(Mm, g[k, keep])
+        assert rel(xx[k], ref) < 1e-3, (k, rel(xx[k], ref))
 
 
 @pytest.mark.parametrize("P,p,B", [(768, 700, 6), (2048, 1990, 5)])
