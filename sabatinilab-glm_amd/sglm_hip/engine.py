@@ -126,11 +126,14 @@ GRAD_FIRST = __import__("os").environ.get("SGLM_GRAD_FIRST", "1") == "1"
 XTR_COCHAIN = __import__("os").environ.get("SGLM_XTR_COCHAIN", "1") == "1"
 # constant-weight Grams of lagged event designs from the event cross-correlations
 LAG_GRAM = __import__("os").environ.get("SGLM_LAG_GRAM", "1") == "1"
-# concurrent factorisation chains for a batch of >= CHOL_SPLIT_MIN new factorisations (off: the
-# second chain of a split measured no gain -- in the C4 kernel trace it starts only as the
-# first one ends -- tools/grid_ab.py split2 vs split1 56.2 / 56.2 ms)
-CHOL_SPLIT = int(__import__("os").environ.get("SGLM_CHOL_SPLIT", "1"))
-CHOL_SPLIT_MIN = int(__import__("os").environ.get("SGLM_CHOL_SPLIT_MIN", "6"))
+# concurrent factorisation chains for a batch of >= CHOL_SPLIT_MIN new factorisations.  Round 3
+# measured no gain (56.2 / 56.2 ms: the second chain started only as the first ended, beside a
+# full-chip gradient); since the first iteration's gradient runs once per start key (GRAD_DEDUP)
+# its 20-fit chain has the chip to itself, and two chains of 10 beat one of 20: C4 29.02 ->
+# 28.83 ms, 13 of 14 interleaved rounds (profiles/r06b_ab_chol_split.json); every fit's
+# arithmetic is the same in either split, so the factors are bitwise unchanged
+CHOL_SPLIT = int(__import__("os").environ.get("SGLM_CHOL_SPLIT", "2"))
+CHOL_SPLIT_MIN = int(__import__("os").environ.get("SGLM_CHOL_SPLIT_MIN", "12"))
 # SGLM_GRAM_PIPE=1: Grams computed one source at a time with each group's factorisation chain
 # started right behind its Gram -- measured slower: the per-group chains are latency-bound
 # (~1.1 ms each at 1-3 fits against 2.6 ms for one chain of 20), so the side stream carried

@@ -433,6 +433,32 @@ def test_first_iteration_gradient_dedup(engine, monkeypatch):
         assert a["converged"] and b["converged"]
 
 
+def test_concurrent_chains_equal_one_chain(engine, monkeypatch):
+    """A batch of new factorisations split over two concurrent chains (CHOL_SPLIT = 2, the
+    default for >= CHOL_SPLIT_MIN) does per fit the arithmetic of one chain: a C3-shape
+    5-split x 20-lambda Poisson grid (20 new factors in its first iteration) gives the same
+    coefficients bit for bit with one chain."""
+    import pandas as pd
+    from sglm_hip import engine as E, folds, grid, synth
+    from sglm_hip.estimators import Objective
+    s = synth.make(N=100_000, m=25, L=10, family="poisson", rho=0.02, seed=4)
+    d = E.Design.from_events(s.E, s.shifts, s.L - 1, s.N)
+    codes = folds.trial_keys_codes(pd.DataFrame({"nTrial": s.trial}), ["nTrial"]).values
+    np.random.seed(6)
+    cv_idx = folds.cv_idx_from_bucket_ids(codes, num_folds=5)
+    objs = [Objective("irls", E.FAM_TWEEDIE_LOG, 1.0, float(a), "n", True, 100)
+            for a in np.logspace(-4, 1, 20)]
+    monkeypatch.setattr(E, "CHOL_SPLIT", 2)
+    monkeypatch.setattr(E, "CHOL_SPLIT_MIN", 12)
+    two = grid.run(d, s.y, cv_idx, objs, [0] * len(objs))
+    monkeypatch.setattr(E, "CHOL_SPLIT", 1)
+    one = grid.run(d, s.y, cv_idx, objs, [0] * len(objs))
+    for a, b in zip(two, one):
+        assert np.array_equal(a["cv_coefs"], b["cv_coefs"])
+        assert np.array_equal(a["refit_coef"], b["refit_coef"])
+        assert a["converged"] and b["converged"]
+
+
 def test_enet_cd_lane_kernel_equals_reg_kernel(engine, monkeypatch):
     """The lane-decision CD kernel (eight fits per 512-thread workgroup, SGLM_CD_FPW=8, the
     default) and the four-fit register kernel (SGLM_CD_FPW=4) perform the same arithmetic per
