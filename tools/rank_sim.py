@@ -108,15 +108,20 @@ def main():
             if os.environ.get("SIM_GC_FREEZE", "1") == "1":
                 gc.collect()
                 gc.freeze()
-            st = E.IrlsStats(record=True)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            res = grid.run(d, s.y, cv_idx, objs, [0] * nlam, stats=st, simulate=sim)
-            torch.cuda.synchronize()
-            per.append({"rank": r, "wall_ms": round((time.perf_counter() - t0) * 1e3, 2),
+            # median of SIM_REPEATS timed runs: one run picks up host jitter of ~2 ms
+            reps = []
+            for _ in range(int(os.environ.get("SIM_REPEATS", "3"))):
+                st = E.IrlsStats(record=True)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                res = grid.run(d, s.y, cv_idx, objs, [0] * nlam, stats=st, simulate=sim)
+                torch.cuda.synchronize()
+                reps.append(round((time.perf_counter() - t0) * 1e3, 2))
+            per.append({"rank": r, "wall_ms": float(np.median(reps)), "repeats_ms": reps,
                         "fits": len(res), "fit_iters": st.fit_iters, "gram_fits": st.gram_fits})
         print(json.dumps({"plan": a.plan, "world": a.world, "per_rank": per,
-                          "max_ms": max(q["wall_ms"] for q in per)}))
+                          "max_ms": max(q["wall_ms"] for q in per),
+                          "wall_ms": "median per rank over SIM_REPEATS timed runs"}))
         return
     sim = (a.rank, a.world)
     for _ in range(int(os.environ.get("SIM_WARMUPS", "2"))):
